@@ -1,0 +1,126 @@
+"""Headline benchmark: MNIST CNN training throughput, images/sec (whole node).
+
+Config = the reference workload: the 2-layer MNIST CNN of
+/root/reference/mpipy.py:155-167, per-rank batch 64, momentum SGD with the
+reference LR schedule, fp32 compute, synthetic MNIST-shaped data and random
+init, data parallel over N GPUs with a per-step gradient all-reduce (RCCL
+over xGMI, overlapped with backward).  Weak scaling: global batch = 64 * N.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+Each rank runs W untimed steps, then EXACTLY K timed steps bracketed by a
+barrier + device synchronize on both sides; the slowest rank's time is
+used; rank 0 prints one JSON line.  Every timed step is a full training
+step (forward, backward, all-reduce, SGD update); eval is outside the
+timed region.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+METRIC = "images/sec (whole node) + final test accuracy, MNIST CNN at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
+    ap.add_argument("--sync", default="grad", choices=("grad", "none"))
+    ap.add_argument("--graph-steps", type=int, default=25)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
+    ap.add_argument("--no-eval", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    from mpi_tensorflow_amd import config as C
+    from mpi_tensorflow_amd.parallel import dist as D
+    from mpi_tensorflow_amd.parallel.comm import make_comm
+    from mpi_tensorflow_amd.runtime.mnist_engine import make_engine
+    from mpi_tensorflow_amd.utils.data import load_mnist_shard
+
+    device = D.resolve_device("auto")
+    di = D.init(str(device))
+    if di.world != a.gpus:
+        print(f"warning: --gpus {a.gpus} but world size {di.world}; using world size", file=sys.stderr)
+    N = di.world
+    cfg = C.TrainConfig(batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
+                        graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend).validate()
+    shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
+    comm = make_comm(di, device) if (N > 1 and a.sync == "grad") else None
+    eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm)
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    if hasattr(eng, "capture"):
+        eng.capture(a.warmup)
+        eng.capture(a.steps)
+    eng.train(a.warmup)
+    sync()
+    D.barrier()
+    sync()
+    t0 = time.perf_counter()
+    eng.train(a.steps)
+    sync()
+    t1 = time.perf_counter()
+    D.barrier()
+    dt = D.allreduce_max_host(t1 - t0)
+    err = float("nan")
+    if not a.no_eval:
+        err = D.allreduce_sum_host(eng.evaluate(shard.test_x, shard.test_y)) / N
+    images = N * a.batch_size * a.steps
+    value = images / dt
+    if di.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/sec",
+            "n_gpus": N,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * dt / a.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (MNIST-shaped 28x28x1, class-conditional; random-init weights)",
+            "config": {
+                "model": "mnist_cnn (2-layer MNIST CNN of mpipy.py: conv5x5x32-pool-conv5x5x64-pool-fc512-dropout-fc10)",
+                "global_batch": a.batch_size * N,
+                "per_gpu_batch": a.batch_size,
+                "seq_len": None,
+                "image": "28x28x1",
+                "parallelism": f"dp{N}",
+                "sync": "per-step gradient all-reduce (RCCL, 2 buckets, overlapped)" if N > 1 else "none (1 rank)",
+                "engine": eng.kind,
+                "comm": getattr(comm, "kind", "none"),
+                "graph_steps": (a.graph_steps if not a.no_graph else 0),
+            },
+            "final_test_accuracy": None if err != err else round(100.0 - err, 3),
+            "test_eval_after_steps": a.warmup + a.steps,
+        }
+        print(json.dumps(out))
+        sys.stdout.flush()
+    D.barrier()
+    D.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,197 @@
+"""Global configuration: the reference's hard-coded constants plus CLI overrides.
+
+The reference keeps every knob as a module global or an inline literal
+(`/root/reference/mpipy.py:14-21` globals, `:57` L2 coefficient, `:60-64`
+learning-rate schedule, `:65` momentum, `:87` sync period, `:166` dropout).
+This module mirrors those defaults exactly and exposes them through one
+dataclass (`TrainConfig`) plus an argparse builder, so the one-script API
+(`mpipy.py`) keeps the reference defaults while every value is overridable.
+
+`--reference-quirks` re-enables the reference's behavioural oddities that
+the framework fixes by default:
+  * Q5  - train shard padded with zero rows (tr_size//P rows, 5000/P zeros)
+  * Q8  - dropout stays active at evaluation time
+  * Q9  - full local test-set evaluation after every training step
+  * Q11 - "bcast" = gather weights (not biases/momentum) to rank 0 and
+          average there only; other ranks never receive the average
+  * Q14 - identical dropout seeds on every rank
+"""
+
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import os
+from typing import List, Optional
+
+# --- reference constants (mpipy.py:14-21) -------------------------------
+# mpipy.py:14 sets TF_CPP_MIN_LOG_LEVEL=2 and :15 MPI_OPTIMAL_PATH=1; the
+# equivalents here are log verbosity knobs, not environment variables.
+DATA_URL = "https://storage.googleapis.com/cvdf-datasets/mnist/"  # mpipy.py:17
+ITERATION = 2  # epochs over the local shard, mpipy.py:18
+IMAGE_SIZE = 28  # mpipy.py:19
+BATCH_SIZE = 64  # per-rank batch, mpipy.py:20
+NUM_CHANNEL = 10  # number of classes (named "channel" in mpipy.py:21)
+NUM_CLASSES = NUM_CHANNEL
+PIXEL_DEPTH = 255.0  # tutorial extract_data scaling: (x - 127.5) / 255
+
+# --- optimisation constants (mpipy.py:57-66) ------------------------------
+BASE_LR = 0.01  # mpipy.py:60
+LR_DECAY = 0.95  # mpipy.py:63
+MOMENTUM = 0.9  # mpipy.py:65
+L2_COEF = 5e-4  # mpipy.py:57
+DROPOUT_KEEP = 0.5  # mpipy.py:166
+SEED = 1  # op seed of every truncated_normal and the dropout, mpipy.py:40,166
+INIT_STDDEV = 0.1  # mpipy.py:39
+
+# --- distributed constants ----------------------------------------------------
+SYNC_EVERY = 50  # mpipy.py:87 (step>0 and step%50==0)
+TRAIN_ROWS = 55000  # mpipy.py:211 (tr_size before rounding)
+TEST_ROWS = 10000  # mpipy.py:212
+VAL_ROWS = 5000  # mpipy.py:213
+TRAIN_FILE_ROWS = 60000  # mpipy.py:216 (extract 60000 train images)
+
+MNIST_FILES = {
+    "train_images": "train-images-idx3-ubyte.gz",  # mpipy.py:203
+    "train_labels": "train-labels-idx1-ubyte.gz",  # mpipy.py:204
+    "test_images": "t10k-images-idx3-ubyte.gz",  # mpipy.py:205
+    "test_labels": "t10k-labels-idx1-ubyte.gz",  # mpipy.py:206
+}
+
+MODELS = ("mnist_cnn", "lenet5", "resnet18")
+SYNC_MODES = ("grad", "param_avg", "none")
+DTYPES = ("fp32", "bf16")
+
+
+@dataclasses.dataclass
+class TrainConfig:
+    """Every knob of a training run.  Defaults = the reference's behaviour
+    with its bugs fixed (see module docstring for the quirk switch)."""
+
+    model: str = "mnist_cnn"
+    epochs: int = ITERATION
+    batch_size: int = BATCH_SIZE
+    dtype: str = "fp32"
+    # gradient all-reduce every step (default, arXiv:1603.02339 intent) or the
+    # reference's periodic weight averaging (mpipy.py:87-91)
+    sync: str = "grad"
+    sync_every: int = SYNC_EVERY
+    # evaluate (and print the reference log line) every N steps; the
+    # reference evaluates every step (Q9) but prints every 50
+    eval_every: int = SYNC_EVERY
+    # data
+    data_dir: str = "data"
+    synthetic: Optional[bool] = None  # None = use real files if present
+    download: bool = False
+    # learning rate / optimiser
+    base_lr: float = BASE_LR
+    lr_decay: float = LR_DECAY
+    momentum: float = MOMENTUM
+    l2: float = L2_COEF
+    dropout_keep: float = DROPOUT_KEEP
+    seed: int = SEED
+    # execution
+    backend: str = "auto"  # auto | native (HIP kernels) | torch (oracle path)
+    device: str = "auto"  # auto | cpu | cuda
+    graph: bool = True  # capture the step into a HIP graph (native backend)
+    graph_steps: int = 10  # training steps per captured graph replay
+    max_steps: Optional[int] = None  # cap on steps (None = epochs-derived)
+    # checkpoint / metrics
+    ckpt: Optional[str] = None
+    ckpt_every: int = 0
+    resume: Optional[str] = None
+    metrics_jsonl: Optional[str] = None
+    quiet: bool = False
+    # compat
+    reference_quirks: bool = False
+
+    def validate(self) -> "TrainConfig":
+        if self.model not in MODELS:
+            raise ValueError(f"unknown model {self.model!r}; choose from {MODELS}")
+        if self.sync not in SYNC_MODES:
+            raise ValueError(f"unknown sync {self.sync!r}; choose from {SYNC_MODES}")
+        if self.dtype not in DTYPES:
+            raise ValueError(f"unknown dtype {self.dtype!r}; choose from {DTYPES}")
+        if self.backend not in ("auto", "native", "torch"):
+            raise ValueError(f"unknown backend {self.backend!r}")
+        if self.batch_size <= 0 or self.epochs <= 0:
+            raise ValueError("batch_size and epochs must be positive")
+        if self.sync_every <= 0 or self.eval_every < 0:
+            raise ValueError("sync_every must be > 0 and eval_every >= 0")
+        if not 0.0 < self.dropout_keep <= 1.0:
+            raise ValueError("dropout_keep must be in (0, 1]")
+        return self
+
+    # quirk accessors ------------------------------------------------------
+    @property
+    def pad_train_shard(self) -> bool:  # Q5
+        return self.reference_quirks
+
+    @property
+    def eval_dropout(self) -> bool:  # Q8
+        return self.reference_quirks
+
+    @property
+    def root_only_average(self) -> bool:  # Q11
+        return self.reference_quirks
+
+    @property
+    def same_seed_all_ranks(self) -> bool:  # Q14
+        return self.reference_quirks
+
+    def effective_eval_every(self) -> int:  # Q9
+        return 1 if self.reference_quirks else self.eval_every
+
+
+def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(
+        prog=prog,
+        description="MI355X-native data-parallel CNN trainer (reference-compatible "
+        "one-script API of mpi-Tensorflow's mpipy.py).",
+    )
+    d = TrainConfig()
+    p.add_argument("--model", default=d.model, choices=MODELS)
+    p.add_argument("--epochs", type=int, default=d.epochs, help="local epochs (mpipy.py:18)")
+    p.add_argument("--batch-size", type=int, default=d.batch_size)
+    p.add_argument("--dtype", default=d.dtype, choices=DTYPES)
+    p.add_argument("--sync", default=d.sync, choices=SYNC_MODES)
+    p.add_argument("--sync-every", type=int, default=d.sync_every)
+    p.add_argument("--eval-every", type=int, default=d.eval_every,
+                   help="0 disables periodic eval")
+    p.add_argument("--data-dir", default=d.data_dir)
+    g = p.add_mutually_exclusive_group()
+    g.add_argument("--synthetic", dest="synthetic", action="store_true", default=None)
+    g.add_argument("--real-data", dest="synthetic", action="store_false")
+    p.add_argument("--download", action="store_true", help="try DATA_URL if files missing")
+    p.add_argument("--base-lr", type=float, default=d.base_lr)
+    p.add_argument("--lr-decay", type=float, default=d.lr_decay)
+    p.add_argument("--momentum", type=float, default=d.momentum)
+    p.add_argument("--l2", type=float, default=d.l2)
+    p.add_argument("--dropout-keep", type=float, default=d.dropout_keep)
+    p.add_argument("--seed", type=int, default=d.seed)
+    p.add_argument("--backend", default=d.backend, choices=("auto", "native", "torch"))
+    p.add_argument("--device", default=d.device)
+    p.add_argument("--no-graph", dest="graph", action="store_false", default=True)
+    p.add_argument("--graph-steps", type=int, default=d.graph_steps)
+    p.add_argument("--max-steps", type=int, default=None)
+    p.add_argument("--ckpt", default=None, help="checkpoint path written at the end")
+    p.add_argument("--ckpt-every", type=int, default=0)
+    p.add_argument("--resume", default=None)
+    p.add_argument("--metrics-jsonl", default=None)
+    p.add_argument("--quiet", action="store_true")
+    p.add_argument("--reference-quirks", action="store_true",
+                   help="reproduce mpipy.py quirks Q5/Q8/Q9/Q11/Q14")
+    return p
+
+
+def config_from_args(argv: Optional[List[str]] = None, prog: str = "mpipy.py") -> TrainConfig:
+    ns = build_arg_parser(prog).parse_args(argv)
+    kw = {f.name: getattr(ns, f.name) for f in dataclasses.fields(TrainConfig) if hasattr(ns, f.name)}
+    return TrainConfig(**kw).validate()
+
+
+def env_flag(name: str, default: bool = False) -> bool:
+    v = os.environ.get(name)
+    if v is None:
+        return default
+    return v.strip().lower() not in ("", "0", "false", "no", "off")

@@ -1,0 +1,230 @@
+// pybind11 module `mpi_tensorflow_amd._C`: the native runtime of the
+// framework (HIP kernels, step executor, RCCL communicator, IDX loader).
+//
+// Device buffers cross the boundary as raw addresses (torch tensors'
+// data_ptr()) and streams as hipStream_t handles (torch's
+// current_stream().cuda_stream); the Python layer (ops/, runtime/) validates
+// shapes, dtypes, devices and contiguity BEFORE calling in, because the
+// kernels assume the geometry they were compiled for.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "idx_loader.h"
+#include "kernels/mnist.h"
+#include "mnist_executor.h"
+#include "rccl_comm.h"
+
+namespace py = pybind11;
+
+template <class T>
+static inline T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+static inline hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
+
+static void check_launch() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native runtime for mpi_tensorflow_amd (gfx950 HIP kernels, RCCL, IDX)";
+  m.attr("ARCH") = "gfx950";
+
+  // ------------------------------------------------------------- kernels
+  auto k = m.def_submodule("mnist", "fused fp32 MNIST CNN kernels (gfx950 MFMA)");
+  k.def("conv1_fwd", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w,
+                        uintptr_t b, uintptr_t out, uintptr_t argmax, uintptr_t s) {
+    mnist::launch_conv1_fwd(P<const float>(data), P<const long long>(step), n_local, batch,
+                            P<const float>(w), P<const float>(b), P<float>(out), P<uint8_t>(argmax),
+                            S(s));
+    check_launch();
+  });
+  k.def("conv2_fwd", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t b, uintptr_t out,
+                        uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
+    mnist::launch_conv2_fwd(P<const float>(a1), batch, P<const float>(w), P<const float>(b),
+                            P<float>(out), P<uint8_t>(argmax), P<float>(w2t), S(s));
+    check_launch();
+  });
+  k.def("fc1_train_splits", &mnist::fc1_train_splits);
+  k.def("conv2_filter_splits", &mnist::conv2_filter_splits);
+  k.def("conv1_filter_blocks", &mnist::conv1_filter_blocks);
+  k.def("part2_floats", &mnist::part2_floats);
+  k.def("part1_floats", &mnist::part1_floats);
+  k.def("fc1_part_floats", &mnist::fc1_part_floats);
+  k.def("fc1_fwd_train", [](uintptr_t a2, uintptr_t w, int batch, uintptr_t part, uintptr_t s) {
+    mnist::launch_fc1_fwd_train(P<const float>(a2), P<const float>(w), batch, P<float>(part), S(s));
+    check_launch();
+  });
+  k.def("fc1_fwd_eval", [](uintptr_t a2, uintptr_t w, uintptr_t b, int M, uintptr_t h,
+                           uint32_t key, float keep, uintptr_t s) {
+    mnist::launch_fc1_fwd_eval(P<const float>(a2), P<const float>(w), P<const float>(b), M,
+                               P<float>(h), key, keep, S(s));
+    check_launch();
+  });
+  k.def("fc_head_train",
+        [](uintptr_t part, uintptr_t b3, uintptr_t w4, uintptr_t b4, uintptr_t labels, int n_local,
+           uintptr_t step, int batch, float keep, uint32_t seed, uint32_t rank, float base_lr,
+           float decay, uintptr_t hd, uintptr_t dh, uintptr_t dlog, uintptr_t loss_rows,
+           uintptr_t lr_out, uintptr_t correct, uintptr_t s) {
+          mnist::launch_fc_head_train(P<const float>(part), P<const float>(b3), P<const float>(w4),
+                                      P<const float>(b4), P<const int>(labels), n_local,
+                                      P<const long long>(step), batch, keep, seed, rank, base_lr,
+                                      decay, P<float>(hd), P<float>(dh), P<float>(dlog),
+                                      P<float>(loss_rows), P<float>(lr_out), P<int>(correct), S(s));
+          check_launch();
+        });
+  k.def("fc_head_eval", [](uintptr_t h, uintptr_t w4, uintptr_t b4, uintptr_t labels, int M,
+                           uintptr_t logits, uintptr_t errors, uintptr_t s) {
+    mnist::launch_fc_head_eval(P<const float>(h), P<const float>(w4), P<const float>(b4),
+                               P<const int>(labels), M, P<float>(logits), P<int>(errors), S(s));
+    check_launch();
+  });
+  k.def("fc1_bwd", [](uintptr_t a2, uintptr_t idx2, uintptr_t dh, uintptr_t hd, uintptr_t dlog,
+                      uintptr_t w1, int batch, uintptr_t g_w3, uintptr_t g_b3, uintptr_t g_w4,
+                      uintptr_t g_b4, uintptr_t dy2, uintptr_t s) {
+    mnist::launch_fc1_bwd(P<const float>(a2), P<const uint8_t>(idx2), P<const float>(dh),
+                          P<const float>(hd), P<const float>(dlog), P<const float>(w1), batch,
+                          P<float>(g_w3), P<float>(g_b3), P<float>(g_w4), P<float>(g_b4),
+                          P<float>(dy2), S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
+                        uintptr_t part2, uintptr_t s) {
+    mnist::launch_conv2_bwd(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,
+                            P<float>(da1m), P<float>(part2), S(s));
+    check_launch();
+  });
+  k.def("conv1_bwd_filter", [](uintptr_t data, uintptr_t step, int n_local, int batch,
+                               uintptr_t da1m, uintptr_t idx1, uintptr_t part1, uintptr_t s) {
+    mnist::launch_conv1_bwd_filter(P<const float>(data), P<const long long>(step), n_local, batch,
+                                   P<const float>(da1m), P<const uint8_t>(idx1), P<float>(part1),
+                                   S(s));
+    check_launch();
+  });
+  k.def("grad_finalize", [](uintptr_t part2, int ns2, uintptr_t part1, int nb1, uintptr_t g_w2,
+                            uintptr_t g_b2, uintptr_t g_w1, uintptr_t g_b1, uintptr_t s) {
+    mnist::launch_grad_finalize(P<const float>(part2), ns2, P<const float>(part1), nb1,
+                                P<float>(g_w2), P<float>(g_b2), P<float>(g_w1), P<float>(g_b1),
+                                S(s));
+    check_launch();
+  });
+
+  auto o = m.def_submodule("optim", "flat-buffer optimizer kernels");
+  o.def("sgd_momentum", [](uintptr_t w, uintptr_t g, uintptr_t mom, long long n, long long l2_end,
+                           float l2, float momentum, float gscale, uintptr_t lr_ptr,
+                           float lr_const, uintptr_t step_ptr, uintptr_t s) {
+    optim::launch_sgd_momentum(P<float>(w), P<const float>(g), P<float>(mom), n, l2_end, l2,
+                               momentum, gscale, P<const float>(lr_ptr), lr_const,
+                               P<long long>(step_ptr), S(s));
+    check_launch();
+  });
+  o.def("scale", [](uintptr_t x, long long n, float a, uintptr_t s) {
+    optim::launch_scale(P<float>(x), n, a, S(s));
+    check_launch();
+  });
+
+  // ------------------------------------------------------------ executor
+  py::class_<MnistPtrs>(m, "MnistPtrs")
+      .def(py::init<>())
+#define RW(f) .def_readwrite(#f, &MnistPtrs::f)
+          RW(train_x) RW(train_y) RW(n_local) RW(batch) RW(params) RW(grads) RW(mom) RW(total)
+              RW(l2_end) RW(bucket1) RW(off_w4) RW(off_b4) RW(off_w3) RW(off_b3) RW(off_w2)
+                  RW(off_b2) RW(off_w1) RW(off_b1) RW(step) RW(lr) RW(correct) RW(a1) RW(idx1)
+                      RW(a2) RW(idx2) RW(fc1_part) RW(hd) RW(dh) RW(dlog) RW(loss_rows) RW(dy2)
+                          RW(da1m) RW(part2) RW(part1) RW(w2t) RW(keep_prob) RW(base_lr) RW(lr_decay)
+                              RW(l2) RW(momentum) RW(seed) RW(rank) RW(world);
+#undef RW
+
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank) {
+             std::string s = uid;
+             return new RcclComm(std::vector<char>(s.begin(), s.end()), nranks, rank);
+           }),
+           py::arg("uid"), py::arg("nranks"), py::arg("rank"))
+      .def_static("load", &RcclComm::load)
+      .def_static("loaded", &RcclComm::loaded)
+      .def_static("version", &RcclComm::version)
+      .def_static("unique_id",
+                  []() {
+                    auto v = RcclComm::unique_id();
+                    return py::bytes(v.data(), v.size());
+                  })
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("all_reduce",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              uintptr_t s) { c.all_reduce(P<void>(send), P<void>(recv), count, dtype, op, S(s)); })
+      .def("broadcast",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int root,
+              uintptr_t s) { c.broadcast(P<void>(send), P<void>(recv), count, dtype, root, S(s)); })
+      .def("reduce",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              int root, uintptr_t s) {
+             c.reduce(P<void>(send), P<void>(recv), count, dtype, op, root, S(s));
+           })
+      .def("all_gather",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t s) {
+             c.all_gather(P<void>(send), P<void>(recv), count, dtype, S(s));
+           })
+      .def("reduce_scatter",
+           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              uintptr_t s) { c.reduce_scatter(P<void>(send), P<void>(recv), count, dtype, op, S(s)); })
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("destroy", &RcclComm::destroy);
+
+  py::class_<MnistExecutor>(m, "MnistExecutor")
+      .def(py::init<const MnistPtrs&>())
+      .def("train_step",
+           [](MnistExecutor& e, uintptr_t s, RcclComm* comm, uintptr_t cs) {
+             e.train_step(S(s), comm, S(cs));
+             check_launch();
+           },
+           py::arg("stream"), py::arg("comm") = nullptr, py::arg("comm_stream") = 0)
+      .def("forward_backward",
+           [](MnistExecutor& e, uintptr_t s) {
+             e.forward_backward(S(s));
+             check_launch();
+           })
+      .def("sgd",
+           [](MnistExecutor& e, uintptr_t s, float gscale) {
+             e.sgd(S(s), gscale);
+             check_launch();
+           })
+      .def_static("eval_chunk",
+                  [](const MnistPtrs& p, uintptr_t x, uintptr_t y, int M, uintptr_t a1,
+                     uintptr_t a2, uintptr_t h, uintptr_t logits, uintptr_t errors, float keep,
+                     uint32_t key, uintptr_t s) {
+                    MnistExecutor::eval_chunk(p, x, y, M, a1, a2, h, logits, errors, keep, key,
+                                              S(s));
+                    check_launch();
+                  });
+
+  // ----------------------------------------------------------------- IDX
+  m.def("idx_header", [](const std::string& path) {
+    IdxHeader h = idx_header(path);
+    return py::make_tuple(h.magic, h.dims);
+  });
+  m.def("idx_read_u8", [](const std::string& path, long long start, long long stop) {
+    IdxHeader h;
+    std::vector<uint8_t> v = idx_read_u8(path, start, stop, &h);
+    std::vector<py::ssize_t> shape{(py::ssize_t)(stop - start)};
+    for (size_t i = 1; i < h.dims.size(); ++i) shape.push_back(h.dims[i]);
+    py::array_t<uint8_t> a(shape);
+    std::memcpy(a.mutable_data(), v.data(), v.size());
+    return a;
+  });
+  m.def("idx_read_images_f32",
+        [](const std::string& path, long long start, long long stop, float depth) {
+          IdxHeader h = idx_header(path);
+          std::vector<float> v = idx_read_images_f32(path, start, stop, depth);
+          std::vector<py::ssize_t> shape{(py::ssize_t)(stop - start)};
+          for (size_t i = 1; i < h.dims.size(); ++i) shape.push_back(h.dims[i]);
+          shape.push_back(1);  // NHWC channel dim, like extract_data
+          py::array_t<float> a(shape);
+          std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(float));
+          return a;
+        });
+}

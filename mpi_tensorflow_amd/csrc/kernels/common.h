@@ -1,0 +1,91 @@
+// Shared device helpers for the gfx950 (CDNA4) kernel set.
+//
+// Wave = 64 lanes everywhere (hard-coded, see cdna_hip_programming.md §1).
+// MFMA fragment maps used by every GEMM-shaped kernel here
+// (v_mfma_f32_32x32x2_f32, f32 in / f32 accumulate, exact fp32):
+//   A operand : lane l holds A[i = l & 31][k = l >> 5]
+//   B operand : lane l holds B[k = l >> 5][j = l & 31]
+//   C / D     : lane l, register r holds C[row = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5)]
+//                                        [col = l & 31]
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+#define WAVE 64
+
+#define HIP_CHECK(expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) +  \
+                               " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+    }                                                                                \
+  } while (0)
+
+// row of accumulator register r for lane l (32x32 MFMA C/D layout)
+__device__ __forceinline__ int mfma32_row(int r, int lane) {
+  return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+// ---------------------------------------------------------------- RNG ----
+// Counter-based dropout RNG; identical to utils/rng.py (the oracle).
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint32_t dropout_key(uint32_t seed, uint32_t rank,
+                                                         uint32_t step, uint32_t salt) {
+  uint32_t a = mix32(seed * 0x9E3779B9u + rank);
+  return mix32(a ^ (step * 0x85EBCA6Bu + salt));
+}
+
+__device__ __forceinline__ bool dropout_keep(uint32_t key, uint32_t idx, float keep_prob) {
+  uint32_t h = mix32(idx ^ key);
+  float u = (float)(h >> 8) * (1.0f / 16777216.0f);
+  return u < keep_prob;
+}
+
+// ------------------------------------------------------- reductions -------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5,
+// "XCD swizzle must be bijective"): consecutive logical tiles land on the
+// same XCD (shared L2) instead of being dealt round-robin over 8 XCDs.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int NX = 8;
+  if (nwg < NX) return bid;
+  int q = nwg / NX, r = nwg % NX;
+  int xcd = bid % NX, idx = bid / NX;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

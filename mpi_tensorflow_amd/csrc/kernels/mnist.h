@@ -1,0 +1,49 @@
+// Host launchers of the MNIST kernel set (mnist.hip) and the flat SGD kernel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace mnist {
+void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
+                      const float* w, const float* b, float* out, uint8_t* argmax, hipStream_t s);
+// w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
+void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
+                      uint8_t* argmax, float* w2t, hipStream_t s);
+int fc1_train_splits();
+void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
+void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
+                         uint32_t key, float keep_prob, hipStream_t s);
+void launch_fc_head_train(const float* part, const float* b3, const float* w4, const float* b4,
+                          const int* labels, int n_local, const long long* step, int batch,
+                          float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
+                          float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
+                          float* lr_out, int* correct, hipStream_t s);
+void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
+                         int M, float* logits, int* errors, hipStream_t s);
+void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
+                    const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
+                    float* g_w4, float* g_b4, float* dy2, hipStream_t s);
+int conv2_filter_splits(int batch);
+void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
+                      float* part2, hipStream_t s);
+int conv1_filter_blocks(int batch);
+void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
+                             const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);
+void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
+                          float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s);
+size_t part2_floats(int batch);
+size_t part1_floats(int batch);
+size_t fc1_part_floats(int batch);
+}  // namespace mnist
+
+namespace optim {
+// w, g, mom: flat fp32 buffers of n floats (n % 4 == 0, 16-B aligned).
+// g_eff = g * gscale (+ l2 * w for i < l2_end); mom = momentum * mom + g_eff;
+// w -= lr * mom.  lr is read from lr_ptr when non-null (device-computed
+// schedule), else lr_const.  step_ptr (optional) is incremented once.
+void launch_sgd_momentum(float* w, const float* g, float* mom, long long n, long long l2_end,
+                         float l2, float momentum, float gscale, const float* lr_ptr,
+                         float lr_const, long long* step_ptr, hipStream_t s);
+void launch_scale(float* x, long long n, float a, hipStream_t s);
+}  // namespace optim

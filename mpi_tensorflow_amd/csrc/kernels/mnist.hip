@@ -1,0 +1,891 @@
+// Fused fp32 HIP kernel set for the reference MNIST CNN on gfx950.
+//
+// Reference graph (/root/reference/mpipy.py:155-167, loss :54-58, optimizer
+// :59-66) and the TF ops each kernel replaces (SURVEY.md §2.4 F1-F12, B1-B7,
+// U1-U2, E1-E2):
+//
+//   conv_pool_fwd<conv1>   F1-F3  conv5x5(1->32)+bias+ReLU+maxpool2 (+argmax)
+//   fc1_fwd                F8     3136x512 GEMM, split-K partial slabs (train)
+//                                 or bias+ReLU(+dropout) epilogue (eval)
+//   fc_head                F8-F11, B1  split-K reduce, bias, ReLU, dropout,
+//                                 fc2, softmax-xent, dlogits, dhidden
+//   fc1_bwd                B1-B4  roles: dW1 (=a2^T dh), dX (=dh W1^T with the
+//                                 pool2/ReLU2 backward scatter fused), dW2/db
+//   conv2_fwd_v3           F4-F6  conv2 from an LDS halo tile (+W2 transpose)
+//   conv2_bwd              B5-B6  roles: bwd-data from an LDS halo tile (ReLU1
+//                                 mask fused), bwd-filter with L2-direct
+//                                 operands (+db2 on the centre tap)
+//   conv1_bwd_filter       B7     sparse VALU filter grad through pool1 argmax
+//   grad_finalize          B2     deterministic slab reduction
+//   fc_head_eval           E1-E2  logits, argmax, on-device error count
+//
+// Activations are NHWC fp32, weights keep the TF layouts (HWIO, [in, out]).
+// Every GEMM-shaped op runs on v_mfma_f32_32x32x2_f32 through gemm_core.h.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "gemm_core.h"
+#include "mnist.h"
+
+namespace mnist {
+
+// ----------------------------------------------------------- geometry ----
+template <int H_, int W_, int CIN_, int COUT_, int KS_, int PAD_, int BK_>
+struct ConvGeo {
+  static constexpr int H = H_, W = W_, CIN = CIN_, COUT = COUT_, KS = KS_, PAD = PAD_;
+  static constexpr int PH = H / 2, PW = W / 2;
+  static constexpr int K = KS * KS * CIN;
+  static constexpr int BK = BK_;
+  static constexpr int KPAD = (K + BK - 1) / BK * BK;
+};
+using Conv1 = ConvGeo<28, 28, 1, 32, 5, 2, 32>;
+
+constexpr int FC1_IN = 3136, FC1_OUT = 512, NCLS = 10;
+constexpr int FC1_SPLITS = 14;  // train fc1 split-K slabs (98 K tiles of 32 -> 7 each)
+
+__device__ __forceinline__ long long batch_offset_dev(const long long* step_ptr, int n_local,
+                                                      int batch) {
+  if (step_ptr == nullptr) return 0;
+  long long s = *step_ptr;
+  return (s * batch) % (long long)(n_local - batch);
+}
+
+// --------------------------------------------- conv + bias + relu + pool ----
+// GEMM view: M = pre-pool pixels ordered (n, py, px, quadrant) so that the 4
+// pixels of one 2x2 pooling window are 4 consecutive C rows = 4 consecutive
+// accumulator registers of ONE lane (rows (r&3) + 8(r>>2) + 4(l>>5)); the
+// pool is then a register max, no LDS, no extra pass.  N = Cout, K = taps*Cin.
+template <class G>
+struct ConvPoolFwdProb {
+  static constexpr bool A_KC = true, B_NC = true;
+  struct ACtx {
+    const float* p;  // input at (n, y, x, ci) of this slot's pixel
+    int y, x, kl;
+    bool v;
+  };
+  struct BCtx {
+    const float* p;
+    int kl;
+  };
+  const float* x;
+  const float* w;
+  int batch;
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const {
+    const int q = m & 3, pix = m >> 2;
+    const int px = pix % G::PW, t = pix / G::PW, py = t % G::PH, n = t / G::PH;
+    const int y = 2 * py + (q >> 1), xx = 2 * px + (q & 1);
+    const bool v = n < batch;
+    const int ci = kl % G::CIN;
+    return {x + ((size_t)((v ? n : 0) * G::H + y) * G::W + xx) * G::CIN + ci, y, xx, kl, v};
+  }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
+    const int k = k0 + c.kl;
+    const int tap = k / G::CIN;
+    const int kh = tap / G::KS, kw = tap % G::KS;
+    const int dy = kh - G::PAD, dx = kw - G::PAD;
+    const int iy = c.y + dy, ix = c.x + dx;
+    const bool ok = c.v && k < G::K && iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
+    return ok ? c.p[(dy * G::W + dx) * G::CIN] : 0.f;
+  }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {w + kl * G::COUT + n, kl}; }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    return (k0 + c.kl < G::K) ? c.p[k0 * G::COUT] : 0.f;
+  }
+};
+
+template <class G, int WM, int WN, int WK>
+__global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
+    const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
+    const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
+    uint8_t* __restrict__ argmax) {
+  using CF = gemm::Cfg<WM, WN, WK, G::BK, true, true>;
+  __shared__ float smem[CF::SMEM_FLOATS];
+  const long long off = batch_offset_dev(step_ptr, n_local, batch);
+  ConvPoolFwdProb<G> p{data + off * (G::H * G::W * G::CIN), w, batch};
+  const int M = batch * G::PH * G::PW * 4;
+  const int mt = (M + CF::BM - 1) / CF::BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * CF::BM, n0 = (bid / mt) * CF::BN;
+  f32x16 acc;
+  int wm, wn;
+  bool own = gemm::run_tile<WM, WN, WK, G::BK>(p, smem, m0, n0, 0, G::KPAD, acc, wm, wn);
+  if (!own) return;
+  const int lane = threadIdx.x & 63;
+  const int co = n0 + 32 * wn + (lane & 31);
+  const float b = bias[co];
+  const int P = batch * G::PH * G::PW;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int pooled = ((m0 + 32 * wm) >> 2) + 2 * g + (lane >> 5);
+    float v = acc[4 * g];
+    int q = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      if (acc[4 * g + j] > v) {  // strict: first max wins (TF MaxPool order)
+        v = acc[4 * g + j];
+        q = j;
+      }
+    }
+    if (pooled < P) {
+      out[pooled * G::COUT + co] = fmaxf(v + b, 0.f);
+      if (argmax) argmax[pooled * G::COUT + co] = (uint8_t)q;
+    }
+  }
+}
+
+// ------------------------------------------------------------- fc1 fwd ----
+struct Fc1FwdProb {
+  static constexpr bool A_KC = true, B_NC = true;
+  using ACtx = gemm::RowMajorA::Ctx;
+  struct BCtx {
+    const float* p;
+  };
+  gemm::RowMajorA A;
+  const float* w;  // [3136][512]
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return A.ctx(m, kl); }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const { return A.get(c, k0); }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {w + kl * FC1_OUT + n}; }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    return c.p[k0 * FC1_OUT];
+  }
+};
+
+// train: split-K partial slabs part[z][m][n]; eval: h = relu(acc + b) (+dropout)
+template <int WM, int WN, int WK, int BK, bool EVAL>
+__global__ __launch_bounds__(64 * WM * WN * WK) void fc1_fwd_kernel(
+    const float* __restrict__ a, const float* __restrict__ w, const float* __restrict__ bias,
+    float* __restrict__ out, int M, int kchunk, uint32_t drop_key, float keep_prob) {
+  using CF = gemm::Cfg<WM, WN, WK, BK, true, true>;
+  __shared__ float smem[CF::SMEM_FLOATS];
+  Fc1FwdProb p{{a, FC1_IN, M}, w};
+  const int mt = (M + CF::BM - 1) / CF::BM;
+  const int z = blockIdx.y;
+  const int bid = blockIdx.x;
+  const int m0 = (bid % mt) * CF::BM, n0 = (bid / mt) * CF::BN;
+  const int kb = z * kchunk, ke = min(FC1_IN, kb + kchunk);
+  f32x16 acc;
+  int wm, wn;
+  bool own = gemm::run_tile<WM, WN, WK, BK>(p, smem, m0, n0, kb, ke, acc, wm, wn);
+  if (!own) return;
+  const int lane = threadIdx.x & 63;
+  const int n = n0 + 32 * wn + (lane & 31);
+  const float b = EVAL ? bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + 32 * wm + mfma32_row(r, lane);
+    if (m >= M) continue;
+    if (EVAL) {
+      float h = fmaxf(acc[r] + b, 0.f);
+      if (keep_prob < 1.f) {
+        h = dropout_keep(drop_key, (uint32_t)(m * FC1_OUT + n), keep_prob) ? h / keep_prob : 0.f;
+      }
+      out[(size_t)m * FC1_OUT + n] = h;
+    } else {
+      out[((size_t)z * M + m) * FC1_OUT + n] = acc[r];
+    }
+  }
+}
+
+// -------------------------------------------------------------- fc head ----
+// One workgroup per batch row: reduce fc1 split-K slabs, bias, ReLU, dropout,
+// fc2 (512x10, too thin for MFMA: VALU dot products), softmax cross-entropy
+// forward AND backward (dlogits = (softmax - onehot) / B), then
+// dhidden = dlogits W2^T through the dropout and ReLU masks.
+__global__ __launch_bounds__(256) void fc_head_train_kernel(
+    const float* __restrict__ part, const float* __restrict__ b3, const float* __restrict__ w4,
+    const float* __restrict__ b4, const int* __restrict__ labels, int n_local,
+    const long long* step_ptr, int batch, float keep_prob, uint32_t seed, uint32_t rank,
+    float base_lr, float lr_decay, float* __restrict__ hd_out, float* __restrict__ dh_out,
+    float* __restrict__ dlog_out, float* __restrict__ loss_rows, float* __restrict__ lr_out,
+    int* __restrict__ correct) {
+  __shared__ float red[4][NCLS];
+  __shared__ float dlog_s[NCLS];
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long long step = step_ptr ? *step_ptr : 0;
+  const long long off = batch_offset_dev(step_ptr, n_local, batch);
+  const uint32_t key = dropout_key(seed, rank, (uint32_t)step, 0u);
+  const float scale = 1.f / keep_prob;
+  // issue every slab load up front (one latency round, not 14)
+  float ps[2][FC1_SPLITS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int q = 0; q < FC1_SPLITS; ++q)
+      ps[u][q] = part[((size_t)q * batch + row) * FC1_OUT + tid + 256 * u];
+  float w4r[2][NCLS];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) w4r[u][c] = w4[(tid + 256 * u) * NCLS + c];
+  float z[2], hd[2];
+  bool kp[2];
+  float lg[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lg[c] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = tid + 256 * u;
+    float s = b3[j];
+#pragma unroll
+    for (int q = 0; q < FC1_SPLITS; ++q) s += ps[u][q];
+    z[u] = s;
+    const float h = fmaxf(s, 0.f);
+    kp[u] = dropout_keep(key, (uint32_t)(row * FC1_OUT + j), keep_prob);
+    hd[u] = kp[u] ? h * scale : 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) lg[c] += hd[u] * w4r[u][c];
+  }
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    float v = wave_sum(lg[c]);
+    if (lane == 0) red[wv][c] = v;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int label = labels[off + row];
+    float logit = -INFINITY;
+    if (lane < NCLS) logit = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] + b4[lane];
+    const float mx = wave_max(logit);
+    const float e = lane < NCLS ? __expf(logit - mx) : 0.f;
+    const float se = wave_sum(e);
+    const float p = e / se;
+    const float lab_logit = wave_sum(lane == label ? logit : 0.f);
+    if (lane < NCLS) dlog_s[lane] = (p - (lane == label ? 1.f : 0.f)) / (float)batch;
+    const unsigned long long bal = __ballot(lane < NCLS && logit == mx);
+    const int am = __ffsll((long long)bal) - 1;
+    if (lane == 0) {
+      loss_rows[row] = (logf(se) + mx) - lab_logit;  // logsumexp - logit[label]
+      if (correct) atomicAdd(correct, am == label ? 1 : 0);
+      if (row == 0 && lr_out) {
+        const float e2 = (float)((step * batch) / n_local);
+        lr_out[0] = base_lr * powf(lr_decay, e2);
+      }
+    }
+  }
+  __syncthreads();
+  float dl[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) dl[c] = dlog_s[c];
+  if (tid < NCLS) dlog_out[row * NCLS + tid] = dl[tid];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int j = tid + 256 * u;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) d += dl[c] * w4r[u][c];
+    d = (kp[u] && z[u] > 0.f) ? d * scale : 0.f;
+    hd_out[row * FC1_OUT + j] = hd[u];
+    dh_out[row * FC1_OUT + j] = d;
+  }
+}
+
+// eval head: logits = h W2 + b, argmax vs label -> error count (E1/E2)
+__global__ __launch_bounds__(256) void fc_head_eval_kernel(const float* __restrict__ h,
+                                                           const float* __restrict__ w4,
+                                                           const float* __restrict__ b4,
+                                                           const int* __restrict__ labels, int M,
+                                                           float* __restrict__ logits_out,
+                                                           int* __restrict__ errors) {
+  // one wave per row, 4 rows per block
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  float lg[NCLS];
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) lg[c] = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < FC1_OUT / 64; ++jj) {
+    const int j = lane + 64 * jj;
+    const float hv = h[(size_t)row * FC1_OUT + j];
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) lg[c] += hv * w4[j * NCLS + c];
+  }
+  float best = -INFINITY;
+  int bi = 0;
+#pragma unroll
+  for (int c = 0; c < NCLS; ++c) {
+    const float v = wave_sum(lg[c]) + b4[c];
+    if (logits_out && lane == 0) logits_out[(size_t)row * NCLS + c] = v;
+    if (v > best) {
+      best = v;
+      bi = c;
+    }
+  }
+  if (lane == 0 && labels && errors) {
+    if (bi != labels[row]) atomicAdd(errors, 1);
+  }
+}
+
+// ------------------------------------------------------------- fc1 bwd ----
+// dW1 = a2^T dh : M = 3136 (fc1 in), N = 512, K = batch
+struct Fc1DwProb {
+  static constexpr bool A_KC = false, B_NC = true;
+  struct ACtx {
+    const float* p;
+    int kl;
+  };
+  using BCtx = ACtx;
+  const float* a2;  // [B][3136]
+  const float* dh;  // [B][512]
+  int batch;
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return {a2 + kl * FC1_IN + m, kl}; }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
+    return k0 + c.kl < batch ? c.p[k0 * FC1_IN] : 0.f;
+  }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {dh + kl * FC1_OUT + n, kl}; }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    return k0 + c.kl < batch ? c.p[k0 * FC1_OUT] : 0.f;
+  }
+};
+
+// dA2 = dh W1^T : M = batch, N = 3136, K = 512
+struct Fc1DxProb {
+  static constexpr bool A_KC = true, B_NC = false;
+  using ACtx = gemm::RowMajorA::Ctx;
+  struct BCtx {
+    const float* p;
+  };
+  gemm::RowMajorA A;  // dh [B][512]
+  const float* w1;
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return A.ctx(m, kl); }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const { return A.get(c, k0); }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {w1 + n * FC1_OUT + kl}; }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const { return c.p[k0]; }
+};
+
+constexpr int FC1BWD_BK = 64;
+constexpr int FC1BWD_DW_WM = 2, FC1BWD_DW_WN = 2;  // 64x64 tiles, 4 waves
+constexpr int FC1BWD_DX_WK = 4;                    // 32x32 tiles, K split over 4 waves
+constexpr int SMALL_BLOCKS = 8;
+
+__device__ void fc1_small_grads(int blk, const float* hd, const float* dh, const float* dlog,
+                                int batch, float* g_w4, float* g_b4, float* g_b3, float* smem) {
+  // block blk handles hidden units j in [64 blk, 64 blk + 64); 4 row groups
+  const int tid = threadIdx.x, jl = tid & 63, rg = tid >> 6;
+  const int j = blk * 64 + jl;
+  float acc[NCLS + 1];
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) acc[c] = 0.f;
+  for (int n = rg; n < batch; n += 4) {
+    const float h = hd[n * FC1_OUT + j];
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) acc[c] += h * dlog[n * NCLS + c];
+    acc[NCLS] += dh[n * FC1_OUT + j];
+  }
+  float* s = smem;  // [4][11][64]
+#pragma unroll
+  for (int c = 0; c <= NCLS; ++c) s[(rg * (NCLS + 1) + c) * 64 + jl] = acc[c];
+  __syncthreads();
+  if (rg == 0) {
+#pragma unroll
+    for (int c = 0; c <= NCLS; ++c) {
+      const float v = s[c * 64 + jl] + s[((NCLS + 1) + c) * 64 + jl] +
+                      s[(2 * (NCLS + 1) + c) * 64 + jl] + s[(3 * (NCLS + 1) + c) * 64 + jl];
+      if (c < NCLS)
+        g_w4[j * NCLS + c] = v;
+      else
+        g_b3[j] = v;
+    }
+  }
+  if (blk == 0 && tid < NCLS) {
+    float v = 0.f;
+    for (int n = 0; n < batch; ++n) v += dlog[n * NCLS + tid];
+    g_b4[tid] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void fc1_bwd_kernel(
+    const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
+    const float* __restrict__ hd, const float* __restrict__ dlog, const float* __restrict__ w1,
+    int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
+    float* __restrict__ g_b4, float* __restrict__ dy2) {
+  using CDX = gemm::Cfg<1, 1, FC1BWD_DX_WK, FC1BWD_BK, true, false>;
+  using CDW = gemm::Cfg<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_BK, false, true>;
+  constexpr int S1 = CDX::SMEM_FLOATS, S2 = CDW::SMEM_FLOATS, S3 = 4 * (NCLS + 1) * 64;
+  constexpr int SM = S1 > S2 ? (S1 > S3 ? S1 : S3) : (S2 > S3 ? S2 : S3);
+  __shared__ float smem[SM];
+  const int n_dx_m = (batch + 31) / 32;
+  const int n_dx = n_dx_m * (FC1_IN / 32);
+  const int n_dw = (FC1_IN / CDW::BM) * (FC1_OUT / CDW::BN);
+  int bid = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  f32x16 acc;
+  int wm, wn;
+  if (bid < n_dx) {
+    // ---- dX with the pool2 / ReLU2 backward scatter fused ----
+    Fc1DxProb p{{dh, FC1_OUT, batch}, w1};
+    const int m0 = (bid % n_dx_m) * 32, n0 = (bid / n_dx_m) * 32;
+    if (!gemm::run_tile<1, 1, FC1BWD_DX_WK, FC1BWD_BK>(p, smem, m0, n0, 0, FC1_OUT, acc, wm, wn))
+      return;
+    const int i = n0 + (lane & 31);  // (py, px, co) flat
+    const int co = i & 63, pp = i >> 6, py = pp / 7, px = pp % 7;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int n = m0 + mfma32_row(r, lane);
+      if (n >= batch) continue;
+      float g = acc[r];
+      if (a2[n * FC1_IN + i] <= 0.f) g = 0.f;  // ReLU2 inactive at the argmax
+      const int q = idx2[n * FC1_IN + i];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+        dy2[((n * 14 + y) * 14 + x) * 64 + co] = (d == q) ? g : 0.f;
+      }
+    }
+    return;
+  }
+  bid -= n_dx;
+  if (bid < n_dw) {
+    Fc1DwProb p{a2, dh, batch};
+    constexpr int mt = FC1_IN / CDW::BM;  // 49
+    const int m0 = (bid % mt) * CDW::BM, n0 = (bid / mt) * CDW::BN;
+    const int kend = (batch + FC1BWD_BK - 1) / FC1BWD_BK * FC1BWD_BK;
+    gemm::run_tile<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_BK>(p, smem, m0, n0, 0, kend, acc, wm,
+                                                             wn);
+    const int n = n0 + 32 * wn + (lane & 31);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + 32 * wm + mfma32_row(r, lane);
+      g_w3[m * FC1_OUT + n] = acc[r];
+    }
+    return;
+  }
+  bid -= n_dw;
+  fc1_small_grads(bid, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
+}
+
+// ------------------------------------------ conv2: dedicated MFMA kernels ----
+// The three conv2 products are the bulk of the step's FLOPs (3 x 1.28 GFLOP at
+// B = 64).  They bypass the generic gather engine:
+//  * fwd and bwd-data stage the block's input halo tile in LDS ONCE (pixel
+//    stride 33 / 65 floats: the 32 lanes of a half-wave read 32 different
+//    pixels of one channel conflict-free) and read every tap's A operand
+//    straight from that image - no im2col, no per-K-tile restaging;
+//  * the B operand (weights, L2 resident) is read straight from global memory
+//    with lanes on the contiguous channel axis (128 B per half-wave), one tap
+//    ahead in registers;
+//  * bwd-filter has channels on the lanes for BOTH operands, so it needs no
+//    LDS at all: coalesced 128 B loads of a1 and dY2 feed the MFMAs directly.
+constexpr int C2_XS_ROWS = 8, C2_XS_COLS = 18;
+
+// conv2 forward + bias + ReLU + 2x2 maxpool (+argmax).  Block = (image, pair of
+// pooled rows); 4 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
+// (N: 32 output channels).  Also writes W2T[t][co][ci] (the transposed weight
+// copy the bwd-data kernel reads) when w2t != nullptr.
+__global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
+    const float* __restrict__ a1, int batch, const float* __restrict__ w2,
+    const float* __restrict__ b2, float* __restrict__ out, uint8_t* __restrict__ argmax,
+    float* __restrict__ w2t) {
+  __shared__ float xs[C2_XS_ROWS * C2_XS_COLS * 33];
+  const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (w2t) {  // 51200 floats over all blocks
+    for (int i = blockIdx.x * 256 + tid; i < 51200; i += gridDim.x * 256) {
+      const int ci = i & 31, co = (i >> 5) & 63, t = i >> 11;
+      w2t[i] = w2[(t * 32 + ci) * 64 + co];
+    }
+  }
+  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 32; i += 256) {
+    const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
+    const int y = 2 * pr0 - 2 + r, x = c - 2;
+    const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
+    xs[(r * C2_XS_COLS + c) * 33 + ci] = ok ? a1[((n * 14 + y) * 14 + x) * 32 + ci] : 0.f;
+  }
+  const int msub = wave & 1, nsub = wave >> 1;
+  const int m = msub * 32 + (lane & 31);
+  const int win = m >> 2, q = m & 3;
+  int ly = 0, lx = 0;
+  if (win < 14) {
+    ly = 2 * (win / 7) + (q >> 1);
+    lx = 2 * (win % 7) + (q & 1);
+  }
+  const int abase = (ly * C2_XS_COLS + lx) * 33 + (lane >> 5);
+  const int co = nsub * 32 + (lane & 31);
+  const float* wp = w2 + (lane >> 5) * 64 + co;  // + (t*32 + 2c) * 64
+  float bc[16], bn[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 64];
+  __syncthreads();
+  f32x16 acc = zero16();
+  for (int t = 0; t < 25; ++t) {
+    if (t + 1 < 25) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) bn[c] = wp[((t + 1) * 32 + 2 * c) * 64];
+    }
+    const int kh = t / 5, kw = t % 5;
+    const float* xa = xs + abase + (kh * C2_XS_COLS + kw) * 33;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc = mfma32x32x2(xa[2 * c], bc[c], acc);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bc[c] = bn[c];
+  }
+  const float bias = b2[co];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int w_ = msub * 8 + 2 * g + (lane >> 5);
+    float v = acc[4 * g];
+    int qq = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      if (acc[4 * g + j] > v) {  // strict: first max wins (TF MaxPool order)
+        v = acc[4 * g + j];
+        qq = j;
+      }
+    }
+    const int pr = pr0 + w_ / 7, pc = w_ % 7;
+    if (w_ < 14 && pr < 7) {
+      const int o = ((n * 7 + pr) * 7 + pc) * 64 + co;
+      out[o] = fmaxf(v + bias, 0.f);
+      if (argmax) argmax[o] = (uint8_t)qq;
+    }
+  }
+}
+
+// conv2 bwd-data (+ReLU1 mask): dA1m[n,y,x,ci] = [a1>0] * sum_{kh,kw,co}
+// dY2[n, y+2-kh, x+2-kw, co] W2[kh,kw,ci,co].  Block = (image, 4 output rows);
+// 4 waves = 2 (M: 2 rows x 16 cols) x 2 (K: co halves, summed through LDS).
+__device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
+                                  const float* __restrict__ dy2, const float* __restrict__ w2t,
+                                  float* __restrict__ da1m, float* smem) {
+  float* ds = smem;  // [8][18][65]
+  const int n = bid >> 2, y0 = 4 * (bid & 3);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 64; i += 256) {
+    const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
+    const int y = y0 - 2 + r, x = c - 2;
+    const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
+    ds[(r * C2_XS_COLS + c) * 65 + co] = ok ? dy2[((n * 14 + y) * 14 + x) * 64 + co] : 0.f;
+  }
+  const int msub = wave & 1, cog = wave >> 1;
+  const int r2 = (lane & 31) >> 4, x = lane & 15;
+  const int ly = 2 * msub + r2, lx = x < 14 ? x : 0;
+  // staged row of source pixel (y+2-kh) is ly + 4 - kh; col lx + 4 - kw
+  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 32 + (lane >> 5);
+  const float* wp = w2t + (cog * 32 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
+  float bc[16], bn[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 32];
+  __syncthreads();
+  f32x16 acc = zero16();
+  for (int t = 0; t < 25; ++t) {
+    if (t + 1 < 25) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c) bn[c] = wp[((t + 1) * 64 + 2 * c) * 32];
+    }
+    const int kh = t / 5, kw = t % 5;
+    const float* xa = ds + abase - (kh * C2_XS_COLS + kw) * 65;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) acc = mfma32x32x2(xa[2 * c], bc[c], acc);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) bc[c] = bn[c];
+  }
+  __syncthreads();  // ds is dead: reuse for the K-split reduction
+  float* red = smem + msub * 16 * 64;
+  if (cog == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (cog == 0) {
+    const int ci = lane & 31;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mr = mfma32_row(r, lane);  // 0..31 = (row r2, col x)
+      const int y = y0 + 2 * msub + (mr >> 4), xx = mr & 15;
+      if (y < 14 && xx < 14) {
+        const int o = ((n * 14 + y) * 14 + xx) * 32 + ci;
+        const float g = acc[r] + red[r * 64 + lane];
+        da1m[o] = a1[o] > 0.f ? g : 0.f;
+      }
+    }
+  }
+}
+
+// conv2 bwd-filter: dW2[t][ci][co] = sum_pix a1[pix shifted by tap t][ci] dY2[pix][co].
+// Block = (tap, group of 4 images); 4 waves = 2 (N: co halves) x 2 (2 images
+// each, summed through LDS).  A[m = ci][k = pixel], B[k = pixel][co]: both
+// gathered straight from L2 with channels on lanes.  The centre tap's blocks
+// also sum dY2 per channel (db2).
+constexpr int C2F_GROUPS_IMG = 4;
+
+__device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict__ a1,
+                                    const float* __restrict__ dy2, float* __restrict__ part2,
+                                    float* __restrict__ part_db2, float* smem) {
+  const int t = bid % 25, g = bid / 25;
+  const int kh = t / 5, kw = t % 5;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nsub = wave & 1, ih = wave >> 1;
+  const int ci = lane & 31, kpar = lane >> 5;
+  const int co = nsub * 32 + (lane & 31);
+  f32x16 acc = zero16();
+  float dbs = 0.f;
+  for (int ii = 0; ii < 2; ++ii) {
+    const int n = g * C2F_GROUPS_IMG + ih * 2 + ii;
+    if (n >= batch) break;
+    const float* an = a1 + (size_t)n * 196 * 32 + ci;
+    const float* dn = dy2 + (size_t)n * 196 * 64 + co;
+    for (int y = 0; y < 14; ++y) {
+      const int iy = y + kh - 2;
+      const bool rv = iy >= 0 && iy < 14;
+      float av[7], bv[7];
+#pragma unroll
+      for (int xp = 0; xp < 7; ++xp) {
+        const int x = 2 * xp + kpar, ix = x + kw - 2;
+        const bool ok = rv && ix >= 0 && ix < 14;
+        av[xp] = ok ? an[(iy * 14 + ix) * 32] : 0.f;
+        bv[xp] = dn[(y * 14 + x) * 64];
+      }
+#pragma unroll
+      for (int xp = 0; xp < 7; ++xp) {
+        acc = mfma32x32x2(av[xp], bv[xp], acc);
+        dbs += bv[xp];
+      }
+    }
+  }
+  // sum the two image halves (ih) through LDS, write one slab per block
+  float* red = smem + nsub * 16 * 64;
+  if (ih == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (ih == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = t * 32 + mfma32_row(r, lane);  // (t, ci)
+      part2[((size_t)g * 800 + row) * 64 + co] = acc[r] + red[r * 64 + lane];
+    }
+  }
+  if (t == 12) {  // centre tap visits every pixel exactly once: db2 partial
+    dbs += __shfl_xor(dbs, 32, 64);
+    if (kpar == 0) part_db2[(g * 2 + ih) * 64 + co] = dbs;
+  }
+}
+
+// conv2 backward launch: bwd-data blocks (batch*4) then bwd-filter blocks
+// (25 taps x ceil(batch/4) image groups) - independent, one launch.
+__global__ __launch_bounds__(256) void conv2_bwd_kernel(
+    const float* __restrict__ a1, const float* __restrict__ dy2, const float* __restrict__ w2t,
+    int batch, float* __restrict__ da1m, float* __restrict__ part2,
+    float* __restrict__ part_db2) {
+  __shared__ float smem[C2_XS_ROWS * C2_XS_COLS * 65];
+  const int n_data = batch * 4;
+  if ((int)blockIdx.x < n_data) {
+    conv2_bwd_data_v3(blockIdx.x, a1, dy2, w2t, da1m, smem);
+  } else {
+    conv2_bwd_filter_v3(blockIdx.x - n_data, batch, a1, dy2, part2, part_db2, smem);
+  }
+}
+
+// ------------------------------------------------------ conv1 bwd filter ----
+// Sparse: each pooled gradient reaches exactly one pre-pool pixel (its argmax),
+// so dW1[t][co] = sum over pooled (n,py,px) of dA1m * x[argmax pixel + tap].
+// Block = (image, pair of pooled rows); thread = (co, position group).  All of
+// a thread's (gradient, argmax) pairs are loaded up front (one latency round).
+constexpr int C1F_SPLIT = 7;                    // pooled-row pairs per image
+constexpr int C1F_POS = 28;                     // pooled positions per block
+constexpr int C1F_PER_T = (C1F_POS + 7) / 8;    // positions per thread (4)
+
+__global__ __launch_bounds__(256) void conv1_bwd_filter_kernel(
+    const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
+    const float* __restrict__ da1m, const uint8_t* __restrict__ idx1, float* __restrict__ part1) {
+  __shared__ float xs[8 * 32];  // rows 4*pair-2 .. 4*pair+5 of the padded image
+  __shared__ float red[8][26 * 32 + 1];
+  const int n = blockIdx.x / C1F_SPLIT, pair = blockIdx.x % C1F_SPLIT;
+  const long long off = batch_offset_dev(step_ptr, n_local, batch);
+  const float* x = data + (off + n) * 784;
+  const int tid = threadIdx.x, co = tid & 31, grp = tid >> 5;
+  const int y0 = 4 * pair - 2;  // first image row held in xs
+  {
+    const int yy = y0 + tid / 32, xx = tid % 32 - 2;
+    xs[tid] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
+  }
+  float v[C1F_PER_T];
+  int q[C1F_PER_T];
+#pragma unroll
+  for (int j = 0; j < C1F_PER_T; ++j) {
+    const int p = grp + 8 * j;
+    v[j] = 0.f;
+    q[j] = 0;
+    if (p < C1F_POS) {
+      const int py = 2 * pair + p / 14, px = p % 14;
+      const int e = ((n * 14 + py) * 14 + px) * 32 + co;
+      v[j] = da1m[e];
+      q[j] = idx1[e];
+    }
+  }
+  __syncthreads();
+  float acc[26];
+#pragma unroll
+  for (int t = 0; t < 26; ++t) acc[t] = 0.f;
+#pragma unroll
+  for (int j = 0; j < C1F_PER_T; ++j) {
+    const int p = grp + 8 * j;
+    if (p < C1F_POS && v[j] != 0.f) {
+      const int py = 2 * pair + p / 14, px = p % 14;
+      const int ly = 2 * py + (q[j] >> 1) - y0 - 2;  // row in xs of tap kh = 0
+      const int lx = 2 * px + (q[j] & 1);            // col in xs (padded by 2) of kw = 0
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += v[j] * xs[(ly + kh) * 32 + lx + kw];
+      acc[25] += v[j];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 26; ++t) red[grp][t * 32 + co] = acc[t];
+  __syncthreads();
+  for (int i = tid; i < 26 * 32; i += 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[g][i];
+    part1[(size_t)blockIdx.x * 832 + i] = s;
+  }
+}
+
+// ------------------------------------------------------------ finalize ----
+// conv2: one thread per dW2 output summing the G image-group slabs; db2 from
+// the 2G centre-tap partials.  conv1: one wave per output (lanes stride over
+// the per-block slabs) + wave reduction.
+__global__ __launch_bounds__(256) void grad_finalize_kernel(
+    const float* __restrict__ part2, const float* __restrict__ part_db2, int ngroups,
+    const float* __restrict__ part1, int nblk1, float* __restrict__ g_w2,
+    float* __restrict__ g_b2, float* __restrict__ g_w1, float* __restrict__ g_b1) {
+  constexpr int N2 = 51200 + 64;
+  constexpr int B2 = (N2 + 255) / 256;
+  if ((int)blockIdx.x < B2) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N2) return;
+    float s = 0.f;
+    if (i < 51200) {
+      if (ngroups == 16) {
+#pragma unroll
+        for (int z = 0; z < 16; ++z) s += part2[(size_t)z * 51200 + i];
+      } else {
+        for (int z = 0; z < ngroups; ++z) s += part2[(size_t)z * 51200 + i];
+      }
+      g_w2[i] = s;
+    } else {
+      const int co = i - 51200;
+      for (int z = 0; z < 2 * ngroups; ++z) s += part_db2[z * 64 + co];
+      g_b2[co] = s;
+    }
+    return;
+  }
+  const int o = ((int)blockIdx.x - B2) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= 832) return;
+  float s = 0.f;
+  for (int b = lane; b < nblk1; b += 64) s += part1[(size_t)b * 832 + o];
+  s = wave_sum(s);
+  if (lane == 0) {
+    if (o < 800)
+      g_w1[o] = s;
+    else
+      g_b1[o - 800] = s;
+  }
+}
+
+}  // namespace mnist
+
+// ======================================================================
+// host launchers
+// ======================================================================
+namespace mnist {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// conv1: 128x32 tiles (4 waves stacked in M), K = 25 -> 32 (one K tile)
+#define C1_WM 4
+#define C1_WN 1
+#define C1_WK 1
+
+void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
+                      const float* w, const float* b, float* out, uint8_t* argmax,
+                      hipStream_t s) {
+  const int M = batch * 14 * 14 * 4;
+  const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
+  conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
+      <<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(data, step, n_local, batch, w, b, out,
+                                                      argmax);
+}
+
+void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
+                      uint8_t* argmax, float* w2t, hipStream_t s) {
+  conv2_fwd_v3_kernel<<<batch * 4, 256, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
+}
+
+int fc1_train_splits() { return FC1_SPLITS; }
+
+void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part,
+                          hipStream_t s) {
+  // 64x32 tiles, 2-way in-block K split, 14 split-K slabs of 224 (7 K tiles)
+  const int kchunk = FC1_IN / FC1_SPLITS;
+  dim3 grid(cdiv(batch, 64) * (FC1_OUT / 32), FC1_SPLITS);
+  fc1_fwd_kernel<2, 1, 2, 32, false><<<grid, 256, 0, s>>>(a2, w, nullptr, part, batch, kchunk, 0u,
+                                                          1.f);
+}
+
+void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
+                         uint32_t key, float keep_prob, hipStream_t s) {
+  dim3 grid(cdiv(M, 64) * (FC1_OUT / 64), 1);
+  fc1_fwd_kernel<2, 2, 1, 64, true><<<grid, 256, 0, s>>>(a2, w, b, h, M, FC1_IN, key, keep_prob);
+}
+
+void launch_fc_head_train(const float* part, const float* b3, const float* w4, const float* b4,
+                          const int* labels, int n_local, const long long* step, int batch,
+                          float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
+                          float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
+                          float* lr_out, int* correct, hipStream_t s) {
+  fc_head_train_kernel<<<batch, 256, 0, s>>>(part, b3, w4, b4, labels, n_local, step, batch,
+                                             keep_prob, seed, rank, base_lr, lr_decay, hd, dh,
+                                             dlog, loss_rows, lr_out, correct);
+}
+
+void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
+                         int M, float* logits, int* errors, hipStream_t s) {
+  fc_head_eval_kernel<<<cdiv(M, 4), 256, 0, s>>>(h, w4, b4, labels, M, logits, errors);
+}
+
+void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
+                    const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
+                    float* g_w4, float* g_b4, float* dy2, hipStream_t s) {
+  const int n_dx = cdiv(batch, 32) * (FC1_IN / 32);
+  const int n_dw = (FC1_IN / (32 * FC1BWD_DW_WM)) * (FC1_OUT / (32 * FC1BWD_DW_WN));
+  fc1_bwd_kernel<<<n_dx + n_dw + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
+                                                            g_w3, g_b3, g_w4, g_b4, dy2);
+}
+
+int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
+
+void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
+                      float* part2, hipStream_t s) {
+  const int G = conv2_filter_splits(batch);
+  float* part_db2 = part2 + (size_t)G * 51200;
+  conv2_bwd_kernel<<<batch * 4 + 25 * G, 256, 0, s>>>(a1, dy2, w2t, batch, da1m, part2, part_db2);
+}
+
+int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }
+
+void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
+                             const float* da1m, const uint8_t* idx1, float* part1,
+                             hipStream_t s) {
+  conv1_bwd_filter_kernel<<<conv1_filter_blocks(batch), 256, 0, s>>>(data, step, n_local, batch,
+                                                                     da1m, idx1, part1);
+}
+
+void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
+                          float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s) {
+  const int b2 = cdiv(51200 + 64, 256);
+  const int b1 = cdiv(832, 4);
+  grad_finalize_kernel<<<b2 + b1, 256, 0, s>>>(part2, part2 + (size_t)ngroups * 51200, ngroups,
+                                               part1, nblk1, g_w2, g_b2, g_w1, g_b1);
+}
+
+size_t part2_floats(int batch) { return (size_t)conv2_filter_splits(batch) * (51200 + 128); }
+size_t part1_floats(int batch) { return (size_t)conv1_filter_blocks(batch) * 832; }
+size_t fc1_part_floats(int batch) { return (size_t)FC1_SPLITS * batch * FC1_OUT; }
+
+}  // namespace mnist

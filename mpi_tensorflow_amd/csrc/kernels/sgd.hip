@@ -1,0 +1,74 @@
+// Flat-buffer momentum SGD (replaces TF ApplyMomentum x8 + AssignAdd + the
+// LR scalar ops of /root/reference/mpipy.py:59-66).
+//
+// One memory-bound pass over the whole flat parameter buffer, 16 B per lane:
+//   g   = grad * gscale (+ l2 * w on the L2-regularised FC prefix, mpipy.py:57)
+//   acc = momentum * acc + g            (TF1 ApplyMomentum, non-Nesterov)
+//   w  -= lr * acc
+// lr comes from the device (written by the fc head from the device step
+// counter), so the kernel is graph-replayable; one thread bumps the step.
+#include "common.h"
+#include "mnist.h"
+
+namespace optim {
+
+__global__ __launch_bounds__(256) void sgd_momentum_flat_kernel(
+    float4* __restrict__ w, const float4* __restrict__ g, float4* __restrict__ mom, long long n4,
+    long long l2_end4, float l2, float momentum, float gscale, const float* lr_ptr,
+    float lr_const, long long* step_ptr) {
+  const float lr = lr_ptr ? *lr_ptr : lr_const;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 wv = w[i], gv = g[i], mv = mom[i];
+    const float lc = i < l2_end4 ? l2 : 0.f;
+    gv.x = gv.x * gscale + lc * wv.x;
+    gv.y = gv.y * gscale + lc * wv.y;
+    gv.z = gv.z * gscale + lc * wv.z;
+    gv.w = gv.w * gscale + lc * wv.w;
+    mv.x = momentum * mv.x + gv.x;
+    mv.y = momentum * mv.y + gv.y;
+    mv.z = momentum * mv.z + gv.z;
+    mv.w = momentum * mv.w + gv.w;
+    wv.x -= lr * mv.x;
+    wv.y -= lr * mv.y;
+    wv.z -= lr * mv.z;
+    wv.w -= lr * mv.w;
+    w[i] = wv;
+    mom[i] = mv;
+  }
+  if (step_ptr && blockIdx.x == 0 && threadIdx.x == 0) *step_ptr += 1;
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(float4* __restrict__ x, long long n4, float a) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 v = x[i];
+    v.x *= a;
+    v.y *= a;
+    v.z *= a;
+    v.w *= a;
+    x[i] = v;
+  }
+}
+
+static inline int grid_for(long long n4) {
+  long long b = (n4 + 255) / 256;
+  return (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
+}
+
+void launch_sgd_momentum(float* w, const float* g, float* mom, long long n, long long l2_end,
+                         float l2, float momentum, float gscale, const float* lr_ptr,
+                         float lr_const, long long* step_ptr, hipStream_t s) {
+  const long long n4 = n / 4;
+  sgd_momentum_flat_kernel<<<grid_for(n4), 256, 0, s>>>(
+      reinterpret_cast<float4*>(w), reinterpret_cast<const float4*>(g),
+      reinterpret_cast<float4*>(mom), n4, l2_end / 4, l2, momentum, gscale, lr_ptr, lr_const,
+      step_ptr);
+}
+
+void launch_scale(float* x, long long n, float a, hipStream_t s) {
+  const long long n4 = n / 4;
+  scale_kernel<<<grid_for(n4), 256, 0, s>>>(reinterpret_cast<float4*>(x), n4, a);
+}
+
+}  // namespace optim

@@ -1,0 +1,106 @@
+#include "mnist_executor.h"
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels/common.h"
+#include "kernels/mnist.h"
+
+template <class T>
+static inline T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+
+MnistExecutor::MnistExecutor(const MnistPtrs& p) : p_(p) {
+  if (p_.batch <= 0 || p_.batch % 32 != 0)
+    throw std::runtime_error("MnistExecutor: batch must be a positive multiple of 32");
+  if (p_.n_local <= p_.batch)
+    throw std::runtime_error("MnistExecutor: local shard must exceed the batch");
+  if (p_.total % 4 != 0 || p_.l2_end % 4 != 0)
+    throw std::runtime_error("MnistExecutor: flat buffer sizes must be multiples of 4");
+  HIP_CHECK(hipEventCreateWithFlags(&ev_b1_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_b2_, hipEventDisableTiming));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+}
+
+MnistExecutor::~MnistExecutor() {
+  if (ev_b1_) (void)hipEventDestroy(ev_b1_);
+  if (ev_b2_) (void)hipEventDestroy(ev_b2_);
+  if (ev_done_) (void)hipEventDestroy(ev_done_);
+}
+
+void MnistExecutor::forward_backward(hipStream_t s) {
+  const MnistPtrs& p = p_;
+  float* W = P<float>(p.params);
+  float* G = P<float>(p.grads);
+  const long long* step = P<const long long>(p.step);
+  const int B = p.batch;
+  // forward
+  mnist::launch_conv1_fwd(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
+                          W + p.off_b1, P<float>(p.a1), P<uint8_t>(p.idx1), s);
+  mnist::launch_conv2_fwd(P<const float>(p.a1), B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
+                          P<uint8_t>(p.idx2), P<float>(p.w2t), s);
+  mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
+  mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
+                              W + p.off_b4, P<const int>(p.train_y), p.n_local, step, B,
+                              p.keep_prob, p.seed, p.rank, p.base_lr, p.lr_decay, P<float>(p.hd),
+                              P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
+                              P<float>(p.lr), P<int>(p.correct), s);
+  // backward: FC grads (bucket 1) first
+  mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
+                        P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
+                        G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
+                        s);
+}
+
+void MnistExecutor::sgd(hipStream_t s, float gscale) {
+  const MnistPtrs& p = p_;
+  optim::launch_sgd_momentum(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom), p.total,
+                             p.l2_end, p.l2, p.momentum, gscale, P<const float>(p.lr), 0.f,
+                             P<long long>(p.step), s);
+}
+
+void MnistExecutor::train_step(hipStream_t s, RcclComm* comm, hipStream_t cs) {
+  const MnistPtrs& p = p_;
+  float* G = P<float>(p.grads);
+  const int B = p.batch;
+  forward_backward(s);
+  const bool sync = comm != nullptr && comm->size() > 1;
+  if (sync) {  // bucket 1 overlaps the conv backward below
+    HIP_CHECK(hipEventRecord(ev_b1_, s));
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_b1_, 0));
+    comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
+  }
+  mnist::launch_conv2_bwd(P<const float>(p.a1), P<const float>(p.dy2), P<const float>(p.w2t), B,
+                          P<float>(p.da1m), P<float>(p.part2), s);
+  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), P<const long long>(p.step), p.n_local,
+                                 B, P<const float>(p.da1m), P<const uint8_t>(p.idx1),
+                                 P<float>(p.part1), s);
+  mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
+                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
+                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+  if (sync) {  // bucket 2 on the same (ordered) comm stream, then join
+    HIP_CHECK(hipEventRecord(ev_b2_, s));
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_b2_, 0));
+    comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
+                     ncclSum, cs);
+    HIP_CHECK(hipEventRecord(ev_done_, cs));
+    HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  }
+  sgd(s, sync ? 1.0f / (float)comm->size() : 1.0f);
+}
+
+void MnistExecutor::eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int M,
+                               uintptr_t ws_a1, uintptr_t ws_a2, uintptr_t ws_h, uintptr_t logits,
+                               uintptr_t errors, float keep_prob, uint32_t drop_key,
+                               hipStream_t s) {
+  const float* W = P<const float>(p.params);
+  mnist::launch_conv1_fwd(P<const float>(x), nullptr, 0, M, W + p.off_w1, W + p.off_b1,
+                          P<float>(ws_a1), nullptr, s);
+  mnist::launch_conv2_fwd(P<const float>(ws_a1), M, W + p.off_w2, W + p.off_b2, P<float>(ws_a2),
+                          nullptr, nullptr, s);
+  mnist::launch_fc1_fwd_eval(P<const float>(ws_a2), W + p.off_w3, W + p.off_b3, M, P<float>(ws_h),
+                             drop_key, keep_prob, s);
+  mnist::launch_fc_head_eval(P<const float>(ws_h), W + p.off_w4, W + p.off_b4, P<const int>(y), M,
+                             P<float>(logits), P<int>(errors), s);
+}

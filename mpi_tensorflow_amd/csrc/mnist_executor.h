@@ -1,0 +1,69 @@
+// Native training-step executor for the MNIST CNN.
+//
+// Replaces TF's Session.run(optimizer) step (/root/reference/mpipy.py:83-85)
+// plus the DP sync (:91, :95-153).  One call enqueues the whole step on a HIP
+// stream — fused forward, backward, all-reduce buckets, SGD — with no host
+// synchronisation, no allocation and no host-side step state: the batch
+// offset, dropout stream and LR are derived on the device from the device
+// step counter.  The call is therefore capturable into a hipGraph and the
+// Python trainer replays the captured graph.
+//
+// Gradient all-reduce (when a communicator is attached) runs in two buckets
+// on a dedicated comm stream:
+//   bucket 1 = FC params (97 % of the bytes), launched as soon as the fc1
+//              backward kernel has written them, overlapping the conv
+//              backward kernels on the compute stream;
+//   bucket 2 = conv params, after the final slab reduction.
+// The SGD kernel waits for both (event join) and divides by world size.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rccl_comm.h"
+
+struct MnistPtrs {
+  // dataset (device resident)
+  uintptr_t train_x = 0, train_y = 0;
+  int n_local = 0, batch = 64;
+  // flat buffers
+  uintptr_t params = 0, grads = 0, mom = 0;
+  long long total = 0, l2_end = 0, bucket1 = 0;  // floats
+  long long off_w4 = 0, off_b4 = 0, off_w3 = 0, off_b3 = 0, off_w2 = 0, off_b2 = 0, off_w1 = 0,
+            off_b1 = 0;
+  // device scalars
+  uintptr_t step = 0, lr = 0, correct = 0;
+  // activations / workspaces
+  uintptr_t a1 = 0, idx1 = 0, a2 = 0, idx2 = 0, fc1_part = 0, hd = 0, dh = 0, dlog = 0,
+            loss_rows = 0, dy2 = 0, da1m = 0, part2 = 0, part1 = 0, w2t = 0;
+  // hyper-parameters
+  float keep_prob = 0.5f, base_lr = 0.01f, lr_decay = 0.95f, l2 = 5e-4f, momentum = 0.9f;
+  uint32_t seed = 1, rank = 0;
+  int world = 1;
+};
+
+class MnistExecutor {
+ public:
+  explicit MnistExecutor(const MnistPtrs& p);
+  ~MnistExecutor();
+
+  // Full training step.  comm may be null (single rank, or periodic
+  // parameter averaging done by the caller); comm_stream is used only when
+  // comm is attached.
+  void train_step(hipStream_t s, RcclComm* comm, hipStream_t comm_stream);
+  // Forward+backward only (grads in the flat grad buffer; no sync, no SGD).
+  void forward_backward(hipStream_t s);
+  void sgd(hipStream_t s, float gscale);
+
+  // Evaluation of M rows starting at x (NHWC [M,28,28,1]): writes logits
+  // [M,10] when logits != 0 and adds the error count to *errors.  ws_* are
+  // caller-provided work buffers sized for `chunk` rows.
+  static void eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int M, uintptr_t ws_a1,
+                         uintptr_t ws_a2, uintptr_t ws_h, uintptr_t logits, uintptr_t errors,
+                         float keep_prob, uint32_t drop_key, hipStream_t s);
+
+  const MnistPtrs& ptrs() const { return p_; }
+
+ private:
+  MnistPtrs p_;
+  hipEvent_t ev_b1_ = nullptr, ev_b2_ = nullptr, ev_done_ = nullptr;
+};

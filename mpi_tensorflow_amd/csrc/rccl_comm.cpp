@@ -1,0 +1,141 @@
+#include "rccl_comm.h"
+
+#include <dlfcn.h>
+
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+
+namespace {
+
+struct RcclApi {
+  void* handle = nullptr;
+  decltype(&ncclGetUniqueId) getUniqueId = nullptr;
+  decltype(&ncclCommInitRank) commInitRank = nullptr;
+  decltype(&ncclCommDestroy) commDestroy = nullptr;
+  decltype(&ncclAllReduce) allReduce = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclReduce) reduce = nullptr;
+  decltype(&ncclAllGather) allGather = nullptr;
+  decltype(&ncclReduceScatter) reduceScatter = nullptr;
+  decltype(&ncclGroupStart) groupStart = nullptr;
+  decltype(&ncclGroupEnd) groupEnd = nullptr;
+  decltype(&ncclGetErrorString) getErrorString = nullptr;
+  decltype(&ncclGetVersion) getVersion = nullptr;
+};
+
+RcclApi g_api;
+std::mutex g_mu;
+
+template <class F>
+void sym(F& f, const char* name) {
+  f = reinterpret_cast<F>(dlsym(g_api.handle, name));
+  if (!f) throw std::runtime_error(std::string("RCCL symbol not found: ") + name);
+}
+
+void check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) {
+    const char* msg = g_api.getErrorString ? g_api.getErrorString(r) : "?";
+    throw std::runtime_error(std::string("RCCL ") + what + " failed: " + msg);
+  }
+}
+
+void require_loaded() {
+  if (!g_api.handle) throw std::runtime_error("RCCL not loaded: call RcclComm.load(path) first");
+}
+
+}  // namespace
+
+void RcclComm::load(const std::string& lib_path) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_api.handle) return;
+  void* h = dlopen(lib_path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+  if (!h) throw std::runtime_error(std::string("dlopen(") + lib_path + ") failed: " + dlerror());
+  g_api.handle = h;
+  sym(g_api.getUniqueId, "ncclGetUniqueId");
+  sym(g_api.commInitRank, "ncclCommInitRank");
+  sym(g_api.commDestroy, "ncclCommDestroy");
+  sym(g_api.allReduce, "ncclAllReduce");
+  sym(g_api.broadcast, "ncclBroadcast");
+  sym(g_api.reduce, "ncclReduce");
+  sym(g_api.allGather, "ncclAllGather");
+  sym(g_api.reduceScatter, "ncclReduceScatter");
+  sym(g_api.groupStart, "ncclGroupStart");
+  sym(g_api.groupEnd, "ncclGroupEnd");
+  sym(g_api.getErrorString, "ncclGetErrorString");
+  sym(g_api.getVersion, "ncclGetVersion");
+}
+
+bool RcclComm::loaded() { return g_api.handle != nullptr; }
+
+int RcclComm::version() {
+  require_loaded();
+  int v = 0;
+  check(g_api.getVersion(&v), "GetVersion");
+  return v;
+}
+
+std::vector<char> RcclComm::unique_id() {
+  require_loaded();
+  ncclUniqueId id;
+  check(g_api.getUniqueId(&id), "GetUniqueId");
+  std::vector<char> out(sizeof(id.internal));
+  std::memcpy(out.data(), id.internal, sizeof(id.internal));
+  return out;
+}
+
+RcclComm::RcclComm(const std::vector<char>& uid, int nranks, int rank)
+    : nranks_(nranks), rank_(rank) {
+  require_loaded();
+  ncclUniqueId id;
+  if (uid.size() != sizeof(id.internal)) throw std::runtime_error("bad RCCL unique id size");
+  std::memcpy(id.internal, uid.data(), sizeof(id.internal));
+  check(g_api.commInitRank(&comm_, nranks, id, rank), "CommInitRank");
+}
+
+RcclComm::~RcclComm() {
+  try {
+    destroy();
+  } catch (...) {
+  }
+}
+
+void RcclComm::destroy() {
+  if (comm_) {
+    ncclComm_t c = comm_;
+    comm_ = nullptr;
+    check(g_api.commDestroy(c), "CommDestroy");
+  }
+}
+
+void RcclComm::all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
+                          hipStream_t s) {
+  check(g_api.allReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, comm_, s),
+        "AllReduce");
+}
+
+void RcclComm::broadcast(const void* send, void* recv, size_t count, int dtype, int root,
+                         hipStream_t s) {
+  check(g_api.broadcast(send, recv, count, (ncclDataType_t)dtype, root, comm_, s), "Broadcast");
+}
+
+void RcclComm::reduce(const void* send, void* recv, size_t count, int dtype, int op, int root,
+                      hipStream_t s) {
+  check(g_api.reduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, root, comm_, s),
+        "Reduce");
+}
+
+void RcclComm::all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                          hipStream_t s) {
+  check(g_api.allGather(send, recv, send_count, (ncclDataType_t)dtype, comm_, s), "AllGather");
+}
+
+void RcclComm::reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                              hipStream_t s) {
+  check(g_api.reduceScatter(send, recv, recv_count, (ncclDataType_t)dtype, (ncclRedOp_t)op, comm_,
+                            s),
+        "ReduceScatter");
+}
+
+void RcclComm::group_start() { check(g_api.groupStart(), "GroupStart"); }
+void RcclComm::group_end() { check(g_api.groupEnd(), "GroupEnd"); }

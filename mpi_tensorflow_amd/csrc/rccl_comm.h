@@ -1,0 +1,48 @@
+// Native RCCL communicator (replaces the reference's mpi4py Scatter/Gather,
+// /root/reference/mpipy.py:121-127, :236-241).
+//
+// RCCL is resolved at run time with dlopen from the librccl that the
+// PyTorch-ROCm wheel already loaded (one HIP runtime and one RCCL per
+// process), so there is no link-time dependency and no second runtime.
+// Collectives are issued on a caller-provided HIP stream and are safe to
+// capture into a hipGraph (the training step replays them).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+class RcclComm {
+ public:
+  // Loads RCCL from `lib_path` (e.g. torch/lib/librccl.so).
+  static void load(const std::string& lib_path);
+  static bool loaded();
+  static std::vector<char> unique_id();
+  static int version();
+
+  RcclComm(const std::vector<char>& uid, int nranks, int rank);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+
+  // dtype: ncclDataType_t value; op: ncclRedOp_t value.
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s);
+  void broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s);
+  void reduce(const void* send, void* recv, size_t count, int dtype, int op, int root,
+              hipStream_t s);
+  void all_gather(const void* send, void* recv, size_t send_count, int dtype, hipStream_t s);
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                      hipStream_t s);
+  void group_start();
+  void group_end();
+  void destroy();
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int nranks_ = 0, rank_ = 0;
+};

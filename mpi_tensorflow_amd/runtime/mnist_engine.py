@@ -1,0 +1,330 @@
+"""Training-step engines for the MNIST CNN.
+
+Both engines own the same state - flat fp32 param / grad / momentum buffers
+(`parallel/flat.py` layout), a step counter and the rank's device-resident
+shard - and implement the same step semantics (reference `Cnn.run_process`
+body, `/root/reference/mpipy.py:79-85`, + optimizer `:59-66`):
+
+    offset = (step * B) % (N_local - B)                 (mpipy.py:80)
+    forward on train[offset:offset+B] with dropout      (mpipy.py:155-167)
+    grads of mean xent; SGD adds 5e-4*w on FC params    (mpipy.py:54-58)
+    [grad all-reduce / world size]                      (DP)
+    acc = 0.9 acc + g;  w -= lr(step) * acc;  step += 1 (mpipy.py:59-66)
+
+* `NativeMnistEngine` (GPU): the fused gfx950 HIP kernels driven by the C++
+  executor (`csrc/mnist_executor.cpp`); batch offset, dropout stream and LR
+  are computed on the device from the device step counter, so G steps are
+  captured ONCE into a hipGraph (torch.cuda.CUDAGraph) and replayed - no
+  per-step host work, no H2D copies (the dataset is device resident).
+* `TorchMnistEngine`: the plain-PyTorch fp32 oracle (CPU/gloo config 1 and
+  the numerics reference for the kernels); it draws the identical dropout
+  mask from utils/rng.py.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import config as C
+from ..models import mnist_cnn as M
+from ..ops import native, ptr, stream_handle
+from ..parallel.comm import DeviceComm
+from ..utils import rng
+from ..utils.data import batch_offset
+from ..utils.schedule import learning_rate
+
+
+class MnistEngineBase:
+    def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
+                 device: torch.device, rank: int = 0, world: int = 1,
+                 comm: Optional[DeviceComm] = None):
+        self.cfg = cfg
+        self.device = device
+        self.rank, self.world = rank, world
+        self.comm = comm
+        self.layout = M.layout()
+        self.B = cfg.batch_size
+        self.n_local = int(train_x.shape[0])
+        if self.n_local <= self.B:
+            raise ValueError(f"local shard of {self.n_local} rows must exceed batch {self.B}")
+        self.params = torch.zeros(self.layout.total, dtype=torch.float32, device=device)
+        self.grads = torch.zeros_like(self.params)
+        self.mom = torch.zeros_like(self.params)
+        host = torch.zeros(self.layout.total, dtype=torch.float32)
+        M.init_params(host, self.layout, seed=cfg.seed)
+        self.params.copy_(host)
+        self.step = 0  # host mirror of the global step (TF iter_)
+        self.drop_seed = cfg.seed
+        self.drop_rank = 0 if cfg.same_seed_all_ranks else rank  # quirk Q14
+        self.grad_sync = cfg.sync == "grad" and world > 1 and comm is not None
+
+    # views -----------------------------------------------------------------
+    def param_views(self) -> Dict[str, torch.Tensor]:
+        return self.layout.views(self.params)
+
+    def lr(self, step: Optional[int] = None) -> float:
+        s = self.step if step is None else step
+        return learning_rate(s, self.n_local, self.B, self.cfg.base_lr, self.cfg.lr_decay)
+
+    def l2_value(self) -> float:
+        p = self.param_views()
+        return float(self.cfg.l2 * M.l2_term(p).item())
+
+    def state_tensors(self):
+        return self.params, self.mom
+
+    def set_step(self, step: int) -> None:
+        self.step = int(step)
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+
+class TorchMnistEngine(MnistEngineBase):
+    """fp32 PyTorch oracle engine (CPU or GPU)."""
+
+    kind = "torch"
+
+    def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None):
+        super().__init__(cfg, train_x, train_y, device, rank, world, comm)
+        self.train_x = torch.from_numpy(np.ascontiguousarray(train_x, np.float32)).to(device)
+        self.train_y = torch.from_numpy(np.asarray(train_y).astype(np.int64)).to(device)
+        self.last_loss = float("nan")
+
+    def dropout_mask(self, step: int, rows: int, salt: int = 0) -> torch.Tensor:
+        key = rng.dropout_key(self.drop_seed, self.drop_rank, step, salt)
+        return rng.keep_mask_torch(key, (rows, M.FC1_OUT), self.cfg.dropout_keep, self.device)
+
+    def forward_backward(self, step: int):
+        off = batch_offset(step, self.n_local, self.B)
+        x = self.train_x[off:off + self.B]
+        y = self.train_y[off:off + self.B]
+        views = {k: v.detach().clone().requires_grad_(True) for k, v in self.param_views().items()}
+        logits = M.forward(views, x, self.dropout_mask(step, self.B), self.cfg.dropout_keep)
+        data_loss = torch.nn.functional.cross_entropy(logits, y)
+        grads = torch.autograd.grad(data_loss, [views[s.name] for s in self.layout.specs])
+        gv = self.layout.views(self.grads)
+        for s, g in zip(self.layout.specs, grads):
+            gv[s.name].copy_(g)
+        self.last_loss = float(data_loss.item())
+        return data_loss
+
+    def train(self, k: int) -> None:
+        for _ in range(k):
+            self.forward_backward(self.step)
+            gscale = 1.0
+            if self.grad_sync:
+                self.comm.all_reduce_(self.grads)
+                gscale = 1.0 / self.world
+            lr = self.lr(self.step)
+            _, l2_end = self.layout.l2_range()
+            g = self.grads * gscale
+            g[:l2_end] += self.cfg.l2 * self.params[:l2_end]
+            self.mom.mul_(self.cfg.momentum).add_(g)
+            self.params.sub_(lr * self.mom)
+            self.step += 1
+
+    def loss_value(self) -> float:
+        return self.last_loss + self.l2_value()
+
+    @torch.no_grad()
+    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 2000, dropout: bool = False):
+        views = self.param_views()
+        wrong = 0
+        for a in range(0, x.shape[0], chunk):
+            xb = torch.from_numpy(x[a:a + chunk]).to(self.device)
+            mask = None
+            if dropout:
+                mask = self.dropout_mask(self.step, xb.shape[0], rng.EVAL_SALT)
+            pred = M.forward(views, xb, mask, self.cfg.dropout_keep).argmax(1).cpu().numpy()
+            wrong += int((pred != y[a:a + chunk]).sum())
+        return 100.0 * wrong / max(1, x.shape[0])
+
+
+class NativeMnistEngine(MnistEngineBase):
+    """fused HIP kernels + C++ executor + hipGraph replay (MI355X)."""
+
+    kind = "native"
+
+    def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None):
+        super().__init__(cfg, train_x, train_y, device, rank, world, comm)
+        if device.type != "cuda":
+            raise RuntimeError("NativeMnistEngine needs a GPU")
+        if self.B % 32 != 0:
+            raise ValueError("native MNIST engine needs a batch size that is a multiple of 32")
+        C_ = native()
+        self._C = C_
+        dev = device
+        B = self.B
+        f32 = dict(dtype=torch.float32, device=dev)
+        u8 = dict(dtype=torch.uint8, device=dev)
+        self.train_x = torch.from_numpy(np.ascontiguousarray(train_x, np.float32)).to(dev)
+        self.train_y = torch.from_numpy(np.ascontiguousarray(train_y).astype(np.int32)).to(dev)
+        assert self.train_x.shape[1:] == (28, 28, 1)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.lr_dev = torch.zeros(1, **f32)
+        self.correct_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        k = C_.mnist
+        self.bufs = dict(
+            a1=torch.empty(B * 14 * 14 * 32, **f32), idx1=torch.empty(B * 14 * 14 * 32, **u8),
+            a2=torch.empty(B * M.FC1_IN, **f32), idx2=torch.empty(B * M.FC1_IN, **u8),
+            fc1_part=torch.empty(k.fc1_part_floats(B), **f32),
+            hd=torch.empty(B * M.FC1_OUT, **f32), dh=torch.empty(B * M.FC1_OUT, **f32),
+            dlog=torch.empty(B * 10, **f32), loss_rows=torch.zeros(B, **f32),
+            dy2=torch.empty(B * 14 * 14 * 64, **f32), da1m=torch.empty(B * 14 * 14 * 32, **f32),
+            part2=torch.empty(k.part2_floats(B), **f32), part1=torch.empty(k.part1_floats(B), **f32),
+            w2t=torch.empty(25 * 64 * 32, **f32),
+        )
+        p = C_.MnistPtrs()
+        p.train_x, p.train_y = ptr(self.train_x), ptr(self.train_y)
+        p.n_local, p.batch = self.n_local, B
+        p.params, p.grads, p.mom = ptr(self.params), ptr(self.grads), ptr(self.mom)
+        lay = self.layout
+        p.total = lay.total
+        p.l2_end = lay.l2_range()[1]
+        p.bucket1 = lay.buckets()[0][1]
+        for attr, name in (("off_w4", "fc2_weight"), ("off_b4", "fc2_bias"), ("off_w3", "fc1_weight"),
+                           ("off_b3", "fc1_bias"), ("off_w2", "conv2_weight"), ("off_b2", "conv2_bias"),
+                           ("off_w1", "conv1_weight"), ("off_b1", "conv1_bias")):
+            setattr(p, attr, lay.offsets[name])
+        p.step, p.lr, p.correct = ptr(self.step_dev), ptr(self.lr_dev), ptr(self.correct_dev)
+        for name, t in self.bufs.items():
+            setattr(p, name, ptr(t))
+        p.keep_prob, p.base_lr, p.lr_decay = cfg.dropout_keep, cfg.base_lr, cfg.lr_decay
+        p.l2, p.momentum = cfg.l2, cfg.momentum
+        p.seed, p.rank, p.world = cfg.seed, self.drop_rank, world
+        self.ptrs = p
+        self.exe = C_.MnistExecutor(p)
+        self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
+        self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
+        if self.grad_sync and self._native_comm is None:
+            raise RuntimeError("grad sync on the native engine needs the native RCCL communicator")
+        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
+        self.use_graph = cfg.graph
+        self.graph_steps = max(1, cfg.graph_steps)
+        self._eval_ws = None
+        if self.grad_sync:  # connection setup outside any capture
+            self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), lay.total,
+                                         7, 0, stream_handle())
+            torch.cuda.synchronize(dev)
+
+    def set_step(self, step: int) -> None:
+        super().set_step(step)
+        self.step_dev.fill_(int(step))
+
+    # --------------------------------------------------------------- steps
+    def _launch_one(self):
+        cs = stream_handle(self.comm_stream) if self.comm_stream is not None else 0
+        self.exe.train_step(stream_handle(), self._native_comm, cs)
+
+    def _graph(self, n: int) -> torch.cuda.CUDAGraph:
+        g = self._graphs.get(n)
+        if g is None:
+            if self.comm_stream is not None:
+                self.comm_stream.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self._launch_one()
+            self._graphs[n] = g
+        return g
+
+    def train(self, k: int) -> None:
+        if k <= 0:
+            return
+        if not self.use_graph:
+            for _ in range(k):
+                self._launch_one()
+        else:
+            G = self.graph_steps
+            full, rem = divmod(k, G)
+            if full:
+                g = self._graph(G)
+                for _ in range(full):
+                    g.replay()
+            if rem:
+                self._graph(rem).replay()
+        self.step += k
+
+    def capture(self, k: int) -> None:
+        """Pre-captures the graphs `train(k)` will replay (outside timing)."""
+        if self.use_graph:
+            G = self.graph_steps
+            if k >= G:
+                self._graph(G)
+            if k % G:
+                self._graph(k % G)
+
+    def forward_backward_only(self) -> None:
+        self.exe.forward_backward(stream_handle())
+        self.exe_backward_rest()
+
+    def exe_backward_rest(self):
+        """conv backward + finalize without sync/SGD (used by numerics tests)."""
+        C_ = self._C
+        p, b, B = self.ptrs, self.bufs, self.B
+        s = stream_handle()
+        W, G = self.params, self.grads
+        lay = self.layout
+        C_.mnist.conv2_bwd(ptr(b["a1"]), ptr(b["dy2"]), ptr(b["w2t"]), B,
+                           ptr(b["da1m"]), ptr(b["part2"]), s)
+        C_.mnist.conv1_bwd_filter(ptr(self.train_x), ptr(self.step_dev), self.n_local, B,
+                                  ptr(b["da1m"]), ptr(b["idx1"]), ptr(b["part1"]), s)
+        C_.mnist.grad_finalize(ptr(b["part2"]), C_.mnist.conv2_filter_splits(B), ptr(b["part1"]),
+                               C_.mnist.conv1_filter_blocks(B),
+                               ptr(G) + 4 * lay.offsets["conv2_weight"],
+                               ptr(G) + 4 * lay.offsets["conv2_bias"],
+                               ptr(G) + 4 * lay.offsets["conv1_weight"],
+                               ptr(G) + 4 * lay.offsets["conv1_bias"], s)
+
+    def loss_value(self) -> float:
+        return float(self.bufs["loss_rows"].mean().item()) + self.l2_value()
+
+    def device_lr(self) -> float:
+        return float(self.lr_dev.item())
+
+    # ---------------------------------------------------------------- eval
+    @torch.no_grad()
+    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 2000, dropout: bool = False,
+                 x_dev: Optional[torch.Tensor] = None, y_dev: Optional[torch.Tensor] = None,
+                 return_logits: bool = False):
+        dev = self.device
+        if x_dev is None:
+            x_dev = torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(dev)
+            y_dev = torch.from_numpy(np.ascontiguousarray(y).astype(np.int32)).to(dev)
+        n = int(x_dev.shape[0])
+        chunk = min(chunk, max(n, 1))
+        if self._eval_ws is None or self._eval_ws[0] < chunk:
+            f32 = dict(dtype=torch.float32, device=dev)
+            self._eval_ws = (chunk, torch.empty(chunk * 14 * 14 * 32, **f32),
+                             torch.empty(chunk * M.FC1_IN, **f32),
+                             torch.empty(chunk * M.FC1_OUT, **f32))
+        _, a1, a2, h = self._eval_ws
+        errors = torch.zeros(1, dtype=torch.int32, device=dev)
+        logits = torch.empty(n, 10, dtype=torch.float32, device=dev) if return_logits else None
+        keep = self.cfg.dropout_keep if dropout else 1.0
+        key = rng.dropout_key(self.drop_seed, self.drop_rank, self.step, rng.EVAL_SALT)
+        s = stream_handle()
+        for a in range(0, n, chunk):
+            m = min(chunk, n - a)
+            lg = ptr(logits) + 4 * 10 * a if logits is not None else 0
+            self._C.MnistExecutor.eval_chunk(self.ptrs, ptr(x_dev) + 4 * 784 * a, ptr(y_dev) + 4 * a,
+                                             m, ptr(a1), ptr(a2), ptr(h), lg, ptr(errors), keep,
+                                             key, s)
+        err = 100.0 * float(errors.item()) / max(1, n)
+        return (err, logits) if return_logits else err
+
+
+def make_engine(cfg: C.TrainConfig, train_x, train_y, device: torch.device, rank=0, world=1,
+                comm=None, backend: Optional[str] = None):
+    backend = backend or cfg.backend
+    if backend == "auto":
+        backend = "native" if device.type == "cuda" else "torch"
+    if backend == "native":
+        return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm)
+    return TorchMnistEngine(cfg, train_x, train_y, device, rank, world, comm)

@@ -1,0 +1,205 @@
+"""The training driver: the reference's `main()` + `Cnn` re-built around the
+engines (`/root/reference/mpipy.py:201-244` main, `:24-93` Cnn).
+
+Flow (reference line refs in brackets):
+  1. acquisition on rank 0 only, then a barrier            [:203-206; fixes Q3]
+  2. rank/world from the launcher, GPU bound to local rank  [:208-210; fixes Q13]
+  3. each rank loads/generates only its shard               [:211-241 Scatter x6]
+  4. engine = fused HIP kernels (GPU) or PyTorch oracle (CPU)
+  5. "Process ID: r  training session starts!"              [:77]
+  6. steps = epochs * N_local // B                          [:79]
+     - train segments run as replays of captured step graphs
+     - every `eval_every` steps: local test error + reference log line [:86-90]
+     - every `sync_every` steps in param_avg mode: weight averaging    [:91]
+  7. final evaluation, throughput summary, optional checkpoint.
+
+Training throughput excludes evaluation (the reference spends ~98 % of its
+wall time evaluating every step); eval time is reported apart.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import time
+from typing import Dict, Optional
+
+import torch
+
+from .. import config as C
+from ..parallel import dist as D
+from ..parallel.comm import make_comm
+from ..parallel.sync import average_params, average_params_root_only
+from ..utils import checkpoint as ckpt_mod
+from ..utils.data import (data_exist_here, load_mnist_shard, local_train_rows, mnist_files_present,
+                          steps_per_run, synthetic_image_shard)
+from ..utils.logging import MetricsWriter, emit, progress_line, start_line
+
+
+@dataclasses.dataclass
+class RunSummary:
+    model: str
+    world: int
+    steps: int
+    batch: int
+    images: int
+    train_seconds: float
+    eval_seconds: float
+    images_per_sec_local: float
+    images_per_sec_global: float
+    final_test_error_local: float
+    final_test_error_global: float
+    final_loss: float
+    final_lr: float
+    engine: str
+    comm: str
+    synthetic: bool
+
+    def as_dict(self) -> Dict:
+        return dataclasses.asdict(self)
+
+
+class Trainer:
+    def __init__(self, cfg: C.TrainConfig, di: Optional[D.DistInfo] = None):
+        self.cfg = cfg.validate()
+        self.device = D.resolve_device(cfg.device)
+        self.di = di or D.init(str(self.device))
+        self.rank, self.world = self.di.rank, self.di.world
+        self._prepare_data()
+        self.comm = make_comm(self.di, self.device) if self.world > 1 else None
+        self.engine = self._make_engine()
+        if cfg.resume:
+            step, _ = ckpt_mod.load(cfg.resume, self.engine.layout, self.engine.params,
+                                    self.engine.mom)
+            self.engine.set_step(step)
+        self.metrics = MetricsWriter(cfg.metrics_jsonl, self.rank)
+
+    # ------------------------------------------------------------------ data
+    def _prepare_data(self):
+        cfg = self.cfg
+        if cfg.model == "mnist_cnn":
+            if self.rank == 0 and cfg.download and not mnist_files_present(cfg.data_dir):
+                for f in C.MNIST_FILES.values():
+                    data_exist_here(f, cfg.data_dir, download=True)
+            D.barrier()
+            self.shard = load_mnist_shard(self.rank, self.world, cfg.data_dir, cfg.synthetic,
+                                          pad=cfg.pad_train_shard, seed=cfg.seed)
+        else:
+            from ..models.generic import model_input_shape
+
+            shape = model_input_shape(cfg.model)
+            rows = 4096 if cfg.model == "lenet5" else 512
+            self.shard = synthetic_image_shard(self.rank, self.world, rows, rows // 4, shape,
+                                               seed=cfg.seed)
+        if self.shard.test_x.shape[0] < 1:
+            raise ValueError("empty local test shard")
+
+    def _make_engine(self):
+        cfg = self.cfg
+        sh = self.shard
+        if cfg.model == "mnist_cnn":
+            from .mnist_engine import make_engine
+
+            return make_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
+                               self.comm)
+        from .generic_engine import GenericEngine
+
+        return GenericEngine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
+                             self.comm)
+
+    # ------------------------------------------------------------------- run
+    def total_steps(self) -> int:
+        if self.cfg.max_steps is not None:
+            return int(self.cfg.max_steps)
+        return steps_per_run(self.engine.n_local, self.cfg.epochs, self.cfg.batch_size)
+
+    def _event(self, s: int) -> bool:
+        cfg = self.cfg
+        if s <= 0:
+            return False
+        ev = cfg.effective_eval_every()
+        if ev and s % ev == 0:
+            return True
+        if cfg.sync == "param_avg" and self.world > 1 and s % cfg.sync_every == 0:
+            return True
+        if cfg.ckpt and cfg.ckpt_every and s % cfg.ckpt_every == 0:
+            return True
+        return False
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def evaluate(self, dropout: Optional[bool] = None) -> float:
+        d = self.cfg.eval_dropout if dropout is None else dropout
+        return self.engine.evaluate(self.shard.test_x, self.shard.test_y, dropout=d)
+
+    def run(self) -> RunSummary:
+        cfg, eng = self.cfg, self.engine
+        emit(start_line(self.rank), cfg.quiet)
+        steps = self.total_steps()
+        s = eng.step
+        train_t = 0.0
+        eval_t = 0.0
+        trained = 0
+        while s < steps:
+            nxt = s
+            while nxt < steps - 1 and not self._event(nxt):
+                nxt += 1
+            k = nxt - s + 1
+            self._sync()
+            t0 = time.perf_counter()
+            eng.train(k)
+            self._sync()
+            train_t += time.perf_counter() - t0
+            trained += k
+            s += k
+            last = s - 1
+            if not self._event(last):
+                continue
+            ev = cfg.effective_eval_every()
+            if ev and last % ev == 0:
+                t1 = time.perf_counter()
+                err = self.evaluate()
+                eval_t += time.perf_counter() - t1
+                if last % (cfg.sync_every if cfg.reference_quirks else ev) == 0:
+                    emit(progress_line(self.rank, last, err), cfg.quiet)
+                    self.metrics.write(step=last, test_error=err, loss=eng.loss_value(),
+                                       lr=eng.lr(last), train_seconds=train_t,
+                                       images_per_sec=trained * cfg.batch_size / max(train_t, 1e-9))
+            if cfg.sync == "param_avg" and self.world > 1 and last % cfg.sync_every == 0:
+                t2 = time.perf_counter()
+                if cfg.root_only_average:
+                    average_params_root_only(self.comm, eng.layout, eng.params)
+                else:
+                    average_params(self.comm, eng.params)
+                self._sync()
+                train_t += time.perf_counter() - t2
+            if cfg.ckpt and cfg.ckpt_every and last % cfg.ckpt_every == 0:
+                self.save_checkpoint(cfg.ckpt)
+        t1 = time.perf_counter()
+        final_err = self.evaluate()
+        eval_t += time.perf_counter() - t1
+        n_test = self.shard.test_x.shape[0]
+        wrong_g = D.allreduce_sum_host(final_err * n_test / 100.0)
+        n_g = D.allreduce_sum_host(float(n_test))
+        train_t_max = D.allreduce_max_host(train_t)
+        images = trained * cfg.batch_size
+        summary = RunSummary(
+            model=cfg.model, world=self.world, steps=trained, batch=cfg.batch_size, images=images,
+            train_seconds=train_t, eval_seconds=eval_t,
+            images_per_sec_local=images / max(train_t, 1e-9),
+            images_per_sec_global=images * self.world / max(train_t_max, 1e-9),
+            final_test_error_local=final_err, final_test_error_global=100.0 * wrong_g / max(n_g, 1),
+            final_loss=eng.loss_value(), final_lr=eng.lr(max(0, s - 1)), engine=eng.kind,
+            comm=getattr(self.comm, "kind", "none"), synthetic=self.shard.synthetic)
+        self.metrics.write(final=True, **summary.as_dict())
+        if cfg.ckpt:
+            self.save_checkpoint(cfg.ckpt)
+        self.metrics.close()
+        return summary
+
+    def save_checkpoint(self, path: str) -> None:
+        if self.rank == 0:
+            ckpt_mod.save(path, self.engine.layout, self.engine.params, self.engine.mom,
+                          self.engine.step, meta={"model": self.cfg.model, "world": self.world})
+        D.barrier()

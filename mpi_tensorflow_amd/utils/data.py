@@ -1,0 +1,255 @@
+"""Data layer: acquisition, sizing/splitting, per-rank sharding, synthetic data.
+
+Reference behaviour (`/root/reference/mpipy.py`):
+  * `data_exist_here` (`:185-199`) creates ./data and downloads missing MNIST
+    files; every rank calls it concurrently (quirk Q3) and the error handler
+    names an undefined exception (Q4).
+  * sizing (`:211-213`): tr_size = 55000//P*P, ts_size = 10000//P*P,
+    val_size = 5000//P*P.
+  * rank 0 reads 60000 train + ts_size test rows (`:215-218`); validation =
+    first val_size train rows, train = rows [val_size, tr_size) (`:219-222`).
+  * `comm.Scatter` x6 (`:236-241`) hands every rank a contiguous chunk.  The
+    train receive buffer is tr_size//P rows but only (tr_size-val_size)/P rows
+    are sent, so the tail stays zero (Q5).
+
+Here every rank loads or generates ONLY its own shard (deterministic row
+ranges), so no collective is needed; rank 0 alone touches the network/disk
+for acquisition and the others wait at a barrier (fixes Q3/Q4).  With no
+MNIST files on disk (the GPU pool has no network) a deterministic synthetic
+MNIST-shaped dataset is used instead: same shapes, dtypes and value range,
+class-conditional so that accuracy is meaningful.
+"""
+
+from __future__ import annotations
+
+import dataclasses
+import os
+import urllib.request
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from .. import config as C
+from .idx import extract_data, extract_labels
+
+
+# ---------------------------------------------------------------- sizing --
+@dataclasses.dataclass(frozen=True)
+class SplitSizes:
+    world: int
+    tr_size: int
+    ts_size: int
+    val_size: int
+
+    @property
+    def train_rows(self) -> int:  # rows actually scattered (mpipy.py:221-222)
+        return self.tr_size - self.val_size
+
+    @property
+    def train_local(self) -> int:  # real rows per rank
+        return self.train_rows // self.world
+
+    @property
+    def train_local_padded(self) -> int:  # receive-buffer rows (mpipy.py:230)
+        return self.tr_size // self.world
+
+    @property
+    def test_local(self) -> int:
+        return self.ts_size // self.world
+
+    @property
+    def val_local(self) -> int:
+        return self.val_size // self.world
+
+
+def split_sizes(world: int, train_rows: int = C.TRAIN_ROWS, test_rows: int = C.TEST_ROWS,
+                val_rows: int = C.VAL_ROWS) -> SplitSizes:
+    """mpipy.py:211-213 rounding of the global splits to multiples of P."""
+    if world <= 0:
+        raise ValueError("world size must be positive")
+    return SplitSizes(world, train_rows // world * world, test_rows // world * world,
+                      val_rows // world * world)
+
+
+def local_train_rows(sizes: SplitSizes, pad: bool) -> int:
+    """N_local: the row count that drives steps/epoch and the LR decay period
+    (mpipy.py:62, :79 use train_data.shape[0]).  Q5 padding => tr_size//P."""
+    return sizes.train_local_padded if pad else sizes.train_local
+
+
+def steps_per_run(n_local: int, epochs: int = C.ITERATION, batch: int = C.BATCH_SIZE) -> int:
+    """mpipy.py:79: iteration * N_local // batch_size."""
+    return epochs * n_local // batch
+
+
+def batch_offset(step: int, n_local: int, batch: int = C.BATCH_SIZE) -> int:
+    """mpipy.py:80: (step * batch) % (N_local - batch)  (quirk Q16 kept)."""
+    if n_local <= batch:
+        raise ValueError(f"local shard ({n_local} rows) must exceed the batch ({batch})")
+    return (step * batch) % (n_local - batch)
+
+
+def num_syncs(steps: int, every: int = C.SYNC_EVERY) -> int:
+    """How many periodic syncs a run performs (step>0 and step%every==0)."""
+    return max(0, (steps - 1) // every)
+
+
+def shard_ranges(sizes: SplitSizes, rank: int) -> Dict[str, Tuple[int, int]]:
+    """Global row ranges [start, stop) this rank owns, per split, in the
+    coordinates of the files (train/val index the 60000-row train file)."""
+    if not 0 <= rank < sizes.world:
+        raise ValueError(f"rank {rank} outside world {sizes.world}")
+    tl, sl, vl = sizes.train_local, sizes.test_local, sizes.val_local
+    return {
+        "train": (sizes.val_size + rank * tl, sizes.val_size + (rank + 1) * tl),
+        "test": (rank * sl, (rank + 1) * sl),
+        "val": (rank * vl, (rank + 1) * vl),
+    }
+
+
+# ----------------------------------------------------------- acquisition --
+def data_exist_here(data_file_name: str, data_dir: str = "data", download: bool = False,
+                    url: str = C.DATA_URL) -> str:
+    """mpipy.py:185-199 without the bugs: call on ONE rank, raise a real error."""
+    os.makedirs(data_dir, exist_ok=True)
+    path = os.path.join(data_dir, data_file_name)
+    if not os.path.exists(path) and download:
+        tmp = path + ".part"
+        try:
+            urllib.request.urlretrieve(url + data_file_name, tmp)
+            os.replace(tmp, path)
+        except Exception as e:  # pragma: no cover - no network in CI
+            if os.path.exists(tmp):
+                os.remove(tmp)
+            raise RuntimeError(f"download of {data_file_name} failed: {e}") from e
+    return path
+
+
+def mnist_files_present(data_dir: str) -> bool:
+    return all(os.path.exists(os.path.join(data_dir, f)) for f in C.MNIST_FILES.values())
+
+
+# ------------------------------------------------------------- synthetic --
+_SYN_CHUNK = 1000
+
+
+def _prototypes(seed: int, classes: int, h: int, w: int, c: int) -> np.ndarray:
+    """Class templates: thresholded smooth random fields (stroke-like masks)."""
+    rng = np.random.default_rng([seed, 7919, classes, h, w, c])
+    coarse = rng.standard_normal((classes, max(2, h // 4), max(2, w // 4), c))
+    # nearest-neighbour upsample + 3x3 box blur -> blobs
+    up = np.repeat(np.repeat(coarse, int(np.ceil(h / coarse.shape[1])), 1),
+                   int(np.ceil(w / coarse.shape[2])), 2)[:, :h, :w, :]
+    pad = np.pad(up, ((0, 0), (1, 1), (1, 1), (0, 0)), mode="edge")
+    blur = sum(pad[:, dy:dy + h, dx:dx + w, :] for dy in range(3) for dx in range(3)) / 9.0
+    thr = np.quantile(blur.reshape(classes, -1), 0.78, axis=1).reshape(classes, 1, 1, 1)
+    return (blur > thr).astype(np.float32)
+
+
+def _synthetic_chunk(kind: str, chunk: int, seed: int, classes: int,
+                     shape: Tuple[int, int, int]) -> Tuple[np.ndarray, np.ndarray]:
+    h, w, c = shape
+    protos = _prototypes(seed, classes, h, w, c)
+    kid = {"train": 1, "test": 2}[kind]
+    rng = np.random.default_rng([seed, kid, chunk, h, w, c])
+    n = _SYN_CHUNK
+    labels = rng.integers(0, classes, size=n).astype(np.int64)
+    imgs = protos[labels]  # [n,h,w,c]
+    # random translation by up to +-2 pixels, done per shift group
+    sy = rng.integers(-2, 3, size=n)
+    sx = rng.integers(-2, 3, size=n)
+    out = np.empty_like(imgs)
+    for dy in range(-2, 3):
+        for dx in range(-2, 3):
+            sel = np.nonzero((sy == dy) & (sx == dx))[0]
+            if sel.size:
+                out[sel] = np.roll(imgs[sel], (dy, dx), axis=(1, 2))
+    noise = rng.standard_normal(out.shape).astype(np.float32)
+    u8 = np.clip((0.85 * out + 0.22 * noise + 0.05) * 255.0, 0, 255).astype(np.uint8)
+    return u8, labels
+
+
+def synthetic_rows(kind: str, start: int, stop: int, seed: int = C.SEED,
+                   classes: int = C.NUM_CLASSES,
+                   shape: Tuple[int, int, int] = (C.IMAGE_SIZE, C.IMAGE_SIZE, 1)
+                   ) -> Tuple[np.ndarray, np.ndarray]:
+    """Rows [start, stop) of the deterministic synthetic split `kind`, as
+    (float32 images in [-0.5, 0.5] NHWC, int64 labels).  Row r is the same
+    no matter which rank or world size asks for it."""
+    if stop <= start:
+        h, w, c = shape
+        return np.zeros((0, h, w, c), np.float32), np.zeros((0,), np.int64)
+    xs, ys = [], []
+    for ch in range(start // _SYN_CHUNK, (stop - 1) // _SYN_CHUNK + 1):
+        u8, lab = _synthetic_chunk(kind, ch, seed, classes, shape)
+        lo = max(start, ch * _SYN_CHUNK) - ch * _SYN_CHUNK
+        hi = min(stop, (ch + 1) * _SYN_CHUNK) - ch * _SYN_CHUNK
+        xs.append(u8[lo:hi])
+        ys.append(lab[lo:hi])
+    u8 = np.concatenate(xs)
+    x = (u8.astype(np.float32) - C.PIXEL_DEPTH / 2.0) / C.PIXEL_DEPTH
+    return x, np.concatenate(ys)
+
+
+# -------------------------------------------------------------- shards --
+@dataclasses.dataclass
+class Shard:
+    train_x: np.ndarray
+    train_y: np.ndarray
+    test_x: np.ndarray
+    test_y: np.ndarray
+    val_x: np.ndarray
+    val_y: np.ndarray
+    synthetic: bool
+    sizes: SplitSizes
+
+    @property
+    def n_local(self) -> int:
+        return self.train_x.shape[0]
+
+
+def load_mnist_shard(rank: int, world: int, data_dir: str = "data",
+                     synthetic: Optional[bool] = None, pad: bool = False,
+                     seed: int = C.SEED) -> Shard:
+    """This rank's train/test/val rows (what the reference's six Scatters
+    deliver, mpipy.py:230-241)."""
+    sizes = split_sizes(world)
+    rng_ = shard_ranges(sizes, rank)
+    use_syn = (not mnist_files_present(data_dir)) if synthetic is None else synthetic
+    if use_syn:
+        tx, ty = synthetic_rows("train", *rng_["train"], seed=seed)
+        sx, sy = synthetic_rows("test", *rng_["test"], seed=seed)
+        vx, vy = synthetic_rows("train", *rng_["val"], seed=seed)
+    else:
+        f = {k: os.path.join(data_dir, v) for k, v in C.MNIST_FILES.items()}
+        a, b = rng_["train"]
+        tx = extract_data(f["train_images"], b)[a:]
+        ty = extract_labels(f["train_labels"], b)[a:]
+        a, b = rng_["test"]
+        sx = extract_data(f["test_images"], b)[a:]
+        sy = extract_labels(f["test_labels"], b)[a:]
+        a, b = rng_["val"]
+        vx = extract_data(f["train_images"], b)[a:]
+        vy = extract_labels(f["train_labels"], b)[a:]
+    if pad:  # quirk Q5: receive buffer tr_size//P rows, tail left zero
+        n_pad = sizes.train_local_padded
+        px = np.zeros((n_pad,) + tx.shape[1:], np.float32)
+        py = np.zeros((n_pad,), np.int64)
+        px[: tx.shape[0]] = tx
+        py[: ty.shape[0]] = ty
+        tx, ty = px, py
+    return Shard(np.ascontiguousarray(tx, np.float32), ty, np.ascontiguousarray(sx, np.float32), sy,
+                 np.ascontiguousarray(vx, np.float32), vy, use_syn, sizes)
+
+
+def synthetic_image_shard(rank: int, world: int, rows_per_rank: int, test_per_rank: int,
+                          shape: Tuple[int, int, int], classes: int = 10,
+                          seed: int = C.SEED) -> Shard:
+    """Synthetic CIFAR-shaped (32x32x3) or ImageNet-shaped (224x224x3) shard
+    for the LeNet-5 / ResNet-18 configs (BASELINE.json configs 4-5)."""
+    a = rank * rows_per_rank
+    tx, ty = synthetic_rows("train", a, a + rows_per_rank, seed, classes, shape)
+    b = rank * test_per_rank
+    sx, sy = synthetic_rows("test", b, b + test_per_rank, seed, classes, shape)
+    sizes = SplitSizes(world, rows_per_rank * world, test_per_rank * world, 0)
+    return Shard(tx, ty, sx, sy, sx[:0], sy[:0], True, sizes)

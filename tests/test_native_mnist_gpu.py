@@ -1,0 +1,147 @@
+"""Numerics of the fused gfx950 MNIST kernels vs the plain-PyTorch fp32 oracle.
+
+Each test runs the HIP path (`_C`, loaded in-tree) and compares against
+`models/mnist_cnn.py` evaluated with torch ops in fp32 on the same inputs,
+the same weights and the same dropout mask (utils/rng.py).
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mpi_tensorflow_amd import config as C
+from mpi_tensorflow_amd.models import mnist_cnn as M
+from mpi_tensorflow_amd.ops import native, ptr, stream_handle
+from mpi_tensorflow_amd.runtime.mnist_engine import NativeMnistEngine, TorchMnistEngine
+from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return (a - b).abs().max().item() / max(1e-6, b.abs().max().item())
+
+
+@pytest.fixture(scope="module")
+def data():
+    x, y = synthetic_rows("train", 0, 1024)
+    return x, y
+
+
+def _engines(cuda_dev, data, **kw):
+    x, y = data
+    cfg = C.TrainConfig(graph=kw.pop("graph", False), **kw).validate()
+    return NativeMnistEngine(cfg, x, y, cuda_dev), TorchMnistEngine(cfg, x, y, cuda_dev)
+
+
+def test_conv_pool_forward_matches_oracle(cuda_dev, data):
+    Cn = native()
+    x, _ = data
+    B = 96
+    xd = torch.from_numpy(x[:B]).to(cuda_dev)
+    g = torch.Generator().manual_seed(3)
+    w1 = (torch.randn(5, 5, 1, 32, generator=g) * 0.2).to(cuda_dev)
+    b1 = (torch.randn(32, generator=g) * 0.1).to(cuda_dev)
+    w2 = (torch.randn(5, 5, 32, 64, generator=g) * 0.05).to(cuda_dev)
+    b2 = (torch.randn(64, generator=g) * 0.1).to(cuda_dev)
+    a1 = torch.empty(B, 14, 14, 32, device=cuda_dev)
+    i1 = torch.empty(B, 14, 14, 32, dtype=torch.uint8, device=cuda_dev)
+    a2 = torch.empty(B, 7, 7, 64, device=cuda_dev)
+    i2 = torch.empty(B, 7, 7, 64, dtype=torch.uint8, device=cuda_dev)
+    s = stream_handle()
+    Cn.mnist.conv1_fwd(ptr(xd), 0, 0, B, ptr(w1), ptr(b1), ptr(a1), ptr(i1), s)
+    w2t = torch.empty(25 * 64 * 32, device=cuda_dev)
+    Cn.mnist.conv2_fwd(ptr(a1), B, ptr(w2), ptr(b2), ptr(a2), ptr(i2), ptr(w2t), s)
+    torch.cuda.synchronize()
+    xn = xd.permute(0, 3, 1, 2)
+    z1 = F.conv2d(xn, w1.permute(3, 2, 0, 1), b1, padding=2)
+    r1, ri1 = F.max_pool2d(F.relu(z1), 2, 2, return_indices=True)
+    z2 = F.conv2d(r1, w2.permute(3, 2, 0, 1), b2, padding=2)
+    r2 = F.max_pool2d(F.relu(z2), 2, 2)
+    assert _rel(a1, r1.permute(0, 2, 3, 1)) < 1e-5
+    assert _rel(a2, r2.permute(0, 2, 3, 1)) < 1e-5
+    assert torch.equal(w2t.view(25, 64, 32), w2.view(25, 32, 64).transpose(1, 2))
+    # argmax code of pool1 (where the ReLU output is positive the max is unique a.s.)
+    iy = (ri1 // 28) % 2
+    ix = (ri1 % 28) % 2
+    code = (iy * 2 + ix).permute(0, 2, 3, 1).to(torch.uint8)
+    pos = r1.permute(0, 2, 3, 1) > 0
+    assert torch.equal(i1[pos], code[pos])
+
+
+def test_forward_backward_grads_match_oracle(cuda_dev, data):
+    nat, ref = _engines(cuda_dev, data)
+    nat.set_step(7)
+    ref.set_step(7)
+    nat.forward_backward_only()
+    ref.forward_backward(7)
+    torch.cuda.synchronize()
+    assert abs(nat.bufs["loss_rows"].mean().item() - ref.last_loss) < 1e-4
+    nv, rv = nat.layout.views(nat.grads), ref.layout.views(ref.grads)
+    for s in nat.layout.specs:
+        err = _rel(nv[s.name], rv[s.name])
+        assert err < 2e-4, (s.name, err)
+
+
+def test_training_trajectory_matches_oracle(cuda_dev, data):
+    nat, ref = _engines(cuda_dev, data)
+    p0 = ref.params.clone()
+    nat.train(30)
+    ref.train(30)
+    torch.cuda.synchronize()
+    assert nat.step == ref.step == 30
+    assert int(nat.step_dev.item()) == 30
+    assert abs(nat.device_lr() - ref.lr(29)) < 1e-9
+    # fp32 rounding differences can flip a ReLU/max-pool decision at a tie and
+    # route one element's gradient differently, so compare in relative L2
+    # (max-abs is reported for information)
+    d = nat.params - ref.params
+    rel_upd = (d.norm() / (ref.params - p0).norm()).item()  # error relative to the update
+    print(f"trajectory: rel_update_err={rel_upd:.3e} max_abs={d.abs().max().item():.3e}")
+    assert rel_upd < 1e-2, rel_upd
+    assert abs(nat.loss_value() - (ref.last_loss + ref.l2_value())) < 1e-3
+
+
+def test_graph_replay_equals_eager(cuda_dev, data):
+    eager, _ = _engines(cuda_dev, data)
+    graphed, _ = _engines(cuda_dev, data, graph=True, graph_steps=4)
+    eager.train(10)
+    graphed.train(10)  # 2 replays of a 4-step graph + a 2-step graph
+    torch.cuda.synchronize()
+    assert torch.equal(eager.params, graphed.params)
+    assert torch.equal(eager.mom, graphed.mom)
+
+
+def test_eval_matches_oracle(cuda_dev, data):
+    nat, ref = _engines(cuda_dev, data)
+    nat.train(20)
+    ref.params.copy_(nat.params)
+    x, y = synthetic_rows("test", 0, 777)
+    e_nat, logits = nat.evaluate(x, y, chunk=300, return_logits=True)
+    e_ref = ref.evaluate(x, y)
+    with torch.no_grad():
+        lref = M.forward(ref.param_views(), torch.from_numpy(x).to(cuda_dev))
+    assert _rel(logits, lref) < 1e-4
+    assert abs(e_nat - e_ref) <= 100.0 * 2 / 777  # ties may flip at most a row or two
+
+
+def test_sgd_kernel(cuda_dev):
+    Cn = native()
+    n = 4096
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(n, generator=g).to(cuda_dev)
+    gr = torch.randn(n, generator=g).to(cuda_dev)
+    m = torch.randn(n, generator=g).to(cuda_dev)
+    lr = torch.tensor([0.05], device=cuda_dev)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda_dev)
+    w0, m0 = w.clone(), m.clone()
+    Cn.optim.sgd_momentum(ptr(w), ptr(gr), ptr(m), n, 1024, 5e-4, 0.9, 0.5, ptr(lr), 0.0,
+                          ptr(step), stream_handle())
+    torch.cuda.synchronize()
+    ge = gr * 0.5
+    ge[:1024] += 5e-4 * w0[:1024]
+    me = 0.9 * m0 + ge
+    we = w0 - 0.05 * me
+    assert _rel(m, me) < 1e-6 and _rel(w, we) < 1e-6
+    assert int(step.item()) == 1
