@@ -96,6 +96,17 @@ PYBIND11_MODULE(_C, m) {
                             P<float>(da1m), P<float>(part2), S(s));
     check_launch();
   });
+  k.def("conv2_bwd_data", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
+                             uintptr_t s) {
+    mnist::launch_conv2_bwd_data(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,
+                                 P<float>(da1m), S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd_filter", [](uintptr_t a1, uintptr_t dy2, int batch, uintptr_t part2, uintptr_t s) {
+    mnist::launch_conv2_bwd_filter(P<const float>(a1), P<const float>(dy2), batch, P<float>(part2),
+                                   S(s));
+    check_launch();
+  });
   k.def("conv1_bwd_filter", [](uintptr_t data, uintptr_t step, int n_local, int batch,
                                uintptr_t da1m, uintptr_t idx1, uintptr_t part1, uintptr_t s) {
     mnist::launch_conv1_bwd_filter(P<const float>(data), P<const long long>(step), n_local, batch,

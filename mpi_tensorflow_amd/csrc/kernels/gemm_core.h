@@ -169,6 +169,95 @@ __device__ __forceinline__ bool run_tile(const Prob& p, float* smem, int m0, int
   }
 }
 
+// One-shot variant for short K ranges (KT = (k_end-k_begin)/BK tiles, known at
+// compile time): EVERY K tile of the block is gathered into LDS up front (all
+// global loads in flight together, one barrier), then the MFMAs run without
+// further synchronisation.  Trades LDS (KT stage buffers) for the serial
+// per-tile latency chain of run_tile - the right shape for the small-M FC
+// GEMMs of the MNIST step (K per block 224..512).
+template <int WM, int WN, int WK, int BK, int KT, class Prob>
+__device__ __forceinline__ bool run_tile_oneshot(const Prob& p, float* smem, int m0, int n0,
+                                                 int k_begin, f32x16& acc, int& wm, int& wn) {
+  using CF = Cfg<WM, WN, WK, BK, Prob::A_KC, Prob::B_NC>;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  wm = wave % WM;
+  wn = (wave / WM) % WN;
+  const int wk = wave / (WM * WN);
+  {
+    float ra[KT][CF::RA];
+    float rb[KT][CF::RB];
+#pragma unroll
+    for (int i = 0; i < CF::RA; ++i) {
+      int ml, kl;
+      CF::a_slot(tid, i, ml, kl);
+      const auto c = p.a_ctx(m0 + ml, kl);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) ra[kt][i] = p.a_get(c, k_begin + kt * BK);
+    }
+#pragma unroll
+    for (int i = 0; i < CF::RB; ++i) {
+      int kl, nl;
+      CF::b_slot(tid, i, kl, nl);
+      const auto c = p.b_ctx(kl, n0 + nl);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) rb[kt][i] = p.b_get(c, k_begin + kt * BK);
+    }
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      float* As = smem + kt * CF::STAGE_FLOATS;
+      float* Bs = As + BK * CF::LDA;
+#pragma unroll
+      for (int i = 0; i < CF::RA; ++i) {
+        int ml, kl;
+        CF::a_slot(tid, i, ml, kl);
+        As[kl * CF::LDA + ml] = ra[kt][i];
+      }
+#pragma unroll
+      for (int i = 0; i < CF::RB; ++i) {
+        int kl, nl;
+        CF::b_slot(tid, i, kl, nl);
+        Bs[kl * CF::LDB + nl] = rb[kt][i];
+      }
+    }
+  }
+  __syncthreads();
+  acc = zero16();
+  constexpr int KS = BK / WK;
+  const int khalf = lane >> 5;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    const float* As = smem + kt * CF::STAGE_FLOATS;
+    const float* Aw = As + wm * 32 + (lane & 31) + (wk * KS + khalf) * CF::LDA;
+    const float* Bw = As + BK * CF::LDA + wn * 32 + (lane & 31) + (wk * KS + khalf) * CF::LDB;
+#pragma unroll
+    for (int kk = 0; kk < KS; kk += 2) acc = mfma32x32x2(Aw[kk * CF::LDA], Bw[kk * CF::LDB], acc);
+  }
+  if constexpr (WK > 1) {
+    __syncthreads();
+    float* red = smem;
+    const int sub = wm + WM * wn;
+    if (wk > 0) {
+      float* dst = red + (((wk - 1) * WM * WN + sub) * 16) * 64 + lane;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[r * 64] = acc[r];
+    }
+    __syncthreads();
+    if (wk == 0) {
+#pragma unroll
+      for (int g = 1; g < WK; ++g) {
+        const float* src = red + (((g - 1) * WM * WN + sub) * 16) * 64 + lane;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += src[r * 64];
+      }
+    }
+    return wk == 0;
+  } else {
+    return true;
+  }
+}
+
 // ------------------------------------------------- plain matrix operands ----
 // A row-major [M][lda] walked along K (A_KC) with rows >= M reading zero.
 struct RowMajorA {
@@ -181,7 +270,10 @@ struct RowMajorA {
   __device__ __forceinline__ Ctx ctx(int m, int kl) const {
     return {a + (size_t)(m < M ? m : 0) * lda + kl, m < M};
   }
-  __device__ __forceinline__ float get(const Ctx& c, int k0) const { return c.v ? c.p[k0] : 0.f; }
+  __device__ __forceinline__ float get(const Ctx& c, int k0) const {
+    const float v = c.p[k0];  // always a valid address (row clamped to 0)
+    return c.v ? v : 0.f;
+  }
 };
 
 }  // namespace gemm

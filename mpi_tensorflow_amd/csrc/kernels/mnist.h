@@ -25,6 +25,11 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
                     float* g_w4, float* g_b4, float* dy2, hipStream_t s);
 int conv2_filter_splits(int batch);
+void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
+                           float* da1m, hipStream_t s);
+void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
+                             hipStream_t s);
+
 void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
                       float* part2, hipStream_t s);
 int conv1_filter_blocks(int batch);

@@ -60,7 +60,7 @@ template <class G>
 struct ConvPoolFwdProb {
   static constexpr bool A_KC = true, B_NC = true;
   struct ACtx {
-    const float* p;  // input at (n, y, x, ci) of this slot's pixel
+    const float* p;  // input at (n, 0, 0, ci) of this slot's image
     int y, x, kl;
     bool v;
   };
@@ -77,20 +77,25 @@ struct ConvPoolFwdProb {
     const int y = 2 * py + (q >> 1), xx = 2 * px + (q & 1);
     const bool v = n < batch;
     const int ci = kl % G::CIN;
-    return {x + ((size_t)((v ? n : 0) * G::H + y) * G::W + xx) * G::CIN + ci, y, xx, kl, v};
+    return {x + (size_t)(v ? n : 0) * G::H * G::W * G::CIN + ci, y, xx, kl, v};
   }
+  // unconditional load from a clamped (always valid) address + select: a
+  // guarded load would compile to an exec-mask branch per element
   __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
     const int k = k0 + c.kl;
     const int tap = k / G::CIN;
     const int kh = tap / G::KS, kw = tap % G::KS;
-    const int dy = kh - G::PAD, dx = kw - G::PAD;
-    const int iy = c.y + dy, ix = c.x + dx;
+    const int iy = c.y + kh - G::PAD, ix = c.x + kw - G::PAD;
     const bool ok = c.v && k < G::K && iy >= 0 && iy < G::H && ix >= 0 && ix < G::W;
-    return ok ? c.p[(dy * G::W + dx) * G::CIN] : 0.f;
+    const int iyc = min(max(iy, 0), G::H - 1), ixc = min(max(ix, 0), G::W - 1);
+    const float v = c.p[(iyc * G::W + ixc) * G::CIN];
+    return ok ? v : 0.f;
   }
   __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {w + kl * G::COUT + n, kl}; }
   __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
-    return (k0 + c.kl < G::K) ? c.p[k0 * G::COUT] : 0.f;
+    const int k = k0 + c.kl;
+    const float v = c.p[(min(k, G::K - 1) - c.kl) * G::COUT];
+    return k < G::K ? v : 0.f;
   }
 };
 
@@ -152,12 +157,14 @@ struct Fc1FwdProb {
 };
 
 // train: split-K partial slabs part[z][m][n]; eval: h = relu(acc + b) (+dropout)
-template <int WM, int WN, int WK, int BK, bool EVAL>
+template <int WM, int WN, int WK, int BK, bool EVAL, int ONESHOT_KT = 0>
 __global__ __launch_bounds__(64 * WM * WN * WK) void fc1_fwd_kernel(
     const float* __restrict__ a, const float* __restrict__ w, const float* __restrict__ bias,
     float* __restrict__ out, int M, int kchunk, uint32_t drop_key, float keep_prob) {
   using CF = gemm::Cfg<WM, WN, WK, BK, true, true>;
-  __shared__ float smem[CF::SMEM_FLOATS];
+  constexpr int SM1 = ONESHOT_KT > 0 ? ONESHOT_KT * CF::STAGE_FLOATS : CF::SMEM_FLOATS;
+  constexpr int SM = SM1 > CF::SMEM_FLOATS_RED ? SM1 : CF::SMEM_FLOATS_RED;
+  __shared__ float smem[SM];
   Fc1FwdProb p{{a, FC1_IN, M}, w};
   const int mt = (M + CF::BM - 1) / CF::BM;
   const int z = blockIdx.y;
@@ -166,7 +173,11 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void fc1_fwd_kernel(
   const int kb = z * kchunk, ke = min(FC1_IN, kb + kchunk);
   f32x16 acc;
   int wm, wn;
-  bool own = gemm::run_tile<WM, WN, WK, BK>(p, smem, m0, n0, kb, ke, acc, wm, wn);
+  bool own;
+  if constexpr (ONESHOT_KT > 0)
+    own = gemm::run_tile_oneshot<WM, WN, WK, BK, ONESHOT_KT>(p, smem, m0, n0, kb, acc, wm, wn);
+  else
+    own = gemm::run_tile<WM, WN, WK, BK>(p, smem, m0, n0, kb, ke, acc, wm, wn);
   if (!own) return;
   const int lane = threadIdx.x & 63;
   const int n = n0 + 32 * wn + (lane & 31);
@@ -332,11 +343,15 @@ struct Fc1DwProb {
   int batch;
   __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return {a2 + kl * FC1_IN + m, kl}; }
   __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
-    return k0 + c.kl < batch ? c.p[k0 * FC1_IN] : 0.f;
+    const int k = k0 + c.kl;
+    const float v = c.p[(min(k, batch - 1) - c.kl) * FC1_IN];
+    return k < batch ? v : 0.f;
   }
   __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {dh + kl * FC1_OUT + n, kl}; }
   __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
-    return k0 + c.kl < batch ? c.p[k0 * FC1_OUT] : 0.f;
+    const int k = k0 + c.kl;
+    const float v = c.p[(min(k, batch - 1) - c.kl) * FC1_OUT];
+    return k < batch ? v : 0.f;
   }
 };
 
@@ -368,11 +383,23 @@ __device__ void fc1_small_grads(int blk, const float* hd, const float* dh, const
   float acc[NCLS + 1];
 #pragma unroll
   for (int c = 0; c <= NCLS; ++c) acc[c] = 0.f;
-  for (int n = rg; n < batch; n += 4) {
-    const float h = hd[n * FC1_OUT + j];
+  for (int n0 = rg; n0 < batch; n0 += 32) {  // 8 rows per round, loads issued together
+    float hv[8], dv[8];
 #pragma unroll
-    for (int c = 0; c < NCLS; ++c) acc[c] += h * dlog[n * NCLS + c];
-    acc[NCLS] += dh[n * FC1_OUT + j];
+    for (int u = 0; u < 8; ++u) {
+      const int n = min(n0 + 4 * u, batch - 1);
+      hv[u] = hd[n * FC1_OUT + j];
+      dv[u] = dh[n * FC1_OUT + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int n = n0 + 4 * u;
+      if (n < batch) {
+#pragma unroll
+        for (int c = 0; c < NCLS; ++c) acc[c] += hv[u] * dlog[n * NCLS + c];
+        acc[NCLS] += dv[u];
+      }
+    }
   }
   float* s = smem;  // [4][11][64]
 #pragma unroll
@@ -396,13 +423,18 @@ __device__ void fc1_small_grads(int blk, const float* hd, const float* dh, const
   }
 }
 
+// fc1 backward, one launch: blocks [0, n_dx) compute dX (+ the pool2/ReLU2
+// backward scatter into dY2, the critical path), then dW1 tiles, then the
+// small fc2/bias grads.  All roles fit 33 KB of LDS (4 blocks per CU).
+constexpr int FC1BWD_DW_BK = 32;
+
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
     const float* __restrict__ hd, const float* __restrict__ dlog, const float* __restrict__ w1,
     int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
     float* __restrict__ g_b4, float* __restrict__ dy2) {
   using CDX = gemm::Cfg<1, 1, FC1BWD_DX_WK, FC1BWD_BK, true, false>;
-  using CDW = gemm::Cfg<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_BK, false, true>;
+  using CDW = gemm::Cfg<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_DW_BK, false, true>;
   constexpr int S1 = CDX::SMEM_FLOATS, S2 = CDW::SMEM_FLOATS, S3 = 4 * (NCLS + 1) * 64;
   constexpr int SM = S1 > S2 ? (S1 > S3 ? S1 : S3) : (S2 > S3 ? S2 : S3);
   __shared__ float smem[SM];
@@ -414,7 +446,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   f32x16 acc;
   int wm, wn;
   if (bid < n_dx) {
-    // ---- dX with the pool2 / ReLU2 backward scatter fused ----
     Fc1DxProb p{{dh, FC1_OUT, batch}, w1};
     const int m0 = (bid % n_dx_m) * 32, n0 = (bid / n_dx_m) * 32;
     if (!gemm::run_tile<1, 1, FC1BWD_DX_WK, FC1BWD_BK>(p, smem, m0, n0, 0, FC1_OUT, acc, wm, wn))
@@ -441,9 +472,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     Fc1DwProb p{a2, dh, batch};
     constexpr int mt = FC1_IN / CDW::BM;  // 49
     const int m0 = (bid % mt) * CDW::BM, n0 = (bid / mt) * CDW::BN;
-    const int kend = (batch + FC1BWD_BK - 1) / FC1BWD_BK * FC1BWD_BK;
-    gemm::run_tile<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_BK>(p, smem, m0, n0, 0, kend, acc, wm,
-                                                             wn);
+    const int kend = (batch + FC1BWD_DW_BK - 1) / FC1BWD_DW_BK * FC1BWD_DW_BK;
+    gemm::run_tile<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_DW_BK>(p, smem, m0, n0, 0, kend, acc, wm,
+                                                                wn);
     const int n = n0 + 32 * wn + (lane & 31);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -471,29 +502,35 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 constexpr int C2_XS_ROWS = 8, C2_XS_COLS = 18;
 
 // conv2 forward + bias + ReLU + 2x2 maxpool (+argmax).  Block = (image, pair of
-// pooled rows); 4 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
-// (N: 32 output channels).  Also writes W2T[t][co][ci] (the transposed weight
-// copy the bwd-data kernel reads) when w2t != nullptr.
-__global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
+// pooled rows); 8 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
+// (N: 32 output channels) x 2 (K: input-channel halves, summed through LDS),
+// i.e. two waves per SIMD so one wave's LDS/L2 latency hides under the
+// other's MFMAs.  A and B operands are fetched one tap ahead.  Also writes
+// W2T[t][co][ci] (the transposed weight copy bwd-data reads) when w2t != 0.
+constexpr int C2_XS = C2_XS_ROWS * C2_XS_COLS * 33;
+
+__global__ __launch_bounds__(512) void conv2_fwd_v3_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ b2, float* __restrict__ out, uint8_t* __restrict__ argmax,
     float* __restrict__ w2t) {
-  __shared__ float xs[C2_XS_ROWS * C2_XS_COLS * 33];
+  __shared__ float xs[C2_XS + 4 * 16 * 64];
+  float* red = xs + C2_XS;
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (w2t) {  // 51200 floats over all blocks
-    for (int i = blockIdx.x * 256 + tid; i < 51200; i += gridDim.x * 256) {
+    for (int i = blockIdx.x * 512 + tid; i < 51200; i += gridDim.x * 512) {
       const int ci = i & 31, co = (i >> 5) & 63, t = i >> 11;
       w2t[i] = w2[(t * 32 + ci) * 64 + co];
     }
   }
-  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 32; i += 256) {
+  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 32; i += 512) {
     const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
     const int y = 2 * pr0 - 2 + r, x = c - 2;
     const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
-    xs[(r * C2_XS_COLS + c) * 33 + ci] = ok ? a1[((n * 14 + y) * 14 + x) * 32 + ci] : 0.f;
+    const float v = a1[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 32 + ci];
+    xs[(r * C2_XS_COLS + c) * 33 + ci] = ok ? v : 0.f;
   }
-  const int msub = wave & 1, nsub = wave >> 1;
+  const int msub = wave & 1, nsub = (wave >> 1) & 1, kg = wave >> 2;
   const int m = msub * 32 + (lane & 31);
   const int win = m >> 2, q = m & 3;
   int ly = 0, lx = 0;
@@ -501,26 +538,48 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
     ly = 2 * (win / 7) + (q >> 1);
     lx = 2 * (win % 7) + (q & 1);
   }
-  const int abase = (ly * C2_XS_COLS + lx) * 33 + (lane >> 5);
+  const int abase = (ly * C2_XS_COLS + lx) * 33 + kg * 16 + (lane >> 5);
   const int co = nsub * 32 + (lane & 31);
-  const float* wp = w2 + (lane >> 5) * 64 + co;  // + (t*32 + 2c) * 64
-  float bc[16], bn[16];
+  const float* wp = w2 + (kg * 16 + (lane >> 5)) * 64 + co;  // + (t*32 + 2c) * 64
+  float bc[8], bn[8], ac[8], an[8];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 64];
+  for (int c = 0; c < 8; ++c) bc[c] = wp[(2 * c) * 64];
   __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 8; ++c) ac[c] = xs[abase + 2 * c];
   f32x16 acc = zero16();
+#pragma unroll
   for (int t = 0; t < 25; ++t) {
     if (t + 1 < 25) {
+      const int kh = (t + 1) / 5, kw = (t + 1) % 5;
+      const float* xa = xs + abase + (kh * C2_XS_COLS + kw) * 33;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) bn[c] = wp[((t + 1) * 32 + 2 * c) * 64];
+      for (int c = 0; c < 8; ++c) {
+        bn[c] = wp[((t + 1) * 32 + 2 * c) * 64];
+        an[c] = xa[2 * c];
+      }
     }
-    const int kh = t / 5, kw = t % 5;
-    const float* xa = xs + abase + (kh * C2_XS_COLS + kw) * 33;
+    // keep the next tap's loads issued HERE (the scheduler would otherwise sink
+    // them next to their use and expose the L2 latency on every MFMA)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc = mfma32x32x2(xa[2 * c], bc[c], acc);
+    for (int c = 0; c < 8; ++c) acc = mfma32x32x2(ac[c], bc[c], acc);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) bc[c] = bn[c];
+    for (int c = 0; c < 8; ++c) {
+      bc[c] = bn[c];
+      ac[c] = an[c];
+    }
   }
+  const int sub = msub + 2 * nsub;
+  if (kg == 1) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[(sub * 16 + r) * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (kg == 1) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += red[(sub * 16 + r) * 64 + lane];
   const float bias = b2[co];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -545,47 +604,61 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
 
 // conv2 bwd-data (+ReLU1 mask): dA1m[n,y,x,ci] = [a1>0] * sum_{kh,kw,co}
 // dY2[n, y+2-kh, x+2-kw, co] W2[kh,kw,ci,co].  Block = (image, 4 output rows);
-// 4 waves = 2 (M: 2 rows x 16 cols) x 2 (K: co halves, summed through LDS).
+// 8 waves = 2 (M: 2 rows x 16 cols) x 4 (K: co quarters, summed through LDS).
+constexpr int C2_DS = C2_XS_ROWS * C2_XS_COLS * 65;
+constexpr int C2B_SMEM = C2_DS + 3 * 2 * 16 * 64;
+
 __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
                                   const float* __restrict__ dy2, const float* __restrict__ w2t,
                                   float* __restrict__ da1m, float* smem) {
   float* ds = smem;  // [8][18][65]
+  float* red = smem + C2_DS;
   const int n = bid >> 2, y0 = 4 * (bid & 3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 64; i += 256) {
+  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 64; i += 512) {
     const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
     const int y = y0 - 2 + r, x = c - 2;
     const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
-    ds[(r * C2_XS_COLS + c) * 65 + co] = ok ? dy2[((n * 14 + y) * 14 + x) * 64 + co] : 0.f;
+    const float v = dy2[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 64 + co];
+    ds[(r * C2_XS_COLS + c) * 65 + co] = ok ? v : 0.f;
   }
-  const int msub = wave & 1, cog = wave >> 1;
+  const int msub = wave & 1, cog = wave >> 1;  // cog: co quarter (16 channels)
   const int r2 = (lane & 31) >> 4, x = lane & 15;
   const int ly = 2 * msub + r2, lx = x < 14 ? x : 0;
   // staged row of source pixel (y+2-kh) is ly + 4 - kh; col lx + 4 - kw
-  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 32 + (lane >> 5);
-  const float* wp = w2t + (cog * 32 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
-  float bc[16], bn[16];
+  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 16 + (lane >> 5);
+  const float* wp = w2t + (cog * 16 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
+  float bc[8], bn[8], ac[8], an[8];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 32];
+  for (int c = 0; c < 8; ++c) bc[c] = wp[(2 * c) * 32];
   __syncthreads();
+#pragma unroll
+  for (int c = 0; c < 8; ++c) ac[c] = ds[abase + 2 * c];
   f32x16 acc = zero16();
+#pragma unroll
   for (int t = 0; t < 25; ++t) {
     if (t + 1 < 25) {
+      const int kh = (t + 1) / 5, kw = (t + 1) % 5;
+      const float* xa = ds + abase - (kh * C2_XS_COLS + kw) * 65;
 #pragma unroll
-      for (int c = 0; c < 16; ++c) bn[c] = wp[((t + 1) * 64 + 2 * c) * 32];
+      for (int c = 0; c < 8; ++c) {
+        bn[c] = wp[((t + 1) * 64 + 2 * c) * 32];
+        an[c] = xa[2 * c];
+      }
     }
-    const int kh = t / 5, kw = t % 5;
-    const float* xa = ds + abase - (kh * C2_XS_COLS + kw) * 65;
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) acc = mfma32x32x2(xa[2 * c], bc[c], acc);
+    for (int c = 0; c < 8; ++c) acc = mfma32x32x2(ac[c], bc[c], acc);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 16; ++c) bc[c] = bn[c];
+    for (int c = 0; c < 8; ++c) {
+      bc[c] = bn[c];
+      ac[c] = an[c];
+    }
   }
-  __syncthreads();  // ds is dead: reuse for the K-split reduction
-  float* red = smem + msub * 16 * 64;
-  if (cog == 1) {
+  if (cog > 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
+    for (int r = 0; r < 16; ++r) red[(((cog - 1) * 2 + msub) * 16 + r) * 64 + lane] = acc[r];
   }
   __syncthreads();
   if (cog == 0) {
@@ -596,7 +669,9 @@ __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
       const int y = y0 + 2 * msub + (mr >> 4), xx = mr & 15;
       if (y < 14 && xx < 14) {
         const int o = ((n * 14 + y) * 14 + xx) * 32 + ci;
-        const float g = acc[r] + red[r * 64 + lane];
+        float g = acc[r];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) g += red[((j * 2 + msub) * 16 + r) * 64 + lane];
         da1m[o] = a1[o] > 0.f ? g : 0.f;
       }
     }
@@ -604,16 +679,28 @@ __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
 }
 
 // conv2 bwd-filter: dW2[t][ci][co] = sum_pix a1[pix shifted by tap t][ci] dY2[pix][co].
-// Block = (tap, group of 4 images); 4 waves = 2 (N: co halves) x 2 (2 images
+// Block = (tap, group of 4 images); 8 waves = 2 (N: co halves) x 4 (one image
 // each, summed through LDS).  A[m = ci][k = pixel], B[k = pixel][co]: both
-// gathered straight from L2 with channels on lanes.  The centre tap's blocks
-// also sum dY2 per channel (db2).
+// gathered straight from L2 with channels on lanes, one image row ahead.  The
+// centre tap's blocks also sum dY2 per channel (db2).
 constexpr int C2F_GROUPS_IMG = 4;
 
 __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict__ a1,
                                     const float* __restrict__ dy2, float* __restrict__ part2,
                                     float* __restrict__ part_db2, float* smem) {
-  const int t = bid % 25, g = bid / 25;
+  // XCD-aware mapping (blocks b, b+8, ... share an XCD's L2): every tap of an
+  // image group runs on ONE XCD, so the group's a1/dY2 tiles are fetched into
+  // that L2 once instead of into all eight.
+  const int ngroups = (batch + C2F_GROUPS_IMG - 1) / C2F_GROUPS_IMG;
+  int t, g;
+  if (ngroups % 8 == 0) {
+    const int x = bid & 7, idx = bid >> 3;
+    t = idx % 25;
+    g = x + 8 * (idx / 25);
+  } else {
+    t = bid % 25;
+    g = bid / 25;
+  }
   const int kh = t / 5, kw = t % 5;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsub = wave & 1, ih = wave >> 1;
@@ -621,62 +708,80 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   const int co = nsub * 32 + (lane & 31);
   f32x16 acc = zero16();
   float dbs = 0.f;
-  for (int ii = 0; ii < 2; ++ii) {
-    const int n = g * C2F_GROUPS_IMG + ih * 2 + ii;
-    if (n >= batch) break;
+  const int n = g * C2F_GROUPS_IMG + ih;
+  if (n < batch) {
     const float* an = a1 + (size_t)n * 196 * 32 + ci;
     const float* dn = dy2 + (size_t)n * 196 * 64 + co;
-    for (int y = 0; y < 14; ++y) {
+    float av[7], bv[7], avn[7], bvn[7];
+    auto fetch = [&](int y, float* A, float* Bv) {
       const int iy = y + kh - 2;
       const bool rv = iy >= 0 && iy < 14;
-      float av[7], bv[7];
+      const int iyc = min(max(iy, 0), 13);
 #pragma unroll
       for (int xp = 0; xp < 7; ++xp) {
         const int x = 2 * xp + kpar, ix = x + kw - 2;
         const bool ok = rv && ix >= 0 && ix < 14;
-        av[xp] = ok ? an[(iy * 14 + ix) * 32] : 0.f;
-        bv[xp] = dn[(y * 14 + x) * 64];
+        const float v = an[(iyc * 14 + min(max(ix, 0), 13)) * 32];
+        A[xp] = ok ? v : 0.f;
+        Bv[xp] = dn[(y * 14 + x) * 64];
       }
+    };
+    fetch(0, av, bv);
+#pragma unroll 2
+    for (int y = 0; y < 14; ++y) {
+      if (y + 1 < 14) fetch(y + 1, avn, bvn);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int xp = 0; xp < 7; ++xp) {
         acc = mfma32x32x2(av[xp], bv[xp], acc);
         dbs += bv[xp];
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int xp = 0; xp < 7; ++xp) {
+        av[xp] = avn[xp];
+        bv[xp] = bvn[xp];
+      }
     }
   }
-  // sum the two image halves (ih) through LDS, write one slab per block
-  float* red = smem + nsub * 16 * 64;
-  if (ih == 1) {
+  // sum the four images (ih) through LDS, write one slab per block
+  float* red = smem;
+  if (ih > 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc[r];
+    for (int r = 0; r < 16; ++r) red[(((ih - 1) * 2 + nsub) * 16 + r) * 64 + lane] = acc[r];
   }
   __syncthreads();
   if (ih == 0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
+      float s = acc[r];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) s += red[((j * 2 + nsub) * 16 + r) * 64 + lane];
       const int row = t * 32 + mfma32_row(r, lane);  // (t, ci)
-      part2[((size_t)g * 800 + row) * 64 + co] = acc[r] + red[r * 64 + lane];
+      part2[((size_t)g * 800 + row) * 64 + co] = s;
     }
   }
   if (t == 12) {  // centre tap visits every pixel exactly once: db2 partial
     dbs += __shfl_xor(dbs, 32, 64);
-    if (kpar == 0) part_db2[(g * 2 + ih) * 64 + co] = dbs;
+    if (kpar == 0) part_db2[(g * 4 + ih) * 64 + co] = dbs;
   }
 }
 
-// conv2 backward launch: bwd-data blocks (batch*4) then bwd-filter blocks
-// (25 taps x ceil(batch/4) image groups) - independent, one launch.
-__global__ __launch_bounds__(256) void conv2_bwd_kernel(
-    const float* __restrict__ a1, const float* __restrict__ dy2, const float* __restrict__ w2t,
-    int batch, float* __restrict__ da1m, float* __restrict__ part2,
-    float* __restrict__ part_db2) {
-  __shared__ float smem[C2_XS_ROWS * C2_XS_COLS * 65];
-  const int n_data = batch * 4;
-  if ((int)blockIdx.x < n_data) {
-    conv2_bwd_data_v3(blockIdx.x, a1, dy2, w2t, da1m, smem);
-  } else {
-    conv2_bwd_filter_v3(blockIdx.x - n_data, batch, a1, dy2, part2, part_db2, smem);
-  }
+__global__ __launch_bounds__(512) void conv2_bwd_data_kernel(const float* __restrict__ a1,
+                                                            const float* __restrict__ dy2,
+                                                            const float* __restrict__ w2t,
+                                                            float* __restrict__ da1m) {
+  __shared__ float smem[C2B_SMEM];
+  conv2_bwd_data_v3(blockIdx.x, a1, dy2, w2t, da1m, smem);
+}
+
+__global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(int batch,
+                                                              const float* __restrict__ a1,
+                                                              const float* __restrict__ dy2,
+                                                              float* __restrict__ part2,
+                                                              float* __restrict__ part_db2) {
+  __shared__ float smem[3 * 2 * 16 * 64];
+  conv2_bwd_filter_v3(blockIdx.x, batch, a1, dy2, part2, part_db2, smem);
 }
 
 // ------------------------------------------------------ conv1 bwd filter ----
@@ -753,13 +858,11 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(
     const float* __restrict__ part2, const float* __restrict__ part_db2, int ngroups,
     const float* __restrict__ part1, int nblk1, float* __restrict__ g_w2,
     float* __restrict__ g_b2, float* __restrict__ g_w1, float* __restrict__ g_b1) {
-  constexpr int N2 = 51200 + 64;
-  constexpr int B2 = (N2 + 255) / 256;
+  constexpr int B2 = 51200 / 256;
   if ((int)blockIdx.x < B2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= N2) return;
     float s = 0.f;
-    if (i < 51200) {
+    {
       if (ngroups == 16) {
 #pragma unroll
         for (int z = 0; z < 16; ++z) s += part2[(size_t)z * 51200 + i];
@@ -767,14 +870,18 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(
         for (int z = 0; z < ngroups; ++z) s += part2[(size_t)z * 51200 + i];
       }
       g_w2[i] = s;
-    } else {
-      const int co = i - 51200;
-      for (int z = 0; z < 2 * ngroups; ++z) s += part_db2[z * 64 + co];
-      g_b2[co] = s;
     }
     return;
   }
-  const int o = ((int)blockIdx.x - B2) * 4 + (threadIdx.x >> 6);
+  if ((int)blockIdx.x < B2 + 16) {  // db2: one wave per channel
+    const int co = ((int)blockIdx.x - B2) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    float s = 0.f;
+    for (int z = lane; z < 4 * ngroups; z += 64) s += part_db2[z * 64 + co];
+    s = wave_sum(s);
+    if (lane == 0) g_b2[co] = s;
+    return;
+  }
+  const int o = ((int)blockIdx.x - B2 - 16) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (o >= 832) return;
   float s = 0.f;
@@ -814,7 +921,7 @@ void launch_conv1_fwd(const float* data, const long long* step, int n_local, int
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s) {
-  conv2_fwd_v3_kernel<<<batch * 4, 256, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
+  conv2_fwd_v3_kernel<<<batch * 4, 512, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
 }
 
 int fc1_train_splits() { return FC1_SPLITS; }
@@ -824,8 +931,8 @@ void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* par
   // 64x32 tiles, 2-way in-block K split, 14 split-K slabs of 224 (7 K tiles)
   const int kchunk = FC1_IN / FC1_SPLITS;
   dim3 grid(cdiv(batch, 64) * (FC1_OUT / 32), FC1_SPLITS);
-  fc1_fwd_kernel<2, 1, 2, 32, false><<<grid, 256, 0, s>>>(a2, w, nullptr, part, batch, kchunk, 0u,
-                                                          1.f);
+  fc1_fwd_kernel<2, 1, 2, 32, false, FC1_IN / FC1_SPLITS / 32>
+      <<<grid, 256, 0, s>>>(a2, w, nullptr, part, batch, kchunk, 0u, 1.f);
 }
 
 void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
@@ -860,11 +967,21 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
 
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
 
+void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
+                           float* da1m, hipStream_t s) {
+  conv2_bwd_data_kernel<<<batch * 4, 512, 0, s>>>(a1, dy2, w2t, da1m);
+}
+
+void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
+                             hipStream_t s) {
+  const int G = conv2_filter_splits(batch);
+  conv2_bwd_filter_kernel<<<25 * G, 512, 0, s>>>(batch, a1, dy2, part2, part2 + (size_t)G * 51200);
+}
+
 void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
                       float* part2, hipStream_t s) {
-  const int G = conv2_filter_splits(batch);
-  float* part_db2 = part2 + (size_t)G * 51200;
-  conv2_bwd_kernel<<<batch * 4 + 25 * G, 256, 0, s>>>(a1, dy2, w2t, batch, da1m, part2, part_db2);
+  launch_conv2_bwd_data(a1, dy2, w2t, batch, da1m, s);
+  launch_conv2_bwd_filter(a1, dy2, batch, part2, s);
 }
 
 int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }
@@ -878,13 +995,13 @@ void launch_conv1_bwd_filter(const float* data, const long long* step, int n_loc
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s) {
-  const int b2 = cdiv(51200 + 64, 256);
+  const int b2 = 51200 / 256 + 16;
   const int b1 = cdiv(832, 4);
   grad_finalize_kernel<<<b2 + b1, 256, 0, s>>>(part2, part2 + (size_t)ngroups * 51200, ngroups,
                                                part1, nblk1, g_w2, g_b2, g_w1, g_b1);
 }
 
-size_t part2_floats(int batch) { return (size_t)conv2_filter_splits(batch) * (51200 + 128); }
+size_t part2_floats(int batch) { return (size_t)conv2_filter_splits(batch) * (51200 + 256); }
 size_t part1_floats(int batch) { return (size_t)conv1_filter_blocks(batch) * 832; }
 size_t fc1_part_floats(int batch) { return (size_t)FC1_SPLITS * batch * FC1_OUT; }
 

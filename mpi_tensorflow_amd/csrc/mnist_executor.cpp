@@ -18,18 +18,23 @@ MnistExecutor::MnistExecutor(const MnistPtrs& p) : p_(p) {
     throw std::runtime_error("MnistExecutor: local shard must exceed the batch");
   if (p_.total % 4 != 0 || p_.l2_end % 4 != 0)
     throw std::runtime_error("MnistExecutor: flat buffer sizes must be multiples of 4");
-  HIP_CHECK(hipEventCreateWithFlags(&ev_b1_, hipEventDisableTiming));
-  HIP_CHECK(hipEventCreateWithFlags(&ev_b2_, hipEventDisableTiming));
-  HIP_CHECK(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming));
+  for (hipEvent_t* e : {&ev_head_, &ev_dx_, &ev_dw_, &ev_filt_, &ev_fin_, &ev_done_})
+    HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
 MnistExecutor::~MnistExecutor() {
-  if (ev_b1_) (void)hipEventDestroy(ev_b1_);
-  if (ev_b2_) (void)hipEventDestroy(ev_b2_);
-  if (ev_done_) (void)hipEventDestroy(ev_done_);
+  for (hipEvent_t e : {ev_head_, ev_dx_, ev_dw_, ev_filt_, ev_fin_, ev_done_})
+    if (e) (void)hipEventDestroy(e);
 }
 
-void MnistExecutor::forward_backward(hipStream_t s) {
+// forward + backward into the flat grad buffer, all on ONE stream: in hipGraph
+// replay a same-stream kernel boundary costs ~0.1 us while every cross-stream
+// event dependency was measured at 5-18 us of idle gap (rocprofv3 timeline,
+// profiles/), and the two MFMA-bound conv2 backward kernels gain nothing from
+// running concurrently.  Independent work is therefore merged into single
+// launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
+// ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
+void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -46,12 +51,25 @@ void MnistExecutor::forward_backward(hipStream_t s) {
                               p.keep_prob, p.seed, p.rank, p.base_lr, p.lr_decay, P<float>(p.hd),
                               P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
                               P<float>(p.lr), P<int>(p.correct), s);
-  // backward: FC grads (bucket 1) first
+  // backward: fc1 dX (+pool2/ReLU2 scatter) | dW1 | fc2 grads, one launch
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
                         P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
                         s);
+  HIP_CHECK(hipEventRecord(ev_dw_, s));
+  mnist::launch_conv2_bwd_data(P<const float>(p.a1), P<const float>(p.dy2),
+                               P<const float>(p.w2t), B, P<float>(p.da1m), s);
+  mnist::launch_conv2_bwd_filter(P<const float>(p.a1), P<const float>(p.dy2), B,
+                                 P<float>(p.part2), s);
+  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
+                                 P<const float>(p.da1m), P<const uint8_t>(p.idx1),
+                                 P<float>(p.part1), s);
+  mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
+                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
+                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
 }
+
+void MnistExecutor::forward_backward(hipStream_t s) { enqueue_fwd_bwd(s); }
 
 void MnistExecutor::sgd(hipStream_t s, float gscale) {
   const MnistPtrs& p = p_;
@@ -63,25 +81,16 @@ void MnistExecutor::sgd(hipStream_t s, float gscale) {
 void MnistExecutor::train_step(hipStream_t s, RcclComm* comm, hipStream_t cs) {
   const MnistPtrs& p = p_;
   float* G = P<float>(p.grads);
-  const int B = p.batch;
-  forward_backward(s);
+  enqueue_fwd_bwd(s);
   const bool sync = comm != nullptr && comm->size() > 1;
-  if (sync) {  // bucket 1 overlaps the conv backward below
-    HIP_CHECK(hipEventRecord(ev_b1_, s));
-    HIP_CHECK(hipStreamWaitEvent(cs, ev_b1_, 0));
+  if (sync) {
+    // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1-dW is done; it
+    // overlaps the conv backward still running on the compute streams
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
     comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
-  }
-  mnist::launch_conv2_bwd(P<const float>(p.a1), P<const float>(p.dy2), P<const float>(p.w2t), B,
-                          P<float>(p.da1m), P<float>(p.part2), s);
-  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), P<const long long>(p.step), p.n_local,
-                                 B, P<const float>(p.da1m), P<const uint8_t>(p.idx1),
-                                 P<float>(p.part1), s);
-  mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
-                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
-                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
-  if (sync) {  // bucket 2 on the same (ordered) comm stream, then join
-    HIP_CHECK(hipEventRecord(ev_b2_, s));
-    HIP_CHECK(hipStreamWaitEvent(cs, ev_b2_, 0));
+    // bucket 2 (conv grads) after the slab reduction, same ordered stream
+    HIP_CHECK(hipEventRecord(ev_fin_, s));
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
     comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
                      ncclSum, cs);
     HIP_CHECK(hipEventRecord(ev_done_, cs));

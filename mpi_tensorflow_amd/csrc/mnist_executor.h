@@ -8,6 +8,8 @@
 // step counter.  The call is therefore capturable into a hipGraph and the
 // Python trainer replays the captured graph.
 //
+// Compute runs on ONE stream (cross-stream event hops cost 5-18 us each in
+// graph replay); independent work is merged into single launches instead.
 // Gradient all-reduce (when a communicator is attached) runs in two buckets
 // on a dedicated comm stream:
 //   bucket 1 = FC params (97 % of the bytes), launched as soon as the fc1
@@ -64,6 +66,8 @@ class MnistExecutor {
   const MnistPtrs& ptrs() const { return p_; }
 
  private:
+  void enqueue_fwd_bwd(hipStream_t s);
   MnistPtrs p_;
-  hipEvent_t ev_b1_ = nullptr, ev_b2_ = nullptr, ev_done_ = nullptr;
+  hipEvent_t ev_head_ = nullptr, ev_dx_ = nullptr, ev_dw_ = nullptr, ev_filt_ = nullptr,
+             ev_fin_ = nullptr, ev_done_ = nullptr;
 };

@@ -261,26 +261,9 @@ class NativeMnistEngine(MnistEngineBase):
                 self._graph(k % G)
 
     def forward_backward_only(self) -> None:
+        """Forward + backward into the flat grad buffer; no sync, no SGD, no
+        step increment (used by the numerics tests)."""
         self.exe.forward_backward(stream_handle())
-        self.exe_backward_rest()
-
-    def exe_backward_rest(self):
-        """conv backward + finalize without sync/SGD (used by numerics tests)."""
-        C_ = self._C
-        p, b, B = self.ptrs, self.bufs, self.B
-        s = stream_handle()
-        W, G = self.params, self.grads
-        lay = self.layout
-        C_.mnist.conv2_bwd(ptr(b["a1"]), ptr(b["dy2"]), ptr(b["w2t"]), B,
-                           ptr(b["da1m"]), ptr(b["part2"]), s)
-        C_.mnist.conv1_bwd_filter(ptr(self.train_x), ptr(self.step_dev), self.n_local, B,
-                                  ptr(b["da1m"]), ptr(b["idx1"]), ptr(b["part1"]), s)
-        C_.mnist.grad_finalize(ptr(b["part2"]), C_.mnist.conv2_filter_splits(B), ptr(b["part1"]),
-                               C_.mnist.conv1_filter_blocks(B),
-                               ptr(G) + 4 * lay.offsets["conv2_weight"],
-                               ptr(G) + 4 * lay.offsets["conv2_bias"],
-                               ptr(G) + 4 * lay.offsets["conv1_weight"],
-                               ptr(G) + 4 * lay.offsets["conv1_bias"], s)
 
     def loss_value(self) -> float:
         return float(self.bufs["loss_rows"].mean().item()) + self.l2_value()
