@@ -501,36 +501,71 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 //    LDS at all: coalesced 128 B loads of a1 and dY2 feed the MFMAs directly.
 constexpr int C2_XS_ROWS = 8, C2_XS_COLS = 18;
 
+#ifdef MNIST_STAMPS
+#define STAMP(slot)                                                                  \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
+    if ((threadIdx.x & 63) == 0)                                                     \
+      g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + slot] = _t; \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+  } while (0)
+__device__ unsigned long long* g_stamps;
+#else
+#define STAMP(slot) \
+  do {              \
+  } while (0)
+#endif
+
 // conv2 forward + bias + ReLU + 2x2 maxpool (+argmax).  Block = (image, pair of
-// pooled rows); 8 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
-// (N: 32 output channels) x 2 (K: input-channel halves, summed through LDS),
-// i.e. two waves per SIMD so one wave's LDS/L2 latency hides under the
-// other's MFMAs.  A and B operands are fetched one tap ahead.  Also writes
-// W2T[t][co][ci] (the transposed weight copy bwd-data reads) when w2t != 0.
+// pooled rows); 4 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
+// (N: 32 output channels), one wave per SIMD, each wave owning the FULL K
+// (800) of its tile with two independent accumulator chains (even / odd
+// channel pairs) so consecutive MFMAs never wait on each other's result and
+// no cross-wave K reduction (barrier + LDS round trip) is needed.  A operands
+// come from the LDS halo tile, B (weights, L2 resident) one tap ahead in
+// registers.  Also writes W2T[t][co][ci] for bwd-data when w2t != nullptr.
 constexpr int C2_XS = C2_XS_ROWS * C2_XS_COLS * 33;
 
-__global__ __launch_bounds__(512) void conv2_fwd_v3_kernel(
+__global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ b2, float* __restrict__ out, uint8_t* __restrict__ argmax,
     float* __restrict__ w2t) {
-  __shared__ float xs[C2_XS + 4 * 16 * 64];
-  float* red = xs + C2_XS;
+  STAMP(0);
+#ifdef MNIST_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + 5] =
+        __builtin_amdgcn_s_memrealtime();
+#endif
+  __shared__ float xs[C2_XS];
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (w2t) {  // 51200 floats over all blocks
-    for (int i = blockIdx.x * 512 + tid; i < 51200; i += gridDim.x * 512) {
+    for (int i = blockIdx.x * 256 + tid; i < 51200; i += gridDim.x * 256) {
       const int ci = i & 31, co = (i >> 5) & 63, t = i >> 11;
       w2t[i] = w2[(t * 32 + ci) * 64 + co];
     }
   }
-  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 32; i += 512) {
-    const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
-    const int y = 2 * pr0 - 2 + r, x = c - 2;
-    const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
-    const float v = a1[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 32 + ci];
-    xs[(r * C2_XS_COLS + c) * 33 + ci] = ok ? v : 0.f;
+  {  // stage the halo tile: all loads in flight first, then the LDS writes
+    constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 32 / 256;  // 18
+    float sv[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + 256 * j;
+      const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
+      const int y = 2 * pr0 - 2 + r, x = c - 2;
+      const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
+      const float v = a1[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 32 + ci];
+      sv[j] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + 256 * j;
+      const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
+      xs[(r * C2_XS_COLS + c) * 33 + ci] = sv[j];
+    }
   }
-  const int msub = wave & 1, nsub = (wave >> 1) & 1, kg = wave >> 2;
+  const int msub = wave & 1, nsub = wave >> 1;
   const int m = msub * 32 + (lane & 31);
   const int win = m >> 2, q = m & 3;
   int ly = 0, lx = 0;
@@ -538,23 +573,24 @@ __global__ __launch_bounds__(512) void conv2_fwd_v3_kernel(
     ly = 2 * (win / 7) + (q >> 1);
     lx = 2 * (win % 7) + (q & 1);
   }
-  const int abase = (ly * C2_XS_COLS + lx) * 33 + kg * 16 + (lane >> 5);
+  const int abase = (ly * C2_XS_COLS + lx) * 33 + (lane >> 5);
   const int co = nsub * 32 + (lane & 31);
-  const float* wp = w2 + (kg * 16 + (lane >> 5)) * 64 + co;  // + (t*32 + 2c) * 64
-  float bc[8], bn[8], ac[8], an[8];
+  const float* wp = w2 + (lane >> 5) * 64 + co;  // + (t*32 + 2c) * 64
+  float bc[16], bn[16], ac[16], an[16];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) bc[c] = wp[(2 * c) * 64];
+  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 64];
   __syncthreads();
+  STAMP(1);
 #pragma unroll
-  for (int c = 0; c < 8; ++c) ac[c] = xs[abase + 2 * c];
-  f32x16 acc = zero16();
+  for (int c = 0; c < 16; ++c) ac[c] = xs[abase + 2 * c];
+  f32x16 acc0 = zero16(), acc1 = zero16();
 #pragma unroll
   for (int t = 0; t < 25; ++t) {
     if (t + 1 < 25) {
       const int kh = (t + 1) / 5, kw = (t + 1) % 5;
       const float* xa = xs + abase + (kh * C2_XS_COLS + kw) * 33;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < 16; ++c) {
         bn[c] = wp[((t + 1) * 32 + 2 * c) * 64];
         an[c] = xa[2 * c];
       }
@@ -563,23 +599,27 @@ __global__ __launch_bounds__(512) void conv2_fwd_v3_kernel(
     // them next to their use and expose the L2 latency on every MFMA)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc = mfma32x32x2(ac[c], bc[c], acc);
+    for (int c = 0; c < 16; c += 2) {
+      acc0 = mfma32x32x2(ac[c], bc[c], acc0);
+      acc1 = mfma32x32x2(ac[c + 1], bc[c + 1], acc1);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 16; ++c) {
       bc[c] = bn[c];
       ac[c] = an[c];
     }
   }
-  const int sub = msub + 2 * nsub;
-  if (kg == 1) {
+  STAMP(2);
+  f32x16 acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(sub * 16 + r) * 64 + lane] = acc[r];
-  }
-  __syncthreads();
-  if (kg == 1) return;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] += red[(sub * 16 + r) * 64 + lane];
+  for (int r = 0; r < 16; ++r) acc[r] = acc0[r] + acc1[r];
+  STAMP(3);
+#ifdef MNIST_STAMPS
+  if ((threadIdx.x & 63) == 0)
+    g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + 6] =
+        __builtin_amdgcn_s_memrealtime();
+#endif
   const float bias = b2[co];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -604,61 +644,78 @@ __global__ __launch_bounds__(512) void conv2_fwd_v3_kernel(
 
 // conv2 bwd-data (+ReLU1 mask): dA1m[n,y,x,ci] = [a1>0] * sum_{kh,kw,co}
 // dY2[n, y+2-kh, x+2-kw, co] W2[kh,kw,ci,co].  Block = (image, 4 output rows);
-// 8 waves = 2 (M: 2 rows x 16 cols) x 4 (K: co quarters, summed through LDS).
+// 4 waves (one per SIMD) = 2 (M: 2 rows x 16 cols) x 2 (K: co halves, summed
+// once through LDS at the end); each wave runs two accumulator chains.
 constexpr int C2_DS = C2_XS_ROWS * C2_XS_COLS * 65;
-constexpr int C2B_SMEM = C2_DS + 3 * 2 * 16 * 64;
+constexpr int C2B_SMEM = C2_DS;
 
 __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
                                   const float* __restrict__ dy2, const float* __restrict__ w2t,
                                   float* __restrict__ da1m, float* smem) {
   float* ds = smem;  // [8][18][65]
-  float* red = smem + C2_DS;
   const int n = bid >> 2, y0 = 4 * (bid & 3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < C2_XS_ROWS * C2_XS_COLS * 64; i += 512) {
-    const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
-    const int y = y0 - 2 + r, x = c - 2;
-    const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
-    const float v = dy2[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 64 + co];
-    ds[(r * C2_XS_COLS + c) * 65 + co] = ok ? v : 0.f;
+  {  // stage the halo tile: all loads in flight first, then the LDS writes
+    constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 64 / 256;  // 36
+    float sv[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + 256 * j;
+      const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
+      const int y = y0 - 2 + r, x = c - 2;
+      const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
+      const float v = dy2[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 64 + co];
+      sv[j] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + 256 * j;
+      const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
+      ds[(r * C2_XS_COLS + c) * 65 + co] = sv[j];
+    }
   }
-  const int msub = wave & 1, cog = wave >> 1;  // cog: co quarter (16 channels)
+  const int msub = wave & 1, cog = wave >> 1;  // cog: co half (32 channels)
   const int r2 = (lane & 31) >> 4, x = lane & 15;
   const int ly = 2 * msub + r2, lx = x < 14 ? x : 0;
   // staged row of source pixel (y+2-kh) is ly + 4 - kh; col lx + 4 - kw
-  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 16 + (lane >> 5);
-  const float* wp = w2t + (cog * 16 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
-  float bc[8], bn[8], ac[8], an[8];
+  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 32 + (lane >> 5);
+  const float* wp = w2t + (cog * 32 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
+  float bc[16], bn[16], ac[16], an[16];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) bc[c] = wp[(2 * c) * 32];
+  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 32];
   __syncthreads();
 #pragma unroll
-  for (int c = 0; c < 8; ++c) ac[c] = ds[abase + 2 * c];
-  f32x16 acc = zero16();
+  for (int c = 0; c < 16; ++c) ac[c] = ds[abase + 2 * c];
+  f32x16 acc0 = zero16(), acc1 = zero16();
 #pragma unroll
   for (int t = 0; t < 25; ++t) {
     if (t + 1 < 25) {
       const int kh = (t + 1) / 5, kw = (t + 1) % 5;
       const float* xa = ds + abase - (kh * C2_XS_COLS + kw) * 65;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < 16; ++c) {
         bn[c] = wp[((t + 1) * 64 + 2 * c) * 32];
         an[c] = xa[2 * c];
       }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) acc = mfma32x32x2(ac[c], bc[c], acc);
+    for (int c = 0; c < 16; c += 2) {
+      acc0 = mfma32x32x2(ac[c], bc[c], acc0);
+      acc1 = mfma32x32x2(ac[c + 1], bc[c + 1], acc1);
+    }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < 16; ++c) {
       bc[c] = bn[c];
       ac[c] = an[c];
     }
   }
-  if (cog > 0) {
+  __syncthreads();  // ds is dead: reuse it for the 2-way K reduction
+  float* red = smem + msub * 16 * 64;
+  if (cog == 1) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) red[(((cog - 1) * 2 + msub) * 16 + r) * 64 + lane] = acc[r];
+    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc0[r] + acc1[r];
   }
   __syncthreads();
   if (cog == 0) {
@@ -669,9 +726,7 @@ __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
       const int y = y0 + 2 * msub + (mr >> 4), xx = mr & 15;
       if (y < 14 && xx < 14) {
         const int o = ((n * 14 + y) * 14 + xx) * 32 + ci;
-        float g = acc[r];
-#pragma unroll
-        for (int j = 0; j < 3; ++j) g += red[((j * 2 + msub) * 16 + r) * 64 + lane];
+        const float g = acc0[r] + acc1[r] + red[r * 64 + lane];
         da1m[o] = a1[o] > 0.f ? g : 0.f;
       }
     }
@@ -706,7 +761,7 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   const int nsub = wave & 1, ih = wave >> 1;
   const int ci = lane & 31, kpar = lane >> 5;
   const int co = nsub * 32 + (lane & 31);
-  f32x16 acc = zero16();
+  f32x16 acc = zero16(), acc1 = zero16();
   float dbs = 0.f;
   const int n = g * C2F_GROUPS_IMG + ih;
   if (n < batch) {
@@ -733,7 +788,10 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int xp = 0; xp < 7; ++xp) {
-        acc = mfma32x32x2(av[xp], bv[xp], acc);
+        if (xp & 1)
+          acc1 = mfma32x32x2(av[xp], bv[xp], acc1);
+        else
+          acc = mfma32x32x2(av[xp], bv[xp], acc);
         dbs += bv[xp];
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -744,6 +802,8 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
       }
     }
   }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] += acc1[r];
   // sum the four images (ih) through LDS, write one slab per block
   float* red = smem;
   if (ih > 0) {
@@ -767,7 +827,7 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   }
 }
 
-__global__ __launch_bounds__(512) void conv2_bwd_data_kernel(const float* __restrict__ a1,
+__global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const float* __restrict__ a1,
                                                             const float* __restrict__ dy2,
                                                             const float* __restrict__ w2t,
                                                             float* __restrict__ da1m) {
@@ -921,7 +981,7 @@ void launch_conv1_fwd(const float* data, const long long* step, int n_local, int
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s) {
-  conv2_fwd_v3_kernel<<<batch * 4, 512, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
+  conv2_fwd_v3_kernel<<<batch * 4, 256, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
 }
 
 int fc1_train_splits() { return FC1_SPLITS; }
@@ -969,7 +1029,7 @@ int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
 
 void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
                            float* da1m, hipStream_t s) {
-  conv2_bwd_data_kernel<<<batch * 4, 512, 0, s>>>(a1, dy2, w2t, da1m);
+  conv2_bwd_data_kernel<<<batch * 4, 256, 0, s>>>(a1, dy2, w2t, da1m);
 }
 
 void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,

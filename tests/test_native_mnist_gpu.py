@@ -84,23 +84,49 @@ def test_forward_backward_grads_match_oracle(cuda_dev, data):
         assert err < 2e-4, (s.name, err)
 
 
+def test_per_step_grads_along_native_trajectory(cuda_dev, data):
+    """Strict per-step check: at every step the native grads equal the oracle's
+    grads evaluated at the NATIVE parameters (no chaotic accumulation)."""
+    nat, ref = _engines(cuda_dev, data)
+    for step in range(12):
+        ref.params.copy_(nat.params)
+        ref.set_step(step)
+        nat.forward_backward_only()
+        ref.forward_backward(step)
+        torch.cuda.synchronize()
+        nv, rv = nat.layout.views(nat.grads), ref.layout.views(ref.grads)
+        errs = {s.name: ((nv[s.name] - rv[s.name]).norm() / rv[s.name].norm()).item()
+                for s in nat.layout.specs}
+        print(step, {k: f"{v:.1e}" for k, v in errs.items()})
+        # a max-pool near-tie (fp32 summation order) can re-route single
+        # elements; everything else must agree to fp32 rounding
+        assert max(errs.values()) < 5e-3, (step, errs)
+        assert sorted(errs.values())[len(errs) // 2] < 1e-4, (step, errs)
+        nat.train(1)
+
+
 def test_training_trajectory_matches_oracle(cuda_dev, data):
     nat, ref = _engines(cuda_dev, data)
     p0 = ref.params.clone()
-    nat.train(30)
-    ref.train(30)
-    torch.cuda.synchronize()
+    losses_n, losses_r = [], []
+    for _ in range(6):
+        nat.train(5)
+        ref.train(5)
+        torch.cuda.synchronize()
+        losses_n.append(nat.loss_value())
+        losses_r.append(ref.loss_value())
     assert nat.step == ref.step == 30
     assert int(nat.step_dev.item()) == 30
     assert abs(nat.device_lr() - ref.lr(29)) < 1e-9
-    # fp32 rounding differences can flip a ReLU/max-pool decision at a tie and
-    # route one element's gradient differently, so compare in relative L2
-    # (max-abs is reported for information)
+    # fp32 summation-order differences can flip a ReLU / max-pool tie and route
+    # one element's gradient differently; over 30 steps that drift compounds,
+    # so the trajectory is compared loosely (the strict check is per step)
     d = nat.params - ref.params
-    rel_upd = (d.norm() / (ref.params - p0).norm()).item()  # error relative to the update
-    print(f"trajectory: rel_update_err={rel_upd:.3e} max_abs={d.abs().max().item():.3e}")
-    assert rel_upd < 1e-2, rel_upd
-    assert abs(nat.loss_value() - (ref.last_loss + ref.l2_value())) < 1e-3
+    rel_upd = (d.norm() / (ref.params - p0).norm()).item()
+    print(f"trajectory: rel_update_err={rel_upd:.3e} losses native={losses_n} ref={losses_r}")
+    assert rel_upd < 5e-2, rel_upd
+    for a, b in zip(losses_n, losses_r):
+        assert abs(a - b) < 2e-2 * max(1.0, abs(b))
 
 
 def test_graph_replay_equals_eager(cuda_dev, data):
