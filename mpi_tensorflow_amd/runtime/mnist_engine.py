@@ -151,8 +151,11 @@ class NativeMnistEngine(MnistEngineBase):
 
     kind = "native"
 
-    def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None):
+    def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None,
+                 force_sync: bool = False):
         super().__init__(cfg, train_x, train_y, device, rank, world, comm)
+        if force_sync and comm is not None:  # exercise the collective path at world 1
+            self.grad_sync = True
         if device.type != "cuda":
             raise RuntimeError("NativeMnistEngine needs a GPU")
         if self.B % 32 != 0:

@@ -171,3 +171,26 @@ def test_sgd_kernel(cuda_dev):
     we = w0 - 0.05 * me
     assert _rel(m, me) < 1e-6 and _rel(w, we) < 1e-6
     assert int(step.item()) == 1
+
+
+def test_native_rccl_comm_and_graph_capture(cuda_dev, data):
+    """World-size-1 RCCL communicator: dlopen of torch's librccl, unique-id
+    bootstrap, all-reduce on a HIP stream, and the training step with both
+    gradient buckets captured into a hipGraph (the 8-GPU path)."""
+    from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
+    from mpi_tensorflow_amd.parallel.dist import DistInfo
+
+    comm = RcclDeviceComm(DistInfo())
+    t = torch.arange(1000, dtype=torch.float32, device=cuda_dev)
+    comm.all_reduce_(t)
+    torch.cuda.synchronize()
+    assert torch.equal(t, torch.arange(1000, dtype=torch.float32, device=cuda_dev))
+    x, y = data
+    cfg = C.TrainConfig(graph=True, graph_steps=3).validate()
+    synced = NativeMnistEngine(cfg, x, y, cuda_dev, comm=comm, force_sync=True)
+    plain = NativeMnistEngine(C.TrainConfig(graph=False).validate(), x, y, cuda_dev)
+    assert synced.grad_sync and synced.comm_stream is not None
+    synced.train(7)  # 2 replays of a captured 3-step graph (with RCCL) + a 1-step graph
+    plain.train(7)
+    torch.cuda.synchronize()
+    assert torch.equal(synced.params, plain.params)
