@@ -12,6 +12,7 @@
 
 #include "idx_loader.h"
 #include "kernels/mnist.h"
+#include "kernels/ops_generic.h"
 #include "mnist_executor.h"
 #include "rccl_comm.h"
 
@@ -133,6 +134,103 @@ PYBIND11_MODULE(_C, m) {
   });
   o.def("scale", [](uintptr_t x, long long n, float a, uintptr_t s) {
     optim::launch_scale(P<float>(x), n, a, S(s));
+    check_launch();
+  });
+
+  // ------------------------------------------------------- generic ops
+  auto g = m.def_submodule("ops", "generic NHWC layer kernels (conv/bn/pool/xent)");
+  py::class_<gops::ConvShape>(g, "ConvShape")
+      .def(py::init([](int N, int H, int W, int C, int K, int R, int S, int stride, int pad) {
+             gops::ConvShape s{N, H, W, C, K, R, S, stride, pad, (H + 2 * pad - R) / stride + 1,
+                               (W + 2 * pad - S) / stride + 1};
+             return s;
+           }))
+      .def_readonly("N", &gops::ConvShape::N).def_readonly("H", &gops::ConvShape::H)
+      .def_readonly("W", &gops::ConvShape::W).def_readonly("C", &gops::ConvShape::C)
+      .def_readonly("K", &gops::ConvShape::K).def_readonly("R", &gops::ConvShape::R)
+      .def_readonly("S", &gops::ConvShape::S).def_readonly("stride", &gops::ConvShape::stride)
+      .def_readonly("pad", &gops::ConvShape::pad).def_readonly("OH", &gops::ConvShape::OH)
+      .def_readonly("OW", &gops::ConvShape::OW);
+  py::class_<gops::PoolShape>(g, "PoolShape")
+      .def(py::init([](int N, int H, int W, int C, int k, int stride, int pad) {
+        gops::PoolShape p{N, H, W, C, k, stride, pad, (H + 2 * pad - k) / stride + 1,
+                          (W + 2 * pad - k) / stride + 1};
+        return p;
+      }))
+      .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
+  g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
+                       bool relu, uintptr_t st) {
+    gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu, S(st));
+    check_launch();
+  });
+  g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
+                            uintptr_t st) {
+    gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), S(st));
+    check_launch();
+  });
+  g.def("conv_filter_splits", &gops::conv_filter_splits);
+  g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,
+                              uintptr_t dw, uintptr_t st) {
+    gops::conv_bwd_filter(s, P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), S(st));
+    check_launch();
+  });
+  g.def("colsum2", [](uintptr_t a, uintptr_t b, long long rows, int C, uintptr_t s1, uintptr_t s2,
+                      int mode, uintptr_t st) {
+    gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode, S(st));
+    check_launch();
+  });
+  g.def("bn_fwd", [](uintptr_t x, long long rows, int C, uintptr_t gm, uintptr_t bt, uintptr_t res,
+                     uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t sum, uintptr_t sumsq,
+                     float eps, bool relu, bool training, uintptr_t rmean, uintptr_t rvar,
+                     uintptr_t st) {
+    gops::bn_fwd(P<const float>(x), rows, C, P<const float>(gm), P<const float>(bt),
+                 P<const float>(res), P<float>(y), P<float>(mean), P<float>(rstd), P<float>(sum),
+                 P<float>(sumsq), eps, relu, training, P<const float>(rmean), P<const float>(rvar), S(st));
+    check_launch();
+  });
+  g.def("bn_bwd", [](uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
+                     uintptr_t gm, long long rows, int C, bool relu, uintptr_t dym, uintptr_t xh,
+                     uintptr_t dg, uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st) {
+    gops::bn_bwd(P<const float>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
+                 P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(dym), P<float>(xh),
+                 P<float>(dg), P<float>(db), P<float>(dx), P<float>(dres), S(st));
+    check_launch();
+  });
+  g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {
+    gops::maxpool_fwd(p, P<const float>(x), P<float>(y), P<int>(arg), S(st));
+    check_launch();
+  });
+  g.def("maxpool_bwd", [](const gops::PoolShape& p, uintptr_t dy, uintptr_t arg, uintptr_t dx, uintptr_t st) {
+    gops::maxpool_bwd(p, P<const float>(dy), P<const int>(arg), P<float>(dx), S(st));
+    check_launch();
+  });
+  g.def("avgpool_fwd", [](uintptr_t x, uintptr_t y, int N, int HW, int C, uintptr_t st) {
+    gops::avgpool_fwd(P<const float>(x), P<float>(y), N, HW, C, S(st));
+    check_launch();
+  });
+  g.def("avgpool_bwd", [](uintptr_t dy, uintptr_t dx, int N, int HW, int C, uintptr_t st) {
+    gops::avgpool_bwd(P<const float>(dy), P<float>(dx), N, HW, C, S(st));
+    check_launch();
+  });
+  g.def("xent", [](uintptr_t logits, uintptr_t labels, int B, int C, uintptr_t loss_rows,
+                   uintptr_t dlogits, uintptr_t correct, uintptr_t st) {
+    gops::xent(P<const float>(logits), P<const int>(labels), B, C, P<float>(loss_rows),
+               P<float>(dlogits), P<int>(correct), S(st));
+    check_launch();
+  });
+  g.def("relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, long long n, uintptr_t st) {
+    gops::relu_bwd(P<const float>(dy), P<const float>(y), P<float>(dx), n, S(st));
+    check_launch();
+  });
+  g.def("lr_from_step", [](uintptr_t step, int n_local, int batch, float base, float decay,
+                           uintptr_t lr, uintptr_t st) {
+    gops::lr_from_step(P<const long long>(step), n_local, batch, base, decay, P<float>(lr), S(st));
+    check_launch();
+  });
+  g.def("gather_batch", [](uintptr_t data, uintptr_t labels, uintptr_t step, int n_local, int batch,
+                           long long row_elems, uintptr_t xb, uintptr_t yb, uintptr_t st) {
+    gops::gather_batch(P<const float>(data), P<const int>(labels), P<const long long>(step), n_local,
+                       batch, row_elems, P<float>(xb), P<int>(yb), S(st));
     check_launch();
   });
 

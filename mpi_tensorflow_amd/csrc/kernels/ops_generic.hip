@@ -1,0 +1,610 @@
+// Generic NHWC layer kernels for the LeNet-5 / ResNet-18 configs (BASELINE.json
+// configs 4-5) on gfx950: implicit-GEMM convolution (forward with fused bias
+// + ReLU, backward-data, backward-filter with split-K slabs), BatchNorm
+// (training statistics, fused apply + residual + ReLU, backward), max / global
+// average pooling, fused softmax cross-entropy, batch gather and slab
+// reduction.  Linear layers are 1x1 convolutions over a 1x1 image.
+//
+// Every GEMM-shaped op runs on v_mfma_f32_32x32x2_f32 through gemm_core.h;
+// shapes are runtime values (one code object serves every layer), with the
+// per-slot address decode hoisted out of the K loop by the gather contexts.
+#include <stdexcept>
+
+#include "common.h"
+#include "gemm_core.h"
+#include "ops_generic.h"
+
+namespace gops {
+
+// ---------------------------------------------------------------- conv ----
+struct ConvFwdProb {
+  static constexpr bool A_KC = true, B_NC = true;
+  struct ACtx {
+    const float* img;  // x + n*H*W*C + ci0 (slot's channel inside the tile)
+    int iy0, ix0, kl;
+    bool v;
+  };
+  struct BCtx {
+    const float* p;
+    int kl;
+    bool v;
+  };
+  ConvShape s;
+  const float* x;
+  const float* w;
+  int Ktot, M;
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const {
+    const bool v = m < M;
+    const int mm = v ? m : 0;
+    const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+    return {x + (size_t)n * s.H * s.W * s.C, oy * s.stride - s.pad, ox * s.stride - s.pad, kl, v};
+  }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
+    const int k = k0 + c.kl;
+    const int ci = k % s.C, t = k / s.C;
+    const int kh = t / s.S, kw = t % s.S;
+    const int iy = c.iy0 + kh, ix = c.ix0 + kw;
+    const bool ok = c.v && k < Ktot && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+    const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+    const float val = c.img[(iyc * s.W + ixc) * s.C + ci];
+    return ok ? val : 0.f;
+  }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const {
+    const bool v = n < s.K;
+    return {w + (v ? n : 0), kl, v};
+  }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    const int k = k0 + c.kl;
+    const float val = c.p[(size_t)min(k, Ktot - 1) * s.K];
+    return (c.v && k < Ktot) ? val : 0.f;
+  }
+};
+
+// dX[n,iy,ix,ci] = sum_{kh,kw,co} dY[n,oy,ox,co] W[kh,kw,ci,co], iy = oy*s - p + kh
+struct ConvDataProb {
+  static constexpr bool A_KC = true, B_NC = false;
+  struct ACtx {
+    const float* img;  // dy + n*OH*OW*K
+    int iyp, ixp, kl;  // iy + pad, ix + pad
+    bool v;
+  };
+  struct BCtx {
+    const float* p;  // w + ci*K
+    int kl;
+    bool v;
+  };
+  ConvShape s;
+  const float* dy;
+  const float* w;
+  int Ktot, M;  // Ktot = R*S*K (co fastest)
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const {
+    const bool v = m < M;
+    const int mm = v ? m : 0;
+    const int ix = mm % s.W, t = mm / s.W, iy = t % s.H, n = t / s.H;
+    return {dy + (size_t)n * s.OH * s.OW * s.K, iy + s.pad, ix + s.pad, kl, v};
+  }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
+    const int k = k0 + c.kl;
+    const int co = k % s.K, t = k / s.K;
+    const int kh = t / s.S, kw = t % s.S;
+    const int ny = c.iyp - kh, nx = c.ixp - kw;
+    const int oy = ny / s.stride, ox = nx / s.stride;
+    const bool ok = c.v && k < Ktot && ny >= 0 && nx >= 0 && oy * s.stride == ny &&
+                    ox * s.stride == nx && oy < s.OH && ox < s.OW;
+    const int oyc = min(max(oy, 0), s.OH - 1), oxc = min(max(ox, 0), s.OW - 1);
+    const float val = c.img[(oyc * s.OW + oxc) * s.K + co];
+    return ok ? val : 0.f;
+  }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const {
+    const bool v = n < s.C;
+    return {w + (size_t)(v ? n : 0) * s.K, kl, v};
+  }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    const int k = min(k0 + c.kl, Ktot - 1);
+    const int co = k % s.K, t = k / s.K;
+    const float val = c.p[(size_t)t * s.C * s.K + co];
+    return (c.v && k0 + c.kl < Ktot) ? val : 0.f;
+  }
+};
+
+// dW[(kh,kw,ci)][co] = sum_pix X[n, oy*s+kh-p, ox*s+kw-p, ci] dY[pix][co]
+struct ConvFilterProb {
+  static constexpr bool A_KC = false, B_NC = true;
+  struct ACtx {
+    int kh, kw, ci, kl;
+    bool v;
+  };
+  struct BCtx {
+    const float* p;
+    int kl;
+    bool v;
+  };
+  ConvShape s;
+  const float* x;
+  const float* dy;
+  int Mw, npix;  // Mw = R*S*C
+  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const {
+    const bool v = m < Mw;
+    const int mm = v ? m : 0;
+    const int ci = mm % s.C, t = mm / s.C;
+    return {t / s.S, t % s.S, ci, kl, v};
+  }
+  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
+    const int pix = k0 + c.kl;
+    const int pc = min(pix, npix - 1);
+    const int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
+    const int iy = oy * s.stride + c.kh - s.pad, ix = ox * s.stride + c.kw - s.pad;
+    const bool ok = c.v && pix < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+    const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+    const float val = x[(((size_t)n * s.H + iyc) * s.W + ixc) * s.C + c.ci];
+    return ok ? val : 0.f;
+  }
+  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const {
+    const bool v = n < s.K;
+    return {dy + (size_t)kl * s.K + (v ? n : 0), kl, v};
+  }
+  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
+    const int pix = k0 + c.kl;
+    const float val = c.p[(size_t)(min(pix, npix - 1) - c.kl) * s.K];
+    return (c.v && pix < npix) ? val : 0.f;
+  }
+};
+
+constexpr int WM = 2, WN = 2, BK = 32;
+using CFG_F = gemm::Cfg<WM, WN, 1, BK, true, true>;
+
+__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvShape s, const float* __restrict__ x,
+                                                       const float* __restrict__ w,
+                                                       const float* __restrict__ bias,
+                                                       float* __restrict__ y, int relu) {
+  __shared__ float smem[CFG_F::SMEM_FLOATS];
+  const int M = s.N * s.OH * s.OW, Ktot = s.R * s.S * s.C;
+  ConvFwdProb p{s, x, w, Ktot, M};
+  const int mt = (M + CFG_F::BM - 1) / CFG_F::BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * CFG_F::BM, n0 = (bid / mt) * CFG_F::BN;
+  const int kend = (Ktot + BK - 1) / BK * BK;
+  f32x16 acc;
+  int wm, wn;
+  gemm::run_tile<WM, WN, 1, BK>(p, smem, m0, n0, 0, kend, acc, wm, wn);
+  const int lane = threadIdx.x & 63;
+  const int co = n0 + 32 * wn + (lane & 31);
+  if (co >= s.K) return;
+  const float b = bias ? bias[co] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + 32 * wm + mfma32_row(r, lane);
+    if (m >= M) continue;
+    float v = acc[r] + b;
+    if (relu) v = fmaxf(v, 0.f);
+    y[(size_t)m * s.K + co] = v;
+  }
+}
+
+using CFG_D = gemm::Cfg<WM, WN, 1, BK, true, false>;
+__global__ __launch_bounds__(256) void conv_bwd_data_kernel(ConvShape s,
+                                                            const float* __restrict__ dy,
+                                                            const float* __restrict__ w,
+                                                            float* __restrict__ dx) {
+  __shared__ float smem[CFG_D::SMEM_FLOATS];
+  const int M = s.N * s.H * s.W, Ktot = s.R * s.S * s.K;
+  ConvDataProb p{s, dy, w, Ktot, M};
+  const int mt = (M + CFG_D::BM - 1) / CFG_D::BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * CFG_D::BM, n0 = (bid / mt) * CFG_D::BN;
+  const int kend = (Ktot + BK - 1) / BK * BK;
+  f32x16 acc;
+  int wm, wn;
+  gemm::run_tile<WM, WN, 1, BK>(p, smem, m0, n0, 0, kend, acc, wm, wn);
+  const int lane = threadIdx.x & 63;
+  const int ci = n0 + 32 * wn + (lane & 31);
+  if (ci >= s.C) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + 32 * wm + mfma32_row(r, lane);
+    if (m < M) dx[(size_t)m * s.C + ci] = acc[r];
+  }
+}
+
+using CFG_W = gemm::Cfg<WM, WN, 1, BK, false, true>;
+__global__ __launch_bounds__(256) void conv_bwd_filter_kernel(ConvShape s,
+                                                              const float* __restrict__ x,
+                                                              const float* __restrict__ dy,
+                                                              float* __restrict__ part,
+                                                              int kchunk) {
+  __shared__ float smem[CFG_W::SMEM_FLOATS];
+  const int Mw = s.R * s.S * s.C, npix = s.N * s.OH * s.OW;
+  ConvFilterProb p{s, x, dy, Mw, npix};
+  const int mt = (Mw + CFG_W::BM - 1) / CFG_W::BM, nt = (s.K + CFG_W::BN - 1) / CFG_W::BN;
+  const int bid = blockIdx.x;
+  const int tile = bid % (mt * nt), z = bid / (mt * nt);
+  const int m0 = (tile % mt) * CFG_W::BM, n0 = (tile / mt) * CFG_W::BN;
+  const int kb = z * kchunk, ke = min(kb + kchunk, (npix + BK - 1) / BK * BK);
+  f32x16 acc;
+  int wm, wn;
+  gemm::run_tile<WM, WN, 1, BK>(p, smem, m0, n0, kb, ke, acc, wm, wn);
+  const int lane = threadIdx.x & 63;
+  const int co = n0 + 32 * wn + (lane & 31);
+  if (co >= s.K) return;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int m = m0 + 32 * wm + mfma32_row(r, lane);
+    if (m < Mw) part[((size_t)z * Mw + m) * s.K + co] = acc[r];
+  }
+}
+
+// out[i] = sum_z part[z][i]  (+ optional per-column bias-grad: colsum of dY)
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ part, int nz,
+                                                       long long n, float* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float s = 0.f;
+    for (int z = 0; z < nz; ++z) s += part[z * n + i];
+    out[i] = s;
+  }
+}
+
+// ------------------------------------------------- per-channel reductions ----
+// sums[c] = sum_rows a[r][c], sums2[c] = sum_rows a[r][c]*b[r][c] (b optional).
+// Block = 256 threads = (64 channels) x (4 row groups); grid-y splits rows;
+// partials reduced by atomics into zeroed outputs (two scalars per channel).
+__global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ a,
+                                                      const float* __restrict__ b, int rows,
+                                                      int C, int rows_per_block,
+                                                      float* __restrict__ s1,
+                                                      float* __restrict__ s2, int mode) {
+  // mode 0: s1 = sum a, s2 = sum a^2 ; mode 1: s1 = sum a, s2 = sum a*b
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rg = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float x1 = 0.f, x2 = 0.f;
+  if (c < C) {
+    for (int r = r0 + rg; r < r1; r += 4) {
+      const float v = a[(size_t)r * C + c];
+      x1 += v;
+      x2 += mode == 0 ? v * v : v * b[(size_t)r * C + c];
+    }
+  }
+  __shared__ float red[2][4][64];
+  red[0][rg][threadIdx.x & 63] = x1;
+  red[1][rg][threadIdx.x & 63] = x2;
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const int l = threadIdx.x & 63;
+    const float t1 = red[0][0][l] + red[0][1][l] + red[0][2][l] + red[0][3][l];
+    const float t2 = red[1][0][l] + red[1][1][l] + red[1][2][l] + red[1][3][l];
+    atomicAdd(&s1[c], t1);
+    atomicAdd(&s2[c], t2);
+  }
+}
+
+// BN forward apply: y = (x - mean) * rstd * g + b (+ res) (relu)
+__global__ __launch_bounds__(256) void bn_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ sum, const float* __restrict__ sumsq,
+    const float* __restrict__ g, const float* __restrict__ b, const float* __restrict__ res,
+    float* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
+    long long rows, int C, float eps, int relu, int use_stats, const float* __restrict__ rmean,
+    const float* __restrict__ rvar) {
+  const long long n = rows * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float inv = 1.f / (float)rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    float mean, rstd;
+    if (use_stats) {
+      mean = sum[c] * inv;
+      const float var = fmaxf(sumsq[c] * inv - mean * mean, 0.f);
+      rstd = rsqrtf(var + eps);
+      if (i < C && mean_out) {
+        mean_out[c] = mean;
+        rstd_out[c] = rstd;
+      }
+    } else {
+      mean = rmean[c];
+      rstd = rsqrtf(rvar[c] + eps);
+    }
+    float v = (x[i] - mean) * rstd * g[c] + b[c];
+    if (res) v += res[i];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = v;
+  }
+}
+
+// BN backward: dx = g*rstd*(dy' - mean(dy') - xhat*mean(dy'*xhat)), dy' = dy*[y>0]
+// sum_dy, sum_dyx are the per-channel sums of dy' and dy'*xhat.
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
+    const float* __restrict__ sum_dy, const float* __restrict__ sum_dyx, float* __restrict__ dx,
+    float* __restrict__ dres, long long rows, int C, int relu) {
+  const long long n = rows * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float inv = 1.f / (float)rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    float d = dy[i];
+    if (relu && y[i] <= 0.f) d = 0.f;
+    if (dres) dres[i] = d;
+    const float xh = (x[i] - mean[c]) * rstd[c];
+    dx[i] = g[c] * rstd[c] * (d - sum_dy[c] * inv - xh * sum_dyx[c] * inv);
+  }
+}
+
+// dy' (relu-masked) and xhat products for the BN backward reductions
+__global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ dy,
+                                                          const float* __restrict__ y,
+                                                          const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          float* __restrict__ dym,
+                                                          float* __restrict__ xh, long long rows,
+                                                          int C, int relu) {
+  const long long n = rows * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    float d = dy[i];
+    if (relu && y[i] <= 0.f) d = 0.f;
+    dym[i] = d;
+    xh[i] = (x[i] - mean[c]) * rstd[c];
+  }
+}
+
+// ------------------------------------------------------------- pooling ----
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(PoolShape p, const float* __restrict__ x,
+                                                          float* __restrict__ y,
+                                                          int* __restrict__ arg) {
+  const long long n = (long long)p.N * p.OH * p.OW * p.C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % p.C);
+    long long t = i / p.C;
+    const int ox = (int)(t % p.OW);
+    t /= p.OW;
+    const int oy = (int)(t % p.OH);
+    const int nn = (int)(t / p.OH);
+    float best = -INFINITY;
+    int bi = -1;
+    for (int kh = 0; kh < p.k; ++kh)
+      for (int kw = 0; kw < p.k; ++kw) {
+        const int iy = oy * p.stride - p.pad + kh, ix = ox * p.stride - p.pad + kw;
+        if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
+        const int idx = (nn * p.H + iy) * p.W + ix;
+        const float v = x[(size_t)idx * p.C + c];
+        if (v > best) {
+          best = v;
+          bi = idx;
+        }
+      }
+    y[i] = best;
+    arg[i] = bi;
+  }
+}
+
+// gather form (deterministic): each input element sums the outputs whose argmax it is
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolShape p, const float* __restrict__ dy,
+                                                          const int* __restrict__ arg,
+                                                          float* __restrict__ dx) {
+  const long long n = (long long)p.N * p.H * p.W * p.C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % p.C);
+    const long long pix = i / p.C;
+    const int ix = (int)(pix % p.W);
+    const int iy = (int)((pix / p.W) % p.H);
+    const int nn = (int)(pix / ((long long)p.W * p.H));
+    float g = 0.f;
+    const int oy0 = max(0, (iy + p.pad - p.k + p.stride) / p.stride);
+    const int oy1 = min(p.OH - 1, (iy + p.pad) / p.stride);
+    const int ox0 = max(0, (ix + p.pad - p.k + p.stride) / p.stride);
+    const int ox1 = min(p.OW - 1, (ix + p.pad) / p.stride);
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const size_t o = (((size_t)nn * p.OH + oy) * p.OW + ox) * p.C + c;
+        if (arg[o] == (int)pix) g += dy[o];
+      }
+    dx[i] = g;
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x,
+                                                          float* __restrict__ y, int N, int HW,
+                                                          int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  float s = 0.f;
+  for (int p = 0; p < HW; ++p) s += x[((size_t)n * HW + p) * C + c];
+  y[i] = s / (float)HW;
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dy,
+                                                          float* __restrict__ dx, int N, int HW,
+                                                          int C) {
+  const long long n = (long long)N * HW * C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int c = (int)(i % C);
+    const int nn = (int)(i / ((long long)HW * C));
+    dx[i] = dy[nn * C + c] / (float)HW;
+  }
+}
+
+// ----------------------------------------------------- softmax xent ----
+// one wave per row: loss_row = lse - logit[label]; dlogits = (p - onehot)/B
+__global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ logits,
+                                                   const int* __restrict__ labels, int B, int C,
+                                                   float* __restrict__ loss_rows,
+                                                   float* __restrict__ dlogits,
+                                                   int* __restrict__ correct) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const int lab = labels[row];
+  float mx = -INFINITY;
+  for (int c = lane; c < C; c += 64) mx = fmaxf(mx, logits[(size_t)row * C + c]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int c = lane; c < C; c += 64) se += __expf(logits[(size_t)row * C + c] - mx);
+  se = wave_sum(se);
+  int am = C;
+  for (int c = lane; c < C; c += 64)
+    if (logits[(size_t)row * C + c] == mx) am = min(am, c);
+  for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
+  for (int c = lane; c < C; c += 64) {
+    const float p = __expf(logits[(size_t)row * C + c] - mx) / se;
+    if (dlogits) dlogits[(size_t)row * C + c] = (p - (c == lab ? 1.f : 0.f)) / (float)B;
+  }
+  if (lane == 0) {
+    loss_rows[row] = logf(se) + mx - logits[(size_t)row * C + lab];
+    if (correct) atomicAdd(correct, am == lab ? 1 : 0);
+  }
+}
+
+// batch gather from a device-resident dataset at the device-step offset
+__global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ data,
+                                                           const int* __restrict__ labels,
+                                                           const long long* step, int n_local,
+                                                           int batch, long long row_elems,
+                                                           float* __restrict__ xb,
+                                                           int* __restrict__ yb) {
+  const long long s = step ? *step : 0;
+  const long long off = (s * batch) % (long long)(n_local - batch);
+  const long long n = (long long)batch * row_elems;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const float4* src = reinterpret_cast<const float4*>(data + off * row_elems);
+  float4* dst = reinterpret_cast<float4*>(xb);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n / 4; i += stride)
+    dst[i] = src[i];
+  if (blockIdx.x == 0 && threadIdx.x < batch) yb[threadIdx.x] = labels[off + threadIdx.x];
+}
+
+// dx = dy * [y > 0]
+__global__ __launch_bounds__(256) void relu_bwd_kernel(const float* __restrict__ dy,
+                                                       const float* __restrict__ y,
+                                                       float* __restrict__ dx, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dx[i] = y[i] > 0.f ? dy[i] : 0.f;
+}
+
+// device-side learning rate of the reference schedule (mpipy.py:59-64)
+__global__ void lr_kernel(const long long* step, int n_local, int batch, float base, float decay,
+                          float* lr) {
+  const long long s = *step;
+  lr[0] = base * powf(decay, (float)((s * batch) / n_local));
+}
+
+static inline int grid1d(long long n) {
+  long long b = (n + 255) / 256;
+  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+}
+
+// ------------------------------------------------------------ launchers ----
+void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
+              bool relu, hipStream_t st) {
+  const int M = s.N * s.OH * s.OW;
+  const int blocks = ((M + CFG_F::BM - 1) / CFG_F::BM) * ((s.K + CFG_F::BN - 1) / CFG_F::BN);
+  conv_fwd_kernel<<<blocks, 256, 0, st>>>(s, x, w, bias, y, relu ? 1 : 0);
+}
+
+void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, hipStream_t st) {
+  const int M = s.N * s.H * s.W;
+  const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
+  conv_bwd_data_kernel<<<blocks, 256, 0, st>>>(s, dy, w, dx);
+}
+
+int conv_filter_splits(const ConvShape& s) {
+  const int Mw = s.R * s.S * s.C;
+  const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);
+  const int ktiles = (s.N * s.OH * s.OW + BK - 1) / BK;
+  int z = (1024 + tiles - 1) / tiles;  // aim for ~1024 blocks
+  z = z < 1 ? 1 : z;
+  z = z > ktiles ? ktiles : z;
+  z = z > 64 ? 64 : z;
+  return z;
+}
+
+void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* part, float* dw,
+                     hipStream_t st) {
+  const int Mw = s.R * s.S * s.C;
+  const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);
+  const int ktiles = (s.N * s.OH * s.OW + BK - 1) / BK;
+  const int z = conv_filter_splits(s);
+  const int kchunk = ((ktiles + z - 1) / z) * BK;
+  const int zz = (ktiles * BK + kchunk - 1) / kchunk;
+  conv_bwd_filter_kernel<<<tiles * zz, 256, 0, st>>>(s, x, dy, part, kchunk);
+  const long long n = (long long)Mw * s.K;
+  slab_sum_kernel<<<grid1d(n), 256, 0, st>>>(part, zz, n, dw);
+}
+
+void colsum2(const float* a, const float* b, long long rows, int C, float* s1, float* s2, int mode,
+             hipStream_t st) {
+  (void)hipMemsetAsync(s1, 0, C * sizeof(float), st);
+  (void)hipMemsetAsync(s2, 0, C * sizeof(float), st);
+  int gy = (int)((rows + 511) / 512);
+  if (gy > 1024) gy = 1024;
+  const int rpb = (int)((rows + gy - 1) / gy);
+  dim3 grid((C + 63) / 64, gy);
+  colsum2_kernel<<<grid, 256, 0, st>>>(a, b, (int)rows, C, rpb, s1, s2, mode);
+}
+
+void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
+            const float* res, float* y, float* mean, float* rstd, float* sum, float* sumsq,
+            float eps, bool relu, bool training, const float* rmean, const float* rvar,
+            hipStream_t st) {
+  if (training) colsum2(x, nullptr, rows, C, sum, sumsq, 0, st);
+  bn_apply_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, sum, sumsq, g, b, res, y, mean, rstd, rows,
+                                                     C, eps, relu ? 1 : 0, training ? 1 : 0,
+                                                     rmean, rvar);
+}
+
+void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
+            const float* g, long long rows, int C, bool relu, float* dym, float* xh, float* dg,
+            float* db, float* dx, float* dres, hipStream_t st) {
+  bn_bwd_prep_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, dy, y, mean, rstd, dym, xh, rows, C,
+                                                        relu ? 1 : 0);
+  colsum2(dym, xh, rows, C, db, dg, 1, st);  // db = sum dy', dg = sum dy'*xhat
+  bn_bwd_apply_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx, dres,
+                                                         rows, C, relu ? 1 : 0);
+}
+
+void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st) {
+  maxpool_fwd_kernel<<<grid1d((long long)p.N * p.OH * p.OW * p.C), 256, 0, st>>>(p, x, y, arg);
+}
+
+void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st) {
+  maxpool_bwd_kernel<<<grid1d((long long)p.N * p.H * p.W * p.C), 256, 0, st>>>(p, dy, arg, dx);
+}
+
+void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st) {
+  avgpool_fwd_kernel<<<(N * C + 255) / 256, 256, 0, st>>>(x, y, N, HW, C);
+}
+
+void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t st) {
+  avgpool_bwd_kernel<<<grid1d((long long)N * HW * C), 256, 0, st>>>(dy, dx, N, HW, C);
+}
+
+void xent(const float* logits, const int* labels, int B, int C, float* loss_rows, float* dlogits,
+          int* correct, hipStream_t st) {
+  xent_kernel<<<(B + 3) / 4, 256, 0, st>>>(logits, labels, B, C, loss_rows, dlogits, correct);
+}
+
+void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st) {
+  relu_bwd_kernel<<<grid1d(n), 256, 0, st>>>(dy, y, dx, n);
+}
+
+void lr_from_step(const long long* step, int n_local, int batch, float base, float decay,
+                  float* lr, hipStream_t st) {
+  lr_kernel<<<1, 1, 0, st>>>(step, n_local, batch, base, decay, lr);
+}
+
+void gather_batch(const float* data, const int* labels, const long long* step, int n_local,
+                  int batch, long long row_elems, float* xb, int* yb, hipStream_t st) {
+  if (row_elems % 4 != 0 || batch > 256) throw std::runtime_error("gather_batch: unsupported shape");
+  gather_batch_kernel<<<grid1d((long long)batch * row_elems / 4), 256, 0, st>>>(
+      data, labels, step, n_local, batch, row_elems, xb, yb);
+}
+
+}  // namespace gops

@@ -1,0 +1,271 @@
+"""Autograd layer ops for the generic models (LeNet-5, ResNet-18).
+
+Two implementations with identical math, chosen by the device of the input:
+
+* GPU (`x.is_cuda`): the hand-written gfx950 kernels of
+  `csrc/kernels/ops_generic.hip` through `_C.ops` - NHWC implicit-GEMM conv
+  on fp32 MFMA (bias + ReLU fused), BatchNorm with the residual add + ReLU
+  fused, max / average pooling, fused softmax cross-entropy.  Parameter
+  gradients are written by the kernels STRAIGHT into the caller's flat grad
+  buffer views (`Param.grad_view`), so a finished backward leaves the
+  all-reduce buckets ready with no extra copies; the autograd functions
+  return None for parameters.
+* CPU: the plain-PyTorch fp32 oracle of the same ops (NCHW permutes around
+  torch.nn.functional), used for the CPU/gloo config and as the numerics
+  reference of the kernels.  There is no runtime fallback on GPU: the native
+  extension is required there (`ops.require_native`).
+
+Tensors are NHWC, conv weights HWIO, linear weights [in, out] (the layouts
+the reference uses for its TF variables, /root/reference/mpipy.py:38-53).
+"""
+
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import native, ptr, stream_handle
+
+
+@dataclasses.dataclass
+class Param:
+    """A trainable tensor: a view of the flat param buffer plus the matching
+    view of the flat grad buffer the backward kernels write into."""
+
+    value: torch.Tensor
+    grad_view: torch.Tensor
+
+
+def _empty(shape, like):
+    return torch.empty(shape, dtype=like.dtype, device=like.device)
+
+
+# ------------------------------------------------------------------- conv --
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, shape, relu, gw, gb, ws):
+        C = native()
+        x = x.contiguous()
+        y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
+        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, stream_handle())
+        ctx.save_for_backward(x, w, y)
+        ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x, w, y = ctx.saved_tensors
+        s = stream_handle()
+        dy = dy.contiguous()
+        if ctx.relu:
+            dym = torch.empty_like(dy)
+            C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
+            dy = dym
+        sh = ctx.shape
+        C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s)
+        if ctx.has_b:
+            scratch = torch.empty(sh.K, device=dy.device, dtype=dy.dtype)
+            C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0, s)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
+            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), s)
+        return dx, None, None, None, None, None, None, None
+
+
+class ConvWorkspace:
+    """Split-K slab workspace for the filter-gradient kernels (grown lazily;
+    sized once before graph capture)."""
+
+    def __init__(self):
+        self.t: Optional[torch.Tensor] = None
+
+    def get(self, n: int, device) -> torch.Tensor:
+        if self.t is None or self.t.numel() < n or self.t.device != device:
+            self.t = torch.empty(n, dtype=torch.float32, device=device)
+        return self.t
+
+
+_WS = ConvWorkspace()
+
+
+def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: int = 0,
+           relu: bool = False) -> torch.Tensor:
+    """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K]."""
+    N, H, W, Cin = x.shape
+    R, S, _, K = w.value.shape
+    if x.is_cuda:
+        C = native()
+        sh = C.ops.ConvShape(N, H, W, Cin, K, R, S, stride, pad)
+        nws = C.ops.conv_filter_splits(sh) * R * S * Cin * K
+        ws = _WS.get(nws, x.device)
+        return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
+                             None if b is None else b.grad_view, ws)
+    y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
+                 None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
+    return F.relu(y) if relu else y
+
+
+def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) -> torch.Tensor:
+    """x [N,in], w [in,out] -> [N,out] (a 1x1 conv over a 1x1 image on GPU)."""
+    if x.is_cuda:
+        n, fin = x.shape
+        fout = w.value.shape[1]
+        w4 = Param(w.value.view(1, 1, fin, fout), w.grad_view.view(1, 1, fin, fout))
+        y = conv2d(x.reshape(n, 1, 1, fin), w4, b, 1, 0, relu)
+        return y.reshape(n, fout)
+    y = x @ w.value + (0 if b is None else b.value)
+    return F.relu(y) if relu else y
+
+
+# -------------------------------------------------------------- batchnorm --
+class _BNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, res, relu, gg, gb, rmean, rvar, momentum, eps, training):
+        C = native()
+        x = x.contiguous()
+        Cc = x.shape[-1]
+        rows = x.numel() // Cc
+        s = stream_handle()
+        y = torch.empty_like(x)
+        mean = torch.empty(Cc, device=x.device)
+        rstd = torch.empty(Cc, device=x.device)
+        s1 = torch.empty(Cc, device=x.device)
+        s2 = torch.empty(Cc, device=x.device)
+        C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(y), ptr(mean), ptr(rstd),
+                     ptr(s1), ptr(s2), eps, relu, training, ptr(rmean), ptr(rvar), s)
+        if training:  # running statistics for eval (unbiased var, as torch)
+            with torch.no_grad():
+                bm = s1 / rows
+                var = (s2 / rows - bm * bm).clamp_min(0) * (rows / max(rows - 1, 1))
+                rmean.mul_(1 - momentum).add_(momentum * bm)
+                rvar.mul_(1 - momentum).add_(momentum * var)
+        ctx.save_for_backward(x, y, mean, rstd, g)
+        ctx.relu, ctx.gg, ctx.gb, ctx.has_res = relu, gg, gb, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        x, y, mean, rstd, g = ctx.saved_tensors
+        dy = dy.contiguous()
+        Cc = x.shape[-1]
+        rows = x.numel() // Cc
+        dym = torch.empty_like(dy)
+        xh = torch.empty_like(dy)
+        dx = torch.empty_like(dy)
+        dres = torch.empty_like(dy) if ctx.has_res else None
+        C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
+                     ptr(dym), ptr(xh), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres),
+                     stream_handle())
+        return dx, None, None, dres, None, None, None, None, None, None, None, None
+
+
+def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: torch.Tensor,
+              training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None,
+              momentum: float = 0.1, eps: float = 1e-5) -> torch.Tensor:
+    """BatchNorm over N,H,W of an NHWC tensor, optional fused residual + ReLU."""
+    if x.is_cuda:
+        res = None if residual is None else residual.contiguous()
+        if training:
+            return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
+                               rvar, momentum, eps, True)
+        C = native()
+        y = torch.empty_like(x)
+        Cc = x.shape[-1]
+        C.ops.bn_fwd(ptr(x.contiguous()), x.numel() // Cc, Cc, ptr(g.value), ptr(b.value),
+                     ptr(res), ptr(y), 0, 0, 0, 0, eps, relu, False, ptr(rmean), ptr(rvar),
+                     stream_handle())
+        return y
+    xn = x.permute(0, 3, 1, 2)
+    y = F.batch_norm(xn, rmean, rvar, g.value, b.value, training, momentum, eps).permute(0, 2, 3, 1)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+# ---------------------------------------------------------------- pooling --
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, stride, pad):
+        C = native()
+        x = x.contiguous()
+        N, H, W, Cc = x.shape
+        sh = C.ops.PoolShape(N, H, W, Cc, k, stride, pad)
+        y = _empty((N, sh.OH, sh.OW, Cc), x)
+        arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.int32, device=x.device)
+        C.ops.maxpool_fwd(sh, ptr(x), ptr(y), ptr(arg), stream_handle())
+        ctx.save_for_backward(arg)
+        ctx.sh, ctx.xshape = sh, x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        (arg,) = ctx.saved_tensors
+        dx = _empty(ctx.xshape, dy)
+        C.ops.maxpool_bwd(ctx.sh, ptr(dy.contiguous()), ptr(arg), ptr(dx), stream_handle())
+        return dx, None, None, None
+
+
+def maxpool(x: torch.Tensor, k: int, stride: int, pad: int = 0) -> torch.Tensor:
+    if x.is_cuda:
+        return _MaxPoolFn.apply(x, k, stride, pad)
+    return F.max_pool2d(x.permute(0, 3, 1, 2), k, stride, pad).permute(0, 2, 3, 1)
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        C = native()
+        x = x.contiguous()
+        N, H, W, Cc = x.shape
+        y = torch.empty((N, Cc), dtype=x.dtype, device=x.device)
+        C.ops.avgpool_fwd(ptr(x), ptr(y), N, H * W, Cc, stream_handle())
+        ctx.xshape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C = native()
+        N, H, W, Cc = ctx.xshape
+        dx = torch.empty(ctx.xshape, dtype=dy.dtype, device=dy.device)
+        C.ops.avgpool_bwd(ptr(dy.contiguous()), ptr(dx), N, H * W, Cc, stream_handle())
+        return dx
+
+
+def global_avgpool(x: torch.Tensor) -> torch.Tensor:
+    if x.is_cuda:
+        return _AvgPoolFn.apply(x)
+    return x.mean(dim=(1, 2))
+
+
+# ------------------------------------------------------------------- loss --
+class _XentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        C = native()
+        logits = logits.contiguous()
+        B, K = logits.shape
+        loss_rows = torch.empty(B, device=logits.device)
+        dlog = torch.empty_like(logits)
+        C.ops.xent(ptr(logits), ptr(labels), B, K, ptr(loss_rows), ptr(dlog), 0, stream_handle())
+        ctx.save_for_backward(dlog)
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dlog,) = ctx.saved_tensors
+        return dlog * g, None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """mean softmax cross-entropy; labels int32 on GPU."""
+    if logits.is_cuda:
+        return _XentFn.apply(logits, labels.to(torch.int32))
+    return F.cross_entropy(logits, labels.long())

@@ -1,0 +1,182 @@
+"""Training engine for the generic models (LeNet-5, ResNet-18).
+
+Same contract as the MNIST engines (runtime/mnist_engine.py): flat fp32
+param / grad / momentum buffers, the reference's LR schedule and momentum
+SGD (/root/reference/mpipy.py:59-66), batch offset (step*B) % (N-B), DP by
+per-step gradient all-reduce of the flat grad buffer.
+
+On GPU one training step is: batch gather from the device-resident shard at
+the device step offset -> forward/backward through the native NHWC kernels
+(parameter grads land directly in the flat grad buffer) -> RCCL all-reduce
+(world > 1) -> device LR -> flat SGD kernel (which bumps the device step).
+Nothing in the step touches the host, so G steps are captured into one
+hipGraph (torch.cuda.CUDAGraph) after a short eager warm-up and replayed.
+On CPU the same model runs through the PyTorch oracle ops.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import config as C
+from ..models.generic import make_model
+from ..ops import functional as Fn
+from ..ops import native, ptr, stream_handle
+from ..parallel.comm import DeviceComm
+from ..utils.data import batch_offset
+from ..utils.schedule import learning_rate
+
+
+class GenericEngine:
+    kind = "generic"
+
+    def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
+                 device: torch.device, rank: int = 0, world: int = 1,
+                 comm: Optional[DeviceComm] = None):
+        self.cfg, self.device, self.rank, self.world, self.comm = cfg, device, rank, world, comm
+        self.model = make_model(cfg.model)
+        self.layout = self.model.layout
+        self.B = cfg.batch_size
+        self.n_local = int(train_x.shape[0])
+        if self.n_local <= self.B:
+            raise ValueError("local shard must exceed the batch")
+        host = torch.zeros(self.layout.total)
+        self.model.init_params(host, cfg.seed)
+        self.params = host.to(device).requires_grad_(True)
+        self.grads = torch.zeros(self.layout.total, device=device)
+        self.mom = torch.zeros(self.layout.total, device=device)
+        pv = self.layout.views(self.params)
+        gv = self.layout.views(self.grads)
+        self.P = {s.name: Fn.Param(pv[s.name], gv[s.name]) for s in self.layout.specs}
+        self.bn = self.model.make_bn_state(device)
+        self.train_x = torch.from_numpy(np.ascontiguousarray(train_x, np.float32)).to(device)
+        self.train_y = torch.from_numpy(np.asarray(train_y).astype(np.int32)).to(device)
+        self.step = 0
+        self.grad_sync = cfg.sync == "grad" and world > 1 and comm is not None
+        self.on_gpu = device.type == "cuda"
+        self.use_graph = cfg.graph and self.on_gpu
+        self.graph_steps = max(1, cfg.graph_steps)
+        self._graphs = {}
+        self.loss_buf = torch.zeros((), device=device)
+        if self.on_gpu:
+            self._C = native()
+            h, w, c = train_x.shape[1:]
+            self.xb = torch.empty(self.B, h, w, c, device=device)
+            self.yb = torch.empty(self.B, dtype=torch.int32, device=device)
+            self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
+            self.lr_dev = torch.zeros(1, device=device)
+
+    # ------------------------------------------------------------------ util
+    def lr(self, step: Optional[int] = None) -> float:
+        s = self.step if step is None else step
+        return learning_rate(s, self.n_local, self.B, self.cfg.base_lr, self.cfg.lr_decay)
+
+    def set_step(self, step: int) -> None:
+        self.step = int(step)
+        if self.on_gpu:
+            self.step_dev.fill_(int(step))
+
+    def loss_value(self) -> float:
+        return float(self.loss_buf.item())
+
+    def param_views(self):
+        return self.layout.views(self.params.detach())
+
+    # ------------------------------------------------------------------ step
+    def _step_gpu(self):
+        C_ = self._C
+        s = stream_handle()
+        row = int(np.prod(self.xb.shape[1:]))
+        C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
+                            self.B, row, ptr(self.xb), ptr(self.yb), s)
+        logits = self.model.forward(self.P, self.bn, self.xb, True)
+        loss = Fn.cross_entropy(logits, self.yb)
+        loss.backward()
+        self.loss_buf.copy_(loss.detach())
+        gscale = 1.0
+        if self.grad_sync:
+            self.comm.all_reduce_(self.grads)
+            gscale = 1.0 / self.world
+        C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
+                            self.cfg.lr_decay, ptr(self.lr_dev), s)
+        C_.optim.sgd_momentum(ptr(self.params), ptr(self.grads), ptr(self.mom), self.layout.total, 0,
+                              0.0, self.cfg.momentum, gscale, ptr(self.lr_dev), 0.0,
+                              ptr(self.step_dev), s)
+
+    def _step_cpu(self):
+        off = batch_offset(self.step, self.n_local, self.B)
+        x = self.train_x[off:off + self.B]
+        y = self.train_y[off:off + self.B]
+        self.params.grad = None
+        logits = self.model.forward(self.P, self.bn, x, True)
+        loss = Fn.cross_entropy(logits, y)
+        loss.backward()
+        with torch.no_grad():
+            self.grads.copy_(self.params.grad)
+            self.loss_buf.copy_(loss.detach())
+            if self.grad_sync:
+                self.comm.all_reduce_(self.grads)
+                self.grads.mul_(1.0 / self.world)
+            self.mom.mul_(self.cfg.momentum).add_(self.grads)
+            self.params.sub_(self.lr() * self.mom)
+
+    def _graph(self, n: int):
+        g = self._graphs.get(n)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(n):
+                    self._step_gpu()
+            self._graphs[n] = g
+        return g
+
+    def capture(self, k: int) -> None:
+        pass  # graphs are captured lazily after the eager warm-up in train()
+
+    def train(self, k: int) -> None:
+        if k <= 0:
+            return
+        if not self.on_gpu:
+            for _ in range(k):
+                self._step_cpu()
+                self.step += 1
+            return
+        done = 0
+        if self.use_graph and not self._graphs:
+            # eager warm-up on a side stream before the first capture (torch's
+            # documented requirement for capturing autograd); real steps
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(min(3, k)):
+                    self._step_gpu()
+                    done += 1
+            torch.cuda.current_stream().wait_stream(s)
+        left = k - done
+        if not self.use_graph:
+            for _ in range(left):
+                self._step_gpu()
+        else:
+            G = self.graph_steps
+            full, rem = divmod(left, G)
+            if full:
+                g = self._graph(G)
+                for _ in range(full):
+                    g.replay()
+            for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
+                self._step_gpu()
+        self.step += k
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 256, dropout: bool = False):
+        wrong = 0
+        for a in range(0, x.shape[0], chunk):
+            xb = torch.from_numpy(np.ascontiguousarray(x[a:a + chunk], np.float32)).to(self.device)
+            logits = self.model.forward(self.P, self.bn, xb, False)
+            pred = logits.argmax(1).cpu().numpy()
+            wrong += int((pred != y[a:a + chunk]).sum())
+        return 100.0 * wrong / max(1, x.shape[0])

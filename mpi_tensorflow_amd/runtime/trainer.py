@@ -85,11 +85,21 @@ class Trainer:
                                           pad=cfg.pad_train_shard, seed=cfg.seed)
         else:
             from ..models.generic import model_input_shape
+            from ..utils.data import Shard, SplitSizes, synthetic_images_torch
 
             shape = model_input_shape(cfg.model)
-            rows = 4096 if cfg.model == "lenet5" else 512
-            self.shard = synthetic_image_shard(self.rank, self.world, rows, rows // 4, shape,
-                                               seed=cfg.seed)
+            if cfg.model == "lenet5":
+                rows = 8192
+                self.shard = synthetic_image_shard(self.rank, self.world, rows, rows // 4, shape,
+                                                   seed=cfg.seed)
+            else:  # 224x224x3: generated with torch (numpy path is too heavy)
+                rows, trows = 512, 256
+                tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=self.rank * rows)
+                sx, sy = synthetic_images_torch(trows, shape, seed=cfg.seed + 1,
+                                                start=self.rank * trows)
+                self.shard = Shard(tx.numpy(), ty.numpy(), sx.numpy(), sy.numpy(),
+                                   sx.numpy()[:0], sy.numpy()[:0], True,
+                                   SplitSizes(self.world, rows * self.world, trows * self.world, 0))
         if self.shard.test_x.shape[0] < 1:
             raise ValueError("empty local test shard")
 

@@ -253,3 +253,26 @@ def synthetic_image_shard(rank: int, world: int, rows_per_rank: int, test_per_ra
     sx, sy = synthetic_rows("test", b, b + test_per_rank, seed, classes, shape)
     sizes = SplitSizes(world, rows_per_rank * world, test_per_rank * world, 0)
     return Shard(tx, ty, sx, sy, sx[:0], sy[:0], True, sizes)
+
+
+def synthetic_images_torch(n: int, shape: Tuple[int, int, int], classes: int = 10,
+                           seed: int = C.SEED, start: int = 0, device="cpu"):
+    """Large-image synthetic data (ResNet-18 at 224x224x3) generated with torch
+    on the target device: class prototypes (a coarse random field upsampled
+    16x) + per-image noise, values in [-0.5, 0.5], NHWC float32, int64 labels.
+    Deterministic in (seed, start); rows [start, start+n)."""
+    import torch
+
+    h, w, c = shape
+    g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + 17)
+    ch, cw = max(2, h // 16), max(2, w // 16)
+    protos = torch.randn(classes, c, ch, cw, generator=g)
+    protos = torch.nn.functional.interpolate(protos, size=(h, w), mode="bilinear",
+                                             align_corners=False)
+    gl = torch.Generator(device="cpu").manual_seed(seed * 7919 + start)
+    labels = torch.randint(0, classes, (n,), generator=gl)
+    gn = torch.Generator(device=device).manual_seed(seed * 104729 + start)
+    x = protos.to(device)[labels.to(device)] * 0.25
+    x = x + 0.15 * torch.randn(x.shape, generator=gn, device=device)
+    x = x.clamp_(-0.5, 0.5).permute(0, 2, 3, 1).contiguous()
+    return x, labels

@@ -1,0 +1,162 @@
+"""Numerics of the generic gfx950 layer kernels (csrc/kernels/ops_generic.hip)
+vs plain PyTorch fp32, and of whole LeNet-5 / ResNet-18 training steps vs the
+CPU oracle path."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mpi_tensorflow_amd import config as C
+from mpi_tensorflow_amd.ops import functional as Fn
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return ((a.float() - b.float()).norm() / max(1e-12, b.float().norm())).item()
+
+
+def _param(t):
+    return Fn.Param(t.clone().requires_grad_(True), torch.zeros_like(t))
+
+
+@pytest.mark.parametrize("N,H,W,Cin,K,R,stride,pad,relu,bias", [
+    (4, 9, 7, 5, 6, 3, 1, 1, True, True),
+    (4, 12, 12, 8, 16, 3, 2, 1, False, False),
+    (2, 16, 16, 3, 64, 7, 2, 3, False, False),
+    (3, 8, 8, 16, 32, 1, 2, 0, False, False),
+    (5, 1, 1, 40, 70, 1, 1, 0, True, True),  # linear as a 1x1 conv
+])
+def test_conv_fwd_bwd(cuda_dev, N, H, W, Cin, K, R, stride, pad, relu, bias):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(R, R, Cin, K, generator=g) * 0.2
+    b = torch.randn(K, generator=g) * 0.1 if bias else None
+    dy = torch.randn(N, (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1, K,
+                     generator=g)
+    # oracle
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if bias else None
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), br, stride=stride,
+                  padding=pad).permute(0, 2, 3, 1)
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(dy)
+    # native
+    xg = x.to(cuda_dev).requires_grad_(True)
+    wp = _param(w.to(cuda_dev))
+    bp = _param(b.to(cuda_dev)) if bias else None
+    yg = Fn.conv2d(xg, wp, bp, stride, pad, relu)
+    yg.backward(dy.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert _rel(yg.cpu(), yr.detach()) < 1e-5
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-5
+    assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-5
+    if bias:
+        assert _rel(bp.grad_view.cpu(), br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_batchnorm(cuda_dev, relu, res):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(6, 5, 7, 24, generator=g) * 2 + 1
+    r = torch.randn(6, 5, 7, 24, generator=g)
+    gam = torch.rand(24, generator=g) + 0.5
+    bet = torch.randn(24, generator=g)
+    dy = torch.randn(6, 5, 7, 24, generator=g)
+    xr = x.clone().requires_grad_(True)
+    rr = r.clone().requires_grad_(True)
+    gr, br = gam.clone().requires_grad_(True), bet.clone().requires_grad_(True)
+    yr = F.batch_norm(xr.permute(0, 3, 1, 2), None, None, gr, br, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    if res:
+        yr = yr + rr
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(dy)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    rg = r.to(cuda_dev).requires_grad_(True)
+    gp, bp = _param(gam.to(cuda_dev)), _param(bet.to(cuda_dev))
+    rm, rv = torch.zeros(24, device=cuda_dev), torch.ones(24, device=cuda_dev)
+    yg = Fn.batchnorm(xg, gp, bp, rm, rv, True, relu, rg if res else None)
+    yg.backward(dy.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert _rel(yg.cpu(), yr.detach()) < 1e-5
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-4
+    assert _rel(gp.grad_view.cpu(), gr.grad) < 1e-4
+    assert _rel(bp.grad_view.cpu(), br.grad) < 1e-5
+    if res:
+        assert _rel(rg.grad.cpu(), rr.grad) < 1e-6
+    assert torch.allclose(rm.cpu(), 0.1 * x.mean(dim=(0, 1, 2)), atol=1e-5)
+
+
+@pytest.mark.parametrize("k,stride,pad,H", [(2, 2, 0, 12), (3, 2, 1, 13)])
+def test_maxpool(cuda_dev, k, stride, pad, H):
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(3, H, H, 10, generator=g)
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr.permute(0, 3, 1, 2), k, stride, pad).permute(0, 2, 3, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    yg = Fn.maxpool(xg, k, stride, pad)
+    yg.backward(dy.to(cuda_dev))
+    assert torch.equal(yg.cpu(), yr.detach())
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-6
+
+
+def test_avgpool_and_xent(cuda_dev):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(4, 7, 7, 33, generator=g)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    y = Fn.global_avgpool(xg)
+    y.sum().backward()
+    assert _rel(y.cpu(), x.mean(dim=(1, 2))) < 1e-6
+    assert torch.allclose(xg.grad.cpu(), torch.full_like(x, 1 / 49.0))
+    logits = torch.randn(9, 13, generator=g)
+    lab = torch.randint(0, 13, (9,), generator=g)
+    lr_ = logits.clone().requires_grad_(True)
+    F.cross_entropy(lr_, lab).backward()
+    lg = logits.to(cuda_dev).requires_grad_(True)
+    loss = Fn.cross_entropy(lg, lab.to(cuda_dev))
+    loss.backward()
+    assert abs(loss.item() - F.cross_entropy(logits, lab).item()) < 1e-5
+    assert _rel(lg.grad.cpu(), lr_.grad) < 1e-5
+
+
+@pytest.mark.parametrize("model,shape,B", [("lenet5", (32, 32, 3), 8), ("resnet18", (32, 32, 3), 4)])
+def test_model_grads_native_vs_oracle(cuda_dev, model, shape, B):
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 64, shape=shape)
+    cfg = C.TrainConfig(model=model, batch_size=B, graph=False).validate()
+    gpu = GenericEngine(cfg, x, y, cuda_dev)
+    cpu = GenericEngine(C.TrainConfig(model=model, batch_size=B, device="cpu").validate(), x, y,
+                        torch.device("cpu"))
+    cpu.params.data.copy_(gpu.params.detach().cpu())
+    gpu.train(1)
+    cpu._step_cpu()
+    torch.cuda.synchronize()
+    assert abs(gpu.loss_value() - cpu.loss_value()) < 1e-4 * max(1.0, cpu.loss_value())
+    gv, cv = gpu.layout.views(gpu.grads), cpu.layout.views(cpu.grads)
+    for s in gpu.layout.specs:
+        e = _rel(gv[s.name].cpu(), cv[s.name])
+        assert e < 1e-3, (s.name, e)
+    assert _rel(gpu.params.detach().cpu(), cpu.params.detach()) < 1e-4
+
+
+def test_generic_graph_replay_equals_eager(cuda_dev):
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 512, shape=(32, 32, 3))
+    a = GenericEngine(C.TrainConfig(model="lenet5", graph=False).validate(), x, y, cuda_dev)
+    b = GenericEngine(C.TrainConfig(model="lenet5", graph=True, graph_steps=4).validate(), x, y,
+                      cuda_dev)
+    a.train(13)
+    b.train(13)  # 3 eager warm-up + 2 graph replays of 4 + 2 eager
+    torch.cuda.synchronize()
+    assert int(b.step_dev.item()) == 13
+    assert _rel(b.params.detach(), a.params.detach()) < 1e-6
