@@ -35,7 +35,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--batch-size", type=int, default=64)
+    ap.add_argument("--model", default="mnist_cnn", choices=("mnist_cnn", "lenet5", "resnet18"))
+    ap.add_argument("--batch-size", type=int, default=None,
+                    help="per-GPU batch (default 64; 32 for resnet18)")
     ap.add_argument("--dtype", default="fp32", choices=("fp32", "bf16"))
     ap.add_argument("--sync", default="grad", choices=("grad", "none"))
     ap.add_argument("--graph-steps", type=int, default=25)
@@ -58,11 +60,27 @@ def main(argv=None) -> int:
     if di.world != a.gpus:
         print(f"warning: --gpus {a.gpus} but world size {di.world}; using world size", file=sys.stderr)
     N = di.world
-    cfg = C.TrainConfig(batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
+    if a.batch_size is None:
+        a.batch_size = 32 if a.model == "resnet18" else 64
+    cfg = C.TrainConfig(model=a.model, batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
                         graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend).validate()
-    shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
     comm = make_comm(di, device) if (N > 1 and a.sync == "grad") else None
-    eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm)
+    if a.model == "mnist_cnn":
+        shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
+        eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm)
+        test_x, test_y = shard.test_x, shard.test_y
+    else:
+        from mpi_tensorflow_amd.models.generic import model_input_shape
+        from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+        from mpi_tensorflow_amd.utils.data import synthetic_images_torch
+
+        shape = model_input_shape(a.model)
+        rows = max(4 * a.batch_size, 8192 if a.model == "lenet5" else 4 * a.batch_size)
+        tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
+        ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
+                                        start=di.rank * rows)
+        eng = GenericEngine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm)
+        test_x, test_y = ex.numpy(), ey.numpy()
 
     def sync():
         if device.type == "cuda":
@@ -83,12 +101,21 @@ def main(argv=None) -> int:
     dt = D.allreduce_max_host(t1 - t0)
     err = float("nan")
     if not a.no_eval:
-        err = D.allreduce_sum_host(eng.evaluate(shard.test_x, shard.test_y)) / N
+        err = D.allreduce_sum_host(eng.evaluate(test_x, test_y)) / N
     images = N * a.batch_size * a.steps
     value = images / dt
+    if a.model == "mnist_cnn":
+        model_desc = "mnist_cnn (2-layer MNIST CNN of mpipy.py: conv5x5x32-pool-conv5x5x64-pool-fc512-dropout-fc10)"
+        image, data_desc = "28x28x1", "synthetic (MNIST-shaped 28x28x1, class-conditional; random-init weights)"
+    elif a.model == "lenet5":
+        model_desc = "lenet5 (conv5x5x6-pool-conv5x5x16-pool-fc120-fc84-fc10)"
+        image, data_desc = "32x32x3", "synthetic (CIFAR-shaped 32x32x3, class-conditional; random-init weights)"
+    else:
+        model_desc = "resnet18 (BasicBlock [2,2,2,2], BatchNorm, 10 classes)"
+        image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, class-conditional; random-init weights)"
     if di.rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if a.model == "mnist_cnn" else f"images/sec (whole node), {a.model}",
             "value": round(value, 1),
             "unit": "images/sec",
             "n_gpus": N,
@@ -99,15 +126,15 @@ def main(argv=None) -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": a.dtype,
-            "data": "synthetic (MNIST-shaped 28x28x1, class-conditional; random-init weights)",
+            "data": data_desc,
             "config": {
-                "model": "mnist_cnn (2-layer MNIST CNN of mpipy.py: conv5x5x32-pool-conv5x5x64-pool-fc512-dropout-fc10)",
+                "model": model_desc,
                 "global_batch": a.batch_size * N,
                 "per_gpu_batch": a.batch_size,
                 "seq_len": None,
-                "image": "28x28x1",
+                "image": image,
                 "parallelism": f"dp{N}",
-                "sync": "per-step gradient all-reduce (RCCL, 2 buckets, overlapped)" if N > 1 else "none (1 rank)",
+                "sync": "per-step gradient all-reduce (RCCL)" if N > 1 else "none (1 rank)",
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
                 "graph_steps": (a.graph_steps if not a.no_graph else 0),

@@ -12,6 +12,7 @@
 
 #include "idx_loader.h"
 #include "kernels/mnist.h"
+#include "kernels/mnist_bf16.h"
 #include "kernels/ops_generic.h"
 #include "mnist_executor.h"
 #include "rccl_comm.h"
@@ -54,6 +55,8 @@ PYBIND11_MODULE(_C, m) {
   k.def("part2_floats", &mnist::part2_floats);
   k.def("part1_floats", &mnist::part1_floats);
   k.def("fc1_part_floats", &mnist::fc1_part_floats);
+  k.def("part2_floats_bf16", &mnist16::part2_floats);
+  k.def("conv2_filter_groups_bf16", &mnist16::conv2_filter_groups);
   k.def("fc1_fwd_train", [](uintptr_t a2, uintptr_t w, int batch, uintptr_t part, uintptr_t s) {
     mnist::launch_fc1_fwd_train(P<const float>(a2), P<const float>(w), batch, P<float>(part), S(s));
     check_launch();
@@ -243,7 +246,9 @@ PYBIND11_MODULE(_C, m) {
                   RW(off_b2) RW(off_w1) RW(off_b1) RW(step) RW(lr) RW(correct) RW(a1) RW(idx1)
                       RW(a2) RW(idx2) RW(fc1_part) RW(hd) RW(dh) RW(dlog) RW(loss_rows) RW(dy2)
                           RW(da1m) RW(part2) RW(part1) RW(w2t) RW(keep_prob) RW(base_lr) RW(lr_decay)
-                              RW(l2) RW(momentum) RW(seed) RW(rank) RW(world);
+                              RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16)
+                                  RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
+                                      RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b);
 #undef RW
 
   py::class_<RcclComm>(m, "RcclComm")

@@ -18,6 +18,10 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 #define WAVE 64
 
+// row length (elements) of the channel-major zero-padded bf16 activation
+// images of the bf16 MNIST engine ([n][C][rows][MNIST16_T_LD])
+#define MNIST16_T_LD 24
+
 #define HIP_CHECK(expr)                                                              \
   do {                                                                               \
     hipError_t _e = (expr);                                                          \

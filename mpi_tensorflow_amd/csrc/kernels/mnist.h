@@ -7,6 +7,10 @@
 namespace mnist {
 void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
                       const float* w, const float* b, float* out, uint8_t* argmax, hipStream_t s);
+// bf16 engine: pooled conv1 output as zero-bordered bf16 images (see mnist_bf16.h)
+void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
+                           const float* w, const float* b, uint16_t* a1p, uint16_t* a1t,
+                           uint8_t* argmax, int ld_batch, hipStream_t s);
 // w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s);
@@ -18,7 +22,8 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           const int* labels, int n_local, const long long* step, int batch,
                           float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
                           float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
-                          float* lr_out, int* correct, hipStream_t s);
+                          float* lr_out, int* correct, hipStream_t s, uint16_t* dh16 = nullptr,
+                          uint16_t* dht16 = nullptr);
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
                          int M, float* logits, int* errors, hipStream_t s);
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,

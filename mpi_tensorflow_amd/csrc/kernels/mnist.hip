@@ -27,6 +27,7 @@
 #include "common.h"
 #include "gemm_core.h"
 #include "mnist.h"
+#include "mnist_shared.h"
 
 namespace mnist {
 
@@ -41,15 +42,6 @@ struct ConvGeo {
 };
 using Conv1 = ConvGeo<28, 28, 1, 32, 5, 2, 32>;
 
-constexpr int FC1_IN = 3136, FC1_OUT = 512, NCLS = 10;
-constexpr int FC1_SPLITS = 14;  // train fc1 split-K slabs (98 K tiles of 32 -> 7 each)
-
-__device__ __forceinline__ long long batch_offset_dev(const long long* step_ptr, int n_local,
-                                                      int batch) {
-  if (step_ptr == nullptr) return 0;
-  long long s = *step_ptr;
-  return (s * batch) % (long long)(n_local - batch);
-}
 
 // --------------------------------------------- conv + bias + relu + pool ----
 // GEMM view: M = pre-pool pixels ordered (n, py, px, quadrant) so that the 4
@@ -103,7 +95,11 @@ template <class G, int WM, int WN, int WK>
 __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
     const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
-    uint8_t* __restrict__ argmax) {
+    uint8_t* __restrict__ argmax, __bf16* __restrict__ out_p, __bf16* __restrict__ out_t,
+    int ld_batch) {
+  // out_p / out_t (bf16 engine, layouts in mnist_bf16.h): pooled output as
+  // the zero-bordered K-packed image [C/16][ld_batch][PH+4][PW+4][16] and as
+  // [n][PH+4][C][MNIST16_T_LD], instead of the fp32 NHWC `out`
   using CF = gemm::Cfg<WM, WN, WK, G::BK, true, true>;
   __shared__ float smem[CF::SMEM_FLOATS];
   const long long off = batch_offset_dev(step_ptr, n_local, batch);
@@ -133,7 +129,17 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
       }
     }
     if (pooled < P) {
-      out[pooled * G::COUT + co] = fmaxf(v + b, 0.f);
+      const float o = fmaxf(v + b, 0.f);
+      if (out_p) {
+        constexpr int PP = G::PH + 4, PQ = G::PW + 4;
+        const int px = pooled % G::PW, t = pooled / G::PW, py = t % G::PH, n = t / G::PH;
+        out_p[(((size_t)(co >> 4) * ld_batch + n) * PP + py + 2) * PQ * 16 + (px + 2) * 16 +
+              (co & 15)] = (__bf16)o;
+        if (out_t)
+          out_t[((size_t)(n * PP + py + 2) * G::COUT + co) * MNIST16_T_LD + px + 2] = (__bf16)o;
+      } else {
+        out[pooled * G::COUT + co] = o;
+      }
       if (argmax) argmax[pooled * G::COUT + co] = (uint8_t)q;
     }
   }
@@ -209,7 +215,8 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
     const long long* step_ptr, int batch, float keep_prob, uint32_t seed, uint32_t rank,
     float base_lr, float lr_decay, float* __restrict__ hd_out, float* __restrict__ dh_out,
     float* __restrict__ dlog_out, float* __restrict__ loss_rows, float* __restrict__ lr_out,
-    int* __restrict__ correct) {
+    int* __restrict__ correct, __bf16* __restrict__ dh16, __bf16* __restrict__ dht16) {
+  // dh16 / dht16 (bf16 engine): the K-packed MFMA operands of fc1 dX / dW1
   __shared__ float red[4][NCLS];
   __shared__ float dlog_s[NCLS];
   const int row = blockIdx.x;
@@ -289,6 +296,10 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
     d = (kp[u] && z[u] > 0.f) ? d * scale : 0.f;
     hd_out[row * FC1_OUT + j] = hd[u];
     dh_out[row * FC1_OUT + j] = d;
+    if (dh16) {  // K-packed layouts of mnist_bf16.h
+      dh16[((j >> 4) * batch + row) * 16 + (j & 15)] = (__bf16)d;
+      dht16[((row >> 4) * FC1_OUT + j) * 16 + (row & 15)] = (__bf16)d;
+    }
   }
 }
 
@@ -373,55 +384,6 @@ struct Fc1DxProb {
 constexpr int FC1BWD_BK = 64;
 constexpr int FC1BWD_DW_WM = 2, FC1BWD_DW_WN = 2;  // 64x64 tiles, 4 waves
 constexpr int FC1BWD_DX_WK = 4;                    // 32x32 tiles, K split over 4 waves
-constexpr int SMALL_BLOCKS = 8;
-
-__device__ void fc1_small_grads(int blk, const float* hd, const float* dh, const float* dlog,
-                                int batch, float* g_w4, float* g_b4, float* g_b3, float* smem) {
-  // block blk handles hidden units j in [64 blk, 64 blk + 64); 4 row groups
-  const int tid = threadIdx.x, jl = tid & 63, rg = tid >> 6;
-  const int j = blk * 64 + jl;
-  float acc[NCLS + 1];
-#pragma unroll
-  for (int c = 0; c <= NCLS; ++c) acc[c] = 0.f;
-  for (int n0 = rg; n0 < batch; n0 += 32) {  // 8 rows per round, loads issued together
-    float hv[8], dv[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int n = min(n0 + 4 * u, batch - 1);
-      hv[u] = hd[n * FC1_OUT + j];
-      dv[u] = dh[n * FC1_OUT + j];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int n = n0 + 4 * u;
-      if (n < batch) {
-#pragma unroll
-        for (int c = 0; c < NCLS; ++c) acc[c] += hv[u] * dlog[n * NCLS + c];
-        acc[NCLS] += dv[u];
-      }
-    }
-  }
-  float* s = smem;  // [4][11][64]
-#pragma unroll
-  for (int c = 0; c <= NCLS; ++c) s[(rg * (NCLS + 1) + c) * 64 + jl] = acc[c];
-  __syncthreads();
-  if (rg == 0) {
-#pragma unroll
-    for (int c = 0; c <= NCLS; ++c) {
-      const float v = s[c * 64 + jl] + s[((NCLS + 1) + c) * 64 + jl] +
-                      s[(2 * (NCLS + 1) + c) * 64 + jl] + s[(3 * (NCLS + 1) + c) * 64 + jl];
-      if (c < NCLS)
-        g_w4[j * NCLS + c] = v;
-      else
-        g_b3[j] = v;
-    }
-  }
-  if (blk == 0 && tid < NCLS) {
-    float v = 0.f;
-    for (int n = 0; n < batch; ++n) v += dlog[n * NCLS + tid];
-    g_b4[tid] = v;
-  }
-}
 
 // fc1 backward, one launch: blocks [0, n_dx) compute dX (+ the pool2/ReLU2
 // backward scatter into dY2, the critical path), then dW1 tiles, then the
@@ -976,7 +938,17 @@ void launch_conv1_fwd(const float* data, const long long* step, int n_local, int
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
   conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
       <<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(data, step, n_local, batch, w, b, out,
-                                                      argmax);
+                                                      argmax, nullptr, nullptr, 0);
+}
+
+void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
+                           const float* w, const float* b, uint16_t* a1p, uint16_t* a1t,
+                           uint8_t* argmax, int ld_batch, hipStream_t s) {
+  const int M = batch * 14 * 14 * 4;
+  const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
+  conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK><<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(
+      data, step, n_local, batch, w, b, nullptr, argmax, reinterpret_cast<__bf16*>(a1p),
+      reinterpret_cast<__bf16*>(a1t), ld_batch);
 }
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
@@ -1005,10 +977,13 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           const int* labels, int n_local, const long long* step, int batch,
                           float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
                           float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
-                          float* lr_out, int* correct, hipStream_t s) {
+                          float* lr_out, int* correct, hipStream_t s, uint16_t* dh16,
+                          uint16_t* dht16) {
   fc_head_train_kernel<<<batch, 256, 0, s>>>(part, b3, w4, b4, labels, n_local, step, batch,
                                              keep_prob, seed, rank, base_lr, lr_decay, hd, dh,
-                                             dlog, loss_rows, lr_out, correct);
+                                             dlog, loss_rows, lr_out, correct,
+                                             reinterpret_cast<__bf16*>(dh16),
+                                             reinterpret_cast<__bf16*>(dht16));
 }
 
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,

@@ -1,0 +1,500 @@
+// bf16 MFMA kernel set for the reference MNIST CNN on gfx950 (BASELINE config
+// 2).  Same graph and fusion boundaries as the fp32 set (mnist.hip; reference
+// /root/reference/mpipy.py:155-167, loss :54-58), but every GEMM-shaped op
+// runs on v_mfma_f32_32x32x16_bf16 (16x the fp32-MFMA rate) with fp32
+// accumulation, and activations travel in bf16 (layouts: mnist_bf16.h).
+//
+// Operand fetch: every wave owns a 32x32 output tile and streams its K range
+// as 16-byte fragments (8 bf16 per lane: lane l holds A[l&31][8(l>>5)+j] and
+// B[8(l>>5)+j][l&31]) straight from L2 into a D-deep register ring.  The
+// producers of each operand write it K-packed ([K/16][rows][16], mnist_bf16.h)
+// in exactly the form its consumer reads, so each fragment load is one
+// contiguous 1 KB wave access, and no kernel here needs LDS staging, bounds
+// checks or a transpose - only the split-K reductions touch LDS.  The filter
+// grad reads its shifted operand at 2-byte alignment, which runs at full
+// speed on gfx950 (scripts/microbench/unaligned_b128.hip).
+#include <stdexcept>
+
+#include "common.h"
+#include "mnist_bf16.h"
+#include "mnist_shared.h"
+
+namespace mnist16 {
+
+using bf = __bf16;
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+using mnist::FC1_IN;
+using mnist::FC1_OUT;
+using mnist::FC1_SPLITS;
+using mnist::NCLS;
+
+constexpr int TLD = MNIST16_T_LD;  // row length of the channel-major padded images
+
+__device__ __forceinline__ bfx8 ld8(const bf* p) {
+  return __builtin_bit_cast(bfx8, *reinterpret_cast<const uint4*>(p));
+}
+
+__device__ __forceinline__ f32x16 mma(bfx8 a, bfx8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sum8(bfx8 v) {
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s += (float)v[j];
+  return s;
+}
+
+// K loop over nks K-steps (nks % D == 0) with a D-deep register ring:
+// frag(ks, a, b) issues the two 16-byte fragment loads of K-step ks and
+// use(a, b) (optional) sees each fragment pair as it is consumed.  The
+// sched_barriers pin each refill ahead of the MFMA that frees its slot (the
+// scheduler would otherwise sink it next to its use); two accumulator chains
+// keep consecutive MFMAs independent.
+struct NoUse {
+  __device__ __forceinline__ void operator()(const bfx8&, const bfx8&) const {}
+};
+
+template <int D, class F, class U = NoUse>
+__device__ __forceinline__ void kloop(int nks, F&& frag, f32x16& c0, f32x16& c1, U use = U()) {
+  bfx8 ra[D], rb[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) frag(d, ra[d], rb[d]);
+#pragma unroll
+  for (int ks = 0; ks < nks; ks += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const bfx8 a = ra[d], b = rb[d];
+      if (ks + D < nks) frag(ks + D + d, ra[d], rb[d]);
+      __builtin_amdgcn_sched_barrier(0);
+      if (d & 1)
+        c1 = mma(a, b, c1);
+      else
+        c0 = mma(a, b, c0);
+      use(a, b);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// ---------------------------------------------------------- shadows ----
+// blocks [0, 392): one 64x64 tile of W1 (fp32 [3136][512], i0 + 64 rows, j0
+// + 64 cols) -> w1b [j/16][i][16] and, through LDS, w1t [i/16][j][16];
+// blocks [392, 442): 1024 conv2 weights each -> w2t / w2b.
+constexpr int SH_W1_BLOCKS = (FC1_IN / 64) * (FC1_OUT / 64), SH_W2_BLOCKS = 51200 / 1024;
+
+__device__ __forceinline__ void store16(bf* dst, const float* v) {  // 16 floats -> 32 B
+  bf t[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) t[e] = (bf)v[e];
+  const uint4* s4 = reinterpret_cast<const uint4*>(t);
+  reinterpret_cast<uint4*>(dst)[0] = s4[0];
+  reinterpret_cast<uint4*>(dst)[1] = s4[1];
+}
+
+__global__ __launch_bounds__(256) void shadow_kernel(const float* __restrict__ w1,
+                                                     const float* __restrict__ w2,
+                                                     bf* __restrict__ w1b, bf* __restrict__ w1t,
+                                                     bf* __restrict__ w2t, bf* __restrict__ w2b) {
+  __shared__ float tile[64][65];
+  const int tid = threadIdx.x;
+  if ((int)blockIdx.x < SH_W1_BLOCKS) {
+    const int i0 = (blockIdx.x % (FC1_IN / 64)) * 64, j0 = (blockIdx.x / (FC1_IN / 64)) * 64;
+    {  // thread = (row i, 16-col chunk): 4 float4 loads, one 32 B store into w1b
+      const int row = tid >> 2, ck = tid & 3;
+      float v[16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 f = *reinterpret_cast<const float4*>(w1 + (size_t)(i0 + row) * FC1_OUT + j0 +
+                                                           16 * ck + 4 * u);
+        v[4 * u] = f.x;
+        v[4 * u + 1] = f.y;
+        v[4 * u + 2] = f.z;
+        v[4 * u + 3] = f.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tile[row][16 * ck + e] = v[e];
+      store16(w1b + ((size_t)((j0 >> 4) + ck) * FC1_IN + i0 + row) * 16, v);
+    }
+    __syncthreads();
+    {  // thread = (col j, 16-row chunk) -> w1t
+      const int col = tid >> 2, ck = tid & 3;
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = tile[16 * ck + e][col];
+      store16(w1t + ((size_t)((i0 >> 4) + ck) * FC1_OUT + j0 + col) * 16, v);
+    }
+    return;
+  }
+  const int base = ((int)blockIdx.x - SH_W1_BLOCKS) * 1024;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int idx = base + tid + 256 * e;  // HWIO: (t * 32 + ci) * 64 + co
+    const bf v = (bf)w2[idx];
+    const int t = idx >> 11, ci = (idx >> 6) & 31, co = idx & 63;
+    w2t[((t * 2 + (ci >> 4)) * 64 + co) * 16 + (ci & 15)] = v;
+    w2b[((t * 4 + (co >> 4)) * 32 + ci) * 16 + (co & 15)] = v;
+  }
+}
+
+// ------------------------------------------------------------ conv2 fwd ----
+// M = pre-pool pixels of the whole batch in (n, py, px, quadrant) order (the 4
+// pixels of a pooling window = 4 accumulator registers of one lane, see
+// mnist.hip), N = 64 output channels, K = 25 taps x 2 channel halves.  One
+// 32x32 tile per wave, 4 waves per block, no LDS.
+constexpr int IMG = 18 * 18 * 16;  // one padded 16-channel image plane
+
+__global__ __launch_bounds__(256) void conv2_fwd_kernel(const bf* __restrict__ a1p, int batch,
+                                                        const bf* __restrict__ w2t,
+                                                        const float* __restrict__ b2,
+                                                        bf* __restrict__ a2p, bf* __restrict__ a2t,
+                                                        uint8_t* __restrict__ idx2) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mtiles = batch * 49 / 8;
+  const int gw = xcd_remap(blockIdx.x, gridDim.x) * 4 + (threadIdx.x >> 6);
+  if (gw >= 2 * mtiles) return;
+  const int mt = gw >> 1, nt = gw & 1;
+  const int m = mt * 32 + r, q = m & 3, win = m >> 2;
+  const int n = win / 49, pp = win % 49, py = pp / 7, px = pp % 7;
+  const int y = 2 * py + (q >> 1), x = 2 * px + (q & 1);
+  const bf* ap = a1p + (size_t)n * IMG + (y * 18 + x) * 16 + 8 * h;
+  const size_t splane = (size_t)batch * IMG;
+  const bf* bp = w2t + (nt * 32 + r) * 16 + 8 * h;
+  f32x16 c0 = zero16(), c1 = zero16();
+  kloop<5>(
+      50,
+      [&](int ks, bfx8& a, bfx8& b) {
+        const int t = ks >> 1, s = ks & 1, kh = t / 5, kw = t % 5;
+        a = ld8(ap + s * splane + (kh * 18 + kw) * 16);
+        b = ld8(bp + (t * 2 + s) * 1024);
+      },
+      c0, c1);
+  const int co = nt * 32 + r;
+  const float bias = b2[co];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float v = c0[4 * g] + c1[4 * g];
+    int qq = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const float u = c0[4 * g + j] + c1[4 * g + j];
+      if (u > v) {  // strict: first max wins (TF MaxPool order)
+        v = u;
+        qq = j;
+      }
+    }
+    const int w2_ = mt * 8 + 2 * g + h;  // pooling window of registers 4g..4g+3
+    const int n2 = w2_ / 49, p2 = w2_ % 49;
+    const int i = p2 * 64 + co;
+    const bf out = (bf)fmaxf(v + bias, 0.f);
+    a2p[((size_t)(i >> 4) * batch + n2) * 16 + (i & 15)] = out;
+    if (idx2) idx2[(size_t)n2 * FC1_IN + i] = (uint8_t)qq;
+    if (a2t) a2t[((size_t)(n2 >> 4) * FC1_IN + i) * 16 + (n2 & 15)] = out;
+  }
+}
+
+// -------------------------------------------------------------- fc1 fwd ----
+// M = rows, N = 512 hidden units, K = 3136.  Train: split-K slabs (z) of
+// 14 K-steps; eval: the full K with bias + ReLU (+dropout) epilogue.  a2p
+// holds `ld` rows per K-step.
+template <bool EVAL, int D>
+__global__ __launch_bounds__(256) void fc1_fwd_kernel(const bf* __restrict__ a2p, int ld,
+                                                      const bf* __restrict__ w1t,
+                                                      const float* __restrict__ bias,
+                                                      float* __restrict__ out, int M, int nz,
+                                                      uint32_t key, float keep_prob) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int mtiles = (M + 31) / 32;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gw >= mtiles * (FC1_OUT / 32) * nz) return;
+  const int mt = gw % mtiles, rest = gw / mtiles, nt = rest % (FC1_OUT / 32), z = rest / (FC1_OUT / 32);
+  const int nks = FC1_IN / 16 / nz, k0 = z * nks;
+  const int row = min(mt * 32 + r, M - 1);
+  const bf* ap = a2p + ((size_t)k0 * ld + row) * 16 + 8 * h;
+  const bf* bp = w1t + ((size_t)k0 * FC1_OUT + nt * 32 + r) * 16 + 8 * h;
+  f32x16 c0 = zero16(), c1 = zero16();
+  kloop<D>(
+      nks,
+      [&](int ks, bfx8& a, bfx8& b) {
+        a = ld8(ap + (size_t)ks * ld * 16);
+        b = ld8(bp + ks * FC1_OUT * 16);
+      },
+      c0, c1);
+  const int n = nt * 32 + r;
+  const float bn = EVAL ? bias[n] : 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int m = mt * 32 + mfma32_row(i, lane);
+    if (m >= M) continue;
+    const float acc = c0[i] + c1[i];
+    if (EVAL) {
+      float hv = fmaxf(acc + bn, 0.f);
+      if (keep_prob < 1.f)
+        hv = dropout_keep(key, (uint32_t)(m * FC1_OUT + n), keep_prob) ? hv / keep_prob : 0.f;
+      out[(size_t)m * FC1_OUT + n] = hv;
+    } else {
+      out[((size_t)z * M + m) * FC1_OUT + n] = acc;
+    }
+  }
+}
+
+// -------------------------------------------------------------- fc1 bwd ----
+// One launch, block roles: [0, n_dx) dX = dh W1^T (M = rows, N = 3136, K =
+// 512) with the pool2 / ReLU2 backward scatter into dy2p and dy2t; then dW1 =
+// a2^T dh (M = 3136, N = 512, K = rows) tiles; then the small fc2 / bias grads.
+__global__ __launch_bounds__(256) void fc1_bwd_kernel(
+    const bf* __restrict__ a2p, const bf* __restrict__ a2t, const uint8_t* __restrict__ idx2,
+    const bf* __restrict__ dh16, const bf* __restrict__ dht16, const float* __restrict__ hd,
+    const float* __restrict__ dh, const float* __restrict__ dlog, const bf* __restrict__ w1b,
+    int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
+    float* __restrict__ g_b4, bf* __restrict__ dy2p, bf* __restrict__ dy2t) {
+  __shared__ float smem[4 * (NCLS + 1) * 64];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int bm = batch / 32;
+  const int n_dx = (bm * (FC1_IN / 32) + 3) / 4;
+  constexpr int n_dw = (FC1_IN / 32) * (FC1_OUT / 32) / 4;
+  int bid = blockIdx.x;
+  f32x16 c0 = zero16(), c1 = zero16();
+  if (bid < n_dx) {
+    const int gw = bid * 4 + wave;
+    if (gw >= bm * (FC1_IN / 32)) return;
+    const int mt = gw % bm, nt = gw / bm;
+    const bf* ap = dh16 + (size_t)(mt * 32 + r) * 16 + 8 * h;
+    const bf* bp = w1b + (size_t)(nt * 32 + r) * 16 + 8 * h;
+    kloop<8>(
+        FC1_OUT / 16,
+        [&](int ks, bfx8& a, bfx8& b) {
+          a = ld8(ap + (size_t)ks * batch * 16);
+          b = ld8(bp + (size_t)ks * FC1_IN * 16);
+        },
+        c0, c1);
+    const int i = nt * 32 + r;  // (py, px, co) flat
+    const int co = i & 63, pp = i >> 6, py = pp / 7, px = pp % 7;
+    const size_t cplane = (size_t)(co >> 4) * batch * IMG + (co & 15);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int n = mt * 32 + mfma32_row(k, lane);
+      float g = c0[k] + c1[k];
+      const float a = (float)a2p[((size_t)(i >> 4) * batch + n) * 16 + (i & 15)];
+      if (!(a > 0.f)) g = 0.f;  // ReLU2 inactive at the argmax
+      const int q = idx2[(size_t)n * FC1_IN + i];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
+        const bf v = (bf)(d == q ? g : 0.f);
+        dy2p[cplane + (size_t)n * IMG + ((y + 2) * 18 + x + 2) * 16] = v;
+        dy2t[((size_t)(n * 14 + y) * 64 + co) * 16 + x] = v;
+      }
+    }
+    return;
+  }
+  bid -= n_dx;
+  if (bid < n_dw) {
+    const int gw = bid * 4 + wave;
+    const int mi = gw % (FC1_IN / 32), nj = gw / (FC1_IN / 32);
+    const bf* ap = a2t + (size_t)(mi * 32 + r) * 16 + 8 * h;
+    const bf* bp = dht16 + (size_t)(nj * 32 + r) * 16 + 8 * h;
+    kloop<2>(
+        batch / 16,
+        [&](int ks, bfx8& a, bfx8& b) {
+          a = ld8(ap + (size_t)ks * FC1_IN * 16);
+          b = ld8(bp + (size_t)ks * FC1_OUT * 16);
+        },
+        c0, c1);
+    const int n = nj * 32 + r;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int m = mi * 32 + mfma32_row(k, lane);
+      g_w3[(size_t)m * FC1_OUT + n] = c0[k] + c1[k];
+    }
+    return;
+  }
+  bid -= n_dw;
+  mnist::fc1_small_grads(bid, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
+}
+
+// ------------------------------------------------------ conv2 bwd-data ----
+// dA1[n,y,x,ci] = [a1 > 0] sum_{kh,kw,co} dY2[n, y+2-kh, x+2-kw, co] W2[kh,kw,ci,co]:
+// M = pixels (n, y, x), N = 32 input channels, K = 25 taps x 4 channel
+// chunks.  Block = 2 M tiles x 2 K halves (chunks 0-1 / 2-3), summed in LDS.
+__global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restrict__ dy2p,
+                                                             const bf* __restrict__ w2b,
+                                                             const bf* __restrict__ a1p, int batch,
+                                                             float* __restrict__ da1m) {
+  __shared__ float red[2][16][64];
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int mtiles = batch * 196 / 32;
+  const int mt_raw = blockIdx.x * 2 + (wave & 1), kk = wave >> 1;
+  const int mt = min(mt_raw, mtiles - 1);
+  const int m = mt * 32 + r, n = m / 196, p = m % 196, y = p / 14, x = p % 14;
+  const size_t cplane = (size_t)batch * IMG;
+  const bf* ap = dy2p + 2 * kk * cplane + (size_t)n * IMG + ((y + 4) * 18 + x + 4) * 16 + 8 * h;
+  const bf* bp = w2b + (2 * kk * 32 + r) * 16 + 8 * h;
+  f32x16 c0 = zero16(), c1 = zero16();
+  kloop<5>(
+      50,
+      [&](int ks, bfx8& a, bfx8& b) {
+        const int t = ks >> 1, s = ks & 1, kh = t / 5, kw = t % 5;
+        a = ld8(ap + s * cplane - (kh * 18 + kw) * 16);
+        b = ld8(bp + (t * 4 + s) * 512);
+      },
+      c0, c1);
+  if (kk == 1) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[wave & 1][k][lane] = c0[k] + c1[k];
+  }
+  __syncthreads();
+  if (kk == 1 || mt_raw >= mtiles) return;
+  const bf* a1c = a1p + (size_t)(r >> 4) * cplane + (r & 15);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int mm = mt * 32 + mfma32_row(k, lane);
+    const int nn = mm / 196, pq = mm % 196, yy = pq / 14, xx = pq % 14;
+    const float g = c0[k] + c1[k] + red[wave & 1][k][lane];
+    const float a = (float)a1c[(size_t)nn * IMG + ((yy + 2) * 18 + xx + 2) * 16];
+    da1m[(size_t)mm * 32 + r] = a > 0.f ? g : 0.f;
+  }
+}
+
+// ---------------------------------------------------- conv2 bwd-filter ----
+// dW2[t][ci][co] = sum_{n,y,x} a1[n, y+kh-2, x+kw-2, ci] dY2[n, y, x, co]:
+// M = 32 input channels, N = 64 output channels (2 tiles), K = pixels, one
+// K-step = one image row (x = 0..15; dy2t columns 14/15 are zero).  Block =
+// (tap, group of 8 images); 8 waves = 2 (co half) x 4 (image pairs), the
+// image pairs summed through LDS into one slab per group.  The centre tap
+// (which visits every pixel once) also sums dY2 per channel (db2).
+constexpr int C2F_IMG = 8;
+
+__global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(const bf* __restrict__ a1t,
+                                                               const bf* __restrict__ dy2t,
+                                                               int batch, float* __restrict__ part2,
+                                                               float* __restrict__ part_db2) {
+  __shared__ float red[3][2][16][64];
+  const int ngroups = (batch + C2F_IMG - 1) / C2F_IMG;
+  const int bid = blockIdx.x;
+  int t, g;
+  if (ngroups % 8 == 0) {  // all taps of an image group on one XCD (shared L2)
+    const int xx = bid & 7, idx = bid >> 3;
+    t = idx % 25;
+    g = xx + 8 * (idx / 25);
+  } else {
+    t = bid % 25;
+    g = bid / 25;
+  }
+  const int kh = t / 5, kw = t % 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int nt = wave & 1, ip = wave >> 1;
+  const int co = nt * 32 + r;
+  f32x16 c0 = zero16(), c1 = zero16();
+  float dbs = 0.f;
+#pragma unroll
+  for (int im = 0; im < 2; ++im) {
+    const int n = g * C2F_IMG + 2 * ip + im;
+    if (n < batch) {
+      const bf* ap = a1t + ((size_t)(n * 18 + kh) * 32 + r) * TLD + kw + 8 * h;
+      const bf* bp = dy2t + ((size_t)n * 14 * 64 + co) * 16 + 8 * h;
+      kloop<7>(
+          14,
+          [&](int y, bfx8& a, bfx8& b) {
+            a = ld8(ap + y * 32 * TLD);
+            b = ld8(bp + y * 64 * 16);
+          },
+          c0, c1, [&](const bfx8&, const bfx8& b) {
+            if (t == 12) dbs += sum8(b);
+          });
+    }
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc[k] = c0[k] + c1[k];
+  if (ip > 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[ip - 1][nt][k][lane] = acc[k];
+  }
+  __syncthreads();
+  if (ip == 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float s = acc[k] + red[0][nt][k][lane] + red[1][nt][k][lane] + red[2][nt][k][lane];
+      const int ci = mfma32_row(k, lane);
+      part2[((size_t)g * 800 + t * 32 + ci) * 64 + co] = s;
+    }
+  }
+  if (t == 12) {
+    dbs += __shfl_xor(dbs, 32, 64);
+    if (h == 0) part_db2[(g * 4 + ip) * 64 + co] = dbs;
+  }
+}
+
+}  // namespace mnist16
+
+// ======================================================================
+// host launchers
+// ======================================================================
+namespace mnist16 {
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+static inline const bf* C16(const uint16_t* p) { return reinterpret_cast<const bf*>(p); }
+static inline bf* M16(uint16_t* p) { return reinterpret_cast<bf*>(p); }
+
+void launch_shadows(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w1t,
+                    uint16_t* w2t, uint16_t* w2b, hipStream_t s) {
+  shadow_kernel<<<SH_W1_BLOCKS + SH_W2_BLOCKS, 256, 0, s>>>(w1, w2, M16(w1b), M16(w1t), M16(w2t),
+                                                            M16(w2b));
+}
+
+void launch_conv2_fwd(const uint16_t* a1p, int batch, const uint16_t* w2t, const float* b2,
+                      uint16_t* a2p, uint16_t* a2t, uint8_t* idx2, hipStream_t s) {
+  if (batch % 8 != 0) throw std::runtime_error("mnist16 conv2_fwd: batch % 8 != 0");
+  if (a2t && batch % 16 != 0) throw std::runtime_error("mnist16 conv2_fwd: a2t needs batch % 16");
+  const int waves = 2 * (batch * 49 / 8);
+  conv2_fwd_kernel<<<cdiv(waves, 4), 256, 0, s>>>(C16(a1p), batch, C16(w2t), b2, M16(a2p),
+                                                  a2t ? M16(a2t) : nullptr, idx2);
+}
+
+void launch_fc1_fwd_train(const uint16_t* a2p, const uint16_t* w1t, int batch, float* part,
+                          hipStream_t s) {
+  const int waves = cdiv(batch, 32) * (FC1_OUT / 32) * FC1_SPLITS;
+  fc1_fwd_kernel<false, 7><<<cdiv(waves, 4), 256, 0, s>>>(C16(a2p), batch, C16(w1t), nullptr,
+                                                          part, batch, FC1_SPLITS, 0u, 1.f);
+}
+
+void launch_fc1_fwd_eval(const uint16_t* a2p, int ld, const uint16_t* w1t, const float* b, int M,
+                         float* h, uint32_t key, float keep_prob, hipStream_t s) {
+  const int waves = cdiv(M, 32) * (FC1_OUT / 32);
+  fc1_fwd_kernel<true, 4><<<cdiv(waves, 4), 256, 0, s>>>(C16(a2p), ld, C16(w1t), b, h, M, 1, key,
+                                                         keep_prob);
+}
+
+void launch_fc1_bwd(const uint16_t* a2p, const uint16_t* a2t, const uint8_t* idx2,
+                    const uint16_t* dh16, const uint16_t* dht16, const float* hd, const float* dh,
+                    const float* dlog, const uint16_t* w1b, int batch, float* g_w3, float* g_b3,
+                    float* g_w4, float* g_b4, uint16_t* dy2p, uint16_t* dy2t, hipStream_t s) {
+  if (batch % 32 != 0) throw std::runtime_error("mnist16 fc1_bwd: batch % 32 != 0");
+  const int n_dx = cdiv(batch / 32 * (FC1_IN / 32), 4);
+  const int n_dw = (FC1_IN / 32) * (FC1_OUT / 32) / 4;
+  fc1_bwd_kernel<<<n_dx + n_dw + mnist::SMALL_BLOCKS, 256, 0, s>>>(
+      C16(a2p), C16(a2t), idx2, C16(dh16), C16(dht16), hd, dh, dlog, C16(w1b), batch, g_w3, g_b3,
+      g_w4, g_b4, M16(dy2p), M16(dy2t));
+}
+
+void launch_conv2_bwd_data(const uint16_t* dy2p, const uint16_t* w2b, const uint16_t* a1p,
+                           int batch, float* da1m, hipStream_t s) {
+  if (batch % 8 != 0) throw std::runtime_error("mnist16 conv2_bwd_data: batch % 8 != 0");
+  const int mtiles = batch * 196 / 32;
+  conv2_bwd_data_kernel<<<cdiv(mtiles, 2), 256, 0, s>>>(C16(dy2p), C16(w2b), C16(a1p), batch,
+                                                        da1m);
+}
+
+int conv2_filter_groups(int batch) { return cdiv(batch, C2F_IMG); }
+
+void launch_conv2_bwd_filter(const uint16_t* a1t, const uint16_t* dy2t, int batch, float* part2,
+                             hipStream_t s) {
+  const int G = conv2_filter_groups(batch);
+  conv2_bwd_filter_kernel<<<25 * G, 512, 0, s>>>(C16(a1t), C16(dy2t), batch, part2,
+                                                 part2 + (size_t)G * 51200);
+}
+
+size_t part2_floats(int batch) { return (size_t)conv2_filter_groups(batch) * (51200 + 256); }
+
+}  // namespace mnist16

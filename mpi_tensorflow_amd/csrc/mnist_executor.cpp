@@ -5,6 +5,7 @@
 
 #include "kernels/common.h"
 #include "kernels/mnist.h"
+#include "kernels/mnist_bf16.h"
 
 template <class T>
 static inline T* P(uintptr_t v) {
@@ -35,6 +36,7 @@ MnistExecutor::~MnistExecutor() {
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
+  if (p_.bf16) return enqueue_fwd_bwd_bf16(s);
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -65,6 +67,50 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
                                  P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                  P<float>(p.part1), s);
   mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
+                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
+                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+}
+
+// bf16 step: same kernel boundaries; the first launch re-derives the bf16
+// weight shadows from the fp32 master weights, conv1 (K = 25, tiny) stays on
+// fp32 MFMA and writes bf16 images, the conv1 filter grad / fc2 head / slab
+// reductions / SGD stay fp32.
+void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
+  const MnistPtrs& p = p_;
+  float* W = P<float>(p.params);
+  float* G = P<float>(p.grads);
+  const long long* step = P<const long long>(p.step);
+  const int B = p.batch;
+  using U16 = uint16_t;
+  mnist16::launch_shadows(W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
+                          P<U16>(p.w2tb), P<U16>(p.w2b), s);
+  mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
+                               W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1), B,
+                               s);
+  mnist16::launch_conv2_fwd(P<const U16>(p.a1p), B, P<const U16>(p.w2tb), W + p.off_b2,
+                            P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2), s);
+  mnist16::launch_fc1_fwd_train(P<const U16>(p.a2h), P<const U16>(p.w1t), B, P<float>(p.fc1_part),
+                                s);
+  mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
+                              W + p.off_b4, P<const int>(p.train_y), p.n_local, step, B,
+                              p.keep_prob, p.seed, p.rank, p.base_lr, p.lr_decay, P<float>(p.hd),
+                              P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
+                              P<float>(p.lr), P<int>(p.correct), s, P<U16>(p.dh16),
+                              P<U16>(p.dht16));
+  mnist16::launch_fc1_bwd(P<const U16>(p.a2h), P<const U16>(p.a2t), P<const uint8_t>(p.idx2),
+                          P<const U16>(p.dh16), P<const U16>(p.dht16), P<const float>(p.hd),
+                          P<const float>(p.dh), P<const float>(p.dlog), P<const U16>(p.w1b), B,
+                          G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<U16>(p.dy2p),
+                          P<U16>(p.dy2t), s);
+  HIP_CHECK(hipEventRecord(ev_dw_, s));
+  mnist16::launch_conv2_bwd_data(P<const U16>(p.dy2p), P<const U16>(p.w2b), P<const U16>(p.a1p), B,
+                                 P<float>(p.da1m), s);
+  mnist16::launch_conv2_bwd_filter(P<const U16>(p.a1t), P<const U16>(p.dy2t), B,
+                                   P<float>(p.part2), s);
+  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
+                                 P<const float>(p.da1m), P<const uint8_t>(p.idx1),
+                                 P<float>(p.part1), s);
+  mnist::launch_grad_finalize(P<const float>(p.part2), mnist16::conv2_filter_groups(B),
                               P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
                               G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
 }
@@ -104,6 +150,21 @@ void MnistExecutor::eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int
                                uintptr_t errors, float keep_prob, uint32_t drop_key,
                                hipStream_t s) {
   const float* W = P<const float>(p.params);
+  if (p.bf16) {
+    using U16 = uint16_t;
+    const int Mp = (M + 7) / 8 * 8;  // conv2 tiles cover whole groups of 8 images
+    mnist16::launch_shadows(W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
+                            P<U16>(p.w2tb), P<U16>(p.w2b), s);
+    mnist::launch_conv1_fwd_bf16(P<const float>(x), nullptr, 0, M, W + p.off_w1, W + p.off_b1,
+                                 P<U16>(ws_a1), nullptr, nullptr, Mp, s);
+    mnist16::launch_conv2_fwd(P<const U16>(ws_a1), Mp, P<const U16>(p.w2tb), W + p.off_b2,
+                              P<U16>(ws_a2), nullptr, nullptr, s);
+    mnist16::launch_fc1_fwd_eval(P<const U16>(ws_a2), Mp, P<const U16>(p.w1t), W + p.off_b3, M,
+                                 P<float>(ws_h), drop_key, keep_prob, s);
+    mnist::launch_fc_head_eval(P<const float>(ws_h), W + p.off_w4, W + p.off_b4, P<const int>(y),
+                               M, P<float>(logits), P<int>(errors), s);
+    return;
+  }
   mnist::launch_conv1_fwd(P<const float>(x), nullptr, 0, M, W + p.off_w1, W + p.off_b1,
                           P<float>(ws_a1), nullptr, s);
   mnist::launch_conv2_fwd(P<const float>(ws_a1), M, W + p.off_w2, W + p.off_b2, P<float>(ws_a2),

@@ -37,6 +37,11 @@ struct MnistPtrs {
   // activations / workspaces
   uintptr_t a1 = 0, idx1 = 0, a2 = 0, idx2 = 0, fc1_part = 0, hd = 0, dh = 0, dlog = 0,
             loss_rows = 0, dy2 = 0, da1m = 0, part2 = 0, part1 = 0, w2t = 0;
+  // bf16 engine (bf16 != 0): bf16 activation images and weight shadows
+  // (layouts: kernels/mnist_bf16.h); a1 / a2 / dy2 / w2t above are unused
+  int bf16 = 0;
+  uintptr_t a1p = 0, a1t = 0, a2h = 0, a2t = 0, dy2p = 0, dy2t = 0, dh16 = 0, dht16 = 0,
+            w1b = 0, w1t = 0, w2tb = 0, w2b = 0;
   // hyper-parameters
   float keep_prob = 0.5f, base_lr = 0.01f, lr_decay = 0.95f, l2 = 5e-4f, momentum = 0.9f;
   uint32_t seed = 1, rank = 0;
@@ -58,7 +63,9 @@ class MnistExecutor {
 
   // Evaluation of M rows starting at x (NHWC [M,28,28,1]): writes logits
   // [M,10] when logits != 0 and adds the error count to *errors.  ws_* are
-  // caller-provided work buffers sized for `chunk` rows.
+  // caller-provided work buffers sized for `chunk` rows (bf16 engine: ws_a1
+  // = zero-bordered bf16 a1p image of round_up(chunk, 8) rows, ws_a2 = bf16
+  // a2 of as many rows).
   static void eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int M, uintptr_t ws_a1,
                          uintptr_t ws_a2, uintptr_t ws_h, uintptr_t logits, uintptr_t errors,
                          float keep_prob, uint32_t drop_key, hipStream_t s);
@@ -67,6 +74,7 @@ class MnistExecutor {
 
  private:
   void enqueue_fwd_bwd(hipStream_t s);
+  void enqueue_fwd_bwd_bf16(hipStream_t s);
   MnistPtrs p_;
   hipEvent_t ev_head_ = nullptr, ev_dx_ = nullptr, ev_dw_ = nullptr, ev_filt_ = nullptr,
              ev_fin_ = nullptr, ev_done_ = nullptr;

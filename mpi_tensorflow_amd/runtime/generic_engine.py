@@ -37,6 +37,8 @@ class GenericEngine:
                  device: torch.device, rank: int = 0, world: int = 1,
                  comm: Optional[DeviceComm] = None):
         self.cfg, self.device, self.rank, self.world, self.comm = cfg, device, rank, world, comm
+        if cfg.dtype != "fp32":
+            raise NotImplementedError(f"dtype {cfg.dtype} is not implemented for {cfg.model} yet")
         self.model = make_model(cfg.model)
         self.layout = self.model.layout
         self.B = cfg.batch_size

@@ -147,7 +147,9 @@ class TorchMnistEngine(MnistEngineBase):
 
 
 class NativeMnistEngine(MnistEngineBase):
-    """fused HIP kernels + C++ executor + hipGraph replay (MI355X)."""
+    """fused HIP kernels + C++ executor + hipGraph replay (MI355X); fp32
+    (v_mfma_f32_32x32x2_f32) or bf16 (v_mfma_f32_32x32x16_bf16, fp32 master
+    weights / grads / momentum) per cfg.dtype."""
 
     kind = "native"
 
@@ -183,6 +185,23 @@ class NativeMnistEngine(MnistEngineBase):
             part2=torch.empty(k.part2_floats(B), **f32), part1=torch.empty(k.part1_floats(B), **f32),
             w2t=torch.empty(25 * 64 * 32, **f32),
         )
+        self.bf16 = cfg.dtype == "bf16"
+        if self.bf16:
+            # bf16 activation images (zero borders are never written) and
+            # weight shadows; layouts in csrc/kernels/mnist_bf16.h
+            b16 = dict(dtype=torch.bfloat16, device=dev)
+            self.bufs.update(
+                a1p=torch.zeros(B * 18 * 18 * 32, **b16), a1t=torch.zeros(B * 32 * 18 * 24, **b16),
+                a2h=torch.zeros(B * M.FC1_IN, **b16), a2t=torch.zeros(M.FC1_IN * B, **b16),
+                dy2p=torch.zeros(B * 18 * 18 * 64, **b16), dy2t=torch.zeros(B * 64 * 14 * 16, **b16),
+                dh16=torch.zeros(B * M.FC1_OUT, **b16), dht16=torch.zeros(M.FC1_OUT * B, **b16),
+                w1b=torch.zeros(M.FC1_IN * M.FC1_OUT, **b16),
+                w1t=torch.zeros(M.FC1_OUT * M.FC1_IN, **b16),
+                w2tb=torch.zeros(25 * 64 * 32, **b16), w2b=torch.zeros(25 * 32 * 64, **b16),
+                part2=torch.empty(k.part2_floats_bf16(B), **f32),
+            )
+            for name in ("a1", "a2", "dy2", "w2t"):  # fp32-only buffers
+                self.bufs[name] = torch.empty(0, **f32)
         p = C_.MnistPtrs()
         p.train_x, p.train_y = ptr(self.train_x), ptr(self.train_y)
         p.n_local, p.batch = self.n_local, B
@@ -201,6 +220,7 @@ class NativeMnistEngine(MnistEngineBase):
         p.keep_prob, p.base_lr, p.lr_decay = cfg.dropout_keep, cfg.base_lr, cfg.lr_decay
         p.l2, p.momentum = cfg.l2, cfg.momentum
         p.seed, p.rank, p.world = cfg.seed, self.drop_rank, world
+        p.bf16 = 1 if self.bf16 else 0
         self.ptrs = p
         self.exe = C_.MnistExecutor(p)
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
@@ -287,9 +307,16 @@ class NativeMnistEngine(MnistEngineBase):
         chunk = min(chunk, max(n, 1))
         if self._eval_ws is None or self._eval_ws[0] < chunk:
             f32 = dict(dtype=torch.float32, device=dev)
-            self._eval_ws = (chunk, torch.empty(chunk * 14 * 14 * 32, **f32),
-                             torch.empty(chunk * M.FC1_IN, **f32),
-                             torch.empty(chunk * M.FC1_OUT, **f32))
+            if self.bf16:
+                cp = (chunk + 7) // 8 * 8
+                b16 = dict(dtype=torch.bfloat16, device=dev)
+                self._eval_ws = (chunk, torch.zeros(cp * 18 * 18 * 32, **b16),
+                                 torch.zeros(cp * M.FC1_IN, **b16),
+                                 torch.empty(chunk * M.FC1_OUT, **f32))
+            else:
+                self._eval_ws = (chunk, torch.empty(chunk * 14 * 14 * 32, **f32),
+                                 torch.empty(chunk * M.FC1_IN, **f32),
+                                 torch.empty(chunk * M.FC1_OUT, **f32))
         _, a1, a2, h = self._eval_ws
         errors = torch.zeros(1, dtype=torch.int32, device=dev)
         logits = torch.empty(n, 10, dtype=torch.float32, device=dev) if return_logits else None
@@ -311,6 +338,8 @@ def make_engine(cfg: C.TrainConfig, train_x, train_y, device: torch.device, rank
     backend = backend or cfg.backend
     if backend == "auto":
         backend = "native" if device.type == "cuda" else "torch"
+    if cfg.dtype != "fp32" and backend != "native":
+        raise NotImplementedError(f"dtype {cfg.dtype} needs the native (GPU) MNIST engine")
     if backend == "native":
         return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm)
     return TorchMnistEngine(cfg, train_x, train_y, device, rank, world, comm)

@@ -95,7 +95,7 @@ class Trainer:
             else:  # 224x224x3: generated with torch (numpy path is too heavy)
                 rows, trows = 512, 256
                 tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=self.rank * rows)
-                sx, sy = synthetic_images_torch(trows, shape, seed=cfg.seed + 1,
+                sx, sy = synthetic_images_torch(trows, shape, seed=cfg.seed, split="test",
                                                 start=self.rank * trows)
                 self.shard = Shard(tx.numpy(), ty.numpy(), sx.numpy(), sy.numpy(),
                                    sx.numpy()[:0], sy.numpy()[:0], True,

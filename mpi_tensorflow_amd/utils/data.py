@@ -256,11 +256,13 @@ def synthetic_image_shard(rank: int, world: int, rows_per_rank: int, test_per_ra
 
 
 def synthetic_images_torch(n: int, shape: Tuple[int, int, int], classes: int = 10,
-                           seed: int = C.SEED, start: int = 0, device="cpu"):
+                           seed: int = C.SEED, start: int = 0, device="cpu", split: str = "train"):
     """Large-image synthetic data (ResNet-18 at 224x224x3) generated with torch
     on the target device: class prototypes (a coarse random field upsampled
     16x) + per-image noise, values in [-0.5, 0.5], NHWC float32, int64 labels.
-    Deterministic in (seed, start); rows [start, start+n)."""
+    Deterministic in (seed, split, start); rows [start, start+n).  Train and
+    test splits share the class prototypes (same seed) and differ in labels
+    and noise."""
     import torch
 
     h, w, c = shape
@@ -269,9 +271,10 @@ def synthetic_images_torch(n: int, shape: Tuple[int, int, int], classes: int = 1
     protos = torch.randn(classes, c, ch, cw, generator=g)
     protos = torch.nn.functional.interpolate(protos, size=(h, w), mode="bilinear",
                                              align_corners=False)
-    gl = torch.Generator(device="cpu").manual_seed(seed * 7919 + start)
+    salt = {"train": 0, "test": 1 << 40, "val": 2 << 40}[split]
+    gl = torch.Generator(device="cpu").manual_seed(seed * 7919 + start + salt)
     labels = torch.randint(0, classes, (n,), generator=gl)
-    gn = torch.Generator(device=device).manual_seed(seed * 104729 + start)
+    gn = torch.Generator(device=device).manual_seed(seed * 104729 + start + salt)
     x = protos.to(device)[labels.to(device)] * 0.25
     x = x + 0.15 * torch.randn(x.shape, generator=gn, device=device)
     x = x.clamp_(-0.5, 0.5).permute(0, 2, 3, 1).contiguous()
