@@ -162,15 +162,17 @@ PYBIND11_MODULE(_C, m) {
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
-                       bool relu, uintptr_t st) {
-    gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu, S(st));
+                       bool relu, uintptr_t ws, uintptr_t st) {
+    gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
+                   P<float>(ws), S(st));
     check_launch();
   });
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
-                            uintptr_t st) {
-    gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), S(st));
+                            uintptr_t ws, uintptr_t st) {
+    gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st));
     check_launch();
   });
+  g.def("conv_ws_floats", &gops::conv_ws_floats);
   g.def("conv_filter_splits", &gops::conv_filter_splits);
   g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,
                               uintptr_t dw, uintptr_t st) {
@@ -178,25 +180,28 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("colsum2", [](uintptr_t a, uintptr_t b, long long rows, int C, uintptr_t s1, uintptr_t s2,
-                      int mode, uintptr_t st) {
-    gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode, S(st));
+                      int mode, uintptr_t ws, uintptr_t st) {
+    gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode,
+                  P<float>(ws), S(st));
     check_launch();
   });
+  g.def("chan_reduce_ok", &gops::chan_reduce_ok);
+  g.def("chan_reduce_ws_floats", &gops::chan_reduce_ws_floats);
   g.def("bn_fwd", [](uintptr_t x, long long rows, int C, uintptr_t gm, uintptr_t bt, uintptr_t res,
-                     uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t sum, uintptr_t sumsq,
-                     float eps, bool relu, bool training, uintptr_t rmean, uintptr_t rvar,
+                     uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t ws, float eps,
+                     float momentum, bool relu, bool training, uintptr_t rmean, uintptr_t rvar,
                      uintptr_t st) {
     gops::bn_fwd(P<const float>(x), rows, C, P<const float>(gm), P<const float>(bt),
-                 P<const float>(res), P<float>(y), P<float>(mean), P<float>(rstd), P<float>(sum),
-                 P<float>(sumsq), eps, relu, training, P<const float>(rmean), P<const float>(rvar), S(st));
+                 P<const float>(res), P<float>(y), P<float>(mean), P<float>(rstd), P<float>(ws), eps,
+                 momentum, relu, training, P<float>(rmean), P<float>(rvar), S(st));
     check_launch();
   });
   g.def("bn_bwd", [](uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
-                     uintptr_t gm, long long rows, int C, bool relu, uintptr_t dym, uintptr_t xh,
-                     uintptr_t dg, uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st) {
+                     uintptr_t gm, long long rows, int C, bool relu, uintptr_t ws, uintptr_t dg,
+                     uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st) {
     gops::bn_bwd(P<const float>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
-                 P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(dym), P<float>(xh),
-                 P<float>(dg), P<float>(db), P<float>(dx), P<float>(dres), S(st));
+                 P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(ws), P<float>(dg),
+                 P<float>(db), P<float>(dx), P<float>(dres), S(st));
     check_launch();
   });
   g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {

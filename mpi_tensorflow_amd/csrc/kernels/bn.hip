@@ -1,0 +1,271 @@
+// Per-channel reductions and BatchNorm for NHWC tensors (ResNet-18 config).
+//
+// The statistics are a two-pass, deterministic column reduction: pass 1 has
+// each block reduce a slab of rows into per-channel partials (thread = one
+// float4 of channels x a row stride, so every global load is a coalesced
+// 16-byte access; a block covers floor(256 / (C/4)) rows per pass); pass 2
+// has one wave per channel sum the block partials.  No
+// atomics, no memsets: the result (and a graph replay of it) is bitwise
+// reproducible.
+//
+// BN backward needs sum(dy') and sum(dy' * xhat) with dy' = dy [y > 0] when a
+// ReLU is fused; the pass-1 kernel computes both straight from (x, dy, y,
+// mean, rstd), so neither dy' nor xhat is ever materialised.  The BN forward
+// finalize also updates the running statistics (momentum, unbiased variance),
+// so the whole layer is three kernels with no host-side tensor ops.
+#include <stdexcept>
+
+#include "common.h"
+#include "ops_generic.h"
+
+namespace gops {
+namespace bn {
+
+enum Mode { SUM_SQ = 0, SUM_PROD = 1, BN_BWD = 2 };
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+template <int MODE>
+__global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ a,
+                                                      const float* __restrict__ b,
+                                                      const float* __restrict__ yv,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ rstd, int relu,
+                                                      long long rows, int C, int rows_per_block,
+                                                      float* __restrict__ part) {
+  __shared__ float4 red[2][256];
+  const int cq = C >> 2, RP = 256 / cq;
+  const int tid = threadIdx.x, q = tid % cq, rl = tid / cq;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(rows, r0 + rows_per_block);
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  float4 mu = s1, rs = s1;
+  if (MODE == BN_BWD) {
+    mu = ld4(mean + 4 * q);
+    rs = ld4(rstd + 4 * q);
+  }
+  if (rl < RP) {
+#pragma unroll 4
+    for (long long r = r0 + rl; r < r1; r += RP) {
+      const size_t o = (size_t)r * C + 4 * q;
+      const float4 v = ld4(a + o);
+      if (MODE == SUM_SQ) {
+        s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
+        s2.x += v.x * v.x; s2.y += v.y * v.y; s2.z += v.z * v.z; s2.w += v.w * v.w;
+      } else if (MODE == SUM_PROD) {
+        const float4 u = ld4(b + o);
+        s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
+        s2.x += v.x * u.x; s2.y += v.y * u.y; s2.z += v.z * u.z; s2.w += v.w * u.w;
+      } else {  // a = x, b = dy, yv = y (relu mask)
+        float4 d = ld4(b + o);
+        if (relu) {
+          const float4 yy = ld4(yv + o);
+          d.x = yy.x > 0.f ? d.x : 0.f;
+          d.y = yy.y > 0.f ? d.y : 0.f;
+          d.z = yy.z > 0.f ? d.z : 0.f;
+          d.w = yy.w > 0.f ? d.w : 0.f;
+        }
+        s1.x += d.x; s1.y += d.y; s1.z += d.z; s1.w += d.w;
+        s2.x += d.x * (v.x - mu.x) * rs.x;
+        s2.y += d.y * (v.y - mu.y) * rs.y;
+        s2.z += d.z * (v.z - mu.z) * rs.z;
+        s2.w += d.w * (v.w - mu.w) * rs.w;
+      }
+    }
+  }
+  red[0][tid] = s1;
+  red[1][tid] = s2;
+  __syncthreads();
+  if (tid < cq) {  // thread q folds the RP row lanes of its channel quad
+    float4 t1 = red[0][tid], t2 = red[1][tid];
+    for (int j = 1; j < RP; ++j) {
+      const float4 u1 = red[0][tid + j * cq], u2 = red[1][tid + j * cq];
+      t1.x += u1.x; t1.y += u1.y; t1.z += u1.z; t1.w += u1.w;
+      t2.x += u2.x; t2.y += u2.y; t2.z += u2.z; t2.w += u2.w;
+    }
+    float* p = part + (size_t)blockIdx.x * 2 * C;
+    *reinterpret_cast<float4*>(p + 4 * tid) = t1;
+    *reinterpret_cast<float4*>(p + C + 4 * tid) = t2;
+  }
+}
+
+// One wave per channel: s1 / s2 = sums of the nb block partials.  BN
+// forward mode also writes mean / rstd and updates the running statistics.
+__global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nb,
+                                                       int C, float* __restrict__ s1,
+                                                       float* __restrict__ s2, int bn_fwd,
+                                                       long long rows, float eps, float momentum,
+                                                       float* __restrict__ mean,
+                                                       float* __restrict__ rstd,
+                                                       float* __restrict__ rmean,
+                                                       float* __restrict__ rvar) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;
+  float a = 0.f, b = 0.f;
+  for (int k = lane; k < nb; k += 64) {
+    a += part[(size_t)k * 2 * C + c];
+    b += part[(size_t)k * 2 * C + C + c];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  if (lane != 0) return;
+  if (s1) s1[c] = a;
+  if (s2) s2[c] = b;
+  if (bn_fwd) {
+    const float inv = 1.f / (float)rows;
+    const float m = a * inv;
+    const float var = fmaxf(b * inv - m * m, 0.f);
+    mean[c] = m;
+    rstd[c] = rsqrtf(var + eps);
+    if (rmean) {  // torch semantics: unbiased variance in the running estimate
+      const float unb = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * m;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
+    }
+  }
+}
+
+// y = (x - mean) rstd g + b (+ res) (relu); eval: mean / var from running stats
+__global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
+                                                    const float* __restrict__ mean,
+                                                    const float* __restrict__ rstd,
+                                                    const float* __restrict__ g,
+                                                    const float* __restrict__ bb,
+                                                    const float* __restrict__ res,
+                                                    float* __restrict__ y, long long n4, int C,
+                                                    int relu, int eval, float eps) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int cq = C >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int c = (int)(i % cq) * 4;
+    const float4 v = ld4(x + 4 * i);
+    float4 m = ld4(mean + c), r = ld4(rstd + c);
+    if (eval) {
+      r.x = rsqrtf(r.x + eps); r.y = rsqrtf(r.y + eps); r.z = rsqrtf(r.z + eps); r.w = rsqrtf(r.w + eps);
+    }
+    const float4 gg = ld4(g + c), b4 = ld4(bb + c);
+    float4 o;
+    o.x = (v.x - m.x) * r.x * gg.x + b4.x;
+    o.y = (v.y - m.y) * r.y * gg.y + b4.y;
+    o.z = (v.z - m.z) * r.z * gg.z + b4.z;
+    o.w = (v.w - m.w) * r.w * gg.w + b4.w;
+    if (res) {
+      const float4 q = ld4(res + 4 * i);
+      o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+    }
+    if (relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    *reinterpret_cast<float4*>(y + 4 * i) = o;
+  }
+}
+
+// dx = g rstd (dy' - s1/rows - xhat s2/rows); dres = dy' (residual branch)
+__global__ __launch_bounds__(256) void bwd_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
+    const float* __restrict__ s1, const float* __restrict__ s2, float* __restrict__ dx,
+    float* __restrict__ dres, long long n4, int C, long long rows, int relu) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int cq = C >> 2;
+  const float inv = 1.f / (float)rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int c = (int)(i % cq) * 4;
+    float4 d = ld4(dy + 4 * i);
+    if (relu) {
+      const float4 yy = ld4(y + 4 * i);
+      d.x = yy.x > 0.f ? d.x : 0.f;
+      d.y = yy.y > 0.f ? d.y : 0.f;
+      d.z = yy.z > 0.f ? d.z : 0.f;
+      d.w = yy.w > 0.f ? d.w : 0.f;
+    }
+    if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
+    const float4 v = ld4(x + 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
+    const float4 a = ld4(s1 + c), b = ld4(s2 + c);
+    float4 o;
+    o.x = gg.x * r.x * (d.x - a.x * inv - (v.x - m.x) * r.x * b.x * inv);
+    o.y = gg.y * r.y * (d.y - a.y * inv - (v.y - m.y) * r.y * b.y * inv);
+    o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
+    o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
+    *reinterpret_cast<float4*>(dx + 4 * i) = o;
+  }
+}
+
+static inline int grid_elems(long long n) {
+  long long b = (n + 255) / 256;
+  return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
+}
+
+static inline int nblocks(long long rows, int C) {
+  const int RP = 256 / (C / 4);
+  long long nb = (rows + RP * 16 - 1) / (RP * 16);  // >= 16 row passes per block
+  if (nb > 1024) nb = 1024;
+  return (int)(nb < 1 ? 1 : nb);
+}
+
+}  // namespace bn
+
+bool chan_reduce_ok(int C) { return C % 4 == 0 && C >= 4 && C <= 1024; }
+
+long long chan_reduce_ws_floats(long long rows, int C) {
+  return chan_reduce_ok(C) ? (long long)bn::nblocks(rows, C) * 2 * C : 0;
+}
+
+static void run_partials(int mode, const float* a, const float* b, const float* y,
+                         const float* mean, const float* rstd, int relu, long long rows, int C,
+                         float* ws, int nb, hipStream_t st) {
+  const int rpb = (int)((rows + nb - 1) / nb);
+  switch (mode) {
+    case bn::SUM_SQ:
+      bn::partial_kernel<bn::SUM_SQ><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      break;
+    case bn::SUM_PROD:
+      bn::partial_kernel<bn::SUM_PROD><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      break;
+    default:
+      bn::partial_kernel<bn::BN_BWD><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+  }
+}
+
+void chan_reduce(const float* a, const float* b, long long rows, int C, float* s1, float* s2,
+                 int mode, float* ws, hipStream_t st) {
+  if (!chan_reduce_ok(C)) throw std::runtime_error("chan_reduce: unsupported channel count");
+  const int nb = bn::nblocks(rows, C);
+  run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, s1, s2, 0, rows, 0.f, 0.f, nullptr,
+                                                   nullptr, nullptr, nullptr);
+}
+
+void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
+            const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
+            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st) {
+  if (!chan_reduce_ok(C)) throw std::runtime_error("bn_fwd: unsupported channel count");
+  const long long n4 = rows * C / 4;
+  if (training) {
+    const int nb = bn::nblocks(rows, C);
+    run_partials(bn::SUM_SQ, x, nullptr, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+    bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, nullptr, nullptr, 1, rows, eps,
+                                                     momentum, mean, rstd, rmean, rvar);
+    bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
+                                                          relu ? 1 : 0, 0, eps);
+  } else {
+    bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4, C,
+                                                          relu ? 1 : 0, 1, eps);
+  }
+}
+
+void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
+            const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
+            float* dx, float* dres, hipStream_t st) {
+  if (!chan_reduce_ok(C)) throw std::runtime_error("bn_bwd: unsupported channel count");
+  const int nb = bn::nblocks(rows, C);
+  run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, st);
+  // db = sum dy', dg = sum dy' xhat
+  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, db, dg, 0, rows, 0.f, 0.f, nullptr,
+                                                   nullptr, nullptr, nullptr);
+  const long long n4 = rows * C / 4;
+  bn::bwd_apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx,
+                                                            dres, n4, C, rows, relu ? 1 : 0);
+}
+
+}  // namespace gops

@@ -1,0 +1,708 @@
+// LDS-tiled implicit-GEMM convolutions (NHWC activations, HWIO weights, fp32
+// storage and fp32 MFMA v_mfma_f32_32x32x2_f32) for the channel counts of
+// ResNet-18 and wide layers in general: forward, backward-data (stride-s
+// phase decomposition) and backward-filter (split-K slabs).
+//
+// Why a second conv family next to ops_generic.hip's gather engine: that
+// engine decodes (tap, channel) per element per K step (div/mod in the inner
+// loop) and stages one float per lane.  Here a K tile is ONE tap x BK
+// consecutive channels, so each operand row of a tile is BK contiguous
+// floats in memory: the per-row pixel decode and bounds test happen once per
+// tap, global loads are float4 along the channel axis, and the LDS image is
+// k-major ([BK][BM + pad]) so the 32 lanes of a half-wave read 32 consecutive
+// rows of one k for the fp32 MFMA operand (A[i][k] on lane i, B[k][j] on
+// lane j).  Block = 256 threads = 2x2 waves, each wave (BM/2)x(BN/2) =
+// TMxTN 32x32 MFMA tiles; double-buffered LDS, one barrier per K tile, the
+// next tile's global loads in flight during the current tile's MFMAs;
+// XCD-aware block order.
+#include <stdexcept>
+
+#include "common.h"
+#include "ops_generic.h"
+
+namespace gops {
+namespace tiled {
+
+constexpr int BK = 32, PAD = 4, NT = 256;
+
+template <int BM, int BN>
+struct Geo {
+  static constexpr int TM = BM / 64, TN = BN / 64;  // MFMA tiles per wave
+  static constexpr int LDA = BM + PAD, LDB = BN + PAD;
+  static constexpr int STAGE = BK * (LDA + LDB);
+  static constexpr int SMEM = 2 * STAGE;
+};
+
+// One K tile: A[BK][BM] (k-major) and B[BK][BN] from registers to LDS, then
+// the MFMAs of the wave's TMxTN sub-tiles over the tile's BK.
+template <int BM, int BN>
+__device__ __forceinline__ void mma_tile(const float* As, const float* Bs, int wm, int wn,
+                                         int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
+  using G = Geo<BM, BN>;
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int ks = 0; ks < BK / 2; ++ks) {
+    float a[G::TM], b[G::TN];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i) a[i] = As[(2 * ks + h) * G::LDA + wm * (BM / 2) + 32 * i + r];
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) b[j] = Bs[(2 * ks + h) * G::LDB + wn * (BN / 2) + 32 * j + r];
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
+  }
+}
+
+// Double-buffered main loop over K tiles [k0, k0 + nk).  L provides
+//   load(kt)   : issue the global loads of K tile kt into its registers
+//   store(A,B) : write those registers into the LDS stage
+template <int BM, int BN, class L>
+__device__ __forceinline__ void mainloop(L& ld, float* smem, int k0, int nk,
+                                         f32x16 (&acc)[BM / 64][BN / 64]) {
+  using G = Geo<BM, BN>;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+#pragma unroll
+  for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < G::TN; ++j) acc[i][j] = zero16();
+  if (nk <= 0) return;
+  ld.load(k0);
+  ld.store(smem, smem + BK * G::LDA);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    float* cur = smem + (kt & 1) * G::STAGE;
+    float* nxt = smem + ((kt + 1) & 1) * G::STAGE;
+    const bool more = kt + 1 < nk;
+    if (more) ld.load(k0 + kt + 1);
+    mma_tile<BM, BN>(cur, cur + BK * G::LDA, wm, wn, lane, acc);
+    if (more) ld.store(nxt, nxt + BK * G::LDA);
+    __syncthreads();
+  }
+}
+
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// ------------------------------------------------------------- forward ----
+// Y[m = (n, oy, ox)][co] = sum_{kh, kw, ci} X[n, oy s - p + kh, ox s - p + kw, ci] W[kh, kw, ci, co]
+// K tile kt = (tap, 32-channel chunk).  Requires C % 32 == 0, K % 4 == 0.
+template <int BM, int BN>
+struct FwdLoader {
+  static constexpr int AR = BM * BK / 4 / NT;  // float4 of A per thread
+  static constexpr int BR = BN * BK / 4 / NT;  // float4 of B per thread
+  ConvShape s;
+  const float* x;
+  const float* w;
+  int n0, cchunks;
+  // A rows of this thread: pixel base pointer and top-left input coords
+  const float* abase[AR];
+  int iy0[AR], ix0[AR];
+  bool av[AR];
+  float4 ra[AR], rb[BR];
+  bool bv[BR];
+  __device__ FwdLoader(const ConvShape& s_, const float* x_, const float* w_, int m0, int n0_)
+      : s(s_), x(x_), w(w_), n0(n0_) {
+    cchunks = s.C / BK;
+    const int tid = threadIdx.x, c4 = tid & 7;
+    const int M = s.N * s.OH * s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + 32 * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+      abase[i] = x + (size_t)n * s.H * s.W * s.C + 4 * c4;
+      iy0[i] = oy * s.stride - s.pad;
+      ix0[i] = ox * s.stride - s.pad;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = n0 + 4 * (tid % (BN / 4));
+      bv[i] = n < s.K;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tap = kt / cchunks, ci0 = (kt - tap * cchunks) * BK;
+    const int kh = tap / s.S, kw = tap - kh * s.S;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int iy = iy0[i] + kh, ix = ix0[i] + kw;
+      const bool ok = av[i] && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+      const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+      ra[i] = sel4(ok, *reinterpret_cast<const float4*>(abase[i] + ((size_t)iyc * s.W + ixc) * s.C + ci0));
+    }
+    const int tid = threadIdx.x;
+    const float* wb = w + (size_t)(tap * s.C + ci0) * s.K + min(n0 + 4 * (tid % (BN / 4)), s.K - 4);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      rb[i] = sel4(bv[i], *reinterpret_cast<const float4*>(wb + (size_t)k * s.K));
+    }
+  }
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    using G = Geo<BM, BN>;
+    const int tid = threadIdx.x, c4 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = (tid >> 3) + 32 * i;
+      As[(4 * c4 + 0) * G::LDA + m] = ra[i].x;
+      As[(4 * c4 + 1) * G::LDA + m] = ra[i].y;
+      As[(4 * c4 + 2) * G::LDA + m] = ra[i].z;
+      As[(4 * c4 + 3) * G::LDA + m] = ra[i].w;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+    }
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
+                                                 const float* __restrict__ w,
+                                                 const float* __restrict__ bias,
+                                                 float* __restrict__ y, int relu, int kps) {
+  // split-K (gridDim.y > 1, no bias / ReLU): slice z of kps K tiles writes a
+  // raw slab y + z * M * K, summed by slab_sum4 afterwards
+  using G = Geo<BM, BN>;
+  __shared__ float smem[G::SMEM];
+  const int M = s.N * s.OH * s.OW;
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
+  const int nk = s.R * s.S * (s.C / BK), kb = blockIdx.y * kps;
+  FwdLoader<BM, BN> ld(s, x, w, m0, n0);
+  f32x16 acc[G::TM][G::TN];
+  mainloop<BM, BN>(ld, smem, kb, min(kps, nk - kb), acc);
+  y += (size_t)blockIdx.y * M * s.K;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+#pragma unroll
+  for (int j = 0; j < G::TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
+    if (co >= s.K) continue;
+    const float b = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
+        if (m >= M) continue;
+        float v = acc[i][j][r] + b;
+        if (relu) v = fmaxf(v, 0.f);
+        y[(size_t)m * s.K + co] = v;
+      }
+  }
+}
+
+// ------------------------------------------------------- backward-data ----
+// dX[n, iy, ix, ci] = sum_{kh, kw, co} dY[n, oy, ox, co] W[kh, kw, ci, co] over
+// oy = (iy + p - kh) / s when exact.  Phase decomposition: input pixels with
+// (iy mod s, ix mod s) = (py, px) only receive taps kh = (py + p) mod s (mod s)
+// and likewise kw, so each phase is a dense implicit GEMM over its own tap
+// list (no zero MFMA work for stride 2).  Block z-dimension = phase.
+// K tile = (phase tap, 32-channel chunk of co).  Requires K % 32 == 0, C % 4 == 0.
+template <int BM, int BN>
+struct DataLoader {
+  static constexpr int AR = BM * BK / 4 / NT;
+  static constexpr int BR = BN * BK / 4 / NT;
+  ConvShape s;
+  const float* dy;
+  const float* w;
+  int n0, cchunks, nkw, kh0, kw0;
+  const float* abase[AR];
+  int qy[AR], qx[AR];  // iy + p, ix + p
+  bool av[AR];
+  float4 ra[AR], rb[BR];
+  bool bv[BR];
+  __device__ DataLoader(const ConvShape& s_, const float* dy_, const float* w_, int m0, int n0_,
+                        int py, int px, int PH, int PW, int nkw_, int kh0_, int kw0_)
+      : s(s_), dy(dy_), w(w_), n0(n0_), nkw(nkw_), kh0(kh0_), kw0(kw0_) {
+    cchunks = s.K / BK;
+    const int tid = threadIdx.x, c4 = tid & 7;
+    const int M = s.N * PH * PW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + 32 * i;
+      const int mm = m < M ? m : 0;
+      const int jx = mm % PW, t = mm / PW, jy = t % PH, n = t / PH;
+      const int iy = jy * s.stride + py, ix = jx * s.stride + px;
+      av[i] = m < M && iy < s.H && ix < s.W;
+      abase[i] = dy + (size_t)n * s.OH * s.OW * s.K + 4 * c4;
+      qy[i] = iy + s.pad;
+      qx[i] = ix + s.pad;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) bv[i] = n0 + (tid >> 3) + 32 * i < s.C;
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tp = kt / cchunks, co0 = (kt - tp * cchunks) * BK;
+    const int kh = kh0 + (tp / nkw) * s.stride, kw = kw0 + (tp % nkw) * s.stride;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int oy = (qy[i] - kh) / s.stride, ox = (qx[i] - kw) / s.stride;  // exact by phase
+      const bool ok = av[i] && qy[i] >= kh && qx[i] >= kw && oy < s.OH && ox < s.OW;
+      const int oyc = min(max(oy, 0), s.OH - 1), oxc = min(max(ox, 0), s.OW - 1);
+      ra[i] = sel4(ok, *reinterpret_cast<const float4*>(abase[i] + ((size_t)oyc * s.OW + oxc) * s.K + co0));
+    }
+    // B[k = co][n = ci] = W[kh, kw, ci, co]: float4 along co for one ci
+    const int tid = threadIdx.x, c4 = tid & 7;
+    const float* wb = w + (size_t)(kh * s.S + kw) * s.C * s.K + co0 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int ci = min(n0 + (tid >> 3) + 32 * i, s.C - 1);
+      rb[i] = sel4(bv[i], *reinterpret_cast<const float4*>(wb + (size_t)ci * s.K));
+    }
+  }
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    using G = Geo<BM, BN>;
+    const int tid = threadIdx.x, c4 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = (tid >> 3) + 32 * i;
+      As[(4 * c4 + 0) * G::LDA + m] = ra[i].x;
+      As[(4 * c4 + 1) * G::LDA + m] = ra[i].y;
+      As[(4 * c4 + 2) * G::LDA + m] = ra[i].z;
+      As[(4 * c4 + 3) * G::LDA + m] = ra[i].w;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = (tid >> 3) + 32 * i;
+      Bs[(4 * c4 + 0) * G::LDB + n] = rb[i].x;
+      Bs[(4 * c4 + 1) * G::LDB + n] = rb[i].y;
+      Bs[(4 * c4 + 2) * G::LDB + n] = rb[i].z;
+      Bs[(4 * c4 + 3) * G::LDB + n] = rb[i].w;
+    }
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __restrict__ dy,
+                                                  const float* __restrict__ w,
+                                                  float* __restrict__ dx, int kps) {
+  // split-K over gridDim.z: slice z writes the raw slab dx + z * N*H*W*C
+  using G = Geo<BM, BN>;
+  __shared__ float smem[G::SMEM];
+  const int sd = s.stride;
+  const int phase = blockIdx.y, py = phase / sd, px = phase % sd;
+  const int PH = (s.H - py + sd - 1) / sd, PW = (s.W - px + sd - 1) / sd;
+  // taps of this phase: kh = (py + p) mod s, + s, ... < R
+  const int kh0 = ((py + s.pad) % sd + sd) % sd, kw0 = ((px + s.pad) % sd + sd) % sd;
+  const int nkh = kh0 < s.R ? (s.R - kh0 + sd - 1) / sd : 0;
+  const int nkw = kw0 < s.S ? (s.S - kw0 + sd - 1) / sd : 0;
+  const int M = s.N * PH * PW;
+  // the grid is sized for the largest phase (py = px = 0)
+  const int mt = (s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd) + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
+  if (m0 >= M) return;  // phases with fewer pixels than the grid covers
+  DataLoader<BM, BN> ld(s, dy, w, m0, n0, py, px, PH, PW, nkw > 0 ? nkw : 1, kh0, kw0);
+  f32x16 acc[G::TM][G::TN];
+  const int nk = nkh * nkw * (s.K / BK), kb = blockIdx.z * kps;
+  mainloop<BM, BN>(ld, smem, kb, min(kps, nk - kb), acc);
+  dx += (size_t)blockIdx.z * s.N * s.H * s.W * s.C;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+#pragma unroll
+  for (int j = 0; j < G::TN; ++j) {
+    const int ci = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
+    if (ci >= s.C) continue;
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
+        if (m >= M) continue;
+        const int jx = m % PW, t = m / PW, jy = t % PH, n = t / PH;
+        const int iy = jy * sd + py, ix = jx * sd + px;
+        if (iy < s.H && ix < s.W) dx[(((size_t)n * s.H + iy) * s.W + ix) * s.C + ci] = acc[i][j][r];
+      }
+  }
+}
+
+// ----------------------------------------------------- backward-filter ----
+// dW[tap][ci][co] = sum_{pix} X[pix shifted by tap][ci] dY[pix][co]; per
+// block: one tap, a BM x BN (ci x co) tile, one split-K slice of the pixels;
+// K tile = 32 output pixels.  Both operands load float4 along their channel
+// axis straight into the k-major LDS image.  Requires C % 4 == 0, K % 4 == 0.
+template <int BM, int BN>
+struct FilterLoader {
+  static constexpr int AR = BM * BK / 4 / NT;
+  static constexpr int BR = BN * BK / 4 / NT;
+  ConvShape s;
+  const float* x;
+  const float* dy;
+  int m0, n0, kh, kw, pix0, npix;
+  float4 ra[AR], rb[BR];
+  __device__ FilterLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0_, int n0_,
+                          int tap, int pix0_, int npix_)
+      : s(s_), x(x_), dy(dy_), m0(m0_), n0(n0_), pix0(pix0_), npix(npix_) {
+    kh = tap / s.S;
+    kw = tap % s.S;
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tid = threadIdx.x;
+    const int ma = 4 * (tid % (BM / 4)), nb = 4 * (tid % (BN / 4));
+    const int ci = min(m0 + ma, s.C - 4), co = min(n0 + nb, s.K - 4);
+    const bool cv = m0 + ma < s.C, kv = n0 + nb < s.K;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
+      const int pix = pix0 + kt * BK + k;
+      const int pc = min(pix, npix - 1);
+      const int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
+      const int iy = oy * s.stride - s.pad + kh, ix = ox * s.stride - s.pad + kw;
+      const bool ok = cv && pix < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+      const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+      ra[i] = sel4(ok, *reinterpret_cast<const float4*>(
+                           x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ci));
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      const int pix = pix0 + kt * BK + k;
+      const bool ok = kv && pix < npix;
+      rb[i] = sel4(ok, *reinterpret_cast<const float4*>(dy + (size_t)min(pix, npix - 1) * s.K + co));
+    }
+  }
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    using G = Geo<BM, BN>;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
+      *reinterpret_cast<float4*>(As + k * G::LDA + 4 * (tid % (BM / 4))) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+    }
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void filter_kernel(ConvShape s, const float* __restrict__ x,
+                                                    const float* __restrict__ dy,
+                                                    float* __restrict__ part, int kchunk_tiles) {
+  using G = Geo<BM, BN>;
+  __shared__ float smem[G::SMEM];
+  const int mt = (s.C + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
+  const int taps = s.R * s.S;
+  const int tiles = mt * nt * taps;
+  const int bid = blockIdx.x;
+  const int z = bid / tiles, rem = bid % tiles;
+  const int tap = rem % taps, t2 = rem / taps;
+  const int m0 = (t2 % mt) * BM, n0 = (t2 / mt) * BN;
+  const int npix = s.N * s.OH * s.OW;
+  const int pix0 = z * kchunk_tiles * BK;
+  const int nk = min(kchunk_tiles, (npix - pix0 + BK - 1) / BK);
+  FilterLoader<BM, BN> ld(s, x, dy, m0, n0, tap, pix0, npix);
+  f32x16 acc[G::TM][G::TN];
+  mainloop<BM, BN>(ld, smem, 0, nk, acc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+  const size_t slab = (size_t)taps * s.C * s.K;
+#pragma unroll
+  for (int j = 0; j < G::TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
+    if (co >= s.K) continue;
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
+        if (ci >= s.C) continue;
+        part[z * slab + ((size_t)tap * s.C + ci) * s.K + co] = acc[i][j][r];
+      }
+  }
+}
+
+// Backward-filter for channel counts that are not a multiple of 4 (the
+// 3-channel ResNet stem, LeNet's 6-channel conv): M = R*S*C rows (tap, ci)
+// in one GEMM (no per-tap grid split, so a 3-channel layer does not waste a
+// 64-row tile per tap); A elements are scalar gathers whose (tap, ci) decode
+// is done once per thread, the pixel decode once per K tile row.
+template <int BM, int BN>
+struct FilterGatherLoader {
+  static constexpr int AR = BM * BK / 4 / NT;
+  static constexpr int BR = BN * BK / 4 / NT;
+  ConvShape s;
+  const float* x;
+  const float* dy;
+  int n0, pix0, npix;
+  int dh[4], dw[4], ci[4];  // this thread's 4 A columns (m = ma + j)
+  bool mv[4];
+  float4 ra[AR], rb[BR];
+  __device__ FilterGatherLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0,
+                                int n0_, int pix0_, int npix_)
+      : s(s_), x(x_), dy(dy_), n0(n0_), pix0(pix0_), npix(npix_) {
+    const int Mw = s.R * s.S * s.C;
+    const int ma = m0 + 4 * (threadIdx.x % (BM / 4));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = ma + j;
+      mv[j] = m < Mw;
+      const int mm = mv[j] ? m : 0;
+      ci[j] = mm % s.C;
+      const int tap = mm / s.C;
+      dh[j] = tap / s.S - s.pad;
+      dw[j] = tap % s.S - s.pad;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tid = threadIdx.x;
+    const int nb = 4 * (tid % (BN / 4));
+    const int co = min(n0 + nb, s.K - 4);
+    const bool kv = n0 + nb < s.K;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
+      const int pix = pix0 + kt * BK + k;
+      const int pc = min(pix, npix - 1);
+      const int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
+      const float* img = x + (size_t)n * s.H * s.W * s.C;
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int iy = oy * s.stride + dh[j], ix = ox * s.stride + dw[j];
+        const bool ok = mv[j] && pix < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+        const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+        const float e = img[((size_t)iyc * s.W + ixc) * s.C + ci[j]];
+        v[j] = ok ? e : 0.f;
+      }
+      ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      const int pix = pix0 + kt * BK + k;
+      rb[i] = sel4(kv && pix < npix,
+                   *reinterpret_cast<const float4*>(dy + (size_t)min(pix, npix - 1) * s.K + co));
+    }
+  }
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    using G = Geo<BM, BN>;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
+      *reinterpret_cast<float4*>(As + k * G::LDA + 4 * (tid % (BM / 4))) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+    }
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void filter_gather_kernel(ConvShape s, const float* __restrict__ x,
+                                                           const float* __restrict__ dy,
+                                                           float* __restrict__ part,
+                                                           int kchunk_tiles) {
+  using G = Geo<BM, BN>;
+  __shared__ float smem[G::SMEM];
+  const int Mw = s.R * s.S * s.C;
+  const int mt = (Mw + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
+  const int z = blockIdx.x / (mt * nt), rem = blockIdx.x % (mt * nt);
+  const int m0 = (rem % mt) * BM, n0 = (rem / mt) * BN;
+  const int npix = s.N * s.OH * s.OW;
+  const int pix0 = z * kchunk_tiles * BK;
+  const int nk = min(kchunk_tiles, (npix - pix0 + BK - 1) / BK);
+  FilterGatherLoader<BM, BN> ld(s, x, dy, m0, n0, pix0, npix);
+  f32x16 acc[G::TM][G::TN];
+  mainloop<BM, BN>(ld, smem, 0, nk, acc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+#pragma unroll
+  for (int j = 0; j < G::TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
+    if (co >= s.K) continue;
+#pragma unroll
+    for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
+        if (m < Mw) part[(size_t)z * Mw * s.K + (size_t)m * s.K + co] = acc[i][j][r];
+      }
+  }
+}
+
+// Deterministic slab reduction, float4-vectorised (n % 4 == 0).
+__global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
+                                                        long long n4, float4* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = part[i];
+    for (int z = 1; z < nz; ++z) {
+      const float4 b = part[z * n4 + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    out[i] = a;
+  }
+}
+
+// ------------------------------------------------------------ dispatch ----
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Block tile from the GEMM's M and N: 128-wide where the dimension allows it.
+enum Tile { T128x128, T128x64, T64x128, T64x64 };
+static inline Tile pick(long long M, int N) {
+  const bool bm = M >= 128 * 256, bn = N > 64;  // wide M tiles only with >= 256 blocks of them
+  if (bn) return bm ? T128x128 : T64x128;
+  return bm ? T128x64 : T64x64;
+}
+
+#define TILED_DISPATCH(t, KERNEL, GRID, ...)                                          \
+  switch (t) {                                                                         \
+    case T128x128: KERNEL<128, 128><<<GRID(128, 128), NT, 0, st>>>(__VA_ARGS__); break; \
+    case T128x64: KERNEL<128, 64><<<GRID(128, 64), NT, 0, st>>>(__VA_ARGS__); break;    \
+    case T64x128: KERNEL<64, 128><<<GRID(64, 128), NT, 0, st>>>(__VA_ARGS__); break;    \
+    default: KERNEL<64, 64><<<GRID(64, 64), NT, 0, st>>>(__VA_ARGS__); break;           \
+  }
+
+}  // namespace tiled
+
+bool conv_fwd_tiled_ok(const ConvShape& s) { return s.C % 32 == 0 && s.K % 4 == 0; }
+bool conv_bwd_data_tiled_ok(const ConvShape& s) { return s.K % 32 == 0 && s.C % 4 == 0; }
+bool conv_bwd_filter_tiled_ok(const ConvShape& s) { return s.K % 4 == 0; }  // C % 4: vector path
+
+namespace tiled {
+static inline int tile_m(Tile t) { return (t == T128x128 || t == T128x64) ? 128 : 64; }
+static inline int tile_n(Tile t) { return (t == T128x128 || t == T64x128) ? 128 : 64; }
+
+// split-K factor for a GEMM with `blocks` output tiles of nk K tiles each:
+// deep layers (few tiles, long K) get enough blocks to fill 256 CUs twice
+static inline int ksplit(long long blocks, int nk) {
+  if (blocks >= 512 || nk < 8) return 1;
+  int z = cdiv(1024, blocks);
+  if (z > nk / 4) z = nk / 4;
+  if (z > 16) z = 16;
+  if (z < 1) z = 1;
+  const int kps = cdiv(nk, z);
+  return cdiv(nk, kps);
+}
+static inline void fwd_plan(const ConvShape& s, bool epilogue, Tile& t, int& z, int& kps) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  t = pick(M, s.K);
+  const int nk = s.R * s.S * (s.C / BK);
+  z = epilogue ? 1 : ksplit((long long)cdiv(M, tile_m(t)) * cdiv(s.K, tile_n(t)), nk);
+  kps = cdiv(nk, z);
+}
+static inline void data_plan(const ConvShape& s, Tile& t, int& z, int& kps) {
+  const int sd = s.stride;
+  const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
+  t = pick(Mph * sd * sd, s.C);
+  const int ntap = cdiv(s.R, sd) * cdiv(s.S, sd);  // taps of the richest phase
+  const int nk = ntap * (s.K / BK);
+  z = ksplit((long long)cdiv(Mph, tile_m(t)) * cdiv(s.C, tile_n(t)) * sd * sd, nk);
+  kps = cdiv(nk, z);
+}
+static inline void slab_sum(const float* part, int z, long long n, float* out, hipStream_t st) {
+  long long b = (n / 4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(part), z, n / 4,
+                                          reinterpret_cast<float4*>(out));
+}
+}  // namespace tiled
+
+long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
+  tiled::Tile t;
+  int z, kps;
+  tiled::fwd_plan(s, epilogue, t, z, kps);
+  return z > 1 ? (long long)z * s.N * s.OH * s.OW * s.K : 0;
+}
+
+long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
+  tiled::Tile t;
+  int z, kps;
+  tiled::data_plan(s, t, z, kps);
+  return z > 1 ? (long long)z * s.N * s.H * s.W * s.C : 0;
+}
+
+void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
+                    bool relu, float* ws, hipStream_t st) {
+  using namespace tiled;
+  const long long M = (long long)s.N * s.OH * s.OW;
+  Tile t;
+  int z, kps;
+  fwd_plan(s, bias != nullptr || relu, t, z, kps);
+  if (z > 1 && !ws) throw std::runtime_error("conv_fwd_tiled: split-K needs a workspace");
+  float* out = z > 1 ? ws : y;
+#define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), z)
+  TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+#undef GRID
+  if (z > 1) slab_sum(ws, z, M * s.K, y, st);
+}
+
+void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                         hipStream_t st) {
+  using namespace tiled;
+  const int sd = s.stride;
+  const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
+  Tile t;
+  int z, kps;
+  data_plan(s, t, z, kps);
+  if (z > 1 && !ws) throw std::runtime_error("conv_bwd_data_tiled: split-K needs a workspace");
+  float* out = z > 1 ? ws : dx;
+  // phases no tap reaches (odd pixels of a 1x1 stride-2 conv) run zero K
+  // tiles and write zeros
+#define GRID(BM_, BN_) dim3(cdiv(Mph, BM_) * cdiv(s.C, BN_), sd * sd, z)
+  TILED_DISPATCH(t, data_kernel, GRID, s, dy, w, out, kps)
+#undef GRID
+  if (z > 1) slab_sum(ws, z, (long long)s.N * s.H * s.W * s.C, dx, st);
+}
+
+namespace tiled {
+static inline Tile filter_tile(const ConvShape& s) {  // ci x co tiles
+  const bool bm = s.C >= 128, bn = s.K > 64;
+  return bm ? (bn ? T128x128 : T128x64) : (bn ? T64x128 : T64x64);
+}
+static inline int filter_blocks_per_split(const ConvShape& s) {
+  const Tile t = filter_tile(s);
+  const int BM = (t == T128x128 || t == T128x64) ? 128 : 64;
+  const int BN = (t == T128x128 || t == T64x128) ? 128 : 64;
+  return cdiv(s.C, BM) * cdiv(s.K, BN) * s.R * s.S;
+}
+}  // namespace tiled
+
+int conv_filter_tiled_splits(const ConvShape& s) {
+  using namespace tiled;
+  const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
+  const bool vec = s.C % 4 == 0;
+  const int tiles = vec ? filter_blocks_per_split(s) : cdiv(s.R * s.S * s.C, 64) * cdiv(s.K, 64);
+  int z = cdiv(2048, tiles);  // aim for ~2048 blocks
+  if (z < 1) z = 1;
+  if (z > ktiles) z = ktiles;
+  if (z > (vec ? 64 : 128)) z = vec ? 64 : 128;
+  const int kchunk = cdiv(ktiles, z);
+  return cdiv(ktiles, kchunk);  // splits actually launched
+}
+
+void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,
+                           float* dw, hipStream_t st) {
+  using namespace tiled;
+  const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
+  const int z = conv_filter_tiled_splits(s);
+  const int kchunk = cdiv(ktiles, z);
+  const int taps = s.R * s.S;
+  if (s.C % 4 != 0) {  // (tap, ci) gather rows, 64x64 tiles
+    const int Mw = taps * s.C;
+    filter_gather_kernel<64, 64><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
+        s, x, dy, z == 1 ? dw : part, kchunk);
+    if (z > 1) slab_sum(part, z, (long long)Mw * s.K, dw, st);
+    return;
+  }
+  const Tile t = filter_tile(s);
+#define GRID(BM_, BN_) dim3(cdiv(s.C, BM_) * cdiv(s.K, BN_) * taps * z)
+  TILED_DISPATCH(t, filter_kernel, GRID, s, x, dy, z == 1 ? dw : part, kchunk)
+#undef GRID
+  if (z > 1) slab_sum(part, z, (long long)taps * s.C * s.K, dw, st);
+}
+
+}  // namespace gops

@@ -16,23 +16,51 @@ struct PoolShape {
   int N, H, W, C, k, stride, pad, OH, OW;
 };
 
+// ws: split-K workspace of conv_ws_floats(s, bias || relu) floats (shared by
+// the three ops of one layer; dw / dx / y are written, not accumulated)
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, hipStream_t st);
-void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, hipStream_t st);
+              bool relu, float* ws, hipStream_t st);
+void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                   hipStream_t st);
 int conv_filter_splits(const ConvShape& s);
-// part: workspace of conv_filter_splits(s) * R*S*C*K floats; dw written (not accumulated)
-void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* part, float* dw,
+void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
                      hipStream_t st);
-// mode 0: s1 = colsum(a), s2 = colsum(a^2); mode 1: s1 = colsum(a), s2 = colsum(a*b)
+long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue);
+// LDS-tiled conv family (conv_tiled.hip), used by the launchers above for the
+// shapes it supports
+bool conv_fwd_tiled_ok(const ConvShape& s);
+bool conv_bwd_data_tiled_ok(const ConvShape& s);
+bool conv_bwd_filter_tiled_ok(const ConvShape& s);
+void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
+                    bool relu, float* ws, hipStream_t st);
+void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                         hipStream_t st);
+long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
+long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
+int conv_filter_tiled_splits(const ConvShape& s);
+void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,
+                           float* dw, hipStream_t st);
+// mode 0: s1 = colsum(a), s2 = colsum(a^2); mode 1: s1 = colsum(a), s2 = colsum(a*b).
+// ws (chan_reduce_ws_floats) selects the deterministic bn.hip reduction;
+// null falls back to memset + atomics.
 void colsum2(const float* a, const float* b, long long rows, int C, float* s1, float* s2, int mode,
-             hipStream_t st);
+             float* ws, hipStream_t st);
+// bn.hip: deterministic per-channel reductions and BatchNorm (C % 4 == 0,
+// 4 <= C <= 1024)
+bool chan_reduce_ok(int C);
+long long chan_reduce_ws_floats(long long rows, int C);
+void chan_reduce(const float* a, const float* b, long long rows, int C, float* s1, float* s2,
+                 int mode, float* ws, hipStream_t st);
+// training: batch statistics -> mean / rstd, running stats updated in place
+// (momentum, unbiased var); eval: normalise with rmean / rvar.  y = BN(x)
+// (+ res) (ReLU).
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
-            const float* res, float* y, float* mean, float* rstd, float* sum, float* sumsq,
-            float eps, bool relu, bool training, const float* rmean, const float* rvar,
-            hipStream_t st);
+            const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
+            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st);
+// dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu)
 void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
-            const float* g, long long rows, int C, bool relu, float* dym, float* xh, float* dg,
-            float* db, float* dx, float* dres, hipStream_t st);
+            const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
+            float* dx, float* dres, hipStream_t st);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);

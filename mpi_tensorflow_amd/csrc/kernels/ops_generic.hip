@@ -1,13 +1,15 @@
 // Generic NHWC layer kernels for the LeNet-5 / ResNet-18 configs (BASELINE.json
-// configs 4-5) on gfx950: implicit-GEMM convolution (forward with fused bias
-// + ReLU, backward-data, backward-filter with split-K slabs), BatchNorm
-// (training statistics, fused apply + residual + ReLU, backward), max / global
-// average pooling, fused softmax cross-entropy, batch gather and slab
-// reduction.  Linear layers are 1x1 convolutions over a 1x1 image.
+// configs 4-5) on gfx950: the per-element gather implicit-GEMM convolution
+// (forward with fused bias + ReLU, backward-data, backward-filter with
+// split-K slabs) for shapes the LDS-tiled family (conv_tiled.hip) does not
+// take, max / global average pooling, fused softmax cross-entropy, batch
+// gather and slab reduction.  BatchNorm lives in bn.hip.  Linear layers are
+// 1x1 convolutions over a 1x1 image.
 //
 // Every GEMM-shaped op runs on v_mfma_f32_32x32x2_f32 through gemm_core.h;
 // shapes are runtime values (one code object serves every layer), with the
 // per-slot address decode hoisted out of the K loop by the gather contexts.
+#include <algorithm>
 #include <stdexcept>
 
 #include "common.h"
@@ -279,78 +281,6 @@ __global__ __launch_bounds__(256) void colsum2_kernel(const float* __restrict__ 
   }
 }
 
-// BN forward apply: y = (x - mean) * rstd * g + b (+ res) (relu)
-__global__ __launch_bounds__(256) void bn_apply_kernel(
-    const float* __restrict__ x, const float* __restrict__ sum, const float* __restrict__ sumsq,
-    const float* __restrict__ g, const float* __restrict__ b, const float* __restrict__ res,
-    float* __restrict__ y, float* __restrict__ mean_out, float* __restrict__ rstd_out,
-    long long rows, int C, float eps, int relu, int use_stats, const float* __restrict__ rmean,
-    const float* __restrict__ rvar) {
-  const long long n = rows * C;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const float inv = 1.f / (float)rows;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    float mean, rstd;
-    if (use_stats) {
-      mean = sum[c] * inv;
-      const float var = fmaxf(sumsq[c] * inv - mean * mean, 0.f);
-      rstd = rsqrtf(var + eps);
-      if (i < C && mean_out) {
-        mean_out[c] = mean;
-        rstd_out[c] = rstd;
-      }
-    } else {
-      mean = rmean[c];
-      rstd = rsqrtf(rvar[c] + eps);
-    }
-    float v = (x[i] - mean) * rstd * g[c] + b[c];
-    if (res) v += res[i];
-    if (relu) v = fmaxf(v, 0.f);
-    y[i] = v;
-  }
-}
-
-// BN backward: dx = g*rstd*(dy' - mean(dy') - xhat*mean(dy'*xhat)), dy' = dy*[y>0]
-// sum_dy, sum_dyx are the per-channel sums of dy' and dy'*xhat.
-__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
-    const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
-    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
-    const float* __restrict__ sum_dy, const float* __restrict__ sum_dyx, float* __restrict__ dx,
-    float* __restrict__ dres, long long rows, int C, int relu) {
-  const long long n = rows * C;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  const float inv = 1.f / (float)rows;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    float d = dy[i];
-    if (relu && y[i] <= 0.f) d = 0.f;
-    if (dres) dres[i] = d;
-    const float xh = (x[i] - mean[c]) * rstd[c];
-    dx[i] = g[c] * rstd[c] * (d - sum_dy[c] * inv - xh * sum_dyx[c] * inv);
-  }
-}
-
-// dy' (relu-masked) and xhat products for the BN backward reductions
-__global__ __launch_bounds__(256) void bn_bwd_prep_kernel(const float* __restrict__ x,
-                                                          const float* __restrict__ dy,
-                                                          const float* __restrict__ y,
-                                                          const float* __restrict__ mean,
-                                                          const float* __restrict__ rstd,
-                                                          float* __restrict__ dym,
-                                                          float* __restrict__ xh, long long rows,
-                                                          int C, int relu) {
-  const long long n = rows * C;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    float d = dy[i];
-    if (relu && y[i] <= 0.f) d = 0.f;
-    dym[i] = d;
-    xh[i] = (x[i] - mean[c]) * rstd[c];
-  }
-}
-
 // ------------------------------------------------------------- pooling ----
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(PoolShape p, const float* __restrict__ x,
                                                           float* __restrict__ y,
@@ -496,26 +426,35 @@ __global__ void lr_kernel(const long long* step, int n_local, int batch, float b
   lr[0] = base * powf(decay, (float)((s * batch) / n_local));
 }
 
+// one element per thread up to 2^16 blocks (16M elements), grid-stride beyond
 static inline int grid1d(long long n) {
   long long b = (n + 255) / 256;
-  return (int)(b > 4096 ? 4096 : (b < 1 ? 1 : b));
+  return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
 
 // ------------------------------------------------------------ launchers ----
+// The LDS-tiled conv family (conv_tiled.hip) takes every shape it supports
+// (channel counts that are multiples of 32 / 4: all of ResNet-18 but its
+// 3-channel stem); the per-element gather engine above covers the rest
+// (LeNet-5's 3- and 6-channel layers, thin FC layers).
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, hipStream_t st) {
+              bool relu, float* ws, hipStream_t st) {
+  if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st);
   const int M = s.N * s.OH * s.OW;
   const int blocks = ((M + CFG_F::BM - 1) / CFG_F::BM) * ((s.K + CFG_F::BN - 1) / CFG_F::BN);
   conv_fwd_kernel<<<blocks, 256, 0, st>>>(s, x, w, bias, y, relu ? 1 : 0);
 }
 
-void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, hipStream_t st) {
+void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                   hipStream_t st) {
+  if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st);
   const int M = s.N * s.H * s.W;
   const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
   conv_bwd_data_kernel<<<blocks, 256, 0, st>>>(s, dy, w, dx);
 }
 
 int conv_filter_splits(const ConvShape& s) {
+  if (conv_bwd_filter_tiled_ok(s)) return conv_filter_tiled_splits(s);
   const int Mw = s.R * s.S * s.C;
   const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);
   const int ktiles = (s.N * s.OH * s.OW + BK - 1) / BK;
@@ -526,8 +465,16 @@ int conv_filter_splits(const ConvShape& s) {
   return z;
 }
 
+long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue) {
+  long long n = (long long)conv_filter_splits(s) * s.R * s.S * s.C * s.K;
+  if (conv_fwd_tiled_ok(s)) n = std::max(n, conv_fwd_tiled_ws_floats(s, fwd_epilogue));
+  if (conv_bwd_data_tiled_ok(s)) n = std::max(n, conv_bwd_data_tiled_ws_floats(s));
+  return n;
+}
+
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* part, float* dw,
                      hipStream_t st) {
+  if (conv_bwd_filter_tiled_ok(s)) return conv_bwd_filter_tiled(s, x, dy, part, dw, st);
   const int Mw = s.R * s.S * s.C;
   const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);
   const int ktiles = (s.N * s.OH * s.OW + BK - 1) / BK;
@@ -540,7 +487,10 @@ void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float*
 }
 
 void colsum2(const float* a, const float* b, long long rows, int C, float* s1, float* s2, int mode,
-             hipStream_t st) {
+             float* ws, hipStream_t st) {
+  // deterministic vectorised two-pass reduction (bn.hip) when the channel
+  // count allows it; the atomic kernel above covers thin odd layers (LeNet)
+  if (ws && chan_reduce_ok(C)) return chan_reduce(a, b, rows, C, s1, s2, mode, ws, st);
   (void)hipMemsetAsync(s1, 0, C * sizeof(float), st);
   (void)hipMemsetAsync(s2, 0, C * sizeof(float), st);
   int gy = (int)((rows + 511) / 512);
@@ -548,26 +498,6 @@ void colsum2(const float* a, const float* b, long long rows, int C, float* s1, f
   const int rpb = (int)((rows + gy - 1) / gy);
   dim3 grid((C + 63) / 64, gy);
   colsum2_kernel<<<grid, 256, 0, st>>>(a, b, (int)rows, C, rpb, s1, s2, mode);
-}
-
-void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
-            const float* res, float* y, float* mean, float* rstd, float* sum, float* sumsq,
-            float eps, bool relu, bool training, const float* rmean, const float* rvar,
-            hipStream_t st) {
-  if (training) colsum2(x, nullptr, rows, C, sum, sumsq, 0, st);
-  bn_apply_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, sum, sumsq, g, b, res, y, mean, rstd, rows,
-                                                     C, eps, relu ? 1 : 0, training ? 1 : 0,
-                                                     rmean, rvar);
-}
-
-void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
-            const float* g, long long rows, int C, bool relu, float* dym, float* xh, float* dg,
-            float* db, float* dx, float* dres, hipStream_t st) {
-  bn_bwd_prep_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, dy, y, mean, rstd, dym, xh, rows, C,
-                                                        relu ? 1 : 0);
-  colsum2(dym, xh, rows, C, db, dg, 1, st);  // db = sum dy', dg = sum dy'*xhat
-  bn_bwd_apply_kernel<<<grid1d(rows * C), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx, dres,
-                                                         rows, C, relu ? 1 : 0);
 }
 
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st) {

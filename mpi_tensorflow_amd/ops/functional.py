@@ -50,7 +50,7 @@ class _ConvFn(torch.autograd.Function):
         C = native()
         x = x.contiguous()
         y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
-        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, stream_handle())
+        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), stream_handle())
         ctx.save_for_backward(x, w, y)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
@@ -70,17 +70,19 @@ class _ConvFn(torch.autograd.Function):
         C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s)
         if ctx.has_b:
             scratch = torch.empty(sh.K, device=dy.device, dtype=dy.dtype)
-            C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0, s)
+            C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0,
+                          ptr(ctx.ws), s)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
-            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), s)
+            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s)
         return dx, None, None, None, None, None, None, None
 
 
 class ConvWorkspace:
-    """Split-K slab workspace for the filter-gradient kernels (grown lazily;
-    sized once before graph capture)."""
+    """Split-K slab / reduction-partials workspace shared by the conv and BN
+    kernels of all layers (they run in stream order).  Grown lazily, so the
+    eager warm-up steps before graph capture size it once."""
 
     def __init__(self):
         self.t: Optional[torch.Tensor] = None
@@ -102,7 +104,8 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
     if x.is_cuda:
         C = native()
         sh = C.ops.ConvShape(N, H, W, Cin, K, R, S, stride, pad)
-        nws = C.ops.conv_filter_splits(sh) * R * S * Cin * K
+        nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
+                  C.ops.chan_reduce_ws_floats(N * sh.OH * sh.OW, K), 4)
         ws = _WS.get(nws, x.device)
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
                              None if b is None else b.grad_view, ws)
@@ -131,22 +134,16 @@ class _BNFn(torch.autograd.Function):
         x = x.contiguous()
         Cc = x.shape[-1]
         rows = x.numel() // Cc
-        s = stream_handle()
         y = torch.empty_like(x)
         mean = torch.empty(Cc, device=x.device)
         rstd = torch.empty(Cc, device=x.device)
-        s1 = torch.empty(Cc, device=x.device)
-        s2 = torch.empty(Cc, device=x.device)
+        ws = _WS.get(max(C.ops.chan_reduce_ws_floats(rows, Cc), 4), x.device)
+        # batch statistics, running-stat update and the fused apply, on device
         C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(y), ptr(mean), ptr(rstd),
-                     ptr(s1), ptr(s2), eps, relu, training, ptr(rmean), ptr(rvar), s)
-        if training:  # running statistics for eval (unbiased var, as torch)
-            with torch.no_grad():
-                bm = s1 / rows
-                var = (s2 / rows - bm * bm).clamp_min(0) * (rows / max(rows - 1, 1))
-                rmean.mul_(1 - momentum).add_(momentum * bm)
-                rvar.mul_(1 - momentum).add_(momentum * var)
+                     ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle())
         ctx.save_for_backward(x, y, mean, rstd, g)
         ctx.relu, ctx.gg, ctx.gb, ctx.has_res = relu, gg, gb, res is not None
+        ctx.ws = ws
         return y
 
     @staticmethod
@@ -156,13 +153,10 @@ class _BNFn(torch.autograd.Function):
         dy = dy.contiguous()
         Cc = x.shape[-1]
         rows = x.numel() // Cc
-        dym = torch.empty_like(dy)
-        xh = torch.empty_like(dy)
         dx = torch.empty_like(dy)
         dres = torch.empty_like(dy) if ctx.has_res else None
         C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
-                     ptr(dym), ptr(xh), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres),
-                     stream_handle())
+                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres), stream_handle())
         return dx, None, None, dres, None, None, None, None, None, None, None, None
 
 
@@ -179,8 +173,8 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
         y = torch.empty_like(x)
         Cc = x.shape[-1]
         C.ops.bn_fwd(ptr(x.contiguous()), x.numel() // Cc, Cc, ptr(g.value), ptr(b.value),
-                     ptr(res), ptr(y), 0, 0, 0, 0, eps, relu, False, ptr(rmean), ptr(rvar),
-                     stream_handle())
+                     ptr(res), ptr(y), 0, 0, 0, eps, momentum, relu, False, ptr(rmean),
+                     ptr(rvar), stream_handle())
         return y
     xn = x.permute(0, 3, 1, 2)
     y = F.batch_norm(xn, rmean, rvar, g.value, b.value, training, momentum, eps).permute(0, 2, 3, 1)

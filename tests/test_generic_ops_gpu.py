@@ -27,6 +27,14 @@ def _param(t):
     (2, 16, 16, 3, 64, 7, 2, 3, False, False),
     (3, 8, 8, 16, 32, 1, 2, 0, False, False),
     (5, 1, 1, 40, 70, 1, 1, 0, True, True),  # linear as a 1x1 conv
+    # LDS-tiled family (conv_tiled.hip): ResNet-18 layer shapes, small batch
+    (2, 14, 14, 64, 64, 3, 1, 1, False, False),
+    (2, 14, 14, 64, 128, 3, 2, 1, False, False),  # stride-2 dgrad phases
+    (2, 13, 13, 64, 128, 1, 2, 0, False, False),  # 1x1 s2 downsample, odd size
+    (3, 7, 7, 256, 96, 3, 1, 1, True, True),
+    (2, 9, 9, 32, 36, 5, 2, 2, False, True),
+    (8, 1, 1, 512, 12, 1, 1, 0, False, True),     # FC 512 -> 12
+    (10, 56, 56, 64, 64, 3, 1, 1, False, False),  # M >= 32768: 128-row tiles
 ])
 def test_conv_fwd_bwd(cuda_dev, N, H, W, Cin, K, R, stride, pad, relu, bias):
     g = torch.Generator().manual_seed(0)
