@@ -43,6 +43,24 @@ def _empty(shape, like):
     return torch.empty(shape, dtype=like.dtype, device=like.device)
 
 
+# Gradient-ready hook: when set (parallel/overlap.py BucketedAllReduce), the
+# backward of every op reports each parameter-gradient view it has finished
+# writing, so gradient buckets can be all-reduced while backward continues.
+_GRAD_HOOK = None
+
+
+def set_grad_hook(fn) -> None:
+    global _GRAD_HOOK
+    _GRAD_HOOK = fn
+
+
+def _grad_done(*views) -> None:
+    if _GRAD_HOOK is not None:
+        for v in views:
+            if v is not None:
+                _GRAD_HOOK(v)
+
+
 # ------------------------------------------------------------------- conv --
 class _ConvFn(torch.autograd.Function):
     @staticmethod
@@ -72,6 +90,7 @@ class _ConvFn(torch.autograd.Function):
             scratch = torch.empty(sh.K, device=dy.device, dtype=dy.dtype)
             C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0,
                           ptr(ctx.ws), s)
+        _grad_done(ctx.gw, ctx.gb if ctx.has_b else None)
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
@@ -157,6 +176,7 @@ class _BNFn(torch.autograd.Function):
         dres = torch.empty_like(dy) if ctx.has_res else None
         C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
                      ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres), stream_handle())
+        _grad_done(ctx.gg, ctx.gb)
         return dx, None, None, dres, None, None, None, None, None, None, None, None
 
 

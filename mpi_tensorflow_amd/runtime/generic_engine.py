@@ -7,8 +7,10 @@ per-step gradient all-reduce of the flat grad buffer.
 
 On GPU one training step is: batch gather from the device-resident shard at
 the device step offset -> forward/backward through the native NHWC kernels
-(parameter grads land directly in the flat grad buffer) -> RCCL all-reduce
-(world > 1) -> device LR -> flat SGD kernel (which bumps the device step).
+(parameter grads land directly in the flat grad buffer; with world > 1 each
+gradient bucket is all-reduced over RCCL on a comm stream as soon as backward
+has completed it, parallel/overlap.py) -> device LR -> flat SGD kernel (which
+bumps the device step).
 Nothing in the step touches the host, so G steps are captured into one
 hipGraph (torch.cuda.CUDAGraph) after a short eager warm-up and replayed.
 On CPU the same model runs through the PyTorch oracle ops.
@@ -26,6 +28,7 @@ from ..models.generic import make_model
 from ..ops import functional as Fn
 from ..ops import native, ptr, stream_handle
 from ..parallel.comm import DeviceComm
+from ..parallel.overlap import BucketedAllReduce
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
@@ -35,7 +38,7 @@ class GenericEngine:
 
     def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
                  device: torch.device, rank: int = 0, world: int = 1,
-                 comm: Optional[DeviceComm] = None):
+                 comm: Optional[DeviceComm] = None, force_sync: bool = False):
         self.cfg, self.device, self.rank, self.world, self.comm = cfg, device, rank, world, comm
         if cfg.dtype != "fp32":
             raise NotImplementedError(f"dtype {cfg.dtype} is not implemented for {cfg.model} yet")
@@ -58,13 +61,22 @@ class GenericEngine:
         self.train_y = torch.from_numpy(np.asarray(train_y).astype(np.int32)).to(device)
         self.step = 0
         self.grad_sync = cfg.sync == "grad" and world > 1 and comm is not None
+        if force_sync and comm is not None:  # exercise the collective path at world 1
+            self.grad_sync = True
         self.on_gpu = device.type == "cuda"
         self.use_graph = cfg.graph and self.on_gpu
         self.graph_steps = max(1, cfg.graph_steps)
         self._graphs = {}
         self.loss_buf = torch.zeros((), device=device)
+        self.bucketer = None
         if self.on_gpu:
             self._C = native()
+            if self.grad_sync:
+                if comm.native_handle is None:
+                    raise RuntimeError("GPU grad sync needs the native RCCL communicator")
+                self.bucketer = BucketedAllReduce(self.layout, self.grads, comm, device)
+                comm.all_reduce_(self.grads)  # connection setup outside any capture
+                torch.cuda.synchronize(device)
             h, w, c = train_x.shape[1:]
             self.xb = torch.empty(self.B, h, w, c, device=device)
             self.yb = torch.empty(self.B, dtype=torch.int32, device=device)
@@ -96,12 +108,20 @@ class GenericEngine:
                             self.B, row, ptr(self.xb), ptr(self.yb), s)
         logits = self.model.forward(self.P, self.bn, self.xb, True)
         loss = Fn.cross_entropy(logits, self.yb)
-        loss.backward()
-        self.loss_buf.copy_(loss.detach())
         gscale = 1.0
-        if self.grad_sync:
-            self.comm.all_reduce_(self.grads)
+        if self.bucketer is not None:
+            # buckets all-reduce on the comm stream as backward completes them
+            self.bucketer.begin()
+            Fn.set_grad_hook(self.bucketer.grad_ready)
+            try:
+                loss.backward()
+            finally:
+                Fn.set_grad_hook(None)
+            self.bucketer.finish()
             gscale = 1.0 / self.world
+        else:
+            loss.backward()
+        self.loss_buf.copy_(loss.detach())
         C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
                             self.cfg.lr_decay, ptr(self.lr_dev), s)
         C_.optim.sgd_momentum(ptr(self.params), ptr(self.grads), ptr(self.mom), self.layout.total, 0,
