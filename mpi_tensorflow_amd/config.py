@@ -102,6 +102,11 @@ class TrainConfig:
     resume: Optional[str] = None
     metrics_jsonl: Optional[str] = None
     quiet: bool = False
+    # robustness: process-group / collective timeout (a dead rank turns into
+    # an error instead of a hang) and a cross-replica consistency probe at
+    # every eval event in grad-sync mode (replicas must stay identical)
+    collective_timeout_s: float = 600.0
+    check_replicas: bool = False
     # compat
     reference_quirks: bool = False
 
@@ -179,6 +184,10 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--resume", default=None)
     p.add_argument("--metrics-jsonl", default=None)
     p.add_argument("--quiet", action="store_true")
+    p.add_argument("--collective-timeout-s", type=float, default=d.collective_timeout_s,
+                   help="process-group / collective timeout (seconds)")
+    p.add_argument("--check-replicas", action="store_true",
+                   help="verify at every eval that all ranks hold identical weights (grad sync)")
     p.add_argument("--reference-quirks", action="store_true",
                    help="reproduce mpipy.py quirks Q5/Q8/Q9/Q11/Q14")
     return p

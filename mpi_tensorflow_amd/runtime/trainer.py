@@ -28,11 +28,12 @@ import torch
 from .. import config as C
 from ..parallel import dist as D
 from ..parallel.comm import make_comm
-from ..parallel.sync import average_params, average_params_root_only
+from ..parallel.sync import average_params, average_params_root_only, replica_checksum
 from ..utils import checkpoint as ckpt_mod
 from ..utils.data import (data_exist_here, load_mnist_shard, local_train_rows, mnist_files_present,
                           steps_per_run, synthetic_image_shard)
 from ..utils.logging import MetricsWriter, emit, progress_line, start_line
+from ..utils.profiling import SegmentTimer
 
 
 @dataclasses.dataclass
@@ -50,6 +51,7 @@ class RunSummary:
     final_test_error_global: float
     final_loss: float
     final_lr: float
+    device_step_ms: float
     engine: str
     comm: str
     synthetic: bool
@@ -62,7 +64,7 @@ class Trainer:
     def __init__(self, cfg: C.TrainConfig, di: Optional[D.DistInfo] = None):
         self.cfg = cfg.validate()
         self.device = D.resolve_device(cfg.device)
-        self.di = di or D.init(str(self.device))
+        self.di = di or D.init(str(self.device), timeout_s=cfg.collective_timeout_s)
         self.rank, self.world = self.di.rank, self.di.world
         self._prepare_data()
         self.comm = make_comm(self.di, self.device) if self.world > 1 else None
@@ -143,6 +145,17 @@ class Trainer:
         d = self.cfg.eval_dropout if dropout is None else dropout
         return self.engine.evaluate(self.shard.test_x, self.shard.test_y, dropout=d)
 
+    def check_replicas(self, step: int) -> None:
+        """All ranks must hold bit-identical weights under per-step gradient
+        all-reduce; a mismatch means a lost / corrupted collective."""
+        if self.world <= 1 or self.cfg.sync != "grad":
+            return
+        c = replica_checksum(self.engine.params)
+        hi = D.allreduce_max_host(c)
+        lo = -D.allreduce_max_host(-c)
+        if hi != lo:
+            raise RuntimeError(f"replicas diverged at step {step}: checksum range [{lo}, {hi}]")
+
     def run(self) -> RunSummary:
         cfg, eng = self.cfg, self.engine
         emit(start_line(self.rank), cfg.quiet)
@@ -151,6 +164,7 @@ class Trainer:
         train_t = 0.0
         eval_t = 0.0
         trained = 0
+        timer = SegmentTimer(self.device)
         while s < steps:
             nxt = s
             while nxt < steps - 1 and not self._event(nxt):
@@ -158,8 +172,11 @@ class Trainer:
             k = nxt - s + 1
             self._sync()
             t0 = time.perf_counter()
+            timer.start()
             eng.train(k)
+            timer.stop(k)
             self._sync()
+            timer.collect()
             train_t += time.perf_counter() - t0
             trained += k
             s += k
@@ -175,7 +192,10 @@ class Trainer:
                     emit(progress_line(self.rank, last, err), cfg.quiet)
                     self.metrics.write(step=last, test_error=err, loss=eng.loss_value(),
                                        lr=eng.lr(last), train_seconds=train_t,
+                                       device_step_ms=timer.step_ms(),
                                        images_per_sec=trained * cfg.batch_size / max(train_t, 1e-9))
+                if cfg.check_replicas:
+                    self.check_replicas(last)
             if cfg.sync == "param_avg" and self.world > 1 and last % cfg.sync_every == 0:
                 t2 = time.perf_counter()
                 if cfg.root_only_average:
@@ -186,6 +206,8 @@ class Trainer:
                 train_t += time.perf_counter() - t2
             if cfg.ckpt and cfg.ckpt_every and last % cfg.ckpt_every == 0:
                 self.save_checkpoint(cfg.ckpt)
+        if cfg.check_replicas:
+            self.check_replicas(s - 1)
         t1 = time.perf_counter()
         final_err = self.evaluate()
         eval_t += time.perf_counter() - t1
@@ -200,7 +222,8 @@ class Trainer:
             images_per_sec_local=images / max(train_t, 1e-9),
             images_per_sec_global=images * self.world / max(train_t_max, 1e-9),
             final_test_error_local=final_err, final_test_error_global=100.0 * wrong_g / max(n_g, 1),
-            final_loss=eng.loss_value(), final_lr=eng.lr(max(0, s - 1)), engine=eng.kind,
+            final_loss=eng.loss_value(), final_lr=eng.lr(max(0, s - 1)),
+            device_step_ms=timer.step_ms(), engine=eng.kind,
             comm=getattr(self.comm, "kind", "none"), synthetic=self.shard.synthetic)
         self.metrics.write(final=True, **summary.as_dict())
         if cfg.ckpt:

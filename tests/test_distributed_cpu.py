@@ -167,3 +167,19 @@ def test_bench_two_ranks_cpu():
         assert k in j
     assert j["n_gpus"] == 2 and j["steps"] == 3 and j["config"]["global_batch"] == 128
     assert j["config"]["parallelism"] == "dp2" and j["value"] > 0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("model", ["mnist_cnn", "lenet5"])
+def test_mpipy_torchrun_grad_sync_replicas_identical(tmp_path, model):
+    """Per-step gradient all-reduce over gloo: --check-replicas compares the
+    ranks' weight checksums at every eval event and at the end (a mismatch
+    raises); device_step_ms is reported."""
+    port = _free_port()
+    out = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                "--master-addr", "127.0.0.1", "--master-port", str(port), "mpipy.py", "--device",
+                "cpu", "--model", model, "--max-steps", "41", "--eval-every", "20",
+                "--check-replicas", "--collective-timeout-s", "120"])
+    summ = json.loads([l for l in out.splitlines() if l.startswith('{"summary"')][-1])["summary"]
+    assert summ["world"] == 2 and summ["steps"] == 41 and summ["model"] == model
+    assert summ["device_step_ms"] > 0
