@@ -17,14 +17,15 @@ MnistExecutor::MnistExecutor(const MnistPtrs& p) : p_(p) {
     throw std::runtime_error("MnistExecutor: batch must be a positive multiple of 32");
   if (p_.n_local <= p_.batch)
     throw std::runtime_error("MnistExecutor: local shard must exceed the batch");
-  if (p_.total % 4 != 0 || p_.l2_end % 4 != 0)
-    throw std::runtime_error("MnistExecutor: flat buffer sizes must be multiples of 4");
-  for (hipEvent_t* e : {&ev_head_, &ev_dx_, &ev_dw_, &ev_filt_, &ev_fin_, &ev_done_})
+  if (p_.total % 4 != 0 || p_.l2_end % 4 != 0 || p_.bucket1 % 4 != 0 || p_.l2_end > p_.bucket1)
+    throw std::runtime_error(
+        "MnistExecutor: flat segments must be multiples of 4 floats with the L2 prefix in bucket 1");
+  for (hipEvent_t* e : {&ev_dw_, &ev_b1_, &ev_fin_, &ev_done_})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
 MnistExecutor::~MnistExecutor() {
-  for (hipEvent_t e : {ev_head_, ev_dx_, ev_dw_, ev_filt_, ev_fin_, ev_done_})
+  for (hipEvent_t e : {ev_dw_, ev_b1_, ev_fin_, ev_done_})
     if (e) (void)hipEventDestroy(e);
 }
 
@@ -117,32 +118,47 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
 
 void MnistExecutor::forward_backward(hipStream_t s) { enqueue_fwd_bwd(s); }
 
-void MnistExecutor::sgd(hipStream_t s, float gscale) {
+void MnistExecutor::sgd(hipStream_t s, float gscale) { sgd_range(s, 0, p_.total, gscale, true); }
+
+// momentum SGD over flat floats [lo, hi) (lo, hi multiples of 4); the L2
+// prefix [0, l2_end) is clipped to the range; bump_step increments the
+// device step once (the last segment of a step)
+void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float gscale,
+                              bool bump_step) {
   const MnistPtrs& p = p_;
-  optim::launch_sgd_momentum(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom), p.total,
-                             p.l2_end, p.l2, p.momentum, gscale, P<const float>(p.lr), 0.f,
-                             P<long long>(p.step), s);
+  const long long l2 = p.l2_end > lo ? (p.l2_end < hi ? p.l2_end : hi) - lo : 0;
+  optim::launch_sgd_momentum(P<float>(p.params) + lo, P<const float>(p.grads) + lo,
+                             P<float>(p.mom) + lo, hi - lo, l2, p.l2, p.momentum, gscale,
+                             P<const float>(p.lr), 0.f,
+                             bump_step ? P<long long>(p.step) : nullptr, s);
 }
 
 void MnistExecutor::train_step(hipStream_t s, RcclComm* comm, hipStream_t cs) {
   const MnistPtrs& p = p_;
   float* G = P<float>(p.grads);
   enqueue_fwd_bwd(s);
-  const bool sync = comm != nullptr;  // size-1 comms are allowed (tests the capture path)
-  if (sync) {
-    // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1-dW is done; it
-    // overlaps the conv backward still running on the compute streams
-    HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
-    comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
-    // bucket 2 (conv grads) after the slab reduction, same ordered stream
-    HIP_CHECK(hipEventRecord(ev_fin_, s));
-    HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
-    comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
-                     ncclSum, cs);
-    HIP_CHECK(hipEventRecord(ev_done_, cs));
-    HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
+    sgd(s, 1.0f);
+    return;
   }
-  sgd(s, sync ? 1.0f / (float)comm->size() : 1.0f);
+  // size-1 comms are allowed (they exercise the capture path on one GPU)
+  const float gscale = 1.0f / (float)comm->size();
+  // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1 backward is done;
+  // it overlaps the conv backward still running on the compute stream
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
+  comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
+  HIP_CHECK(hipEventRecord(ev_b1_, cs));
+  // bucket 2 (conv grads) after the slab reduction, same ordered stream
+  HIP_CHECK(hipEventRecord(ev_fin_, s));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
+  comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
+                   ncclSum, cs);
+  HIP_CHECK(hipEventRecord(ev_done_, cs));
+  // FC update while bucket 2 is in flight, then the conv update
+  HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
+  sgd_range(s, 0, p.bucket1, gscale, false);
+  HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  sgd_range(s, p.bucket1, p.total, gscale, true);
 }
 
 void MnistExecutor::eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int M,

@@ -16,7 +16,9 @@
 //              backward kernel has written them, overlapping the conv
 //              backward kernels on the compute stream;
 //   bucket 2 = conv params, after the final slab reduction.
-// The SGD kernel waits for both (event join) and divides by world size.
+// The SGD runs in two parts: the FC segment (97 % of the update traffic)
+// as soon as bucket 1 is reduced - overlapping bucket 2's all-reduce - and
+// the conv segment after bucket 2; both divide by the world size.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -76,6 +78,8 @@ class MnistExecutor {
   void enqueue_fwd_bwd(hipStream_t s);
   void enqueue_fwd_bwd_bf16(hipStream_t s);
   MnistPtrs p_;
-  hipEvent_t ev_head_ = nullptr, ev_dx_ = nullptr, ev_dw_ = nullptr, ev_filt_ = nullptr,
-             ev_fin_ = nullptr, ev_done_ = nullptr;
+  void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
+  // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;
+  // ev_fin_: conv grads final (bucket 2 may start); ev_done_: bucket 2 reduced
+  hipEvent_t ev_dw_ = nullptr, ev_b1_ = nullptr, ev_fin_ = nullptr, ev_done_ = nullptr;
 };

@@ -149,9 +149,16 @@ class GenericEngine:
         g = self._graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(n):
-                    self._step_gpu()
+            try:
+                with torch.cuda.graph(g):
+                    for _ in range(n):
+                        self._step_gpu()
+            except RuntimeError as e:  # keep training eagerly rather than fail the run
+                print(f"[rank {self.rank}] hipGraph capture failed ({e}); using eager launches",
+                      flush=True)
+                self.use_graph = False
+                torch.cuda.synchronize(self.device)
+                return None
             self._graphs[n] = g
         return g
 
@@ -184,10 +191,12 @@ class GenericEngine:
         else:
             G = self.graph_steps
             full, rem = divmod(left, G)
-            if full:
-                g = self._graph(G)
+            g = self._graph(G) if full else None
+            if g is not None:
                 for _ in range(full):
                     g.replay()
+            else:
+                rem = left
             for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
                 self._step_gpu()
         self.step += k

@@ -245,33 +245,46 @@ class NativeMnistEngine(MnistEngineBase):
         cs = stream_handle(self.comm_stream) if self.comm_stream is not None else 0
         self.exe.train_step(stream_handle(), self._native_comm, cs)
 
-    def _graph(self, n: int) -> torch.cuda.CUDAGraph:
+    def _graph(self, n: int) -> Optional[torch.cuda.CUDAGraph]:
         g = self._graphs.get(n)
         if g is None:
             if self.comm_stream is not None:
                 self.comm_stream.wait_stream(torch.cuda.current_stream())
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(n):
-                    self._launch_one()
+            try:
+                with torch.cuda.graph(g):
+                    for _ in range(n):
+                        self._launch_one()
+            except RuntimeError as e:
+                # e.g. a collective library build that cannot be captured:
+                # keep training with eager launches instead of failing the run
+                print(f"[rank {self.rank}] hipGraph capture failed ({e}); using eager launches",
+                      flush=True)
+                self.use_graph = False
+                torch.cuda.synchronize(self.device)
+                return None
             self._graphs[n] = g
         return g
 
     def train(self, k: int) -> None:
         if k <= 0:
             return
-        if not self.use_graph:
-            for _ in range(k):
-                self._launch_one()
-        else:
+        done = 0
+        if self.use_graph:
             G = self.graph_steps
             full, rem = divmod(k, G)
-            if full:
-                g = self._graph(G)
+            g = self._graph(G) if full else None
+            if g is not None:
                 for _ in range(full):
                     g.replay()
-            if rem:
-                self._graph(rem).replay()
+                done = full * G
+            if rem and self.use_graph:
+                g = self._graph(rem)
+                if g is not None:
+                    g.replay()
+                    done += rem
+        for _ in range(k - done):  # eager (no graphs, or capture unavailable)
+            self._launch_one()
         self.step += k
 
     def capture(self, k: int) -> None:
