@@ -87,23 +87,23 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("fc1_bwd", [](uintptr_t a2, uintptr_t idx2, uintptr_t dh, uintptr_t hd, uintptr_t dlog,
                       uintptr_t w1, int batch, uintptr_t g_w3, uintptr_t g_b3, uintptr_t g_w4,
-                      uintptr_t g_b4, uintptr_t dy2, uintptr_t s) {
+                      uintptr_t g_b4, uintptr_t dy2, uintptr_t dy2t, uintptr_t s) {
     mnist::launch_fc1_bwd(P<const float>(a2), P<const uint8_t>(idx2), P<const float>(dh),
                           P<const float>(hd), P<const float>(dlog), P<const float>(w1), batch,
                           P<float>(g_w3), P<float>(g_b3), P<float>(g_w4), P<float>(g_b4),
-                          P<float>(dy2), S(s));
-    check_launch();
-  });
-  k.def("conv2_bwd", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
-                        uintptr_t part2, uintptr_t s) {
-    mnist::launch_conv2_bwd(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,
-                            P<float>(da1m), P<float>(part2), S(s));
+                          P<float>(dy2), P<float>(dy2t), S(s));
     check_launch();
   });
   k.def("conv2_bwd_data", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
                              uintptr_t s) {
     mnist::launch_conv2_bwd_data(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,
                                  P<float>(da1m), S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd_data_l2", [](uintptr_t dy2t, uintptr_t w2t, uintptr_t a1, int batch,
+                                uintptr_t da1m, uintptr_t s) {
+    mnist::launch_conv2_bwd_data_l2(P<const float>(dy2t), P<const float>(w2t), P<const float>(a1),
+                                    batch, P<float>(da1m), S(s));
     check_launch();
   });
   k.def("conv2_bwd_filter", [](uintptr_t a1, uintptr_t dy2, int batch, uintptr_t part2, uintptr_t s) {

@@ -21,6 +21,8 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 // row length (elements) of the channel-major zero-padded bf16 activation
 // images of the bf16 MNIST engine ([n][C][rows][MNIST16_T_LD])
 #define MNIST16_T_LD 24
+// ... and of the fp32 engine's channel-major zero-padded dY2 image ([n][64][18][MNIST32_T_LD])
+#define MNIST32_T_LD 20
 
 #define HIP_CHECK(expr)                                                              \
   do {                                                                               \

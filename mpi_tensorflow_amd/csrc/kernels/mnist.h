@@ -26,17 +26,22 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           uint16_t* dht16 = nullptr);
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
                          int M, float* logits, int* errors, hipStream_t s);
+// dY2 as NHWC dy2 [B][14][14][64] and channel-major zero-bordered dy2t
+// [B][64][18][MNIST32_T_LD]
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
-                    float* g_w4, float* g_b4, float* dy2, hipStream_t s);
+                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s);
 int conv2_filter_splits(int batch);
 void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
                            float* da1m, hipStream_t s);
 void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
                              hipStream_t s);
+// L2-direct bwd-data (the one the executor uses): dy2t from launch_fc1_bwd,
+// w2t from launch_conv2_fwd; batch % 8 == 0
+void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
+                              float* da1m, hipStream_t s);
 
-void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
-                      float* part2, hipStream_t s);
+
 int conv1_filter_blocks(int batch);
 void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);

@@ -12,9 +12,10 @@
 //   fc1_bwd                B1-B4  roles: dW1 (=a2^T dh), dX (=dh W1^T with the
 //                                 pool2/ReLU2 backward scatter fused), dW2/db
 //   conv2_fwd_v3           F4-F6  conv2 from an LDS halo tile (+W2 transpose)
-//   conv2_bwd              B5-B6  roles: bwd-data from an LDS halo tile (ReLU1
-//                                 mask fused), bwd-filter with L2-direct
-//                                 operands (+db2 on the centre tap)
+//   conv2_bwd_data_l2      B6     L2-direct bwd-data over the channel-major
+//                                 dY2 image (ReLU1 mask fused)
+//   conv2_bwd_filter       B5     bwd-filter with L2-direct NHWC operands
+//                                 (+db2 on the centre tap)
 //   conv1_bwd_filter       B7     sparse VALU filter grad through pool1 argmax
 //   grad_finalize          B2     deterministic slab reduction
 //   fc_head_eval           E1-E2  logits, argmax, on-device error count
@@ -394,7 +395,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
     const float* __restrict__ hd, const float* __restrict__ dlog, const float* __restrict__ w1,
     int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
-    float* __restrict__ g_b4, float* __restrict__ dy2) {
+    float* __restrict__ g_b4, float* __restrict__ dy2, float* __restrict__ dy2t) {
+  // dy2: NHWC [n][14][14][64] (filter-grad operand); dy2t: channel-major,
+  // zero-bordered [n][64][18][MNIST32_T_LD] (bwd-data operand)
   using CDX = gemm::Cfg<1, 1, FC1BWD_DX_WK, FC1BWD_BK, true, false>;
   using CDW = gemm::Cfg<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_DW_BK, false, true>;
   constexpr int S1 = CDX::SMEM_FLOATS, S2 = CDW::SMEM_FLOATS, S3 = 4 * (NCLS + 1) * 64;
@@ -424,7 +427,9 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
-        dy2[((n * 14 + y) * 14 + x) * 64 + co] = (d == q) ? g : 0.f;
+        const float v = (d == q) ? g : 0.f;
+        dy2[((n * 14 + y) * 14 + x) * 64 + co] = v;
+        dy2t[((size_t)(n * 64 + co) * 18 + y + 2) * MNIST32_T_LD + x + 2] = v;
       }
     }
     return;
@@ -789,6 +794,81 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   }
 }
 
+// conv2 bwd-data, L2-direct: every wave owns a 32 (pixels) x 32 (ci) tile over
+// half of K (co 0-31 / 32-63, the two halves of a wave pair summed through
+// LDS) and streams its fragments straight from L2 into a 16-deep register
+// ring.  M covers the batch in (n, y, x) order, so no tile is padded (the
+// LDS-halo kernel above computes 30 % padding rows).  The A operand comes from
+// dy2t, dY2 stored channel-major with a zero border ([n][co][18][20], written
+// by fc1 backward): the 32 lanes of a half-wave read ~2 runs of consecutive
+// floats of one channel plane per tap, bounds-check free; B = W2T[t][co][ci]
+// (written by the conv2 forward kernel).  Measured 19.6 us vs 24.2 us for the
+// halo kernel at B = 64 (in-graph).  (A K-permuted float4 variant of this
+// structure touches one 128-B line per lane per load and runs slower: for
+// fp32 MFMA the limit is cache lines per MFMA, not load instructions.)
+constexpr int P32_LD = MNIST32_T_LD;
+constexpr int A1T_PLANE = 18 * P32_LD;
+
+template <int D, int NKS, class F>
+__device__ __forceinline__ void kloop32(F&& frag, f32x16& c0, f32x16& c1) {
+  float ra[D], rb[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) frag(d, ra[d], rb[d]);
+#pragma unroll
+  for (int ks = 0; ks < NKS; ks += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (ks + d < NKS) {
+        const float a = ra[d], b = rb[d];
+        if (ks + D + d < NKS) frag(ks + D + d, ra[d], rb[d]);
+        __builtin_amdgcn_sched_barrier(0);
+        if (d & 1)
+          c1 = mfma32x32x2(a, b, c1);
+        else
+          c0 = mfma32x32x2(a, b, c0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void conv2_bwd_data_l2_kernel(const float* __restrict__ dy2t,
+                                                                const float* __restrict__ w2t,
+                                                                const float* __restrict__ a1,
+                                                                int batch,
+                                                                float* __restrict__ da1m) {
+  __shared__ float red[2][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int mtiles = batch * 49 / 8;
+  const int mt_raw = xcd_remap(blockIdx.x, gridDim.x) * 2 + (wave & 1), kk = wave >> 1;
+  const int mt = min(mt_raw, mtiles - 1);
+  const int m = mt * 32 + r, n = m / 196, p = m % 196, y = p / 14, x = p % 14;
+  // padded source pixel of tap (kh, kw): (y + 4 - kh, x + 4 - kw)
+  const float* ap = dy2t + ((size_t)(n * 64 + 32 * kk + h) * 18 + y + 4) * P32_LD + x + 4;
+  const float* bp = w2t + (32 * kk + h) * 32 + r;
+  f32x16 c0 = zero16(), c1 = zero16();
+  kloop32<16, 400>(
+      [&](int ks, float& a, float& b) {  // tap t, channel pair s
+        const int t = ks >> 4, s2 = 2 * (ks & 15), kh = t / 5, kw = t % 5;
+        a = ap[s2 * A1T_PLANE - kh * P32_LD - kw];
+        b = bp[(t * 64 + s2) * 32];
+      },
+      c0, c1);
+  if (kk == 1) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[wave & 1][k][lane] = c0[k] + c1[k];
+  }
+  __syncthreads();
+  if (kk == 1 || mt_raw >= mtiles) return;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int mm = mt * 32 + mfma32_row(k, lane);
+    const float g = c0[k] + c1[k] + red[wave & 1][k][lane];
+    const size_t o = (size_t)mm * 32 + r;  // (n, y, x, ci) flat
+    da1m[o] = a1[o] > 0.f ? g : 0.f;
+  }
+}
+
 __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const float* __restrict__ a1,
                                                             const float* __restrict__ dy2,
                                                             const float* __restrict__ w2t,
@@ -993,11 +1073,11 @@ void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const
 
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
-                    float* g_w4, float* g_b4, float* dy2, hipStream_t s) {
+                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s) {
   const int n_dx = cdiv(batch, 32) * (FC1_IN / 32);
   const int n_dw = (FC1_IN / (32 * FC1BWD_DW_WM)) * (FC1_OUT / (32 * FC1BWD_DW_WN));
   fc1_bwd_kernel<<<n_dx + n_dw + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
-                                                            g_w3, g_b3, g_w4, g_b4, dy2);
+                                                            g_w3, g_b3, g_w4, g_b4, dy2, dy2t);
 }
 
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
@@ -1007,16 +1087,17 @@ void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, 
   conv2_bwd_data_kernel<<<batch * 4, 256, 0, s>>>(a1, dy2, w2t, da1m);
 }
 
+void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
+                              float* da1m, hipStream_t s) {
+  if (batch % 8 != 0) throw std::runtime_error("conv2_bwd_data_l2: batch % 8 != 0");
+  const int mtiles = batch * 49 / 8;
+  conv2_bwd_data_l2_kernel<<<cdiv(mtiles, 2), 256, 0, s>>>(dy2t, w2t, a1, batch, da1m);
+}
+
 void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
                              hipStream_t s) {
   const int G = conv2_filter_splits(batch);
   conv2_bwd_filter_kernel<<<25 * G, 512, 0, s>>>(batch, a1, dy2, part2, part2 + (size_t)G * 51200);
-}
-
-void launch_conv2_bwd(const float* a1, const float* dy2, const float* w2t, int batch, float* da1m,
-                      float* part2, hipStream_t s) {
-  launch_conv2_bwd_data(a1, dy2, w2t, batch, da1m, s);
-  launch_conv2_bwd_filter(a1, dy2, batch, part2, s);
 }
 
 int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }

@@ -58,10 +58,10 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
                         P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
-                        s);
+                        P<float>(p.dy2t), s);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
-  mnist::launch_conv2_bwd_data(P<const float>(p.a1), P<const float>(p.dy2),
-                               P<const float>(p.w2t), B, P<float>(p.da1m), s);
+  mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
+                                  P<const float>(p.a1), B, P<float>(p.da1m), s);
   mnist::launch_conv2_bwd_filter(P<const float>(p.a1), P<const float>(p.dy2), B,
                                  P<float>(p.part2), s);
   mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,

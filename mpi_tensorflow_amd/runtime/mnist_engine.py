@@ -182,6 +182,8 @@ class NativeMnistEngine(MnistEngineBase):
             hd=torch.empty(B * M.FC1_OUT, **f32), dh=torch.empty(B * M.FC1_OUT, **f32),
             dlog=torch.empty(B * 10, **f32), loss_rows=torch.zeros(B, **f32),
             dy2=torch.empty(B * 14 * 14 * 64, **f32), da1m=torch.empty(B * 14 * 14 * 32, **f32),
+            # channel-major dY2 with a zero border that is never written
+            dy2t=torch.zeros(B * 64 * 18 * 20, **f32),
             part2=torch.empty(k.part2_floats(B), **f32), part1=torch.empty(k.part1_floats(B), **f32),
             w2t=torch.empty(25 * 64 * 32, **f32),
         )

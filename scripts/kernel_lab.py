@@ -44,9 +44,9 @@ def main():
                                            ptr(e.lr_dev), 0, s),
         "fc1_bwd": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]), ptr(b["dlog"]),
                                      W("fc1_weight"), B, G("fc1_weight"), G("fc1_bias"), G("fc2_weight"),
-                                     G("fc2_bias"), ptr(b["dy2"]), s),
-        "conv2_bwd_data": lambda: k.conv2_bwd_data(ptr(b["a1"]), ptr(b["dy2"]), ptr(b["w2t"]), B,
-                                                   ptr(b["da1m"]), s),
+                                     G("fc2_bias"), ptr(b["dy2"]), ptr(b["dy2t"]), s),
+        "conv2_bwd_data": lambda: k.conv2_bwd_data_l2(ptr(b["dy2t"]), ptr(b["w2t"]), ptr(b["a1"]), B,
+                                                      ptr(b["da1m"]), s),
         "conv2_bwd_filter": lambda: k.conv2_bwd_filter(ptr(b["a1"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
         "conv1_bwd_filter": lambda: k.conv1_bwd_filter(ptr(e.train_x), ptr(e.step_dev), e.n_local, B,
                                                        ptr(b["da1m"]), ptr(b["idx1"]), ptr(b["part1"]), s),
