@@ -162,23 +162,28 @@ PYBIND11_MODULE(_C, m) {
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
-                       bool relu, uintptr_t ws, uintptr_t st) {
+                       bool relu, uintptr_t ws, uintptr_t st, bool bf16) {
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
-                   P<float>(ws), S(st));
+                   P<float>(ws), S(st), bf16);
     check_launch();
-  });
+  }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
+     py::arg("ws"), py::arg("st"), py::arg("bf16") = false);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
-                            uintptr_t ws, uintptr_t st) {
-    gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st));
+                            uintptr_t ws, uintptr_t st, bool bf16) {
+    gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st),
+                        bf16);
     check_launch();
-  });
+  }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
+     py::arg("bf16") = false);
   g.def("conv_ws_floats", &gops::conv_ws_floats);
   g.def("conv_filter_splits", &gops::conv_filter_splits);
   g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,
-                              uintptr_t dw, uintptr_t st) {
-    gops::conv_bwd_filter(s, P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw), S(st));
+                              uintptr_t dw, uintptr_t st, bool bf16) {
+    gops::conv_bwd_filter(s, P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw),
+                          S(st), bf16);
     check_launch();
-  });
+  }, py::arg("s"), py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("st"),
+     py::arg("bf16") = false);
   g.def("colsum2", [](uintptr_t a, uintptr_t b, long long rows, int C, uintptr_t s1, uintptr_t s2,
                       int mode, uintptr_t ws, uintptr_t st) {
     gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode,

@@ -1,5 +1,6 @@
 // LDS-tiled implicit-GEMM convolutions (NHWC activations, HWIO weights, fp32
-// storage and fp32 MFMA v_mfma_f32_32x32x2_f32) for the channel counts of
+// storage; fp32 MFMA v_mfma_f32_32x32x2_f32 or, with bf16 = true, operands
+// converted to bf16 while staged into LDS and v_mfma_f32_32x32x16_bf16) for the channel counts of
 // ResNet-18 and wide layers in general: forward, backward-data (stride-s
 // phase decomposition) and backward-filter (split-K slabs).
 //
@@ -25,42 +26,112 @@ namespace tiled {
 
 constexpr int BK = 32, PAD = 4, NT = 256;
 
-template <int BM, int BN>
+// Operand precision of the MFMA.  fp32 storage everywhere; BF16 converts the
+// tiles to bf16 as they are staged into LDS and runs v_mfma_f32_32x32x16_bf16
+// (16x the fp32-MFMA rate) with fp32 accumulation.
+enum Prec { F32 = 0, BF16 = 1 };
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+
+// LDS image of one K tile of an operand with ROWS rows (M or N):
+//   F32 : k-major [BK][ROWS + PAD] floats - the 32 lanes of a half-wave read
+//         32 consecutive rows of one k (the fp32 MFMA takes one k per lane)
+//   BF16: row-major [ROWS][BK + 8] bf16 - each lane reads one 16-byte
+//         fragment (8 consecutive k of its row); the 80-byte row stride makes
+//         the ds_read_b128 lane groups conflict-free
+// put_k4 stores 4 consecutive k of one row, put_r4 4 consecutive rows of one k.
+template <int P, int ROWS>
+struct Stage;
+
+template <int ROWS>
+struct Stage<F32, ROWS> {
+  static constexpr int LD = ROWS + PAD;
+  static constexpr int FLOATS = BK * LD;
+  static __device__ __forceinline__ void put_k4(float* T, int row, int k0, float4 v) {
+    T[(k0 + 0) * LD + row] = v.x;
+    T[(k0 + 1) * LD + row] = v.y;
+    T[(k0 + 2) * LD + row] = v.z;
+    T[(k0 + 3) * LD + row] = v.w;
+  }
+  static __device__ __forceinline__ void put_r4(float* T, int row0, int k, float4 v) {
+    *reinterpret_cast<float4*>(T + k * LD + row0) = v;
+  }
+};
+
+template <int ROWS>
+struct Stage<BF16, ROWS> {
+  static constexpr int LDK = BK + 8;  // bf16 elements per row
+  static constexpr int FLOATS = ROWS * LDK / 2;
+  static __device__ __forceinline__ void put_k4(float* T, int row, int k0, float4 v) {
+    const __bf16 h[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    *reinterpret_cast<uint2*>(reinterpret_cast<__bf16*>(T) + row * LDK + k0) =
+        __builtin_bit_cast(uint2, h);
+  }
+  static __device__ __forceinline__ void put_r4(float* T, int row0, int k, float4 v) {
+    __bf16* b = reinterpret_cast<__bf16*>(T) + row0 * LDK + k;
+    b[0] = (__bf16)v.x;
+    b[LDK] = (__bf16)v.y;
+    b[2 * LDK] = (__bf16)v.z;
+    b[3 * LDK] = (__bf16)v.w;
+  }
+};
+
+template <int BM, int BN, int P = F32>
 struct Geo {
   static constexpr int TM = BM / 64, TN = BN / 64;  // MFMA tiles per wave
-  static constexpr int LDA = BM + PAD, LDB = BN + PAD;
-  static constexpr int STAGE = BK * (LDA + LDB);
+  static constexpr int A_FLOATS = Stage<P, BM>::FLOATS;
+  static constexpr int STAGE = A_FLOATS + Stage<P, BN>::FLOATS;
   static constexpr int SMEM = 2 * STAGE;
 };
 
-// One K tile: A[BK][BM] (k-major) and B[BK][BN] from registers to LDS, then
-// the MFMAs of the wave's TMxTN sub-tiles over the tile's BK.
-template <int BM, int BN>
+// The MFMAs of one staged K tile for the wave's TMxTN 32x32 sub-tiles.
+template <int BM, int BN, int P>
 __device__ __forceinline__ void mma_tile(const float* As, const float* Bs, int wm, int wn,
                                          int lane, f32x16 (&acc)[BM / 64][BN / 64]) {
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   const int r = lane & 31, h = lane >> 5;
+  if constexpr (P == F32) {
+    constexpr int LDA = Stage<F32, BM>::LD, LDB = Stage<F32, BN>::LD;
 #pragma unroll
-  for (int ks = 0; ks < BK / 2; ++ks) {
-    float a[G::TM], b[G::TN];
+    for (int ks = 0; ks < BK / 2; ++ks) {
+      float a[G::TM], b[G::TN];
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i) a[i] = As[(2 * ks + h) * G::LDA + wm * (BM / 2) + 32 * i + r];
+      for (int i = 0; i < G::TM; ++i) a[i] = As[(2 * ks + h) * LDA + wm * (BM / 2) + 32 * i + r];
 #pragma unroll
-    for (int j = 0; j < G::TN; ++j) b[j] = Bs[(2 * ks + h) * G::LDB + wn * (BN / 2) + 32 * j + r];
+      for (int j = 0; j < G::TN; ++j) b[j] = Bs[(2 * ks + h) * LDB + wn * (BN / 2) + 32 * j + r];
 #pragma unroll
-    for (int i = 0; i < G::TM; ++i)
+      for (int i = 0; i < G::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < G::TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
+        for (int j = 0; j < G::TN; ++j) acc[i][j] = mfma32x32x2(a[i], b[j], acc[i][j]);
+    }
+  } else {
+    constexpr int LDK = Stage<BF16, BM>::LDK;
+    const __bf16* A = reinterpret_cast<const __bf16*>(As);
+    const __bf16* B = reinterpret_cast<const __bf16*>(Bs);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bfx8 a[G::TM], b[G::TN];
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+        a[i] = *reinterpret_cast<const bfx8*>(A + (wm * (BM / 2) + 32 * i + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+      for (int j = 0; j < G::TN; ++j)
+        b[j] = *reinterpret_cast<const bfx8*>(B + (wn * (BN / 2) + 32 * j + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+      for (int i = 0; i < G::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < G::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
   }
 }
 
 // Double-buffered main loop over K tiles [k0, k0 + nk).  L provides
-//   load(kt)   : issue the global loads of K tile kt into its registers
-//   store(A,B) : write those registers into the LDS stage
-template <int BM, int BN, class L>
+//   load(kt)       : issue the global loads of K tile kt into its registers
+//   store<P>(A, B) : write those registers into the LDS stage (Stage<P, .>)
+template <int BM, int BN, int P, class L>
 __device__ __forceinline__ void mainloop(L& ld, float* smem, int k0, int nk,
                                          f32x16 (&acc)[BM / 64][BN / 64]) {
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 1, wn = wave >> 1;
 #pragma unroll
@@ -69,15 +140,15 @@ __device__ __forceinline__ void mainloop(L& ld, float* smem, int k0, int nk,
     for (int j = 0; j < G::TN; ++j) acc[i][j] = zero16();
   if (nk <= 0) return;
   ld.load(k0);
-  ld.store(smem, smem + BK * G::LDA);
+  ld.template store<P>(smem, smem + G::A_FLOATS);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     float* cur = smem + (kt & 1) * G::STAGE;
     float* nxt = smem + ((kt + 1) & 1) * G::STAGE;
     const bool more = kt + 1 < nk;
     if (more) ld.load(k0 + kt + 1);
-    mma_tile<BM, BN>(cur, cur + BK * G::LDA, wm, wn, lane, acc);
-    if (more) ld.store(nxt, nxt + BK * G::LDA);
+    mma_tile<BM, BN, P>(cur, cur + G::A_FLOATS, wm, wn, lane, acc);
+    if (more) ld.template store<P>(nxt, nxt + G::A_FLOATS);
     __syncthreads();
   }
 }
@@ -142,33 +213,27 @@ struct FwdLoader {
       rb[i] = sel4(bv[i], *reinterpret_cast<const float4*>(wb + (size_t)k * s.K));
     }
   }
+  template <int P>
   __device__ __forceinline__ void store(float* As, float* Bs) const {
-    using G = Geo<BM, BN>;
     const int tid = threadIdx.x, c4 = tid & 7;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int m = (tid >> 3) + 32 * i;
-      As[(4 * c4 + 0) * G::LDA + m] = ra[i].x;
-      As[(4 * c4 + 1) * G::LDA + m] = ra[i].y;
-      As[(4 * c4 + 2) * G::LDA + m] = ra[i].z;
-      As[(4 * c4 + 3) * G::LDA + m] = ra[i].w;
-    }
+    for (int i = 0; i < AR; ++i) Stage<P, BM>::put_k4(As, (tid >> 3) + 32 * i, 4 * c4, ra[i]);
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
-      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+      Stage<P, BN>::put_r4(Bs, 4 * (tid % (BN / 4)), k, rb[i]);
     }
   }
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps) {
   // split-K (gridDim.y > 1, no bias / ReLU): slice z of kps K tiles writes a
   // raw slab y + z * M * K, summed by slab_sum4 afterwards
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int M = s.N * s.OH * s.OW;
   const int mt = (M + BM - 1) / BM;
@@ -177,7 +242,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
   const int nk = s.R * s.S * (s.C / BK), kb = blockIdx.y * kps;
   FwdLoader<BM, BN> ld(s, x, w, m0, n0);
   f32x16 acc[G::TM][G::TN];
-  mainloop<BM, BN>(ld, smem, kb, min(kps, nk - kb), acc);
+  mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
   y += (size_t)blockIdx.y * M * s.K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
 #pragma unroll
@@ -257,34 +322,22 @@ struct DataLoader {
       rb[i] = sel4(bv[i], *reinterpret_cast<const float4*>(wb + (size_t)ci * s.K));
     }
   }
+  template <int P>
   __device__ __forceinline__ void store(float* As, float* Bs) const {
-    using G = Geo<BM, BN>;
     const int tid = threadIdx.x, c4 = tid & 7;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int m = (tid >> 3) + 32 * i;
-      As[(4 * c4 + 0) * G::LDA + m] = ra[i].x;
-      As[(4 * c4 + 1) * G::LDA + m] = ra[i].y;
-      As[(4 * c4 + 2) * G::LDA + m] = ra[i].z;
-      As[(4 * c4 + 3) * G::LDA + m] = ra[i].w;
-    }
+    for (int i = 0; i < AR; ++i) Stage<P, BM>::put_k4(As, (tid >> 3) + 32 * i, 4 * c4, ra[i]);
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = (tid >> 3) + 32 * i;
-      Bs[(4 * c4 + 0) * G::LDB + n] = rb[i].x;
-      Bs[(4 * c4 + 1) * G::LDB + n] = rb[i].y;
-      Bs[(4 * c4 + 2) * G::LDB + n] = rb[i].z;
-      Bs[(4 * c4 + 3) * G::LDB + n] = rb[i].w;
-    }
+    for (int i = 0; i < BR; ++i) Stage<P, BN>::put_k4(Bs, (tid >> 3) + 32 * i, 4 * c4, rb[i]);
   }
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __restrict__ dy,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ dx, int kps) {
   // split-K over gridDim.z: slice z writes the raw slab dx + z * N*H*W*C
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int sd = s.stride;
   const int phase = blockIdx.y, py = phase / sd, px = phase % sd;
@@ -302,7 +355,7 @@ __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __re
   DataLoader<BM, BN> ld(s, dy, w, m0, n0, py, px, PH, PW, nkw > 0 ? nkw : 1, kh0, kw0);
   f32x16 acc[G::TM][G::TN];
   const int nk = nkh * nkw * (s.K / BK), kb = blockIdx.z * kps;
-  mainloop<BM, BN>(ld, smem, kb, min(kps, nk - kb), acc);
+  mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
   dx += (size_t)blockIdx.z * s.N * s.H * s.W * s.C;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
 #pragma unroll
@@ -367,27 +420,27 @@ struct FilterLoader {
       rb[i] = sel4(ok, *reinterpret_cast<const float4*>(dy + (size_t)min(pix, npix - 1) * s.K + co));
     }
   }
+  template <int P>
   __device__ __forceinline__ void store(float* As, float* Bs) const {
-    using G = Geo<BM, BN>;
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
-      *reinterpret_cast<float4*>(As + k * G::LDA + 4 * (tid % (BM / 4))) = ra[i];
+      Stage<P, BM>::put_r4(As, 4 * (tid % (BM / 4)), k, ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
-      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+      Stage<P, BN>::put_r4(Bs, 4 * (tid % (BN / 4)), k, rb[i]);
     }
   }
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void filter_kernel(ConvShape s, const float* __restrict__ x,
                                                     const float* __restrict__ dy,
                                                     float* __restrict__ part, int kchunk_tiles) {
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int mt = (s.C + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
   const int taps = s.R * s.S;
@@ -401,7 +454,7 @@ __global__ __launch_bounds__(NT) void filter_kernel(ConvShape s, const float* __
   const int nk = min(kchunk_tiles, (npix - pix0 + BK - 1) / BK);
   FilterLoader<BM, BN> ld(s, x, dy, m0, n0, tap, pix0, npix);
   f32x16 acc[G::TM][G::TN];
-  mainloop<BM, BN>(ld, smem, 0, nk, acc);
+  mainloop<BM, BN, P>(ld, smem, 0, nk, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
   const size_t slab = (size_t)taps * s.C * s.K;
 #pragma unroll
@@ -482,28 +535,28 @@ struct FilterGatherLoader {
                    *reinterpret_cast<const float4*>(dy + (size_t)min(pix, npix - 1) * s.K + co));
     }
   }
+  template <int P>
   __device__ __forceinline__ void store(float* As, float* Bs) const {
-    using G = Geo<BM, BN>;
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
-      *reinterpret_cast<float4*>(As + k * G::LDA + 4 * (tid % (BM / 4))) = ra[i];
+      Stage<P, BM>::put_r4(As, 4 * (tid % (BM / 4)), k, ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
-      *reinterpret_cast<float4*>(Bs + k * G::LDB + 4 * (tid % (BN / 4))) = rb[i];
+      Stage<P, BN>::put_r4(Bs, 4 * (tid % (BN / 4)), k, rb[i]);
     }
   }
 };
 
-template <int BM, int BN>
+template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void filter_gather_kernel(ConvShape s, const float* __restrict__ x,
                                                            const float* __restrict__ dy,
                                                            float* __restrict__ part,
                                                            int kchunk_tiles) {
-  using G = Geo<BM, BN>;
+  using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int Mw = s.R * s.S * s.C;
   const int mt = (Mw + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
@@ -514,7 +567,7 @@ __global__ __launch_bounds__(NT) void filter_gather_kernel(ConvShape s, const fl
   const int nk = min(kchunk_tiles, (npix - pix0 + BK - 1) / BK);
   FilterGatherLoader<BM, BN> ld(s, x, dy, m0, n0, pix0, npix);
   f32x16 acc[G::TM][G::TN];
-  mainloop<BM, BN>(ld, smem, 0, nk, acc);
+  mainloop<BM, BN, P>(ld, smem, 0, nk, acc);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
 #pragma unroll
   for (int j = 0; j < G::TN; ++j) {
@@ -558,12 +611,18 @@ static inline Tile pick(long long M, int N) {
   return bm ? T128x64 : T64x64;
 }
 
-#define TILED_DISPATCH(t, KERNEL, GRID, ...)                                          \
-  switch (t) {                                                                         \
-    case T128x128: KERNEL<128, 128><<<GRID(128, 128), NT, 0, st>>>(__VA_ARGS__); break; \
-    case T128x64: KERNEL<128, 64><<<GRID(128, 64), NT, 0, st>>>(__VA_ARGS__); break;    \
-    case T64x128: KERNEL<64, 128><<<GRID(64, 128), NT, 0, st>>>(__VA_ARGS__); break;    \
-    default: KERNEL<64, 64><<<GRID(64, 64), NT, 0, st>>>(__VA_ARGS__); break;           \
+#define TILED_DISPATCH_P(P, t, KERNEL, GRID, ...)                                        \
+  switch (t) {                                                                            \
+    case T128x128: KERNEL<128, 128, P><<<GRID(128, 128), NT, 0, st>>>(__VA_ARGS__); break; \
+    case T128x64: KERNEL<128, 64, P><<<GRID(128, 64), NT, 0, st>>>(__VA_ARGS__); break;    \
+    case T64x128: KERNEL<64, 128, P><<<GRID(64, 128), NT, 0, st>>>(__VA_ARGS__); break;    \
+    default: KERNEL<64, 64, P><<<GRID(64, 64), NT, 0, st>>>(__VA_ARGS__); break;           \
+  }
+#define TILED_DISPATCH(t, KERNEL, GRID, ...)                  \
+  if (bf16) {                                                 \
+    TILED_DISPATCH_P(BF16, t, KERNEL, GRID, __VA_ARGS__)      \
+  } else {                                                    \
+    TILED_DISPATCH_P(F32, t, KERNEL, GRID, __VA_ARGS__)       \
   }
 
 }  // namespace tiled
@@ -626,7 +685,7 @@ long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
 }
 
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                    bool relu, float* ws, hipStream_t st) {
+                    bool relu, float* ws, hipStream_t st, bool bf16) {
   using namespace tiled;
   const long long M = (long long)s.N * s.OH * s.OW;
   Tile t;
@@ -641,7 +700,7 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st) {
+                         hipStream_t st, bool bf16) {
   using namespace tiled;
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
@@ -685,7 +744,7 @@ int conv_filter_tiled_splits(const ConvShape& s) {
 }
 
 void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,
-                           float* dw, hipStream_t st) {
+                           float* dw, hipStream_t st, bool bf16) {
   using namespace tiled;
   const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
   const int z = conv_filter_tiled_splits(s);
@@ -693,8 +752,12 @@ void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, 
   const int taps = s.R * s.S;
   if (s.C % 4 != 0) {  // (tap, ci) gather rows, 64x64 tiles
     const int Mw = taps * s.C;
-    filter_gather_kernel<64, 64><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
-        s, x, dy, z == 1 ? dw : part, kchunk);
+    if (bf16)
+      filter_gather_kernel<64, 64, BF16><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
+          s, x, dy, z == 1 ? dw : part, kchunk);
+    else
+      filter_gather_kernel<64, 64, F32><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
+          s, x, dy, z == 1 ? dw : part, kchunk);
     if (z > 1) slab_sum(part, z, (long long)Mw * s.K, dw, st);
     return;
   }

@@ -18,13 +18,15 @@ struct PoolShape {
 
 // ws: split-K workspace of conv_ws_floats(s, bias || relu) floats (shared by
 // the three ops of one layer; dw / dx / y are written, not accumulated)
+// bf16: MFMA operands converted to bf16 (fp32 accumulate, fp32 in / out); the
+// tiled family only - shapes it does not take run the fp32 gather engine
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, float* ws, hipStream_t st);
+              bool relu, float* ws, hipStream_t st, bool bf16 = false);
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                   hipStream_t st);
+                   hipStream_t st, bool bf16 = false);
 int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
-                     hipStream_t st);
+                     hipStream_t st, bool bf16 = false);
 long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue);
 // LDS-tiled conv family (conv_tiled.hip), used by the launchers above for the
 // shapes it supports
@@ -32,14 +34,14 @@ bool conv_fwd_tiled_ok(const ConvShape& s);
 bool conv_bwd_data_tiled_ok(const ConvShape& s);
 bool conv_bwd_filter_tiled_ok(const ConvShape& s);
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                    bool relu, float* ws, hipStream_t st);
+                    bool relu, float* ws, hipStream_t st, bool bf16);
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st);
+                         hipStream_t st, bool bf16);
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
 int conv_filter_tiled_splits(const ConvShape& s);
 void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,
-                           float* dw, hipStream_t st);
+                           float* dw, hipStream_t st, bool bf16);
 // mode 0: s1 = colsum(a), s2 = colsum(a^2); mode 1: s1 = colsum(a), s2 = colsum(a*b).
 // ws (chan_reduce_ws_floats) selects the deterministic bn.hip reduction;
 // null falls back to memset + atomics.

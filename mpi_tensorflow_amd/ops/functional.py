@@ -43,6 +43,19 @@ def _empty(shape, like):
     return torch.empty(shape, dtype=like.dtype, device=like.device)
 
 
+# MFMA operand precision of the tiled conv kernels: False = fp32 MFMA, True =
+# operands converted to bf16 while staged into LDS (v_mfma_f32_32x32x16_bf16,
+# fp32 accumulation; activations, BN and grads stay fp32).  Set by the engine
+# (cfg.dtype); captured per op call, so a graph keeps the mode it was
+# captured with.
+_CONV_BF16 = False
+
+
+def set_conv_bf16(on: bool) -> None:
+    global _CONV_BF16
+    _CONV_BF16 = bool(on)
+
+
 # Gradient-ready hook: when set (parallel/overlap.py BucketedAllReduce), the
 # backward of every op reports each parameter-gradient view it has finished
 # writing, so gradient buckets can be all-reduced while backward continues.
@@ -68,7 +81,9 @@ class _ConvFn(torch.autograd.Function):
         C = native()
         x = x.contiguous()
         y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
-        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), stream_handle())
+        ctx.bf16 = _CONV_BF16
+        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), stream_handle(),
+                       ctx.bf16)
         ctx.save_for_backward(x, w, y)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
@@ -85,7 +100,7 @@ class _ConvFn(torch.autograd.Function):
             C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
             dy = dym
         sh = ctx.shape
-        C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s)
+        C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s, ctx.bf16)
         if ctx.has_b:
             scratch = torch.empty(sh.K, device=dy.device, dtype=dy.dtype)
             C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0,
@@ -94,7 +109,7 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
-            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s)
+            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16)
         return dx, None, None, None, None, None, None, None
 
 

@@ -5,6 +5,10 @@ param / grad / momentum buffers, the reference's LR schedule and momentum
 SGD (/root/reference/mpipy.py:59-66), batch offset (step*B) % (N-B), DP by
 per-step gradient all-reduce of the flat grad buffer.
 
+With cfg.dtype == "bf16" the convolutions (and linear layers) run their
+MFMAs on bf16 operands converted while staged into LDS (fp32 accumulation;
+activations, BatchNorm, gradients and the optimizer stay fp32).
+
 On GPU one training step is: batch gather from the device-resident shard at
 the device step offset -> forward/backward through the native NHWC kernels
 (parameter grads land directly in the flat grad buffer; with world > 1 each
@@ -40,8 +44,9 @@ class GenericEngine:
                  device: torch.device, rank: int = 0, world: int = 1,
                  comm: Optional[DeviceComm] = None, force_sync: bool = False):
         self.cfg, self.device, self.rank, self.world, self.comm = cfg, device, rank, world, comm
-        if cfg.dtype != "fp32":
-            raise NotImplementedError(f"dtype {cfg.dtype} is not implemented for {cfg.model} yet")
+        self.bf16 = cfg.dtype == "bf16"
+        if self.bf16 and device.type != "cuda":
+            raise NotImplementedError("dtype bf16 needs the GPU kernels (bf16 MFMA convolutions)")
         self.model = make_model(cfg.model)
         self.layout = self.model.layout
         self.B = cfg.batch_size
@@ -102,6 +107,7 @@ class GenericEngine:
     # ------------------------------------------------------------------ step
     def _step_gpu(self):
         C_ = self._C
+        Fn.set_conv_bf16(self.bf16)
         s = stream_handle()
         row = int(np.prod(self.xb.shape[1:]))
         C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
@@ -204,6 +210,8 @@ class GenericEngine:
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
     def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 256, dropout: bool = False):
+        if self.on_gpu:
+            Fn.set_conv_bf16(self.bf16)
         wrong = 0
         for a in range(0, x.shape[0], chunk):
             xb = torch.from_numpy(np.ascontiguousarray(x[a:a + chunk], np.float32)).to(self.device)

@@ -192,3 +192,51 @@ def test_generic_bucketed_allreduce_overlap(cuda_dev):
     nb = len(synced.layout.buckets())
     assert nb == 4 and synced.bucketer.order == list(range(nb))  # backward completion order
     assert torch.equal(synced.params.detach(), plain.params.detach())
+
+
+@pytest.mark.parametrize("N,H,W,Cin,K,R,stride,pad", [
+    (2, 14, 14, 64, 128, 3, 2, 1),
+    (10, 56, 56, 64, 64, 3, 1, 1),
+    (2, 9, 9, 3, 64, 7, 2, 3),  # stem-like: gather filter path
+])
+def test_conv_bf16_mfma(cuda_dev, N, H, W, Cin, K, R, stride, pad):
+    """bf16-operand MFMA convolutions (fp32 accumulate) vs fp32 torch: relative
+    error of bf16 input rounding (~2^-9 per operand)."""
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, H, W, Cin, generator=g)
+    w = torch.randn(R, R, Cin, K, generator=g) * 0.1
+    dy = torch.randn(N, (H + 2 * pad - R) // stride + 1, (W + 2 * pad - R) // stride + 1, K,
+                     generator=g)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), stride=stride,
+                  padding=pad).permute(0, 2, 3, 1)
+    yr.backward(dy)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    wp = _param(w.to(cuda_dev))
+    Fn.set_conv_bf16(True)
+    try:
+        yg = Fn.conv2d(xg, wp, None, stride, pad, False)
+        yg.backward(dy.to(cuda_dev))
+    finally:
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    assert _rel(yg.cpu(), yr.detach()) < 1e-2
+    assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-2
+    if Cin % 4 == 0:
+        assert _rel(xg.grad.cpu(), xr.grad) < 1e-2
+
+
+def test_resnet18_bf16_trains(cuda_dev):
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 256, shape=(32, 32, 3))
+    tx, ty = synthetic_rows("test", 0, 128, shape=(32, 32, 3))
+    eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=32, dtype="bf16",
+                                      graph_steps=5).validate(), x, y, cuda_dev)
+    e0 = eng.evaluate(tx, ty)
+    eng.train(40)
+    torch.cuda.synchronize()
+    assert np.isfinite(eng.loss_value())
+    assert eng.evaluate(tx, ty) < min(e0, 60.0)
