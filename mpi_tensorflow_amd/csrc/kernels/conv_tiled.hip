@@ -638,6 +638,8 @@ static inline int tile_n(Tile t) { return (t == T128x128 || t == T64x128) ? 128 
 // split-K factor for a GEMM with `blocks` output tiles of nk K tiles each:
 // deep layers (few tiles, long K) get enough blocks to fill 256 CUs twice
 static inline int ksplit(long long blocks, int nk) {
+  // measured (ResNet-18, B=32): filling the chip beats the extra slab traffic
+  // (a 256-block / 8-slice cap cost +15 % step time in fp32 and bf16)
   if (blocks >= 512 || nk < 8) return 1;
   int z = cdiv(1024, blocks);
   if (z > nk / 4) z = nk / 4;
@@ -735,7 +737,9 @@ int conv_filter_tiled_splits(const ConvShape& s) {
   const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
   const bool vec = s.C % 4 == 0;
   const int tiles = vec ? filter_blocks_per_split(s) : cdiv(s.R * s.S * s.C, 64) * cdiv(s.K, 64);
-  int z = cdiv(2048, tiles);  // aim for ~2048 blocks
+  // aim for ~2048 blocks (measured: fewer, larger slices - 512 or 1024 blocks -
+  // cost 4-20 % ResNet-18 step time despite the smaller slab traffic)
+  int z = cdiv(2048, tiles);
   if (z < 1) z = 1;
   if (z > ktiles) z = ktiles;
   if (z > (vec ? 64 : 128)) z = vec ? 64 : 128;
