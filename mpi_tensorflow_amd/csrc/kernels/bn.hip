@@ -89,6 +89,41 @@ __global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ 
   }
 }
 
+// Scalar variant of pass 1 for channel counts that are not a multiple of 4
+// (thin layers: LeNet's 6 / 10 channel convs and FCs): thread = one channel
+// x a row stride.  Modes SUM_SQ / SUM_PROD only.
+__global__ __launch_bounds__(256) void partial1_kernel(const float* __restrict__ a,
+                                                       const float* __restrict__ b, int mode,
+                                                       long long rows, int C, int rows_per_block,
+                                                       float* __restrict__ part) {
+  __shared__ float red[2][256];
+  const int RP = 256 / C;
+  const int tid = threadIdx.x, c = tid % C, rl = tid / C;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = min(rows, r0 + rows_per_block);
+  float s1 = 0.f, s2 = 0.f;
+  if (rl < RP) {
+#pragma unroll 4
+    for (long long r = r0 + rl; r < r1; r += RP) {
+      const float v = a[(size_t)r * C + c];
+      s1 += v;
+      s2 += mode == SUM_SQ ? v * v : v * b[(size_t)r * C + c];
+    }
+  }
+  red[0][tid] = s1;
+  red[1][tid] = s2;
+  __syncthreads();
+  if (tid < C) {
+    float t1 = 0.f, t2 = 0.f;
+    for (int j = 0; j < RP; ++j) {
+      t1 += red[0][tid + j * C];
+      t2 += red[1][tid + j * C];
+    }
+    part[(size_t)blockIdx.x * 2 * C + tid] = t1;
+    part[(size_t)blockIdx.x * 2 * C + C + tid] = t2;
+  }
+}
+
 // One wave per channel: s1 / s2 = sums of the nb block partials.  BN
 // forward mode also writes mean / rstd and updates the running statistics.
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nb,
@@ -197,7 +232,7 @@ static inline int grid_elems(long long n) {
 }
 
 static inline int nblocks(long long rows, int C) {
-  const int RP = 256 / (C / 4);
+  const int RP = C % 4 == 0 ? 256 / (C / 4) : 256 / C;
   long long nb = (rows + RP * 16 - 1) / (RP * 16);  // >= 16 row passes per block
   if (nb > 1024) nb = 1024;
   return (int)(nb < 1 ? 1 : nb);
@@ -205,7 +240,8 @@ static inline int nblocks(long long rows, int C) {
 
 }  // namespace bn
 
-bool chan_reduce_ok(int C) { return C % 4 == 0 && C >= 4 && C <= 1024; }
+// vector path: C % 4 == 0, C <= 1024; scalar path (column sums only): C <= 256
+bool chan_reduce_ok(int C) { return (C % 4 == 0 && C >= 4 && C <= 1024) || (C >= 1 && C <= 256); }
 
 long long chan_reduce_ws_floats(long long rows, int C) {
   return chan_reduce_ok(C) ? (long long)bn::nblocks(rows, C) * 2 * C : 0;
@@ -231,7 +267,12 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
                  int mode, float* ws, hipStream_t st) {
   if (!chan_reduce_ok(C)) throw std::runtime_error("chan_reduce: unsupported channel count");
   const int nb = bn::nblocks(rows, C);
-  run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+  if (C % 4 == 0 && C <= 1024) {
+    run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+  } else {
+    const int rpb = (int)((rows + nb - 1) / nb);
+    bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
+  }
   bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, s1, s2, 0, rows, 0.f, 0.f, nullptr,
                                                    nullptr, nullptr, nullptr);
 }
@@ -239,7 +280,7 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
             float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st) {
-  if (!chan_reduce_ok(C)) throw std::runtime_error("bn_fwd: unsupported channel count");
+  if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_fwd: needs C % 4 == 0, C <= 1024");
   const long long n4 = rows * C / 4;
   if (training) {
     const int nb = bn::nblocks(rows, C);
@@ -257,7 +298,7 @@ void bn_fwd(const float* x, long long rows, int C, const float* g, const float* 
 void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
             float* dx, float* dres, hipStream_t st) {
-  if (!chan_reduce_ok(C)) throw std::runtime_error("bn_bwd: unsupported channel count");
+  if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
   const int nb = bn::nblocks(rows, C);
   run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, st);
   // db = sum dy', dg = sum dy' xhat

@@ -705,7 +705,8 @@ __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
 // each, summed through LDS).  A[m = ci][k = pixel], B[k = pixel][co]: both
 // gathered straight from L2 with channels on lanes, one image row ahead.  The
 // centre tap's blocks also sum dY2 per channel (db2).
-constexpr int C2F_GROUPS_IMG = 4;
+constexpr int C2F_IPW = 2;                   // images per wave
+constexpr int C2F_GROUPS_IMG = 4 * C2F_IPW;  // images per block (4 image slots)
 
 __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict__ a1,
                                     const float* __restrict__ dy2, float* __restrict__ part2,
@@ -730,12 +731,17 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   const int co = nsub * 32 + (lane & 31);
   f32x16 acc = zero16(), acc1 = zero16();
   float dbs = 0.f;
-  const int n = g * C2F_GROUPS_IMG + ih;
-  if (n < batch) {
-    const float* an = a1 + (size_t)n * 196 * 32 + ci;
-    const float* dn = dy2 + (size_t)n * 196 * 64 + co;
+  // this wave's images: n0 + 4 i (i < C2F_IPW); rows of all of them form one
+  // continuous prefetch pipeline (longer waves amortise the first-load latency
+  // and the LDS-reduction epilogue)
+  const int n0 = g * C2F_GROUPS_IMG + ih;
+  if (n0 < batch) {
+    const int nimg = min(C2F_IPW, (batch - n0 + 3) / 4);
     float av[7], bv[7], avn[7], bvn[7];
-    auto fetch = [&](int y, float* A, float* Bv) {
+    auto fetch = [&](int rr, float* A, float* Bv) {
+      const int n = n0 + 4 * (rr / 14), y = rr % 14;
+      const float* an = a1 + (size_t)n * 196 * 32 + ci;
+      const float* dn = dy2 + (size_t)n * 196 * 64 + co;
       const int iy = y + kh - 2;
       const bool rv = iy >= 0 && iy < 14;
       const int iyc = min(max(iy, 0), 13);
@@ -749,9 +755,10 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
       }
     };
     fetch(0, av, bv);
+    const int nrows = 14 * nimg;
 #pragma unroll 2
-    for (int y = 0; y < 14; ++y) {
-      if (y + 1 < 14) fetch(y + 1, avn, bvn);
+    for (int rr = 0; rr < nrows; ++rr) {
+      if (rr + 1 < nrows) fetch(rr + 1, avn, bvn);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int xp = 0; xp < 7; ++xp) {

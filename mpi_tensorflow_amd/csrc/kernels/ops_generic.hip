@@ -488,8 +488,9 @@ void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float*
 
 void colsum2(const float* a, const float* b, long long rows, int C, float* s1, float* s2, int mode,
              float* ws, hipStream_t st) {
-  // deterministic vectorised two-pass reduction (bn.hip) when the channel
-  // count allows it; the atomic kernel above covers thin odd layers (LeNet)
+  // deterministic two-pass reduction (bn.hip); the memset + atomic kernel
+  // above is only a fallback for callers without a workspace (memset nodes +
+  // atomics inside captured graphs were the source of a replay divergence)
   if (ws && chan_reduce_ok(C)) return chan_reduce(a, b, rows, C, s1, s2, mode, ws, st);
   (void)hipMemsetAsync(s1, 0, C * sizeof(float), st);
   (void)hipMemsetAsync(s2, 0, C * sizeof(float), st);

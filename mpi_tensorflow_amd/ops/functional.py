@@ -115,14 +115,20 @@ class _ConvFn(torch.autograd.Function):
 
 class ConvWorkspace:
     """Split-K slab / reduction-partials workspace shared by the conv and BN
-    kernels of all layers (they run in stream order).  Grown lazily, so the
-    eager warm-up steps before graph capture size it once."""
+    kernels of all layers (they run in stream order).  Grown lazily.  A
+    buffer is never released once handed out: captured hipGraphs keep its
+    address, and a later, larger request (e.g. evaluation at a bigger batch
+    between graph replays) must not let the allocator hand that memory to
+    another tensor."""
 
     def __init__(self):
         self.t: Optional[torch.Tensor] = None
+        self._retired = []
 
     def get(self, n: int, device) -> torch.Tensor:
         if self.t is None or self.t.numel() < n or self.t.device != device:
+            if self.t is not None:
+                self._retired.append(self.t)
             self.t = torch.empty(n, dtype=torch.float32, device=device)
         return self.t
 

@@ -240,3 +240,15 @@ def test_resnet18_bf16_trains(cuda_dev):
     torch.cuda.synchronize()
     assert np.isfinite(eng.loss_value())
     assert eng.evaluate(tx, ty) < min(e0, 60.0)
+
+
+def test_trainer_eval_between_graph_replays(cuda_dev):
+    """Eval at a larger batch between captured-graph segments must not
+    invalidate buffers the graphs still use (regression: LeNet NaN)."""
+    from mpi_tensorflow_amd.runtime.trainer import Trainer
+
+    cfg = C.TrainConfig(model="lenet5", max_steps=120, eval_every=30, graph_steps=10,
+                        quiet=True).validate()
+    s = Trainer(cfg).run()
+    assert np.isfinite(s.final_loss), s
+    assert s.final_test_error_global < 50.0, s
