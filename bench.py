@@ -44,6 +44,13 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded"))
+    ap.add_argument("--comm-emulate", default=None, metavar="LAT_US,BUSBW_GBPS[,N[,BLOCKS]]",
+                    help="1 GPU: replace the collectives by timing stand-ins of an N-rank ring "
+                         "(default N=8, 32 workgroups) to measure sync/compute overlap")
+    ap.add_argument("--force-sync", action="store_true",
+                    help="1 GPU: run the RCCL all-reduce path anyway (world-1 communicator), "
+                         "to measure the overhead of the comm stream and buckets")
     return ap.parse_args(argv)
 
 
@@ -63,11 +70,22 @@ def main(argv=None) -> int:
     if a.batch_size is None:
         a.batch_size = 32 if a.model == "resnet18" else 64
     cfg = C.TrainConfig(model=a.model, batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
-                        graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend).validate()
+                        graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend,
+                        sync_schedule=a.sync_schedule).validate()
     comm = make_comm(di, device) if (N > 1 and a.sync == "grad") else None
+    force = bool((a.force_sync or a.comm_emulate) and N == 1 and device.type == "cuda")
+    if force and a.comm_emulate:
+        from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
+        f = [float(v) for v in a.comm_emulate.split(",")]
+        comm = EmulatedDeviceComm(int(f[2]) if len(f) > 2 else 8, f[0], f[1],
+                                  int(f[3]) if len(f) > 3 else 32)
+    elif force:
+        from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
+        comm = RcclDeviceComm(di)
     if a.model == "mnist_cnn":
         shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
-        eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm)
+        eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
+                          force_sync=force)
         test_x, test_y = shard.test_x, shard.test_y
     else:
         from mpi_tensorflow_amd.models.generic import model_input_shape
@@ -79,13 +97,17 @@ def main(argv=None) -> int:
         tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
         ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
                                         start=di.rank * rows)
-        eng = GenericEngine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm)
+        eng = GenericEngine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
+                            force_sync=force)
         test_x, test_y = ex.numpy(), ey.numpy()
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
+    # startup autotune of the gradient-sync schedule (N > 1, native MNIST
+    # engine): real training steps, before the warm-up, outside the timing
+    tune_steps = eng.tune_schedule() if hasattr(eng, "tune_schedule") else 0
     if hasattr(eng, "capture"):
         eng.capture(a.warmup)
         eng.capture(a.steps)
@@ -134,9 +156,13 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "image": image,
                 "parallelism": f"dp{N}",
-                "sync": "per-step gradient all-reduce (RCCL)" if N > 1 else "none (1 rank)",
+                "sync": ("per-step gradient all-reduce (RCCL)" if (N > 1 or force)
+                         else "none (1 rank)"),
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
+                "sync_schedule": getattr(eng, "sync_schedule", "n/a"),
+                "sync_tune_us_per_step": getattr(eng, "tune_log", {}) or None,
+                "sync_tune_steps": tune_steps,
                 "graph_steps": (a.graph_steps if not a.no_graph else 0),
             },
             "final_test_accuracy": None if err != err else round(100.0 - err, 3),

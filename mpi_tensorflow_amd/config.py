@@ -60,6 +60,10 @@ MNIST_FILES = {
 
 MODELS = ("mnist_cnn", "lenet5", "resnet18")
 SYNC_MODES = ("grad", "param_avg", "none")
+# gradient-sync schedules of the native MNIST executor (grad sync, world > 1):
+# "buckets" = all-reduce FC bucket then conv bucket; "sharded" = reduce-scatter
+# FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
+SYNC_SCHEDULES = ("auto", "buckets", "sharded")
 DTYPES = ("fp32", "bf16")
 
 
@@ -76,6 +80,7 @@ class TrainConfig:
     # reference's periodic weight averaging (mpipy.py:87-91)
     sync: str = "grad"
     sync_every: int = SYNC_EVERY
+    sync_schedule: str = "auto"
     # evaluate (and print the reference log line) every N steps; the
     # reference evaluates every step (Q9) but prints every 50
     eval_every: int = SYNC_EVERY
@@ -115,6 +120,9 @@ class TrainConfig:
             raise ValueError(f"unknown model {self.model!r}; choose from {MODELS}")
         if self.sync not in SYNC_MODES:
             raise ValueError(f"unknown sync {self.sync!r}; choose from {SYNC_MODES}")
+        if self.sync_schedule not in SYNC_SCHEDULES:
+            raise ValueError(f"unknown sync schedule {self.sync_schedule!r}; "
+                             f"choose from {SYNC_SCHEDULES}")
         if self.dtype not in DTYPES:
             raise ValueError(f"unknown dtype {self.dtype!r}; choose from {DTYPES}")
         if self.backend not in ("auto", "native", "torch"):
@@ -161,6 +169,8 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--dtype", default=d.dtype, choices=DTYPES)
     p.add_argument("--sync", default=d.sync, choices=SYNC_MODES)
     p.add_argument("--sync-every", type=int, default=d.sync_every)
+    p.add_argument("--sync-schedule", default=d.sync_schedule, choices=SYNC_SCHEDULES,
+                   help="native MNIST grad-sync schedule (auto / buckets / sharded FC update)")
     p.add_argument("--eval-every", type=int, default=d.eval_every,
                    help="0 disables periodic eval")
     p.add_argument("--data-dir", default=d.data_dir)

@@ -30,6 +30,33 @@ static void check_launch() {
   if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
 }
 
+// Host-callback communicator (tests only): every collective calls a Python
+// function (op, send, recv, count, dtype) that stages the data through the
+// host and a gloo group.  Lets several ranks share ONE GPU and drive the
+// native executors' sync schedules eagerly (not capturable).
+class PyComm : public Collective {
+ public:
+  PyComm(int nranks, int rank, py::function fn) : n_(nranks), r_(rank), fn_(std::move(fn)) {}
+  int rank() const override { return r_; }
+  int size() const override { return n_; }
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, int,
+                  hipStream_t) override {
+    fn_("all_reduce", (uintptr_t)send, (uintptr_t)recv, count, dtype);
+  }
+  void all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                  hipStream_t) override {
+    fn_("all_gather", (uintptr_t)send, (uintptr_t)recv, send_count, dtype);
+  }
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int,
+                      hipStream_t) override {
+    fn_("reduce_scatter", (uintptr_t)send, (uintptr_t)recv, recv_count, dtype);
+  }
+
+ private:
+  int n_, r_;
+  py::function fn_;
+};
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X-native runtime for mpi_tensorflow_amd (gfx950 HIP kernels, RCCL, IDX)";
   m.attr("ARCH") = "gfx950";
@@ -261,7 +288,30 @@ PYBIND11_MODULE(_C, m) {
                                       RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b);
 #undef RW
 
-  py::class_<RcclComm>(m, "RcclComm")
+  py::class_<Collective>(m, "Collective")
+      .def_property_readonly("rank", &Collective::rank)
+      .def_property_readonly("size", &Collective::size)
+      .def("all_reduce",
+           [](Collective& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              uintptr_t s) { c.all_reduce(P<void>(send), P<void>(recv), count, dtype, op, S(s)); })
+      .def("all_gather",
+           [](Collective& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t s) {
+             c.all_gather(P<void>(send), P<void>(recv), count, dtype, S(s));
+           })
+      .def("reduce_scatter",
+           [](Collective& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              uintptr_t s) { c.reduce_scatter(P<void>(send), P<void>(recv), count, dtype, op, S(s)); });
+
+  py::class_<EmuComm, Collective>(m, "EmuComm")
+      .def(py::init<int, int, double, double, int>(), py::arg("nranks"), py::arg("rank"),
+           py::arg("lat_us"), py::arg("busbw_gbps"), py::arg("blocks"))
+      .def("all_reduce_us", &EmuComm::all_reduce_us)
+      .def("gather_us", &EmuComm::gather_us);
+
+  py::class_<PyComm, Collective>(m, "PyComm")
+      .def(py::init<int, int, py::function>(), py::arg("nranks"), py::arg("rank"), py::arg("fn"));
+
+  py::class_<RcclComm, Collective>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank) {
              std::string s = uid;
              return new RcclComm(std::vector<char>(s.begin(), s.end()), nranks, rank);
@@ -275,11 +325,6 @@ PYBIND11_MODULE(_C, m) {
                     auto v = RcclComm::unique_id();
                     return py::bytes(v.data(), v.size());
                   })
-      .def_property_readonly("rank", &RcclComm::rank)
-      .def_property_readonly("size", &RcclComm::size)
-      .def("all_reduce",
-           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
-              uintptr_t s) { c.all_reduce(P<void>(send), P<void>(recv), count, dtype, op, S(s)); })
       .def("broadcast",
            [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int root,
               uintptr_t s) { c.broadcast(P<void>(send), P<void>(recv), count, dtype, root, S(s)); })
@@ -288,13 +333,6 @@ PYBIND11_MODULE(_C, m) {
               int root, uintptr_t s) {
              c.reduce(P<void>(send), P<void>(recv), count, dtype, op, root, S(s));
            })
-      .def("all_gather",
-           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, uintptr_t s) {
-             c.all_gather(P<void>(send), P<void>(recv), count, dtype, S(s));
-           })
-      .def("reduce_scatter",
-           [](RcclComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
-              uintptr_t s) { c.reduce_scatter(P<void>(send), P<void>(recv), count, dtype, op, S(s)); })
       .def("group_start", &RcclComm::group_start)
       .def("group_end", &RcclComm::group_end)
       .def("destroy", &RcclComm::destroy);
@@ -302,11 +340,20 @@ PYBIND11_MODULE(_C, m) {
   py::class_<MnistExecutor>(m, "MnistExecutor")
       .def(py::init<const MnistPtrs&>())
       .def("train_step",
-           [](MnistExecutor& e, uintptr_t s, RcclComm* comm, uintptr_t cs) {
+           [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs) {
              e.train_step(S(s), comm, S(cs));
              check_launch();
            },
            py::arg("stream"), py::arg("comm") = nullptr, py::arg("comm_stream") = 0)
+      .def("set_schedule", &MnistExecutor::set_schedule)
+      .def_property_readonly("schedule", &MnistExecutor::schedule)
+      .def("sharded_ok", &MnistExecutor::sharded_ok)
+      .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
+      .def("gather_optimizer_state",
+           [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs) {
+             e.gather_optimizer_state(S(s), comm, S(cs));
+             check_launch();
+           })
       .def("forward_backward",
            [](MnistExecutor& e, uintptr_t s) {
              e.forward_backward(S(s));
@@ -325,6 +372,9 @@ PYBIND11_MODULE(_C, m) {
                                               S(s));
                     check_launch();
                   });
+
+  m.attr("MnistExecutor").attr("SCHED_BUCKETS") = (int)MnistExecutor::SCHED_BUCKETS;
+  m.attr("MnistExecutor").attr("SCHED_SHARDED_FC") = (int)MnistExecutor::SCHED_SHARDED_FC;
 
   // ----------------------------------------------------------------- IDX
   m.def("idx_header", [](const std::string& path) {

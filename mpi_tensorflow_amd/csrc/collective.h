@@ -1,0 +1,64 @@
+// Device-collective interface of the step executors.
+//
+// The executors issue their gradient / parameter collectives through this
+// interface, on a HIP stream, inside the captured step.  Two implementations:
+//   RcclComm (rccl_comm.h) - RCCL over xGMI, the production path;
+//   EmuComm  (below)       - a timing stand-in for an N-rank communicator on
+//                            ONE GPU, used to measure how a comm schedule
+//                            overlaps with the compute stream before the
+//                            multi-GPU node is available (bench.py
+//                            --comm-emulate).  It moves no data between ranks
+//                            (the numerics of an emulated run are NOT those
+//                            of N ranks); it only occupies `blocks`
+//                            workgroups and the stream for the time a ring
+//                            collective of that size would take.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+class Collective {
+ public:
+  virtual ~Collective() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  // dtype: ncclDataType_t value; op: ncclRedOp_t value.  In-place forms are
+  // allowed as in RCCL (reduce_scatter: recv == send + rank * recv_count;
+  // all_gather: send == recv + rank * send_count).
+  virtual void all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
+                          hipStream_t s) = 0;
+  virtual void all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                          hipStream_t s) = 0;
+  virtual void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                              hipStream_t s) = 0;
+};
+
+// Ring cost model (rccl-tests conventions): an all-reduce of S bytes takes
+// lat + 2 (N-1)/N * S / busbw; a reduce-scatter or all-gather whose FULL
+// buffer is S bytes takes lat + (N-1)/N * S / busbw.
+class EmuComm : public Collective {
+ public:
+  EmuComm(int nranks, int rank, double lat_us, double busbw_gbps, int blocks);
+  int rank() const override { return rank_; }
+  int size() const override { return nranks_; }
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
+                  hipStream_t s) override;
+  void all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                  hipStream_t s) override;
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                      hipStream_t s) override;
+  double all_reduce_us(size_t bytes) const;
+  double gather_us(size_t full_bytes) const;  // reduce-scatter / all-gather
+
+ private:
+  void occupy(void* buf, size_t bytes, double us, hipStream_t s);
+  int nranks_, rank_, blocks_;
+  double lat_us_, busbw_;
+};
+
+size_t dtype_bytes(int dtype);
+
+namespace commemu {
+// `blocks` workgroups touch `bytes` of buf (load + store in place) and stay
+// resident until `us` microseconds have passed since they started.
+void launch_occupy(void* buf, size_t bytes, double us, int blocks, hipStream_t s);
+}  // namespace commemu

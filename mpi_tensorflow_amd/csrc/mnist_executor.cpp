@@ -48,6 +48,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
                           W + p.off_b1, P<float>(p.a1), P<uint8_t>(p.idx1), s);
   mnist::launch_conv2_fwd(P<const float>(p.a1), B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
                           P<uint8_t>(p.idx2), P<float>(p.w2t), s);
+  wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
   mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
   mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
                               W + p.off_b4, P<const int>(p.train_y), p.n_local, step, B,
@@ -83,6 +84,7 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
   const long long* step = P<const long long>(p.step);
   const int B = p.batch;
   using U16 = uint16_t;
+  wait_fc_params(s);  // the shadow launch reads the FC weights
   mnist16::launch_shadows(W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
                           P<U16>(p.w2tb), P<U16>(p.w2b), s);
   mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
@@ -116,9 +118,15 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
                               G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
 }
 
-void MnistExecutor::forward_backward(hipStream_t s) { enqueue_fwd_bwd(s); }
+void MnistExecutor::forward_backward(hipStream_t s) {
+  wait_fc_params(s);
+  enqueue_fwd_bwd(s);
+}
 
-void MnistExecutor::sgd(hipStream_t s, float gscale) { sgd_range(s, 0, p_.total, gscale, true); }
+void MnistExecutor::sgd(hipStream_t s, float gscale) {
+  wait_fc_params(s);
+  sgd_range(s, 0, p_.total, gscale, true);
+}
 
 // momentum SGD over flat floats [lo, hi) (lo, hi multiples of 4); the L2
 // prefix [0, l2_end) is clipped to the range; bump_step increments the
@@ -133,14 +141,40 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
                              bump_step ? P<long long>(p.step) : nullptr, s);
 }
 
-void MnistExecutor::train_step(hipStream_t s, RcclComm* comm, hipStream_t cs) {
-  const MnistPtrs& p = p_;
-  float* G = P<float>(p.grads);
-  enqueue_fwd_bwd(s);
+void MnistExecutor::set_schedule(int sched) {
+  if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC)
+    throw std::runtime_error("MnistExecutor: unknown sync schedule");
+  if (fc_pending_)
+    throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
+  sched_ = sched;
+}
+
+bool MnistExecutor::sharded_ok(int nranks) const {
+  return nranks > 1 && p_.bucket1 % (4LL * nranks) == 0;
+}
+
+void MnistExecutor::wait_fc_params(hipStream_t s) {
+  if (fc_pending_) {
+    HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
+    fc_pending_ = false;
+  }
+}
+
+void MnistExecutor::join(hipStream_t s) { wait_fc_params(s); }
+
+void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs) {
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
+    enqueue_fwd_bwd(s);
     sgd(s, 1.0f);
     return;
   }
+  if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
+    train_step_sharded(s, comm, cs);
+    return;
+  }
+  const MnistPtrs& p = p_;
+  float* G = P<float>(p.grads);
+  enqueue_fwd_bwd(s);
   // size-1 comms are allowed (they exercise the capture path on one GPU)
   const float gscale = 1.0f / (float)comm->size();
   // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1 backward is done;
@@ -159,6 +193,51 @@ void MnistExecutor::train_step(hipStream_t s, RcclComm* comm, hipStream_t cs) {
   sgd_range(s, 0, p.bucket1, gscale, false);
   HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
   sgd_range(s, p.bucket1, p.total, gscale, true);
+}
+
+// Sharded FC update (ZeRO-1 style for bucket 1).  Comm stream, per step:
+//   reduce-scatter(FC grads) -> momentum SGD of this rank's 1/N shard ->
+//   [conv grads final] all-reduce(conv grads) -> all-gather(FC params)
+// Compute stream: conv SGD after the conv all-reduce, then the NEXT step's
+// conv forward runs while the FC all-gather is still in flight; only its fc1
+// forward waits for the gathered FC params (wait_fc_params).  Same bytes on
+// the wire as the all-reduce (RS + AG is how the ring all-reduce moves them),
+// but the FC momentum / SGD traffic drops by N and the all-gather half of the
+// FC collective overlaps the next forward instead of extending this step.
+// The FC momentum is sharded: gather_optimizer_state() before reading it.
+void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs) {
+  const MnistPtrs& p = p_;
+  float* G = P<float>(p.grads);
+  float* W = P<float>(p.params);
+  const int n = comm->size();
+  const float gscale = 1.0f / (float)n;
+  const long long chunk = p.bucket1 / n, lo = chunk * comm->rank();
+  enqueue_fwd_bwd(s);
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
+  comm->reduce_scatter(G, G + lo, (size_t)chunk, ncclFloat32, ncclSum, cs);
+  sgd_range(cs, lo, lo + chunk, gscale, false);
+  HIP_CHECK(hipEventRecord(ev_fin_, s));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
+  comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
+                   ncclSum, cs);
+  HIP_CHECK(hipEventRecord(ev_done_, cs));
+  comm->all_gather(W + lo, W, (size_t)chunk, ncclFloat32, cs);
+  HIP_CHECK(hipEventRecord(ev_b1_, cs));
+  fc_pending_ = true;
+  HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  sgd_range(s, p.bucket1, p.total, gscale, true);
+}
+
+void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {
+  wait_fc_params(s);
+  if (comm == nullptr || sched_ != SCHED_SHARDED_FC || !sharded_ok(comm->size())) return;
+  float* Mo = P<float>(p_.mom);
+  const long long chunk = p_.bucket1 / comm->size(), lo = chunk * comm->rank();
+  HIP_CHECK(hipEventRecord(ev_fin_, s));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
+  comm->all_gather(Mo + lo, Mo, (size_t)chunk, ncclFloat32, cs);
+  HIP_CHECK(hipEventRecord(ev_done_, cs));
+  HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
 }
 
 void MnistExecutor::eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int M,

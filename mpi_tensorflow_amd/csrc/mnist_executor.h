@@ -19,10 +19,14 @@
 // The SGD runs in two parts: the FC segment (97 % of the update traffic)
 // as soon as bucket 1 is reduced - overlapping bucket 2's all-reduce - and
 // the conv segment after bucket 2; both divide by the world size.
+// The alternative SCHED_SHARDED_FC schedule (train_step_sharded) splits the
+// FC collective into reduce-scatter + all-gather around a 1/N-shard update so
+// the all-gather overlaps the next step's conv forward.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "collective.h"
 #include "rccl_comm.h"
 
 struct MnistPtrs {
@@ -59,7 +63,22 @@ class MnistExecutor {
   // Full training step.  comm may be null (single rank, or periodic
   // parameter averaging done by the caller); comm_stream is used only when
   // comm is attached.
-  void train_step(hipStream_t s, RcclComm* comm, hipStream_t comm_stream);
+  void train_step(hipStream_t s, Collective* comm, hipStream_t comm_stream);
+  // Gradient-sync schedule used when a communicator of size > 1 is attached:
+  //   SCHED_BUCKETS    - all-reduce of bucket 1 (FC) then bucket 2 (conv);
+  //   SCHED_SHARDED_FC - reduce-scatter FC grads, SGD on the local 1/N shard,
+  //                      all-gather FC params overlapped with the next
+  //                      step's conv forward (see train_step_sharded).
+  static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1;
+  void set_schedule(int sched);
+  int schedule() const { return sched_; }
+  bool sharded_ok(int nranks) const;
+  // Makes stream s wait for any collective still in flight from the last
+  // step (call at the end of every captured / eager run of steps).
+  void join(hipStream_t s);
+  // Sharded schedule: all-gathers the FC momentum shards so the whole
+  // momentum buffer is valid (before checkpointing).  No-op otherwise.
+  void gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t comm_stream);
   // Forward+backward only (grads in the flat grad buffer; no sync, no SGD).
   void forward_backward(hipStream_t s);
   void sgd(hipStream_t s, float gscale);
@@ -77,10 +96,15 @@ class MnistExecutor {
 
  private:
   void enqueue_fwd_bwd(hipStream_t s);
+  void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
+  void wait_fc_params(hipStream_t s);
+  int sched_ = SCHED_BUCKETS;
+  bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on
   void enqueue_fwd_bwd_bf16(hipStream_t s);
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;
-  // ev_fin_: conv grads final (bucket 2 may start); ev_done_: bucket 2 reduced
+  // ev_fin_: conv grads final (bucket 2 may start); ev_done_: bucket 2 reduced.
+  // Sharded schedule: ev_b1_ = FC params gathered
   hipEvent_t ev_dw_ = nullptr, ev_b1_ = nullptr, ev_fin_ = nullptr, ev_done_ = nullptr;
 };

@@ -14,7 +14,9 @@
 
 #include <rccl/rccl.h>
 
-class RcclComm {
+#include "collective.h"
+
+class RcclComm : public Collective {
  public:
   // Loads RCCL from `lib_path` (e.g. torch/lib/librccl.so).
   static void load(const std::string& lib_path);
@@ -23,21 +25,23 @@ class RcclComm {
   static int version();
 
   RcclComm(const std::vector<char>& uid, int nranks, int rank);
-  ~RcclComm();
+  ~RcclComm() override;
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
-  int rank() const { return rank_; }
-  int size() const { return nranks_; }
+  int rank() const override { return rank_; }
+  int size() const override { return nranks_; }
 
   // dtype: ncclDataType_t value; op: ncclRedOp_t value.
-  void all_reduce(const void* send, void* recv, size_t count, int dtype, int op, hipStream_t s);
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
+                  hipStream_t s) override;
   void broadcast(const void* send, void* recv, size_t count, int dtype, int root, hipStream_t s);
   void reduce(const void* send, void* recv, size_t count, int dtype, int op, int root,
               hipStream_t s);
-  void all_gather(const void* send, void* recv, size_t send_count, int dtype, hipStream_t s);
+  void all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                  hipStream_t s) override;
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
-                      hipStream_t s);
+                      hipStream_t s) override;
   void group_start();
   void group_end();
   void destroy();

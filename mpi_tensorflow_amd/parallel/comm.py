@@ -107,6 +107,93 @@ class RcclDeviceComm(DeviceComm):
         self._c.destroy()
 
 
+class EmulatedDeviceComm(DeviceComm):
+    """Timing stand-in for an `nranks`-rank RCCL communicator on ONE GPU
+    (`_C.EmuComm`, csrc/collective.h): every collective holds `blocks`
+    workgroups and the stream for the time a ring collective of that size
+    takes under `lat_us` + bytes / `busbw_gbps`, and moves no data.  Used by
+    `bench.py --comm-emulate` to measure how a sync schedule overlaps with the
+    compute stream; the numerics of an emulated run are not those of N ranks."""
+
+    kind = "emulated"
+
+    def __init__(self, nranks: int, lat_us: float, busbw_gbps: float, blocks: int = 32,
+                 rank: int = 0):
+        self._c = native().EmuComm(nranks, rank, lat_us, busbw_gbps, blocks)
+        self.rank, self.size = rank, nranks
+        self.kind = f"emulated(n={nranks},lat={lat_us}us,busbw={busbw_gbps}GB/s,blocks={blocks})"
+
+    def all_reduce_(self, t, stream=None):
+        self._c.all_reduce(ptr(t), ptr(t), t.numel(), _DT[t.dtype], NCCL_SUM, stream_handle(stream))
+        return t
+
+    def all_gather(self, out, inp, stream=None):
+        self._c.all_gather(ptr(inp), ptr(out), inp.numel(), _DT[inp.dtype], stream_handle(stream))
+        return out
+
+    @property
+    def native_handle(self):
+        return self._c
+
+
+class HostStagedComm(DeviceComm):
+    """Test communicator: the native executors call back into Python for
+    every collective, which synchronizes the device, stages the slice through
+    the host and runs it on the gloo group.  Several ranks can then share ONE
+    GPU and still exercise the executors' sync schedules (buckets / sharded
+    FC update) end to end.  Eager only - an engine given this comm must not
+    capture hipGraphs.  `bases` are the device tensors the collectives may
+    address (the engine's flat grads / params / momentum)."""
+
+    kind = "host-staged"
+
+    def __init__(self, di: DistInfo):
+        self.rank, self.size = di.rank, di.world
+        self.bases = []
+        self._c = native().PyComm(di.world, di.rank, self._callback)
+
+    def _view(self, p: int, count: int) -> torch.Tensor:
+        for b in self.bases:
+            off = p - b.data_ptr()
+            if 0 <= off and off + 4 * count <= 4 * b.numel():
+                return b.view(-1)[off // 4: off // 4 + count]
+        raise ValueError("HostStagedComm: pointer outside the registered tensors")
+
+    def _callback(self, op: str, send: int, recv: int, count: int, dtype: int) -> None:
+        if dtype != NCCL_FLOAT32:
+            raise ValueError("HostStagedComm handles float32 only")
+        torch.cuda.synchronize()
+        n = self.size
+        if op == "all_reduce":
+            t = self._view(send, count).cpu()
+            dist.all_reduce(t)
+            self._view(recv, count).copy_(t)
+        elif op == "reduce_scatter":
+            t = self._view(send, count * n).cpu()
+            dist.all_reduce(t)
+            self._view(recv, count).copy_(t[self.rank * count:(self.rank + 1) * count])
+        elif op == "all_gather":
+            t = self._view(send, count).cpu()
+            parts = [torch.empty_like(t) for _ in range(n)]
+            dist.all_gather(parts, t)
+            self._view(recv, count * n).copy_(torch.cat(parts))
+        else:
+            raise ValueError(op)
+        torch.cuda.synchronize()
+
+    def all_reduce_(self, t, stream=None):
+        self.bases.append(t)
+        try:
+            self._callback("all_reduce", t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype])
+        finally:
+            self.bases.pop()
+        return t
+
+    @property
+    def native_handle(self):
+        return self._c
+
+
 class TorchDeviceComm(DeviceComm):
     kind = "torch"
 

@@ -93,6 +93,9 @@ class GenericEngine:
         s = self.step if step is None else step
         return learning_rate(s, self.n_local, self.B, self.cfg.base_lr, self.cfg.lr_decay)
 
+    def sync_optimizer_state(self) -> None:
+        """Replicated optimizer state: nothing to gather."""
+
     def set_step(self, step: int) -> None:
         self.step = int(step)
         if self.on_gpu:

@@ -37,6 +37,15 @@ from ..utils import rng
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
+# sync_schedule="auto": both gradient-sync schedules are timed on the first
+# train() call of at least TUNE_REPLAYS * 2 * graph_steps steps (real training
+# steps, bit-identical under either schedule) and the faster one is kept; all
+# ranks take the decision from the same (max-over-ranks) timings.  Which one
+# wins depends on the all-reduce bandwidth: with a comm-emulated ring
+# (bench.py --comm-emulate) the sharded FC update was 4-6 % faster at 100-200
+# GB/s bus bandwidth and 5 % slower at 400 GB/s (docs/PERF_NOTES.md).
+TUNE_REPLAYS = 2
+
 
 class MnistEngineBase:
     def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
@@ -76,6 +85,10 @@ class MnistEngineBase:
 
     def state_tensors(self):
         return self.params, self.mom
+
+    def sync_optimizer_state(self) -> None:
+        """Makes `mom` whole on every rank (a sharded optimizer keeps only
+        its own shard current); no-op for replicated optimizers."""
 
     def set_step(self, step: int) -> None:
         self.step = int(step)
@@ -229,9 +242,16 @@ class NativeMnistEngine(MnistEngineBase):
         self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
         if self.grad_sync and self._native_comm is None:
             raise RuntimeError("grad sync on the native engine needs the native RCCL communicator")
-        self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
-        self.use_graph = cfg.graph
+        if self.grad_sync:
+            self.exe.set_schedule(self._pick_schedule(cfg.sync_schedule, self._native_comm.size))
+        if getattr(self.comm, "kind", "") == "host-staged":  # test comm: eager only
+            self.comm.bases = [self.grads, self.params, self.mom]
+        self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
+        self.use_graph = cfg.graph and getattr(self.comm, "kind", "") != "host-staged"
         self.graph_steps = max(1, cfg.graph_steps)
+        self._tuned = not (self.grad_sync and cfg.sync_schedule == "auto" and self.use_graph
+                           and self.exe.sharded_ok(self._native_comm.size))
+        self.tune_log: Dict[str, float] = {}
         self._eval_ws = None
         if self.grad_sync:  # connection setup outside any capture
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), lay.total,
@@ -242,13 +262,34 @@ class NativeMnistEngine(MnistEngineBase):
         super().set_step(step)
         self.step_dev.fill_(int(step))
 
+    def _pick_schedule(self, name: str, nranks: int) -> int:
+        E = self._C.MnistExecutor
+        if name == "buckets" or not self.exe.sharded_ok(nranks):
+            return E.SCHED_BUCKETS
+        if name == "sharded":
+            return E.SCHED_SHARDED_FC
+        return E.SCHED_BUCKETS  # "auto": until tune_schedule() has timed both
+
+    @property
+    def sync_schedule(self) -> str:
+        if not self.grad_sync:
+            return "none"
+        E = self._C.MnistExecutor
+        return "sharded" if self.exe.schedule == E.SCHED_SHARDED_FC else "buckets"
+
+    def sync_optimizer_state(self) -> None:
+        if self.grad_sync:
+            self.exe.gather_optimizer_state(stream_handle(), self._native_comm,
+                                            stream_handle(self.comm_stream))
+
     # --------------------------------------------------------------- steps
     def _launch_one(self):
         cs = stream_handle(self.comm_stream) if self.comm_stream is not None else 0
         self.exe.train_step(stream_handle(), self._native_comm, cs)
 
     def _graph(self, n: int) -> Optional[torch.cuda.CUDAGraph]:
-        g = self._graphs.get(n)
+        key = (self.exe.schedule, n)
+        g = self._graphs.get(key)
         if g is None:
             if self.comm_stream is not None:
                 self.comm_stream.wait_stream(torch.cuda.current_stream())
@@ -257,6 +298,7 @@ class NativeMnistEngine(MnistEngineBase):
                 with torch.cuda.graph(g):
                     for _ in range(n):
                         self._launch_one()
+                    self.exe.join(stream_handle())  # comm stream rejoins inside the capture
             except RuntimeError as e:
                 # e.g. a collective library build that cannot be captured:
                 # keep training with eager launches instead of failing the run
@@ -265,12 +307,51 @@ class NativeMnistEngine(MnistEngineBase):
                 self.use_graph = False
                 torch.cuda.synchronize(self.device)
                 return None
-            self._graphs[n] = g
+            self._graphs[key] = g
         return g
+
+    def tune_schedule(self) -> int:
+        """Times TUNE_REPLAYS graph replays of each sync schedule (after one
+        untimed replay each) and keeps the faster; returns the number of
+        training steps it ran.  Collective over the ranks."""
+        if self._tuned:
+            return 0
+        from ..parallel import dist as D
+        E = self._C.MnistExecutor
+        G = self.graph_steps
+        steps = 0
+        best = None
+        for sched, name in ((E.SCHED_BUCKETS, "buckets"), (E.SCHED_SHARDED_FC, "sharded")):
+            self.exe.set_schedule(sched)
+            g = self._graph(G)
+            if g is None:  # capture unavailable: keep the default schedule
+                self.exe.set_schedule(E.SCHED_BUCKETS)
+                break
+            g.replay()
+            torch.cuda.synchronize(self.device)
+            t0 = torch.cuda.Event(enable_timing=True)
+            t1 = torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(TUNE_REPLAYS):
+                g.replay()
+            t1.record()
+            torch.cuda.synchronize(self.device)
+            steps += (1 + TUNE_REPLAYS) * G
+            us = D.allreduce_max_host(1000.0 * t0.elapsed_time(t1) / (TUNE_REPLAYS * G))
+            self.tune_log[name] = round(us, 2)
+            if best is None or us < best[0]:
+                best = (us, sched)
+        if best is not None:
+            self.exe.set_schedule(best[1])
+        self._tuned = True
+        self.step += steps
+        return steps
 
     def train(self, k: int) -> None:
         if k <= 0:
             return
+        if not self._tuned and k >= 2 * (1 + TUNE_REPLAYS) * self.graph_steps:
+            k -= self.tune_schedule()
         done = 0
         if self.use_graph:
             G = self.graph_steps
@@ -287,6 +368,7 @@ class NativeMnistEngine(MnistEngineBase):
                     done += rem
         for _ in range(k - done):  # eager (no graphs, or capture unavailable)
             self._launch_one()
+        self.exe.join(stream_handle())
         self.step += k
 
     def capture(self, k: int) -> None:
@@ -349,12 +431,12 @@ class NativeMnistEngine(MnistEngineBase):
 
 
 def make_engine(cfg: C.TrainConfig, train_x, train_y, device: torch.device, rank=0, world=1,
-                comm=None, backend: Optional[str] = None):
+                comm=None, backend: Optional[str] = None, force_sync: bool = False):
     backend = backend or cfg.backend
     if backend == "auto":
         backend = "native" if device.type == "cuda" else "torch"
     if cfg.dtype != "fp32" and backend != "native":
         raise NotImplementedError(f"dtype {cfg.dtype} needs the native (GPU) MNIST engine")
     if backend == "native":
-        return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm)
+        return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)
     return TorchMnistEngine(cfg, train_x, train_y, device, rank, world, comm)

@@ -232,6 +232,7 @@ class Trainer:
         return summary
 
     def save_checkpoint(self, path: str) -> None:
+        self.engine.sync_optimizer_state()  # sharded FC momentum -> whole buffer
         if self.rank == 0:
             ckpt_mod.save(path, self.engine.layout, self.engine.params, self.engine.mom,
                           self.engine.step, meta={"model": self.cfg.model, "world": self.world})

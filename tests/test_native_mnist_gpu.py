@@ -194,3 +194,26 @@ def test_native_rccl_comm_and_graph_capture(cuda_dev, data):
     plain.train(7)
     torch.cuda.synchronize()
     assert torch.equal(synced.params, plain.params)
+
+
+def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
+    """Startup autotune of the gradient-sync schedule (runtime/mnist_engine.py:
+    tune_schedule) against an emulated 8-rank ring (csrc/collective.h EmuComm):
+    both schedules are captured and timed, the faster one is kept, and the
+    tuning steps are real steps (step counter advances)."""
+    from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
+
+    x, y = data
+    comm = EmulatedDeviceComm(8, lat_us=10.0, busbw_gbps=150.0, blocks=32)
+    cfg = C.TrainConfig(graph=True, graph_steps=5).validate()
+    eng = NativeMnistEngine(cfg, x, y, cuda_dev, comm=comm, force_sync=True)
+    assert eng.sync_schedule == "buckets"  # until tuned
+    n = eng.tune_schedule()
+    assert n == 2 * 3 * 5 and eng.step == n
+    assert int(eng.step_dev.item()) == n
+    log = eng.tune_log
+    assert set(log) == {"buckets", "sharded"}
+    assert eng.sync_schedule == min(log, key=log.get)
+    eng.train(7)
+    torch.cuda.synchronize()
+    assert torch.isfinite(eng.params).all()
