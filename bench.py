@@ -44,7 +44,7 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
-    ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded"))
+    ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded", "split"))
     ap.add_argument("--comm-emulate", default=None, metavar="LAT_US,BUSBW_GBPS[,N[,BLOCKS]]",
                     help="1 GPU: replace the collectives by timing stand-ins of an N-rank ring "
                          "(default N=8, 32 workgroups) to measure sync/compute overlap")

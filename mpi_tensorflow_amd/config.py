@@ -63,7 +63,9 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # gradient-sync schedules of the native MNIST executor (grad sync, world > 1):
 # "buckets" = all-reduce FC bucket then conv bucket; "sharded" = reduce-scatter
 # FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
-SYNC_SCHEDULES = ("auto", "buckets", "sharded")
+# "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
+# compute stream over a second communicator
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split")
 DTYPES = ("fp32", "bf16")
 
 

@@ -340,11 +340,12 @@ PYBIND11_MODULE(_C, m) {
   py::class_<MnistExecutor>(m, "MnistExecutor")
       .def(py::init<const MnistPtrs&>())
       .def("train_step",
-           [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs) {
-             e.train_step(S(s), comm, S(cs));
+           [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs, Collective* comm2) {
+             e.train_step(S(s), comm, S(cs), comm2);
              check_launch();
            },
-           py::arg("stream"), py::arg("comm") = nullptr, py::arg("comm_stream") = 0)
+           py::arg("stream"), py::arg("comm") = nullptr, py::arg("comm_stream") = 0,
+           py::arg("comm2") = nullptr)
       .def("set_schedule", &MnistExecutor::set_schedule)
       .def_property_readonly("schedule", &MnistExecutor::schedule)
       .def("sharded_ok", &MnistExecutor::sharded_ok)
@@ -375,6 +376,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.attr("MnistExecutor").attr("SCHED_BUCKETS") = (int)MnistExecutor::SCHED_BUCKETS;
   m.attr("MnistExecutor").attr("SCHED_SHARDED_FC") = (int)MnistExecutor::SCHED_SHARDED_FC;
+  m.attr("MnistExecutor").attr("SCHED_SPLIT") = (int)MnistExecutor::SCHED_SPLIT;
 
   // ----------------------------------------------------------------- IDX
   m.def("idx_header", [](const std::string& path) {

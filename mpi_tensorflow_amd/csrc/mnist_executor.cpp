@@ -142,7 +142,7 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
 }
 
 void MnistExecutor::set_schedule(int sched) {
-  if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC)
+  if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -162,7 +162,8 @@ void MnistExecutor::wait_fc_params(hipStream_t s) {
 
 void MnistExecutor::join(hipStream_t s) { wait_fc_params(s); }
 
-void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs) {
+void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
+                               Collective* comm2) {
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
     enqueue_fwd_bwd(s);
     sgd(s, 1.0f);
@@ -170,6 +171,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs) 
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
     train_step_sharded(s, comm, cs);
+    return;
+  }
+  if (sched_ == SCHED_SPLIT && comm2 != nullptr && comm2->size() == comm->size()) {
+    train_step_split(s, comm, cs, comm2);
     return;
   }
   const MnistPtrs& p = p_;
@@ -225,6 +230,28 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   fc_pending_ = true;
   HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  sgd_range(s, p.bucket1, p.total, gscale, true);
+}
+
+// Split schedule: ONE fork and ONE join per step.  The FC all-reduce and the
+// FC momentum SGD run on the comm stream; the conv all-reduce (0.2 MB,
+// latency-bound) runs on the compute stream itself through a second
+// communicator (two ops on one communicator must not run concurrently), so it
+// costs a same-queue kernel boundary instead of two cross-queue hops; the
+// join sits in front of the NEXT step's fc1 forward, behind its conv forward.
+void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_t cs,
+                                     Collective* comm2) {
+  const MnistPtrs& p = p_;
+  float* G = P<float>(p.grads);
+  const float gscale = 1.0f / (float)comm->size();
+  enqueue_fwd_bwd(s);
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
+  comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
+  sgd_range(cs, 0, p.bucket1, gscale, false);
+  HIP_CHECK(hipEventRecord(ev_b1_, cs));
+  fc_pending_ = true;
+  comm2->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
+                    ncclSum, s);
   sgd_range(s, p.bucket1, p.total, gscale, true);
 }
 

@@ -63,13 +63,19 @@ class MnistExecutor {
   // Full training step.  comm may be null (single rank, or periodic
   // parameter averaging done by the caller); comm_stream is used only when
   // comm is attached.
-  void train_step(hipStream_t s, Collective* comm, hipStream_t comm_stream);
+  // comm2 (optional): second communicator of the same ranks, used by
+  // SCHED_SPLIT for the conv bucket on the compute stream.
+  void train_step(hipStream_t s, Collective* comm, hipStream_t comm_stream,
+                  Collective* comm2 = nullptr);
   // Gradient-sync schedule used when a communicator of size > 1 is attached:
   //   SCHED_BUCKETS    - all-reduce of bucket 1 (FC) then bucket 2 (conv);
   //   SCHED_SHARDED_FC - reduce-scatter FC grads, SGD on the local 1/N shard,
   //                      all-gather FC params overlapped with the next
-  //                      step's conv forward (see train_step_sharded).
-  static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1;
+  //                      step's conv forward (see train_step_sharded);
+  //   SCHED_SPLIT      - FC all-reduce + FC SGD on the comm stream, conv
+  //                      all-reduce on the compute stream via comm2 (one
+  //                      fork + one join per step, see train_step_split).
+  static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
@@ -97,6 +103,7 @@ class MnistExecutor {
  private:
   void enqueue_fwd_bwd(hipStream_t s);
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
+  void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void wait_fc_params(hipStream_t s);
   int sched_ = SCHED_BUCKETS;
   bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on

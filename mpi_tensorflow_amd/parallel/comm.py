@@ -59,6 +59,10 @@ class DeviceComm:
     def native_handle(self):
         return None
 
+    def duplicate(self) -> "DeviceComm":
+        """A second communicator over the same ranks (collective call)."""
+        raise NotImplementedError
+
 
 class RcclDeviceComm(DeviceComm):
     kind = "rccl-native"
@@ -71,6 +75,10 @@ class RcclDeviceComm(DeviceComm):
             dist.broadcast_object_list(objs, src=0)
         self._c = C.RcclComm(objs[0], di.world, di.rank)
         self.rank, self.size = di.rank, di.world
+        self._di = di
+
+    def duplicate(self):
+        return RcclDeviceComm(self._di)
 
     def _check(self, t: torch.Tensor):
         if not t.is_cuda or not t.is_contiguous() or t.dtype not in _DT:
@@ -120,6 +128,7 @@ class EmulatedDeviceComm(DeviceComm):
     def __init__(self, nranks: int, lat_us: float, busbw_gbps: float, blocks: int = 32,
                  rank: int = 0):
         self._c = native().EmuComm(nranks, rank, lat_us, busbw_gbps, blocks)
+        self._args = (nranks, lat_us, busbw_gbps, blocks, rank)
         self.rank, self.size = rank, nranks
         self.kind = f"emulated(n={nranks},lat={lat_us}us,busbw={busbw_gbps}GB/s,blocks={blocks})"
 
@@ -134,6 +143,9 @@ class EmulatedDeviceComm(DeviceComm):
     @property
     def native_handle(self):
         return self._c
+
+    def duplicate(self):
+        return EmulatedDeviceComm(*self._args)
 
 
 class HostStagedComm(DeviceComm):
@@ -192,6 +204,9 @@ class HostStagedComm(DeviceComm):
     @property
     def native_handle(self):
         return self._c
+
+    def duplicate(self):
+        return self  # synchronous host staging: one object serves both streams
 
 
 class TorchDeviceComm(DeviceComm):

@@ -37,13 +37,13 @@ from ..utils import rng
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
-# sync_schedule="auto": both gradient-sync schedules are timed on the first
-# train() call of at least TUNE_REPLAYS * 2 * graph_steps steps (real training
-# steps, bit-identical under either schedule) and the faster one is kept; all
-# ranks take the decision from the same (max-over-ranks) timings.  Which one
-# wins depends on the all-reduce bandwidth: with a comm-emulated ring
-# (bench.py --comm-emulate) the sharded FC update was 4-6 % faster at 100-200
-# GB/s bus bandwidth and 5 % slower at 400 GB/s (docs/PERF_NOTES.md).
+# sync_schedule="auto": the gradient-sync schedules (buckets / sharded /
+# split, csrc/mnist_executor.h) are timed on the first train() call of at
+# least tune_steps() steps (real training steps, bit-identical under every
+# schedule) and the fastest is kept; all ranks take the decision from the same
+# (max-over-ranks) timings.  With a comm-emulated 8-rank ring (bench.py
+# --comm-emulate, docs/PERF_NOTES.md) split won at every bus bandwidth tried
+# (100-800 GB/s); sharded beat buckets below ~250 GB/s.
 TUNE_REPLAYS = 2
 
 
@@ -242,6 +242,10 @@ class NativeMnistEngine(MnistEngineBase):
         self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
         if self.grad_sync and self._native_comm is None:
             raise RuntimeError("grad sync on the native engine needs the native RCCL communicator")
+        self.comm2 = None  # second communicator (split schedule: conv bucket on the compute stream)
+        if self.grad_sync and cfg.sync_schedule in ("auto", "split"):
+            self.comm2 = self.comm.duplicate()
+        self._native_comm2 = self.comm2.native_handle if self.comm2 is not None else None
         if self.grad_sync:
             self.exe.set_schedule(self._pick_schedule(cfg.sync_schedule, self._native_comm.size))
         if getattr(self.comm, "kind", "") == "host-staged":  # test comm: eager only
@@ -253,9 +257,15 @@ class NativeMnistEngine(MnistEngineBase):
                            and self.exe.sharded_ok(self._native_comm.size))
         self.tune_log: Dict[str, float] = {}
         self._eval_ws = None
-        if self.grad_sync:  # connection setup outside any capture
-            self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), lay.total,
-                                         7, 0, stream_handle())
+        if self.grad_sync:  # connection setup of every collective used, outside any capture
+            c, g, n, hs = self._native_comm, ptr(self.grads), lay.total, stream_handle()
+            c.all_reduce(g, g, n, 7, 0, hs)
+            if self.exe.sharded_ok(c.size):  # grads are zero: RS / AG leave them zero
+                chunk = self.ptrs.bucket1 // c.size
+                c.reduce_scatter(g, g + 4 * chunk * c.rank, chunk, 7, 0, hs)
+                c.all_gather(g + 4 * chunk * c.rank, g, chunk, 7, hs)
+            if self._native_comm2 is not None:
+                self._native_comm2.all_reduce(g, g, n, 7, 0, hs)
             torch.cuda.synchronize(dev)
 
     def set_step(self, step: int) -> None:
@@ -264,18 +274,21 @@ class NativeMnistEngine(MnistEngineBase):
 
     def _pick_schedule(self, name: str, nranks: int) -> int:
         E = self._C.MnistExecutor
-        if name == "buckets" or not self.exe.sharded_ok(nranks):
+        if name == "buckets":
             return E.SCHED_BUCKETS
-        if name == "sharded":
+        if name == "sharded" and self.exe.sharded_ok(nranks):
             return E.SCHED_SHARDED_FC
-        return E.SCHED_BUCKETS  # "auto": until tune_schedule() has timed both
+        if name == "split" or (name == "auto" and self._native_comm2 is not None):
+            return E.SCHED_SPLIT  # "auto": the best in every emulated-ring point, until tuned
+        return E.SCHED_BUCKETS
 
     @property
     def sync_schedule(self) -> str:
         if not self.grad_sync:
             return "none"
         E = self._C.MnistExecutor
-        return "sharded" if self.exe.schedule == E.SCHED_SHARDED_FC else "buckets"
+        return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split"}.get(self.exe.schedule,
+                                                                          "buckets")
 
     def sync_optimizer_state(self) -> None:
         if self.grad_sync:
@@ -285,7 +298,7 @@ class NativeMnistEngine(MnistEngineBase):
     # --------------------------------------------------------------- steps
     def _launch_one(self):
         cs = stream_handle(self.comm_stream) if self.comm_stream is not None else 0
-        self.exe.train_step(stream_handle(), self._native_comm, cs)
+        self.exe.train_step(stream_handle(), self._native_comm, cs, self._native_comm2)
 
     def _graph(self, n: int) -> Optional[torch.cuda.CUDAGraph]:
         key = (self.exe.schedule, n)
@@ -310,6 +323,10 @@ class NativeMnistEngine(MnistEngineBase):
             self._graphs[key] = g
         return g
 
+    def tune_steps(self) -> int:
+        return 0 if self._tuned else \
+            (3 if self._native_comm2 is not None else 2) * (1 + TUNE_REPLAYS) * self.graph_steps
+
     def tune_schedule(self) -> int:
         """Times TUNE_REPLAYS graph replays of each sync schedule (after one
         untimed replay each) and keeps the faster; returns the number of
@@ -321,7 +338,10 @@ class NativeMnistEngine(MnistEngineBase):
         G = self.graph_steps
         steps = 0
         best = None
-        for sched, name in ((E.SCHED_BUCKETS, "buckets"), (E.SCHED_SHARDED_FC, "sharded")):
+        cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SHARDED_FC, "sharded")]
+        if self._native_comm2 is not None:
+            cands.append((E.SCHED_SPLIT, "split"))
+        for sched, name in cands:
             self.exe.set_schedule(sched)
             g = self._graph(G)
             if g is None:  # capture unavailable: keep the default schedule
@@ -350,7 +370,7 @@ class NativeMnistEngine(MnistEngineBase):
     def train(self, k: int) -> None:
         if k <= 0:
             return
-        if not self._tuned and k >= 2 * (1 + TUNE_REPLAYS) * self.graph_steps:
+        if not self._tuned and k >= self.tune_steps():
             k -= self.tune_schedule()
         done = 0
         if self.use_graph:

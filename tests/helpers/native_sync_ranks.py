@@ -35,9 +35,10 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     dtype = sys.argv[2] if len(sys.argv) > 2 else "fp32"
     pb, mb = run("buckets", dtype, steps, di)
-    ps, ms = run("sharded", dtype, steps, di)
-    assert torch.equal(pb, ps), f"params differ: {(pb - ps).abs().max().item()}"
-    assert torch.equal(mb, ms), f"momentum differs: {(mb - ms).abs().max().item()}"
+    for sched in ("sharded", "split"):
+        ps, ms = run(sched, dtype, steps, di)
+        assert torch.equal(pb, ps), f"{sched}: params differ: {(pb - ps).abs().max().item()}"
+        assert torch.equal(mb, ms), f"{sched}: momentum differs: {(mb - ms).abs().max().item()}"
     ref = pb.clone()
     dist.broadcast(ref, 0)
     assert torch.equal(ref, pb), "replicas diverged"
