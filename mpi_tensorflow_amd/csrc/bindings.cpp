@@ -114,13 +114,15 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("fc1_bwd", [](uintptr_t a2, uintptr_t idx2, uintptr_t dh, uintptr_t hd, uintptr_t dlog,
                       uintptr_t w1, int batch, uintptr_t g_w3, uintptr_t g_b3, uintptr_t g_w4,
-                      uintptr_t g_b4, uintptr_t dy2, uintptr_t dy2t, uintptr_t s) {
+                      uintptr_t g_b4, uintptr_t dy2, uintptr_t dy2t, uintptr_t s, int roles) {
     mnist::launch_fc1_bwd(P<const float>(a2), P<const uint8_t>(idx2), P<const float>(dh),
                           P<const float>(hd), P<const float>(dlog), P<const float>(w1), batch,
                           P<float>(g_w3), P<float>(g_b3), P<float>(g_w4), P<float>(g_b4),
-                          P<float>(dy2), P<float>(dy2t), S(s));
+                          P<float>(dy2), P<float>(dy2t), S(s), roles);
     check_launch();
-  });
+  }, py::arg("a2"), py::arg("idx2"), py::arg("dh"), py::arg("hd"), py::arg("dlog"), py::arg("w1"),
+     py::arg("batch"), py::arg("g_w3"), py::arg("g_b3"), py::arg("g_w4"), py::arg("g_b4"),
+     py::arg("dy2"), py::arg("dy2t"), py::arg("stream"), py::arg("roles") = 7);
   k.def("conv2_bwd_data", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
                              uintptr_t s) {
     mnist::launch_conv2_bwd_data(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,

@@ -30,7 +30,8 @@ void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const
 // [B][64][18][MNIST32_T_LD]
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
-                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s);
+                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
+                    int roles = 7);  // roles: bit 0 dX, bit 1 dW1, bit 2 small grads (profiling)
 int conv2_filter_splits(int batch);
 void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
                            float* da1m, hipStream_t s);

@@ -342,116 +342,187 @@ __global__ __launch_bounds__(256) void fc_head_eval_kernel(const float* __restri
 }
 
 // ------------------------------------------------------------- fc1 bwd ----
-// dW1 = a2^T dh : M = 3136 (fc1 in), N = 512, K = batch
-struct Fc1DwProb {
-  static constexpr bool A_KC = false, B_NC = true;
-  struct ACtx {
-    const float* p;
-    int kl;
-  };
-  using BCtx = ACtx;
-  const float* a2;  // [B][3136]
-  const float* dh;  // [B][512]
-  int batch;
-  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return {a2 + kl * FC1_IN + m, kl}; }
-  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const {
-    const int k = k0 + c.kl;
-    const float v = c.p[(min(k, batch - 1) - c.kl) * FC1_IN];
-    return k < batch ? v : 0.f;
+// One launch, three block roles; every block is 4 waves and no operand goes
+// through LDS (the previous LDS-staged version was a serial chain of 8 K tiles,
+// 17.6 us in graph replay):
+//  * dX   dA2 = dh W1^T (M = batch, N = 3136, K = 512), one 32x32 tile per
+//         block, K split over the 4 waves (128 each).  Both operands have k
+//         contiguous, but the fp32 MFMA wants one k per lane with lanes on
+//         rows, so each wave loads its rows coalesced (float4, lanes along k,
+//         all 32 loads in flight) and transposes them through a wave-private
+//         LDS image (no block barrier).  Loading the fragments directly
+//         (32 rows = 32 cache lines per wave load) measured 11 us; the
+//         staged form touches 8x fewer lines.  Partial tiles are summed
+//         through LDS; wave 0 applies the ReLU2 mask and scatters through the
+//         pool2 argmax into dY2 (NHWC, filter-grad operand) and dY2t
+//         (channel-major, bwd-data operand).
+//  * dW1  M = 3136 features, N = 512, K = batch; block = 32 features x 256
+//         hidden (each wave 32x64 with one shared A fragment); lanes on the
+//         contiguous axis of a2 / dh (one 128-B line per half-wave), K in
+//         chunks of 32 MFMA steps with all loads of a chunk in flight.
+//  * fc2 weight / bias and fc1 bias grads (fc1_small_grads).
+// Logical block ids are XCD-remapped so the two M tiles of a dX N tile (same
+// W1 rows) and the two halves of a dW1 M tile (same a2 columns) share an L2.
+constexpr int FC1BWD_DW_BLOCKS = (FC1_IN / 32) * (FC1_OUT / 256);  // 196
+
+constexpr int FC1DX_LD = 33;                     // LDS row (k) length: 32 rows + 1
+constexpr int FC1DX_WAVE = 2 * 64 * FC1DX_LD;    // per-wave LDS: A and B, 64 k each
+
+__device__ __forceinline__ void fc1_bwd_dx(int L, const float* __restrict__ a2,
+                                           const uint8_t* __restrict__ idx2,
+                                           const float* __restrict__ dh,
+                                           const float* __restrict__ w1, int batch,
+                                           float* __restrict__ dy2, float* __restrict__ dy2t,
+                                           float* smem) {
+  const int n_m = batch / 32;
+  const int mt = L % n_m, nt = L / n_m;
+  const int m0 = mt * 32, n0 = nt * 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  // wave-private LDS transpose: coalesced float4 row loads (lanes along k,
+  // 4 rows x 256 B per wave load) -> k-major [64][33] images -> one k per lane
+  float* TA = smem + wave * FC1DX_WAVE;
+  float* TB = TA + 64 * FC1DX_LD;
+  const int lr = lane >> 4, lk = (lane & 15) * 4;
+  const float* ap = dh + (size_t)(m0 + lr) * FC1_OUT + wave * 128 + lk;
+  const float* bp = w1 + (size_t)(n0 + lr) * FC1_OUT + wave * 128 + lk;
+  float4 a[2][8], b[2][8];
+#pragma unroll
+  for (int rho = 0; rho < 2; ++rho)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[rho][i] = *reinterpret_cast<const float4*>(ap + (size_t)4 * i * FC1_OUT + 64 * rho);
+      b[rho][i] = *reinterpret_cast<const float4*>(bp + (size_t)4 * i * FC1_OUT + 64 * rho);
+    }
+  // epilogue operands of this wave's 4 accumulator registers (k = 4 wave + j),
+  // prefetched so their latency hides under the MFMAs
+  const int fi = n0 + r;  // (py, px, co) flat feature index
+  float relu_in[4];
+  int qsel[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = m0 + mfma32_row(4 * wave + j, lane);
+    relu_in[j] = a2[(size_t)n * FC1_IN + fi];
+    qsel[j] = idx2[(size_t)n * FC1_IN + fi];
   }
-  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {dh + kl * FC1_OUT + n, kl}; }
-  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const {
-    const int k = k0 + c.kl;
-    const float v = c.p[(min(k, batch - 1) - c.kl) * FC1_OUT];
-    return k < batch ? v : 0.f;
+  f32x16 c0 = zero16(), c1 = zero16();
+#pragma unroll
+  for (int rho = 0; rho < 2; ++rho) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = 4 * i + lr;
+      TA[(lk + 0) * FC1DX_LD + row] = a[rho][i].x;
+      TA[(lk + 1) * FC1DX_LD + row] = a[rho][i].y;
+      TA[(lk + 2) * FC1DX_LD + row] = a[rho][i].z;
+      TA[(lk + 3) * FC1DX_LD + row] = a[rho][i].w;
+      TB[(lk + 0) * FC1DX_LD + row] = b[rho][i].x;
+      TB[(lk + 1) * FC1DX_LD + row] = b[rho][i].y;
+      TB[(lk + 2) * FC1DX_LD + row] = b[rho][i].z;
+      TB[(lk + 3) * FC1DX_LD + row] = b[rho][i].w;
+    }
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      const float av = TA[(2 * t + h) * FC1DX_LD + r], bv = TB[(2 * t + h) * FC1DX_LD + r];
+      if (t & 1)
+        c1 = mfma32x32x2(av, bv, c1);
+      else
+        c0 = mfma32x32x2(av, bv, c0);
+    }
   }
-};
+  // K reduction over the 4 waves through LDS (each wave's own region, now
+  // free), then every wave finishes 4 of the 16 accumulator registers
+#pragma unroll
+  for (int k = 0; k < 16; ++k) TA[k * 64 + lane] = c0[k] + c1[k];
+  __syncthreads();
+  if (dy2 == nullptr) {  // profiling variant (roles bit 3): no scatter epilogue
+    if (smem[lane] == 12345.f) smem[64 + lane] = 0.f;
+    return;
+  }
+  const int co = fi & 63, pp = fi >> 6, py = pp / 7, px = pp % 7;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = 4 * wave + j;
+    const int n = m0 + mfma32_row(k, lane);
+    float g = smem[k * 64 + lane] + smem[FC1DX_WAVE + k * 64 + lane] +
+              smem[2 * FC1DX_WAVE + k * 64 + lane] + smem[3 * FC1DX_WAVE + k * 64 + lane];
+    if (relu_in[j] <= 0.f) g = 0.f;  // ReLU2 inactive at the argmax
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      const int y = 2 * py + dy, x = 2 * px;
+      const float v0 = (qsel[j] == 2 * dy) ? g : 0.f, v1 = (qsel[j] == 2 * dy + 1) ? g : 0.f;
+      dy2[((n * 14 + y) * 14 + x) * 64 + co] = v0;
+      dy2[((n * 14 + y) * 14 + x + 1) * 64 + co] = v1;
+      // x + 2 is even and MNIST32_T_LD is even: one 8-byte store per row pair
+      if (dy2t != nullptr)
+        *reinterpret_cast<float2*>(dy2t + ((size_t)(n * 64 + co) * 18 + y + 2) * MNIST32_T_LD +
+                                   x + 2) = make_float2(v0, v1);
+    }
+  }
+}
 
-// dA2 = dh W1^T : M = batch, N = 3136, K = 512
-struct Fc1DxProb {
-  static constexpr bool A_KC = true, B_NC = false;
-  using ACtx = gemm::RowMajorA::Ctx;
-  struct BCtx {
-    const float* p;
-  };
-  gemm::RowMajorA A;  // dh [B][512]
-  const float* w1;
-  __device__ __forceinline__ ACtx a_ctx(int m, int kl) const { return A.ctx(m, kl); }
-  __device__ __forceinline__ float a_get(const ACtx& c, int k0) const { return A.get(c, k0); }
-  __device__ __forceinline__ BCtx b_ctx(int kl, int n) const { return {w1 + n * FC1_OUT + kl}; }
-  __device__ __forceinline__ float b_get(const BCtx& c, int k0) const { return c.p[k0]; }
-};
-
-constexpr int FC1BWD_BK = 64;
-constexpr int FC1BWD_DW_WM = 2, FC1BWD_DW_WN = 2;  // 64x64 tiles, 4 waves
-constexpr int FC1BWD_DX_WK = 4;                    // 32x32 tiles, K split over 4 waves
-
-// fc1 backward, one launch: blocks [0, n_dx) compute dX (+ the pool2/ReLU2
-// backward scatter into dY2, the critical path), then dW1 tiles, then the
-// small fc2/bias grads.  All roles fit 33 KB of LDS (4 blocks per CU).
-constexpr int FC1BWD_DW_BK = 32;
+__device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
+                                           const float* __restrict__ dh, int batch,
+                                           float* __restrict__ g_w3) {
+  const int mt = L >> 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
+  const int m0 = mt * 32, n0 = (L & 1) * 256 + wave * 64;
+  const float* ap = a2 + m0 + r;
+  const float* bp = dh + n0 + r;
+  f32x16 c0 = zero16(), c1 = zero16();
+  for (int k0 = 0; k0 < batch; k0 += 64) {  // 32 MFMA steps (k = k0 + 2t + h)
+    float av[32], b0[32], b1[32];
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      const int k = k0 + 2 * t + h;
+      const int kc = min(k, batch - 1);
+      const bool ok = k < batch;
+      const float x = ap[(size_t)kc * FC1_IN];
+      const float y0 = bp[kc * FC1_OUT], y1 = bp[kc * FC1_OUT + 32];
+      av[t] = ok ? x : 0.f;
+      b0[t] = y0;
+      b1[t] = y1;
+    }
+#pragma unroll
+    for (int t = 0; t < 32; ++t) {
+      c0 = mfma32x32x2(av[t], b0[t], c0);
+      c1 = mfma32x32x2(av[t], b1[t], c1);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int m = m0 + mfma32_row(k, lane);
+    g_w3[(size_t)m * FC1_OUT + n0 + r] = c0[k];
+    g_w3[(size_t)m * FC1_OUT + n0 + 32 + r] = c1[k];
+  }
+}
 
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
     const float* __restrict__ hd, const float* __restrict__ dlog, const float* __restrict__ w1,
     int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
-    float* __restrict__ g_b4, float* __restrict__ dy2, float* __restrict__ dy2t) {
-  // dy2: NHWC [n][14][14][64] (filter-grad operand); dy2t: channel-major,
-  // zero-bordered [n][64][18][MNIST32_T_LD] (bwd-data operand)
-  using CDX = gemm::Cfg<1, 1, FC1BWD_DX_WK, FC1BWD_BK, true, false>;
-  using CDW = gemm::Cfg<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_DW_BK, false, true>;
-  constexpr int S1 = CDX::SMEM_FLOATS, S2 = CDW::SMEM_FLOATS, S3 = 4 * (NCLS + 1) * 64;
-  constexpr int SM = S1 > S2 ? (S1 > S3 ? S1 : S3) : (S2 > S3 ? S2 : S3);
-  __shared__ float smem[SM];
-  const int n_dx_m = (batch + 31) / 32;
-  const int n_dx = n_dx_m * (FC1_IN / 32);
-  const int n_dw = (FC1_IN / CDW::BM) * (FC1_OUT / CDW::BN);
-  int bid = blockIdx.x;
-  const int lane = threadIdx.x & 63;
-  f32x16 acc;
-  int wm, wn;
-  if (bid < n_dx) {
-    Fc1DxProb p{{dh, FC1_OUT, batch}, w1};
-    const int m0 = (bid % n_dx_m) * 32, n0 = (bid / n_dx_m) * 32;
-    if (!gemm::run_tile<1, 1, FC1BWD_DX_WK, FC1BWD_BK>(p, smem, m0, n0, 0, FC1_OUT, acc, wm, wn))
+    float* __restrict__ g_b4, float* __restrict__ dy2, float* __restrict__ dy2t, int roles) {
+  // dy2: NHWC [n][14][14][64]; dy2t: channel-major, zero-bordered
+  // [n][64][18][MNIST32_T_LD] (its border is never written)
+  constexpr int S_DX = 4 * FC1DX_WAVE, S_SMALL = 4 * (NCLS + 1) * 64;
+  __shared__ float smem[S_DX > S_SMALL ? S_DX : S_SMALL];
+  const int n_dx = (batch / 32) * (FC1_IN / 32);
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  const int role = L < n_dx ? 0 : (L < n_dx + FC1BWD_DW_BLOCKS ? 1 : 2);
+  if (!((roles >> role) & 1)) return;
+  if (L < n_dx) {
+    if (roles & 8) {  // profiling: dX without the scatter epilogue
+      fc1_bwd_dx(L, a2, idx2, dh, w1, batch, nullptr, nullptr, smem);
       return;
-    const int i = n0 + (lane & 31);  // (py, px, co) flat
-    const int co = i & 63, pp = i >> 6, py = pp / 7, px = pp % 7;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int n = m0 + mfma32_row(r, lane);
-      if (n >= batch) continue;
-      float g = acc[r];
-      if (a2[n * FC1_IN + i] <= 0.f) g = 0.f;  // ReLU2 inactive at the argmax
-      const int q = idx2[n * FC1_IN + i];
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
-        const float v = (d == q) ? g : 0.f;
-        dy2[((n * 14 + y) * 14 + x) * 64 + co] = v;
-        dy2t[((size_t)(n * 64 + co) * 18 + y + 2) * MNIST32_T_LD + x + 2] = v;
-      }
     }
-    return;
-  }
-  bid -= n_dx;
-  if (bid < n_dw) {
-    Fc1DwProb p{a2, dh, batch};
-    constexpr int mt = FC1_IN / CDW::BM;  // 49
-    const int m0 = (bid % mt) * CDW::BM, n0 = (bid / mt) * CDW::BN;
-    const int kend = (batch + FC1BWD_DW_BK - 1) / FC1BWD_DW_BK * FC1BWD_DW_BK;
-    gemm::run_tile<FC1BWD_DW_WM, FC1BWD_DW_WN, 1, FC1BWD_DW_BK>(p, smem, m0, n0, 0, kend, acc, wm,
-                                                                wn);
-    const int n = n0 + 32 * wn + (lane & 31);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + 32 * wm + mfma32_row(r, lane);
-      g_w3[m * FC1_OUT + n] = acc[r];
+    if (roles & 16) {  // profiling: dX without the channel-major dY2t copy
+      fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, nullptr, smem);
+      return;
     }
-    return;
+    fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, dy2t, smem);
+  } else if (L < n_dx + FC1BWD_DW_BLOCKS) {
+    fc1_bwd_dw(L - n_dx, a2, dh, batch, g_w3);
+  } else {
+    fc1_small_grads(L - n_dx - FC1BWD_DW_BLOCKS, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
   }
-  bid -= n_dw;
-  fc1_small_grads(bid, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
 }
 
 // ------------------------------------------ conv2: dedicated MFMA kernels ----
@@ -1080,11 +1151,13 @@ void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const
 
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
-                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s) {
-  const int n_dx = cdiv(batch, 32) * (FC1_IN / 32);
-  const int n_dw = (FC1_IN / (32 * FC1BWD_DW_WM)) * (FC1_OUT / (32 * FC1BWD_DW_WN));
-  fc1_bwd_kernel<<<n_dx + n_dw + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
-                                                            g_w3, g_b3, g_w4, g_b4, dy2, dy2t);
+                    float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
+                    int roles) {
+  if (batch <= 0 || batch % 32 != 0) throw std::runtime_error("fc1_bwd: batch % 32 != 0");
+  const int n_dx = (batch / 32) * (FC1_IN / 32);
+  fc1_bwd_kernel<<<n_dx + FC1BWD_DW_BLOCKS + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
+                                                            g_w3, g_b3, g_w4, g_b4, dy2, dy2t,
+                                                            roles);
 }
 
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }

@@ -20,6 +20,8 @@ MnistExecutor::MnistExecutor(const MnistPtrs& p) : p_(p) {
   if (p_.total % 4 != 0 || p_.l2_end % 4 != 0 || p_.bucket1 % 4 != 0 || p_.l2_end > p_.bucket1)
     throw std::runtime_error(
         "MnistExecutor: flat segments must be multiples of 4 floats with the L2 prefix in bucket 1");
+  // (hipEventDisableSystemFence / hipEventReleaseToDevice on these events
+  // changed nothing in graph replay: captured edges do not use the flags)
   for (hipEvent_t* e : {&ev_dw_, &ev_b1_, &ev_fin_, &ev_done_})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }

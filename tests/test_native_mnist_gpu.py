@@ -70,8 +70,11 @@ def test_conv_pool_forward_matches_oracle(cuda_dev, data):
     assert torch.equal(i1[pos], code[pos])
 
 
-def test_forward_backward_grads_match_oracle(cuda_dev, data):
-    nat, ref = _engines(cuda_dev, data)
+@pytest.mark.parametrize("batch", [64, 96, 128])
+def test_forward_backward_grads_match_oracle(cuda_dev, data, batch):
+    """All grads of one native step vs the fp32 PyTorch oracle; batch 96
+    exercises the partial K chunk of the fc1 dW role (K = batch)."""
+    nat, ref = _engines(cuda_dev, data, batch_size=batch)
     nat.set_step(7)
     ref.set_step(7)
     nat.forward_backward_only()
@@ -88,6 +91,7 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data):
     """Strict per-step check: at every step the native grads equal the oracle's
     grads evaluated at the NATIVE parameters (no chaotic accumulation)."""
     nat, ref = _engines(cuda_dev, data)
+    ties = 0
     for step in range(12):
         ref.params.copy_(nat.params)
         ref.set_step(step)
@@ -98,11 +102,15 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data):
         errs = {s.name: ((nv[s.name] - rv[s.name]).norm() / rv[s.name].norm()).item()
                 for s in nat.layout.specs}
         print(step, {k: f"{v:.1e}" for k, v in errs.items()})
-        # a max-pool near-tie (fp32 summation order) can re-route single
-        # elements; everything else must agree to fp32 rounding
+        # a max-pool near-tie (fp32 summation order) can re-route a single
+        # element of dY2 / dA1, which shifts the conv grads (never the FC
+        # grads) by ~1e-3; everything else must agree to fp32 rounding
         assert max(errs.values()) < 5e-3, (step, errs)
-        assert sorted(errs.values())[len(errs) // 2] < 1e-4, (step, errs)
+        assert max(v for k, v in errs.items() if k.startswith("fc")) < 1e-4, (step, errs)
+        if max(errs.values()) > 1e-4:
+            ties += 1
         nat.train(1)
+    assert ties <= 2, ties
 
 
 def test_training_trajectory_matches_oracle(cuda_dev, data):
