@@ -26,19 +26,28 @@ def model_input_shape(name: str) -> Tuple[int, int, int]:
     return {"lenet5": (32, 32, 3), "resnet18": (224, 224, 3)}[name]
 
 
+BUCKET_BYTES = 8 << 20  # target gradient bytes per all-reduce bucket
+MAX_BUCKETS = 8
+
+
 class GenericModel:
     name = "generic"
     num_classes = 10
 
     def __init__(self):
         self.specs: List[ParamSpec] = self._specs()
-        # buckets: ~4 contiguous groups in backward order (reverse forward)
-        n = len(self.specs)
+        # all-reduce buckets: contiguous groups in backward order (reverse
+        # forward) of ~BUCKET_BYTES each.  Every extra bucket costs a
+        # cross-queue fork/join (~5-10 us each in graph replay, PERF_NOTES),
+        # so small models get ONE bucket, reduced on the compute stream.
         flat_order = list(reversed(self.specs))
-        nb = min(4, n)
-        sized = []
-        for i, s in enumerate(flat_order):
-            sized.append(ParamSpec(s.name, s.tf_name, s.shape, s.init, s.l2, bucket=(i * nb) // n))
+        total = sum(4 * s.numel for s in flat_order)
+        nb = max(1, min(MAX_BUCKETS, -(-total // BUCKET_BYTES)))
+        sized, acc = [], 0
+        for s in flat_order:
+            b = min(nb - 1, (acc * nb) // total)
+            acc += 4 * s.numel
+            sized.append(ParamSpec(s.name, s.tf_name, s.shape, s.init, s.l2, bucket=b))
         self.layout = FlatLayout.build(sized)
         self.bn_channels: Dict[str, int] = self._bn()
 

@@ -16,7 +16,10 @@ in buckets on a dedicated comm stream while the backward pass continues:
   all-reduce is issued there;
 * `finish()` issues any bucket that was never completed (parameters without
   a gradient this step) and joins the comm stream back into the compute
-  stream before the optimizer.
+  stream before the optimizer;
+* a model whose gradients fit in one bucket (models/generic.py BUCKET_BYTES:
+  LeNet-5) all-reduces on the compute stream itself, after backward: a
+  cross-queue fork + join would cost more than the overlap saves.
 
 All of it is stream/event work, so it is captured into the step's hipGraph
 together with the compute (the RCCL communicator must have run once before
@@ -60,6 +63,9 @@ class BucketedAllReduce:
     def _launch(self, b: int) -> None:
         self.launched[b] = True
         self.order.append(b)
+        if len(self.slices) == 1:  # one bucket: no overlap to gain, no cross-queue hop
+            self.comm.all_reduce_(self.slices[b], stream=torch.cuda.current_stream())
+            return
         ev = self.events[b]
         ev.record(torch.cuda.current_stream())
         self.stream.wait_event(ev)
@@ -80,4 +86,5 @@ class BucketedAllReduce:
         for b in range(len(self.slices)):
             if not self.launched[b]:
                 self._launch(b)
-        torch.cuda.current_stream().wait_stream(self.stream)
+        if len(self.slices) > 1:
+            torch.cuda.current_stream().wait_stream(self.stream)

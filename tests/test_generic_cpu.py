@@ -20,7 +20,8 @@ def test_param_counts():
     assert model_input_shape("resnet18") == (224, 224, 3)
     # buckets are contiguous, in backward (reverse forward) order
     buckets = [s.bucket for s in rn.layout.specs]
-    assert buckets == sorted(buckets) and len(set(buckets)) == 4
+    assert buckets == sorted(buckets) and len(set(buckets)) == 6  # ~8 MB buckets of 44.7 MB
+    assert {s.bucket for s in le.layout.specs} == {0}  # LeNet-5: one 250 KB bucket
     assert rn.layout.specs[0].name == "fc_b" or rn.layout.specs[0].name == "fc_w"
 
 
