@@ -63,13 +63,15 @@ PYBIND11_MODULE(_C, m) {
 
   // ------------------------------------------------------------- kernels
   auto k = m.def_submodule("mnist", "fused fp32 MNIST CNN kernels (gfx950 MFMA)");
+  k.def("set_variant", &mnist::set_variant, py::arg("slot"), py::arg("value"));
   k.def("conv1_fwd", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w,
-                        uintptr_t b, uintptr_t out, uintptr_t argmax, uintptr_t s) {
+                        uintptr_t b, uintptr_t out, uintptr_t argmax, uintptr_t s, uintptr_t out_pad) {
     mnist::launch_conv1_fwd(P<const float>(data), P<const long long>(step), n_local, batch,
                             P<const float>(w), P<const float>(b), P<float>(out), P<uint8_t>(argmax),
-                            S(s));
+                            S(s), P<float>(out_pad));
     check_launch();
-  });
+  }, py::arg("data"), py::arg("step"), py::arg("n_local"), py::arg("batch"), py::arg("w"),
+     py::arg("b"), py::arg("out"), py::arg("argmax"), py::arg("stream"), py::arg("out_pad") = 0);
   k.def("conv2_fwd", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t b, uintptr_t out,
                         uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
     mnist::launch_conv2_fwd(P<const float>(a1), batch, P<const float>(w), P<const float>(b),
@@ -135,8 +137,8 @@ PYBIND11_MODULE(_C, m) {
                                     batch, P<float>(da1m), S(s));
     check_launch();
   });
-  k.def("conv2_bwd_filter", [](uintptr_t a1, uintptr_t dy2, int batch, uintptr_t part2, uintptr_t s) {
-    mnist::launch_conv2_bwd_filter(P<const float>(a1), P<const float>(dy2), batch, P<float>(part2),
+  k.def("conv2_bwd_filter", [](uintptr_t a1p, uintptr_t dy2, int batch, uintptr_t part2, uintptr_t s) {
+    mnist::launch_conv2_bwd_filter(P<const float>(a1p), P<const float>(dy2), batch, P<float>(part2),
                                    S(s));
     check_launch();
   });
@@ -284,7 +286,7 @@ PYBIND11_MODULE(_C, m) {
               RW(l2_end) RW(bucket1) RW(off_w4) RW(off_b4) RW(off_w3) RW(off_b3) RW(off_w2)
                   RW(off_b2) RW(off_w1) RW(off_b1) RW(step) RW(lr) RW(correct) RW(a1) RW(idx1)
                       RW(a2) RW(idx2) RW(fc1_part) RW(hd) RW(dh) RW(dlog) RW(loss_rows) RW(dy2)
-                          RW(da1m) RW(part2) RW(part1) RW(w2t) RW(keep_prob) RW(base_lr) RW(lr_decay)
+                          RW(da1m) RW(part2) RW(part1) RW(w2t) RW(a1pf) RW(keep_prob) RW(base_lr) RW(lr_decay)
                               RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16)
                                   RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
                                       RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b);

@@ -5,8 +5,15 @@
 #include <stdint.h>
 
 namespace mnist {
+// Kernel-variant switches for A/B timing in one process (scripts/kernel_lab.py
+// --variant SLOT=V); 0 = the production choice.  Slot 0: conv2 filter grad.
+extern int g_variant[8];
+void set_variant(int slot, int v);
+// out_pad (optional): zero-bordered NHWC copy [batch][18][18][32] of the pooled
+// output (its border is never written: allocate it zeroed)
 void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
-                      const float* w, const float* b, float* out, uint8_t* argmax, hipStream_t s);
+                      const float* w, const float* b, float* out, uint8_t* argmax, hipStream_t s,
+                      float* out_pad = nullptr);
 // bf16 engine: pooled conv1 output as zero-bordered bf16 images (see mnist_bf16.h)
 void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
                            const float* w, const float* b, uint16_t* a1p, uint16_t* a1t,
@@ -35,7 +42,8 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
 int conv2_filter_splits(int batch);
 void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
                            float* da1m, hipStream_t s);
-void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
+// a1p: the zero-bordered NHWC pooled conv1 output [batch][18][18][32]
+void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
                              hipStream_t s);
 // L2-direct bwd-data (the one the executor uses): dy2t from launch_fc1_bwd,
 // w2t from launch_conv2_fwd; batch % 8 == 0

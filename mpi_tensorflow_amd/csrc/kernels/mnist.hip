@@ -23,6 +23,7 @@
 // Activations are NHWC fp32, weights keep the TF layouts (HWIO, [in, out]).
 // Every GEMM-shaped op runs on v_mfma_f32_32x32x2_f32 through gemm_core.h.
 #include <stdexcept>
+#include <type_traits>
 #include <string>
 
 #include "common.h"
@@ -31,6 +32,12 @@
 #include "mnist_shared.h"
 
 namespace mnist {
+
+int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+void set_variant(int slot, int v) {
+  if (slot < 0 || slot >= 8) throw std::runtime_error("set_variant: slot out of range");
+  g_variant[slot] = v;
+}
 
 // ----------------------------------------------------------- geometry ----
 template <int H_, int W_, int CIN_, int COUT_, int KS_, int PAD_, int BK_>
@@ -97,10 +104,12 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
     const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
     uint8_t* __restrict__ argmax, __bf16* __restrict__ out_p, __bf16* __restrict__ out_t,
-    int ld_batch) {
+    int ld_batch, float* __restrict__ out_pad) {
   // out_p / out_t (bf16 engine, layouts in mnist_bf16.h): pooled output as
   // the zero-bordered K-packed image [C/16][ld_batch][PH+4][PW+4][16] and as
-  // [n][PH+4][C][MNIST16_T_LD], instead of the fp32 NHWC `out`
+  // [n][PH+4][C][MNIST16_T_LD], instead of the fp32 NHWC `out`.  out_pad
+  // (fp32 engine, optional): a zero-bordered NHWC copy [n][PH+4][PW+4][C]
+  // whose border is never written (bounds-check-free conv2 filter operand)
   using CF = gemm::Cfg<WM, WN, WK, G::BK, true, true>;
   __shared__ float smem[CF::SMEM_FLOATS];
   const long long off = batch_offset_dev(step_ptr, n_local, batch);
@@ -140,6 +149,10 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
           out_t[((size_t)(n * PP + py + 2) * G::COUT + co) * MNIST16_T_LD + px + 2] = (__bf16)o;
       } else {
         out[pooled * G::COUT + co] = o;
+        if (out_pad) {
+          const int px = pooled % G::PW, t = pooled / G::PW, py = t % G::PH, n = t / G::PH;
+          out_pad[((size_t)(n * (G::PH + 4) + py + 2) * (G::PW + 4) + px + 2) * G::COUT + co] = o;
+        }
       }
       if (argmax) argmax[pooled * G::COUT + co] = (uint8_t)q;
     }
@@ -779,7 +792,8 @@ __device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
 constexpr int C2F_IPW = 2;                   // images per wave
 constexpr int C2F_GROUPS_IMG = 4 * C2F_IPW;  // images per block (4 image slots)
 
-__device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict__ a1,
+template <int C2F_DEPTH, bool CENTRE_ONLY>
+__device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict__ a1p,
                                     const float* __restrict__ dy2, float* __restrict__ part2,
                                     float* __restrict__ part_db2, float* smem) {
   // XCD-aware mapping (blocks b, b+8, ... share an XCD's L2): every tap of an
@@ -808,44 +822,61 @@ __device__ void conv2_bwd_filter_v3(int bid, int batch, const float* __restrict_
   const int n0 = g * C2F_GROUPS_IMG + ih;
   if (n0 < batch) {
     const int nimg = min(C2F_IPW, (batch - n0 + 3) / 4);
-    float av[7], bv[7], avn[7], bvn[7];
+    // a1p is zero-bordered ([n][18][18][32]): input pixel (y + kh - 2, x + kw
+    // - 2) is padded pixel (y + kh, x + kw), always in range, and the 7
+    // fragments of a row sit at compile-time offsets from one row pointer
     auto fetch = [&](int rr, float* A, float* Bv) {
       const int n = n0 + 4 * (rr / 14), y = rr % 14;
-      const float* an = a1 + (size_t)n * 196 * 32 + ci;
-      const float* dn = dy2 + (size_t)n * 196 * 64 + co;
-      const int iy = y + kh - 2;
-      const bool rv = iy >= 0 && iy < 14;
-      const int iyc = min(max(iy, 0), 13);
+      const float* an = a1p + ((size_t)(n * 18 + y + kh) * 18 + kpar + kw) * 32 + ci;
+      const float* dn = dy2 + ((size_t)n * 196 + y * 14 + kpar) * 64 + co;
 #pragma unroll
       for (int xp = 0; xp < 7; ++xp) {
-        const int x = 2 * xp + kpar, ix = x + kw - 2;
-        const bool ok = rv && ix >= 0 && ix < 14;
-        const float v = an[(iyc * 14 + min(max(ix, 0), 13)) * 32];
-        A[xp] = ok ? v : 0.f;
-        Bv[xp] = dn[(y * 14 + x) * 64];
+        A[xp] = an[2 * xp * 32];
+        Bv[xp] = dn[2 * xp * 64];
       }
     };
-    fetch(0, av, bv);
+    // C2F_DEPTH image rows in flight: row rr's fragments are moved out of
+    // their ring slot and the slot is refilled with row rr + C2F_DEPTH
+    // BEFORE row rr's MFMAs issue, so the loads have C2F_DEPTH rows of MFMA
+    // work (7 MFMAs each) to land (measured: consuming in place and refilling
+    // after the MFMAs, one row less of cover, was 1 us slower).  Only the
+    // centre tap (which visits every dY2 element once) sums the bias grad.
+    float ra[C2F_DEPTH][7], rb[C2F_DEPTH][7];
     const int nrows = 14 * nimg;
-#pragma unroll 2
-    for (int rr = 0; rr < nrows; ++rr) {
-      if (rr + 1 < nrows) fetch(rr + 1, avn, bvn);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int xp = 0; xp < 7; ++xp) {
-        if (xp & 1)
-          acc1 = mfma32x32x2(av[xp], bv[xp], acc1);
-        else
-          acc = mfma32x32x2(av[xp], bv[xp], acc);
-        dbs += bv[xp];
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int d = 0; d < C2F_DEPTH; ++d)
+      if (d < nrows) fetch(d, ra[d], rb[d]);
+    auto rows = [&](auto centre) {
+      for (int rr = 0; rr < nrows; rr += C2F_DEPTH) {
 #pragma unroll
-      for (int xp = 0; xp < 7; ++xp) {
-        av[xp] = avn[xp];
-        bv[xp] = bvn[xp];
+        for (int d = 0; d < C2F_DEPTH; ++d) {
+          const int row = rr + d;
+          if (row < nrows) {
+            float av[7], bv[7];
+#pragma unroll
+            for (int xp = 0; xp < 7; ++xp) {
+              av[xp] = ra[d][xp];
+              bv[xp] = rb[d][xp];
+            }
+            if (row + C2F_DEPTH < nrows) fetch(row + C2F_DEPTH, ra[d], rb[d]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int xp = 0; xp < 7; ++xp) {
+              if (xp & 1)
+                acc1 = mfma32x32x2(av[xp], bv[xp], acc1);
+              else
+                acc = mfma32x32x2(av[xp], bv[xp], acc);
+              if constexpr (decltype(centre)::value) dbs += bv[xp];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
       }
-    }
+    };
+    if (!CENTRE_ONLY || t == 12)
+      rows(std::true_type{});
+    else
+      rows(std::false_type{});
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] += acc1[r];
@@ -955,13 +986,14 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const float* __rest
   conv2_bwd_data_v3(blockIdx.x, a1, dy2, w2t, da1m, smem);
 }
 
+template <int DEPTH, bool CENTRE_ONLY>
 __global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(int batch,
-                                                              const float* __restrict__ a1,
+                                                              const float* __restrict__ a1p,
                                                               const float* __restrict__ dy2,
                                                               float* __restrict__ part2,
                                                               float* __restrict__ part_db2) {
   __shared__ float smem[3 * 2 * 16 * 64];
-  conv2_bwd_filter_v3(blockIdx.x, batch, a1, dy2, part2, part_db2, smem);
+  conv2_bwd_filter_v3<DEPTH, CENTRE_ONLY>(blockIdx.x, batch, a1p, dy2, part2, part_db2, smem);
 }
 
 // ------------------------------------------------------ conv1 bwd filter ----
@@ -1091,12 +1123,12 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
                       const float* w, const float* b, float* out, uint8_t* argmax,
-                      hipStream_t s) {
+                      hipStream_t s, float* out_pad) {
   const int M = batch * 14 * 14 * 4;
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
   conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
       <<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(data, step, n_local, batch, w, b, out,
-                                                      argmax, nullptr, nullptr, 0);
+                                                      argmax, nullptr, nullptr, 0, out_pad);
 }
 
 void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
@@ -1106,7 +1138,7 @@ void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
   conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK><<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(
       data, step, n_local, batch, w, b, nullptr, argmax, reinterpret_cast<__bf16*>(a1p),
-      reinterpret_cast<__bf16*>(a1t), ld_batch);
+      reinterpret_cast<__bf16*>(a1t), ld_batch, nullptr);
 }
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
@@ -1174,10 +1206,23 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
   conv2_bwd_data_l2_kernel<<<cdiv(mtiles, 2), 256, 0, s>>>(dy2t, w2t, a1, batch, da1m);
 }
 
-void launch_conv2_bwd_filter(const float* a1, const float* dy2, int batch, float* part2,
+void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
                              hipStream_t s) {
   const int G = conv2_filter_splits(batch);
-  conv2_bwd_filter_kernel<<<25 * G, 512, 0, s>>>(batch, a1, dy2, part2, part2 + (size_t)G * 51200);
+  float* db = part2 + (size_t)G * 51200;
+  switch (g_variant[0]) {  // A/B experiments (kernel_lab.py --variant)
+    case 1:
+      conv2_bwd_filter_kernel<3, false><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
+      break;
+    case 2:
+      conv2_bwd_filter_kernel<4, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
+      break;
+    case 3:
+      conv2_bwd_filter_kernel<2, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
+      break;
+    default:
+      conv2_bwd_filter_kernel<3, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
+  }
 }
 
 int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }

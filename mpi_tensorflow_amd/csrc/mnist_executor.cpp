@@ -47,7 +47,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
   const int B = p.batch;
   // forward
   mnist::launch_conv1_fwd(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
-                          W + p.off_b1, P<float>(p.a1), P<uint8_t>(p.idx1), s);
+                          W + p.off_b1, P<float>(p.a1), P<uint8_t>(p.idx1), s, P<float>(p.a1pf));
   mnist::launch_conv2_fwd(P<const float>(p.a1), B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
                           P<uint8_t>(p.idx2), P<float>(p.w2t), s);
   wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
@@ -65,7 +65,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
                                   P<const float>(p.a1), B, P<float>(p.da1m), s);
-  mnist::launch_conv2_bwd_filter(P<const float>(p.a1), P<const float>(p.dy2), B,
+  mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
                                  P<float>(p.part2), s);
   mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
                                  P<const float>(p.da1m), P<const uint8_t>(p.idx1),

@@ -199,6 +199,8 @@ class NativeMnistEngine(MnistEngineBase):
             dy2t=torch.zeros(B * 64 * 18 * 20, **f32),
             part2=torch.empty(k.part2_floats(B), **f32), part1=torch.empty(k.part1_floats(B), **f32),
             w2t=torch.empty(25 * 64 * 32, **f32),
+            # zero-bordered NHWC a1 (filter-grad operand; the border is never written)
+            a1pf=torch.zeros(B * 18 * 18 * 32, **f32),
         )
         self.bf16 = cfg.dtype == "bf16"
         if self.bf16:
@@ -215,7 +217,7 @@ class NativeMnistEngine(MnistEngineBase):
                 w2tb=torch.zeros(25 * 64 * 32, **b16), w2b=torch.zeros(25 * 32 * 64, **b16),
                 part2=torch.empty(k.part2_floats_bf16(B), **f32),
             )
-            for name in ("a1", "a2", "dy2", "w2t"):  # fp32-only buffers
+            for name in ("a1", "a2", "dy2", "w2t", "a1pf"):  # fp32-only buffers
                 self.bufs[name] = torch.empty(0, **f32)
         p = C_.MnistPtrs()
         p.train_x, p.train_y = ptr(self.train_x), ptr(self.train_y)

@@ -18,6 +18,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--ab", default=None, metavar="SLOT=V1,V2,...[:KERNEL]",
+                    help="A/B the kernel variants of a mnist.set_variant slot: per variant, "
+                         "in interleaved rounds, the kernel in a 20-launch graph and the whole "
+                         "graph-replayed step")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     x, y = synthetic_rows("train", 0, 4096)
@@ -34,7 +38,7 @@ def main():
     s = stream_handle()
     ops = {
         "conv1_fwd": lambda: k.conv1_fwd(ptr(e.train_x), ptr(e.step_dev), e.n_local, B, W("conv1_weight"),
-                                         W("conv1_bias"), ptr(b["a1"]), ptr(b["idx1"]), s),
+                                         W("conv1_bias"), ptr(b["a1"]), ptr(b["idx1"]), s, ptr(b["a1pf"])),
         "conv2_fwd": lambda: k.conv2_fwd(ptr(b["a1"]), B, W("conv2_weight"), W("conv2_bias"), ptr(b["a2"]),
                                          ptr(b["idx2"]), ptr(b["w2t"]), s),
         "fc1_fwd": lambda: k.fc1_fwd_train(ptr(b["a2"]), W("fc1_weight"), B, ptr(b["fc1_part"]), s),
@@ -71,7 +75,7 @@ def main():
                                             ptr(b["dy2"]), ptr(b["dy2t"]), s, 4),
         "conv2_bwd_data": lambda: k.conv2_bwd_data_l2(ptr(b["dy2t"]), ptr(b["w2t"]), ptr(b["a1"]), B,
                                                       ptr(b["da1m"]), s),
-        "conv2_bwd_filter": lambda: k.conv2_bwd_filter(ptr(b["a1"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
+        "conv2_bwd_filter": lambda: k.conv2_bwd_filter(ptr(b["a1pf"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
         "conv1_bwd_filter": lambda: k.conv1_bwd_filter(ptr(e.train_x), ptr(e.step_dev), e.n_local, B,
                                                        ptr(b["da1m"]), ptr(b["idx1"]), ptr(b["part1"]), s),
         "grad_finalize": lambda: k.grad_finalize(ptr(b["part2"]), k.conv2_filter_splits(B), ptr(b["part1"]),
@@ -80,6 +84,49 @@ def main():
         "sgd": lambda: Cn.optim.sgd_momentum(ptr(e.params), ptr(e.grads), ptr(e.mom), lay.total,
                                              lay.l2_range()[1], 5e-4, 0.9, 1.0, ptr(e.lr_dev), 0.0, 0, s),
     }
+    if a.ab:
+        spec, _, kname = a.ab.partition(":")
+        slot, vals = spec.split("=")
+        slot, vals = int(slot), [int(v) for v in vals.split(",")]
+        kname = kname or "conv2_bwd_filter"
+        res = {v: ([], []) for v in vals}
+        e.cfg.graph = True
+        e.use_graph = True
+        for rnd in range(3):
+            for v in vals:
+                k.set_variant(slot, v)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    s = stream_handle()  # the capture stream (the op lambdas read `s` late)
+                    for _ in range(20):
+                        ops[kname]()
+                s = stream_handle()
+                g.replay()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    g.replay()
+                e1.record()
+                e1.synchronize()
+                res[v][0].append(e0.elapsed_time(e1) * 1000.0 / 200)
+                e._graphs.clear()
+                e.capture(250)
+                e.train(250)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                e.train(500)
+                e1.record()
+                e1.synchronize()
+                res[v][1].append(e0.elapsed_time(e1) * 1000.0 / 500)
+        k.set_variant(slot, 0)
+        print(f"A/B slot {slot} kernel {kname}: variant, kernel-in-graph us (min of rounds), "
+              f"step us (min of rounds)")
+        for v in vals:
+            print(f"  {v}: {min(res[v][0]):8.2f} {min(res[v][1]):8.2f}   "
+                  f"rounds {['%.2f' % t for t in res[v][0]]} {['%.2f' % t for t in res[v][1]]}")
+        return
     total = 0.0
     print(f"{'kernel':20s} {'median_us':>10s} {'min_us':>8s}")
     for name, fn in ops.items():
