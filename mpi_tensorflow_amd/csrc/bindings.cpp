@@ -192,6 +192,7 @@ PYBIND11_MODULE(_C, m) {
         return p;
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
+  g.def("set_conv_variant", &gops::set_conv_variant, py::arg("slot"), py::arg("value"));
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
                        bool relu, uintptr_t ws, uintptr_t st, bool bf16) {
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,

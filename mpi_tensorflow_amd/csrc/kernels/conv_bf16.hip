@@ -1,0 +1,573 @@
+// bf16 MFMA implicit-GEMM convolution for wide NHWC layers (C % 64 == 0,
+// K % 64 == 0: every ResNet-18 conv but the 3-channel stem), forward and the
+// stride-1 backward-data (a forward conv of dY with flipped, transposed taps).
+//
+// Why a second bf16 path next to conv_tiled.hip's: that family stages K tiles
+// of 32 channels, i.e. 2 bf16 MFMA k-steps between barriers, and writes its
+// B operand into LDS one bf16 at a time (put_r4) because the HWIO weights are
+// co-contiguous.  Here:
+//   * the weights are re-laid once per call into bf16 [tap][n][k] (k
+//     contiguous) by wcvt_kernel, so B tiles are 16-byte bf16 vectors in and
+//     16-byte ds_write_b128 out, no transposes;
+//   * a K tile is one tap x 64 channels: 4 k-steps of v_mfma_f32_32x32x16_bf16
+//     on TMxTN 32x32 tiles per wave (16 MFMAs per barrier for 128x128);
+//   * A (fp32 NHWC activations) is loaded as float4 pairs = 8 consecutive
+//     channels, converted to bf16 in registers and stored as one 16-byte
+//     vector into the row-major [row][64 + 8] LDS image (144-byte rows: the
+//     ds_read_b128 fragments of 8 consecutive lanes hit disjoint banks);
+//   * double-buffered LDS, next tile's global loads in flight during the
+//     current tile's MFMAs, one barrier per K tile, XCD-aware block order;
+//   * split-K (gridDim.y) for deep layers writes fp32 slabs, summed
+//     deterministically by the caller.
+// fp32 accumulate; fp32 in / out (the rest of the generic engine is fp32).
+#include <stdexcept>
+
+#include "common.h"
+#include "ops_generic.h"
+
+namespace gops {
+int g_conv_variant[4] = {0, 0, 0, 0};
+void set_conv_variant(int slot, int v) {
+  if (slot < 0 || slot >= 4) throw std::runtime_error("set_conv_variant: slot out of range");
+  g_conv_variant[slot] = v;
+}
+namespace cbf {
+
+constexpr int BK = 64;       // channels per K tile
+constexpr int LDK = BK + 8;  // bf16 per LDS row (144 B)
+constexpr int NT = 256;      // 4 waves, 2 x 2
+
+typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint4 pack8(float4 a, float4 b) {
+  bfx8 v;
+  v[0] = (__bf16)a.x;
+  v[1] = (__bf16)a.y;
+  v[2] = (__bf16)a.z;
+  v[3] = (__bf16)a.w;
+  v[4] = (__bf16)b.x;
+  v[5] = (__bf16)b.y;
+  v[6] = (__bf16)b.z;
+  v[7] = (__bf16)b.w;
+  return __builtin_bit_cast(uint4, v);
+}
+
+// Weights HWIO fp32 [R][S][C][K] -> bf16
+//   mode 0 (forward):            Wt[tap][co][ci]            = W[tap][ci][co]
+//   mode 1 (stride-1 bwd-data):  Wt[R*S-1-tap][ci][co]      = W[tap][ci][co]
+// (mode 1 is the forward weight of the conv dX = conv(dY, W'), whose input
+// channels are co and output channels ci.)  32x32 transpose tiles via LDS.
+__global__ __launch_bounds__(256) void wcvt_kernel(const float* __restrict__ w, int taps, int C,
+                                                   int K, int mode, __bf16* __restrict__ out) {
+  __shared__ float t[32][33];
+  const int ct = C / 32, kt = K / 32;
+  const int b = blockIdx.x;
+  const int tap = b / (ct * kt), rem = b % (ct * kt), c0 = (rem / kt) * 32, k0 = (rem % kt) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  const float* src = w + (size_t)tap * C * K;
+  if (mode == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[ty + 8 * i][tx] = src[(size_t)(c0 + ty + 8 * i) * K + k0 + tx];
+    __syncthreads();
+    __bf16* dst = out + (size_t)tap * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = (__bf16)t[tx][ty + 8 * i];
+  } else {
+    __bf16* dst = out + (size_t)(taps - 1 - tap) * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t o = (size_t)(c0 + ty + 8 * i) * K + k0 + tx;
+      dst[o] = (__bf16)src[o];
+    }
+  }
+}
+
+// Forward conv Y[m = (n, oy, ox)][co] = sum_{tap, ci} X[n, iy, ix, ci] Wt[tap][co][ci].
+template <int BM, int BN>
+struct Loader {
+  static constexpr int AR = BM * BK / 8 / NT;  // 8-channel A chunks per thread
+  static constexpr int BR = BN * BK / 8 / NT;  // 8-channel B chunks per thread
+  ConvShape s;
+  const __bf16* wt;
+  int cchunks;
+  const float* abase[AR];
+  int iy0[AR], ix0[AR];
+  bool av[AR];
+  const __bf16* bbase[BR];
+  float4 ra[AR][2];
+  uint4 rb[BR];
+  __device__ Loader(const ConvShape& s_, const float* x, const __bf16* wt_, int m0, int n0)
+      : s(s_), wt(wt_) {
+    cchunks = s.C / BK;
+    const int tid = threadIdx.x, c8 = tid & 7;
+    const int M = s.N * s.OH * s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + (NT / 8) * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+      abase[i] = x + (size_t)n * s.H * s.W * s.C + 8 * c8;
+      iy0[i] = oy * s.stride - s.pad;
+      ix0[i] = ox * s.stride - s.pad;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = min(n0 + (tid >> 3) + (NT / 8) * i, s.K - 1);  // K % 64 == 0: never clamps
+      bbase[i] = wt + (size_t)n * s.C + 8 * c8;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tap = kt / cchunks, ci0 = (kt - tap * cchunks) * BK;
+    const int kh = tap / s.S, kw = tap - kh * s.S;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int iy = iy0[i] + kh, ix = ix0[i] + kw;
+      const bool ok = av[i] && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+      const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+      const float4* p =
+          reinterpret_cast<const float4*>(abase[i] + ((size_t)iyc * s.W + ixc) * s.C + ci0);
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v0 = p[0], v1 = p[1];
+      ra[i][0] = ok ? v0 : z;
+      ra[i][1] = ok ? v1 : z;
+    }
+    const size_t wo = (size_t)tap * s.K * s.C + ci0;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const uint4*>(bbase[i] + wo);
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x, c8 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) =
+          pack8(ra[i][0], ra[i][1]);
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[i];
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
+                                                 const __bf16* __restrict__ wt,
+                                                 const float* __restrict__ bias,
+                                                 float* __restrict__ y, int relu, int kps) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int STAGE = (BM + BN) * LDK;  // bf16 elements
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int M = s.N * s.OH * s.OW;
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
+  const int nk_all = s.R * s.S * (s.C / BK), kb = blockIdx.y * kps;
+  const int nk = min(kps, nk_all - kb);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5;
+  Loader<BM, BN> ld(s, x, wt, m0, n0);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero16();
+  if (nk > 0) {
+    ld.load(kb);
+    ld.store(smem, smem + BM * LDK);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const __bf16* A = smem + (kt & 1) * STAGE;
+      const __bf16* B = A + BM * LDK;
+      __bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
+      const bool more = kt + 1 < nk;
+      if (more) ld.load(kb + kt + 1);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bfx8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bfx8*>(A + (wm * (BM / 2) + 32 * i + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const bfx8*>(B + (wn * (BN / 2) + 32 * j + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) ld.store(nxt, nxt + BM * LDK);
+      __syncthreads();
+    }
+  }
+  y += (size_t)blockIdx.y * M * s.K;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + r;
+    const float bv = bias ? bias[co] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q, lane);
+        if (m >= M) continue;
+        float v = acc[i][j][q] + bv;
+        if (relu) v = fmaxf(v, 0.f);
+        y[(size_t)m * s.K + co] = v;
+      }
+  }
+}
+
+
+// ----------------------------------------------------- backward-filter ----
+// dW[tap][ci][co] = sum_pix X[pix shifted by tap][ci] dY[pix][co].  GEMM
+// M = (tap, ci), N = co, reduction over output pixels; block = (128-row M
+// tile, co tile, pixel slice z).  The MFMA wants 8 consecutive pixels per lane and
+// NHWC keeps channels contiguous, so every thread loads 8 pixels x 4
+// channels (8 float4; 64-row tiles: 4 pixels) and writes them transposed as
+// 4 [channel][8 (4) pixels] 16 (8)-byte vectors into the [row][64 + 8] LDS
+// image - no per-element LDS stores.
+template <int BM, int BN>
+struct WgLoader {
+  static constexpr int GA = BM / 4, GB = BN / 4;          // channel quads per tile
+  static constexpr int PA = BK * GA / NT, PB = BK * GB / NT;  // pixels per thread (4 or 8)
+  static_assert((PA == 4 || PA == 8) && (PB == 4 || PB == 8), "tile shape");
+  ConvShape s;
+  const float* x;
+  const float* dy;
+  int kh, kw, pix0, npix, ca, cb;
+  bool mv;
+  float4 ra[PA], rb[PB];
+  // A rows are the flattened (tap, ci) index m = tap * C + ci: a 128-row tile
+  // spans two taps of a 64-channel layer, so the dY tile it multiplies is
+  // fetched once for both (C % 64 == 0: a channel quad never straddles taps)
+  __device__ WgLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0, int n0,
+                      int pix0_, int npix_)
+      : s(s_), x(x_), dy(dy_), pix0(pix0_), npix(npix_) {
+    const int m = m0 + 4 * (threadIdx.x % GA);
+    mv = m < s.R * s.S * s.C;
+    const int mm = mv ? m : 0, tap = mm / s.C;
+    kh = tap / s.S;
+    kw = tap % s.S;
+    ca = mm % s.C;
+    cb = n0 + 4 * (threadIdx.x % GB);
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tid = threadIdx.x;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    {
+      const int p = pix0 + kt * BK + PA * (tid / GA);
+      int pc = min(p, npix - 1);
+      int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
+#pragma unroll
+      for (int q = 0; q < PA; ++q) {
+        const int iy = oy * s.stride - s.pad + kh, ix = ox * s.stride - s.pad + kw;
+        const bool ok = mv && p + q < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+        const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+        const float4 v = *reinterpret_cast<const float4*>(
+            x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ca);
+        ra[q] = ok ? v : z;
+        if (++ox == s.OW) {  // next output pixel (rows past the end are masked)
+          ox = 0;
+          if (++oy == s.OH) {
+            oy = 0;
+            n = min(n + 1, s.N - 1);
+          }
+        }
+      }
+    }
+    {
+      const int p = pix0 + kt * BK + PB * (tid / GB);
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const float4 v = *reinterpret_cast<const float4*>(dy + (size_t)min(p + q, npix - 1) * s.K + cb);
+        rb[q] = p + q < npix ? v : z;
+      }
+    }
+  }
+  // channel c of the P pixels held in r, as P consecutive bf16 (one LDS row run)
+  template <int P>
+  __device__ __forceinline__ static void put_col(__bf16* dst, const float4 (&r)[P], int c) {
+    __bf16 v[P];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+      v[q] = (__bf16)(c == 0 ? r[q].x : c == 1 ? r[q].y : c == 2 ? r[q].z : r[q].w);
+    if constexpr (P == 8)
+      *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, v);
+    else
+      *reinterpret_cast<uint2*>(dst) = __builtin_bit_cast(uint2, v);
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x;
+    const int ra0 = 4 * (tid % GA), ka = PA * (tid / GA);
+    const int rb0 = 4 * (tid % GB), kb = PB * (tid / GB);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      put_col<PA>(As + (ra0 + c) * LDK + ka, ra, c);
+      put_col<PB>(Bs + (rb0 + c) * LDK + kb, rb, c);
+    }
+  }
+};
+
+template <int BM, int BN>
+__global__ __launch_bounds__(NT) void wgrad_kernel(ConvShape s, const float* __restrict__ x,
+                                                   const float* __restrict__ dy,
+                                                   float* __restrict__ part, int kchunk) {
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int STAGE = (BM + BN) * LDK;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
+  const int Mw = s.R * s.S * s.C;
+  const int mt = (Mw + BM - 1) / BM, ntl = s.K / BN;
+  const int tiles = mt * ntl;
+  const int z = blockIdx.x / tiles, rem = blockIdx.x % tiles;
+  const int m0 = (rem % mt) * BM, n0 = (rem / mt) * BN;
+  const int npix = s.N * s.OH * s.OW;
+  const int pix0 = z * kchunk * BK;
+  const int nk = min(kchunk, (npix - pix0 + BK - 1) / BK);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5;
+  WgLoader<BM, BN> ld(s, x, dy, m0, n0, pix0, npix);
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero16();
+  if (nk > 0) {
+    ld.load(0);
+    ld.store(smem, smem + BM * LDK);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const __bf16* A = smem + (kt & 1) * STAGE;
+      const __bf16* B = A + BM * LDK;
+      __bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
+      const bool more = kt + 1 < nk;
+      if (more) ld.load(kt + 1);
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        bfx8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bfx8*>(A + (wm * (BM / 2) + 32 * i + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          b[j] = *reinterpret_cast<const bfx8*>(B + (wn * (BN / 2) + 32 * j + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) ld.store(nxt, nxt + BM * LDK);
+      __syncthreads();
+    }
+  }
+  float* out = part + (size_t)z * Mw * s.K;  // HWIO flattened: row m = tap * C + ci
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + r;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q, lane);
+        if (m < Mw) out[(size_t)m * s.K + co] = acc[i][j][q];
+      }
+  }
+}
+
+__global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
+                                                        long long n4, float4* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = part[i];
+    for (int z = 1; z < nz; ++z) {
+      const float4 b = part[z * n4 + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    out[i] = a;
+  }
+}
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+enum Tile { T128x128, T128x64, T64x128, T64x64 };
+static inline int tm(Tile t) { return (t == T128x128 || t == T128x64) ? 128 : 64; }
+static inline int tn(Tile t) { return (t == T128x128 || t == T64x128) ? 128 : 64; }
+
+// Largest tile that still gives >= 256 blocks (one per CU); deep layers that
+// cannot reach it take 64x64 (or 64x128) tiles plus split-K.
+struct Plan {
+  Tile t;
+  int z, kps;
+};
+static inline Plan plan(const ConvShape& s, bool epilogue) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const Tile order[4] = {T128x128, T128x64, T64x128, T64x64};
+  Tile t = T64x64;
+  for (Tile c : order) {
+    if (tn(c) > s.K) continue;
+    if ((long long)cdiv(M, tm(c)) * cdiv(s.K, tn(c)) >= 256) {
+      t = c;
+      break;
+    }
+  }
+  const long long blocks = (long long)cdiv(M, tm(t)) * cdiv(s.K, tn(t));
+  const int nk = s.R * s.S * (s.C / BK);
+  int z = 1;
+  if (!epilogue && blocks < 256 && nk >= 8) {
+    z = cdiv(512, blocks);
+    if (z > nk / 4) z = nk / 4;
+    if (z > 8) z = 8;
+    if (z < 1) z = 1;
+  }
+  const int kps = cdiv(nk, z);
+  return {t, cdiv(nk, kps), kps};
+}
+
+static inline long long wt_elems(const ConvShape& s) { return (long long)s.R * s.S * s.C * s.K; }
+// bf16 weight copy at the front of the workspace, split-K slabs after it
+static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 127) / 128) * 64; }
+
+static void launch(const ConvShape& s, const float* x, const __bf16* wt, const float* bias,
+                   float* y, bool relu, float* ws, hipStream_t st) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const Plan p = plan(s, bias != nullptr || relu);
+  float* slabs = ws + wt_floats(s);
+  float* out = p.z > 1 ? slabs : y;
+  const int r = relu ? 1 : 0;
+#define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
+  switch (p.t) {
+    case T128x128: fwd_kernel<128, 128><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T128x64: fwd_kernel<128, 64><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T64x128: fwd_kernel<64, 128><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    default: fwd_kernel<64, 64><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+  }
+#undef GRID
+  if (p.z > 1) {
+    const long long n4 = M * s.K / 4;
+    long long b = (n4 + 255) / 256;
+    if (b > 4096) b = 4096;
+    slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), p.z, n4,
+                                            reinterpret_cast<float4*>(y));
+  }
+}
+
+// wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
+// at least 4 K tiles per slice, at most 64 slices
+struct WgPlan {
+  int bm, bn, z, kchunk;
+};
+static inline WgPlan wg_plan(const ConvShape& s) {
+  // A/B knobs (set_conv_variant): slot 0 = 1 folds two taps of a 64-channel
+  // layer into one 128-row tile; slot 1 = target block count (cap 128 slices)
+  const int bm = (s.C % 128 == 0 || g_conv_variant[0] == 1) ? 128 : 64;
+  const int bn = s.K % 128 == 0 ? 128 : 64;
+  const long long tiles = (long long)cdiv((long long)s.R * s.S * s.C, bm) * (s.K / bn);
+  const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
+  const int target = g_conv_variant[1] > 0 ? g_conv_variant[1] : 1024;
+  int z = cdiv(target, tiles);
+  if (z > ktiles / 4) z = ktiles / 4;
+  if (z > (g_conv_variant[1] > 0 ? 128 : 64)) z = g_conv_variant[1] > 0 ? 128 : 64;
+  if (z < 1) z = 1;
+  const int kchunk = cdiv(ktiles, z);
+  return {bm, bn, cdiv(ktiles, kchunk), kchunk};
+}
+
+static void convert(const ConvShape& s, const float* w, int mode, __bf16* out, hipStream_t st) {
+  const int taps = s.R * s.S;
+  wcvt_kernel<<<taps * (s.C / 32) * (s.K / 32), 256, 0, st>>>(w, taps, s.C, s.K, mode, out);
+}
+
+// the stride-1 backward-data conv as a forward conv: input dY [N, OH, OW, K],
+// output dX [N, H, W, C], padding R - 1 - pad
+static inline ConvShape dgrad_shape(const ConvShape& s) {
+  ConvShape d;
+  d.N = s.N;
+  d.H = s.OH;
+  d.W = s.OW;
+  d.C = s.K;
+  d.K = s.C;
+  d.R = s.R;
+  d.S = s.S;
+  d.stride = 1;
+  d.pad = s.R - 1 - s.pad;
+  d.OH = s.H;
+  d.OW = s.W;
+  return d;
+}
+
+}  // namespace cbf
+
+bool conv_fwd_bf16_ok(const ConvShape& s) { return s.C % 64 == 0 && s.K % 64 == 0; }
+bool conv_bwd_filter_bf16_ok(const ConvShape& s) { return s.C % 64 == 0 && s.K % 64 == 0; }
+bool conv_bwd_data_bf16_ok(const ConvShape& s) {
+  return s.C % 64 == 0 && s.K % 64 == 0 && s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 &&
+         s.OH == s.H + 2 * s.pad - s.R + 1 && s.OW == s.W + 2 * s.pad - s.S + 1;
+}
+
+long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
+  using namespace cbf;
+  long long n = 0;
+  if (conv_fwd_bf16_ok(s)) {
+    const Plan p = plan(s, fwd_epilogue);
+    n = std::max(n, wt_floats(s) + (p.z > 1 ? (long long)p.z * s.N * s.OH * s.OW * s.K : 0));
+  }
+  if (conv_bwd_data_bf16_ok(s)) {
+    const ConvShape d = dgrad_shape(s);
+    const Plan p = plan(d, false);
+    n = std::max(n, wt_floats(d) + (p.z > 1 ? (long long)p.z * d.N * d.OH * d.OW * d.K : 0));
+  }
+  if (conv_bwd_filter_bf16_ok(s)) {
+    const WgPlan p = wg_plan(s);
+    if (p.z > 1) n = std::max(n, (long long)p.z * s.R * s.S * s.C * s.K);
+  }
+  return n;
+}
+
+void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
+                   bool relu, float* ws, hipStream_t st) {
+  using namespace cbf;
+  if (!conv_fwd_bf16_ok(s) || !ws) throw std::runtime_error("conv_fwd_bf16: unsupported shape");
+  __bf16* wt = reinterpret_cast<__bf16*>(ws);
+  convert(s, w, 0, wt, st);
+  launch(s, x, wt, bias, y, relu, ws, st);
+}
+
+void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                        hipStream_t st) {
+  using namespace cbf;
+  if (!conv_bwd_data_bf16_ok(s) || !ws) throw std::runtime_error("conv_bwd_data_bf16: unsupported shape");
+  __bf16* wt = reinterpret_cast<__bf16*>(ws);
+  convert(s, w, 1, wt, st);
+  launch(dgrad_shape(s), dy, wt, nullptr, dx, false, ws, st);
+}
+
+void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
+                          float* dw, hipStream_t st) {
+  using namespace cbf;
+  if (!conv_bwd_filter_bf16_ok(s)) throw std::runtime_error("conv_bwd_filter_bf16: unsupported shape");
+  const WgPlan p = wg_plan(s);
+  if (p.z > 1 && !ws) throw std::runtime_error("conv_bwd_filter_bf16: split-K needs a workspace");
+  float* out = p.z > 1 ? ws : dw;
+  const int blocks = cdiv((long long)s.R * s.S * s.C, p.bm) * (s.K / p.bn) * p.z;
+  if (p.bm == 128 && p.bn == 128)
+    wgrad_kernel<128, 128><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  else if (p.bm == 128)
+    wgrad_kernel<128, 64><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  else if (p.bn == 128)
+    wgrad_kernel<64, 128><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  else
+    wgrad_kernel<64, 64><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  if (p.z > 1) {
+    const long long n4 = (long long)s.R * s.S * s.C * s.K / 4;
+    long long b = (n4 + 255) / 256;
+    if (b > 4096) b = 4096;
+    slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(ws), p.z, n4,
+                                            reinterpret_cast<float4*>(dw));
+  }
+}
+
+}  // namespace gops

@@ -28,6 +28,20 @@ int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
                      hipStream_t st, bool bf16 = false);
 long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue);
+// bf16 MFMA convs with 64-channel K tiles and pre-laid-out bf16 weights
+// (conv_bf16.hip): forward for C, K % 64 == 0, stride-1 backward-data; the
+// bf16 weight copy and split-K slabs live in the layer workspace
+bool conv_fwd_bf16_ok(const ConvShape& s);
+void set_conv_variant(int slot, int v);  // tiling A/B knobs (scripts/conv_lab.py)
+bool conv_bwd_data_bf16_ok(const ConvShape& s);
+long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
+void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
+                   bool relu, float* ws, hipStream_t st);
+void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
+                        hipStream_t st);
+bool conv_bwd_filter_bf16_ok(const ConvShape& s);
+void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
+                          float* dw, hipStream_t st);
 // LDS-tiled conv family (conv_tiled.hip), used by the launchers above for the
 // shapes it supports
 bool conv_fwd_tiled_ok(const ConvShape& s);

@@ -1,0 +1,90 @@
+"""Times the generic conv ops (forward / backward-data / backward-filter) on
+every distinct ResNet-18 layer shape at batch B, per op and per layer, with
+optional A/B of the gops.set_conv_variant tiling knobs.
+    python scripts/conv_lab.py [--batch 32] [--dtype bf16] [--ab SLOT=V1,V2,...] [--reps 20]"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from mpi_tensorflow_amd.ops import native, ptr, stream_handle
+
+
+def shapes(B):
+    # (H, Cin, K, R, stride, pad, count per step)
+    return [
+        (112, 3, 64, 7, 2, 3, 1),
+        (56, 64, 64, 3, 1, 1, 4),
+        (56, 64, 128, 3, 2, 1, 1), (28, 128, 128, 3, 1, 1, 3), (56, 64, 128, 1, 2, 0, 1),
+        (28, 128, 256, 3, 2, 1, 1), (14, 256, 256, 3, 1, 1, 3), (28, 128, 256, 1, 2, 0, 1),
+        (14, 256, 512, 3, 2, 1, 1), (7, 512, 512, 3, 1, 1, 3), (14, 256, 512, 1, 2, 0, 1),
+    ]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--ab", default=None)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    C = native()
+    g = C.ops
+    bf16 = a.dtype == "bf16"
+    dev = torch.device("cuda:0")
+    s = stream_handle()
+    variants = [(None, 0)]
+    if a.ab:
+        slot, vals = a.ab.split("=")
+        variants = [(int(slot), int(v)) for v in vals.split(",")]
+    tot = {v: [0.0, 0.0, 0.0] for v in variants}
+    for (H, Cin, K, R, st, pd, cnt) in shapes(a.batch):
+        Hin = 224 if Cin == 3 else (H if st == 1 else 2 * H)
+        sh = g.ConvShape(a.batch, Hin, Hin, Cin, K, R, R, st, pd)
+        x = torch.randn(a.batch, Hin, Hin, Cin, device=dev)
+        w = torch.randn(R, R, Cin, K, device=dev) * 0.05
+        y = torch.empty(a.batch, sh.OH, sh.OW, K, device=dev)
+        dy = torch.randn_like(y)
+        dx = torch.empty_like(x)
+        dw = torch.empty_like(w)
+        ws = torch.empty(max(g.conv_ws_floats(sh, False), 4) * 2, device=dev)
+        ops = {
+            "fwd": lambda: g.conv_fwd(sh, ptr(x), ptr(w), 0, ptr(y), False, ptr(ws), s, bf16),
+            "dgrad": lambda: g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ws), s, bf16),
+            "wgrad": lambda: g.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ws), ptr(dw), s, bf16),
+        }
+        line = f"H{Hin:3d} {Cin:3d}->{K:3d} {R}x{R} s{st} x{cnt}:"
+        for v in variants:
+            if v[0] is not None:
+                g.set_conv_variant(v[0], v[1])
+            res = []
+            for i, (name, fn) in enumerate(ops.items()):
+                if name == "dgrad" and Cin == 3:
+                    res.append(0.0)
+                    continue
+                for _ in range(3):
+                    fn()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(a.reps):
+                    fn()
+                e1.record()
+                e1.synchronize()
+                us = e0.elapsed_time(e1) * 1000.0 / a.reps
+                res.append(us)
+                tot[v][i] += us * cnt
+            line += f"  [{v[1]}] " + " ".join(f"{t:7.1f}" for t in res)
+            if v[0] is not None:
+                g.set_conv_variant(v[0], 0)
+        print(line, flush=True)
+    for v in variants:
+        t = tot[v]
+        print(f"variant {v}: per-step fwd {t[0]:.0f} dgrad {t[1]:.0f} wgrad {t[2]:.0f} "
+              f"total {sum(t):.0f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -198,6 +198,10 @@ def test_generic_bucketed_allreduce_overlap(cuda_dev):
     (2, 14, 14, 64, 128, 3, 2, 1),
     (10, 56, 56, 64, 64, 3, 1, 1),
     (2, 9, 9, 3, 64, 7, 2, 3),  # stem-like: gather filter path
+    (4, 7, 7, 512, 512, 3, 1, 1),  # layer4: split-K forward / backward-data
+    (4, 14, 14, 128, 256, 1, 2, 0),  # 1x1 stride-2 downsample
+    (8, 28, 28, 128, 128, 3, 1, 1),  # 128x128 tiles
+    (3, 11, 13, 64, 192, 3, 1, 1),  # ragged M, non-square image
 ])
 def test_conv_bf16_mfma(cuda_dev, N, H, W, Cin, K, R, stride, pad):
     """bf16-operand MFMA convolutions (fp32 accumulate) vs fp32 torch: relative
