@@ -187,7 +187,9 @@ using CFG_D = gemm::Cfg<WM, WN, 1, BK, true, false>;
 __global__ __launch_bounds__(256) void conv_bwd_data_kernel(ConvShape s,
                                                             const float* __restrict__ dy,
                                                             const float* __restrict__ w,
-                                                            float* __restrict__ dx) {
+                                                            float* __restrict__ dx, int kchunk) {
+  // split-K over gridDim.y (kchunk K per slice): slice y writes the raw slab
+  // dx + y * M * C, summed by slab_sum_kernel
   __shared__ float smem[CFG_D::SMEM_FLOATS];
   const int M = s.N * s.H * s.W, Ktot = s.R * s.S * s.K;
   ConvDataProb p{s, dy, w, Ktot, M};
@@ -195,9 +197,11 @@ __global__ __launch_bounds__(256) void conv_bwd_data_kernel(ConvShape s,
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid % mt) * CFG_D::BM, n0 = (bid / mt) * CFG_D::BN;
   const int kend = (Ktot + BK - 1) / BK * BK;
+  const int kb = blockIdx.y * kchunk, ke = min(kend, kb + kchunk);
+  dx += (size_t)blockIdx.y * M * s.C;
   f32x16 acc;
   int wm, wn;
-  gemm::run_tile<WM, WN, 1, BK>(p, smem, m0, n0, 0, kend, acc, wm, wn);
+  gemm::run_tile<WM, WN, 1, BK>(p, smem, m0, n0, kb, ke, acc, wm, wn);
   const int lane = threadIdx.x & 63;
   const int ci = n0 + 32 * wn + (lane & 31);
   if (ci >= s.C) return;
@@ -243,6 +247,30 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
     float s = 0.f;
     for (int z = 0; z < nz; ++z) s += part[z * n + i];
     out[i] = s;
+  }
+}
+
+// Many slabs over few elements (thin-layer filter grads: 512 slabs x 450
+// floats): block = 16 consecutive elements x 16 slab lanes; lane j sums slabs
+// j, j + 16, ... (independent loads, 8 in flight), then a fixed-order LDS fold
+// over the 16 lanes - deterministic, and no 512-long serial chain per thread.
+__global__ __launch_bounds__(256) void slab_sum_wide_kernel(const float* __restrict__ part, int nz,
+                                                            long long n, float* __restrict__ out) {
+  __shared__ float red[16][17];
+  const int e = threadIdx.x & 15, zl = threadIdx.x >> 4;
+  const long long i = (long long)blockIdx.x * 16 + e;
+  float acc = 0.f;
+  if (i < n) {
+#pragma unroll 8
+    for (int z = zl; z < nz; z += 16) acc += part[(long long)z * n + i];
+  }
+  red[zl][e] = acc;
+  __syncthreads();
+  if (zl == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) t += red[j][e];
+    out[i] = t;
   }
 }
 
@@ -446,13 +474,34 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
   conv_fwd_kernel<<<blocks, 256, 0, st>>>(s, x, w, bias, y, relu ? 1 : 0);
 }
 
+// gather-engine backward-data split-K: a block's K tiles are a serial chain,
+// so with few output tiles (LeNet conv2: 196 blocks x 13 K tiles) slice K to
+// reach ~1024 blocks of >= 3 K tiles
+static void gather_data_plan(const ConvShape& s, int& z, int& kchunk) {
+  const int M = s.N * s.H * s.W;
+  const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
+  const int ktiles = (s.R * s.S * s.K + BK - 1) / BK;
+  z = (1024 + blocks - 1) / blocks;
+  if (z > ktiles / 3) z = ktiles / 3;
+  if (z < 1) z = 1;
+  kchunk = ((ktiles + z - 1) / z) * BK;
+  z = (ktiles * BK + kchunk - 1) / kchunk;
+}
+
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                    hipStream_t st, bool bf16) {
   if (bf16 && conv_bwd_data_bf16_ok(s)) return conv_bwd_data_bf16(s, dy, w, dx, ws, st);
   if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16);
   const int M = s.N * s.H * s.W;
   const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
-  conv_bwd_data_kernel<<<blocks, 256, 0, st>>>(s, dy, w, dx);
+  int z, kchunk;
+  gather_data_plan(s, z, kchunk);
+  if (z > 1 && !ws) z = 1, kchunk = (s.R * s.S * s.K + BK - 1) / BK * BK;
+  conv_bwd_data_kernel<<<dim3(blocks, z), 256, 0, st>>>(s, dy, w, z > 1 ? ws : dx, kchunk);
+  if (z > 1) {
+    const long long n = (long long)M * s.C;
+    slab_sum_kernel<<<grid1d(n), 256, 0, st>>>(ws, z, n, dx);
+  }
 }
 
 int conv_filter_splits(const ConvShape& s) {
@@ -460,15 +509,24 @@ int conv_filter_splits(const ConvShape& s) {
   const int Mw = s.R * s.S * s.C;
   const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);
   const int ktiles = (s.N * s.OH * s.OW + BK - 1) / BK;
-  int z = (1024 + tiles - 1) / tiles;  // aim for ~1024 blocks
+  // aim for ~1024 blocks of >= 2 K tiles: a block's K tiles form a serial
+  // latency chain (~4 us each on this engine), so thin layers with few output
+  // tiles (LeNet conv1: 2 tiles, 1568 K tiles) need many slices (measured:
+  // a 64-slice cap left that layer at 101 us per step)
+  int z = (1024 + tiles - 1) / tiles;
   z = z < 1 ? 1 : z;
-  z = z > ktiles ? ktiles : z;
-  z = z > 64 ? 64 : z;
-  return z;
+  z = z > ktiles / 2 ? ktiles / 2 : z;
+  z = z > 512 ? 512 : z;
+  return z < 1 ? 1 : z;
 }
 
 long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue) {
   long long n = (long long)conv_filter_splits(s) * s.R * s.S * s.C * s.K;
+  if (!conv_bwd_data_tiled_ok(s)) {
+    int z, kchunk;
+    gather_data_plan(s, z, kchunk);
+    if (z > 1) n = std::max(n, (long long)z * s.N * s.H * s.W * s.C);
+  }
   if (conv_fwd_tiled_ok(s)) n = std::max(n, conv_fwd_tiled_ws_floats(s, fwd_epilogue));
   if (conv_bwd_data_tiled_ok(s)) n = std::max(n, conv_bwd_data_tiled_ws_floats(s));
   return std::max(n, conv_bf16_ws_floats(s, fwd_epilogue));
@@ -486,7 +544,10 @@ void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float*
   const int zz = (ktiles * BK + kchunk - 1) / kchunk;
   conv_bwd_filter_kernel<<<tiles * zz, 256, 0, st>>>(s, x, dy, part, kchunk);
   const long long n = (long long)Mw * s.K;
-  slab_sum_kernel<<<grid1d(n), 256, 0, st>>>(part, zz, n, dw);
+  if (zz >= 32)
+    slab_sum_wide_kernel<<<(int)((n + 15) / 16), 256, 0, st>>>(part, zz, n, dw);
+  else
+    slab_sum_kernel<<<grid1d(n), 256, 0, st>>>(part, zz, n, dw);
 }
 
 void colsum2(const float* a, const float* b, long long rows, int C, float* s1, float* s2, int mode,

@@ -154,14 +154,43 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
     return F.relu(y) if relu else y
 
 
+class _LinearFn(torch.autograd.Function):
+    """Fully connected layer on GPU as plain library GEMMs (rocBLAS via
+    torch.mm / addmm), gradients written straight into the flat-buffer
+    views.  The batch-sized FC GEMMs of LeNet-5 / the ResNet-18 head (M = 32..64
+    rows, K = 84..512) leave the conv kernels' tile machinery with one or two
+    blocks and a serial K chain (ResNet-18's 512 -> 10 head: 76 us forward on
+    the gather engine); the library GEMM splits them properly."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, relu, gw, gb):
+        x = x.contiguous()
+        y = torch.addmm(b, x, w) if b is not None else torch.mm(x, w)
+        if relu:
+            y = torch.relu_(y)
+        ctx.save_for_backward(x, w, y if relu else None)
+        ctx.relu, ctx.gw, ctx.gb = relu, gw, gb
+        ctx.has_b = b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        if ctx.relu:
+            dy = dy * (y > 0)
+        torch.mm(x.t(), dy, out=ctx.gw)
+        if ctx.has_b:
+            torch.sum(dy, dim=0, out=ctx.gb)
+        _grad_done(ctx.gw, ctx.gb if ctx.has_b else None)
+        dx = torch.mm(dy, w.t()) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None, None
+
+
 def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) -> torch.Tensor:
-    """x [N,in], w [in,out] -> [N,out] (a 1x1 conv over a 1x1 image on GPU)."""
+    """x [N,in], w [in,out] -> [N,out]."""
     if x.is_cuda:
-        n, fin = x.shape
-        fout = w.value.shape[1]
-        w4 = Param(w.value.view(1, 1, fin, fout), w.grad_view.view(1, 1, fin, fout))
-        y = conv2d(x.reshape(n, 1, 1, fin), w4, b, 1, 0, relu)
-        return y.reshape(n, fout)
+        return _LinearFn.apply(x, w.value, None if b is None else b.value, relu, w.grad_view,
+                               None if b is None else b.grad_view)
     y = x @ w.value + (0 if b is None else b.value)
     return F.relu(y) if relu else y
 
