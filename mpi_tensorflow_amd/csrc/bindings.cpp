@@ -193,29 +193,34 @@ PYBIND11_MODULE(_C, m) {
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
   g.def("set_conv_variant", &gops::set_conv_variant, py::arg("slot"), py::arg("value"));
+  g.def("conv_bf16_ok", &gops::conv_fwd_bf16_ok);
+  g.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
+    gops::to_bf16(P<const float>(x), P<void>(y), n, S(st));
+    check_launch();
+  });
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
-                       bool relu, uintptr_t ws, uintptr_t st, bool bf16) {
+                       bool relu, uintptr_t ws, uintptr_t st, bool bf16, uintptr_t xb) {
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
-                   P<float>(ws), S(st), bf16);
+                   P<float>(ws), S(st), bf16, P<const void>(xb));
     check_launch();
   }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
-     py::arg("ws"), py::arg("st"), py::arg("bf16") = false);
+     py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
-                            uintptr_t ws, uintptr_t st, bool bf16) {
+                            uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb) {
     gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st),
-                        bf16);
+                        bf16, P<const void>(dyb));
     check_launch();
   }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
-     py::arg("bf16") = false);
+     py::arg("bf16") = false, py::arg("dyb") = 0);
   g.def("conv_ws_floats", &gops::conv_ws_floats);
   g.def("conv_filter_splits", &gops::conv_filter_splits);
   g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,
-                              uintptr_t dw, uintptr_t st, bool bf16) {
+                              uintptr_t dw, uintptr_t st, bool bf16, uintptr_t xb, uintptr_t dyb) {
     gops::conv_bwd_filter(s, P<const float>(x), P<const float>(dy), P<float>(part), P<float>(dw),
-                          S(st), bf16);
+                          S(st), bf16, P<const void>(xb), P<const void>(dyb));
     check_launch();
   }, py::arg("s"), py::arg("x"), py::arg("dy"), py::arg("part"), py::arg("dw"), py::arg("st"),
-     py::arg("bf16") = false);
+     py::arg("bf16") = false, py::arg("xb") = 0, py::arg("dyb") = 0);
   g.def("colsum2", [](uintptr_t a, uintptr_t b, long long rows, int C, uintptr_t s1, uintptr_t s2,
                       int mode, uintptr_t ws, uintptr_t st) {
     gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode,

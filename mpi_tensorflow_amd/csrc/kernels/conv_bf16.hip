@@ -11,16 +11,20 @@
 //     16-byte ds_write_b128 out, no transposes;
 //   * a K tile is one tap x 64 channels: 4 k-steps of v_mfma_f32_32x32x16_bf16
 //     on TMxTN 32x32 tiles per wave (16 MFMAs per barrier for 128x128);
-//   * A (fp32 NHWC activations) is loaded as float4 pairs = 8 consecutive
-//     channels, converted to bf16 in registers and stored as one 16-byte
-//     vector into the row-major [row][64 + 8] LDS image (144-byte rows: the
-//     ds_read_b128 fragments of 8 consecutive lanes hit disjoint banks);
+//   * A is a bf16 copy of the NHWC activations (to_bf16_kernel, written once
+//     per conv and kept for the filter gradient): one 16-byte load per 8
+//     channels straight into the row-major [row][64 + 8] LDS image (144-byte
+//     rows: the ds_read_b128 fragments of 8 consecutive lanes hit disjoint
+//     banks).  These kernels are bound by vector-L1 bytes per MFMA, so
+//     halving the A bytes is the lever (fp32 activations, converted while
+//     staged, remain the fallback when no copy is passed);
 //   * double-buffered LDS, next tile's global loads in flight during the
 //     current tile's MFMAs, one barrier per K tile, XCD-aware block order;
 //   * split-K (gridDim.y) for deep layers writes fp32 slabs, summed
 //     deterministically by the caller.
 // fp32 accumulate; fp32 in / out (the rest of the generic engine is fp32).
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "ops_generic.h"
@@ -50,6 +54,14 @@ __device__ __forceinline__ uint4 pack8(float4 a, float4 b) {
   v[6] = (__bf16)b.z;
   v[7] = (__bf16)b.w;
   return __builtin_bit_cast(uint4, v);
+}
+
+// fp32 -> bf16 (round to nearest even), 8 elements per thread-iteration.
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float4* __restrict__ x,
+                                                      uint4* __restrict__ y, long long n8) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride)
+    y[i] = pack8(x[2 * i], x[2 * i + 1]);
 }
 
 // Weights HWIO fp32 [R][S][C][K] -> bf16
@@ -84,20 +96,24 @@ __global__ __launch_bounds__(256) void wcvt_kernel(const float* __restrict__ w, 
 }
 
 // Forward conv Y[m = (n, oy, ox)][co] = sum_{tap, ci} X[n, iy, ix, ci] Wt[tap][co][ci].
-template <int BM, int BN>
+// XT = __bf16: bf16 activation copy (16-byte loads); XT = float: fp32
+// activations converted while staged.
+template <int BM, int BN, class XT>
 struct Loader {
+  static constexpr bool XB = sizeof(XT) == 2;
   static constexpr int AR = BM * BK / 8 / NT;  // 8-channel A chunks per thread
   static constexpr int BR = BN * BK / 8 / NT;  // 8-channel B chunks per thread
   ConvShape s;
   const __bf16* wt;
   int cchunks;
-  const float* abase[AR];
+  const XT* abase[AR];
   int iy0[AR], ix0[AR];
   bool av[AR];
   const __bf16* bbase[BR];
-  float4 ra[AR][2];
+  float4 ra[XB ? 1 : AR][2];
+  uint4 rab[XB ? AR : 1];
   uint4 rb[BR];
-  __device__ Loader(const ConvShape& s_, const float* x, const __bf16* wt_, int m0, int n0)
+  __device__ Loader(const ConvShape& s_, const XT* x, const __bf16* wt_, int m0, int n0)
       : s(s_), wt(wt_) {
     cchunks = s.C / BK;
     const int tid = threadIdx.x, c8 = tid & 7;
@@ -126,12 +142,17 @@ struct Loader {
       const int iy = iy0[i] + kh, ix = ix0[i] + kw;
       const bool ok = av[i] && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
       const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
-      const float4* p =
-          reinterpret_cast<const float4*>(abase[i] + ((size_t)iyc * s.W + ixc) * s.C + ci0);
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 v0 = p[0], v1 = p[1];
-      ra[i][0] = ok ? v0 : z;
-      ra[i][1] = ok ? v1 : z;
+      const XT* src = abase[i] + ((size_t)iyc * s.W + ixc) * s.C + ci0;
+      if constexpr (XB) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src);
+        rab[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        const float4* p = reinterpret_cast<const float4*>(src);
+        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 v0 = p[0], v1 = p[1];
+        ra[i][0] = ok ? v0 : z;
+        ra[i][1] = ok ? v1 : z;
+      }
     }
     const size_t wo = (size_t)tap * s.K * s.C + ci0;
 #pragma unroll
@@ -140,17 +161,22 @@ struct Loader {
   __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
     const int tid = threadIdx.x, c8 = tid & 7;
 #pragma unroll
-    for (int i = 0; i < AR; ++i)
-      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) =
-          pack8(ra[i][0], ra[i][1]);
+    for (int i = 0; i < AR; ++i) {
+      uint4 v;
+      if constexpr (XB)
+        v = rab[i];
+      else
+        v = pack8(ra[i][0], ra[i][1]);
+      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = v;
+    }
 #pragma unroll
     for (int i = 0; i < BR; ++i)
       *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[i];
   }
 };
 
-template <int BM, int BN>
-__global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
+template <int BM, int BN, class XT>
+__global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restrict__ x,
                                                  const __bf16* __restrict__ wt,
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps) {
@@ -165,7 +191,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
   const int nk = min(kps, nk_all - kb);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
   const int r = lane & 31, h = lane >> 5;
-  Loader<BM, BN> ld(s, x, wt, m0, n0);
+  Loader<BM, BN, XT> ld(s, x, wt, m0, n0);
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -227,21 +253,24 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
 // channels (8 float4; 64-row tiles: 4 pixels) and writes them transposed as
 // 4 [channel][8 (4) pixels] 16 (8)-byte vectors into the [row][64 + 8] LDS
 // image - no per-element LDS stores.
-template <int BM, int BN>
+// XB: x and dY are bf16 copies (8-byte loads of 4 channels), else fp32.
+template <int BM, int BN, bool XB>
 struct WgLoader {
+  using T = typename std::conditional<XB, __bf16, float>::type;
+  using V = typename std::conditional<XB, uint2, float4>::type;  // 4 channels
   static constexpr int GA = BM / 4, GB = BN / 4;          // channel quads per tile
   static constexpr int PA = BK * GA / NT, PB = BK * GB / NT;  // pixels per thread (4 or 8)
   static_assert((PA == 4 || PA == 8) && (PB == 4 || PB == 8), "tile shape");
   ConvShape s;
-  const float* x;
-  const float* dy;
+  const T* x;
+  const T* dy;
   int kh, kw, pix0, npix, ca, cb;
   bool mv;
-  float4 ra[PA], rb[PB];
+  V ra[PA], rb[PB];
   // A rows are the flattened (tap, ci) index m = tap * C + ci: a 128-row tile
   // spans two taps of a 64-channel layer, so the dY tile it multiplies is
   // fetched once for both (C % 64 == 0: a channel quad never straddles taps)
-  __device__ WgLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0, int n0,
+  __device__ WgLoader(const ConvShape& s_, const T* x_, const T* dy_, int m0, int n0,
                       int pix0_, int npix_)
       : s(s_), x(x_), dy(dy_), pix0(pix0_), npix(npix_) {
     const int m = m0 + 4 * (threadIdx.x % GA);
@@ -254,7 +283,11 @@ struct WgLoader {
   }
   __device__ __forceinline__ void load(int kt) {
     const int tid = threadIdx.x;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    V z;
+    if constexpr (XB)
+      z = make_uint2(0u, 0u);
+    else
+      z = make_float4(0.f, 0.f, 0.f, 0.f);
     {
       const int p = pix0 + kt * BK + PA * (tid / GA);
       int pc = min(p, npix - 1);
@@ -264,8 +297,7 @@ struct WgLoader {
         const int iy = oy * s.stride - s.pad + kh, ix = ox * s.stride - s.pad + kw;
         const bool ok = mv && p + q < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
         const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
-        const float4 v = *reinterpret_cast<const float4*>(
-            x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ca);
+        const V v = *reinterpret_cast<const V*>(x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ca);
         ra[q] = ok ? v : z;
         if (++ox == s.OW) {  // next output pixel (rows past the end are masked)
           ox = 0;
@@ -280,18 +312,24 @@ struct WgLoader {
       const int p = pix0 + kt * BK + PB * (tid / GB);
 #pragma unroll
       for (int q = 0; q < PB; ++q) {
-        const float4 v = *reinterpret_cast<const float4*>(dy + (size_t)min(p + q, npix - 1) * s.K + cb);
+        const V v = *reinterpret_cast<const V*>(dy + (size_t)min(p + q, npix - 1) * s.K + cb);
         rb[q] = p + q < npix ? v : z;
       }
     }
   }
   // channel c of the P pixels held in r, as P consecutive bf16 (one LDS row run)
+  __device__ __forceinline__ static __bf16 chan(const float4& r, int c) {
+    return (__bf16)(c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w);
+  }
+  __device__ __forceinline__ static __bf16 chan(const uint2& r, int c) {
+    const uint32_t w = c < 2 ? r.x : r.y;
+    return __builtin_bit_cast(__bf16, (uint16_t)(c & 1 ? w >> 16 : w & 0xffffu));
+  }
   template <int P>
-  __device__ __forceinline__ static void put_col(__bf16* dst, const float4 (&r)[P], int c) {
+  __device__ __forceinline__ static void put_col(__bf16* dst, const V (&r)[P], int c) {
     __bf16 v[P];
 #pragma unroll
-    for (int q = 0; q < P; ++q)
-      v[q] = (__bf16)(c == 0 ? r[q].x : c == 1 ? r[q].y : c == 2 ? r[q].z : r[q].w);
+    for (int q = 0; q < P; ++q) v[q] = chan(r[q], c);
     if constexpr (P == 8)
       *reinterpret_cast<uint4*>(dst) = __builtin_bit_cast(uint4, v);
     else
@@ -309,10 +347,11 @@ struct WgLoader {
   }
 };
 
-template <int BM, int BN>
-__global__ __launch_bounds__(NT) void wgrad_kernel(ConvShape s, const float* __restrict__ x,
-                                                   const float* __restrict__ dy,
-                                                   float* __restrict__ part, int kchunk) {
+template <int BM, int BN, bool XB>
+__global__ __launch_bounds__(NT) void wgrad_kernel(
+    ConvShape s, const typename WgLoader<BM, BN, XB>::T* __restrict__ x,
+    const typename WgLoader<BM, BN, XB>::T* __restrict__ dy, float* __restrict__ part,
+    int kchunk) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int STAGE = (BM + BN) * LDK;
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
@@ -326,7 +365,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(ConvShape s, const float* __r
   const int nk = min(kchunk, (npix - pix0 + BK - 1) / BK);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
   const int r = lane & 31, h = lane >> 5;
-  WgLoader<BM, BN> ld(s, x, dy, m0, n0, pix0, npix);
+  WgLoader<BM, BN, XB> ld(s, x, dy, m0, n0, pix0, npix);
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -431,7 +470,8 @@ static inline long long wt_elems(const ConvShape& s) { return (long long)s.R * s
 // bf16 weight copy at the front of the workspace, split-K slabs after it
 static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 127) / 128) * 64; }
 
-static void launch(const ConvShape& s, const float* x, const __bf16* wt, const float* bias,
+template <class XT>
+static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const float* bias,
                    float* y, bool relu, float* ws, hipStream_t st) {
   const long long M = (long long)s.N * s.OH * s.OW;
   const Plan p = plan(s, bias != nullptr || relu);
@@ -440,10 +480,10 @@ static void launch(const ConvShape& s, const float* x, const __bf16* wt, const f
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    case T128x64: fwd_kernel<128, 64><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    case T64x128: fwd_kernel<64, 128><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    default: fwd_kernel<64, 64><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
   }
 #undef GRID
   if (p.z > 1) {
@@ -527,40 +567,67 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
   return n;
 }
 
+void to_bf16(const float* x, void* y, long long n, hipStream_t st) {
+  if (n % 8 != 0) throw std::runtime_error("to_bf16: n % 8 != 0");
+  long long b = (n / 8 + 255) / 256;
+  if (b > 8192) b = 8192;
+  cbf::to_bf16_kernel<<<(int)(b < 1 ? 1 : b), 256, 0, st>>>(
+      reinterpret_cast<const float4*>(x), reinterpret_cast<uint4*>(y), n / 8);
+}
+
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                   bool relu, float* ws, hipStream_t st) {
+                   bool relu, float* ws, hipStream_t st, const void* xb) {
   using namespace cbf;
   if (!conv_fwd_bf16_ok(s) || !ws) throw std::runtime_error("conv_fwd_bf16: unsupported shape");
   __bf16* wt = reinterpret_cast<__bf16*>(ws);
   convert(s, w, 0, wt, st);
-  launch(s, x, wt, bias, y, relu, ws, st);
+  if (xb)
+    launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st);
+  else
+    launch(s, x, wt, bias, y, relu, ws, st);
 }
 
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st) {
+                        hipStream_t st, const void* dyb) {
   using namespace cbf;
   if (!conv_bwd_data_bf16_ok(s) || !ws) throw std::runtime_error("conv_bwd_data_bf16: unsupported shape");
   __bf16* wt = reinterpret_cast<__bf16*>(ws);
   convert(s, w, 1, wt, st);
-  launch(dgrad_shape(s), dy, wt, nullptr, dx, false, ws, st);
+  if (dyb)
+    launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st);
+  else
+    launch(dgrad_shape(s), dy, wt, nullptr, dx, false, ws, st);
 }
 
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
-                          float* dw, hipStream_t st) {
+                          float* dw, hipStream_t st, const void* xb, const void* dyb) {
   using namespace cbf;
   if (!conv_bwd_filter_bf16_ok(s)) throw std::runtime_error("conv_bwd_filter_bf16: unsupported shape");
   const WgPlan p = wg_plan(s);
   if (p.z > 1 && !ws) throw std::runtime_error("conv_bwd_filter_bf16: split-K needs a workspace");
   float* out = p.z > 1 ? ws : dw;
   const int blocks = cdiv((long long)s.R * s.S * s.C, p.bm) * (s.K / p.bn) * p.z;
-  if (p.bm == 128 && p.bn == 128)
-    wgrad_kernel<128, 128><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
-  else if (p.bm == 128)
-    wgrad_kernel<128, 64><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
-  else if (p.bn == 128)
-    wgrad_kernel<64, 128><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
-  else
-    wgrad_kernel<64, 64><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  if (xb && dyb) {
+    const __bf16* xh = reinterpret_cast<const __bf16*>(xb);
+    const __bf16* dh = reinterpret_cast<const __bf16*>(dyb);
+    if (p.bm == 128 && p.bn == 128)
+      wgrad_kernel<128, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+    else if (p.bm == 128)
+      wgrad_kernel<128, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+    else if (p.bn == 128)
+      wgrad_kernel<64, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+    else
+      wgrad_kernel<64, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+  } else {
+    if (p.bm == 128 && p.bn == 128)
+      wgrad_kernel<128, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+    else if (p.bm == 128)
+      wgrad_kernel<128, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+    else if (p.bn == 128)
+      wgrad_kernel<64, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+    else
+      wgrad_kernel<64, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+  }
   if (p.z > 1) {
     const long long n4 = (long long)s.R * s.S * s.C * s.K / 4;
     long long b = (n4 + 255) / 256;

@@ -20,13 +20,15 @@ struct PoolShape {
 // the three ops of one layer; dw / dx / y are written, not accumulated)
 // bf16: MFMA operands converted to bf16 (fp32 accumulate, fp32 in / out); the
 // tiled family only - shapes it does not take run the fp32 gather engine
+// xb / dyb: optional bf16 copies of x / dy (to_bf16) for the bf16 family
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, float* ws, hipStream_t st, bool bf16 = false);
+              bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr);
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                   hipStream_t st, bool bf16 = false);
+                   hipStream_t st, bool bf16 = false, const void* dyb = nullptr);
 int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
-                     hipStream_t st, bool bf16 = false);
+                     hipStream_t st, bool bf16 = false, const void* xb = nullptr,
+                     const void* dyb = nullptr);
 long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue);
 // bf16 MFMA convs with 64-channel K tiles and pre-laid-out bf16 weights
 // (conv_bf16.hip): forward for C, K % 64 == 0, stride-1 backward-data; the
@@ -35,13 +37,15 @@ bool conv_fwd_bf16_ok(const ConvShape& s);
 void set_conv_variant(int slot, int v);  // tiling A/B knobs (scripts/conv_lab.py)
 bool conv_bwd_data_bf16_ok(const ConvShape& s);
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
+void to_bf16(const float* x, void* y, long long n, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                   bool relu, float* ws, hipStream_t st);
+                   bool relu, float* ws, hipStream_t st, const void* xb = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st);
+                        hipStream_t st, const void* dyb = nullptr);
 bool conv_bwd_filter_bf16_ok(const ConvShape& s);
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
-                          float* dw, hipStream_t st);
+                          float* dw, hipStream_t st, const void* xb = nullptr,
+                          const void* dyb = nullptr);
 // LDS-tiled conv family (conv_tiled.hip), used by the launchers above for the
 // shapes it supports
 bool conv_fwd_tiled_ok(const ConvShape& s);

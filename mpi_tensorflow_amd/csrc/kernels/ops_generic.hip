@@ -466,8 +466,8 @@ static inline int grid1d(long long n) {
 // 3-channel stem); the per-element gather engine above covers the rest
 // (LeNet-5's 3- and 6-channel layers, thin FC layers).
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, float* ws, hipStream_t st, bool bf16) {
-  if (bf16 && conv_fwd_bf16_ok(s)) return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st);
+              bool relu, float* ws, hipStream_t st, bool bf16, const void* xb) {
+  if (bf16 && conv_fwd_bf16_ok(s)) return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb);
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
   const int M = s.N * s.OH * s.OW;
   const int blocks = ((M + CFG_F::BM - 1) / CFG_F::BM) * ((s.K + CFG_F::BN - 1) / CFG_F::BN);
@@ -489,8 +489,8 @@ static void gather_data_plan(const ConvShape& s, int& z, int& kchunk) {
 }
 
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                   hipStream_t st, bool bf16) {
-  if (bf16 && conv_bwd_data_bf16_ok(s)) return conv_bwd_data_bf16(s, dy, w, dx, ws, st);
+                   hipStream_t st, bool bf16, const void* dyb) {
+  if (bf16 && conv_bwd_data_bf16_ok(s)) return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb);
   if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16);
   const int M = s.N * s.H * s.W;
   const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
@@ -533,8 +533,10 @@ long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue) {
 }
 
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* part, float* dw,
-                     hipStream_t st, bool bf16) {
-  if (bf16 && conv_bwd_filter_bf16_ok(s)) return conv_bwd_filter_bf16(s, x, dy, part, dw, st);
+                     hipStream_t st, bool bf16, const void* xb,
+                     const void* dyb) {
+  if (bf16 && conv_bwd_filter_bf16_ok(s))
+    return conv_bwd_filter_bf16(s, x, dy, part, dw, st, xb, dyb);
   if (conv_bwd_filter_tiled_ok(s)) return conv_bwd_filter_tiled(s, x, dy, part, dw, st, bf16);
   const int Mw = s.R * s.S * s.C;
   const int tiles = ((Mw + CFG_W::BM - 1) / CFG_W::BM) * ((s.K + CFG_W::BN - 1) / CFG_W::BN);

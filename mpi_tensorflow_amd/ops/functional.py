@@ -82,9 +82,16 @@ class _ConvFn(torch.autograd.Function):
         x = x.contiguous()
         y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
         ctx.bf16 = _CONV_BF16
-        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), stream_handle(),
-                       ctx.bf16)
-        ctx.save_for_backward(x, w, y)
+        s = stream_handle()
+        # bf16 family: the conv reads a bf16 copy of its input (half the
+        # operand bytes of the fp32 tensor; kept for the filter gradient)
+        xb = None
+        if ctx.bf16 and C.ops.conv_bf16_ok(shape):
+            xb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+            C.ops.to_bf16(ptr(x), ptr(xb), x.numel(), s)
+        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), s, ctx.bf16,
+                       ptr(xb))
+        ctx.save_for_backward(x, w, y, xb)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
         return y
@@ -92,7 +99,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        x, w, y = ctx.saved_tensors
+        x, w, y, xb = ctx.saved_tensors
         s = stream_handle()
         dy = dy.contiguous()
         if ctx.relu:
@@ -100,7 +107,12 @@ class _ConvFn(torch.autograd.Function):
             C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
             dy = dym
         sh = ctx.shape
-        C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s, ctx.bf16)
+        dyb = None
+        if xb is not None:  # one bf16 copy of dY feeds the filter grad and the dgrad
+            dyb = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device)
+            C.ops.to_bf16(ptr(dy), ptr(dyb), dy.numel(), s)
+        C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s, ctx.bf16, ptr(xb),
+                              ptr(dyb))
         if ctx.has_b:
             scratch = torch.empty(sh.K, device=dy.device, dtype=dy.dtype)
             C.ops.colsum2(ptr(dy), 0, sh.N * sh.OH * sh.OW, sh.K, ptr(ctx.gb), ptr(scratch), 0,
@@ -109,7 +121,7 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
-            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16)
+            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16, ptr(dyb))
         return dx, None, None, None, None, None, None, None
 
 
