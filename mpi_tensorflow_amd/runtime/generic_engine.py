@@ -5,9 +5,11 @@ param / grad / momentum buffers, the reference's LR schedule and momentum
 SGD (/root/reference/mpipy.py:59-66), batch offset (step*B) % (N-B), DP by
 per-step gradient all-reduce of the flat grad buffer.
 
-With cfg.dtype == "bf16" the convolutions (and linear layers) run their
-MFMAs on bf16 operands converted while staged into LDS (fp32 accumulation;
-activations, BatchNorm, gradients and the optimizer stay fp32).
+With cfg.dtype == "bf16" the convolutions run their MFMAs on bf16 operands
+(bf16 copies of activations / output gradients and re-laid bf16 weights,
+csrc/kernels/conv_bf16.hip; fp32 accumulation); the stored activations,
+BatchNorm, linear layers (fp32 library GEMMs), gradients and the optimizer
+stay fp32.
 
 On GPU one training step is: batch gather from the device-resident shard at
 the device step offset -> forward/backward through the native NHWC kernels
@@ -72,6 +74,7 @@ class GenericEngine:
         self.use_graph = cfg.graph and self.on_gpu
         self.graph_steps = max(1, cfg.graph_steps)
         self._graphs = {}
+        self._warm = False
         self.loss_buf = torch.zeros((), device=device)
         self.bucketer = None
         if self.on_gpu:
@@ -171,8 +174,35 @@ class GenericEngine:
             self._graphs[n] = g
         return g
 
+    def _warmup(self, k: int) -> int:
+        """Eager warm-up on a side stream before the first capture (torch's
+        documented requirement for capturing autograd); real training steps.
+        Returns how many it ran."""
+        if not self.use_graph or self._warm or k <= 0:
+            return 0
+        n = min(3, k)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(n):
+                self._step_gpu()
+        torch.cuda.current_stream().wait_stream(s)
+        self._warm = True
+        self.step += n
+        return n
+
     def capture(self, k: int) -> None:
-        pass  # graphs are captured lazily after the eager warm-up in train()
+        """Pre-captures the graphs `train(k)` will replay (G-step graph and the
+        k % G remainder), so a timed train(k) launches only graph replays.  May
+        run the (untimed) eager warm-up steps first."""
+        if not (self.on_gpu and self.use_graph) or k <= 0:
+            return
+        self._warmup(3)
+        G = self.graph_steps
+        if k >= G:
+            self._graph(G)
+        if k % G:
+            self._graph(k % G)
 
     def train(self, k: int) -> None:
         if k <= 0:
@@ -182,18 +212,7 @@ class GenericEngine:
                 self._step_cpu()
                 self.step += 1
             return
-        done = 0
-        if self.use_graph and not self._graphs:
-            # eager warm-up on a side stream before the first capture (torch's
-            # documented requirement for capturing autograd); real steps
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for _ in range(min(3, k)):
-                    self._step_gpu()
-                    done += 1
-            torch.cuda.current_stream().wait_stream(s)
-        left = k - done
+        left = k - self._warmup(k)
         if not self.use_graph:
             for _ in range(left):
                 self._step_gpu()
@@ -206,9 +225,13 @@ class GenericEngine:
                     g.replay()
             else:
                 rem = left
-            for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
-                self._step_gpu()
-        self.step += k
+            gr = self._graphs.get(rem) if (rem and self.use_graph) else None
+            if gr is not None:  # remainder graph pre-captured by capture()
+                gr.replay()
+            else:
+                for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
+                    self._step_gpu()
+        self.step += left
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
