@@ -194,6 +194,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
   g.def("set_conv_variant", &gops::set_conv_variant, py::arg("slot"), py::arg("value"));
   g.def("conv_bf16_ok", &gops::conv_fwd_bf16_ok);
+  g.def("im2col_bf16", [](const gops::ConvShape& s, uintptr_t x, int kp, uintptr_t col,
+                          uintptr_t st) {
+    gops::im2col_bf16(s, P<const float>(x), kp, P<void>(col), S(st));
+    check_launch();
+  });
   g.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
     gops::to_bf16(P<const float>(x), P<void>(y), n, S(st));
     check_launch();

@@ -415,12 +415,13 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(
 }
 
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
-                                                        long long n4, float4* __restrict__ out) {
+                                                        long long zs, long long n4,
+                                                        float4* __restrict__ out) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
     for (int z = 1; z < nz; ++z) {
-      const float4 b = part[z * n4 + i];
+      const float4 b = part[z * zs + i];
       a.x += b.x;
       a.y += b.y;
       a.z += b.z;
@@ -430,7 +431,43 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
   }
 }
 
+// In-place first stage for deep, narrow slab stacks (the im2col'd stem's
+// filter gradient: 256 slices of 192 x 64): group g of G slices is summed
+// into its first slice, so the final slab_sum4 pass (zstride G) reads nz / G
+// slices per thread instead of nz on 12 blocks.
+__global__ __launch_bounds__(256) void slab_fold4_kernel(float4* __restrict__ part, int nz, int G,
+                                                         long long n4) {
+  const int z0 = blockIdx.y * G, z1 = min(nz, z0 + G);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 a = part[z0 * n4 + i];
+    for (int z = z0 + 1; z < z1; ++z) {
+      const float4 b = part[z * n4 + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    part[z0 * n4 + i] = a;
+  }
+}
+
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// Deterministic sum of nz slabs of n4 float4s into out (fixed association
+// order for a given nz).
+static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st) {
+  long long b = (n4 + 255) / 256;
+  if (b > 4096) b = 4096;
+  int G = 1;
+  if (b < 128 && nz >= 32) {
+    G = 8;
+    slab_fold4_kernel<<<dim3((int)b, cdiv(nz, G)), 256, 0, st>>>(reinterpret_cast<float4*>(slabs),
+                                                                 nz, G, n4);
+  }
+  slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), cdiv(nz, G),
+                                          n4 * G, n4, reinterpret_cast<float4*>(out));
+}
 
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
 static inline int tm(Tile t) { return (t == T128x128 || t == T128x64) ? 128 : 64; }
@@ -486,13 +523,7 @@ static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const floa
     default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
   }
 #undef GRID
-  if (p.z > 1) {
-    const long long n4 = M * s.K / 4;
-    long long b = (n4 + 255) / 256;
-    if (b > 4096) b = 4096;
-    slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), p.z, n4,
-                                            reinterpret_cast<float4*>(y));
-  }
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st);
 }
 
 // wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
@@ -510,7 +541,11 @@ static inline WgPlan wg_plan(const ConvShape& s) {
   const int target = g_conv_variant[1] > 0 ? g_conv_variant[1] : 1024;
   int z = cdiv(target, tiles);
   if (z > ktiles / 4) z = ktiles / 4;
-  if (z > (g_conv_variant[1] > 0 ? 128 : 64)) z = g_conv_variant[1] > 0 ? 128 : 64;
+  // <= 4 output tiles (the im2col'd stem: 192 x 64) need deep pixel splits to
+  // fill the chip; otherwise 64 slices (measured: more slices cost more slab
+  // traffic than they win on ResNet-18 layer1)
+  const int zcap = g_conv_variant[1] > 0 ? 128 : (tiles <= 4 ? 256 : 64);
+  if (z > zcap) z = zcap;
   if (z < 1) z = 1;
   const int kchunk = cdiv(ktiles, z);
   return {bm, bn, cdiv(ktiles, kchunk), kchunk};
@@ -565,6 +600,48 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
     if (p.z > 1) n = std::max(n, (long long)p.z * s.R * s.S * s.C * s.K);
   }
   return n;
+}
+
+// bf16 im2col for thin-input convs (the 3-channel ResNet stem).  Per-tap row
+// segments: for tap row kh the S*C inputs X[n, oy s - p + kh, ox s - p + kw,
+// ci] (kw, ci) are contiguous in NHWC, so col[m][kh * seg + j] = that run
+// (j < S C, zero-padded to seg = roundup(S C, 8)), zero from R seg up to kp
+// (% 64).  The conv then runs as a 1x1 conv over kp channels on the kernels
+// above (forward and filter gradient) with the weights laid out to match
+// (ops/functional.py _ConvIm2colFn).  Thread = 8 consecutive k (one 16-byte
+// store, consecutive threads -> consecutive stores); 32-bit index math with
+// one divide per coordinate instead of the per-element (kh, kw, ci) divides.
+__global__ __launch_bounds__(256) void im2col_bf16_kernel(ConvShape s, const float* __restrict__ x,
+                                                          int kp, int seg, uint4* __restrict__ col) {
+  const int kq = kp / 8, sq = seg / 8, sc = s.S * s.C;
+  const int total = s.N * s.OH * s.OW * kq;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int m = i / kq, c = i - m * kq;
+    const int kh = c / sq, j0 = (c - kh * sq) * 8;
+    const int ox = m % s.OW, t = m / s.OW;
+    const int oy = t % s.OH, n = t / s.OH;
+    const int iy = oy * s.stride - s.pad + kh, ix0 = ox * s.stride - s.pad;
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (kh < s.R && iy >= 0 && iy < s.H) {
+      const int jlo = max(0, -ix0) * s.C, jhi = min(sc, (s.W - ix0) * s.C);
+      const long long rowbase = ((long long)(n * s.H + iy) * s.W + ix0) * s.C;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j0 + j >= jlo && j0 + j < jhi) v[j] = x[rowbase + j0 + j];
+    }
+    col[i] = cbf::pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+  }
+}
+
+void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStream_t st) {
+  const int seg = (s.S * s.C + 7) / 8 * 8;
+  if (kp % 64 != 0 || kp < s.R * seg) throw std::runtime_error("im2col_bf16: bad kp");
+  const long long total = (long long)s.N * s.OH * s.OW * kp / 8;
+  if (total >= (1LL << 31) || (long long)s.N * s.H * s.W * s.C >= (1LL << 31))
+    throw std::runtime_error("im2col_bf16: tensor too large for 32-bit indexing");
+  long long b = (total + 255) / 256;
+  if (b > 16384) b = 16384;
+  im2col_bf16_kernel<<<(int)b, 256, 0, st>>>(s, x, kp, seg, reinterpret_cast<uint4*>(col));
 }
 
 void to_bf16(const float* x, void* y, long long n, hipStream_t st) {
@@ -628,13 +705,7 @@ void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, f
     else
       wgrad_kernel<64, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
   }
-  if (p.z > 1) {
-    const long long n4 = (long long)s.R * s.S * s.C * s.K / 4;
-    long long b = (n4 + 255) / 256;
-    if (b > 4096) b = 4096;
-    slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(ws), p.z, n4,
-                                            reinterpret_cast<float4*>(dw));
-  }
+  if (p.z > 1) slab_reduce(ws, p.z, (long long)s.R * s.S * s.C * s.K / 4, dw, st);
 }
 
 }  // namespace gops

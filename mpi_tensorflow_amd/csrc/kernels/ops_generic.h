@@ -38,6 +38,7 @@ void set_conv_variant(int slot, int v);  // tiling A/B knobs (scripts/conv_lab.p
 bool conv_bwd_data_bf16_ok(const ConvShape& s);
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
 void to_bf16(const float* x, void* y, long long n, hipStream_t st);
+void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,

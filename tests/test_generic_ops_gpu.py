@@ -99,10 +99,11 @@ def test_batchnorm(cuda_dev, relu, res):
     assert torch.allclose(rm.cpu(), 0.1 * x.mean(dim=(0, 1, 2)), atol=1e-5)
 
 
+@pytest.mark.parametrize("C", [10, 16])  # scalar and float4 kernels
 @pytest.mark.parametrize("k,stride,pad,H", [(2, 2, 0, 12), (3, 2, 1, 13)])
-def test_maxpool(cuda_dev, k, stride, pad, H):
+def test_maxpool(cuda_dev, k, stride, pad, H, C):
     g = torch.Generator().manual_seed(2)
-    x = torch.randn(3, H, H, 10, generator=g)
+    x = torch.randn(3, H, H, C, generator=g)
     xr = x.clone().requires_grad_(True)
     yr = F.max_pool2d(xr.permute(0, 3, 1, 2), k, stride, pad).permute(0, 2, 3, 1)
     dy = torch.randn(yr.shape, generator=g)
@@ -256,3 +257,33 @@ def test_trainer_eval_between_graph_replays(cuda_dev):
     s = Trainer(cfg).run()
     assert np.isfinite(s.final_loss), s
     assert s.final_test_error_global < 50.0, s
+
+
+@pytest.mark.parametrize("R,st,pad,K,kp", [(7, 2, 3, 64, 192), (5, 1, 2, 128, 128)])
+def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp):
+    """bf16 mode: a thin-input conv whose input needs no gradient (ResNet stem,
+    7x7 s2, 3 -> 64) runs as a bf16 im2col + 1x1 conv on the bf16 family;
+    output and filter gradient vs fp32 torch within bf16 operand rounding."""
+    from mpi_tensorflow_amd.ops import native
+
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 37, 41, 3, generator=g)
+    w = torch.randn(R, R, 3, K, generator=g) * 0.1
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(x.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), stride=st,
+                  padding=pad).permute(0, 2, 3, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    wp = _param(w.to(cuda_dev))
+    xg = x.to(cuda_dev)
+    sh = native().ops.ConvShape(2, 37, 41, 3, K, R, R, st, pad)
+    Fn.set_conv_bf16(True)
+    try:
+        assert Fn._im2col_kp(sh, xg, False, False) == kp
+        yg = Fn.conv2d(xg, wp, None, st, pad, False)
+        yg.backward(dy.to(cuda_dev))
+    finally:
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    assert _rel(yg.detach().cpu(), yr.detach()) < 1e-2
+    assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-2
