@@ -237,18 +237,18 @@ PYBIND11_MODULE(_C, m) {
   g.def("bn_fwd", [](uintptr_t x, long long rows, int C, uintptr_t gm, uintptr_t bt, uintptr_t res,
                      uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t ws, float eps,
                      float momentum, bool relu, bool training, uintptr_t rmean, uintptr_t rvar,
-                     uintptr_t st) {
+                     uintptr_t st, uintptr_t yb) {
     gops::bn_fwd(P<const float>(x), rows, C, P<const float>(gm), P<const float>(bt),
                  P<const float>(res), P<float>(y), P<float>(mean), P<float>(rstd), P<float>(ws), eps,
-                 momentum, relu, training, P<float>(rmean), P<float>(rvar), S(st));
+                 momentum, relu, training, P<float>(rmean), P<float>(rvar), S(st), P<void>(yb));
     check_launch();
   });
   g.def("bn_bwd", [](uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                      uintptr_t gm, long long rows, int C, bool relu, uintptr_t ws, uintptr_t dg,
-                     uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st) {
+                     uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st, uintptr_t dxb) {
     gops::bn_bwd(P<const float>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
                  P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(ws), P<float>(dg),
-                 P<float>(db), P<float>(dx), P<float>(dres), S(st));
+                 P<float>(db), P<float>(dx), P<float>(dres), S(st), P<void>(dxb));
     check_launch();
   });
   g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {

@@ -13,6 +13,11 @@
 // mean, rstd), so neither dy' nor xhat is ever materialised.  The BN forward
 // finalize also updates the running statistics (momentum, unbiased variance),
 // so the whole layer is three kernels with no host-side tensor ops.
+//
+// bf16 conv mode: the apply kernels can also write a bf16 copy of their
+// output (y forward, dx backward), which the next conv reads as its bf16
+// operand (forward input / dY of the filter and data gradients) instead of
+// a separate to_bf16 pass over the fp32 tensor.
 #include <stdexcept>
 
 #include "common.h"
@@ -24,6 +29,11 @@ namespace bn {
 enum Mode { SUM_SQ = 0, SUM_PROD = 1, BN_BWD = 2 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// 4 floats -> 4 bf16 (round to nearest even, as to_bf16_kernel)
+__device__ __forceinline__ uint2 pack4(float4 a) {
+  __bf16 v[4] = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w};
+  return __builtin_bit_cast(uint2, v);
+}
 
 template <int MODE>
 __global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ a,
@@ -168,7 +178,8 @@ __global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
                                                     const float* __restrict__ bb,
                                                     const float* __restrict__ res,
                                                     float* __restrict__ y, long long n4, int C,
-                                                    int relu, int eval, float eps) {
+                                                    int relu, int eval, float eps,
+                                                    uint2* __restrict__ yb) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int cq = C >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -192,6 +203,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
       o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
     }
     *reinterpret_cast<float4*>(y + 4 * i) = o;
+    if (yb) yb[i] = pack4(o);
   }
 }
 
@@ -200,7 +212,8 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
     const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ s1, const float* __restrict__ s2, float* __restrict__ dx,
-    float* __restrict__ dres, long long n4, int C, long long rows, int relu) {
+    float* __restrict__ dres, long long n4, int C, long long rows, int relu,
+    uint2* __restrict__ dxb) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int cq = C >> 2;
   const float inv = 1.f / (float)rows;
@@ -223,6 +236,7 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
     o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
     o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
     *reinterpret_cast<float4*>(dx + 4 * i) = o;
+    if (dxb) dxb[i] = pack4(o);
   }
 }
 
@@ -279,7 +293,8 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
-            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st) {
+            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
+            void* yb) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_fwd: needs C % 4 == 0, C <= 1024");
   const long long n4 = rows * C / 4;
   if (training) {
@@ -288,16 +303,18 @@ void bn_fwd(const float* x, long long rows, int C, const float* g, const float* 
     bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, nullptr, nullptr, 1, rows, eps,
                                                      momentum, mean, rstd, rmean, rvar);
     bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
-                                                          relu ? 1 : 0, 0, eps);
+                                                          relu ? 1 : 0, 0, eps,
+                                                          reinterpret_cast<uint2*>(yb));
   } else {
     bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4, C,
-                                                          relu ? 1 : 0, 1, eps);
+                                                          relu ? 1 : 0, 1, eps,
+                                                          reinterpret_cast<uint2*>(yb));
   }
 }
 
 void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st) {
+            float* dx, float* dres, hipStream_t st, void* dxb) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
   const int nb = bn::nblocks(rows, C);
   run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, st);
@@ -306,7 +323,8 @@ void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, 
                                                    nullptr, nullptr, nullptr);
   const long long n4 = rows * C / 4;
   bn::bwd_apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx,
-                                                            dres, n4, C, rows, relu ? 1 : 0);
+                                                            dres, n4, C, rows, relu ? 1 : 0,
+                                                            reinterpret_cast<uint2*>(dxb));
 }
 
 }  // namespace gops

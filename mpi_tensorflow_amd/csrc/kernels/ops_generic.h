@@ -77,11 +77,13 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 // (+ res) (ReLU).
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
-            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st);
+            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
+            void* yb = nullptr);  // yb: optional bf16 copy of y
 // dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu)
 void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st);
+            float* dx, float* dres, hipStream_t st,
+            void* dxb = nullptr);  // dxb: optional bf16 copy of dx
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);

@@ -74,6 +74,31 @@ def _grad_done(*views) -> None:
                 _GRAD_HOOK(v)
 
 
+# Producer-written bf16 copies: in bf16 conv mode the BatchNorm apply kernels
+# also write a bf16 copy of their output (forward y, backward dx), attached to
+# the fp32 tensor; a consuming conv reads it as its bf16 operand instead of
+# running its own to_bf16 pass.  The copy is used only while the tensor is
+# unmodified (same version counter and storage), else the conv converts.
+def _attach_bf16(t: torch.Tensor, tb: torch.Tensor) -> None:
+    t._mta_bf16 = (tb, t._version, t.data_ptr())
+
+
+def _bf16_copy(t: torch.Tensor, s) -> torch.Tensor:
+    a = getattr(t, "_mta_bf16", None)
+    if a is not None and a[1] == t._version and a[2] == t.data_ptr() and t.is_contiguous():
+        return a[0]
+    tb = torch.empty(t.shape, dtype=torch.bfloat16, device=t.device)
+    native().ops.to_bf16(ptr(t), ptr(tb), t.numel(), s)
+    return tb
+
+
+def _bf16_out(like: torch.Tensor) -> Optional[torch.Tensor]:
+    """A bf16 twin for a BN output when a bf16 conv can consume it."""
+    if not _CONV_BF16 or like.shape[-1] % 64 != 0:
+        return None
+    return torch.empty(like.shape, dtype=torch.bfloat16, device=like.device)
+
+
 # ------------------------------------------------------------------- conv --
 class _ConvFn(torch.autograd.Function):
     @staticmethod
@@ -87,8 +112,7 @@ class _ConvFn(torch.autograd.Function):
         # operand bytes of the fp32 tensor; kept for the filter gradient)
         xb = None
         if ctx.bf16 and C.ops.conv_bf16_ok(shape):
-            xb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-            C.ops.to_bf16(ptr(x), ptr(xb), x.numel(), s)
+            xb = _bf16_copy(x, s)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), s, ctx.bf16,
                        ptr(xb))
         ctx.save_for_backward(x, w, y, xb)
@@ -109,8 +133,7 @@ class _ConvFn(torch.autograd.Function):
         sh = ctx.shape
         dyb = None
         if xb is not None:  # one bf16 copy of dY feeds the filter grad and the dgrad
-            dyb = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device)
-            C.ops.to_bf16(ptr(dy), ptr(dyb), dy.numel(), s)
+            dyb = _bf16_copy(dy, s)
         C.ops.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ctx.ws), ptr(ctx.gw), s, ctx.bf16, ptr(xb),
                               ptr(dyb))
         if ctx.has_b:
@@ -161,8 +184,7 @@ class _ConvIm2colFn(torch.autograd.Function):
         s1 = ctx.s1
         s = stream_handle()
         dy = dy.contiguous()
-        dyb = torch.empty(dy.shape, dtype=torch.bfloat16, device=dy.device)
-        C.ops.to_bf16(ptr(dy), ptr(dyb), dy.numel(), s)
+        dyb = _bf16_copy(dy, s)
         gpad = torch.empty((s1.C, s1.K), device=dy.device, dtype=torch.float32)
         C.ops.conv_bwd_filter(s1, 0, 0, ptr(ctx.ws), ptr(gpad), s, True, ptr(col), ptr(dyb))
         ctx.gw.view(ctx.R, ctx.sc, s1.K).copy_(
@@ -288,9 +310,13 @@ class _BNFn(torch.autograd.Function):
         mean = torch.empty(Cc, device=x.device)
         rstd = torch.empty(Cc, device=x.device)
         ws = _WS.get(max(C.ops.chan_reduce_ws_floats(rows, Cc), 4), x.device)
+        yb = _bf16_out(y)
         # batch statistics, running-stat update and the fused apply, on device
         C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(y), ptr(mean), ptr(rstd),
-                     ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle())
+                     ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle(),
+                     ptr(yb))
+        if yb is not None:
+            _attach_bf16(y, yb)
         ctx.save_for_backward(x, y, mean, rstd, g)
         ctx.relu, ctx.gg, ctx.gb, ctx.has_res = relu, gg, gb, res is not None
         ctx.ws = ws
@@ -305,8 +331,12 @@ class _BNFn(torch.autograd.Function):
         rows = x.numel() // Cc
         dx = torch.empty_like(dy)
         dres = torch.empty_like(dy) if ctx.has_res else None
+        dxb = _bf16_out(dx)
         C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
-                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres), stream_handle())
+                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres), stream_handle(),
+                     ptr(dxb))
+        if dxb is not None:
+            _attach_bf16(dx, dxb)
         _grad_done(ctx.gg, ctx.gb)
         return dx, None, None, dres, None, None, None, None, None, None, None, None
 
@@ -325,7 +355,7 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
         Cc = x.shape[-1]
         C.ops.bn_fwd(ptr(x.contiguous()), x.numel() // Cc, Cc, ptr(g.value), ptr(b.value),
                      ptr(res), ptr(y), 0, 0, 0, eps, momentum, relu, False, ptr(rmean),
-                     ptr(rvar), stream_handle())
+                     ptr(rvar), stream_handle(), 0)
         return y
     xn = x.permute(0, 3, 1, 2)
     y = F.batch_norm(xn, rmean, rvar, g.value, b.value, training, momentum, eps).permute(0, 2, 3, 1)

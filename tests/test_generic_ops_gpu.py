@@ -287,3 +287,40 @@ def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp):
     torch.cuda.synchronize()
     assert _rel(yg.detach().cpu(), yr.detach()) < 1e-2
     assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-2
+
+
+def test_bn_bf16_twin_feeds_conv(cuda_dev):
+    """bf16 mode: BatchNorm writes a bf16 twin of y (forward) and dx
+    (backward); the consuming conv reads it instead of converting.  The result
+    must be bit-identical to the convert-it-yourself path."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 10, 10, 64, generator=g).to(cuda_dev)
+    w = (torch.randn(3, 3, 64, 64, generator=g) * 0.05).to(cuda_dev)
+    dy = torch.randn(4, 10, 10, 64, generator=g).to(cuda_dev)
+    outs = []
+    Fn.set_conv_bf16(True)
+    try:
+        for use_twin in (True, False):
+            xg = x.clone().requires_grad_(True)
+            gam, bet = _param(torch.ones(64, device=cuda_dev)), _param(torch.zeros(64, device=cuda_dev))
+            wp = _param(w)
+            rm, rv = torch.zeros(64, device=cuda_dev), torch.ones(64, device=cuda_dev)
+            attach = Fn._attach_bf16
+            if not use_twin:  # twins are written but never handed to the conv
+                Fn._attach_bf16 = lambda t, tb: None
+            try:
+                h = Fn.batchnorm(xg, gam, bet, rm, rv, True, relu=True)
+                assert hasattr(h, "_mta_bf16") == use_twin
+                z = Fn.conv2d(h, wp, None, 1, 1, False)
+                h2 = Fn.batchnorm(z, _param(torch.ones(64, device=cuda_dev)),
+                                  _param(torch.zeros(64, device=cuda_dev)), rm.clone(), rv.clone(),
+                                  True)
+                h2.backward(dy)
+            finally:
+                Fn._attach_bf16 = attach
+            torch.cuda.synchronize()
+            outs.append((h2.detach().clone(), xg.grad.clone(), wp.grad_view.clone()))
+    finally:
+        Fn.set_conv_bf16(False)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
