@@ -583,6 +583,53 @@ __global__ __launch_bounds__(NT) void filter_gather_kernel(ConvShape s, const fl
   }
 }
 
+__device__ __forceinline__ void add4(float4& a, const float4 b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+
+// Deep, narrow slab stacks (the thin gather-path filter gradients of LeNet:
+// 128 slices of a few hundred floats, 1-3 blocks of slab_sum4_kernel whose
+// threads each walk a 128-long chain of dependent L2 loads, ~26 us): block =
+// 64 float4 outputs x 4 slice groups, 4 independent partial sums per thread
+// (16 loads in flight), groups combined through LDS in a fixed order, so the
+// result is deterministic for a given nz.
+__global__ __launch_bounds__(256) void slab_sum4_deep_kernel(const float4* __restrict__ part,
+                                                             int nz, long long n4,
+                                                             float4* __restrict__ out) {
+  __shared__ float4 red[4][64];
+  const int o = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const long long i = (long long)blockIdx.x * 64 + o;
+  float4 a[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) a[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    int z = g;
+    for (; z + 12 < nz; z += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(long long)(z + 4 * u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) add4(a[u], v[u]);
+    }
+    for (; z < nz; z += 4) add4(a[0], part[(long long)z * n4 + i]);
+  }
+  add4(a[0], a[1]);
+  add4(a[2], a[3]);
+  add4(a[0], a[2]);
+  red[g][o] = a[0];
+  __syncthreads();
+  if (g == 0 && i < n4) {
+    float4 r = red[0][o];
+    add4(r, red[1][o]);
+    add4(r, red[2][o]);
+    add4(r, red[3][o]);
+    out[i] = r;
+  }
+}
+
 // Deterministic slab reduction, float4-vectorised (n % 4 == 0).
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
                                                         long long n4, float4* __restrict__ out) {
@@ -667,6 +714,11 @@ static inline void data_plan(const ConvShape& s, Tile& t, int& z, int& kps) {
 static inline void slab_sum(const float* part, int z, long long n, float* out, hipStream_t st) {
   long long b = (n / 4 + 255) / 256;
   if (b > 4096) b = 4096;
+  if (b < 64 && z >= 16) {  // deep, narrow stack: spread the slices over the block
+    slab_sum4_deep_kernel<<<cdiv(n / 4, 64), 256, 0, st>>>(reinterpret_cast<const float4*>(part),
+                                                            z, n / 4, reinterpret_cast<float4*>(out));
+    return;
+  }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(part), z, n / 4,
                                           reinterpret_cast<float4*>(out));
 }
