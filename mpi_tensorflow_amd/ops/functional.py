@@ -268,9 +268,12 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, relu, gw, gb):
         x = x.contiguous()
-        y = torch.addmm(b, x, w) if b is not None else torch.mm(x, w)
-        if relu:
-            y = torch.relu_(y)
+        if relu and b is not None:  # bias + ReLU in the library GEMM's epilogue
+            y = torch._addmm_activation(b, x, w)
+        else:
+            y = torch.addmm(b, x, w) if b is not None else torch.mm(x, w)
+            if relu:
+                y = torch.relu_(y)
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.relu, ctx.gw, ctx.gb = relu, gw, gb
         ctx.has_b = b is not None
@@ -279,8 +282,11 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
-        if ctx.relu:
-            dy = dy * (y > 0)
+        if ctx.relu:  # one native mask launch instead of compare + multiply
+            dy = dy.contiguous()
+            dym = torch.empty_like(dy)
+            native().ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), stream_handle())
+            dy = dym
         torch.mm(x.t(), dy, out=ctx.gw)
         if ctx.has_b:
             torch.sum(dy, dim=0, out=ctx.gb)
