@@ -527,6 +527,61 @@ static inline int grid1d(long long n) {
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
 
+// Direct VALU forward conv for thin layers (LeNet-5: 3 / 6 input channels,
+// 6 / 16 outputs; reduction length R S C <= 512).  The gather engine's
+// 64-wide output tiles leave 90 % of the MFMA lanes idle on K = 6 / 16 and
+// run the short reduction as a serial K-tile chain (24 us per LeNet conv);
+// here the whole HWIO filter sits in LDS, one thread computes one (pixel,
+// output channel) with bias + ReLU fused, consecutive threads take
+// consecutive channels (coalesced stores, conflict-free LDS reads, the
+// input pixel is a wave-wide broadcast).
+constexpr int DIRECT_W_MAX = 8192;  // filter floats staged in LDS (32 KB)
+
+// CT: compile-time input channel count (0 = runtime s.C); with it the
+// channel and filter-column loops unroll, so a thread issues its input loads
+// back to back instead of one dependent load -> FMA round trip at a time.
+template <int CT>
+__global__ __launch_bounds__(256) void conv_fwd_direct_kernel(ConvShape s,
+                                                              const float* __restrict__ x,
+                                                              const float* __restrict__ w,
+                                                              const float* __restrict__ bias,
+                                                              float* __restrict__ y, int relu) {
+  __shared__ float wl[DIRECT_W_MAX];
+  const int nw = s.R * s.S * s.C * s.K;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) wl[i] = w[i];
+  __syncthreads();
+  const long long total = (long long)s.N * s.OH * s.OW * s.K;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int C = CT > 0 ? CT : s.C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int co = (int)(i % s.K);
+    const long long m = i / s.K;
+    const int ox = (int)(m % s.OW);
+    const long long t = m / s.OW;
+    const int oy = (int)(t % s.OH), n = (int)(t / s.OH);
+    float acc = bias ? bias[co] : 0.f;
+    for (int r = 0; r < s.R; ++r) {
+      const int iy = oy * s.stride - s.pad + r;
+      if (iy < 0 || iy >= s.H) continue;
+#pragma unroll 5
+      for (int q = 0; q < s.S; ++q) {
+        const int ix = ox * s.stride - s.pad + q;
+        if (ix < 0 || ix >= s.W) continue;
+        const float* xp = x + (((long long)n * s.H + iy) * s.W + ix) * C;
+        const float* wp = wl + (r * s.S + q) * C * s.K + co;
+#pragma unroll
+        for (int ci = 0; ci < C; ++ci) acc = fmaf(xp[ci], wp[ci * s.K], acc);
+      }
+    }
+    y[i] = relu ? fmaxf(acc, 0.f) : acc;
+  }
+}
+
+static inline bool conv_fwd_direct_ok(const ConvShape& s) {
+  return s.C < 32 && s.K <= 64 && s.R * s.S * s.C <= 512 &&
+         (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX;
+}
+
 // ------------------------------------------------------------ launchers ----
 // The LDS-tiled conv family (conv_tiled.hip) takes every shape it supports
 // (channel counts that are multiples of 32 / 4: all of ResNet-18 but its
@@ -536,6 +591,18 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
               bool relu, float* ws, hipStream_t st, bool bf16, const void* xb) {
   if (bf16 && conv_fwd_bf16_ok(s)) return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb);
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
+  if (conv_fwd_direct_ok(s)) {
+    const long long total = (long long)s.N * s.OH * s.OW * s.K;
+    const int b = grid1d(total), rl = relu ? 1 : 0;
+    switch (s.C) {
+      case 1: conv_fwd_direct_kernel<1><<<b, 256, 0, st>>>(s, x, w, bias, y, rl); break;
+      case 3: conv_fwd_direct_kernel<3><<<b, 256, 0, st>>>(s, x, w, bias, y, rl); break;
+      case 6: conv_fwd_direct_kernel<6><<<b, 256, 0, st>>>(s, x, w, bias, y, rl); break;
+      case 8: conv_fwd_direct_kernel<8><<<b, 256, 0, st>>>(s, x, w, bias, y, rl); break;
+      default: conv_fwd_direct_kernel<0><<<b, 256, 0, st>>>(s, x, w, bias, y, rl);
+    }
+    return;
+  }
   const int M = s.N * s.OH * s.OW;
   const int blocks = ((M + CFG_F::BM - 1) / CFG_F::BM) * ((s.K + CFG_F::BN - 1) / CFG_F::BN);
   conv_fwd_kernel<<<blocks, 256, 0, st>>>(s, x, w, bias, y, relu ? 1 : 0);

@@ -27,6 +27,9 @@ def _param(t):
     (2, 16, 16, 3, 64, 7, 2, 3, False, False),
     (3, 8, 8, 16, 32, 1, 2, 0, False, False),
     (5, 1, 1, 40, 70, 1, 1, 0, True, True),  # linear as a 1x1 conv
+    # direct VALU forward (thin layers): the LeNet-5 conv shapes
+    (4, 32, 32, 3, 6, 5, 1, 0, True, True),
+    (4, 14, 14, 6, 16, 5, 1, 0, True, True),
     # LDS-tiled family (conv_tiled.hip): ResNet-18 layer shapes, small batch
     (2, 14, 14, 64, 64, 3, 1, 1, False, False),
     (2, 14, 14, 64, 128, 3, 2, 1, False, False),  # stride-2 dgrad phases
