@@ -577,6 +577,58 @@ __global__ __launch_bounds__(256) void conv_fwd_direct_kernel(ConvShape s,
   }
 }
 
+// Direct VALU backward-data conv for thin layers (LeNet-5 conv2: 6 input,
+// 16 output channels), the transpose of the kernel above: one thread per
+// (input pixel, input channel) sums dY[n, oy, ox, :] W[r][q][ci][:] over the
+// taps that reach it (oy = (iy + pad - r) / stride when divisible).  KT:
+// compile-time output channel count, so the dY row (KT contiguous floats)
+// loads as float4s back to back.
+template <int KT>
+__global__ __launch_bounds__(256) void conv_bwd_data_direct_kernel(ConvShape s,
+                                                                   const float* __restrict__ dy,
+                                                                   const float* __restrict__ w,
+                                                                   float* __restrict__ dx) {
+  __shared__ float wl[DIRECT_W_MAX];
+  const int nw = s.R * s.S * s.C * KT;
+  for (int i = threadIdx.x; i < nw; i += blockDim.x) wl[i] = w[i];
+  __syncthreads();
+  const long long total = (long long)s.N * s.H * s.W * s.C;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const int ci = (int)(i % s.C);
+    const long long m = i / s.C;
+    const int ix = (int)(m % s.W);
+    const long long t = m / s.W;
+    const int iy = (int)(t % s.H), n = (int)(t / s.H);
+    float acc = 0.f;
+    for (int r = 0; r < s.R; ++r) {
+      const int ty = iy + s.pad - r;
+      if (ty < 0 || ty % s.stride != 0) continue;
+      const int oy = ty / s.stride;
+      if (oy >= s.OH) continue;
+#pragma unroll 5
+      for (int q = 0; q < s.S; ++q) {
+        const int tx = ix + s.pad - q;
+        if (tx < 0 || tx % s.stride != 0) continue;
+        const int ox = tx / s.stride;
+        if (ox >= s.OW) continue;
+        const float4* dp =
+            reinterpret_cast<const float4*>(dy + (((long long)n * s.OH + oy) * s.OW + ox) * KT);
+        const float* wp = wl + ((r * s.S + q) * s.C + ci) * KT;
+#pragma unroll
+        for (int k = 0; k < KT / 4; ++k) {
+          const float4 d = dp[k];
+          acc = fmaf(d.x, wp[4 * k], acc);
+          acc = fmaf(d.y, wp[4 * k + 1], acc);
+          acc = fmaf(d.z, wp[4 * k + 2], acc);
+          acc = fmaf(d.w, wp[4 * k + 3], acc);
+        }
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
 static inline bool conv_fwd_direct_ok(const ConvShape& s) {
   return s.C < 32 && s.K <= 64 && s.R * s.S * s.C <= 512 &&
          (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX;
@@ -626,6 +678,14 @@ void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* d
                    hipStream_t st, bool bf16, const void* dyb) {
   if (bf16 && conv_bwd_data_bf16_ok(s)) return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb);
   if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16);
+  if (s.C < 32 && (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX && (s.K == 8 || s.K == 16)) {
+    const int b = grid1d((long long)s.N * s.H * s.W * s.C);
+    if (s.K == 8)
+      conv_bwd_data_direct_kernel<8><<<b, 256, 0, st>>>(s, dy, w, dx);
+    else
+      conv_bwd_data_direct_kernel<16><<<b, 256, 0, st>>>(s, dy, w, dx);
+    return;
+  }
   const int M = s.N * s.H * s.W;
   const int blocks = ((M + CFG_D::BM - 1) / CFG_D::BM) * ((s.C + CFG_D::BN - 1) / CFG_D::BN);
   int z, kchunk;

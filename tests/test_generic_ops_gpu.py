@@ -30,6 +30,7 @@ def _param(t):
     # direct VALU forward (thin layers): the LeNet-5 conv shapes
     (4, 32, 32, 3, 6, 5, 1, 0, True, True),
     (4, 14, 14, 6, 16, 5, 1, 0, True, True),
+    (3, 10, 11, 4, 8, 3, 1, 1, True, False),     # direct dgrad, K = 8
     # LDS-tiled family (conv_tiled.hip): ResNet-18 layer shapes, small batch
     (2, 14, 14, 64, 64, 3, 1, 1, False, False),
     (2, 14, 14, 64, 128, 3, 2, 1, False, False),  # stride-2 dgrad phases
