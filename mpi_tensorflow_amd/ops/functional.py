@@ -60,6 +60,16 @@ def set_conv_bf16(on: bool) -> None:
 # backward of every op reports each parameter-gradient view it has finished
 # writing, so gradient buckets can be all-reduced while backward continues.
 _GRAD_HOOK = None
+# True while an engine runs backward seeded with an exact 1.0 (its persistent
+# ones scalar): the loss backward then returns dlogits as is, with no seed
+# fill and no dlogits * g launch per step
+_UNIT_SEED = False
+
+
+def set_unit_loss_seed(on: bool) -> None:
+    global _UNIT_SEED
+    _UNIT_SEED = bool(on)
+
 
 
 def set_grad_hook(fn) -> None:
@@ -442,6 +452,8 @@ class _XentFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (dlog,) = ctx.saved_tensors
+        if _UNIT_SEED:
+            return dlog, None
         return dlog * g, None
 
 

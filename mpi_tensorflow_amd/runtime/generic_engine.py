@@ -90,6 +90,7 @@ class GenericEngine:
             self.yb = torch.empty(self.B, dtype=torch.int32, device=device)
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
             self.lr_dev = torch.zeros(1, device=device)
+            self.seed = torch.ones((), device=device)  # backward seed, never written
 
     # ------------------------------------------------------------------ util
     def lr(self, step: Optional[int] = None) -> float:
@@ -121,18 +122,22 @@ class GenericEngine:
         logits = self.model.forward(self.P, self.bn, self.xb, True)
         loss = Fn.cross_entropy(logits, self.yb)
         gscale = 1.0
-        if self.bucketer is not None:
-            # buckets all-reduce on the comm stream as backward completes them
-            self.bucketer.begin()
-            Fn.set_grad_hook(self.bucketer.grad_ready)
-            try:
-                loss.backward()
-            finally:
-                Fn.set_grad_hook(None)
-            self.bucketer.finish()
-            gscale = 1.0 / self.world
-        else:
-            loss.backward()
+        Fn.set_unit_loss_seed(True)
+        try:
+            if self.bucketer is not None:
+                # buckets all-reduce on the comm stream as backward completes them
+                self.bucketer.begin()
+                Fn.set_grad_hook(self.bucketer.grad_ready)
+                try:
+                    loss.backward(self.seed)
+                finally:
+                    Fn.set_grad_hook(None)
+                self.bucketer.finish()
+                gscale = 1.0 / self.world
+            else:
+                loss.backward(self.seed)
+        finally:
+            Fn.set_unit_loss_seed(False)
         self.loss_buf.copy_(loss.detach())
         C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
                             self.cfg.lr_decay, ptr(self.lr_dev), s)
