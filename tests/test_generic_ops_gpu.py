@@ -136,6 +136,16 @@ def test_avgpool_and_xent(cuda_dev):
     loss.backward()
     assert abs(loss.item() - F.cross_entropy(logits, lab).item()) < 1e-5
     assert _rel(lg.grad.cpu(), lr_.grad) < 1e-5
+    for B, K in ((64, 10), (257, 1000)):  # many blocks, K > 64 (lanes loop over classes)
+        logits = torch.randn(B, K, generator=g) * 3
+        lab = torch.randint(0, K, (B,), generator=g)
+        lr_ = logits.clone().requires_grad_(True)
+        F.cross_entropy(lr_, lab).backward()
+        lg = logits.to(cuda_dev).requires_grad_(True)
+        loss = Fn.cross_entropy(lg, lab.to(cuda_dev))
+        loss.backward()
+        assert abs(loss.item() - F.cross_entropy(logits, lab).item()) < 1e-4
+        assert _rel(lg.grad.cpu(), lr_.grad) < 1e-5
 
 
 @pytest.mark.parametrize("model,shape,B", [("lenet5", (32, 32, 3), 8), ("resnet18", (32, 32, 3), 4)])
