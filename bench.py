@@ -10,6 +10,11 @@ over xGMI, overlapped with backward).  Weak scaling: global batch = 64 * N.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
+Without a launcher, `--gpus N` (N > 1) starts the N rank processes itself
+(one per GPU, LOCAL_RANK = GPU index, rendezvous on 127.0.0.1) before this
+process touches the GPU, relays their output and exits non-zero if any rank
+fails; a rank whose world size differs from --gpus exits non-zero too.
+
 Each rank runs W untimed steps, then EXACTLY K timed steps bracketed by a
 barrier + device synchronize on both sides; the slowest rank's time is
 used; rank 0 prints one JSON line.  Every timed step is a full training
@@ -22,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -51,21 +58,75 @@ def parse(argv=None):
     ap.add_argument("--force-sync", action="store_true",
                     help="1 GPU: run the RCCL all-reduce path anyway (world-1 communicator), "
                          "to measure the overhead of the comm stream and buckets")
+    ap.add_argument("--collective-timeout-s", type=float, default=300.0,
+                    help="watchdog deadline per device-waiting region (N > 1): a hung or "
+                         "failed collective aborts the communicators and exits non-zero")
     return ap.parse_args(argv)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Starts n rank processes of this script (no torchrun / mpirun in the
+    environment).  The parent never initialises the GPU (it only counts
+    devices), so the children are fresh processes, not re-execs.  Rank 0's
+    stdout (the JSON line) is inherited; the first failing rank makes the
+    parent stop the others and return its exit code."""
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    if 0 < ndev < n:
+        print(f"error: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    rc = 0
+    live = list(range(n))
+    while live:
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c
+                print(f"error: rank {r} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for o in live:
+                    procs[o].terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc
+
+
 def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
     from mpi_tensorflow_amd import config as C
     from mpi_tensorflow_amd.parallel import dist as D
     from mpi_tensorflow_amd.parallel.comm import make_comm
+    from mpi_tensorflow_amd.parallel.watchdog import make_watchdog
     from mpi_tensorflow_amd.runtime.mnist_engine import make_engine
     from mpi_tensorflow_amd.utils.data import load_mnist_shard
 
+    if a.gpus > 1 and D.discover().launcher == "none":
+        return launch_ranks(a.gpus, argv)
+    if D.discover().world != a.gpus:
+        print(f"error: --gpus {a.gpus} but the launcher started {D.discover().world} rank(s)",
+              file=sys.stderr)
+        return 2
     device = D.resolve_device("auto")
     di = D.init(str(device))
-    if di.world != a.gpus:
-        print(f"warning: --gpus {a.gpus} but world size {di.world}; using world size", file=sys.stderr)
     N = di.world
     if a.batch_size is None:
         a.batch_size = 32 if a.model == "resnet18" else 64
@@ -105,20 +166,23 @@ def main(argv=None) -> int:
         if device.type == "cuda":
             torch.cuda.synchronize()
 
+    wd = make_watchdog([comm, getattr(eng, "comm2", None)], a.collective_timeout_s, di.rank, N)
     # startup autotune of the gradient-sync schedule (N > 1, native MNIST
     # engine): real training steps, before the warm-up, outside the timing
-    tune_steps = eng.tune_schedule() if hasattr(eng, "tune_schedule") else 0
-    if hasattr(eng, "capture"):
-        eng.capture(a.warmup)
-        eng.capture(a.steps)
-    eng.train(a.warmup)
-    sync()
+    with wd.guard("sync-schedule autotune"):
+        tune_steps = eng.tune_schedule() if hasattr(eng, "tune_schedule") else 0
+        if hasattr(eng, "capture"):
+            eng.capture(a.warmup)
+            eng.capture(a.steps)
+        eng.train(a.warmup)
+        sync()
     D.barrier()
     sync()
-    t0 = time.perf_counter()
-    eng.train(a.steps)
-    sync()
-    t1 = time.perf_counter()
+    with wd.guard(f"timed steps ({a.steps})"):  # arming is two attribute writes
+        t0 = time.perf_counter()
+        eng.train(a.steps)
+        sync()
+        t1 = time.perf_counter()
     D.barrier()
     dt = D.allreduce_max_host(t1 - t0)
     err = float("nan")
@@ -135,6 +199,10 @@ def main(argv=None) -> int:
     else:
         model_desc = "resnet18 (BasicBlock [2,2,2,2], BatchNorm, 10 classes)"
         image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, class-conditional; random-init weights)"
+    rccl_nranks = comm.nranks if hasattr(comm, "nranks") else None
+    if rccl_nranks is not None and rccl_nranks != N:
+        print(f"error: RCCL communicator has {rccl_nranks} ranks, expected {N}", file=sys.stderr)
+        return 3
     if di.rank == 0:
         out = {
             "metric": METRIC if a.model == "mnist_cnn" else f"images/sec (whole node), {a.model}",
@@ -160,17 +228,20 @@ def main(argv=None) -> int:
                          else "none (1 rank)"),
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
+                "ranks": N,
+                "rccl_nranks": rccl_nranks,
                 "sync_schedule": getattr(eng, "sync_schedule", "n/a"),
                 "sync_tune_us_per_step": getattr(eng, "tune_log", {}) or None,
                 "sync_tune_steps": tune_steps,
                 "graph_steps": (a.graph_steps if not a.no_graph else 0),
             },
             "final_test_accuracy": None if err != err else round(100.0 - err, 3),
-            "test_eval_after_steps": a.warmup + a.steps,
+            "test_eval_after_steps": int(eng.step),
         }
         print(json.dumps(out))
         sys.stdout.flush()
     D.barrier()
+    wd.stop()
     D.shutdown()
     return 0
 

@@ -350,7 +350,11 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("group_start", &RcclComm::group_start)
       .def("group_end", &RcclComm::group_end)
-      .def("destroy", &RcclComm::destroy);
+      .def("destroy", &RcclComm::destroy)
+      .def("async_error", &RcclComm::async_error, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
+      .def("comm_count", &RcclComm::comm_count)
+      .def_static("error_string", &RcclComm::error_string);
 
   py::class_<MnistExecutor>(m, "MnistExecutor")
       .def(py::init<const MnistPtrs&>())

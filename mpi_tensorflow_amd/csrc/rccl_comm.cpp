@@ -22,6 +22,9 @@ struct RcclApi {
   decltype(&ncclGroupEnd) groupEnd = nullptr;
   decltype(&ncclGetErrorString) getErrorString = nullptr;
   decltype(&ncclGetVersion) getVersion = nullptr;
+  decltype(&ncclCommGetAsyncError) getAsyncError = nullptr;
+  decltype(&ncclCommAbort) commAbort = nullptr;
+  decltype(&ncclCommCount) commCount = nullptr;
 };
 
 RcclApi g_api;
@@ -64,6 +67,9 @@ void RcclComm::load(const std::string& lib_path) {
   sym(g_api.groupEnd, "ncclGroupEnd");
   sym(g_api.getErrorString, "ncclGetErrorString");
   sym(g_api.getVersion, "ncclGetVersion");
+  sym(g_api.getAsyncError, "ncclCommGetAsyncError");
+  sym(g_api.commAbort, "ncclCommAbort");
+  sym(g_api.commCount, "ncclCommCount");
 }
 
 bool RcclComm::loaded() { return g_api.handle != nullptr; }
@@ -90,7 +96,9 @@ RcclComm::RcclComm(const std::vector<char>& uid, int nranks, int rank)
   ncclUniqueId id;
   if (uid.size() != sizeof(id.internal)) throw std::runtime_error("bad RCCL unique id size");
   std::memcpy(id.internal, uid.data(), sizeof(id.internal));
-  check(g_api.commInitRank(&comm_, nranks, id, rank), "CommInitRank");
+  ncclComm_t c = nullptr;
+  check(g_api.commInitRank(&c, nranks, id, rank), "CommInitRank");
+  comm_.store(c);
 }
 
 RcclComm::~RcclComm() {
@@ -101,38 +109,76 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::destroy() {
-  if (comm_) {
-    ncclComm_t c = comm_;
-    comm_ = nullptr;
-    check(g_api.commDestroy(c), "CommDestroy");
+  ncclComm_t c = comm_.exchange(nullptr);
+  if (c) check(g_api.commDestroy(c), "CommDestroy");
+}
+
+// Failure detection (SURVEY §5 failure row).  Both calls are documented as
+// safe from a thread other than the one issuing collectives: the host
+// watchdog (parallel/watchdog.py) polls async_error() while the training
+// thread is blocked on a device synchronize, and abort()s the communicator
+// when a peer died or a collective overran its deadline.  Abort makes the
+// in-flight RCCL kernels exit, so the stuck synchronize returns.
+int RcclComm::async_error() const {
+  ncclComm_t c = comm_.load();
+  if (!c) return aborted_.load() ? (int)ncclRemoteError : (int)ncclSuccess;
+  ncclResult_t e = ncclSuccess;
+  check(g_api.getAsyncError(c, &e), "CommGetAsyncError");
+  return (int)e;
+}
+
+void RcclComm::abort() {
+  ncclComm_t c = comm_.exchange(nullptr);
+  if (c) {
+    aborted_.store(true);
+    (void)g_api.commAbort(c);
   }
+}
+
+int RcclComm::comm_count() const {
+  ncclComm_t c = comm_.load();
+  if (!c) throw std::runtime_error("RCCL communicator was destroyed or aborted");
+  int n = 0;
+  check(g_api.commCount(c, &n), "CommCount");
+  return n;
+}
+
+std::string RcclComm::error_string(int code) {
+  require_loaded();
+  return g_api.getErrorString((ncclResult_t)code);
+}
+
+ncclComm_t RcclComm::live() const {
+  ncclComm_t c = comm_.load();
+  if (!c) throw std::runtime_error("RCCL communicator was destroyed or aborted");
+  return c;
 }
 
 void RcclComm::all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
                           hipStream_t s) {
-  check(g_api.allReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, comm_, s),
+  check(g_api.allReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, live(), s),
         "AllReduce");
 }
 
 void RcclComm::broadcast(const void* send, void* recv, size_t count, int dtype, int root,
                          hipStream_t s) {
-  check(g_api.broadcast(send, recv, count, (ncclDataType_t)dtype, root, comm_, s), "Broadcast");
+  check(g_api.broadcast(send, recv, count, (ncclDataType_t)dtype, root, live(), s), "Broadcast");
 }
 
 void RcclComm::reduce(const void* send, void* recv, size_t count, int dtype, int op, int root,
                       hipStream_t s) {
-  check(g_api.reduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, root, comm_, s),
+  check(g_api.reduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, root, live(), s),
         "Reduce");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t send_count, int dtype,
                           hipStream_t s) {
-  check(g_api.allGather(send, recv, send_count, (ncclDataType_t)dtype, comm_, s), "AllGather");
+  check(g_api.allGather(send, recv, send_count, (ncclDataType_t)dtype, live(), s), "AllGather");
 }
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                               hipStream_t s) {
-  check(g_api.reduceScatter(send, recv, recv_count, (ncclDataType_t)dtype, (ncclRedOp_t)op, comm_,
+  check(g_api.reduceScatter(send, recv, recv_count, (ncclDataType_t)dtype, (ncclRedOp_t)op, live(),
                             s),
         "ReduceScatter");
 }

@@ -9,6 +9,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -45,8 +46,17 @@ class RcclComm : public Collective {
   void group_start();
   void group_end();
   void destroy();
+  // failure detection: ncclResult_t of the communicator's asynchronous state
+  // (0 = ok, 7 = in progress), abort (idempotent, thread safe), rank count as
+  // seen by RCCL itself
+  int async_error() const;
+  void abort();
+  int comm_count() const;
+  static std::string error_string(int code);
 
  private:
-  ncclComm_t comm_ = nullptr;
+  ncclComm_t live() const;
+  std::atomic<ncclComm_t> comm_{nullptr};
+  std::atomic<bool> aborted_{false};
   int nranks_ = 0, rank_ = 0;
 };

@@ -15,7 +15,7 @@ Reference (`/root/reference/mpipy.py`):
 Activations are NHWC throughout, like the reference; the oracle permutes
 to NCHW only to call `F.conv2d`.  The MI355X training step does NOT use
 this module: it runs the fused HIP kernels of `ops/` through the executor
-in `runtime/mnist_native.py`; this file is the numerics oracle and the
+in `runtime/mnist_engine.py` (NativeMnistEngine, kernels in `csrc/kernels/mnist.hip`); this file is the numerics oracle and the
 CPU/gloo (BASELINE config 1) path.
 """
 

@@ -69,13 +69,31 @@ class RcclDeviceComm(DeviceComm):
 
     def __init__(self, di: DistInfo):
         C = native()
-        C.RcclComm.load(os.path.join(torch_lib_dir(), "librccl.so"))
-        objs = [C.RcclComm.unique_id() if di.rank == 0 else None]
+        # every rank must agree that RCCL is usable BEFORE anyone enters the
+        # collective ncclCommInitRank: a rank that failed to load RCCL (or a
+        # root that failed to make the unique id) would otherwise leave the
+        # others blocked in the id broadcast / init until the gloo timeout
+        err = None
+        uid = None
+        try:
+            C.RcclComm.load(os.path.join(torch_lib_dir(), "librccl.so"))
+            if di.rank == 0:
+                uid = C.RcclComm.unique_id()
+        except Exception as e:  # noqa: BLE001 - reported after the vote
+            err = e
+        if not _all_ranks_ok(err is None, di.world):
+            raise RuntimeError(f"native RCCL unavailable on at least one rank (here: {err!r})")
+        objs = [uid]
         if di.world > 1:
             dist.broadcast_object_list(objs, src=0)
         self._c = C.RcclComm(objs[0], di.world, di.rank)
         self.rank, self.size = di.rank, di.world
         self._di = di
+
+    @property
+    def nranks(self) -> int:
+        """Rank count as RCCL itself reports it (ncclCommCount)."""
+        return int(self._c.comm_count())
 
     def duplicate(self):
         return RcclDeviceComm(self._di)
@@ -238,16 +256,24 @@ class TorchDeviceComm(DeviceComm):
         return out
 
 
+def _all_ranks_ok(ok: bool, world: int) -> bool:
+    """Gloo vote: True iff `ok` holds on every rank."""
+    if world <= 1 or not dist.is_initialized():
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(t.item())
+
+
 def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto") -> Optional[DeviceComm]:
     """Communicator for `device`, or None at world size 1."""
     if di.world <= 1:
         return None
     if device.type == "cuda" and prefer in ("auto", "native"):
-        try:
+        try:  # every rank takes the same branch: RcclDeviceComm votes first
             return RcclDeviceComm(di)
-        except Exception as e:
-            if prefer == "native":
+        except RuntimeError as e:
+            if prefer == "native" or "unavailable on at least one rank" not in str(e):
                 raise
-            print(f"[rank {di.rank}] native RCCL unavailable ({e}); using torch.distributed nccl",
-                  flush=True)
+            print(f"[rank {di.rank}] {e}; using torch.distributed nccl", flush=True)
     return TorchDeviceComm(di, device)

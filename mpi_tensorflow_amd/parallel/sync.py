@@ -30,14 +30,18 @@ from .flat import FlatLayout
 REFERENCE_AVERAGED = ("conv1_weight", "conv2_weight", "fc1_weight", "fc2_weight")  # mpipy.py:121-127
 
 
+@torch.no_grad()
 def average_params(comm: DeviceComm, params: torch.Tensor) -> None:
-    comm.all_reduce_(params)
-    params.mul_(1.0 / comm.size)
+    # `params` may be an autograd leaf (generic engine): work on its storage
+    p = params.detach()
+    comm.all_reduce_(p)
+    p.mul_(1.0 / comm.size)
 
 
+@torch.no_grad()
 def average_params_root_only(comm: DeviceComm, layout: FlatLayout, params: torch.Tensor,
                              names: Iterable[str] = REFERENCE_AVERAGED) -> None:
-    views = layout.views(params)
+    views = layout.views(params.detach())
     for n in names:
         v = views[n]
         buf = v.detach().clone().contiguous().view(-1)  # reduce may scratch non-root buffers

@@ -37,13 +37,14 @@ from ..utils import rng
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
-# sync_schedule="auto": the gradient-sync schedules (buckets / sharded /
-# split, csrc/mnist_executor.h) are timed on the first train() call of at
-# least tune_steps() steps (real training steps, bit-identical under every
-# schedule) and the fastest is kept; all ranks take the decision from the same
-# (max-over-ranks) timings.  With a comm-emulated 8-rank ring (bench.py
-# --comm-emulate, docs/PERF_NOTES.md) split won at every bus bandwidth tried
-# (100-800 GB/s); sharded beat buckets below ~250 GB/s.
+# sync_schedule="auto": the single-communicator gradient-sync schedules
+# (buckets / sharded, csrc/mnist_executor.h) are timed on real training steps
+# (bit-identical under every schedule) and the fastest is kept; all ranks take
+# the decision from the same (max-over-ranks) timings.  The two-communicator
+# "split" schedule (fastest against the comm-emulated 8-rank ring,
+# docs/PERF_NOTES.md) issues collectives on two RCCL communicators from two
+# streams at once; it is opt-in (--sync-schedule split) and never picked by
+# auto until it has run on a real multi-GPU node.
 TUNE_REPLAYS = 2
 
 
@@ -89,6 +90,10 @@ class MnistEngineBase:
     def sync_optimizer_state(self) -> None:
         """Makes `mom` whole on every rank (a sharded optimizer keeps only
         its own shard current); no-op for replicated optimizers."""
+
+    def extra_state(self):
+        """Non-trained state saved with checkpoints (none for this model)."""
+        return {}
 
     def set_step(self, step: int) -> None:
         self.step = int(step)
@@ -245,7 +250,7 @@ class NativeMnistEngine(MnistEngineBase):
         if self.grad_sync and self._native_comm is None:
             raise RuntimeError("grad sync on the native engine needs the native RCCL communicator")
         self.comm2 = None  # second communicator (split schedule: conv bucket on the compute stream)
-        if self.grad_sync and cfg.sync_schedule in ("auto", "split"):
+        if self.grad_sync and cfg.sync_schedule == "split":
             self.comm2 = self.comm.duplicate()
         self._native_comm2 = self.comm2.native_handle if self.comm2 is not None else None
         if self.grad_sync:
@@ -280,9 +285,19 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_BUCKETS
         if name == "sharded" and self.exe.sharded_ok(nranks):
             return E.SCHED_SHARDED_FC
-        if name == "split" or (name == "auto" and self._native_comm2 is not None):
-            return E.SCHED_SPLIT  # "auto": the best in every emulated-ring point, until tuned
-        return E.SCHED_BUCKETS
+        if name == "split" and self._native_comm2 is not None:
+            return E.SCHED_SPLIT
+        return E.SCHED_BUCKETS  # "auto" until tuned
+
+    def _set_schedule(self, sched: int) -> None:
+        """Switches the executor's sync schedule.  Leaving the sharded FC
+        schedule first all-gathers the FC momentum (each rank only kept its own
+        1/N shard current), otherwise the replicas would continue with
+        different momenta on the shards they do not own and diverge."""
+        if sched == self.exe.schedule:
+            return
+        self.sync_optimizer_state()
+        self.exe.set_schedule(sched)
 
     @property
     def sync_schedule(self) -> str:
@@ -326,8 +341,7 @@ class NativeMnistEngine(MnistEngineBase):
         return g
 
     def tune_steps(self) -> int:
-        return 0 if self._tuned else \
-            (3 if self._native_comm2 is not None else 2) * (1 + TUNE_REPLAYS) * self.graph_steps
+        return 0 if self._tuned else 2 * (1 + TUNE_REPLAYS) * self.graph_steps
 
     def tune_schedule(self) -> int:
         """Times TUNE_REPLAYS graph replays of each sync schedule (after one
@@ -341,13 +355,11 @@ class NativeMnistEngine(MnistEngineBase):
         steps = 0
         best = None
         cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SHARDED_FC, "sharded")]
-        if self._native_comm2 is not None:
-            cands.append((E.SCHED_SPLIT, "split"))
         for sched, name in cands:
-            self.exe.set_schedule(sched)
+            self._set_schedule(sched)
             g = self._graph(G)
             if g is None:  # capture unavailable: keep the default schedule
-                self.exe.set_schedule(E.SCHED_BUCKETS)
+                self._set_schedule(E.SCHED_BUCKETS)
                 break
             g.replay()
             torch.cuda.synchronize(self.device)
@@ -364,7 +376,7 @@ class NativeMnistEngine(MnistEngineBase):
             if best is None or us < best[0]:
                 best = (us, sched)
         if best is not None:
-            self.exe.set_schedule(best[1])
+            self._set_schedule(best[1])
         self._tuned = True
         self.step += steps
         return steps

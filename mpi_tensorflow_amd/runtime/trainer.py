@@ -28,6 +28,7 @@ import torch
 from .. import config as C
 from ..parallel import dist as D
 from ..parallel.comm import make_comm
+from ..parallel.watchdog import make_watchdog
 from ..parallel.sync import average_params, average_params_root_only, replica_checksum
 from ..utils import checkpoint as ckpt_mod
 from ..utils.data import (data_exist_here, load_mnist_shard, local_train_rows, mnist_files_present,
@@ -71,9 +72,12 @@ class Trainer:
         self.engine = self._make_engine()
         if cfg.resume:
             step, _ = ckpt_mod.load(cfg.resume, self.engine.layout, self.engine.params,
-                                    self.engine.mom)
+                                    self.engine.mom, extra=self.engine.extra_state(),
+                                    expect={"model": cfg.model, "world": self.world})
             self.engine.set_step(step)
         self.metrics = MetricsWriter(cfg.metrics_jsonl, self.rank)
+        self.watchdog = make_watchdog([self.comm, getattr(self.engine, "comm2", None)],
+                                      cfg.collective_timeout_s, self.rank, self.world)
 
     # ------------------------------------------------------------------ data
     def _prepare_data(self):
@@ -172,10 +176,11 @@ class Trainer:
             k = nxt - s + 1
             self._sync()
             t0 = time.perf_counter()
-            timer.start()
-            eng.train(k)
-            timer.stop(k)
-            self._sync()
+            with self.watchdog.guard(f"train steps {s}..{s + k - 1}"):
+                timer.start()
+                eng.train(k)
+                timer.stop(k)
+                self._sync()
             timer.collect()
             train_t += time.perf_counter() - t0
             trained += k
@@ -198,11 +203,12 @@ class Trainer:
                     self.check_replicas(last)
             if cfg.sync == "param_avg" and self.world > 1 and last % cfg.sync_every == 0:
                 t2 = time.perf_counter()
-                if cfg.root_only_average:
-                    average_params_root_only(self.comm, eng.layout, eng.params)
-                else:
-                    average_params(self.comm, eng.params)
-                self._sync()
+                with self.watchdog.guard(f"parameter averaging at step {last}"):
+                    if cfg.root_only_average:
+                        average_params_root_only(self.comm, eng.layout, eng.params)
+                    else:
+                        average_params(self.comm, eng.params)
+                    self._sync()
                 train_t += time.perf_counter() - t2
             if cfg.ckpt and cfg.ckpt_every and last % cfg.ckpt_every == 0:
                 self.save_checkpoint(cfg.ckpt)
@@ -229,11 +235,13 @@ class Trainer:
         if cfg.ckpt:
             self.save_checkpoint(cfg.ckpt)
         self.metrics.close()
+        self.watchdog.stop()
         return summary
 
     def save_checkpoint(self, path: str) -> None:
         self.engine.sync_optimizer_state()  # sharded FC momentum -> whole buffer
         if self.rank == 0:
             ckpt_mod.save(path, self.engine.layout, self.engine.params, self.engine.mom,
-                          self.engine.step, meta={"model": self.cfg.model, "world": self.world})
+                          self.engine.step, meta={"model": self.cfg.model, "world": self.world},
+                          extra=self.engine.extra_state())
         D.barrier()

@@ -1,8 +1,14 @@
 """Worker for tests/test_native_sync_gpu.py: N ranks share ONE GPU, each runs
-the native MNIST executor with a host-staged gloo communicator, once with the
-bucketed all-reduce schedule and once with the sharded FC update, and checks
-  * both schedules give bit-identical params (same sums, same elementwise SGD),
-  * the gathered momentum is identical too,
+the native MNIST executor with a host-staged gloo communicator (real
+cross-rank data), and checks
+  * buckets == a SERIAL emulation of data parallelism on rank 0 (both ranks'
+    gradients computed by the same kernels, summed, one SGD with gscale 1/N):
+    bit-identical params and momentum;
+  * the sharded FC update and the split schedule give bit-identical params
+    and (gathered) momentum to buckets;
+  * switching schedules mid-run (buckets -> sharded -> buckets, what the
+    startup autotune does) keeps the replicas identical to a buckets-only run
+    (the FC momentum shards are gathered before leaving the sharded schedule);
   * every rank holds the same params (replica consistency).
 Launch: torchrun --nproc-per-node 2 --master-addr 127.0.0.1 tests/helpers/native_sync_ranks.py"""
 import sys
@@ -11,23 +17,83 @@ import torch
 import torch.distributed as dist
 
 from mpi_tensorflow_amd import config as C
+from mpi_tensorflow_amd.ops import native, ptr, stream_handle
 from mpi_tensorflow_amd.parallel import dist as D
 from mpi_tensorflow_amd.parallel.comm import HostStagedComm
 from mpi_tensorflow_amd.runtime.mnist_engine import NativeMnistEngine
 from mpi_tensorflow_amd.utils.data import load_mnist_shard
 
+ROWS = 4096
 
-def run(schedule: str, dtype: str, steps: int, di):
+
+def _shard(rank, world, seed):
+    sh = load_mnist_shard(rank, world, synthetic=True, seed=seed)
+    return sh.train_x[:ROWS], sh.train_y[:ROWS]
+
+
+def make(schedule, dtype, di):
     cfg = C.TrainConfig(sync_schedule=schedule, dtype=dtype, graph=False).validate()
-    shard = load_mnist_shard(di.rank, di.world, synthetic=True, seed=cfg.seed)
+    x, y = _shard(di.rank, di.world, cfg.seed)
     comm = HostStagedComm(di)
-    eng = NativeMnistEngine(cfg, shard.train_x[:4096], shard.train_y[:4096],
-                            torch.device("cuda"), di.rank, di.world, comm)
-    assert eng.grad_sync and eng.sync_schedule == schedule, eng.sync_schedule
-    eng.train(steps)
+    eng = NativeMnistEngine(cfg, x, y, torch.device("cuda"), di.rank, di.world, comm)
+    want = "buckets" if schedule == "auto" else schedule
+    assert eng.grad_sync and eng.sync_schedule == want, eng.sync_schedule
+    return eng
+
+
+def finish(eng):
     eng.sync_optimizer_state()
     torch.cuda.synchronize()
     return eng.params.cpu(), eng.mom.cpu()
+
+
+def run(schedule, dtype, steps, di):
+    eng = make(schedule, dtype, di)
+    eng.train(steps)
+    return finish(eng)
+
+
+def run_switching(dtype, steps, di):
+    eng = make("auto", dtype, di)
+    E = native().MnistExecutor
+    k = steps // 3
+    eng.train(k)
+    eng._set_schedule(E.SCHED_SHARDED_FC)
+    assert eng.sync_schedule == "sharded"
+    eng.train(k)
+    eng._set_schedule(E.SCHED_BUCKETS)
+    eng.train(steps - 2 * k)
+    return finish(eng)
+
+
+def serial(dtype, steps, world):
+    """One process plays every rank: same kernels, summed grads, one SGD."""
+    C_ = native()
+    cfg = C.TrainConfig(dtype=dtype, graph=False).validate()
+    engs = []
+    for r in range(world):
+        x, y = _shard(r, world, cfg.seed)
+        engs.append(NativeMnistEngine(cfg, x, y, torch.device("cuda"), r, world, None))
+    lead = engs[0]
+    gsum = torch.empty_like(lead.grads)
+    lo, hi = lead.layout.l2_range()
+    assert lo == 0
+    s = stream_handle()
+    for _ in range(steps):
+        for e in engs:
+            if e is not lead:
+                e.params.copy_(lead.params)
+                e.step_dev.copy_(lead.step_dev)
+            e.forward_backward_only()
+        gsum.copy_(engs[0].grads)
+        for e in engs[1:]:
+            gsum.add_(e.grads)
+        # lead.lr_dev was written by its head kernel from the device step
+        C_.optim.sgd_momentum(ptr(lead.params), ptr(gsum), ptr(lead.mom), lead.layout.total, hi,
+                              cfg.l2, cfg.momentum, 1.0 / world, ptr(lead.lr_dev), 0.0,
+                              ptr(lead.step_dev), s)
+    torch.cuda.synchronize()
+    return lead.params.cpu(), lead.mom.cpu()
 
 
 def main():
@@ -39,11 +105,17 @@ def main():
         ps, ms = run(sched, dtype, steps, di)
         assert torch.equal(pb, ps), f"{sched}: params differ: {(pb - ps).abs().max().item()}"
         assert torch.equal(mb, ms), f"{sched}: momentum differs: {(mb - ms).abs().max().item()}"
+    pw, mw = run_switching(dtype, steps, di)
+    assert torch.equal(pb, pw), f"switching: params differ: {(pb - pw).abs().max().item()}"
+    assert torch.equal(mb, mw), f"switching: momentum differs: {(mb - mw).abs().max().item()}"
     ref = pb.clone()
     dist.broadcast(ref, 0)
     assert torch.equal(ref, pb), "replicas diverged"
     assert float(pb.abs().sum()) > 0 and float(mb.abs().sum()) > 0
     if di.rank == 0:
+        p1, m1 = serial(dtype, steps, di.world)
+        assert torch.equal(pb, p1), f"serial emulation: params differ: {(pb - p1).abs().max().item()}"
+        assert torch.equal(mb, m1), f"serial emulation: momentum differs: {(mb - m1).abs().max().item()}"
         print(f"NATIVE_SYNC_OK world={di.world} steps={steps} dtype={dtype}", flush=True)
     D.barrier()
     D.shutdown()

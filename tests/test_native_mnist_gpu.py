@@ -215,12 +215,13 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     comm = EmulatedDeviceComm(8, lat_us=10.0, busbw_gbps=150.0, blocks=32)
     cfg = C.TrainConfig(graph=True, graph_steps=5).validate()
     eng = NativeMnistEngine(cfg, x, y, cuda_dev, comm=comm, force_sync=True)
-    assert eng.sync_schedule == "split"  # default until tuned
+    assert eng.sync_schedule == "buckets"  # default until tuned
+    assert eng.comm2 is None  # auto never builds the two-communicator schedule
     n = eng.tune_schedule()
-    assert n == 3 * 3 * 5 and eng.step == n
+    assert n == 2 * 3 * 5 and eng.step == n
     assert int(eng.step_dev.item()) == n
     log = eng.tune_log
-    assert set(log) == {"buckets", "sharded", "split"}
+    assert set(log) == {"buckets", "sharded"}
     assert eng.sync_schedule == min(log, key=log.get)
     eng.train(7)
     torch.cuda.synchronize()
