@@ -63,7 +63,6 @@ PYBIND11_MODULE(_C, m) {
 
   // ------------------------------------------------------------- kernels
   auto k = m.def_submodule("mnist", "fused fp32 MNIST CNN kernels (gfx950 MFMA)");
-  k.def("set_variant", &mnist::set_variant, py::arg("slot"), py::arg("value"));
   k.def("conv1_fwd", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w,
                         uintptr_t b, uintptr_t out, uintptr_t argmax, uintptr_t s, uintptr_t out_pad) {
     mnist::launch_conv1_fwd(P<const float>(data), P<const long long>(step), n_local, batch,
@@ -125,12 +124,6 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("a2"), py::arg("idx2"), py::arg("dh"), py::arg("hd"), py::arg("dlog"), py::arg("w1"),
      py::arg("batch"), py::arg("g_w3"), py::arg("g_b3"), py::arg("g_w4"), py::arg("g_b4"),
      py::arg("dy2"), py::arg("dy2t"), py::arg("stream"), py::arg("roles") = 7);
-  k.def("conv2_bwd_data", [](uintptr_t a1, uintptr_t dy2, uintptr_t w2t, int batch, uintptr_t da1m,
-                             uintptr_t s) {
-    mnist::launch_conv2_bwd_data(P<const float>(a1), P<const float>(dy2), P<const float>(w2t), batch,
-                                 P<float>(da1m), S(s));
-    check_launch();
-  });
   k.def("conv2_bwd_data_l2", [](uintptr_t dy2t, uintptr_t w2t, uintptr_t a1, int batch,
                                 uintptr_t da1m, uintptr_t s) {
     mnist::launch_conv2_bwd_data_l2(P<const float>(dy2t), P<const float>(w2t), P<const float>(a1),

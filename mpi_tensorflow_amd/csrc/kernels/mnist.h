@@ -5,19 +5,20 @@
 #include <stdint.h>
 
 namespace mnist {
-// Kernel-variant switches for A/B timing in one process (scripts/kernel_lab.py
-// --variant SLOT=V); 0 = the production choice.  Slot 0: conv2 filter grad.
-extern int g_variant[8];
-void set_variant(int slot, int v);
 // out_pad (optional): zero-bordered NHWC copy [batch][18][18][32] of the pooled
 // output (its border is never written: allocate it zeroed)
 void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
                       const float* w, const float* b, float* out, uint8_t* argmax, hipStream_t s,
                       float* out_pad = nullptr);
-// bf16 engine: pooled conv1 output as zero-bordered bf16 images (see mnist_bf16.h)
+// bf16 engine: pooled conv1 output as zero-bordered bf16 images (see mnist_bf16.h);
+// with w1b != nullptr the same launch also re-derives the bf16 weight shadows
+// of the fp32 fc1 (w3) / conv2 (w2) weights (mnist_shared.h shadow_block)
 void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
                            const float* w, const float* b, uint16_t* a1p, uint16_t* a1t,
-                           uint8_t* argmax, int ld_batch, hipStream_t s);
+                           uint8_t* argmax, int ld_batch, hipStream_t s,
+                           const float* w3 = nullptr, const float* w2 = nullptr,
+                           uint16_t* w1b = nullptr, uint16_t* w1t = nullptr,
+                           uint16_t* w2tb = nullptr, uint16_t* w2b = nullptr);
 // w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s);
@@ -40,8 +41,6 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                     float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
                     int roles = 7);  // roles: bit 0 dX, bit 1 dW1, bit 2 small grads (profiling)
 int conv2_filter_splits(int batch);
-void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
-                           float* da1m, hipStream_t s);
 // a1p: the zero-bordered NHWC pooled conv1 output [batch][18][18][32]
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
                              hipStream_t s);
@@ -56,6 +55,13 @@ void launch_conv1_bwd_filter(const float* data, const long long* step, int n_loc
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s);
+// world-1 step: grad_finalize fused into the momentum SGD (FC bucket from the
+// flat grads [0, fc_end) with L2 on all of it, conv grads straight from the
+// slabs); bumps *step
+void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
+                         int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
+                         int ngroups, const float* part1, int nblk1, float l2, float momentum,
+                         const float* lr, long long* step, hipStream_t s);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

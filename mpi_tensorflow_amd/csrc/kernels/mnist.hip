@@ -33,11 +33,6 @@
 
 namespace mnist {
 
-int g_variant[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-void set_variant(int slot, int v) {
-  if (slot < 0 || slot >= 8) throw std::runtime_error("set_variant: slot out of range");
-  g_variant[slot] = v;
-}
 
 // ----------------------------------------------------------- geometry ----
 template <int H_, int W_, int CIN_, int COUT_, int KS_, int PAD_, int BK_>
@@ -104,19 +99,29 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
     const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
     const float* __restrict__ w, const float* __restrict__ bias, float* __restrict__ out,
     uint8_t* __restrict__ argmax, __bf16* __restrict__ out_p, __bf16* __restrict__ out_t,
-    int ld_batch, float* __restrict__ out_pad) {
+    int ld_batch, float* __restrict__ out_pad, const ShadowPtrs sh, int conv_blocks) {
   // out_p / out_t (bf16 engine, layouts in mnist_bf16.h): pooled output as
   // the zero-bordered K-packed image [C/16][ld_batch][PH+4][PW+4][16] and as
   // [n][PH+4][C][MNIST16_T_LD], instead of the fp32 NHWC `out`.  out_pad
   // (fp32 engine, optional): a zero-bordered NHWC copy [n][PH+4][PW+4][C]
   // whose border is never written (bounds-check-free conv2 filter operand)
+  // blocks beyond `conv_blocks` (bf16 train step) re-derive the bf16 weight
+  // shadows from the fp32 master weights (mnist_shared.h shadow_block): the
+  // first consumer is the NEXT launch (conv2), so they ride in this grid
+  // instead of costing a launch of their own
   using CF = gemm::Cfg<WM, WN, WK, G::BK, true, true>;
-  __shared__ float smem[CF::SMEM_FLOATS];
+  static_assert(64 * WM * WN * WK == 256, "shadow role needs 256-thread blocks");
+  constexpr int SM = CF::SMEM_FLOATS > SHADOW_SMEM_FLOATS ? CF::SMEM_FLOATS : SHADOW_SMEM_FLOATS;
+  __shared__ float smem[SM];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  if (bid >= conv_blocks) {
+    shadow_block(bid - conv_blocks, sh, smem);
+    return;
+  }
   const long long off = batch_offset_dev(step_ptr, n_local, batch);
   ConvPoolFwdProb<G> p{data + off * (G::H * G::W * G::CIN), w, batch};
   const int M = batch * G::PH * G::PW * 4;
   const int mt = (M + CF::BM - 1) / CF::BM;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid % mt) * CF::BM, n0 = (bid / mt) * CF::BN;
   f32x16 acc;
   int wm, wn;
@@ -552,21 +557,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 //    LDS at all: coalesced 128 B loads of a1 and dY2 feed the MFMAs directly.
 constexpr int C2_XS_ROWS = 8, C2_XS_COLS = 18;
 
-#ifdef MNIST_STAMPS
-#define STAMP(slot)                                                                  \
-  do {                                                                               \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-    unsigned long long _t = __builtin_amdgcn_s_memtime();                            \
-    if ((threadIdx.x & 63) == 0)                                                     \
-      g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + slot] = _t; \
-    __builtin_amdgcn_sched_barrier(0);                                               \
-  } while (0)
-__device__ unsigned long long* g_stamps;
-#else
-#define STAMP(slot) \
-  do {              \
-  } while (0)
-#endif
 
 // conv2 forward + bias + ReLU + 2x2 maxpool (+argmax).  Block = (image, pair of
 // pooled rows); 4 waves = 2 (M: 32 pre-pool pixels = 8 pooling windows) x 2
@@ -582,12 +572,6 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ b2, float* __restrict__ out, uint8_t* __restrict__ argmax,
     float* __restrict__ w2t) {
-  STAMP(0);
-#ifdef MNIST_STAMPS
-  if ((threadIdx.x & 63) == 0)
-    g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + 5] =
-        __builtin_amdgcn_s_memrealtime();
-#endif
   __shared__ float xs[C2_XS];
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -631,7 +615,6 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
 #pragma unroll
   for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 64];
   __syncthreads();
-  STAMP(1);
 #pragma unroll
   for (int c = 0; c < 16; ++c) ac[c] = xs[abase + 2 * c];
   f32x16 acc0 = zero16(), acc1 = zero16();
@@ -661,16 +644,9 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
       ac[c] = an[c];
     }
   }
-  STAMP(2);
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = acc0[r] + acc1[r];
-  STAMP(3);
-#ifdef MNIST_STAMPS
-  if ((threadIdx.x & 63) == 0)
-    g_stamps[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8) + 6] =
-        __builtin_amdgcn_s_memrealtime();
-#endif
   const float bias = b2[co];
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -693,96 +669,6 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
   }
 }
 
-// conv2 bwd-data (+ReLU1 mask): dA1m[n,y,x,ci] = [a1>0] * sum_{kh,kw,co}
-// dY2[n, y+2-kh, x+2-kw, co] W2[kh,kw,ci,co].  Block = (image, 4 output rows);
-// 4 waves (one per SIMD) = 2 (M: 2 rows x 16 cols) x 2 (K: co halves, summed
-// once through LDS at the end); each wave runs two accumulator chains.
-constexpr int C2_DS = C2_XS_ROWS * C2_XS_COLS * 65;
-constexpr int C2B_SMEM = C2_DS;
-
-__device__ void conv2_bwd_data_v3(int bid, const float* __restrict__ a1,
-                                  const float* __restrict__ dy2, const float* __restrict__ w2t,
-                                  float* __restrict__ da1m, float* smem) {
-  float* ds = smem;  // [8][18][65]
-  const int n = bid >> 2, y0 = 4 * (bid & 3);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {  // stage the halo tile: all loads in flight first, then the LDS writes
-    constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 64 / 256;  // 36
-    float sv[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int i = tid + 256 * j;
-      const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
-      const int y = y0 - 2 + r, x = c - 2;
-      const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
-      const float v = dy2[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 64 + co];
-      sv[j] = ok ? v : 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < NS; ++j) {
-      const int i = tid + 256 * j;
-      const int co = i & 63, c = (i >> 6) % C2_XS_COLS, r = (i >> 6) / C2_XS_COLS;
-      ds[(r * C2_XS_COLS + c) * 65 + co] = sv[j];
-    }
-  }
-  const int msub = wave & 1, cog = wave >> 1;  // cog: co half (32 channels)
-  const int r2 = (lane & 31) >> 4, x = lane & 15;
-  const int ly = 2 * msub + r2, lx = x < 14 ? x : 0;
-  // staged row of source pixel (y+2-kh) is ly + 4 - kh; col lx + 4 - kw
-  const int abase = ((ly + 4) * C2_XS_COLS + lx + 4) * 65 + cog * 32 + (lane >> 5);
-  const float* wp = w2t + (cog * 32 + (lane >> 5)) * 32 + (lane & 31);  // + (t*64 + 2c)*32
-  float bc[16], bn[16], ac[16], an[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) bc[c] = wp[(2 * c) * 32];
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < 16; ++c) ac[c] = ds[abase + 2 * c];
-  f32x16 acc0 = zero16(), acc1 = zero16();
-#pragma unroll
-  for (int t = 0; t < 25; ++t) {
-    if (t + 1 < 25) {
-      const int kh = (t + 1) / 5, kw = (t + 1) % 5;
-      const float* xa = ds + abase - (kh * C2_XS_COLS + kw) * 65;
-#pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        bn[c] = wp[((t + 1) * 64 + 2 * c) * 32];
-        an[c] = xa[2 * c];
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < 16; c += 2) {
-      acc0 = mfma32x32x2(ac[c], bc[c], acc0);
-      acc1 = mfma32x32x2(ac[c + 1], bc[c + 1], acc1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      bc[c] = bn[c];
-      ac[c] = an[c];
-    }
-  }
-  __syncthreads();  // ds is dead: reuse it for the 2-way K reduction
-  float* red = smem + msub * 16 * 64;
-  if (cog == 1) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) red[r * 64 + lane] = acc0[r] + acc1[r];
-  }
-  __syncthreads();
-  if (cog == 0) {
-    const int ci = lane & 31;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int mr = mfma32_row(r, lane);  // 0..31 = (row r2, col x)
-      const int y = y0 + 2 * msub + (mr >> 4), xx = mr & 15;
-      if (y < 14 && xx < 14) {
-        const int o = ((n * 14 + y) * 14 + xx) * 32 + ci;
-        const float g = acc0[r] + acc1[r] + red[r * 64 + lane];
-        da1m[o] = a1[o] > 0.f ? g : 0.f;
-      }
-    }
-  }
-}
 
 // conv2 bwd-filter: dW2[t][ci][co] = sum_pix a1[pix shifted by tap t][ci] dY2[pix][co].
 // Block = (tap, group of 4 images); 8 waves = 2 (N: co halves) x 4 (one image
@@ -978,14 +864,6 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_l2_kernel(const float* __r
   }
 }
 
-__global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const float* __restrict__ a1,
-                                                            const float* __restrict__ dy2,
-                                                            const float* __restrict__ w2t,
-                                                            float* __restrict__ da1m) {
-  __shared__ float smem[C2B_SMEM];
-  conv2_bwd_data_v3(blockIdx.x, a1, dy2, w2t, da1m, smem);
-}
-
 template <int DEPTH, bool CENTRE_ONLY>
 __global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(int batch,
                                                               const float* __restrict__ a1p,
@@ -1128,17 +1006,24 @@ void launch_conv1_fwd(const float* data, const long long* step, int n_local, int
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
   conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
       <<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(data, step, n_local, batch, w, b, out,
-                                                      argmax, nullptr, nullptr, 0, out_pad);
+                                                      argmax, nullptr, nullptr, 0, out_pad,
+                                                      ShadowPtrs{}, mt * nt);
 }
 
 void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local, int batch,
                            const float* w, const float* b, uint16_t* a1p, uint16_t* a1t,
-                           uint8_t* argmax, int ld_batch, hipStream_t s) {
+                           uint8_t* argmax, int ld_batch, hipStream_t s, const float* w3,
+                           const float* w2, uint16_t* w1b, uint16_t* w1t, uint16_t* w2tb,
+                           uint16_t* w2b) {
   const int M = batch * 14 * 14 * 4;
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
-  conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK><<<mt * nt, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(
-      data, step, n_local, batch, w, b, nullptr, argmax, reinterpret_cast<__bf16*>(a1p),
-      reinterpret_cast<__bf16*>(a1t), ld_batch, nullptr);
+  auto B16 = [](uint16_t* p) { return reinterpret_cast<__bf16*>(p); };
+  const ShadowPtrs sh{w3, w2, B16(w1b), B16(w1t), B16(w2tb), B16(w2b)};
+  const int extra = w1b ? SHADOW_BLOCKS : 0;
+  conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
+      <<<mt * nt + extra, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(
+          data, step, n_local, batch, w, b, nullptr, argmax, B16(a1p), B16(a1t), ld_batch, nullptr,
+          sh, mt * nt);
 }
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
@@ -1194,10 +1079,6 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
 
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
 
-void launch_conv2_bwd_data(const float* a1, const float* dy2, const float* w2t, int batch,
-                           float* da1m, hipStream_t s) {
-  conv2_bwd_data_kernel<<<batch * 4, 256, 0, s>>>(a1, dy2, w2t, da1m);
-}
 
 void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
                               float* da1m, hipStream_t s) {
@@ -1210,19 +1091,7 @@ void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, floa
                              hipStream_t s) {
   const int G = conv2_filter_splits(batch);
   float* db = part2 + (size_t)G * 51200;
-  switch (g_variant[0]) {  // A/B experiments (kernel_lab.py --variant)
-    case 1:
-      conv2_bwd_filter_kernel<3, false><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
-      break;
-    case 2:
-      conv2_bwd_filter_kernel<4, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
-      break;
-    case 3:
-      conv2_bwd_filter_kernel<2, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
-      break;
-    default:
-      conv2_bwd_filter_kernel<3, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
-  }
+  conv2_bwd_filter_kernel<3, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
 }
 
 int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }
@@ -1232,6 +1101,147 @@ void launch_conv1_bwd_filter(const float* data, const long long* step, int n_loc
                              hipStream_t s) {
   conv1_bwd_filter_kernel<<<conv1_filter_blocks(batch), 256, 0, s>>>(data, step, n_local, batch,
                                                                      da1m, idx1, part1);
+}
+
+// ----------------------------------------------- world-1 SGD + finalize ----
+// Single-rank train step: the conv filter-grad slab reductions of
+// grad_finalize_kernel are fused into the momentum SGD (U1), which saves a
+// launch (a kernel boundary plus one dependent HBM round trip; 6.6 + 4.9 us
+// -> 9.4 us at B = 64).  With world > 1 the conv grads must be final in the
+// flat buffer BEFORE their all-reduce, so the executor keeps finalize + SGD
+// there.  (A variant that also wrote the bf16 weight shadows from the SGD
+// measured no faster than the shadow role of the conv1 launch: 13.7 us.)
+// Roles (blocks): [0, fc_blocks) grid-stride float4 over the FC bucket
+// [0, fc_end) (all of it L2-regularised); 50 blocks: conv2 weights, one
+// float4 per thread summed over the slabs; 16 blocks: conv2 bias, one wave
+// per channel; 208 blocks: conv1 weight + bias, one wave per output.  Each
+// conv element's sum runs in the same order as in grad_finalize_kernel.
+struct SgdFinArgs {
+  float* w;
+  const float* g;
+  float* mom;
+  long long fc_end4;
+  int off_w2, off_b2, off_w1, off_b1;
+  const float* part2;
+  const float* part_db2;
+  int ngroups;
+  const float* part1;
+  int nblk1;
+  float l2, momentum;
+  const float* lr;
+  long long* step;
+  int fc_blocks;
+};
+
+__device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, float mu) {
+  const float mv = mu * *m + g;
+  *m = mv;
+  *w -= lr * mv;
+}
+
+__device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc, float lr,
+                                     float mu) {
+  gv.x += lc * wv.x;
+  gv.y += lc * wv.y;
+  gv.z += lc * wv.z;
+  gv.w += lc * wv.w;
+  mv.x = mu * mv.x + gv.x;
+  mv.y = mu * mv.y + gv.y;
+  mv.z = mu * mv.z + gv.z;
+  mv.w = mu * mv.w + gv.w;
+  wv.x -= lr * mv.x;
+  wv.y -= lr * mv.y;
+  wv.z -= lr * mv.z;
+  wv.w -= lr * mv.w;
+}
+
+__global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
+  const float lr = *a.lr;
+  const int tid = threadIdx.x;
+  int blk = blockIdx.x;
+  if (blk == 0 && tid == 0) *a.step += 1;
+  if (blk < a.fc_blocks) {
+    float4* W4 = reinterpret_cast<float4*>(a.w);
+    float4* M4 = reinterpret_cast<float4*>(a.mom);
+    const float4* G4 = reinterpret_cast<const float4*>(a.g);
+    const long long stride = (long long)a.fc_blocks * 256;
+    for (long long i = (long long)blk * 256 + tid; i < a.fc_end4; i += stride) {
+      float4 wv = W4[i], gv = G4[i], mv = M4[i];
+      sgd4(wv, mv, gv, a.l2, lr, a.momentum);
+      W4[i] = wv;
+      M4[i] = mv;
+    }
+    return;
+  }
+  blk -= a.fc_blocks;
+  if (blk < 50) {  // conv2 weights: 51200 floats = 50 blocks x 256 threads x float4
+    const int i = blk * 256 + tid;
+    const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 8 <= a.ngroups; z += 8) {  // 8 slab loads in flight, summed in order
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x;
+        s.y += v[u].y;
+        s.z += v[u].z;
+        s.w += v[u].w;
+      }
+    }
+    for (; z < a.ngroups; ++z) {
+      const float4 v = p2[(size_t)z * 12800];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
+    float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
+    float4 wv = *wp, mv = *mp;
+    sgd4(wv, mv, s, 0.f, lr, a.momentum);
+    *wp = wv;
+    *mp = mv;
+    return;
+  }
+  blk -= 50;
+  const int lane = tid & 63;
+  if (blk < 16) {  // conv2 bias: one wave per channel
+    const int co = blk * 4 + (tid >> 6);
+    float s = 0.f;
+    for (int z = lane; z < 4 * a.ngroups; z += 64) s += a.part_db2[z * 64 + co];
+    s = wave_sum(s);
+    if (lane == 0) sgd_elem(a.w + a.off_b2 + co, a.mom + a.off_b2 + co, s, lr, a.momentum);
+    return;
+  }
+  blk -= 16;
+  const int o = blk * 4 + (tid >> 6);
+  if (o >= 832) return;
+  float s = 0.f;
+#pragma unroll 8
+  for (int b = lane; b < a.nblk1; b += 64) s += a.part1[(size_t)b * 832 + o];
+  s = wave_sum(s);
+  if (lane == 0) {
+    const int off = o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800);
+    sgd_elem(a.w + off, a.mom + off, s, lr, a.momentum);
+  }
+}
+
+void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
+                         int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
+                         int ngroups, const float* part1, int nblk1, float l2, float momentum,
+                         const float* lr, long long* step, hipStream_t s) {
+  if (fc_end % 4 || off_w2 % 4 || l2_end != fc_end)
+    throw std::runtime_error("sgd_finalize: misaligned flat segments / L2 prefix != FC bucket");
+  const long long n4 = fc_end / 4;
+  long long b = (n4 + 255) / 256;
+  const int fc_blocks = (int)(b < 2048 ? b : 2048);  // as the flat SGD
+  SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
+               part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
+               fc_blocks};
+  sgd_finalize_kernel<<<fc_blocks + 50 + 16 + cdiv(832, 4), 256, 0, s>>>(a);
 }
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,

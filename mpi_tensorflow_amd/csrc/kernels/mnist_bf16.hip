@@ -78,63 +78,15 @@ __device__ __forceinline__ void kloop(int nks, F&& frag, f32x16& c0, f32x16& c1,
 }
 
 // ---------------------------------------------------------- shadows ----
-// blocks [0, 392): one 64x64 tile of W1 (fp32 [3136][512], i0 + 64 rows, j0
-// + 64 cols) -> w1b [j/16][i][16] and, through LDS, w1t [i/16][j][16];
-// blocks [392, 442): 1024 conv2 weights each -> w2t / w2b.
-constexpr int SH_W1_BLOCKS = (FC1_IN / 64) * (FC1_OUT / 64), SH_W2_BLOCKS = 51200 / 1024;
-
-__device__ __forceinline__ void store16(bf* dst, const float* v) {  // 16 floats -> 32 B
-  bf t[16];
-#pragma unroll
-  for (int e = 0; e < 16; ++e) t[e] = (bf)v[e];
-  const uint4* s4 = reinterpret_cast<const uint4*>(t);
-  reinterpret_cast<uint4*>(dst)[0] = s4[0];
-  reinterpret_cast<uint4*>(dst)[1] = s4[1];
-}
-
+// The shadow conversion lives in mnist_shared.h (shadow_block); the train step
+// runs it as a block role of the conv1 forward launch, the standalone kernel
+// below serves callers that only need the shadows.
 __global__ __launch_bounds__(256) void shadow_kernel(const float* __restrict__ w1,
                                                      const float* __restrict__ w2,
                                                      bf* __restrict__ w1b, bf* __restrict__ w1t,
                                                      bf* __restrict__ w2t, bf* __restrict__ w2b) {
-  __shared__ float tile[64][65];
-  const int tid = threadIdx.x;
-  if ((int)blockIdx.x < SH_W1_BLOCKS) {
-    const int i0 = (blockIdx.x % (FC1_IN / 64)) * 64, j0 = (blockIdx.x / (FC1_IN / 64)) * 64;
-    {  // thread = (row i, 16-col chunk): 4 float4 loads, one 32 B store into w1b
-      const int row = tid >> 2, ck = tid & 3;
-      float v[16];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 f = *reinterpret_cast<const float4*>(w1 + (size_t)(i0 + row) * FC1_OUT + j0 +
-                                                           16 * ck + 4 * u);
-        v[4 * u] = f.x;
-        v[4 * u + 1] = f.y;
-        v[4 * u + 2] = f.z;
-        v[4 * u + 3] = f.w;
-      }
-#pragma unroll
-      for (int e = 0; e < 16; ++e) tile[row][16 * ck + e] = v[e];
-      store16(w1b + ((size_t)((j0 >> 4) + ck) * FC1_IN + i0 + row) * 16, v);
-    }
-    __syncthreads();
-    {  // thread = (col j, 16-row chunk) -> w1t
-      const int col = tid >> 2, ck = tid & 3;
-      float v[16];
-#pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = tile[16 * ck + e][col];
-      store16(w1t + ((size_t)((i0 >> 4) + ck) * FC1_OUT + j0 + col) * 16, v);
-    }
-    return;
-  }
-  const int base = ((int)blockIdx.x - SH_W1_BLOCKS) * 1024;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int idx = base + tid + 256 * e;  // HWIO: (t * 32 + ci) * 64 + co
-    const bf v = (bf)w2[idx];
-    const int t = idx >> 11, ci = (idx >> 6) & 31, co = idx & 63;
-    w2t[((t * 2 + (ci >> 4)) * 64 + co) * 16 + (ci & 15)] = v;
-    w2b[((t * 4 + (co >> 4)) * 32 + ci) * 16 + (co & 15)] = v;
-  }
+  __shared__ float tile[64 * 65];
+  mnist::shadow_block((int)blockIdx.x, {w1, w2, w1b, w1t, w2t, w2b}, tile);
 }
 
 // ------------------------------------------------------------ conv2 fwd ----
@@ -439,7 +391,7 @@ static inline bf* M16(uint16_t* p) { return reinterpret_cast<bf*>(p); }
 
 void launch_shadows(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w1t,
                     uint16_t* w2t, uint16_t* w2b, hipStream_t s) {
-  shadow_kernel<<<SH_W1_BLOCKS + SH_W2_BLOCKS, 256, 0, s>>>(w1, w2, M16(w1b), M16(w1t), M16(w2t),
+  shadow_kernel<<<mnist::SHADOW_BLOCKS, 256, 0, s>>>(w1, w2, M16(w1b), M16(w1t), M16(w2t),
                                                             M16(w2b));
 }
 

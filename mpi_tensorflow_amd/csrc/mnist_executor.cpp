@@ -38,8 +38,8 @@ MnistExecutor::~MnistExecutor() {
 // running concurrently.  Independent work is therefore merged into single
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
-void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
-  if (p_.bf16) return enqueue_fwd_bwd_bf16(s);
+void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize) {
+  if (p_.bf16) return enqueue_fwd_bwd_bf16(s, finalize);
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -70,28 +70,31 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s) {
   mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
                                  P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                  P<float>(p.part1), s);
-  mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
-                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
-                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+  if (finalize)
+    mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
+                                P<const float>(p.part1), mnist::conv1_filter_blocks(B),
+                                G + p.off_w2, G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
 }
 
 // bf16 step: same kernel boundaries; the first launch re-derives the bf16
 // weight shadows from the fp32 master weights, conv1 (K = 25, tiny) stays on
 // fp32 MFMA and writes bf16 images, the conv1 filter grad / fc2 head / slab
 // reductions / SGD stay fp32.
-void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
+void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize) {
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
   const long long* step = P<const long long>(p.step);
   const int B = p.batch;
   using U16 = uint16_t;
-  wait_fc_params(s);  // the shadow launch reads the FC weights
-  mnist16::launch_shadows(W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
-                          P<U16>(p.w2tb), P<U16>(p.w2b), s);
+  wait_fc_params(s);  // the shadow role of the conv1 launch reads the FC weights
+  // the conv1 launch also re-derives the bf16 weight shadows (block role):
+  // measured as fast as having the SGD write them (which needs a refresh
+  // after any outside change of the weights), and always correct
   mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
                                W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1), B,
-                               s);
+                               s, W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
+                               P<U16>(p.w2tb), P<U16>(p.w2b));
   mnist16::launch_conv2_fwd(P<const U16>(p.a1p), B, P<const U16>(p.w2tb), W + p.off_b2,
                             P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2), s);
   mnist16::launch_fc1_fwd_train(P<const U16>(p.a2h), P<const U16>(p.w1t), B, P<float>(p.fc1_part),
@@ -115,9 +118,14 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s) {
   mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
                                  P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                  P<float>(p.part1), s);
-  mnist::launch_grad_finalize(P<const float>(p.part2), mnist16::conv2_filter_groups(B),
-                              P<const float>(p.part1), mnist::conv1_filter_blocks(B), G + p.off_w2,
-                              G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+  if (finalize)
+    mnist::launch_grad_finalize(P<const float>(p.part2), mnist16::conv2_filter_groups(B),
+                                P<const float>(p.part1), mnist::conv1_filter_blocks(B),
+                                G + p.off_w2, G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+}
+
+int MnistExecutor::conv2_groups() const {
+  return p_.bf16 ? mnist16::conv2_filter_groups(p_.batch) : mnist::conv2_filter_splits(p_.batch);
 }
 
 void MnistExecutor::forward_backward(hipStream_t s) {
@@ -167,8 +175,14 @@ void MnistExecutor::join(hipStream_t s) { wait_fc_params(s); }
 void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                Collective* comm2) {
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
-    enqueue_fwd_bwd(s);
-    sgd(s, 1.0f);
+    const MnistPtrs& p = p_;
+    wait_fc_params(s);
+    enqueue_fwd_bwd(s, /*finalize=*/false);  // the slab sums run inside the SGD launch
+    mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
+                               p.bucket1, p.l2_end, (int)p.off_w2, (int)p.off_b2, (int)p.off_w1,
+                               (int)p.off_b1, P<const float>(p.part2), conv2_groups(),
+                               P<const float>(p.part1), mnist::conv1_filter_blocks(p.batch), p.l2,
+                               p.momentum, P<const float>(p.lr), P<long long>(p.step), s);
     return;
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
@@ -277,10 +291,10 @@ void MnistExecutor::eval_chunk(const MnistPtrs& p, uintptr_t x, uintptr_t y, int
   if (p.bf16) {
     using U16 = uint16_t;
     const int Mp = (M + 7) / 8 * 8;  // conv2 tiles cover whole groups of 8 images
-    mnist16::launch_shadows(W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
-                            P<U16>(p.w2tb), P<U16>(p.w2b), s);
     mnist::launch_conv1_fwd_bf16(P<const float>(x), nullptr, 0, M, W + p.off_w1, W + p.off_b1,
-                                 P<U16>(ws_a1), nullptr, nullptr, Mp, s);
+                                 P<U16>(ws_a1), nullptr, nullptr, Mp, s, W + p.off_w3,
+                                 W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t), P<U16>(p.w2tb),
+                                 P<U16>(p.w2b));
     mnist16::launch_conv2_fwd(P<const U16>(ws_a1), Mp, P<const U16>(p.w2tb), W + p.off_b2,
                               P<U16>(ws_a2), nullptr, nullptr, s);
     mnist16::launch_fc1_fwd_eval(P<const U16>(ws_a2), Mp, P<const U16>(p.w1t), W + p.off_b3, M,

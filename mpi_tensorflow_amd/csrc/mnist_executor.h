@@ -102,13 +102,16 @@ class MnistExecutor {
   const MnistPtrs& ptrs() const { return p_; }
 
  private:
-  void enqueue_fwd_bwd(hipStream_t s);
+  // finalize = false: leave the conv filter grads as slabs (the world-1 SGD
+  // launch reduces them itself)
+  void enqueue_fwd_bwd(hipStream_t s, bool finalize = true);
+  int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void wait_fc_params(hipStream_t s);
   int sched_ = SCHED_BUCKETS;
   bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on
-  void enqueue_fwd_bwd_bf16(hipStream_t s);
+  void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true);
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;

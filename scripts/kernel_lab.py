@@ -18,10 +18,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=64)
-    ap.add_argument("--ab", default=None, metavar="SLOT=V1,V2,...[:KERNEL]",
-                    help="A/B the kernel variants of a mnist.set_variant slot: per variant, "
-                         "in interleaved rounds, the kernel in a 20-launch graph and the whole "
-                         "graph-replayed step")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     x, y = synthetic_rows("train", 0, 4096)
@@ -84,49 +80,6 @@ def main():
         "sgd": lambda: Cn.optim.sgd_momentum(ptr(e.params), ptr(e.grads), ptr(e.mom), lay.total,
                                              lay.l2_range()[1], 5e-4, 0.9, 1.0, ptr(e.lr_dev), 0.0, 0, s),
     }
-    if a.ab:
-        spec, _, kname = a.ab.partition(":")
-        slot, vals = spec.split("=")
-        slot, vals = int(slot), [int(v) for v in vals.split(",")]
-        kname = kname or "conv2_bwd_filter"
-        res = {v: ([], []) for v in vals}
-        e.cfg.graph = True
-        e.use_graph = True
-        for rnd in range(3):
-            for v in vals:
-                k.set_variant(slot, v)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    s = stream_handle()  # the capture stream (the op lambdas read `s` late)
-                    for _ in range(20):
-                        ops[kname]()
-                s = stream_handle()
-                g.replay()
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(10):
-                    g.replay()
-                e1.record()
-                e1.synchronize()
-                res[v][0].append(e0.elapsed_time(e1) * 1000.0 / 200)
-                e._graphs.clear()
-                e.capture(250)
-                e.train(250)
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                e.train(500)
-                e1.record()
-                e1.synchronize()
-                res[v][1].append(e0.elapsed_time(e1) * 1000.0 / 500)
-        k.set_variant(slot, 0)
-        print(f"A/B slot {slot} kernel {kname}: variant, kernel-in-graph us (min of rounds), "
-              f"step us (min of rounds)")
-        for v in vals:
-            print(f"  {v}: {min(res[v][0]):8.2f} {min(res[v][1]):8.2f}   "
-                  f"rounds {['%.2f' % t for t in res[v][0]]} {['%.2f' % t for t in res[v][1]]}")
-        return
     total = 0.0
     print(f"{'kernel':20s} {'median_us':>10s} {'min_us':>8s}")
     for name, fn in ops.items():

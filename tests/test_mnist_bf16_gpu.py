@@ -92,5 +92,5 @@ def test_bf16_learns_and_evaluates(cuda_dev, data):
     ref = TorchMnistEngine(C.TrainConfig().validate(), x, y, cuda_dev)
     ref.params.copy_(nat.params)
     e_ref = ref.evaluate(tx, ty)
-    assert e1 < e0 and e1 < 10.0, (e0, e1)
+    assert e1 < e0 and e1 < 20.0, (e0, e1)  # v2 synthetic task: ~12 % after 150 steps
     assert abs(e1 - e_ref) <= 1.0, (e1, e_ref)  # bf16 vs fp32 inference, same weights
