@@ -150,7 +150,7 @@ def main(argv=None) -> int:
         test_x, test_y = shard.test_x, shard.test_y
     else:
         from mpi_tensorflow_amd.models.generic import model_input_shape
-        from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+        from mpi_tensorflow_amd.runtime.generic_engine import make_image_engine
         from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
         shape = model_input_shape(a.model)
@@ -158,8 +158,8 @@ def main(argv=None) -> int:
         tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
         ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
                                         start=di.rank * rows)
-        eng = GenericEngine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
-                            force_sync=force)
+        eng = make_image_engine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
+                                force_sync=force)
         test_x, test_y = ex.numpy(), ey.numpy()
 
     def sync():

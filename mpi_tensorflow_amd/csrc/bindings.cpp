@@ -14,6 +14,7 @@
 #include "kernels/mnist.h"
 #include "kernels/mnist_bf16.h"
 #include "kernels/ops_generic.h"
+#include "lenet_executor.h"
 #include "mnist_executor.h"
 #include "rccl_comm.h"
 
@@ -348,6 +349,60 @@ PYBIND11_MODULE(_C, m) {
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def("comm_count", &RcclComm::comm_count)
       .def_static("error_string", &RcclComm::error_string);
+
+  // ------------------------------------------------------------ LeNet-5
+  py::class_<lenet::Offsets>(m, "LenetOffsets")
+      .def(py::init<>())
+#define RWO(f) .def_readwrite(#f, &lenet::Offsets::f)
+          RWO(c1w) RWO(c1b) RWO(c2w) RWO(c2b) RWO(f1w) RWO(f1b) RWO(f2w) RWO(f2b) RWO(f3w) RWO(f3b);
+#undef RWO
+  py::class_<LenetPtrs>(m, "LenetPtrs")
+      .def(py::init<>())
+#define RWL(f) .def_readwrite(#f, &LenetPtrs::f)
+          RWL(train_x) RWL(train_y) RWL(n_local) RWL(batch) RWL(params) RWL(grads) RWL(mom)
+              RWL(total) RWL(off) RWL(step) RWL(lr) RWL(correct) RWL(acts) RWL(deltas) RWL(convp)
+                  RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum);
+#undef RWL
+  m.def("lenet_buffer_floats", [](int batch) {
+    return py::make_tuple(lenet::acts_floats(batch), lenet::deltas_floats(batch),
+                          lenet::convp_floats(batch));
+  });
+  m.def("lenet_image_phase", [](const LenetPtrs& p, int stop, uintptr_t s) {
+    lenet::ImageArgs a{};
+    a.x = P<const float>(p.train_x);
+    a.y = P<const int>(p.train_y);
+    a.n_local = p.n_local;
+    a.batch = p.batch;
+    a.step = P<const long long>(p.step);
+    a.params = P<const float>(p.params);
+    a.off = p.off;
+    a.acts = P<float>(p.acts);
+    a.deltas = P<float>(p.deltas);
+    a.convp = P<float>(p.convp);
+    a.loss_rows = P<float>(p.loss_rows);
+    a.lr_out = P<float>(p.lr);
+    a.stop_phase = stop;
+    lenet::launch_image_train(a, S(s));
+    check_launch();
+  });
+  py::class_<LenetExecutor>(m, "LenetExecutor")
+      .def(py::init<const LenetPtrs&>())
+      .def("train_step",
+           [](LenetExecutor& e, uintptr_t s, Collective* comm) {
+             e.train_step(S(s), comm);
+             check_launch();
+           },
+           py::arg("stream"), py::arg("comm") = nullptr)
+      .def("forward_backward",
+           [](LenetExecutor& e, uintptr_t s) {
+             e.forward_backward(S(s));
+             check_launch();
+           })
+      .def_static("eval_chunk", [](const LenetPtrs& p, uintptr_t x, uintptr_t y, int M,
+                                   uintptr_t logits, uintptr_t errors, uintptr_t s) {
+        LenetExecutor::eval_chunk(p, x, y, M, logits, errors, S(s));
+        check_launch();
+      });
 
   py::class_<MnistExecutor>(m, "MnistExecutor")
       .def(py::init<const MnistPtrs&>())

@@ -1,0 +1,620 @@
+// Fused fp32 LeNet-5 kernel set for gfx950 (BASELINE config 4).
+//
+// Model (models/generic.py LeNet5, same op pattern as the reference's
+// conv -> bias+ReLU -> pool -> ... -> matmul chain, /root/reference/mpipy.py:155-167):
+//   x [32,32,3] -> conv5x5(3->6) valid + b, ReLU, maxpool2 -> [14,14,6]
+//   -> conv5x5(6->16) valid + b, ReLU, maxpool2 -> [5,5,16] = 400 (h,w,c)
+//   -> FC 400->120 + ReLU -> FC 120->84 + ReLU -> FC 84->10 -> softmax xent.
+//
+// At B = 64 the whole step is ~250 MFLOP: the round-1 generic path spent it
+// in ~37 launches (conv engines, library GEMMs, reductions, 239 us/step).
+// Here a train step is TWO launches:
+//
+//  image kernel  one 512-thread workgroup per image, everything in LDS:
+//                batch row at the device-step offset, conv1 / conv2 with the
+//                pool + argmax in the epilogue (pool windows = 4 accumulators
+//                of one thread, as float2 pairs -> v_pk_fma_f32), the FC chain
+//                and softmax xent forward, then the whole backward pass: FC
+//                dX chain, pool2/ReLU2 scatter, conv2 filter grad (sparse:
+//                only the 25 argmax pixels per channel carry gradient),
+//                conv2 data grad, pool1/ReLU1, conv1 filter grad (sparse
+//                again).  Per image it writes the FC layer inputs / deltas and
+//                its 2872 conv weight-gradient partials.
+//  update kernel FC weight grads as act^T delta over the batch (LDS-staged
+//                tiles), conv grads as the sum of the per-image partials (in
+//                image order: deterministic), then momentum SGD with the
+//                device LR, and the device-step bump.
+//
+// Eval is the image kernel's forward half, ending in argmax + error count.
+#include <stdexcept>
+
+#include "common.h"
+#include "lenet.h"
+
+namespace lenet {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int NT = 512;  // threads per image workgroup
+constexpr int IH = 32, IC = 3;
+constexpr int C1 = 6, P1 = 14;
+constexpr int C2 = 16, O2 = 10, P2 = 5;
+constexpr int F0 = 400, F1 = 120, F2 = 84, F3 = 10;
+constexpr int W1N = 25 * IC * C1;  // 450
+constexpr int W2N = 25 * C1 * C2;  // 2400
+constexpr int DP = O2 + 8;         // zero-bordered dpre2 plane (18 x 18)
+constexpr int DPS = 20;            // dpre2 pixel stride: 16 channels + 4 pad (bank spread)
+constexpr int XRS = 36, XPL = IH * XRS + 20;  // input row / plane strides (bank spread)
+
+// LDS layout (floats).  gfx950 lets one workgroup own up to 160 KiB.
+constexpr int S_X = 0;                        // input planes [3][32][XRS]
+constexpr int S_W1 = S_X + IC * XPL;          // conv1 HWIO weights + bias
+constexpr int S_B1 = S_W1 + 456;
+constexpr int S_W2 = S_B1 + 8;                // conv2 HWIO [tap][ci][co]
+constexpr int S_W2T = S_W2 + W2N;             // conv2 [tap][co][ci] (data grad operand)
+constexpr int S_B2 = S_W2T + W2N;
+constexpr int S_P1 = S_B2 + C2;               // pooled conv1 [14][14][6]
+constexpr int S_P2 = S_P1 + P1 * P1 * C1;     // pooled conv2 [5][5][16] = a2
+constexpr int S_H1 = S_P2 + F0;
+constexpr int S_H2 = S_H1 + 128;
+constexpr int S_D3 = S_H2 + 88;               // dlogits
+constexpr int S_D2 = S_D3 + 16;               // dz2
+constexpr int S_D1 = S_D2 + 88;               // dz1
+constexpr int S_T2 = S_D1 + 128;              // (g2, p1 offset of the argmax) per (pp, co)
+constexpr int S_DPRE2 = S_T2 + 2 * F0;        // dpre2 [18][18][DPS], zero border
+constexpr int S_T1 = S_DPRE2;                 // (g1, x offset of the argmax) per (p, c): after I
+constexpr int S_G1 = S_DPRE2 + DP * DP * DPS; // data-grad partial of the 2nd channel group
+constexpr int S_RED = S_G1 + P1 * P1 * C1;    // split-K partials
+constexpr int S_TOTAL = S_RED + NT;
+static_assert(S_TOTAL * 4 <= 160 * 1024, "image kernel LDS budget");
+static_assert(2 * P1 * P1 * C1 <= DP * DP * DPS, "T1 must fit in the dpre2 region");
+
+__device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
+
+// 2x2 max pool of accumulators (q order: (0,0) (0,1) (1,0) (1,1), strict >
+// so the first maximum wins, like TF / torch max pooling)
+__device__ __forceinline__ void pool4(f2 a01, f2 a23, float& v, int& q) {
+  v = a01.x;
+  q = 0;
+  if (a01.y > v) { v = a01.y; q = 1; }
+  if (a23.x > v) { v = a23.x; q = 2; }
+  if (a23.y > v) { v = a23.y; q = 3; }
+}
+
+template <bool TRAIN>
+__global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
+  __shared__ float sm[S_TOTAL];
+  __shared__ uint8_t q1s[P1 * P1 * C1];
+  __shared__ uint8_t q2s[F0];
+  const int tid = threadIdx.x;
+  const int img = blockIdx.x;
+  long long row = img;
+  if (TRAIN) {
+    const long long st = *a.step;
+    row = (st * a.batch) % (long long)(a.n_local - a.batch) + img;
+    if (img == 0 && tid == 0)  // reference LR schedule (mpipy.py:59-64), staircase per local epoch
+      *a.lr_out = a.base_lr * powf(a.lr_decay, (float)((st * a.batch) / a.n_local));
+  }
+  const float* W = a.params;
+  const Offsets o = a.off;
+
+  // ---- A: every global load of the phase issued before any LDS store (one
+  // memory round trip): image rows (NHWC float4 -> padded planes), conv
+  // weights (+ the [tap][co][ci] copy of W2 for the data grad)
+  {
+    const float4* xr4 = reinterpret_cast<const float4*>(a.x + row * (IH * IH * IC));
+    float4 xv[2];
+    xv[0] = xr4[tid];
+    if (tid < 256) xv[1] = xr4[tid + NT];
+    const float w1v = tid < W1N ? W[o.c1w + tid] : 0.f;
+    const float b1v = tid < C1 ? W[o.c1b + tid] : 0.f;
+    const float b2v = tid < C2 ? W[o.c2b + tid] : 0.f;
+    float w2v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int e = tid + NT * k;
+      w2v[k] = e < W2N ? W[o.c2w + e] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (k == 1 && tid >= 256) break;
+      const int e0 = 4 * (tid + NT * k);
+      const float v[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = e0 + j, ci = e % IC, pix = e / IC;
+        sm[S_X + ci * XPL + (pix >> 5) * XRS + (pix & 31)] = v[j];
+      }
+    }
+    if (tid < W1N) sm[S_W1 + tid] = w1v;
+    if (tid < C1) sm[S_B1 + tid] = b1v;
+    if (tid < C2) sm[S_B2 + tid] = b2v;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int e = tid + NT * k;
+      if (e < W2N) {
+        sm[S_W2 + e] = w2v[k];
+        const int co = e & 15, ci = (e >> 4) % C1, t = (e >> 4) / C1;
+        sm[S_W2T + (t * C2 + co) * C1 + ci] = w2v[k];
+      }
+    }
+    if (TRAIN)
+#pragma unroll
+      for (int k = 0; k < (DP * DP * DPS + NT - 1) / NT; ++k) {
+        const int e = tid + NT * k;
+        if (e < DP * DP * DPS) sm[S_DPRE2 + e] = 0.f;
+      }
+  }
+  const int label = a.y[row];
+  __syncthreads();
+  if (a.stop_phase == 0) return;
+
+  // ---- B: conv1 + bias + ReLU + pool: thread = (pooled pixel, 3 channels);
+  // the channel triple is wave-uniform (weights are LDS broadcasts)
+  {
+    const int cg = tid >> 8, p = tid & 255;
+    if (p < P1 * P1) {
+      const int py = p / P1, px = p % P1;
+      f2 s01[3], s23[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) s01[c] = s23[c] = f2{0.f, 0.f};
+#pragma unroll
+      for (int ci = 0; ci < IC; ++ci)
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) {
+            const float* xp = sm + S_X + ci * XPL + (2 * py + kh) * XRS + 2 * px + kw;
+            const f2 x01 = {xp[0], xp[1]}, x23 = {xp[XRS], xp[XRS + 1]};
+            const float* wp = sm + S_W1 + ((kh * 5 + kw) * IC + ci) * C1 + 3 * cg;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+              const f2 w = {wp[c], wp[c]};
+              s01[c] = __builtin_elementwise_fma(x01, w, s01[c]);
+              s23[c] = __builtin_elementwise_fma(x23, w, s23[c]);
+            }
+          }
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float v;
+        int q;
+        pool4(s01[c], s23[c], v, q);
+        const int co = 3 * cg + c;
+        sm[S_P1 + p * C1 + co] = relu(v + sm[S_B1 + co]);
+        q1s[p * C1 + co] = (uint8_t)q;
+      }
+    }
+  }
+  __syncthreads();
+  if (a.stop_phase == 1) return;
+
+  // ---- C: conv2 + bias + ReLU + pool: thread = (pooled pixel, channel)
+  if (tid < F0) {
+    const int co = tid & 15, pp = tid >> 4, py = pp / P2, px = pp % P2;
+    f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+        for (int ci = 0; ci < C1; ++ci) {
+          const float* xp = sm + S_P1 + ((2 * py + kh) * P1 + 2 * px + kw) * C1 + ci;
+          const f2 x01 = {xp[0], xp[C1]}, x23 = {xp[P1 * C1], xp[P1 * C1 + C1]};
+          const float wv = sm[S_W2 + ((kh * 5 + kw) * C1 + ci) * C2 + co];
+          const f2 w = {wv, wv};
+          s01 = __builtin_elementwise_fma(x01, w, s01);
+          s23 = __builtin_elementwise_fma(x23, w, s23);
+        }
+    float v;
+    int q;
+    pool4(s01, s23, v, q);
+    sm[S_P2 + tid] = relu(v + sm[S_B2 + co]);  // (h, w, c) flatten = FC1 input order
+    q2s[tid] = (uint8_t)q;
+  }
+  __syncthreads();
+  if (a.stop_phase == 2) return;
+
+  // ---- D: FC1 400 -> 120 + ReLU: 4-way split K, coalesced weight columns,
+  // all 100 loads of a thread in flight
+  {
+    const int j = tid & 127, g = tid >> 7;
+    float acc = 0.f;
+    if (j < F1) {
+      const float* wp = W + o.f1w + (g * 100) * F1 + j;
+      const float* xp = sm + S_P2 + g * 100;
+      float wv[100];
+#pragma unroll
+      for (int i = 0; i < 100; ++i) wv[i] = wp[i * F1];
+#pragma unroll
+      for (int i = 0; i < 100; ++i) acc = fmaf(xp[i], wv[i], acc);
+    }
+    sm[S_RED + tid] = acc;
+  }
+  __syncthreads();
+  if (tid < F1) {
+    const float z = W[o.f1b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
+                    sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
+    sm[S_H1 + tid] = relu(z);
+  }
+  __syncthreads();
+  // ---- E: FC2 120 -> 84 + ReLU
+  {
+    const int j = tid & 127, g = tid >> 7;
+    float acc = 0.f;
+    if (j < F2) {
+      const float* wp = W + o.f2w + (g * 30) * F2 + j;
+      const float* xp = sm + S_H1 + g * 30;
+      float wv[30];
+#pragma unroll
+      for (int i = 0; i < 30; ++i) wv[i] = wp[i * F2];
+#pragma unroll
+      for (int i = 0; i < 30; ++i) acc = fmaf(xp[i], wv[i], acc);
+    }
+    sm[S_RED + tid] = acc;
+  }
+  __syncthreads();
+  if (tid < F2) {
+    const float z = W[o.f2b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
+                    sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
+    sm[S_H2 + tid] = relu(z);
+  }
+  __syncthreads();
+  // ---- F: FC3 84 -> 10: 32 K groups of <= 3
+  {
+    const int j = tid & 15, g = tid >> 4;
+    float acc = 0.f;
+    if (j < F3)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int i = g + 32 * u;
+        if (i < F2) acc = fmaf(sm[S_H2 + i], W[o.f3w + i * F3 + j], acc);
+      }
+    sm[S_RED + tid] = acc;
+  }
+  __syncthreads();
+  if (tid < 64) {  // one wave: logits, softmax xent, argmax
+    float lg = -INFINITY;
+    if (tid < F3) {
+      float z = W[o.f3b + tid];
+      for (int g = 0; g < 32; ++g) z += sm[S_RED + g * 16 + tid];
+      lg = z;
+    }
+    const float mx = wave_max(lg);
+    const unsigned long long bal = __ballot(tid < F3 && lg == mx);
+    const int am = __ffsll((long long)bal) - 1;
+    if (!TRAIN) {
+      if (a.logits && tid < F3) a.logits[(size_t)img * F3 + tid] = lg;
+      if (tid == 0 && a.errors && am != label) atomicAdd(a.errors, 1);
+      return;
+    }
+    const float e = tid < F3 ? __expf(lg - mx) : 0.f;
+    const float se = wave_sum(e);
+    const float lab = wave_sum(tid == label ? lg : 0.f);
+    if (tid < F3) sm[S_D3 + tid] = (e / se - (tid == label ? 1.f : 0.f)) / (float)a.batch;
+    if (tid == 0) {
+      a.loss_rows[img] = logf(se) + mx - lab;
+      if (a.correct && am == label) atomicAdd(a.correct, 1);
+    }
+  }
+  if (!TRAIN) return;
+  __syncthreads();
+  if (a.stop_phase == 3) return;
+
+  // ---- G: FC backward (dX chain), ReLU masks from the stored activations
+  float* act = a.acts + (size_t)img * ACT_STRIDE;
+  float* del = a.deltas + (size_t)img * DELTA_STRIDE;
+  if (tid < F2) {  // dz2 = relu'(h2) * W3 dz3
+    const float* wp = W + o.f3w + tid * F3;
+    float wv[F3];
+#pragma unroll
+    for (int j = 0; j < F3; ++j) wv[j] = wp[j];
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < F3; ++j) s = fmaf(wv[j], sm[S_D3 + j], s);
+    sm[S_D2 + tid] = sm[S_H2 + tid] > 0.f ? s : 0.f;
+  }
+  __syncthreads();
+  {  // dz1 = relu'(h1) * W2f dz2: 4 lanes per row, 21 columns each
+    const int i = tid >> 2, part = tid & 3;
+    float s = 0.f;
+    if (i < F1) {
+      const float* wp = W + o.f2w + i * F2 + part * 21;
+      float wv[21];
+#pragma unroll
+      for (int j = 0; j < 21; ++j) wv[j] = wp[j];
+#pragma unroll
+      for (int j = 0; j < 21; ++j) s = fmaf(wv[j], sm[S_D2 + part * 21 + j], s);
+    }
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (i < F1 && part == 0) sm[S_D1 + i] = sm[S_H1 + i] > 0.f ? s : 0.f;
+  }
+  __syncthreads();
+  if (tid < F0) {  // da2 = W1f dz1, through ReLU2 (pooled > 0) -> g2
+    const float4* wp = reinterpret_cast<const float4*>(W + o.f1w + tid * F1);
+    float4 wv[F1 / 4];
+#pragma unroll
+    for (int j4 = 0; j4 < F1 / 4; ++j4) wv[j4] = wp[j4];
+    float s = 0.f;
+#pragma unroll
+    for (int j4 = 0; j4 < F1 / 4; ++j4) {
+      const float* d = sm + S_D1 + 4 * j4;
+      s = fmaf(wv[j4].x, d[0], s);
+      s = fmaf(wv[j4].y, d[1], s);
+      s = fmaf(wv[j4].z, d[2], s);
+      s = fmaf(wv[j4].w, d[3], s);
+    }
+    const float g2 = sm[S_P2 + tid] > 0.f ? s : 0.f;
+    // pool2 backward: the gradient lands on the argmax pixel of the window
+    const int co = tid & 15, pp = tid >> 4, py = pp / P2, px = pp % P2, q = q2s[tid];
+    const int u = 2 * py + (q >> 1), v = 2 * px + (q & 1);
+    sm[S_DPRE2 + ((u + 4) * DP + v + 4) * DPS + co] = g2;
+    sm[S_T2 + 2 * tid] = g2;
+    sm[S_T2 + 2 * tid + 1] = __int_as_float((u * P1 + v) * C1);
+  }
+  // FC layer inputs / deltas for the batch-level weight gradients
+  if (tid < F0) act[tid] = sm[S_P2 + tid];
+  if (tid < F1) act[F0 + tid] = sm[S_H1 + tid];
+  if (tid < F2) act[F0 + F1 + tid] = sm[S_H2 + tid];
+  if (tid < F1) del[tid] = sm[S_D1 + tid];
+  if (tid < F2) del[F1 + tid] = sm[S_D2 + tid];
+  if (tid < F3) del[F1 + F2 + tid] = sm[S_D3 + tid];
+  __syncthreads();
+
+  float* cp = a.convp + (size_t)img * CONVP_STRIDE;
+  if (a.stop_phase == 4) return;
+  // ---- H: conv2 filter grad, sparse over the 25 argmax pixels per channel
+  // (table T2 = (g2, p1 offset of the argmax pixel) per (pp, co)):
+  // dW2[kh,kw,ci,co] = sum_pp g2[pp,co] * p1[u_pp + kh, v_pp + kw, ci]
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const int e = tid + NT * k;
+    if (e < W2N) {
+      const int co = e & 15, r = e >> 4, ci = r % C1, t = r / C1, kh = t / 5, kw = t % 5;
+      const float* p1 = sm + S_P1 + (kh * P1 + kw) * C1 + ci;
+      const float2* t2 = reinterpret_cast<const float2*>(sm + S_T2) + co;
+      float s = 0.f;
+#pragma unroll
+      for (int pp = 0; pp < P2 * P2; ++pp) {
+        const float2 tv = t2[pp * C2];
+        s = fmaf(tv.x, p1[__float_as_int(tv.y)], s);
+      }
+      cp[W1N + 8 + e] = s;
+    }
+  }
+  if (tid < C2) {  // db2
+    float s = 0.f;
+    for (int pp = 0; pp < P2 * P2; ++pp) s += sm[S_T2 + 2 * (pp * C2 + tid)];
+    cp[W1N + 8 + W2N + tid] = s;
+  }
+  if (a.stop_phase == 5) return;
+  // ---- I: conv2 data grad over the zero-bordered dpre2 plane:
+  // dp1[y,x,ci] = sum_{kh,kw,co} dpre2[y-kh, x-kw, co] W2[kh,kw,ci,co].
+  // Thread = (pooled1 pixel, half of the 16 channels co), all 6 ci as 3
+  // packed pairs (v_pk_fma_f32): per tap 2 float4 dpre2 reads + 8 x 3 float2
+  // weight broadcasts ([tap][co][ci] copy of W2).
+  {
+    const int grp = tid >> 8, p = tid & 255;
+    f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f}, s45 = {0.f, 0.f};
+    if (p < P1 * P1) {
+      const int y = p / P1, x = p % P1;
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const float4* dp = reinterpret_cast<const float4*>(
+              sm + S_DPRE2 + ((y - kh + 4) * DP + x - kw + 4) * DPS + 8 * grp);
+          const float4 da = dp[0], db = dp[1];
+          const float d[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+          const f2* wp =
+              reinterpret_cast<const f2*>(sm + S_W2T + ((kh * 5 + kw) * C2 + 8 * grp) * C1);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            const f2 dd = {d[c], d[c]};
+            s01 = __builtin_elementwise_fma(dd, wp[3 * c], s01);
+            s23 = __builtin_elementwise_fma(dd, wp[3 * c + 1], s23);
+            s45 = __builtin_elementwise_fma(dd, wp[3 * c + 2], s45);
+          }
+        }
+      if (grp == 1) {
+        float* gp = sm + S_G1 + p * C1;
+        gp[0] = s01.x, gp[1] = s01.y, gp[2] = s23.x, gp[3] = s23.y, gp[4] = s45.x, gp[5] = s45.y;
+      }
+    }
+    __syncthreads();  // every dpre2 read is done: the T1 table may overwrite it
+    if (grp == 0 && p < P1 * P1) {
+      const int py = p / P1, px = p % P1;
+      const float sv[6] = {s01.x, s01.y, s23.x, s23.y, s45.x, s45.y};
+#pragma unroll
+      for (int c = 0; c < C1; ++c) {
+        const float g = sm[S_G1 + p * C1 + c] + sv[c];
+        const int q = q1s[p * C1 + c];
+        const int u = 2 * py + (q >> 1), v = 2 * px + (q & 1);
+        // ReLU1 through the pooled output; T1 = (g1, input offset of the argmax)
+        sm[S_T1 + 2 * (p * C1 + c)] = sm[S_P1 + p * C1 + c] > 0.f ? g : 0.f;
+        sm[S_T1 + 2 * (p * C1 + c) + 1] = __int_as_float(u * XRS + v);
+      }
+    }
+  }
+  __syncthreads();
+  if (a.stop_phase == 6) return;
+  // ---- J: conv1 filter grad, sparse over the 196 argmax pixels per channel:
+  // dW1[kh,kw,ci,c] = sum_p g1[p,c] * x[ci, u_p + kh, v_p + kw]
+  if (tid < W1N) {
+    const int c = tid % C1, ci = (tid / C1) % IC, t = tid / (C1 * IC), kh = t / 5, kw = t % 5;
+    const float* xp = sm + S_X + ci * XPL + kh * XRS + kw;
+    const float2* t1 = reinterpret_cast<const float2*>(sm + S_T1) + c;
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll 14
+    for (int p = 0; p < P1 * P1; p += 2) {
+      const float2 ta = t1[p * C1], tb = t1[(p + 1) * C1];
+      s0 = fmaf(ta.x, xp[__float_as_int(ta.y)], s0);
+      s1 = fmaf(tb.x, xp[__float_as_int(tb.y)], s1);
+    }
+    cp[tid] = s0 + s1;
+  } else if (tid < W1N + C1) {  // db1
+    const int c = tid - W1N;
+    float s = 0.f;
+    for (int p = 0; p < P1 * P1; ++p) s += sm[S_T1 + 2 * (p * C1 + c)];
+    cp[W1N + c] = s;
+  }
+}
+
+// ------------------------------------------------------------- update ----
+// Blocks: FC weight tiles of 16 input rows x all outputs (f1: 25, f2: 8,
+// f3: 6; tile 0 of each layer also reduces the bias), then 12 blocks of 256
+// conv parameters.  FC grads: g[i][j] = sum_n act[n][i] delta[n][j], act and
+// delta staged through LDS in chunks of 64 images.
+constexpr int UT = 16;
+constexpr int UB_F1 = F0 / UT, UB_F2 = (F1 + UT - 1) / UT, UB_F3 = (F2 + UT - 1) / UT;
+constexpr int UB_FC = UB_F1 + UB_F2 + UB_F3;
+constexpr int CONV_N = W1N + 8 + W2N + C2;  // 2874 slots (2872 used)
+constexpr int UB_CONV = (CONV_N + 255) / 256;
+
+template <bool APPLY>
+__device__ __forceinline__ void apply_one(float* w, float* g, float* m, int i, float gv, float mu,
+                                          float lr) {
+  if (APPLY) {
+    const float mv = mu * m[i] + gv;
+    m[i] = mv;
+    w[i] -= lr * mv;
+  } else {
+    g[i] = gv;
+  }
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ acts,
+                                                     const float* __restrict__ deltas,
+                                                     const float* __restrict__ convp, int batch,
+                                                     const Offsets o, float* __restrict__ w,
+                                                     float* __restrict__ g, float* __restrict__ m,
+                                                     float mu, const float* lr_ptr,
+                                                     long long* step) {
+  __shared__ float sa[64 * UT];
+  __shared__ float sd[64 * 128];
+  const int tid = threadIdx.x;
+  const float lr = APPLY ? *lr_ptr : 0.f;
+  int blk = blockIdx.x;
+  if (APPLY && blk == 0 && tid == 0) *step += 1;
+  if (blk < UB_FC) {
+    int layer, tile;
+    if (blk < UB_F1) {
+      layer = 0;
+      tile = blk;
+    } else if (blk < UB_F1 + UB_F2) {
+      layer = 1;
+      tile = blk - UB_F1;
+    } else {
+      layer = 2;
+      tile = blk - UB_F1 - UB_F2;
+    }
+    const int nin = layer == 0 ? F0 : (layer == 1 ? F1 : F2);
+    const int nout = layer == 0 ? F1 : (layer == 1 ? F2 : F3);
+    const int aoff = layer == 0 ? 0 : (layer == 1 ? F0 : F0 + F1);
+    const int doff = layer == 0 ? 0 : (layer == 1 ? F1 : F1 + F2);
+    const int woff = layer == 0 ? o.f1w : (layer == 1 ? o.f2w : o.f3w);
+    const int boff = layer == 0 ? o.f1b : (layer == 1 ? o.f2b : o.f3b);
+    const int i0 = tile * UT;
+    // thread -> (row i0 + r, columns j = c, c + 32, c + 64, c + 96) ; r < 16 (tid >> 5... )
+    const int r = tid >> 4, c0 = tid & 15;  // 16 rows x 16 column lanes, 8 columns each
+    float acc[8], bacc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = bacc[u] = 0.f;
+    for (int n0 = 0; n0 < batch; n0 += 64) {
+      const int nn = min(64, batch - n0);
+      __syncthreads();
+      // all staging loads in flight before the LDS stores (one round trip)
+      float va[4], vd[32];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = tid + 256 * k, n = e / UT, i = e % UT;
+        va[k] = (n < nn && i0 + i < nin) ? acts[(size_t)(n0 + n) * ACT_STRIDE + aoff + i0 + i]
+                                        : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        const int e = tid + 256 * k, n = e >> 7, j = e & 127;
+        vd[k] = (n < nn && j < nout) ? deltas[(size_t)(n0 + n) * DELTA_STRIDE + doff + j] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sa[tid + 256 * k] = va[k];
+#pragma unroll
+      for (int k = 0; k < 32; ++k) sd[tid + 256 * k] = vd[k];
+      __syncthreads();
+      for (int n = 0; n < nn; ++n) {
+        const float av = sa[n * UT + r];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float dv = sd[n * 128 + c0 + 16 * u];
+          acc[u] = fmaf(av, dv, acc[u]);
+          bacc[u] += dv;
+        }
+      }
+    }
+    if (i0 + r < nin) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = c0 + 16 * u;
+        if (j < nout) apply_one<APPLY>(w, g, m, woff + (i0 + r) * nout + j, acc[u], mu, lr);
+      }
+    }
+    if (tile == 0 && r == 0) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = c0 + 16 * u;
+        if (j < nout) apply_one<APPLY>(w, g, m, boff + j, bacc[u], mu, lr);
+      }
+    }
+    return;
+  }
+  // conv parameters: sum of the per-image partials, in image order
+  const int e = (blk - UB_FC) * 256 + tid;
+  if (e >= CONV_N) return;
+  int dst;
+  if (e < W1N) dst = o.c1w + e;
+  else if (e < W1N + C1) dst = o.c1b + (e - W1N);
+  else if (e < W1N + 8) return;
+  else if (e < W1N + 8 + W2N) dst = o.c2w + (e - W1N - 8);
+  else dst = o.c2b + (e - W1N - 8 - W2N);
+  float s = 0.f;
+  for (int n0 = 0; n0 < batch; n0 += 32) {  // 32 image partials in flight, summed in order
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      v[u] = n0 + u < batch ? convp[(size_t)(n0 + u) * CONVP_STRIDE + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += v[u];
+  }
+  apply_one<APPLY>(w, g, m, dst, s, mu, lr);
+}
+
+// ------------------------------------------------------------- launchers ----
+void launch_image_train(const ImageArgs& a, hipStream_t s) {
+  if (a.batch <= 0 || a.n_local <= a.batch)
+    throw std::runtime_error("lenet: the local shard must exceed the batch");
+  image_kernel<true><<<a.batch, NT, 0, s>>>(a);
+}
+
+void launch_image_eval(const ImageArgs& a, int rows, hipStream_t s) {
+  if (rows <= 0) return;
+  image_kernel<false><<<rows, NT, 0, s>>>(a);
+}
+
+void launch_update(const float* acts, const float* deltas, const float* convp, int batch,
+                   const Offsets& off, float* params, float* grads, float* mom, float momentum,
+                   const float* lr, long long* step, bool apply, hipStream_t s) {
+  const int blocks = UB_FC + UB_CONV;
+  if (apply)
+    update_kernel<true><<<blocks, 256, 0, s>>>(acts, deltas, convp, batch, off, params, grads, mom,
+                                               momentum, lr, step);
+  else
+    update_kernel<false><<<blocks, 256, 0, s>>>(acts, deltas, convp, batch, off, params, grads,
+                                                mom, momentum, lr, step);
+}
+
+size_t acts_floats(int batch) { return (size_t)batch * ACT_STRIDE; }
+size_t deltas_floats(int batch) { return (size_t)batch * DELTA_STRIDE; }
+size_t convp_floats(int batch) { return (size_t)batch * CONVP_STRIDE; }
+
+}  // namespace lenet

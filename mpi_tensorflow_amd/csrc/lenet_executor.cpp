@@ -1,0 +1,72 @@
+#include "lenet_executor.h"
+
+#include <stdexcept>
+
+#include "kernels/mnist.h"  // optim::launch_sgd_momentum
+
+template <class T>
+static inline T* P(uintptr_t v) {
+  return reinterpret_cast<T*>(v);
+}
+
+LenetExecutor::LenetExecutor(const LenetPtrs& p) : p_(p) {
+  if (p_.batch <= 0 || p_.n_local <= p_.batch)
+    throw std::runtime_error("LenetExecutor: the local shard must exceed the batch");
+  if (p_.total % 4 != 0) throw std::runtime_error("LenetExecutor: flat buffer not float4-sized");
+}
+
+lenet::ImageArgs LenetExecutor::image_args() const {
+  lenet::ImageArgs a{};
+  a.x = P<const float>(p_.train_x);
+  a.y = P<const int>(p_.train_y);
+  a.n_local = p_.n_local;
+  a.batch = p_.batch;
+  a.step = P<const long long>(p_.step);
+  a.params = P<const float>(p_.params);
+  a.off = p_.off;
+  a.acts = P<float>(p_.acts);
+  a.deltas = P<float>(p_.deltas);
+  a.convp = P<float>(p_.convp);
+  a.loss_rows = P<float>(p_.loss_rows);
+  a.lr_out = P<float>(p_.lr);
+  a.base_lr = p_.base_lr;
+  a.lr_decay = p_.lr_decay;
+  a.correct = P<int>(p_.correct);
+  return a;
+}
+
+void LenetExecutor::forward_backward(hipStream_t s) {
+  lenet::launch_image_train(image_args(), s);
+  lenet::launch_update(P<const float>(p_.acts), P<const float>(p_.deltas), P<const float>(p_.convp),
+                       p_.batch, p_.off, P<float>(p_.params), P<float>(p_.grads), P<float>(p_.mom),
+                       p_.momentum, P<const float>(p_.lr), P<long long>(p_.step), false, s);
+}
+
+void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
+  lenet::launch_image_train(image_args(), s);
+  const bool apply = comm == nullptr;
+  lenet::launch_update(P<const float>(p_.acts), P<const float>(p_.deltas), P<const float>(p_.convp),
+                       p_.batch, p_.off, P<float>(p_.params), P<float>(p_.grads), P<float>(p_.mom),
+                       p_.momentum, P<const float>(p_.lr), P<long long>(p_.step), apply, s);
+  if (apply) return;
+  float* G = P<float>(p_.grads);
+  comm->all_reduce(G, G, (size_t)p_.total, 7 /*ncclFloat32*/, 0 /*ncclSum*/, s);
+  optim::launch_sgd_momentum(P<float>(p_.params), G, P<float>(p_.mom), p_.total, 0, 0.f,
+                             p_.momentum, 1.0f / (float)comm->size(), P<const float>(p_.lr), 0.f,
+                             P<long long>(p_.step), s);
+}
+
+void LenetExecutor::eval_chunk(const LenetPtrs& p, uintptr_t x, uintptr_t y, int M,
+                               uintptr_t logits, uintptr_t errors, hipStream_t s) {
+  lenet::ImageArgs a{};
+  a.x = P<const float>(x);
+  a.y = P<const int>(y);
+  a.n_local = M;
+  a.batch = M;
+  a.step = nullptr;
+  a.params = P<const float>(p.params);
+  a.off = p.off;
+  a.errors = P<int>(errors);
+  a.logits = P<float>(logits);
+  lenet::launch_image_eval(a, M, s);
+}

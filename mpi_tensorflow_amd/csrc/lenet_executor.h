@@ -1,0 +1,45 @@
+// Native training-step executor for LeNet-5 (BASELINE config 4).
+//
+// Same contract as MnistExecutor (mnist_executor.h): one call enqueues a whole
+// training step on a HIP stream with no host synchronisation, no allocation
+// and no host-side step state (batch offset and LR come from the device step
+// counter), so the Python engine captures G steps into one hipGraph.
+//   world 1:  image kernel -> update kernel (grads + momentum SGD)   2 launches
+//   world N:  image kernel -> update kernel (grads into the flat buffer)
+//             -> in-place all-reduce of the whole 250 KB flat gradient on
+//             the compute stream (one latency-bound bucket: a cross-stream
+//             fork/join would cost more than it hides) -> flat SGD with
+//             gscale 1/N                                    3 launches + 1 collective
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "collective.h"
+#include "kernels/lenet.h"
+
+struct LenetPtrs {
+  uintptr_t train_x = 0, train_y = 0;
+  int n_local = 0, batch = 64;
+  uintptr_t params = 0, grads = 0, mom = 0;
+  long long total = 0;
+  lenet::Offsets off{};
+  uintptr_t step = 0, lr = 0, correct = 0;
+  uintptr_t acts = 0, deltas = 0, convp = 0, loss_rows = 0;
+  float base_lr = 0.01f, lr_decay = 0.95f, momentum = 0.9f;
+};
+
+class LenetExecutor {
+ public:
+  explicit LenetExecutor(const LenetPtrs& p);
+  void train_step(hipStream_t s, Collective* comm);
+  // forward + backward with the weight grads in the flat grad buffer (no
+  // sync, no SGD, no step bump): numerics tests
+  void forward_backward(hipStream_t s);
+  // forward of rows [x, x + M) (device), argmax vs labels -> *errors (+ logits)
+  static void eval_chunk(const LenetPtrs& p, uintptr_t x, uintptr_t y, int M, uintptr_t logits,
+                         uintptr_t errors, hipStream_t s);
+
+ private:
+  lenet::ImageArgs image_args() const;
+  LenetPtrs p_;
+};

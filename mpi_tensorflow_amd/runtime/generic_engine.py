@@ -290,3 +290,16 @@ class GenericEngine:
             rows = torch.empty(m, device=self.device)
             self._C.ops.xent(ptr(logits), ptr(yb), m, k, ptr(rows), 0, ptr(correct), s)
         return 100.0 * (n - int(correct.item())) / max(1, n)
+
+
+def make_image_engine(cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
+                      device: torch.device, rank: int = 0, world: int = 1,
+                      comm: Optional[DeviceComm] = None, force_sync: bool = False):
+    """Engine for the extra image models: LeNet-5 in fp32 on a GPU runs the
+    fused two-launch executor (runtime/lenet_engine.py); everything else
+    (ResNet-18, LeNet-5 bf16, the CPU oracle) runs the op-by-op engine."""
+    if cfg.model == "lenet5" and device.type == "cuda" and cfg.dtype == "fp32":
+        from .lenet_engine import NativeLenetEngine
+
+        return NativeLenetEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)
+    return GenericEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)

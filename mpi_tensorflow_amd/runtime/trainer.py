@@ -117,10 +117,10 @@ class Trainer:
 
             return make_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
                                self.comm)
-        from .generic_engine import GenericEngine
+        from .generic_engine import make_image_engine
 
-        return GenericEngine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
-                             self.comm)
+        return make_image_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
+                                 self.comm)
 
     # ------------------------------------------------------------------- run
     def total_steps(self) -> int:

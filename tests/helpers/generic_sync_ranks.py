@@ -5,6 +5,8 @@ host-staged gloo communicator, so the backward-overlapped bucketed all-reduce
 cross-rank sums.  Rank 0 then replays the same steps SERIALLY (every rank's
 forward/backward on the same kernels, grads summed, one SGD with gscale 1/N)
 and the params must be bit-identical; all ranks must hold the same params.
+MODEL "lenet5-native" runs the fused LeNet-5 executor (runtime/lenet_engine.py)
+instead, whose single flat-gradient all-reduce goes through the same comm.
 Launch: torchrun --nproc-per-node 2 ... generic_sync_ranks.py MODEL STEPS BATCH"""
 import sys
 
@@ -16,7 +18,9 @@ from mpi_tensorflow_amd import config as C
 from mpi_tensorflow_amd.models.generic import model_input_shape
 from mpi_tensorflow_amd.parallel import dist as D
 from mpi_tensorflow_amd.parallel.comm import HostStagedComm
+from mpi_tensorflow_amd.ops import native, ptr, stream_handle
 from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+from mpi_tensorflow_amd.runtime.lenet_engine import NativeLenetEngine
 from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
 
@@ -27,6 +31,10 @@ def shard(model, rank, rows, seed):
 
 def main():
     model = sys.argv[1]
+    fused = model == "lenet5-native"
+    if fused:
+        model = "lenet5"
+    Eng = NativeLenetEngine if fused else GenericEngine
     steps = int(sys.argv[2])
     B = int(sys.argv[3])
     rows = 4 * B
@@ -34,9 +42,9 @@ def main():
     dev = torch.device("cuda")
     cfg = C.TrainConfig(model=model, batch_size=B, graph=False).validate()
     x, y = shard(model, di.rank, rows, cfg.seed)
-    eng = GenericEngine(cfg, x, y, dev, di.rank, di.world, HostStagedComm(di))
-    assert eng.bucketer is not None
-    nb = len(eng.bucketer.slices)
+    eng = Eng(cfg, x, y, dev, di.rank, di.world, HostStagedComm(di))
+    assert eng.grad_sync
+    nb = 1 if fused else len(eng.bucketer.slices)
     eng.train(steps)
     torch.cuda.synchronize()
     p = eng.params.detach().cpu()
@@ -44,7 +52,7 @@ def main():
     dist.broadcast(ref, 0)
     assert torch.equal(ref, p), "replicas diverged"
     if di.rank == 0:
-        engs = [GenericEngine(cfg, *shard(model, r, rows, cfg.seed), dev, r, di.world, None)
+        engs = [Eng(cfg, *shard(model, r, rows, cfg.seed), dev, r, di.world, None)
                 for r in range(di.world)]
         lead = engs[0]
         for _ in range(steps):
@@ -52,16 +60,25 @@ def main():
                 if e is not lead:
                     e.params.data.copy_(lead.params.data)
                     e.step_dev.copy_(lead.step_dev)
-                e.forward_backward_gpu()
+                if fused:
+                    e.forward_backward_only()
+                else:
+                    e.forward_backward_gpu()
             for e in engs[1:]:
                 lead.grads.add_(e.grads)
-            lead.update_gpu(1.0 / di.world)
+            if fused:  # the flat SGD the executor runs after its all-reduce
+                native().optim.sgd_momentum(ptr(lead.params), ptr(lead.grads), ptr(lead.mom),
+                                            lead.layout.total, 0, 0.0, cfg.momentum,
+                                            1.0 / di.world, ptr(lead.lr_dev), 0.0,
+                                            ptr(lead.step_dev), stream_handle())
+            else:
+                lead.update_gpu(1.0 / di.world)
         torch.cuda.synchronize()
         q = lead.params.detach().cpu()
         d = (p - q).abs().max().item()
         assert torch.equal(p, q), f"serial emulation differs by {d}"
         assert np.isfinite(p.numpy()).all()
-        print(f"GENERIC_SYNC_OK model={model} world={di.world} buckets={nb} steps={steps}",
+        print(f"GENERIC_SYNC_OK model={sys.argv[1]} world={di.world} buckets={nb} steps={steps}",
               flush=True)
     D.barrier()
     D.shutdown()

@@ -34,7 +34,8 @@ def test_sharded_schedule_matches_buckets_two_ranks(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,steps,batch", [("lenet5", 5, 64), ("resnet18", 3, 4)])
+@pytest.mark.parametrize("model,steps,batch", [("lenet5", 5, 64), ("resnet18", 3, 4),
+                                               ("lenet5-native", 6, 64)])
 def test_generic_bucketed_allreduce_matches_serial_two_ranks(model, steps, batch):
     """Backward-overlapped bucketed all-reduce (parallel/overlap.py) with real
     cross-rank sums vs a serial averaged-gradient emulation: bit-identical."""
