@@ -53,6 +53,8 @@ __global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ 
   if (MODE == BN_BWD) {
     mu = ld4(mean + 4 * q);
     rs = ld4(rstd + 4 * q);
+  } else if (MODE == SUM_SQ && mean) {
+    mu = ld4(mean + 4 * q);  // shifted data: sums of (x - K), K = a sample of the channel
   }
   if (rl < RP) {
 #pragma unroll 4
@@ -60,8 +62,9 @@ __global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ 
       const size_t o = (size_t)r * C + 4 * q;
       const float4 v = ld4(a + o);
       if (MODE == SUM_SQ) {
-        s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
-        s2.x += v.x * v.x; s2.y += v.y * v.y; s2.z += v.z * v.z; s2.w += v.w * v.w;
+        const float4 w = make_float4(v.x - mu.x, v.y - mu.y, v.z - mu.z, v.w - mu.w);
+        s1.x += w.x; s1.y += w.y; s1.z += w.z; s1.w += w.w;
+        s2.x += w.x * w.x; s2.y += w.y * w.y; s2.z += w.z * w.z; s2.w += w.w * w.w;
       } else if (MODE == SUM_PROD) {
         const float4 u = ld4(b + o);
         s1.x += v.x; s1.y += v.y; s1.z += v.z; s1.w += v.w;
@@ -136,6 +139,11 @@ __global__ __launch_bounds__(256) void partial1_kernel(const float* __restrict__
 
 // One wave per channel: s1 / s2 = sums of the nb block partials.  BN
 // forward mode also writes mean / rstd and updates the running statistics.
+// The BN forward partials are SHIFTED sums, of (x - K) and (x - K)^2 with
+// K = the channel's value in row 0 (`shift`): var = E[(x-K)^2] - E[x-K]^2
+// cancels only (mean - K)^2 / var, a few units for a sample of the channel,
+// instead of mean^2 / var for the plain E[x^2] - mean^2 (a channel with mean
+// 1e3 and std 1 loses every digit of its variance in fp32 that way).
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nb,
                                                        int C, float* __restrict__ s1,
                                                        float* __restrict__ s2, int bn_fwd,
@@ -143,7 +151,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
                                                        float* __restrict__ mean,
                                                        float* __restrict__ rstd,
                                                        float* __restrict__ rmean,
-                                                       float* __restrict__ rvar) {
+                                                       float* __restrict__ rvar,
+                                                       const float* __restrict__ shift) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
   float a = 0.f, b = 0.f;
@@ -158,8 +167,9 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
   if (s2) s2[c] = b;
   if (bn_fwd) {
     const float inv = 1.f / (float)rows;
-    const float m = a * inv;
-    const float var = fmaxf(b * inv - m * m, 0.f);
+    const float ms = a * inv;  // mean of the shifted data
+    const float var = fmaxf(b * inv - ms * ms, 0.f);
+    const float m = ms + (shift ? shift[c] : 0.f);
     mean[c] = m;
     rstd[c] = rsqrtf(var + eps);
     if (rmean) {  // torch semantics: unbiased variance in the running estimate
@@ -288,7 +298,7 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
   }
   bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, s1, s2, 0, rows, 0.f, 0.f, nullptr,
-                                                   nullptr, nullptr, nullptr);
+                                                   nullptr, nullptr, nullptr, nullptr);
 }
 
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
@@ -299,9 +309,10 @@ void bn_fwd(const float* x, long long rows, int C, const float* g, const float* 
   const long long n4 = rows * C / 4;
   if (training) {
     const int nb = bn::nblocks(rows, C);
-    run_partials(bn::SUM_SQ, x, nullptr, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+    // shift K = row 0 of x (passed as the partials' `mean`)
+    run_partials(bn::SUM_SQ, x, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, st);
     bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, nullptr, nullptr, 1, rows, eps,
-                                                     momentum, mean, rstd, rmean, rvar);
+                                                     momentum, mean, rstd, rmean, rvar, x);
     bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
                                                           relu ? 1 : 0, 0, eps,
                                                           reinterpret_cast<uint2*>(yb));
@@ -320,7 +331,7 @@ void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, 
   run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, st);
   // db = sum dy', dg = sum dy' xhat
   bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, db, dg, 0, rows, 0.f, 0.f, nullptr,
-                                                   nullptr, nullptr, nullptr);
+                                                   nullptr, nullptr, nullptr, nullptr);
   const long long n4 = rows * C / 4;
   bn::bwd_apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx,
                                                             dres, n4, C, rows, relu ? 1 : 0,

@@ -85,6 +85,20 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Component-wise select of a vector struct.  `ok ? v : zero` on a
+// HIP_vector_type (a struct) is lowered by clang to a select between two
+// stack slots, i.e. scratch stores + a scratch load per element (it cost the
+// bf16 conv loaders 24-48 B of scratch per thread); these stay in VGPRs.
+__device__ __forceinline__ uint4 sel(bool ok, uint4 v) {
+  return make_uint4(ok ? v.x : 0u, ok ? v.y : 0u, ok ? v.z : 0u, ok ? v.w : 0u);
+}
+__device__ __forceinline__ uint2 sel(bool ok, uint2 v) {
+  return make_uint2(ok ? v.x : 0u, ok ? v.y : 0u);
+}
+__device__ __forceinline__ float4 sel(bool ok, float4 v) {
+  return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): consecutive logical tiles land on the
 // same XCD (shared L2) instead of being dealt round-robin over 8 XCDs.

@@ -145,13 +145,13 @@ struct Loader {
       const XT* src = abase[i] + ((size_t)iyc * s.W + ixc) * s.C + ci0;
       if constexpr (XB) {
         const uint4 v = *reinterpret_cast<const uint4*>(src);
-        rab[i] = ok ? v : make_uint4(0u, 0u, 0u, 0u);
+        rab[i] = sel(ok, v);
       } else {
         const float4* p = reinterpret_cast<const float4*>(src);
         const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
         const float4 v0 = p[0], v1 = p[1];
-        ra[i][0] = ok ? v0 : z;
-        ra[i][1] = ok ? v1 : z;
+        ra[i][0] = sel(ok, v0);
+        ra[i][1] = sel(ok, v1);
       }
     }
     const size_t wo = (size_t)tap * s.K * s.C + ci0;
@@ -298,7 +298,7 @@ struct WgLoader {
         const bool ok = mv && p + q < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
         const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
         const V v = *reinterpret_cast<const V*>(x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ca);
-        ra[q] = ok ? v : z;
+        ra[q] = sel(ok, v);
         if (++ox == s.OW) {  // next output pixel (rows past the end are masked)
           ox = 0;
           if (++oy == s.OH) {
@@ -313,7 +313,7 @@ struct WgLoader {
 #pragma unroll
       for (int q = 0; q < PB; ++q) {
         const V v = *reinterpret_cast<const V*>(dy + (size_t)min(p + q, npix - 1) * s.K + cb);
-        rb[q] = p + q < npix ? v : z;
+        rb[q] = sel(p + q < npix, v);
       }
     }
   }
@@ -574,6 +574,267 @@ static inline ConvShape dgrad_shape(const ConvShape& s) {
   return d;
 }
 
+// ------------------------------------------ 3x3 stride-1 filter gradient ----
+// dW[kh,kw,ci,co] = sum_{n,y,x} X[n, y+kh-1, x+kw-1, ci] dY[n, y, x, co] for
+// the 3x3 / stride-1 / pad-1 layers that make up most of ResNet-18.  The
+// generic wgrad above re-fetches (and per-element transposes) the shifted X
+// tile once per tap and ran layer 1 at ~86 TFLOP/s (4 x 86 us per step).
+// Here a block owns a 64 (ci) x 64 (co) pair for ALL 9 taps and streams
+// 64-pixel chunks (TR whole output rows of one image):
+//   * the chunk's X halo ((TR + 2) x (W + 2) pixels x 64 ci) and its dY tile
+//     (64 pixels x 64 co) are staged once into LDS as plain [pixel][channel]
+//     rows (16-byte global loads, 16-byte LDS stores, zero borders);
+//   * the MFMA wants 8 consecutive PIXELS of one channel per lane for both
+//     operands (the reduction axis is the pixel), which is a column of those
+//     images: gfx950's ds_read_b64_tr_b16 delivers it transposed for free
+//     (cdna_hip_programming.md T10), and each lane supplies its own pixel-row
+//     address, so the tap shift is just an address offset into the halo;
+//   * per 16-pixel k-step a wave reads its dY fragment ONCE and reuses it for
+//     the 9 taps' MFMAs (9 accumulators of 32 x 32), i.e. 20 transposed reads
+//     per 9 v_mfma_f32_32x32x16_bf16;
+//   * rows are 192 B apart, so the four rows of a transposed read and the two
+//     16-lane groups of a half-wave hit 8 distinct 8-bank windows;
+//   * double-buffered LDS stages, the next chunk's global loads in flight
+//     during the current chunk's MFMAs, one barrier per chunk;
+//   * pixel splits write fp32 slabs [z][tap][ci][co] summed by slab_reduce
+//     (deterministic); the split count keeps the slabs near 38 MB.
+// ResNet-18 at B = 32, the 13 such layers: 489 us per step vs 658 us for the
+// generic wgrad kernels above (scripts/wgrad3_lab.py).
+namespace w3 {
+constexpr int LD = 96;  // bf16 per LDS pixel row (192 B)
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+
+// chunk geometry: NPX output pixels (TR whole rows of one image) per chunk;
+// 128-pixel chunks for W >= 28 (twice the MFMAs per staging round trip and
+// 2 / 3 of the halo re-reads), 64 below (a 7 x 7 image is one 49-pixel chunk)
+template <int NPX>
+struct Cfg {
+  static constexpr int MAXH = NPX == 128 ? 264 : 200;  // halo pixels (W = 64: 4 x 66 / 3 x 66)
+  static constexpr int STG = (MAXH + NPX) * LD;
+  static constexpr int XR = (MAXH * 8 + NT - 1) / NT;  // 16-byte halo pieces per thread
+  static constexpr int YR = NPX * 8 / NT;              // 16-byte dY pieces per thread
+  static constexpr int KS = NPX / 16;                  // MFMA k-steps per chunk
+};
+
+__device__ __forceinline__ v4s tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
+}
+
+__device__ __forceinline__ bfx8 frag(const __bf16* p0, const __bf16* p1) {
+  const v8s v = __builtin_shufflevector(tr_read(p0), tr_read(p1), 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bfx8, v);
+}
+
+__host__ __device__ __forceinline__ int rows_per_chunk(const ConvShape& s, int npx) {
+  const int tr = npx / s.W;
+  return tr < s.H ? tr : s.H;
+}
+
+__host__ __device__ __forceinline__ int chunk_pixels(const ConvShape& s) {
+  return s.W >= 28 ? 128 : 64;
+}
+}  // namespace w3
+
+// Global -> register prefetch of one chunk (halo + dY tile), and the
+// register -> LDS store of it (plain functions: the arrays must stay in VGPRs)
+template <int NPX>
+struct W3Regs {
+  uint4 rx[w3::Cfg<NPX>::XR], ry[w3::Cfg<NPX>::YR];
+};
+
+template <int NPX>
+__device__ __forceinline__ void w3_load(W3Regs<NPX>& R, const ConvShape& s, const __bf16* x,
+                                        const __bf16* dy, int ch, int rpi, int TR, int HW2,
+                                        int hpx, int ci0, int co0) {
+  using CF = w3::Cfg<NPX>;
+  const int tid = threadIdx.x, H = s.H, W = s.W;
+  const int n = ch / rpi, r0 = (ch - n * rpi) * TR, nvalid = min(TR, H - r0) * W;
+#pragma unroll
+  for (int i = 0; i < CF::XR; ++i) {
+    const int e = tid + NT * i, hp = e >> 3, c8 = e & 7;
+    const int hy = hp / HW2, hx = hp - hy * HW2, y = r0 + hy - 1, xx = hx - 1;
+    const bool ok = hp < hpx && y >= 0 && y < H && xx >= 0 && xx < W;
+    const int yc = min(max(y, 0), H - 1), xc = min(max(xx, 0), W - 1);
+    const uint4 v =
+        *reinterpret_cast<const uint4*>(x + (((size_t)n * H + yc) * W + xc) * s.C + ci0 + 8 * c8);
+    R.rx[i] = sel(ok, v);
+  }
+#pragma unroll
+  for (int i = 0; i < CF::YR; ++i) {
+    const int e = tid + NT * i, p = e >> 3, c8 = e & 7;
+    const bool ok = p < nvalid;
+    const int pc = min(p, nvalid - 1), py = pc / W, px = pc - py * W;
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        dy + (((size_t)n * H + r0 + py) * W + px) * s.K + co0 + 8 * c8);
+    R.ry[i] = sel(ok, v);
+  }
+}
+
+template <int NPX>
+__device__ __forceinline__ void w3_store(const W3Regs<NPX>& R, __bf16* Xs, __bf16* Ys, int hpx) {
+  using CF = w3::Cfg<NPX>;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < CF::XR; ++i) {
+    const int e = tid + NT * i, hp = e >> 3;
+    if (hp < hpx) *reinterpret_cast<uint4*>(Xs + hp * w3::LD + 8 * (e & 7)) = R.rx[i];
+  }
+#pragma unroll
+  for (int i = 0; i < CF::YR; ++i) {
+    const int e = tid + NT * i;
+    *reinterpret_cast<uint4*>(Ys + (e >> 3) * w3::LD + 8 * (e & 7)) = R.ry[i];
+  }
+}
+
+template <int NPX>
+__global__ __launch_bounds__(NT) void wgrad3_kernel(ConvShape s, const __bf16* __restrict__ x,
+                                                    const __bf16* __restrict__ dy,
+                                                    float* __restrict__ out, int cps) {
+  using CF = w3::Cfg<NPX>;
+  using w3::LD;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[2 * CF::STG];
+  const int C = s.C, K = s.K, H = s.H, W = s.W;
+  const int TR = w3::rows_per_chunk(s, NPX), HW2 = W + 2, hpx = (TR + 2) * HW2;
+  const int cpairs = C / 64, pairs = cpairs * (K / 64);
+  const int pair = blockIdx.x % pairs, z = blockIdx.x / pairs;
+  const int ci0 = (pair % cpairs) * 64, co0 = (pair / cpairs) * 64;
+  const int rpi = (H + TR - 1) / TR, nchunks = s.N * rpi;
+  const int c_begin = z * cps, c_end = min(nchunks, c_begin + cps);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+
+  // per-lane transposed-read offsets (chunk invariant): lane 4q + p of its
+  // 16-lane group G supplies pixel row q of the 4-pixel block, channels
+  // 4p .. 4p + 3 of the group's 16; 8 pixels per lane = 2 reads per k-step
+  const int G = lane >> 4, q = (lane >> 2) & 3, p4 = lane & 3;
+  const int csub = 16 * (G & 1) + 4 * p4, kb = 8 * (G >> 1);
+  int aoff[CF::KS][2], boff[CF::KS][2];
+#pragma unroll
+  for (int ks = 0; ks < CF::KS; ++ks)
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int pix = 16 * ks + kb + 4 * r + q;
+      const int pa = min(pix, TR * W - 1), pr = pa / W, pc = pa - pr * W;  // padded pixels: dY = 0
+      aoff[ks][r] = (pr * HW2 + pc) * LD + wm * 32 + csub;
+      boff[ks][r] = pix * LD + wn * 32 + csub;
+    }
+  int toff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) toff[t] = ((t / 3) * HW2 + (t % 3)) * LD;
+
+  f32x16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = zero16();
+  if (c_begin < c_end) {
+    W3Regs<NPX> R;
+    w3_load<NPX>(R, s, x, dy, c_begin, rpi, TR, HW2, hpx, ci0, co0);
+    w3_store<NPX>(R, smem, smem + CF::MAXH * LD, hpx);
+    __syncthreads();
+    for (int ch = c_begin; ch < c_end; ++ch) {
+      const int stage = (ch - c_begin) & 1;
+      const bool more = ch + 1 < c_end;
+      if (more) w3_load<NPX>(R, s, x, dy, ch + 1, rpi, TR, HW2, hpx, ci0, co0);
+      // the next chunk's global loads are issued here, ahead of this chunk's
+      // MFMAs (the scheduler would otherwise sink them to their LDS stores)
+      __builtin_amdgcn_sched_barrier(0);
+      const __bf16* Xs = smem + stage * CF::STG;
+      {
+      const __bf16* Ys = Xs + CF::MAXH * LD;
+      // fragments of k-step ks + 1 are read while the 9 MFMAs of ks run (one
+      // wave per SIMD: nothing else hides the LDS latency)
+      bfx8 fb[2], fa[2][9];
+      fb[0] = w3::frag(Ys + boff[0][0], Ys + boff[0][1]);
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+        fa[0][t] = w3::frag(Xs + aoff[0][0] + toff[t], Xs + aoff[0][1] + toff[t]);
+#pragma unroll
+      for (int ks = 0; ks < CF::KS; ++ks) {
+        const int cur = ks & 1, nx = cur ^ 1;
+        if (ks + 1 < CF::KS) {
+          fb[nx] = w3::frag(Ys + boff[ks + 1][0], Ys + boff[ks + 1][1]);
+#pragma unroll
+          for (int t = 0; t < 9; ++t)
+            fa[nx][t] = w3::frag(Xs + aoff[ks + 1][0] + toff[t], Xs + aoff[ks + 1][1] + toff[t]);
+        }
+        // keep the next k-step's 20 reads ahead of this k-step's MFMAs (the
+        // scheduler otherwise sinks each read next to its MFMA and every
+        // MFMA then waits out a full LDS latency)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][t], fb[cur], acc[t], 0, 0, 0);
+      }
+      }
+      if (more) {
+        __bf16* nx = smem + (stage ^ 1) * CF::STG;
+        w3_store<NPX>(R, nx, nx + CF::MAXH * LD, hpx);
+      }
+      __syncthreads();
+    }
+  }
+  // slab store, one tap at a time through LDS so every lane writes 16-byte
+  // vectors (4 consecutive co): [64 ci][64 co] fp32 tile per tap, row pitch 68
+  float* o = out + (size_t)z * 9 * C * K;
+  float* tile = reinterpret_cast<float*>(smem);
+  const int col = wn * 32 + (lane & 31);
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    __syncthreads();
+#pragma unroll
+    for (int qq = 0; qq < 16; ++qq) tile[(wm * 32 + mfma32_row(qq, lane)) * 68 + col] = acc[t][qq];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // 64 rows x 16 float4 = 1024 vectors, 4 per thread
+      const int e = tid + NT * k, row = e >> 4, c4 = (e & 15) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(tile + row * 68 + c4);
+      *reinterpret_cast<float4*>(o + ((size_t)t * C + ci0 + row) * K + co0 + c4) = v;
+    }
+  }
+}
+
+static bool wgrad3_ok(const ConvShape& s) {
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.OH == s.H && s.OW == s.W))
+    return false;
+  const int npx = w3::chunk_pixels(s);
+  if (s.C % 64 || s.K % 64 || s.W > npx) return false;
+  const int tr = w3::rows_per_chunk(s, npx);
+  return (tr + 2) * (s.W + 2) <= (npx == 128 ? w3::Cfg<128>::MAXH : w3::Cfg<64>::MAXH);
+}
+
+static int wgrad3_chunks(const ConvShape& s) {
+  const int tr = w3::rows_per_chunk(s, w3::chunk_pixels(s));
+  return s.N * ((s.H + tr - 1) / tr);
+}
+
+// pixel splits: slabs of ~38 MB in total, >= 1 chunk per split.  Measured at
+// B = 32 (scripts/wgrad3_lab.py): the slab writes + their reduction cost ~15 us
+// per call at 19 MB, but halving the splits to that leaves the per-block
+// chunk chains (load -> 9 x 4 MFMAs -> barrier) too long: 607 vs 489 us per
+// step for the 13 layers; 76 MB: 681 us.
+static int wgrad3_splits(const ConvShape& s) {
+  const int nchunks = wgrad3_chunks(s);
+  const long long budget = 9437184LL;
+  long long z = (budget + 9LL * s.C * s.K - 1) / (9LL * s.C * s.K);
+  z = std::max(1LL, std::min(z, (long long)nchunks));
+  const int cps = (int)((nchunks + z - 1) / z);
+  return (nchunks + cps - 1) / cps;
+}
+
+static void wgrad3(const ConvShape& s, const __bf16* xb, const __bf16* dyb, float* ws, float* dw,
+                   hipStream_t st) {
+  const int nchunks = wgrad3_chunks(s);
+  const int z = wgrad3_splits(s);
+  const int cps = (nchunks + z - 1) / z;
+  const int blocks = (s.C / 64) * (s.K / 64) * z;
+  if (z > 1 && !ws) throw std::runtime_error("wgrad3: split-K needs a workspace");
+  float* out = z > 1 ? ws : dw;
+  if (w3::chunk_pixels(s) == 128)
+    wgrad3_kernel<128><<<blocks, NT, 0, st>>>(s, xb, dyb, out, cps);
+  else
+    wgrad3_kernel<64><<<blocks, NT, 0, st>>>(s, xb, dyb, out, cps);
+  if (z > 1) slab_reduce(ws, z, 9LL * s.C * s.K / 4, dw, st);
+}
+
 }  // namespace cbf
 
 bool conv_fwd_bf16_ok(const ConvShape& s) { return s.C % 64 == 0 && s.K % 64 == 0; }
@@ -599,6 +860,7 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
     const WgPlan p = wg_plan(s);
     if (p.z > 1) n = std::max(n, (long long)p.z * s.R * s.S * s.C * s.K);
   }
+  if (wgrad3_ok(s)) n = std::max(n, (long long)wgrad3_splits(s) * 9 * s.C * s.K);
   return n;
 }
 
@@ -680,6 +942,9 @@ void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, f
                           float* dw, hipStream_t st, const void* xb, const void* dyb) {
   using namespace cbf;
   if (!conv_bwd_filter_bf16_ok(s)) throw std::runtime_error("conv_bwd_filter_bf16: unsupported shape");
+  if (xb && dyb && wgrad3_ok(s))
+    return wgrad3(s, reinterpret_cast<const __bf16*>(xb), reinterpret_cast<const __bf16*>(dyb), ws,
+                  dw, st);
   const WgPlan p = wg_plan(s);
   if (p.z > 1 && !ws) throw std::runtime_error("conv_bwd_filter_bf16: split-K needs a workspace");
   float* out = p.z > 1 ? ws : dw;

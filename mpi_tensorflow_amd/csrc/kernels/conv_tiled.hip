@@ -154,7 +154,7 @@ __device__ __forceinline__ void mainloop(L& ld, float* smem, int k0, int nk,
 }
 
 __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
-  return ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+  return sel(ok, v);
 }
 
 // ------------------------------------------------------------- forward ----

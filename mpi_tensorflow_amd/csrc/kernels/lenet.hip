@@ -548,7 +548,7 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
         for (int u = 0; u < 8; ++u) {
           const float dv = sd[n * 128 + c0 + 16 * u];
           acc[u] = fmaf(av, dv, acc[u]);
-          bacc[u] += dv;
+          if (tile == 0) bacc[u] += dv;  // block-uniform: the bias row
         }
       }
     }

@@ -217,6 +217,7 @@ def test_generic_bucketed_allreduce_overlap(cuda_dev):
     (4, 14, 14, 128, 256, 1, 2, 0),  # 1x1 stride-2 downsample
     (8, 28, 28, 128, 128, 3, 1, 1),  # 128x128 tiles
     (3, 11, 13, 64, 192, 3, 1, 1),  # ragged M, non-square image
+    (2, 14, 14, 256, 256, 3, 1, 1),  # layer3: all-taps wgrad, partial last row chunk
 ])
 def test_conv_bf16_mfma(cuda_dev, N, H, W, Cin, K, R, stride, pad):
     """bf16-operand MFMA convolutions (fp32 accumulate) vs fp32 torch: relative
@@ -338,3 +339,32 @@ def test_bn_bf16_twin_feeds_conv(cuda_dev):
         Fn.set_conv_bf16(False)
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
+
+
+def test_batchnorm_large_mean_channels(cuda_dev):
+    """Channels with mean ~1e3 and std ~1: the plain fp32 E[x^2] - mean^2
+    variance loses every digit (mean^2 / var ~ 1e6 ~ 2^20 of a 2^24 mantissa);
+    the shifted sums of bn.hip keep it within 1e-4 of an fp64 torch reference
+    (output, running statistics and input gradient)."""
+    g = torch.Generator().manual_seed(3)
+    C = 32
+    x = (torch.randn(8, 9, 11, C, generator=g, dtype=torch.float64) +
+         1e3 * (1 + torch.rand(C, generator=g, dtype=torch.float64)))
+    gam = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    bet = torch.randn(C, generator=g, dtype=torch.float64)
+    dy = torch.randn(8, 9, 11, C, generator=g, dtype=torch.float64)
+    xr = x.clone().requires_grad_(True)
+    rm_ref, rv_ref = torch.zeros(C, dtype=torch.float64), torch.ones(C, dtype=torch.float64)
+    yr = F.batch_norm(xr.permute(0, 3, 1, 2), rm_ref, rv_ref, gam, bet, True, 0.1,
+                      1e-5).permute(0, 2, 3, 1)
+    yr.backward(dy)
+    xg = x.float().to(cuda_dev).requires_grad_(True)
+    gp, bp = _param(gam.float().to(cuda_dev)), _param(bet.float().to(cuda_dev))
+    rm, rv = torch.zeros(C, device=cuda_dev), torch.ones(C, device=cuda_dev)
+    yg = Fn.batchnorm(xg, gp, bp, rm, rv, True, False, None)
+    yg.backward(dy.float().to(cuda_dev))
+    torch.cuda.synchronize()
+    assert _rel(yg.cpu().double(), yr.detach()) < 1e-4
+    assert _rel(rv.cpu().double(), rv_ref) < 1e-4
+    assert _rel(rm.cpu().double(), rm_ref) < 1e-6
+    assert _rel(xg.grad.cpu().double(), xr.grad) < 1e-3
