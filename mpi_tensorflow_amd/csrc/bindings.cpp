@@ -186,8 +186,8 @@ PYBIND11_MODULE(_C, m) {
         return p;
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
-  g.def("set_conv_variant", &gops::set_conv_variant, py::arg("slot"), py::arg("value"));
   g.def("conv_bf16_ok", &gops::conv_fwd_bf16_ok);
+  g.def("conv_bwd_data_join_ok", &gops::conv_bwd_data_join_ok);
   g.def("im2col_bf16", [](const gops::ConvShape& s, uintptr_t x, int kp, uintptr_t col,
                           uintptr_t st) {
     gops::im2col_bf16(s, P<const float>(x), kp, P<void>(col), S(st));
@@ -205,12 +205,12 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
      py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
-                            uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb) {
+                            uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend) {
     gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st),
-                        bf16, P<const void>(dyb));
+                        bf16, P<const void>(dyb), P<const float>(addend));
     check_launch();
   }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
-     py::arg("bf16") = false, py::arg("dyb") = 0);
+     py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0);
   g.def("conv_ws_floats", &gops::conv_ws_floats);
   g.def("conv_filter_splits", &gops::conv_filter_splits);
   g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,
@@ -265,6 +265,24 @@ PYBIND11_MODULE(_C, m) {
                    uintptr_t dlogits, uintptr_t correct, uintptr_t st) {
     gops::xent(P<const float>(logits), P<const int>(labels), B, C, P<float>(loss_rows),
                P<float>(dlogits), P<int>(correct), S(st));
+    check_launch();
+  });
+  g.def("xent_mean", [](uintptr_t logits, uintptr_t labels, int B, int C, uintptr_t loss_rows,
+                        uintptr_t dlogits, uintptr_t mean, uintptr_t correct, uintptr_t st) {
+    gops::xent_mean(P<const float>(logits), P<const int>(labels), B, C, P<float>(loss_rows),
+                    P<float>(dlogits), P<float>(mean), P<int>(correct), S(st));
+    check_launch();
+  });
+  g.def("linear_fwd", [](uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y, int M, int K, int N,
+                         bool relu, uintptr_t st) {
+    gops::linear_fwd(P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), M, K, N,
+                     relu, S(st));
+    check_launch();
+  });
+  g.def("linear_bwd", [](uintptr_t x, uintptr_t w, uintptr_t y, uintptr_t dy, uintptr_t dw,
+                         uintptr_t db, uintptr_t dx, int M, int K, int N, bool relu, uintptr_t st) {
+    gops::linear_bwd(P<const float>(x), P<const float>(w), P<const float>(y), P<const float>(dy),
+                     P<float>(dw), P<float>(db), P<float>(dx), M, K, N, relu, S(st));
     check_launch();
   });
   g.def("relu_bwd", [](uintptr_t dy, uintptr_t y, uintptr_t dx, long long n, uintptr_t st) {

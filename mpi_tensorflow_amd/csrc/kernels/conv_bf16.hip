@@ -30,11 +30,6 @@
 #include "ops_generic.h"
 
 namespace gops {
-int g_conv_variant[4] = {0, 0, 0, 0};
-void set_conv_variant(int slot, int v) {
-  if (slot < 0 || slot >= 4) throw std::runtime_error("set_conv_variant: slot out of range");
-  g_conv_variant[slot] = v;
-}
 namespace cbf {
 
 constexpr int BK = 64;       // channels per K tile
@@ -179,7 +174,8 @@ template <int BM, int BN, class XT>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restrict__ x,
                                                  const __bf16* __restrict__ wt,
                                                  const float* __restrict__ bias,
-                                                 float* __restrict__ y, int relu, int kps) {
+                                                 float* __restrict__ y, int relu, int kps,
+                                                 const float* __restrict__ addend) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int STAGE = (BM + BN) * LDK;  // bf16 elements
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
@@ -239,6 +235,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
         if (m >= M) continue;
         float v = acc[i][j][q] + bv;
         if (relu) v = fmaxf(v, 0.f);
+        if (addend) v += addend[(size_t)m * s.K + co];  // gradient junction (dX accumulate)
         y[(size_t)m * s.K + co] = v;
       }
   }
@@ -416,12 +413,20 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(
 
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
                                                         long long zs, long long n4,
-                                                        float4* __restrict__ out) {
+                                                        float4* __restrict__ out,
+                                                        const float4* __restrict__ addend) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
     for (int z = 1; z < nz; ++z) {
       const float4 b = part[z * zs + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    if (addend) {
+      const float4 b = addend[i];
       a.x += b.x;
       a.y += b.y;
       a.z += b.z;
@@ -456,7 +461,8 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 
 // Deterministic sum of nz slabs of n4 float4s into out (fixed association
 // order for a given nz).
-static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st) {
+static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st,
+                        const float* addend = nullptr) {
   long long b = (n4 + 255) / 256;
   if (b > 4096) b = 4096;
   int G = 1;
@@ -466,7 +472,8 @@ static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStrea
                                                                  nz, G, n4);
   }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), cdiv(nz, G),
-                                          n4 * G, n4, reinterpret_cast<float4*>(out));
+                                          n4 * G, n4, reinterpret_cast<float4*>(out),
+                                          reinterpret_cast<const float4*>(addend));
 }
 
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
@@ -509,21 +516,23 @@ static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 1
 
 template <class XT>
 static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const float* bias,
-                   float* y, bool relu, float* ws, hipStream_t st) {
+                   float* y, bool relu, float* ws, hipStream_t st,
+                   const float* addend = nullptr) {
   const long long M = (long long)s.N * s.OH * s.OW;
   const Plan p = plan(s, bias != nullptr || relu);
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
+  const float* add = p.z > 1 ? nullptr : addend;  // split-K: added by the slab reduction
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
-    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
   }
 #undef GRID
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend);
 }
 
 // wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
@@ -532,19 +541,17 @@ struct WgPlan {
   int bm, bn, z, kchunk;
 };
 static inline WgPlan wg_plan(const ConvShape& s) {
-  // A/B knobs (set_conv_variant): slot 0 = 1 folds two taps of a 64-channel
-  // layer into one 128-row tile; slot 1 = target block count (cap 128 slices)
-  const int bm = (s.C % 128 == 0 || g_conv_variant[0] == 1) ? 128 : 64;
+  const int bm = s.C % 128 == 0 ? 128 : 64;
   const int bn = s.K % 128 == 0 ? 128 : 64;
   const long long tiles = (long long)cdiv((long long)s.R * s.S * s.C, bm) * (s.K / bn);
   const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
-  const int target = g_conv_variant[1] > 0 ? g_conv_variant[1] : 1024;
+  const int target = 1024;
   int z = cdiv(target, tiles);
   if (z > ktiles / 4) z = ktiles / 4;
   // <= 4 output tiles (the im2col'd stem: 192 x 64) need deep pixel splits to
   // fill the chip; otherwise 64 slices (measured: more slices cost more slab
   // traffic than they win on ResNet-18 layer1)
-  const int zcap = g_conv_variant[1] > 0 ? 128 : (tiles <= 4 ? 256 : 64);
+  const int zcap = tiles <= 4 ? 256 : 64;
   if (z > zcap) z = zcap;
   if (z < 1) z = 1;
   const int kchunk = cdiv(ktiles, z);
@@ -927,15 +934,16 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
 }
 
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st, const void* dyb) {
+                        hipStream_t st, const void* dyb, const float* addend) {
   using namespace cbf;
   if (!conv_bwd_data_bf16_ok(s) || !ws) throw std::runtime_error("conv_bwd_data_bf16: unsupported shape");
   __bf16* wt = reinterpret_cast<__bf16*>(ws);
   convert(s, w, 1, wt, st);
   if (dyb)
-    launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st);
+    launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st,
+           addend);
   else
-    launch(dgrad_shape(s), dy, wt, nullptr, dx, false, ws, st);
+    launch(dgrad_shape(s), dy, wt, nullptr, dx, false, ws, st, addend);
 }
 
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,

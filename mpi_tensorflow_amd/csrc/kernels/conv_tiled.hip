@@ -335,7 +335,10 @@ struct DataLoader {
 template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __restrict__ dy,
                                                   const float* __restrict__ w,
-                                                  float* __restrict__ dx, int kps) {
+                                                  float* __restrict__ dx, int kps,
+                                                  const float* __restrict__ addend) {
+  // addend (unsplit only): a gradient that joins dX at this tensor, added in
+  // the epilogue instead of by a separate elementwise pass
   // split-K over gridDim.z: slice z writes the raw slab dx + z * N*H*W*C
   using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
@@ -370,7 +373,10 @@ __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __re
         if (m >= M) continue;
         const int jx = m % PW, t = m / PW, jy = t % PH, n = t / PH;
         const int iy = jy * sd + py, ix = jx * sd + px;
-        if (iy < s.H && ix < s.W) dx[(((size_t)n * s.H + iy) * s.W + ix) * s.C + ci] = acc[i][j][r];
+        if (iy < s.H && ix < s.W) {
+          const size_t o = (((size_t)n * s.H + iy) * s.W + ix) * s.C + ci;
+          dx[o] = addend ? acc[i][j][r] + addend[o] : acc[i][j][r];
+        }
       }
   }
 }
@@ -632,12 +638,20 @@ __global__ __launch_bounds__(256) void slab_sum4_deep_kernel(const float4* __res
 
 // Deterministic slab reduction, float4-vectorised (n % 4 == 0).
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
-                                                        long long n4, float4* __restrict__ out) {
+                                                        long long n4, float4* __restrict__ out,
+                                                        const float4* __restrict__ addend) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
     for (int z = 1; z < nz; ++z) {
       const float4 b = part[z * n4 + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    if (addend) {
+      const float4 b = addend[i];
       a.x += b.x;
       a.y += b.y;
       a.z += b.z;
@@ -711,16 +725,18 @@ static inline void data_plan(const ConvShape& s, Tile& t, int& z, int& kps) {
   z = ksplit((long long)cdiv(Mph, tile_m(t)) * cdiv(s.C, tile_n(t)) * sd * sd, nk);
   kps = cdiv(nk, z);
 }
-static inline void slab_sum(const float* part, int z, long long n, float* out, hipStream_t st) {
+static inline void slab_sum(const float* part, int z, long long n, float* out, hipStream_t st,
+                            const float* addend = nullptr) {
   long long b = (n / 4 + 255) / 256;
   if (b > 4096) b = 4096;
-  if (b < 64 && z >= 16) {  // deep, narrow stack: spread the slices over the block
+  if (b < 64 && z >= 16 && !addend) {  // deep, narrow stack: spread the slices over the block
     slab_sum4_deep_kernel<<<cdiv(n / 4, 64), 256, 0, st>>>(reinterpret_cast<const float4*>(part),
                                                             z, n / 4, reinterpret_cast<float4*>(out));
     return;
   }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(part), z, n / 4,
-                                          reinterpret_cast<float4*>(out));
+                                          reinterpret_cast<float4*>(out),
+                                          reinterpret_cast<const float4*>(addend));
 }
 }  // namespace tiled
 
@@ -754,7 +770,7 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st, bool bf16) {
+                         hipStream_t st, bool bf16, const float* addend) {
   using namespace tiled;
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
@@ -766,9 +782,9 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
   // phases no tap reaches (odd pixels of a 1x1 stride-2 conv) run zero K
   // tiles and write zeros
 #define GRID(BM_, BN_) dim3(cdiv(Mph, BM_) * cdiv(s.C, BN_), sd * sd, z)
-  TILED_DISPATCH(t, data_kernel, GRID, s, dy, w, out, kps)
+  TILED_DISPATCH(t, data_kernel, GRID, s, dy, w, out, kps, z > 1 ? nullptr : addend)
 #undef GRID
-  if (z > 1) slab_sum(ws, z, (long long)s.N * s.H * s.W * s.C, dx, st);
+  if (z > 1) slab_sum(ws, z, (long long)s.N * s.H * s.W * s.C, dx, st, addend);
 }
 
 namespace tiled {

@@ -23,8 +23,12 @@ struct PoolShape {
 // xb / dyb: optional bf16 copies of x / dy (to_bf16) for the bf16 family
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
               bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr);
+// addend (optional, bf16 / tiled families): a gradient that joins dX at this
+// tensor (a residual branch), added in the epilogue: dx = conv + addend
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                   hipStream_t st, bool bf16 = false, const void* dyb = nullptr);
+                   hipStream_t st, bool bf16 = false, const void* dyb = nullptr,
+                   const float* addend = nullptr);
+bool conv_bwd_data_join_ok(const ConvShape& s, bool bf16);  // takes an addend
 int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
                      hipStream_t st, bool bf16 = false, const void* xb = nullptr,
@@ -34,7 +38,6 @@ long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue);
 // (conv_bf16.hip): forward for C, K % 64 == 0, stride-1 backward-data; the
 // bf16 weight copy and split-K slabs live in the layer workspace
 bool conv_fwd_bf16_ok(const ConvShape& s);
-void set_conv_variant(int slot, int v);  // tiling A/B knobs (scripts/conv_lab.py)
 bool conv_bwd_data_bf16_ok(const ConvShape& s);
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
 void to_bf16(const float* x, void* y, long long n, hipStream_t st);
@@ -42,7 +45,7 @@ void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStrea
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st, const void* dyb = nullptr);
+                        hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr);
 bool conv_bwd_filter_bf16_ok(const ConvShape& s);
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
                           float* dw, hipStream_t st, const void* xb = nullptr,
@@ -55,7 +58,7 @@ bool conv_bwd_filter_tiled_ok(const ConvShape& s);
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                     bool relu, float* ws, hipStream_t st, bool bf16);
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st, bool bf16);
+                         hipStream_t st, bool bf16, const float* addend = nullptr);
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
 int conv_filter_tiled_splits(const ConvShape& s);
@@ -91,6 +94,14 @@ void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t s
 void xent(const float* logits, const int* labels, int B, int C, float* loss_rows, float* dlogits,
           int* correct, hipStream_t st);
 void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st);
+// one-workgroup softmax xent with the mean loss (B rows of C classes)
+void xent_mean(const float* logits, const int* labels, int B, int C, float* loss_rows,
+               float* dlogits, float* mean, int* correct, hipStream_t st);
+// small FC layers: y = x W (+ b) (+ ReLU); backward dW, db, dX (dX optional)
+void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int N,
+                bool relu, hipStream_t st);
+void linear_bwd(const float* x, const float* w, const float* y, const float* dy, float* dw,
+                float* db, float* dx, int M, int K, int N, bool relu, hipStream_t st);
 void lr_from_step(const long long* step, int n_local, int batch, float base, float decay,
                   float* lr, hipStream_t st);
 void gather_batch(const float* data, const int* labels, const long long* step, int n_local,

@@ -487,6 +487,112 @@ __global__ __launch_bounds__(256) void xent_kernel(const float* __restrict__ log
   }
 }
 
+// mean softmax cross-entropy of B rows in ONE workgroup (B <= a few
+// thousand): wave w takes rows w, w + 4, ...; writes loss_rows, dlogits =
+// (p - onehot) / B, the mean loss (fixed summation order) and optionally the
+// argmax hit count.  Replaces xent + torch's mean + the copy into the
+// engine's loss scalar (3 launches, two of them ATen).
+__global__ __launch_bounds__(256) void xent_mean_kernel(const float* __restrict__ logits,
+                                                        const int* __restrict__ labels, int B,
+                                                        int C, float* __restrict__ loss_rows,
+                                                        float* __restrict__ dlogits,
+                                                        float* __restrict__ mean_out,
+                                                        int* __restrict__ correct) {
+  __shared__ float part[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int row = w; row < B; row += 4) {
+    const int lab = labels[row];
+    const float* lg = logits + (size_t)row * C;
+    float mx = -INFINITY;
+    for (int c = lane; c < C; c += 64) mx = fmaxf(mx, lg[c]);
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int c = lane; c < C; c += 64) se += __expf(lg[c] - mx);
+    se = wave_sum(se);
+    int am = C;
+    for (int c = lane; c < C; c += 64)
+      if (lg[c] == mx) am = min(am, c);
+    for (int o = 32; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 64));
+    for (int c = lane; c < C; c += 64)
+      dlogits[(size_t)row * C + c] = (__expf(lg[c] - mx) / se - (c == lab ? 1.f : 0.f)) / (float)B;
+    const float l = logf(se) + mx - lg[lab];
+    if (lane == 0) {
+      loss_rows[row] = l;
+      if (correct && am == lab) atomicAdd(correct, 1);
+    }
+    acc += l;
+  }
+  if (lane == 0) part[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) mean_out[0] = (part[0] + part[1] + part[2] + part[3]) / (float)B;
+}
+
+// Small fully connected layers (LeNet-5's 400-120-84-10 at batch 64, the
+// ResNet-18 512 -> 10 head at batch 32-128): far below MFMA tile sizes, so
+// plain VALU dot products with one output per thread; deterministic.
+// forward: y[m][n] = b[n] + sum_k x[m][k] W[k][n] (+ ReLU)
+__global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict__ x,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ b,
+                                                         float* __restrict__ y, int M, int K,
+                                                         int N, int relu) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= M * N) return;
+  const int m = i / N, n = i - m * N;
+  const float* xr = x + (size_t)m * K;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 4 <= K; k += 4) {
+    s0 = fmaf(xr[k], w[(size_t)k * N + n], s0);
+    s1 = fmaf(xr[k + 1], w[(size_t)(k + 1) * N + n], s1);
+    s2 = fmaf(xr[k + 2], w[(size_t)(k + 2) * N + n], s2);
+    s3 = fmaf(xr[k + 3], w[(size_t)(k + 3) * N + n], s3);
+  }
+  for (; k < K; ++k) s0 = fmaf(xr[k], w[(size_t)k * N + n], s0);
+  float v = (b ? b[n] : 0.f) + ((s0 + s1) + (s2 + s3));
+  if (relu) v = fmaxf(v, 0.f);
+  y[i] = v;
+}
+
+// backward, three block roles in one launch: dW[k][n] = sum_m x[m][k] dy'[m][n],
+// db[n] = sum_m dy'[m][n], dX[m][k] = sum_n dy'[m][n] W[k][n], with dy' = dy
+// masked by ReLU (y > 0) when the forward fused it
+__global__ __launch_bounds__(256) void linear_bwd_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ y,
+    const float* __restrict__ dy, float* __restrict__ dw, float* __restrict__ db,
+    float* __restrict__ dx, int M, int K, int N, int relu, int bw, int bb) {
+  const int blk = blockIdx.x;
+  auto g = [&](int m, int n) {
+    const float d = dy[(size_t)m * N + n];
+    return (relu && y[(size_t)m * N + n] <= 0.f) ? 0.f : d;
+  };
+  if (blk < bw) {  // dW
+    const int i = blk * 256 + threadIdx.x;
+    if (i >= K * N) return;
+    const int k = i / N, n = i - k * N;
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s = fmaf(x[(size_t)m * K + k], g(m, n), s);
+    dw[i] = s;
+    return;
+  }
+  if (blk < bw + bb) {  // db
+    const int n = (blk - bw) * 256 + threadIdx.x;
+    if (n >= N || !db) return;
+    float s = 0.f;
+    for (int m = 0; m < M; ++m) s += g(m, n);
+    db[n] = s;
+    return;
+  }
+  if (!dx) return;  // dX
+  const int i = (blk - bw - bb) * 256 + threadIdx.x;
+  if (i >= M * K) return;
+  const int m = i / K, k = i - m * K;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n) s = fmaf(g(m, n), w[(size_t)k * N + n], s);
+  dx[i] = s;
+}
+
 // batch gather from a device-resident dataset at the device-step offset
 __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ data,
                                                            const int* __restrict__ labels,
@@ -674,10 +780,16 @@ static void gather_data_plan(const ConvShape& s, int& z, int& kchunk) {
   z = (ktiles * BK + kchunk - 1) / kchunk;
 }
 
+bool conv_bwd_data_join_ok(const ConvShape& s, bool bf16) {
+  return (bf16 && conv_bwd_data_bf16_ok(s)) || conv_bwd_data_tiled_ok(s);
+}
+
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                   hipStream_t st, bool bf16, const void* dyb) {
-  if (bf16 && conv_bwd_data_bf16_ok(s)) return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb);
-  if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16);
+                   hipStream_t st, bool bf16, const void* dyb, const float* addend) {
+  if (bf16 && conv_bwd_data_bf16_ok(s))
+    return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb, addend);
+  if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend);
+  if (addend) throw std::runtime_error("conv_bwd_data: no gradient-join epilogue for this shape");
   if (s.C < 32 && (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX && (s.K == 8 || s.K == 16)) {
     const int b = grid1d((long long)s.N * s.H * s.W * s.C);
     if (s.K == 8)
@@ -797,6 +909,23 @@ void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t s
 void xent(const float* logits, const int* labels, int B, int C, float* loss_rows, float* dlogits,
           int* correct, hipStream_t st) {
   xent_kernel<<<(B + 3) / 4, 256, 0, st>>>(logits, labels, B, C, loss_rows, dlogits, correct);
+}
+
+void xent_mean(const float* logits, const int* labels, int B, int C, float* loss_rows,
+               float* dlogits, float* mean, int* correct, hipStream_t st) {
+  xent_mean_kernel<<<1, 256, 0, st>>>(logits, labels, B, C, loss_rows, dlogits, mean, correct);
+}
+
+void linear_fwd(const float* x, const float* w, const float* b, float* y, int M, int K, int N,
+                bool relu, hipStream_t st) {
+  linear_fwd_kernel<<<(M * N + 255) / 256, 256, 0, st>>>(x, w, b, y, M, K, N, relu ? 1 : 0);
+}
+
+void linear_bwd(const float* x, const float* w, const float* y, const float* dy, float* dw,
+                float* db, float* dx, int M, int K, int N, bool relu, hipStream_t st) {
+  const int bw = (K * N + 255) / 256, bb = (N + 255) / 256, bx = dx ? (M * K + 255) / 256 : 0;
+  linear_bwd_kernel<<<bw + bb + bx, 256, 0, st>>>(x, w, y, dy, dw, db, dx, M, K, N, relu ? 1 : 0,
+                                                  bw, bb);
 }
 
 void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st) {

@@ -161,21 +161,28 @@ class ResNet18(GenericModel):
         return d
 
     def forward(self, P, bn, x, training):
-        def BN(h, nm, relu, res=None):
+        def BN(h, nm, relu, res=None, res_join=None):
             rm, rv = bn[nm]
-            return Fn.batchnorm(h, P[nm + "_g"], P[nm + "_b"], rm, rv, training, relu, res)
+            return Fn.batchnorm(h, P[nm + "_g"], P[nm + "_b"], rm, rv, training, relu, res,
+                                res_join=res_join)
 
         h = Fn.conv2d(x, P["conv1_w"], None, 2, 3)
         h = BN(h, "bn1", True)
         h = Fn.maxpool(h, 3, 2, 1)
+        join = x.is_cuda and training and torch.is_grad_enabled()
         for name, cin, c, s, down in self._blocks():
-            o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1)
+            # the block input's two gradients (conv1, shortcut) meet in the
+            # conv1 dgrad epilogue (Fn.GradJoin); the shortcut runs after c2
+            # so its backward comes first
+            j = Fn.GradJoin() if join else None
+            o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final")
             o = BN(o, name + "n1", True)
             o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1)
-            sc = h
             if down:
-                sc = BN(Fn.conv2d(h, P[name + "ds_w"], None, s, 0), name + "nd", False)
-            h = BN(o, name + "n2", True, res=sc)
+                sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash")
+                h = BN(o, name + "n2", True, res=BN(sc, name + "nd", False))
+            else:
+                h = BN(o, name + "n2", True, res=h, res_join=j)
         h = Fn.global_avgpool(h)
         return Fn.linear(h, P["fc_w"], P["fc_b"])
 

@@ -109,10 +109,39 @@ def _bf16_out(like: torch.Tensor) -> Optional[torch.Tensor]:
     return torch.empty(like.shape, dtype=torch.bfloat16, device=like.device)
 
 
+# ------------------------------------------------------------ grad joins --
+class GradJoin:
+    """Fuses the gradient sum at a tensor read by two branches (a ResNet
+    block input: conv1 and the shortcut) into a conv dgrad epilogue instead
+    of autograd's separate add kernel.  The shortcut's backward `stash`es its
+    gradient here and hands autograd None; the conv1 dgrad (`final`) adds the
+    stash in its epilogue.  Autograd runs the shortcut first (it is created
+    later in the forward, so has the higher sequence number); should the
+    order ever flip, `stash` adds into the already-written dX in place, which
+    is still before the consumer of that gradient runs (it waits for both
+    edges)."""
+
+    __slots__ = ("g", "out")
+
+    def __init__(self):
+        self.g: Optional[torch.Tensor] = None
+        self.out: Optional[torch.Tensor] = None
+
+    def stash(self, grad: torch.Tensor) -> None:
+        if self.out is not None:
+            self.out.add_(grad)
+        else:
+            self.g = grad
+
+    def take(self) -> Optional[torch.Tensor]:
+        g, self.g = self.g, None
+        return g
+
+
 # ------------------------------------------------------------------- conv --
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, shape, relu, gw, gb, ws):
+    def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None):
         C = native()
         x = x.contiguous()
         y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
@@ -128,6 +157,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, y, xb)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
+        ctx.join, ctx.role = join, role
         return y
 
     @staticmethod
@@ -154,8 +184,15 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
-            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16, ptr(dyb))
-        return dx, None, None, None, None, None, None, None
+            add = ctx.join.take() if ctx.role == "final" else None
+            C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16, ptr(dyb),
+                                ptr(add))
+            if ctx.role == "stash":
+                ctx.join.stash(dx)
+                dx = None
+            elif ctx.role == "final" and add is None:
+                ctx.join.out = dx
+        return dx, None, None, None, None, None, None, None, None, None
 
 
 class _ConvIm2colFn(torch.autograd.Function):
@@ -245,8 +282,11 @@ _WS = ConvWorkspace()
 
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: int = 0,
-           relu: bool = False) -> torch.Tensor:
-    """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K]."""
+           relu: bool = False, join: Optional[GradJoin] = None,
+           join_role: Optional[str] = None) -> torch.Tensor:
+    """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K].  join / join_role
+    ("stash" | "final"): fuse the gradient sum at x with another branch (see
+    GradJoin); GPU only, ignored on the CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
     if x.is_cuda:
@@ -260,48 +300,47 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
         nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
                   C.ops.chan_reduce_ws_floats(N * sh.OH * sh.OW, K), 4)
         ws = _WS.get(nws, x.device)
+        if join is not None and join_role == "final" and not C.ops.conv_bwd_data_join_ok(sh,
+                                                                                         _CONV_BF16):
+            raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
-                             None if b is None else b.grad_view, ws)
+                             None if b is None else b.grad_view, ws, join, join_role)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y
 
 
 class _LinearFn(torch.autograd.Function):
-    """Fully connected layer on GPU as plain library GEMMs (rocBLAS via
-    torch.mm / addmm), gradients written straight into the flat-buffer
-    views.  The batch-sized FC GEMMs of LeNet-5 / the ResNet-18 head (M = 32..64
-    rows, K = 84..512) leave the conv kernels' tile machinery with one or two
-    blocks and a serial K chain (ResNet-18's 512 -> 10 head: 76 us forward on
-    the gather engine); the library GEMM splits them properly."""
+    """Fully connected layer on GPU through the in-tree VALU kernels
+    (ops_generic.hip linear_fwd / linear_bwd): the FC layers of these models
+    (LeNet-5 400-120-84-10 at batch 64, the ResNet-18 512 -> 10 head) are far
+    below MFMA tile sizes.  Bias + ReLU run in the forward epilogue; backward is
+    ONE launch (dW, db and dX block roles, ReLU mask applied on the fly) whose
+    gradients land straight in the flat-buffer views."""
 
     @staticmethod
     def forward(ctx, x, w, b, relu, gw, gb):
+        C = native()
         x = x.contiguous()
-        if relu and b is not None:  # bias + ReLU in the library GEMM's epilogue
-            y = torch._addmm_activation(b, x, w)
-        else:
-            y = torch.addmm(b, x, w) if b is not None else torch.mm(x, w)
-            if relu:
-                y = torch.relu_(y)
+        M, K = x.shape
+        N = w.shape[1]
+        y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        C.ops.linear_fwd(ptr(x), ptr(w), ptr(b), ptr(y), M, K, N, relu, stream_handle())
         ctx.save_for_backward(x, w, y if relu else None)
         ctx.relu, ctx.gw, ctx.gb = relu, gw, gb
-        ctx.has_b = b is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
+        C = native()
         x, w, y = ctx.saved_tensors
-        if ctx.relu:  # one native mask launch instead of compare + multiply
-            dy = dy.contiguous()
-            dym = torch.empty_like(dy)
-            native().ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), stream_handle())
-            dy = dym
-        torch.mm(x.t(), dy, out=ctx.gw)
-        if ctx.has_b:
-            torch.sum(dy, dim=0, out=ctx.gb)
-        _grad_done(ctx.gw, ctx.gb if ctx.has_b else None)
-        dx = torch.mm(dy, w.t()) if ctx.needs_input_grad[0] else None
+        dy = dy.contiguous()
+        M, K = x.shape
+        N = w.shape[1]
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        C.ops.linear_bwd(ptr(x), ptr(w), ptr(y), ptr(dy), ptr(ctx.gw), ptr(ctx.gb), ptr(dx), M, K,
+                         N, ctx.relu, stream_handle())
+        _grad_done(ctx.gw, ctx.gb)
         return dx, None, None, None, None, None
 
 
@@ -317,7 +356,8 @@ def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) ->
 # -------------------------------------------------------------- batchnorm --
 class _BNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, g, b, res, relu, gg, gb, rmean, rvar, momentum, eps, training):
+    def forward(ctx, x, g, b, res, relu, gg, gb, rmean, rvar, momentum, eps, training,
+                res_join=None):
         C = native()
         x = x.contiguous()
         Cc = x.shape[-1]
@@ -336,6 +376,7 @@ class _BNFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, mean, rstd, g)
         ctx.relu, ctx.gg, ctx.gb, ctx.has_res = relu, gg, gb, res is not None
         ctx.ws = ws
+        ctx.res_join = res_join
         return y
 
     @staticmethod
@@ -354,18 +395,24 @@ class _BNFn(torch.autograd.Function):
         if dxb is not None:
             _attach_bf16(dx, dxb)
         _grad_done(ctx.gg, ctx.gb)
-        return dx, None, None, dres, None, None, None, None, None, None, None, None
+        if dres is not None and ctx.res_join is not None:
+            ctx.res_join.stash(dres)
+            dres = None
+        return dx, None, None, dres, None, None, None, None, None, None, None, None, None
 
 
 def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: torch.Tensor,
               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None,
-              momentum: float = 0.1, eps: float = 1e-5) -> torch.Tensor:
-    """BatchNorm over N,H,W of an NHWC tensor, optional fused residual + ReLU."""
+              momentum: float = 0.1, eps: float = 1e-5,
+              res_join: Optional[GradJoin] = None) -> torch.Tensor:
+    """BatchNorm over N,H,W of an NHWC tensor, optional fused residual + ReLU.
+    res_join: the residual's gradient is stashed there (GradJoin) instead of
+    returned to autograd (GPU training only)."""
     if x.is_cuda:
         res = None if residual is None else residual.contiguous()
         if training:
             return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
-                               rvar, momentum, eps, True)
+                               rvar, momentum, eps, True, res_join)
         C = native()
         y = torch.empty_like(x)
         Cc = x.shape[-1]
@@ -438,6 +485,9 @@ def global_avgpool(x: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------- loss --
 class _XentFn(torch.autograd.Function):
+    """Mean softmax cross-entropy in one launch (xent_mean_kernel writes the
+    loss rows, dlogits and the mean) instead of xent + torch's mean."""
+
     @staticmethod
     def forward(ctx, logits, labels):
         C = native()
@@ -445,9 +495,11 @@ class _XentFn(torch.autograd.Function):
         B, K = logits.shape
         loss_rows = torch.empty(B, device=logits.device)
         dlog = torch.empty_like(logits)
-        C.ops.xent(ptr(logits), ptr(labels), B, K, ptr(loss_rows), ptr(dlog), 0, stream_handle())
+        mean = torch.empty((), device=logits.device)
+        C.ops.xent_mean(ptr(logits), ptr(labels), B, K, ptr(loss_rows), ptr(dlog), ptr(mean), 0,
+                        stream_handle())
         ctx.save_for_backward(dlog)
-        return loss_rows.mean()
+        return mean
 
     @staticmethod
     def backward(ctx, g):

@@ -115,7 +115,8 @@ class GenericEngine:
             self.step_dev.fill_(int(step))
 
     def loss_value(self) -> float:
-        return float(self.loss_buf.item())
+        t = getattr(self, "_loss_t", None) if self.on_gpu else None
+        return float((t if t is not None else self.loss_buf).item())
 
     def param_views(self):
         return self.layout.views(self.params.detach())
@@ -137,6 +138,9 @@ class GenericEngine:
                             self.B, row, ptr(self.xb), ptr(self.yb), s)
         logits = self.model.forward(self.P, self.bn, self.xb, True)
         loss = Fn.cross_entropy(logits, self.yb)
+        # keep the device scalar itself (no copy launch): under graph capture its
+        # storage is the graph's, rewritten by every replay
+        self._loss_t = loss.detach()
         gscale = 1.0
         Fn.set_unit_loss_seed(True)
         try:
@@ -154,7 +158,6 @@ class GenericEngine:
                 loss.backward(self.seed)
         finally:
             Fn.set_unit_loss_seed(False)
-        self.loss_buf.copy_(loss.detach())
         return gscale
 
     def update_gpu(self, gscale: float) -> None:

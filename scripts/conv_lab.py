@@ -1,7 +1,6 @@
 """Times the generic conv ops (forward / backward-data / backward-filter) on
-every distinct ResNet-18 layer shape at batch B, per op and per layer, with
-optional A/B of the gops.set_conv_variant tiling knobs.
-    python scripts/conv_lab.py [--batch 32] [--dtype bf16] [--ab SLOT=V1,V2,...] [--reps 20]"""
+every distinct ResNet-18 layer shape at batch B, per op and per layer.
+    python scripts/conv_lab.py [--batch 32] [--dtype bf16] [--reps 20]"""
 import argparse
 import os
 import sys
@@ -27,7 +26,6 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--dtype", default="bf16")
-    ap.add_argument("--ab", default=None)
     ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     C = native()
@@ -35,11 +33,7 @@ def main():
     bf16 = a.dtype == "bf16"
     dev = torch.device("cuda:0")
     s = stream_handle()
-    variants = [(None, 0)]
-    if a.ab:
-        slot, vals = a.ab.split("=")
-        variants = [(int(slot), int(v)) for v in vals.split(",")]
-    tot = {v: [0.0, 0.0, 0.0] for v in variants}
+    tot = [0.0, 0.0, 0.0]
     for (H, Cin, K, R, st, pd, cnt) in shapes(a.batch):
         Hin = 224 if Cin == 3 else (H if st == 1 else 2 * H)
         sh = g.ConvShape(a.batch, Hin, Hin, Cin, K, R, R, st, pd)
@@ -56,34 +50,27 @@ def main():
             "wgrad": lambda: g.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ws), ptr(dw), s, bf16),
         }
         line = f"H{Hin:3d} {Cin:3d}->{K:3d} {R}x{R} s{st} x{cnt}:"
-        for v in variants:
-            if v[0] is not None:
-                g.set_conv_variant(v[0], v[1])
-            res = []
-            for i, (name, fn) in enumerate(ops.items()):
-                if name == "dgrad" and Cin == 3:
-                    res.append(0.0)
-                    continue
-                for _ in range(3):
-                    fn()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                torch.cuda.synchronize()
-                e0.record()
-                for _ in range(a.reps):
-                    fn()
-                e1.record()
-                e1.synchronize()
-                us = e0.elapsed_time(e1) * 1000.0 / a.reps
-                res.append(us)
-                tot[v][i] += us * cnt
-            line += f"  [{v[1]}] " + " ".join(f"{t:7.1f}" for t in res)
-            if v[0] is not None:
-                g.set_conv_variant(v[0], 0)
+        res = []
+        for i, (name, fn) in enumerate(ops.items()):
+            if name == "dgrad" and Cin == 3:
+                res.append(0.0)
+                continue
+            for _ in range(3):
+                fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(a.reps):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1000.0 / a.reps
+            res.append(us)
+            tot[i] += us * cnt
+        line += "  " + " ".join(f"{t:7.1f}" for t in res)
         print(line, flush=True)
-    for v in variants:
-        t = tot[v]
-        print(f"variant {v}: per-step fwd {t[0]:.0f} dgrad {t[1]:.0f} wgrad {t[2]:.0f} "
-              f"total {sum(t):.0f} us")
+    t = tot
+    print(f"per-step fwd {t[0]:.0f} dgrad {t[1]:.0f} wgrad {t[2]:.0f} total {sum(t):.0f} us")
 
 
 if __name__ == "__main__":

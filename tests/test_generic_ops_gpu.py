@@ -368,3 +368,32 @@ def test_batchnorm_large_mean_channels(cuda_dev):
     assert _rel(rv.cpu().double(), rv_ref) < 1e-4
     assert _rel(rm.cpu().double(), rm_ref) < 1e-6
     assert _rel(xg.grad.cpu().double(), xr.grad) < 1e-3
+
+
+@pytest.mark.parametrize("N,H,Cin,K,R,stride,pad,bf16", [
+    (4, 14, 64, 64, 3, 1, 1, True),  # bf16 family, one K slab
+    (4, 7, 512, 512, 3, 1, 1, True),  # bf16 family, split-K slab reduction
+    (4, 14, 64, 128, 3, 2, 1, True),  # stride 2: tiled family
+    (4, 14, 64, 64, 3, 1, 1, False),  # fp32 tiled
+    (2, 28, 128, 128, 3, 2, 1, False),
+])
+def test_conv_dgrad_gradient_join(cuda_dev, N, H, Cin, K, R, stride, pad, bf16):
+    """The dgrad epilogue addend (Fn.GradJoin) equals dgrad + addend exactly
+    (fp32 add of the same accumulator), on every family the ResNet joins use."""
+    from mpi_tensorflow_amd.ops import native, ptr, stream_handle
+
+    g = native().ops
+    sh = g.ConvShape(N, H, H, Cin, K, R, R, stride, pad)
+    assert g.conv_bwd_data_join_ok(sh, bf16)
+    gen = torch.Generator().manual_seed(3)
+    w = (torch.randn(R, R, Cin, K, generator=gen) * 0.1).to(cuda_dev)
+    dy = torch.randn(N, sh.OH, sh.OW, K, generator=gen).to(cuda_dev)
+    add = torch.randn(N, H, H, Cin, generator=gen).to(cuda_dev)
+    ws = torch.empty(max(g.conv_ws_floats(sh, False), 4), device=cuda_dev)
+    s = stream_handle()
+    dx0 = torch.empty(N, H, H, Cin, device=cuda_dev)
+    dx1 = torch.empty_like(dx0)
+    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx0), ptr(ws), s, bf16)
+    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx1), ptr(ws), s, bf16, 0, ptr(add))
+    torch.cuda.synchronize()
+    assert torch.equal(dx1, dx0 + add)
