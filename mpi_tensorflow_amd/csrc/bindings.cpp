@@ -198,19 +198,26 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
-                       bool relu, uintptr_t ws, uintptr_t st, bool bf16, uintptr_t xb) {
+                       bool relu, uintptr_t ws, uintptr_t st, bool bf16, uintptr_t xb,
+                       uintptr_t wtb) {
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
-                   P<float>(ws), S(st), bf16, P<const void>(xb));
+                   P<float>(ws), S(st), bf16, P<const void>(xb), P<const void>(wtb));
     check_launch();
   }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
-     py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0);
+     py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0, py::arg("wtb") = 0);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
-                            uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend) {
+                            uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend,
+                            uintptr_t wtb) {
     gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st),
-                        bf16, P<const void>(dyb), P<const float>(addend));
+                        bf16, P<const void>(dyb), P<const float>(addend), P<const void>(wtb));
     check_launch();
   }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
-     py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0);
+     py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0, py::arg("wtb") = 0);
+  g.def("wcvt_blocks", &gops::wcvt_blocks);
+  g.def("wcvt_batch", [](uintptr_t jobs, int njobs, long long nblocks, uintptr_t st) {
+    gops::wcvt_batch(P<const long long>(jobs), njobs, nblocks, S(st));
+    check_launch();
+  });
   g.def("conv_ws_floats", &gops::conv_ws_floats);
   g.def("conv_filter_splits", &gops::conv_filter_splits);
   g.def("conv_bwd_filter", [](const gops::ConvShape& s, uintptr_t x, uintptr_t dy, uintptr_t part,

@@ -1,18 +1,25 @@
 // Per-channel reductions and BatchNorm for NHWC tensors (ResNet-18 config).
 //
-// The statistics are a two-pass, deterministic column reduction: pass 1 has
-// each block reduce a slab of rows into per-channel partials (thread = one
-// float4 of channels x a row stride, so every global load is a coalesced
-// 16-byte access; a block covers floor(256 / (C/4)) rows per pass); pass 2
-// has one wave per channel sum the block partials.  No
-// atomics, no memsets: the result (and a graph replay of it) is bitwise
-// reproducible.
+// The statistics are a deterministic two-pass column reduction: pass 1 has
+// each 1024-thread block reduce a slab of rows into per-channel partials
+// (thread = one float4 of channels x a row stride, so every global load is a
+// coalesced 16-byte access; 16 waves per block keep enough loads in flight
+// with ~one block per CU, so there are at most 256 partial rows), stored
+// channel-major; pass 2 has one wave per channel sum its contiguous partials
+// (<= 4 coalesced loads a lane) and apply the per-channel epilogue (sums, or
+// mean / rstd / running statistics).  No atomics, no memsets: the result
+// (and a graph replay of it) is bitwise reproducible.
+// (Measured alternative: fusing pass 2 into pass 1 with a last-block ticket
+// was SLOWER - the write-through partial stores, the ticket round trip and the
+// single block's serial reads cost ~10 us of tail, against ~3 us for the
+// separate launch; a device-scope release fence per block, the textbook
+// version, writes back the XCD's L2 and made the kernel 4x slower.)
 //
 // BN backward needs sum(dy') and sum(dy' * xhat) with dy' = dy [y > 0] when a
 // ReLU is fused; the pass-1 kernel computes both straight from (x, dy, y,
 // mean, rstd), so neither dy' nor xhat is ever materialised.  The BN forward
-// finalize also updates the running statistics (momentum, unbiased variance),
-// so the whole layer is three kernels with no host-side tensor ops.
+// epilogue also updates the running statistics (momentum, unbiased variance),
+// so a BN layer is two kernels per direction with no host-side tensor ops.
 //
 // bf16 conv mode: the apply kernels can also write a bf16 copy of their
 // output (y forward, dx backward), which the next conv reads as its bf16
@@ -35,28 +42,91 @@ __device__ __forceinline__ uint2 pack4(float4 a) {
   return __builtin_bit_cast(uint2, v);
 }
 
+// Epilogue of the reduction (run by the last block): s1 / s2 = the column
+// sums, or (bn_fwd) mean / rstd and the running statistics from shifted sums.
+struct Fin {
+  float* s1;
+  float* s2;
+  int bn_fwd;
+  float eps, momentum;
+  float* mean;
+  float* rstd;
+  float* rmean;
+  float* rvar;
+  const float* shift;
+};
+
+__device__ __forceinline__ void fin_channel(const Fin& f, int c, float a, float b, long long rows) {
+  if (f.s1) f.s1[c] = a;
+  if (f.s2) f.s2[c] = b;
+  if (f.bn_fwd) {
+    // The BN forward partials are SHIFTED sums, of (x - K) and (x - K)^2 with
+    // K = the channel's value in row 0 (`shift`): var = E[(x-K)^2] - E[x-K]^2
+    // cancels only (mean - K)^2 / var, a few units for a sample of the
+    // channel, instead of mean^2 / var for the plain E[x^2] - mean^2 (a
+    // channel with mean 1e3 and std 1 loses every digit of its variance in
+    // fp32 that way).
+    const float inv = 1.f / (float)rows;
+    const float ms = a * inv;  // mean of the shifted data
+    const float var = fmaxf(b * inv - ms * ms, 0.f);
+    const float m = ms + (f.shift ? f.shift[c] : 0.f);
+    f.mean[c] = m;
+    f.rstd[c] = rsqrtf(var + f.eps);
+    if (f.rmean) {  // torch semantics: unbiased variance in the running estimate
+      const float unb = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
+      f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * m;
+      f.rvar[c] = (1.f - f.momentum) * f.rvar[c] + f.momentum * unb;
+    }
+  }
+}
+
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+}
+
+// Tree fold of the row lanes of red[2][PT] (lane rl of quad q at rl * cq +
+// q) into lane 0; fixed order.
+template <int PT>
+__device__ __forceinline__ void fold_rows(float4 (*red)[PT], int cq, int RP, int tid, int rl) {
+  for (int h = RP >> 1; h >= 1; h >>= 1) {
+    if (rl < h) {
+      add4(red[0][tid], red[0][tid + h * cq]);
+      add4(red[1][tid], red[1][tid + h * cq]);
+    }
+    __syncthreads();
+  }
+}
+
+// Vector path (C % 4 == 0): PT = 1024 threads = cq channel quads x RP row
+// lanes (RP = the largest power of two <= PT / cq).  16 waves per block keep
+// enough loads in flight with ~one block per CU, so the partial rows are few
+// (<= 256) and the last block's sum of them is short.
+constexpr int PT = 1024;
+
 template <int MODE>
-__global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ a,
-                                                      const float* __restrict__ b,
-                                                      const float* __restrict__ yv,
-                                                      const float* __restrict__ mean,
-                                                      const float* __restrict__ rstd, int relu,
-                                                      long long rows, int C, int rows_per_block,
-                                                      float* __restrict__ part) {
-  __shared__ float4 red[2][256];
-  const int cq = C >> 2, RP = 256 / cq;
+__global__ __launch_bounds__(PT) void partial_kernel(const float* __restrict__ a,
+                                                     const float* __restrict__ b,
+                                                     const float* __restrict__ yv,
+                                                     const float* __restrict__ mean,
+                                                     const float* __restrict__ rstd, int relu,
+                                                     long long rows, int C, int rows_per_block,
+                                                     float* __restrict__ part) {
+  __shared__ float4 red[2][PT];
+  const int cq = C >> 2;
+  int RP = 1;
+  while (RP * 2 * cq <= PT) RP *= 2;
   const int tid = threadIdx.x, q = tid % cq, rl = tid / cq;
   const long long r0 = (long long)blockIdx.x * rows_per_block;
   const long long r1 = min(rows, r0 + rows_per_block);
   float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
   float4 mu = s1, rs = s1;
-  if (MODE == BN_BWD) {
-    mu = ld4(mean + 4 * q);
-    rs = ld4(rstd + 4 * q);
-  } else if (MODE == SUM_SQ && mean) {
-    mu = ld4(mean + 4 * q);  // shifted data: sums of (x - K), K = a sample of the channel
-  }
   if (rl < RP) {
+    if (MODE == BN_BWD) {
+      mu = ld4(mean + 4 * q);
+      rs = ld4(rstd + 4 * q);
+    } else if (MODE == SUM_SQ && mean) {
+      mu = ld4(mean + 4 * q);  // shifted data: sums of (x - K), K = a sample of the channel
+    }
 #pragma unroll 4
     for (long long r = r0 + rl; r < r1; r += RP) {
       const size_t o = (size_t)r * C + 4 * q;
@@ -89,16 +159,14 @@ __global__ __launch_bounds__(256) void partial_kernel(const float* __restrict__ 
   red[0][tid] = s1;
   red[1][tid] = s2;
   __syncthreads();
-  if (tid < cq) {  // thread q folds the RP row lanes of its channel quad
-    float4 t1 = red[0][tid], t2 = red[1][tid];
-    for (int j = 1; j < RP; ++j) {
-      const float4 u1 = red[0][tid + j * cq], u2 = red[1][tid + j * cq];
-      t1.x += u1.x; t1.y += u1.y; t1.z += u1.z; t1.w += u1.w;
-      t2.x += u2.x; t2.y += u2.y; t2.z += u2.z; t2.w += u2.w;
-    }
-    float* p = part + (size_t)blockIdx.x * 2 * C;
-    *reinterpret_cast<float4*>(p + 4 * tid) = t1;
-    *reinterpret_cast<float4*>(p + C + 4 * tid) = t2;
+  fold_rows<PT>(red, cq, RP, tid, rl);
+  if (tid < cq) {  // channel-major partial table [2][C][nb]
+    const int nb = gridDim.x, k = blockIdx.x;
+    const float4 t1 = red[0][tid], t2 = red[1][tid];
+    float* p = part + (size_t)(4 * tid) * nb + k;
+    p[0] = t1.x; p[nb] = t1.y; p[2 * nb] = t1.z; p[3 * nb] = t1.w;
+    p += (size_t)C * nb;
+    p[0] = t2.x; p[nb] = t2.y; p[2 * nb] = t2.z; p[3 * nb] = t2.w;
   }
 }
 
@@ -132,52 +200,25 @@ __global__ __launch_bounds__(256) void partial1_kernel(const float* __restrict__
       t1 += red[0][tid + j * C];
       t2 += red[1][tid + j * C];
     }
-    part[(size_t)blockIdx.x * 2 * C + tid] = t1;
-    part[(size_t)blockIdx.x * 2 * C + C + tid] = t2;
+    part[(size_t)tid * gridDim.x + blockIdx.x] = t1;
+    part[(size_t)(C + tid) * gridDim.x + blockIdx.x] = t2;
   }
 }
 
-// One wave per channel: s1 / s2 = sums of the nb block partials.  BN
-// forward mode also writes mean / rstd and updates the running statistics.
-// The BN forward partials are SHIFTED sums, of (x - K) and (x - K)^2 with
-// K = the channel's value in row 0 (`shift`): var = E[(x-K)^2] - E[x-K]^2
-// cancels only (mean - K)^2 / var, a few units for a sample of the channel,
-// instead of mean^2 / var for the plain E[x^2] - mean^2 (a channel with mean
-// 1e3 and std 1 loses every digit of its variance in fp32 that way).
+// Pass 2: one wave per channel sums its nb contiguous partials (fixed order),
+// lane 0 applies the epilogue.
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nb,
-                                                       int C, float* __restrict__ s1,
-                                                       float* __restrict__ s2, int bn_fwd,
-                                                       long long rows, float eps, float momentum,
-                                                       float* __restrict__ mean,
-                                                       float* __restrict__ rstd,
-                                                       float* __restrict__ rmean,
-                                                       float* __restrict__ rvar,
-                                                       const float* __restrict__ shift) {
+                                                       int C, long long rows, Fin fin) {
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (c >= C) return;
   float a = 0.f, b = 0.f;
   for (int k = lane; k < nb; k += 64) {
-    a += part[(size_t)k * 2 * C + c];
-    b += part[(size_t)k * 2 * C + C + c];
+    a += part[(size_t)c * nb + k];
+    b += part[(size_t)(C + c) * nb + k];
   }
   a = wave_sum(a);
   b = wave_sum(b);
-  if (lane != 0) return;
-  if (s1) s1[c] = a;
-  if (s2) s2[c] = b;
-  if (bn_fwd) {
-    const float inv = 1.f / (float)rows;
-    const float ms = a * inv;  // mean of the shifted data
-    const float var = fmaxf(b * inv - ms * ms, 0.f);
-    const float m = ms + (shift ? shift[c] : 0.f);
-    mean[c] = m;
-    rstd[c] = rsqrtf(var + eps);
-    if (rmean) {  // torch semantics: unbiased variance in the running estimate
-      const float unb = rows > 1 ? var * (float)rows / (float)(rows - 1) : var;
-      rmean[c] = (1.f - momentum) * rmean[c] + momentum * m;
-      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unb;
-    }
-  }
+  if (lane == 0) fin_channel(fin, c, a, b, rows);
 }
 
 // y = (x - mean) rstd g + b (+ res) (relu); eval: mean / var from running stats
@@ -256,9 +297,17 @@ static inline int grid_elems(long long n) {
 }
 
 static inline int nblocks(long long rows, int C) {
-  const int RP = C % 4 == 0 ? 256 / (C / 4) : 256 / C;
-  long long nb = (rows + RP * 16 - 1) / (RP * 16);  // >= 16 row passes per block
-  if (nb > 1024) nb = 1024;
+  long long nb;
+  if (C % 4 == 0) {  // vector path: PT threads, >= 8 row passes, <= 256 blocks
+    int RP = 1;
+    while (RP * 2 * (C / 4) <= PT) RP *= 2;
+    nb = (rows + RP * 8 - 1) / (RP * 8);
+    if (nb > 256) nb = 256;
+  } else {
+    const int RP = 256 / C;
+    nb = (rows + RP * 16 - 1) / (RP * 16);  // >= 16 row passes per block
+    if (nb > 1024) nb = 1024;
+  }
   return (int)(nb < 1 ? 1 : nb);
 }
 
@@ -273,18 +322,23 @@ long long chan_reduce_ws_floats(long long rows, int C) {
 
 static void run_partials(int mode, const float* a, const float* b, const float* y,
                          const float* mean, const float* rstd, int relu, long long rows, int C,
-                         float* ws, int nb, hipStream_t st) {
+                         float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
   const int rpb = (int)((rows + nb - 1) / nb);
   switch (mode) {
     case bn::SUM_SQ:
-      bn::partial_kernel<bn::SUM_SQ><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_SQ><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     case bn::SUM_PROD:
-      bn::partial_kernel<bn::SUM_PROD><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_PROD><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     default:
-      bn::partial_kernel<bn::BN_BWD><<<nb, 256, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::BN_BWD><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
   }
+  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, fin);
+}
+
+static bn::Fin sums(float* s1, float* s2) {
+  return {s1, s2, 0, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr};
 }
 
 void chan_reduce(const float* a, const float* b, long long rows, int C, float* s1, float* s2,
@@ -292,13 +346,12 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
   if (!chan_reduce_ok(C)) throw std::runtime_error("chan_reduce: unsupported channel count");
   const int nb = bn::nblocks(rows, C);
   if (C % 4 == 0 && C <= 1024) {
-    run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, st);
+    run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, sums(s1, s2), st);
   } else {
     const int rpb = (int)((rows + nb - 1) / nb);
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
+    bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, sums(s1, s2));
   }
-  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, s1, s2, 0, rows, 0.f, 0.f, nullptr,
-                                                   nullptr, nullptr, nullptr, nullptr);
 }
 
 void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
@@ -310,9 +363,8 @@ void bn_fwd(const float* x, long long rows, int C, const float* g, const float* 
   if (training) {
     const int nb = bn::nblocks(rows, C);
     // shift K = row 0 of x (passed as the partials' `mean`)
-    run_partials(bn::SUM_SQ, x, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, st);
-    bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, nullptr, nullptr, 1, rows, eps,
-                                                     momentum, mean, rstd, rmean, rvar, x);
+    const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x};
+    run_partials(bn::SUM_SQ, x, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, fin, st);
     bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
                                                           relu ? 1 : 0, 0, eps,
                                                           reinterpret_cast<uint2*>(yb));
@@ -328,10 +380,8 @@ void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, 
             float* dx, float* dres, hipStream_t st, void* dxb) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
   const int nb = bn::nblocks(rows, C);
-  run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, st);
   // db = sum dy', dg = sum dy' xhat
-  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, db, dg, 0, rows, 0.f, 0.f, nullptr,
-                                                   nullptr, nullptr, nullptr, nullptr);
+  run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, sums(db, dg), st);
   const long long n4 = rows * C / 4;
   bn::bwd_apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx,
                                                             dres, n4, C, rows, relu ? 1 : 0,

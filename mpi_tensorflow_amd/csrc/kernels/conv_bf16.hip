@@ -90,6 +90,44 @@ __global__ __launch_bounds__(256) void wcvt_kernel(const float* __restrict__ w, 
   }
 }
 
+// All the bf16 weight copies of a model in ONE launch (per training step,
+// after the update): jobs[j] = {w, out, taps, C, K, mode, first block, 0} as
+// int64, blocks of job j run wcvt_kernel's 32 x 32 tile at (block - first).
+// Replaces one wcvt launch per conv call (ResNet-18: 40 launches, ~195 us a
+// step, each too small to fill the chip).
+__global__ __launch_bounds__(256) void wcvt_batch_kernel(const long long* __restrict__ jobs,
+                                                         int njobs) {
+  __shared__ float t[32][33];
+  const int b = blockIdx.x;
+  int j = 0;
+  while (j + 1 < njobs && jobs[8 * (j + 1) + 6] <= b) ++j;
+  const long long* J = jobs + 8 * j;
+  const float* w = reinterpret_cast<const float*>(J[0]);
+  __bf16* out = reinterpret_cast<__bf16*>(J[1]);
+  const int taps = (int)J[2], C = (int)J[3], K = (int)J[4], mode = (int)J[5];
+  const int lb = b - (int)J[6];
+  const int ct = C / 32, kt = K / 32;
+  const int tap = lb / (ct * kt), rem = lb % (ct * kt), c0 = (rem / kt) * 32, k0 = (rem % kt) * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const float* src = w + (size_t)tap * C * K;
+  if (mode == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[ty + 8 * i][tx] = src[(size_t)(c0 + ty + 8 * i) * K + k0 + tx];
+    __syncthreads();
+    __bf16* dst = out + (size_t)tap * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      dst[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = (__bf16)t[tx][ty + 8 * i];
+  } else {
+    __bf16* dst = out + (size_t)(taps - 1 - tap) * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t o = (size_t)(c0 + ty + 8 * i) * K + k0 + tx;
+      dst[o] = (__bf16)src[o];
+    }
+  }
+}
+
 // Forward conv Y[m = (n, oy, ox)][co] = sum_{tap, ci} X[n, iy, ix, ci] Wt[tap][co][ci].
 // XT = __bf16: bf16 activation copy (16-byte loads); XT = float: fp32
 // activations converted while staged.
@@ -921,12 +959,27 @@ void to_bf16(const float* x, void* y, long long n, hipStream_t st) {
       reinterpret_cast<const float4*>(x), reinterpret_cast<uint4*>(y), n / 8);
 }
 
+long long wcvt_blocks(int taps, int C, int K) {
+  if (C % 32 || K % 32) throw std::runtime_error("wcvt_blocks: C, K must be multiples of 32");
+  return (long long)taps * (C / 32) * (K / 32);
+}
+
+void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t st) {
+  if (njobs <= 0 || nblocks <= 0 || nblocks >= (1LL << 31))
+    throw std::runtime_error("wcvt_batch: bad job table");
+  cbf::wcvt_batch_kernel<<<(int)nblocks, 256, 0, st>>>(jobs, njobs);
+}
+
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                   bool relu, float* ws, hipStream_t st, const void* xb) {
+                   bool relu, float* ws, hipStream_t st, const void* xb, const void* wtb) {
   using namespace cbf;
   if (!conv_fwd_bf16_ok(s) || !ws) throw std::runtime_error("conv_fwd_bf16: unsupported shape");
-  __bf16* wt = reinterpret_cast<__bf16*>(ws);
-  convert(s, w, 0, wt, st);
+  const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
+  if (!wt) {
+    __bf16* wc = reinterpret_cast<__bf16*>(ws);
+    convert(s, w, 0, wc, st);
+    wt = wc;
+  }
   if (xb)
     launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st);
   else
@@ -934,11 +987,15 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
 }
 
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st, const void* dyb, const float* addend) {
+                        hipStream_t st, const void* dyb, const float* addend, const void* wtb) {
   using namespace cbf;
   if (!conv_bwd_data_bf16_ok(s) || !ws) throw std::runtime_error("conv_bwd_data_bf16: unsupported shape");
-  __bf16* wt = reinterpret_cast<__bf16*>(ws);
-  convert(s, w, 1, wt, st);
+  const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
+  if (!wt) {
+    __bf16* wc = reinterpret_cast<__bf16*>(ws);
+    convert(s, w, 1, wc, st);
+    wt = wc;
+  }
   if (dyb)
     launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st,
            addend);

@@ -21,13 +21,16 @@ struct PoolShape {
 // bf16: MFMA operands converted to bf16 (fp32 accumulate, fp32 in / out); the
 // tiled family only - shapes it does not take run the fp32 gather engine
 // xb / dyb: optional bf16 copies of x / dy (to_bf16) for the bf16 family
+// wtb (optional, bf16 family): the weights already laid out by wcvt_batch
+// (forward copy for conv_fwd, stride-1 dgrad copy for conv_bwd_data)
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr);
+              bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr,
+              const void* wtb = nullptr);
 // addend (optional, bf16 / tiled families): a gradient that joins dX at this
 // tensor (a residual branch), added in the epilogue: dx = conv + addend
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                    hipStream_t st, bool bf16 = false, const void* dyb = nullptr,
-                   const float* addend = nullptr);
+                   const float* addend = nullptr, const void* wtb = nullptr);
 bool conv_bwd_data_join_ok(const ConvShape& s, bool bf16);  // takes an addend
 int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
@@ -43,9 +46,16 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
 void to_bf16(const float* x, void* y, long long n, hipStream_t st);
 void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                   bool relu, float* ws, hipStream_t st, const void* xb = nullptr);
+                   bool relu, float* ws, hipStream_t st, const void* xb = nullptr,
+                   const void* wtb = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr);
+                        hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr,
+                        const void* wtb = nullptr);
+// batched weight re-layout: jobs = device int64 [njobs][8] = {w, out, taps,
+// C, K, mode (0 forward, 1 stride-1 dgrad), first block, 0}, blocks of a job
+// = wcvt_blocks(taps, C, K), first blocks ascending
+long long wcvt_blocks(int taps, int C, int K);
+void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t st);
 bool conv_bwd_filter_bf16_ok(const ConvShape& s);
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
                           float* dw, hipStream_t st, const void* xb = nullptr,

@@ -37,6 +37,45 @@ class Param:
 
     value: torch.Tensor
     grad_view: torch.Tensor
+    # bf16 MFMA convs: weight copies laid out for the forward / the stride-1
+    # dgrad, kept current by the owner's Bf16Weights.refresh()
+    wtb: Optional[torch.Tensor] = None
+    wtb_d: Optional[torch.Tensor] = None
+
+
+class Bf16Weights:
+    """bf16 re-laid copies of every MFMA-family conv weight (C, K % 64 == 0)
+    of a model - the forward layout [tap][co][ci] and the stride-1 dgrad
+    layout (taps reversed) - in one buffer, refreshed by ONE wcvt_batch launch
+    that the engine issues ahead of each forward (after the previous update).
+    The conv ops then skip their per-call conversion (ResNet-18: 40 small
+    launches a step).  Param.wtb / wtb_d point into the buffer."""
+
+    def __init__(self, params, device: torch.device):
+        C = native()
+        eligible = [p for p in params.values()
+                    if p.value.dim() == 4 and p.value.shape[2] % 64 == 0 and p.value.shape[3] % 64 == 0]
+        self.buf = torch.empty(max(1, sum(2 * p.value.numel() for p in eligible)),
+                               dtype=torch.bfloat16, device=device)
+        rows, off, blocks = [], 0, 0
+        for p in eligible:
+            R, S, Ci, K = p.value.shape
+            n = p.value.numel()
+            for mode in (0, 1):
+                out = self.buf[off:off + n]
+                off += n
+                rows.append([ptr(p.value), ptr(out), R * S, Ci, K, mode, blocks, 0])
+                blocks += C.ops.wcvt_blocks(R * S, Ci, K)
+                if mode == 0:
+                    p.wtb = out
+                else:
+                    p.wtb_d = out
+        self.njobs, self.nblocks = len(rows), blocks
+        self.jobs = torch.tensor(rows if rows else [[0] * 8], dtype=torch.int64, device=device)
+
+    def refresh(self) -> None:
+        if self.njobs:
+            native().ops.wcvt_batch(ptr(self.jobs), self.njobs, self.nblocks, stream_handle())
 
 
 def _empty(shape, like):
@@ -141,7 +180,8 @@ class GradJoin:
 # ------------------------------------------------------------------- conv --
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None):
+    def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None, wtb=None,
+                wtb_d=None):
         C = native()
         x = x.contiguous()
         y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
@@ -153,11 +193,11 @@ class _ConvFn(torch.autograd.Function):
         if ctx.bf16 and C.ops.conv_bf16_ok(shape):
             xb = _bf16_copy(x, s)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), s, ctx.bf16,
-                       ptr(xb))
+                       ptr(xb), ptr(wtb))
         ctx.save_for_backward(x, w, y, xb)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
-        ctx.join, ctx.role = join, role
+        ctx.join, ctx.role, ctx.wtb_d = join, role, wtb_d
         return y
 
     @staticmethod
@@ -186,13 +226,13 @@ class _ConvFn(torch.autograd.Function):
             dx = _empty((sh.N, sh.H, sh.W, sh.C), dy)
             add = ctx.join.take() if ctx.role == "final" else None
             C.ops.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ctx.ws), s, ctx.bf16, ptr(dyb),
-                                ptr(add))
+                                ptr(add), ptr(ctx.wtb_d))
             if ctx.role == "stash":
                 ctx.join.stash(dx)
                 dx = None
             elif ctx.role == "final" and add is None:
                 ctx.join.out = dx
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvIm2colFn(torch.autograd.Function):
@@ -304,7 +344,8 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
                                                                                          _CONV_BF16):
             raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
-                             None if b is None else b.grad_view, ws, join, join_role)
+                             None if b is None else b.grad_view, ws, join, join_role, w.wtb,
+                             w.wtb_d)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y

@@ -71,6 +71,7 @@ class GenericEngine:
         if force_sync and comm is not None:  # exercise the collective path at world 1
             self.grad_sync = True
         self.on_gpu = device.type == "cuda"
+        self.wcache = None
         self.use_graph = cfg.graph and self.on_gpu
         self.graph_steps = max(1, cfg.graph_steps)
         self._graphs = {}
@@ -91,6 +92,8 @@ class GenericEngine:
             self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
             self.lr_dev = torch.zeros(1, device=device)
             self.seed = torch.ones((), device=device)  # backward seed, never written
+            # bf16: all conv weight copies in one launch per step
+            self.wcache = Fn.Bf16Weights(self.P, device) if self.bf16 else None
 
     # ------------------------------------------------------------------ util
     def lr(self, step: Optional[int] = None) -> float:
@@ -134,6 +137,8 @@ class GenericEngine:
         Fn.set_conv_bf16(self.bf16)
         s = stream_handle()
         row = int(np.prod(self.xb.shape[1:]))
+        if self.wcache is not None:
+            self.wcache.refresh()
         C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
                             self.B, row, ptr(self.xb), ptr(self.yb), s)
         logits = self.model.forward(self.P, self.bn, self.xb, True)
@@ -286,6 +291,8 @@ class GenericEngine:
         _, xd, yd = self._eval_cache
         correct = torch.zeros(1, dtype=torch.int32, device=self.device)
         s = stream_handle()
+        if self.wcache is not None:
+            self.wcache.refresh()
         for a in range(0, n, chunk):
             xb, yb = xd[a:a + chunk], yd[a:a + chunk]
             logits = self.model.forward(self.P, self.bn, xb, False).contiguous()

@@ -35,7 +35,7 @@ def main():
     s = stream_handle()
     tot = [0.0, 0.0, 0.0]
     for (H, Cin, K, R, st, pd, cnt) in shapes(a.batch):
-        Hin = 224 if Cin == 3 else (H if st == 1 else 2 * H)
+        Hin = 224 if Cin == 3 else H  # the table's H is the input size (stem: output)
         sh = g.ConvShape(a.batch, Hin, Hin, Cin, K, R, R, st, pd)
         x = torch.randn(a.batch, Hin, Hin, Cin, device=dev)
         w = torch.randn(R, R, Cin, K, device=dev) * 0.05
@@ -44,10 +44,17 @@ def main():
         dx = torch.empty_like(x)
         dw = torch.empty_like(w)
         ws = torch.empty(max(g.conv_ws_floats(sh, False), 4) * 2, device=dev)
+        # the engine's bf16 twins of x / dY (written by the BN kernels)
+        xb = dyb = None
+        if bf16 and g.conv_bf16_ok(sh):
+            xb, dyb = x.to(torch.bfloat16), dy.to(torch.bfloat16)
         ops = {
-            "fwd": lambda: g.conv_fwd(sh, ptr(x), ptr(w), 0, ptr(y), False, ptr(ws), s, bf16),
-            "dgrad": lambda: g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ws), s, bf16),
-            "wgrad": lambda: g.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ws), ptr(dw), s, bf16),
+            "fwd": lambda: g.conv_fwd(sh, ptr(x), ptr(w), 0, ptr(y), False, ptr(ws), s, bf16,
+                                      ptr(xb)),
+            "dgrad": lambda: g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ws), s, bf16,
+                                             ptr(dyb)),
+            "wgrad": lambda: g.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ws), ptr(dw), s, bf16,
+                                               ptr(xb), ptr(dyb)),
         }
         line = f"H{Hin:3d} {Cin:3d}->{K:3d} {R}x{R} s{st} x{cnt}:"
         res = []

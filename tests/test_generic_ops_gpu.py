@@ -397,3 +397,57 @@ def test_conv_dgrad_gradient_join(cuda_dev, N, H, Cin, K, R, stride, pad, bf16):
     g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx1), ptr(ws), s, bf16, 0, ptr(add))
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx0 + add)
+
+
+@pytest.mark.parametrize("M,K,N,relu", [(32, 512, 10, False), (64, 400, 120, True),
+                                        (64, 84, 10, False), (5, 7, 200, True), (130, 33, 1, True)])
+def test_linear_native_vs_torch(cuda_dev, M, K, N, relu):
+    """Native FC forward (K split over lanes, LDS reduction) and the
+    three-role backward vs fp32 torch."""
+    gen = torch.Generator().manual_seed(11)
+    x = torch.randn(M, K, generator=gen)
+    w = torch.randn(K, N, generator=gen) * 0.1
+    b = torch.randn(N, generator=gen)
+    dy = torch.randn(M, N, generator=gen)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr + br
+    yr = F.relu(yr) if relu else yr
+    yr.backward(dy)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    wp, bp = _param(w.to(cuda_dev)), _param(b.to(cuda_dev))
+    yg = Fn.linear(xg, wp, bp, relu)
+    yg.backward(dy.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert _rel(yg.detach().cpu(), yr.detach()) < 1e-5
+    assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-5
+    assert _rel(bp.grad_view.cpu(), br.grad) < 1e-5
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-5
+
+
+def test_bn_single_launch_reduction_repeatable(cuda_dev):
+    """The one-launch BN statistics (last block sums the partial rows) on a
+    ResNet layer-1 sized tensor: 20 back-to-back forward + backward passes
+    give bit-identical results (a stale cross-XCD partial read would not),
+    matching fp32 torch."""
+    gen = torch.Generator().manual_seed(5)
+    x = (torch.randn(32, 56, 56, 64, generator=gen) * 3 + 1).to(cuda_dev)
+    dy = torch.randn(32, 56, 56, 64, generator=gen).to(cuda_dev)
+    g, b = _param(torch.rand(64).to(cuda_dev) + 0.5), _param(torch.randn(64).to(cuda_dev))
+    outs = []
+    for _ in range(20):
+        rm, rv = torch.zeros(64, device=cuda_dev), torch.ones(64, device=cuda_dev)
+        xi = x.clone().requires_grad_(True)
+        y = Fn.batchnorm(xi, g, b, rm, rv, True, relu=True)
+        y.backward(dy)
+        outs.append((y.detach().clone(), xi.grad.clone(), g.grad_view.clone(), rm.clone()))
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        for a_, b_ in zip(o, outs[0]):
+            assert torch.equal(a_, b_)
+    # float64 reference: at 100k rows an fp32 reference's own rounding is ~1e-3
+    xr = x.cpu().double().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.relu(F.batch_norm(xr, None, None, g.value.cpu().double(), b.value.cpu().double(), True,
+                             0.1, 1e-5))
+    yr.backward(dy.cpu().double().permute(0, 3, 1, 2))
+    assert _rel(outs[0][0].cpu(), yr.detach().permute(0, 2, 3, 1)) < 1e-5
+    assert _rel(outs[0][1].cpu(), xr.grad.permute(0, 2, 3, 1)) < 1e-4
