@@ -280,6 +280,205 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
 }
 
 
+// ------------------------------------------- 3x3 stride-1 halo forward ----
+// The generic kernels above stage a fresh [128 pixels x 64 ch] A tile for
+// EACH of the 9 taps (the same activations read 9 times through L2) and keep
+// one K tile in flight: on ResNet-18's 3x3 stride-1 layers (forward, and the
+// stride-1 dgrad, which is the same conv) they ran 33-40 us a layer at B = 32,
+// latency bound.  Here a block owns 128 consecutive output pixels x 64
+// output channels and, per 64-channel chunk:
+//   * stages the activation HALO once - the contiguous run of input pixels
+//     from one stacked image row above the tile to one below (<= 344
+//     pixels x 128 B): in NHWC the rows of consecutive images are adjacent,
+//     so it is ONE strided copy, done with global_load_lds_dwordx4 (no VGPR
+//     staging; 8 pixels per wave-instruction);
+//   * reads each tap's A fragments straight out of the halo at a per-lane
+//     shifted pixel row (padding taps and the rows of a neighbouring image
+//     read a zero row), so the activations cross L2 once per chunk, not 9x;
+//   * streams the 9 taps' weight tiles (64 co x 64 ci) through a 4-deep LDS
+//     ring, three in flight (counted vmcnt, raw s_barrier: the DMA queue is
+//     not drained by the barrier);
+//   * 16-byte chunks of every 128-byte LDS row are swizzled through the DMA
+//     source address, slot = chunk ^ ((row >> 1) & 7): a ds_read_b128 lane
+//     group (16 lanes, one LDS cycle when its 16 x 16 B cover the 64 banks)
+//     reads 16 consecutive rows, i.e. both 128-B halves of the bank row x 8
+//     slots.  (chunk ^ (row & 7) left every group 2-way conflicted: half of
+//     the LDS cycles were SQ_LDS_BANK_CONFLICT.)
+// Split-K over channel chunks (deterministic slabs) fills the chip on the
+// small-M deep layers.  LDS 75 KiB: two blocks per CU.
+namespace h3 {
+constexpr int ROWB = 128;  // bytes per LDS row (64 bf16 channels)
+constexpr int HCAP = 344;  // halo pixel rows (multiple of 8); row HCAP is all zeros
+__device__ uint4 g_zero[4];  // never written: the DMA source of rows outside the tensor
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void glds(const void* src, char* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+// halo rows a BM-pixel tile can need: the stacked rows it touches + 2, x W
+inline int halo_rows(const ConvShape& s, int bm) { return ((bm + s.W - 2) / s.W + 3) * s.W; }
+}  // namespace h3
+
+template <int BM, int BN, int RB>
+__global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __restrict__ x,
+                                                   const __bf16* __restrict__ wt,
+                                                   float* __restrict__ y, int cps,
+                                                   const float* __restrict__ addend) {
+  using h3::ROWB;
+  using h3::HCAP;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int GB = BN / 32;  // weight DMA instructions per wave per tap
+  constexpr int HB = (HCAP + 1) * ROWB;
+  constexpr int BSZ = BN * ROWB;
+  static_assert(RB >= 3 && RB <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[HB + RB * BSZ];
+  const int M = s.N * s.H * s.W;
+  const int W = s.W, H = s.H;
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
+  const int nch = s.C / BK;
+  const int cc0 = blockIdx.y * cps, cc1 = min(nch, cc0 + cps);
+  const int g_first = m0 / W, g_last = (min(m0 + BM, M) - 1) / W;
+  const long long hbase = (long long)(g_first - 1) * W;  // global pixel of halo row 0
+  const int npix = (g_last - g_first + 3) * W;
+  const int nins = (npix + 7) >> 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5, lr = lane >> 3;
+  if (tid < 8) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  // this lane's A rows (output pixels)
+  int gl[TM], oxs[TM], oys[TM];
+  bool mv[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / 2) + 32 * i + r;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : m0;
+    const int g = mm / W;
+    oxs[i] = mm - g * W;
+    oys[i] = g % H;
+    gl[i] = g - g_first + 1;
+  }
+  const __bf16* bsrc[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = wave * (BN / 4) + 8 * j + lr;
+    bsrc[j] = wt + (size_t)(n0 + row) * s.C + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  auto issue_b = [&](int tap, int cc, int slot) {
+    const size_t o = (size_t)tap * s.K * s.C + (size_t)cc * BK;
+    char* dst = smem + HB + slot * BSZ + wave * (BN / 4) * ROWB;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) h3::glds(bsrc[j] + o, dst + 8 * j * ROWB);
+  };
+  auto issue_halo = [&](int cc) {
+    for (int ins = wave; ins < nins; ins += 4) {
+      const int p = 8 * ins + lr;
+      const long long gp = hbase + p;
+      const bool ok = p < npix && gp >= 0 && gp < M;
+      const void* src = ok ? (const void*)(x + gp * s.C + (size_t)cc * BK +
+                                           8 * ((lane & 7) ^ ((p >> 1) & 7)))
+                           : (const void*)h3::g_zero;
+      h3::glds(src, smem + ins * 8 * ROWB);
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero16();
+  for (int cc = cc0; cc < cc1; ++cc) {
+    // the previous chunk's halo and ring reads are done (and the zero row is written)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_halo(cc);
+#pragma unroll
+    for (int t = 0; t < RB - 1; ++t) issue_b(t, cc, t);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      // halo and tap t's weights landed (own DMAs; the barrier: every wave's);
+      // the (up to RB - 2) taps issued after t may stay in flight
+      const int ahead = min(RB - 2, 8 - t);
+      if (ahead >= 2)
+        h3::wait_vm<2 * GB>();
+      else if (ahead == 1)
+        h3::wait_vm<GB>();
+      else
+        h3::wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring slot (t - 1) % RB read
+      __builtin_amdgcn_s_barrier();
+      if (t + RB - 1 < 9) issue_b(t + RB - 1, cc, (t + RB - 1) % RB);
+      const int kh = t / 3, kw = t - 3 * kh;
+      int hrow[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int iy = oys[i] + kh - 1, ix = oxs[i] + kw - 1;
+        const bool ok = mv[i] && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        hrow[i] = ok ? (gl[i] + kh - 1) * W + ix : HCAP;
+      }
+      const char* B = smem + HB + (t % RB) * BSZ;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int c = 2 * ks + h;
+        bfx8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bfx8*>(smem + hrow[i] * ROWB +
+                                                ((c ^ ((hrow[i] >> 1) & 7)) << 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int R = wn * (BN / 2) + 32 * j + r;
+          b[j] = *reinterpret_cast<const bfx8*>(B + R * ROWB + ((c ^ ((R >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: lane (r, h) of 32 x 32 tile (i, j) holds rows 4h + (q & 3) +
+  // 8 (q >> 2), column r; per-tile base pointers, the 16 row offsets are
+  // wave-uniform multiples of K, and the bounds / addend branches are taken
+  // once per tile (per element they were ~40 % of the kernel's instructions)
+  y += (size_t)blockIdx.y * M * s.K;
+  const size_t K = s.K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
+    const bool full = m0 + wm * (BM / 2) + 32 * i + 32 <= M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (BN / 2) + 32 * j + r;
+      float* p = y + (size_t)mb * K + co;
+      if (full && addend) {
+        const float* ap = addend + (size_t)mb * K + co;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const size_t o = (size_t)((q & 3) + 8 * (q >> 2)) * K;
+          p[o] = acc[i][j][q] + ap[o];
+        }
+      } else if (full) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[(size_t)((q & 3) + 8 * (q >> 2)) * K] = acc[i][j][q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = (q & 3) + 8 * (q >> 2);
+          if (mb + rr >= M) continue;
+          float v = acc[i][j][q];
+          if (addend) v += addend[(size_t)(mb + rr) * K + co];
+          p[(size_t)rr * K] = v;
+        }
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------- backward-filter ----
 // dW[tap][ci][co] = sum_pix X[pix shifted by tap][ci] dY[pix][co].  GEMM
 // M = (tap, ci), N = co, reduction over output pixels; block = (128-row M
@@ -570,6 +769,40 @@ static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const floa
     default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
   }
 #undef GRID
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend);
+}
+
+// halo conv: 3x3, stride 1, pad 1, C and K % 64 == 0, a 128-pixel tile's
+// halo within HCAP rows (W <= ~84), 32-bit pixel x channel offsets
+static bool conv3_ok(const ConvShape& s) {
+  return s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.OH == s.H && s.OW == s.W &&
+         s.C % 64 == 0 && s.K % 64 == 0 && h3::halo_rows(s, 128) <= h3::HCAP &&
+         (long long)s.N * s.H * s.W * s.C < (1LL << 31);
+}
+// 64-channel output tiles; split-K over channel chunks up to one block per CU
+struct P3 {
+  int z, cps;
+};
+static inline P3 plan3(const ConvShape& s) {
+  const long long M = (long long)s.N * s.H * s.W;
+  const long long blocks = (long long)cdiv(M, 128) * (s.K / 64);
+  const int nch = s.C / BK;
+  int z = 1;
+  if (blocks < 256) {
+    z = cdiv(256, blocks);
+    if (z > nch) z = nch;
+  }
+  const int cps = cdiv(nch, z);
+  return {cdiv(nch, cps), cps};
+}
+static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
+                    hipStream_t st, const float* addend) {
+  const long long M = (long long)s.N * s.H * s.W;
+  const P3 p = plan3(s);
+  float* slabs = ws + wt_floats(s);
+  float* out = p.z > 1 ? slabs : y;
+  const dim3 grid(cdiv(M, 128) * (s.K / 64), p.z);
+  conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, p.z > 1 ? nullptr : addend);
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend);
 }
 
@@ -892,14 +1125,20 @@ bool conv_bwd_data_bf16_ok(const ConvShape& s) {
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
   using namespace cbf;
   long long n = 0;
-  if (conv_fwd_bf16_ok(s)) {
-    const Plan p = plan(s, fwd_epilogue);
-    n = std::max(n, wt_floats(s) + (p.z > 1 ? (long long)p.z * s.N * s.OH * s.OW * s.K : 0));
-  }
+  auto slab_floats = [](const ConvShape& c, bool epi) {
+    const Plan p = plan(c, epi);
+    const long long mk = (long long)c.N * c.OH * c.OW * c.K;
+    long long f = p.z > 1 ? p.z * mk : 0LL;
+    if (conv3_ok(c)) {
+      const P3 q = plan3(c);
+      if (q.z > 1) f = std::max(f, q.z * mk);
+    }
+    return f;
+  };
+  if (conv_fwd_bf16_ok(s)) n = std::max(n, wt_floats(s) + slab_floats(s, fwd_epilogue));
   if (conv_bwd_data_bf16_ok(s)) {
     const ConvShape d = dgrad_shape(s);
-    const Plan p = plan(d, false);
-    n = std::max(n, wt_floats(d) + (p.z > 1 ? (long long)p.z * d.N * d.OH * d.OW * d.K : 0));
+    n = std::max(n, wt_floats(d) + slab_floats(d, false));
   }
   if (conv_bwd_filter_bf16_ok(s)) {
     const WgPlan p = wg_plan(s);
@@ -980,7 +1219,9 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
     convert(s, w, 0, wc, st);
     wt = wc;
   }
-  if (xb)
+  if (xb && !bias && !relu && conv3_ok(s))
+    launch3(s, reinterpret_cast<const __bf16*>(xb), wt, y, ws, st, nullptr);
+  else if (xb)
     launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st);
   else
     launch(s, x, wt, bias, y, relu, ws, st);
@@ -996,7 +1237,9 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
     convert(s, w, 1, wc, st);
     wt = wc;
   }
-  if (dyb)
+  if (dyb && conv3_ok(dgrad_shape(s)))
+    launch3(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend);
+  else if (dyb)
     launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st,
            addend);
   else

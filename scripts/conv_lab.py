@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--layers", default=None, help="comma list of shape-table rows to run")
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
     a = ap.parse_args()
     C = native()
     g = C.ops
@@ -34,7 +36,11 @@ def main():
     dev = torch.device("cuda:0")
     s = stream_handle()
     tot = [0.0, 0.0, 0.0]
-    for (H, Cin, K, R, st, pd, cnt) in shapes(a.batch):
+    rows = None if a.layers is None else {int(v) for v in a.layers.split(",")}
+    want = set(a.ops.split(","))
+    for li, (H, Cin, K, R, st, pd, cnt) in enumerate(shapes(a.batch)):
+        if rows is not None and li not in rows:
+            continue
         Hin = 224 if Cin == 3 else H  # the table's H is the input size (stem: output)
         sh = g.ConvShape(a.batch, Hin, Hin, Cin, K, R, R, st, pd)
         x = torch.randn(a.batch, Hin, Hin, Cin, device=dev)
@@ -59,7 +65,7 @@ def main():
         line = f"H{Hin:3d} {Cin:3d}->{K:3d} {R}x{R} s{st} x{cnt}:"
         res = []
         for i, (name, fn) in enumerate(ops.items()):
-            if name == "dgrad" and Cin == 3:
+            if (name == "dgrad" and Cin == 3) or name not in want:
                 res.append(0.0)
                 continue
             for _ in range(3):

@@ -393,8 +393,9 @@ def test_conv_dgrad_gradient_join(cuda_dev, N, H, Cin, K, R, stride, pad, bf16):
     s = stream_handle()
     dx0 = torch.empty(N, H, H, Cin, device=cuda_dev)
     dx1 = torch.empty_like(dx0)
-    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx0), ptr(ws), s, bf16)
-    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx1), ptr(ws), s, bf16, 0, ptr(add))
+    dyb = dy.to(torch.bfloat16) if bf16 else None  # the pipelined bf16-operand kernel
+    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx0), ptr(ws), s, bf16, ptr(dyb))
+    g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx1), ptr(ws), s, bf16, ptr(dyb), ptr(add))
     torch.cuda.synchronize()
     assert torch.equal(dx1, dx0 + add)
 
