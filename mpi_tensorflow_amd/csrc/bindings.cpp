@@ -199,12 +199,13 @@ PYBIND11_MODULE(_C, m) {
   });
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
                        bool relu, uintptr_t ws, uintptr_t st, bool bf16, uintptr_t xb,
-                       uintptr_t wtb) {
+                       uintptr_t wtb, uintptr_t yb) {
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
-                   P<float>(ws), S(st), bf16, P<const void>(xb), P<const void>(wtb));
+                   P<float>(ws), S(st), bf16, P<const void>(xb), P<const void>(wtb), P<void>(yb));
     check_launch();
   }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
-     py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0, py::arg("wtb") = 0);
+     py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0, py::arg("wtb") = 0,
+     py::arg("yb") = 0);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
                             uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend,
                             uintptr_t wtb) {
@@ -238,20 +239,27 @@ PYBIND11_MODULE(_C, m) {
   g.def("bn_fwd", [](uintptr_t x, long long rows, int C, uintptr_t gm, uintptr_t bt, uintptr_t res,
                      uintptr_t y, uintptr_t mean, uintptr_t rstd, uintptr_t ws, float eps,
                      float momentum, bool relu, bool training, uintptr_t rmean, uintptr_t rvar,
-                     uintptr_t st, uintptr_t yb) {
-    gops::bn_fwd(P<const float>(x), rows, C, P<const float>(gm), P<const float>(bt),
+                     uintptr_t st, uintptr_t yb, bool x_bf16) {
+    gops::bn_fwd(P<const void>(x), rows, C, P<const float>(gm), P<const float>(bt),
                  P<const float>(res), P<float>(y), P<float>(mean), P<float>(rstd), P<float>(ws), eps,
-                 momentum, relu, training, P<float>(rmean), P<float>(rvar), S(st), P<void>(yb));
+                 momentum, relu, training, P<float>(rmean), P<float>(rvar), S(st), P<void>(yb),
+                 x_bf16);
     check_launch();
-  });
+  }, py::arg("x"), py::arg("rows"), py::arg("C"), py::arg("g"), py::arg("b"), py::arg("res"),
+     py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("ws"), py::arg("eps"),
+     py::arg("momentum"), py::arg("relu"), py::arg("training"), py::arg("rmean"), py::arg("rvar"),
+     py::arg("st"), py::arg("yb") = 0, py::arg("x_bf16") = false);
   g.def("bn_bwd", [](uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                      uintptr_t gm, long long rows, int C, bool relu, uintptr_t ws, uintptr_t dg,
-                     uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st, uintptr_t dxb) {
-    gops::bn_bwd(P<const float>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
+                     uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st, uintptr_t dxb,
+                     bool x_bf16) {
+    gops::bn_bwd(P<const void>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
                  P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(ws), P<float>(dg),
-                 P<float>(db), P<float>(dx), P<float>(dres), S(st), P<void>(dxb));
+                 P<float>(db), P<float>(dx), P<float>(dres), S(st), P<void>(dxb), x_bf16);
     check_launch();
-  });
+  }, py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("g"),
+     py::arg("rows"), py::arg("C"), py::arg("relu"), py::arg("ws"), py::arg("dg"), py::arg("db"),
+     py::arg("dx"), py::arg("dres"), py::arg("st"), py::arg("dxb") = 0, py::arg("x_bf16") = false);
   g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {
     gops::maxpool_fwd(p, P<const float>(x), P<float>(y), P<int>(arg), S(st));
     check_launch();

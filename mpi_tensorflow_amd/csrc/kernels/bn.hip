@@ -36,6 +36,18 @@ namespace bn {
 enum Mode { SUM_SQ = 0, SUM_PROD = 1, BN_BWD = 2 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+// 4 consecutive elements of x at element offset i: fp32, or (XB) bf16 - the
+// bf16 conv outputs of the ResNet bf16 path, half the bytes of every x read
+template <bool XB>
+__device__ __forceinline__ float4 ldx(const void* p, size_t i) {
+  if constexpr (XB) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const __bf16*>(p) + i);
+    return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+  }
+}
 // 4 floats -> 4 bf16 (round to nearest even, as to_bf16_kernel)
 __device__ __forceinline__ uint2 pack4(float4 a) {
   __bf16 v[4] = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w};
@@ -53,7 +65,8 @@ struct Fin {
   float* rstd;
   float* rmean;
   float* rvar;
-  const float* shift;
+  const void* shift;  // row 0 of x (fp32, or bf16 when shift_b16)
+  int shift_b16;
 };
 
 __device__ __forceinline__ void fin_channel(const Fin& f, int c, float a, float b, long long rows) {
@@ -69,7 +82,11 @@ __device__ __forceinline__ void fin_channel(const Fin& f, int c, float a, float 
     const float inv = 1.f / (float)rows;
     const float ms = a * inv;  // mean of the shifted data
     const float var = fmaxf(b * inv - ms * ms, 0.f);
-    const float m = ms + (f.shift ? f.shift[c] : 0.f);
+    float k = 0.f;
+    if (f.shift)
+      k = f.shift_b16 ? (float)reinterpret_cast<const __bf16*>(f.shift)[c]
+                      : reinterpret_cast<const float*>(f.shift)[c];
+    const float m = ms + k;
     f.mean[c] = m;
     f.rstd[c] = rsqrtf(var + f.eps);
     if (f.rmean) {  // torch semantics: unbiased variance in the running estimate
@@ -103,11 +120,11 @@ __device__ __forceinline__ void fold_rows(float4 (*red)[PT], int cq, int RP, int
 // (<= 256) and the last block's sum of them is short.
 constexpr int PT = 1024;
 
-template <int MODE>
-__global__ __launch_bounds__(PT) void partial_kernel(const float* __restrict__ a,
+template <int MODE, bool XB>
+__global__ __launch_bounds__(PT) void partial_kernel(const void* __restrict__ a,
                                                      const float* __restrict__ b,
                                                      const float* __restrict__ yv,
-                                                     const float* __restrict__ mean,
+                                                     const void* __restrict__ mean,
                                                      const float* __restrict__ rstd, int relu,
                                                      long long rows, int C, int rows_per_block,
                                                      float* __restrict__ part) {
@@ -122,15 +139,15 @@ __global__ __launch_bounds__(PT) void partial_kernel(const float* __restrict__ a
   float4 mu = s1, rs = s1;
   if (rl < RP) {
     if (MODE == BN_BWD) {
-      mu = ld4(mean + 4 * q);
+      mu = ld4(reinterpret_cast<const float*>(mean) + 4 * q);
       rs = ld4(rstd + 4 * q);
     } else if (MODE == SUM_SQ && mean) {
-      mu = ld4(mean + 4 * q);  // shifted data: sums of (x - K), K = a sample of the channel
+      mu = ldx<XB>(mean, 4 * q);  // shifted data: sums of (x - K), K = a sample of the channel
     }
 #pragma unroll 4
     for (long long r = r0 + rl; r < r1; r += RP) {
       const size_t o = (size_t)r * C + 4 * q;
-      const float4 v = ld4(a + o);
+      const float4 v = ldx<XB>(a, o);
       if (MODE == SUM_SQ) {
         const float4 w = make_float4(v.x - mu.x, v.y - mu.y, v.z - mu.z, v.w - mu.w);
         s1.x += w.x; s1.y += w.y; s1.z += w.z; s1.w += w.w;
@@ -222,7 +239,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
 }
 
 // y = (x - mean) rstd g + b (+ res) (relu); eval: mean / var from running stats
-__global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
+template <bool XB>
+__global__ __launch_bounds__(256) void apply_kernel(const void* __restrict__ x,
                                                     const float* __restrict__ mean,
                                                     const float* __restrict__ rstd,
                                                     const float* __restrict__ g,
@@ -235,7 +253,7 @@ __global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
   const int cq = C >> 2;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const int c = (int)(i % cq) * 4;
-    const float4 v = ld4(x + 4 * i);
+    const float4 v = ldx<XB>(x, 4 * i);
     float4 m = ld4(mean + c), r = ld4(rstd + c);
     if (eval) {
       r.x = rsqrtf(r.x + eps); r.y = rsqrtf(r.y + eps); r.z = rsqrtf(r.z + eps); r.w = rsqrtf(r.w + eps);
@@ -258,9 +276,11 @@ __global__ __launch_bounds__(256) void apply_kernel(const float* __restrict__ x,
   }
 }
 
-// dx = g rstd (dy' - s1/rows - xhat s2/rows); dres = dy' (residual branch)
+// dx = g rstd (dy' - s1/rows - xhat s2/rows); dres = dy' (residual branch).
+// dx (fp32) and dxb (bf16) are each optional.
+template <bool XB>
 __global__ __launch_bounds__(256) void bwd_apply_kernel(
-    const float* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
+    const void* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ s1, const float* __restrict__ s2, float* __restrict__ dx,
     float* __restrict__ dres, long long n4, int C, long long rows, int relu,
@@ -279,14 +299,14 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
       d.w = yy.w > 0.f ? d.w : 0.f;
     }
     if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
-    const float4 v = ld4(x + 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
+    const float4 v = ldx<XB>(x, 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
     const float4 a = ld4(s1 + c), b = ld4(s2 + c);
     float4 o;
     o.x = gg.x * r.x * (d.x - a.x * inv - (v.x - m.x) * r.x * b.x * inv);
     o.y = gg.y * r.y * (d.y - a.y * inv - (v.y - m.y) * r.y * b.y * inv);
     o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
     o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
-    *reinterpret_cast<float4*>(dx + 4 * i) = o;
+    if (dx) *reinterpret_cast<float4*>(dx + 4 * i) = o;
     if (dxb) dxb[i] = pack4(o);
   }
 }
@@ -320,25 +340,35 @@ long long chan_reduce_ws_floats(long long rows, int C) {
   return chan_reduce_ok(C) ? (long long)bn::nblocks(rows, C) * 2 * C : 0;
 }
 
-static void run_partials(int mode, const float* a, const float* b, const float* y,
-                         const float* mean, const float* rstd, int relu, long long rows, int C,
-                         float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
+template <bool XB>
+static void run_partials_t(int mode, const void* a, const float* b, const float* y,
+                           const void* mean, const float* rstd, int relu, long long rows, int C,
+                           float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
   const int rpb = (int)((rows + nb - 1) / nb);
   switch (mode) {
     case bn::SUM_SQ:
-      bn::partial_kernel<bn::SUM_SQ><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_SQ, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     case bn::SUM_PROD:
-      bn::partial_kernel<bn::SUM_PROD><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_PROD, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     default:
-      bn::partial_kernel<bn::BN_BWD><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::BN_BWD, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
   }
   bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, fin);
 }
 
+static void run_partials(int mode, const void* a, bool ab16, const float* b, const float* y,
+                         const void* mean, const float* rstd, int relu, long long rows, int C,
+                         float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
+  if (ab16)
+    run_partials_t<true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+  else
+    run_partials_t<false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+}
+
 static bn::Fin sums(float* s1, float* s2) {
-  return {s1, s2, 0, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr};
+  return {s1, s2, 0, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 }
 
 void chan_reduce(const float* a, const float* b, long long rows, int C, float* s1, float* s2,
@@ -346,7 +376,7 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
   if (!chan_reduce_ok(C)) throw std::runtime_error("chan_reduce: unsupported channel count");
   const int nb = bn::nblocks(rows, C);
   if (C % 4 == 0 && C <= 1024) {
-    run_partials(mode, a, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, sums(s1, s2), st);
+    run_partials(mode, a, false, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, sums(s1, s2), st);
   } else {
     const int rpb = (int)((rows + nb - 1) / nb);
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
@@ -354,38 +384,51 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
   }
 }
 
-void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
+void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
             float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
-            void* yb) {
+            void* yb, bool xb16) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_fwd: needs C % 4 == 0, C <= 1024");
   const long long n4 = rows * C / 4;
+  uint2* ybv = reinterpret_cast<uint2*>(yb);
   if (training) {
     const int nb = bn::nblocks(rows, C);
     // shift K = row 0 of x (passed as the partials' `mean`)
-    const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x};
-    run_partials(bn::SUM_SQ, x, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, fin, st);
-    bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
-                                                          relu ? 1 : 0, 0, eps,
-                                                          reinterpret_cast<uint2*>(yb));
+    const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x, xb16 ? 1 : 0};
+    run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, fin, st);
+    if (xb16)
+      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
+                                                                 relu ? 1 : 0, 0, eps, ybv);
+    else
+      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4,
+                                                                  C, relu ? 1 : 0, 0, eps, ybv);
   } else {
-    bn::apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4, C,
-                                                          relu ? 1 : 0, 1, eps,
-                                                          reinterpret_cast<uint2*>(yb));
+    if (xb16)
+      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
+                                                                 C, relu ? 1 : 0, 1, eps, ybv);
+    else
+      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
+                                                                  C, relu ? 1 : 0, 1, eps, ybv);
   }
 }
 
-void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
+void bn_bwd(const void* x, const float* dy, const float* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st, void* dxb) {
+            float* dx, float* dres, hipStream_t st, void* dxb, bool xb16) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
+  if (!dx && !dxb) throw std::runtime_error("bn_bwd: no dx output");
   const int nb = bn::nblocks(rows, C);
   // db = sum dy', dg = sum dy' xhat
-  run_partials(bn::BN_BWD, x, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, sums(db, dg), st);
+  run_partials(bn::BN_BWD, x, xb16, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, sums(db, dg),
+               st);
   const long long n4 = rows * C / 4;
-  bn::bwd_apply_kernel<<<bn::grid_elems(n4), 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx,
-                                                            dres, n4, C, rows, relu ? 1 : 0,
-                                                            reinterpret_cast<uint2*>(dxb));
+  uint2* dxbv = reinterpret_cast<uint2*>(dxb);
+  if (xb16)
+    bn::bwd_apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(
+        x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0, dxbv);
+  else
+    bn::bwd_apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(
+        x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0, dxbv);
 }
 
 }  // namespace gops

@@ -213,7 +213,8 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
                                                  const __bf16* __restrict__ wt,
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps,
-                                                 const float* __restrict__ addend) {
+                                                 const float* __restrict__ addend,
+                                                 __bf16* __restrict__ yb) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int STAGE = (BM + BN) * LDK;  // bf16 elements
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
@@ -274,7 +275,10 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
         float v = acc[i][j][q] + bv;
         if (relu) v = fmaxf(v, 0.f);
         if (addend) v += addend[(size_t)m * s.K + co];  // gradient junction (dX accumulate)
-        y[(size_t)m * s.K + co] = v;
+        if (yb)  // bf16 output (unsplit only): the conv feeds a bf16-input BatchNorm
+          yb[(size_t)m * s.K + co] = (__bf16)v;
+        else
+          y[(size_t)m * s.K + co] = v;
       }
   }
 }
@@ -326,7 +330,8 @@ template <int BM, int BN, int RB>
 __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __restrict__ x,
                                                    const __bf16* __restrict__ wt,
                                                    float* __restrict__ y, int cps,
-                                                   const float* __restrict__ addend) {
+                                                   const float* __restrict__ addend,
+                                                   __bf16* __restrict__ yb) {
   using h3::ROWB;
   using h3::HCAP;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -455,7 +460,14 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
     for (int j = 0; j < TN; ++j) {
       const int co = n0 + wn * (BN / 2) + 32 * j + r;
       float* p = y + (size_t)mb * K + co;
-      if (full && addend) {
+      if (yb) {  // bf16 output (unsplit, no addend): feeds a bf16-input BatchNorm
+        __bf16* pb = yb + (size_t)mb * K + co;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = (q & 3) + 8 * (q >> 2);
+          if (full || mb + rr < M) pb[(size_t)rr * K] = (__bf16)acc[i][j][q];
+        }
+      } else if (full && addend) {
         const float* ap = addend + (size_t)mb * K + co;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -651,7 +663,8 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
                                                         long long zs, long long n4,
                                                         float4* __restrict__ out,
-                                                        const float4* __restrict__ addend) {
+                                                        const float4* __restrict__ addend,
+                                                        uint2* __restrict__ outb) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
@@ -669,7 +682,12 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
       a.z += b.z;
       a.w += b.w;
     }
-    out[i] = a;
+    if (outb) {
+      const __bf16 hv[4] = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w};
+      outb[i] = __builtin_bit_cast(uint2, hv);
+    } else {
+      out[i] = a;
+    }
   }
 }
 
@@ -698,8 +716,9 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 
 // Deterministic sum of nz slabs of n4 float4s into out (fixed association
 // order for a given nz).
+// outb: bf16 output instead of out
 static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st,
-                        const float* addend = nullptr) {
+                        const float* addend = nullptr, __bf16* outb = nullptr) {
   long long b = (n4 + 255) / 256;
   if (b > 4096) b = 4096;
   int G = 1;
@@ -710,7 +729,8 @@ static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStrea
   }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), cdiv(nz, G),
                                           n4 * G, n4, reinterpret_cast<float4*>(out),
-                                          reinterpret_cast<const float4*>(addend));
+                                          reinterpret_cast<const float4*>(addend),
+                                          reinterpret_cast<uint2*>(outb));
 }
 
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
@@ -754,22 +774,23 @@ static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 1
 template <class XT>
 static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const float* bias,
                    float* y, bool relu, float* ws, hipStream_t st,
-                   const float* addend = nullptr) {
+                   const float* addend = nullptr, __bf16* yb = nullptr) {
   const long long M = (long long)s.N * s.OH * s.OW;
   const Plan p = plan(s, bias != nullptr || relu);
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const float* add = p.z > 1 ? nullptr : addend;  // split-K: added by the slab reduction
+  __bf16* ob = p.z > 1 ? nullptr : yb;             // ... and converted there
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
-    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
-    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
-    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
   }
 #undef GRID
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
 }
 
 // halo conv: 3x3, stride 1, pad 1, C and K % 64 == 0, a 128-pixel tile's
@@ -796,14 +817,15 @@ static inline P3 plan3(const ConvShape& s) {
   return {cdiv(nch, cps), cps};
 }
 static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
-                    hipStream_t st, const float* addend) {
+                    hipStream_t st, const float* addend, __bf16* yb = nullptr) {
   const long long M = (long long)s.N * s.H * s.W;
   const P3 p = plan3(s);
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const dim3 grid(cdiv(M, 128) * (s.K / 64), p.z);
-  conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, p.z > 1 ? nullptr : addend);
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend);
+  conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, p.z > 1 ? nullptr : addend,
+                                                p.z > 1 ? nullptr : yb);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
 }
 
 // wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
@@ -1210,7 +1232,8 @@ void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t
 }
 
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                   bool relu, float* ws, hipStream_t st, const void* xb, const void* wtb) {
+                   bool relu, float* ws, hipStream_t st, const void* xb, const void* wtb,
+                   void* yb) {
   using namespace cbf;
   if (!conv_fwd_bf16_ok(s) || !ws) throw std::runtime_error("conv_fwd_bf16: unsupported shape");
   const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
@@ -1219,12 +1242,13 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
     convert(s, w, 0, wc, st);
     wt = wc;
   }
+  __bf16* ob = reinterpret_cast<__bf16*>(yb);
   if (xb && !bias && !relu && conv3_ok(s))
-    launch3(s, reinterpret_cast<const __bf16*>(xb), wt, y, ws, st, nullptr);
+    launch3(s, reinterpret_cast<const __bf16*>(xb), wt, y, ws, st, nullptr, ob);
   else if (xb)
-    launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st);
+    launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st, nullptr, ob);
   else
-    launch(s, x, wt, bias, y, relu, ws, st);
+    launch(s, x, wt, bias, y, relu, ws, st, nullptr, ob);
 }
 
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,

@@ -270,20 +270,22 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
 // and likewise kw, so each phase is a dense implicit GEMM over its own tap
 // list (no zero MFMA work for stride 2).  Block z-dimension = phase.
 // K tile = (phase tap, 32-channel chunk of co).  Requires K % 32 == 0, C % 4 == 0.
-template <int BM, int BN>
+// DT: element type of dY in global memory (float, or __bf16 when the
+// gradient arrives as the bf16 output of a bf16-input BatchNorm backward)
+template <int BM, int BN, class DT = float>
 struct DataLoader {
   static constexpr int AR = BM * BK / 4 / NT;
   static constexpr int BR = BN * BK / 4 / NT;
   ConvShape s;
-  const float* dy;
+  const DT* dy;
   const float* w;
   int n0, cchunks, nkw, kh0, kw0;
-  const float* abase[AR];
+  const DT* abase[AR];
   int qy[AR], qx[AR];  // iy + p, ix + p
   bool av[AR];
   float4 ra[AR], rb[BR];
   bool bv[BR];
-  __device__ DataLoader(const ConvShape& s_, const float* dy_, const float* w_, int m0, int n0_,
+  __device__ DataLoader(const ConvShape& s_, const DT* dy_, const float* w_, int m0, int n0_,
                         int py, int px, int PH, int PW, int nkw_, int kh0_, int kw0_)
       : s(s_), dy(dy_), w(w_), n0(n0_), nkw(nkw_), kh0(kh0_), kw0(kw0_) {
     cchunks = s.K / BK;
@@ -311,7 +313,16 @@ struct DataLoader {
       const int oy = (qy[i] - kh) / s.stride, ox = (qx[i] - kw) / s.stride;  // exact by phase
       const bool ok = av[i] && qy[i] >= kh && qx[i] >= kw && oy < s.OH && ox < s.OW;
       const int oyc = min(max(oy, 0), s.OH - 1), oxc = min(max(ox, 0), s.OW - 1);
-      ra[i] = sel4(ok, *reinterpret_cast<const float4*>(abase[i] + ((size_t)oyc * s.OW + oxc) * s.K + co0));
+      const DT* src = abase[i] + ((size_t)oyc * s.OW + oxc) * s.K + co0;
+      float4 v;
+      if constexpr (sizeof(DT) == 2) {
+        const uint2 u = *reinterpret_cast<const uint2*>(src);
+        v = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                        __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+      } else {
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      ra[i] = sel4(ok, v);
     }
     // B[k = co][n = ci] = W[kh, kw, ci, co]: float4 along co for one ci
     const int tid = threadIdx.x, c4 = tid & 7;
@@ -332,11 +343,10 @@ struct DataLoader {
   }
 };
 
-template <int BM, int BN, int P>
-__global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __restrict__ dy,
-                                                  const float* __restrict__ w,
-                                                  float* __restrict__ dx, int kps,
-                                                  const float* __restrict__ addend) {
+template <int BM, int BN, int P, class DT>
+__device__ __forceinline__ void data_body(const ConvShape& s, const DT* __restrict__ dy,
+                                          const float* __restrict__ w, float* __restrict__ dx,
+                                          int kps, const float* __restrict__ addend) {
   // addend (unsplit only): a gradient that joins dX at this tensor, added in
   // the epilogue instead of by a separate elementwise pass
   // split-K over gridDim.z: slice z writes the raw slab dx + z * N*H*W*C
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __re
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
   if (m0 >= M) return;  // phases with fewer pixels than the grid covers
-  DataLoader<BM, BN> ld(s, dy, w, m0, n0, py, px, PH, PW, nkw > 0 ? nkw : 1, kh0, kw0);
+  DataLoader<BM, BN, DT> ld(s, dy, w, m0, n0, py, px, PH, PW, nkw > 0 ? nkw : 1, kh0, kw0);
   f32x16 acc[G::TM][G::TN];
   const int nk = nkh * nkw * (s.K / BK), kb = blockIdx.z * kps;
   mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
@@ -379,6 +389,21 @@ __global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __re
         }
       }
   }
+}
+
+template <int BM, int BN, int P>
+__global__ __launch_bounds__(NT) void data_kernel(ConvShape s, const float* __restrict__ dy,
+                                                  const float* __restrict__ w,
+                                                  float* __restrict__ dx, int kps,
+                                                  const float* __restrict__ addend) {
+  data_body<BM, BN, P, float>(s, dy, w, dx, kps, addend);
+}
+template <int BM, int BN, int P>
+__global__ __launch_bounds__(NT) void data_b16_kernel(ConvShape s, const __bf16* __restrict__ dy,
+                                                      const float* __restrict__ w,
+                                                      float* __restrict__ dx, int kps,
+                                                      const float* __restrict__ addend) {
+  data_body<BM, BN, P, __bf16>(s, dy, w, dx, kps, addend);
 }
 
 // ----------------------------------------------------- backward-filter ----
@@ -770,7 +795,7 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st, bool bf16, const float* addend) {
+                         hipStream_t st, bool bf16, const float* addend, const void* dyb) {
   using namespace tiled;
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
@@ -782,7 +807,12 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
   // phases no tap reaches (odd pixels of a 1x1 stride-2 conv) run zero K
   // tiles and write zeros
 #define GRID(BM_, BN_) dim3(cdiv(Mph, BM_) * cdiv(s.C, BN_), sd * sd, z)
-  TILED_DISPATCH(t, data_kernel, GRID, s, dy, w, out, kps, z > 1 ? nullptr : addend)
+  if (!dy && dyb) {  // dY only as bf16: bf16 loads, converted in registers
+    const __bf16* d16 = reinterpret_cast<const __bf16*>(dyb);
+    TILED_DISPATCH(t, data_b16_kernel, GRID, s, d16, w, out, kps, z > 1 ? nullptr : addend)
+  } else {
+    TILED_DISPATCH(t, data_kernel, GRID, s, dy, w, out, kps, z > 1 ? nullptr : addend)
+  }
 #undef GRID
   if (z > 1) slab_sum(ws, z, (long long)s.N * s.H * s.W * s.C, dx, st, addend);
 }

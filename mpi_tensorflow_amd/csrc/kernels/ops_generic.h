@@ -23,9 +23,10 @@ struct PoolShape {
 // xb / dyb: optional bf16 copies of x / dy (to_bf16) for the bf16 family
 // wtb (optional, bf16 family): the weights already laid out by wcvt_batch
 // (forward copy for conv_fwd, stride-1 dgrad copy for conv_bwd_data)
+// yb (optional, bf16 family only): write the output as bf16 there instead of y
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
               bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr,
-              const void* wtb = nullptr);
+              const void* wtb = nullptr, void* yb = nullptr);
 // addend (optional, bf16 / tiled families): a gradient that joins dX at this
 // tensor (a residual branch), added in the epilogue: dx = conv + addend
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
@@ -47,7 +48,7 @@ void to_bf16(const float* x, void* y, long long n, hipStream_t st);
 void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr,
-                   const void* wtb = nullptr);
+                   const void* wtb = nullptr, void* yb = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                         hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr,
                         const void* wtb = nullptr);
@@ -67,8 +68,10 @@ bool conv_bwd_data_tiled_ok(const ConvShape& s);
 bool conv_bwd_filter_tiled_ok(const ConvShape& s);
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                     bool relu, float* ws, hipStream_t st, bool bf16);
+// dy may be null when dyb (bf16 dY) is given
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st, bool bf16, const float* addend = nullptr);
+                         hipStream_t st, bool bf16, const float* addend = nullptr,
+                         const void* dyb = nullptr);
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
 int conv_filter_tiled_splits(const ConvShape& s);
@@ -88,15 +91,17 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 // training: batch statistics -> mean / rstd, running stats updated in place
 // (momentum, unbiased var); eval: normalise with rmean / rvar.  y = BN(x)
 // (+ res) (ReLU).
-void bn_fwd(const float* x, long long rows, int C, const float* g, const float* b,
+// x: fp32, or bf16 when xb16 (the ResNet bf16 path's conv outputs)
+void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
             float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
-            void* yb = nullptr);  // yb: optional bf16 copy of y
-// dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu)
-void bn_bwd(const float* x, const float* dy, const float* y, const float* mean, const float* rstd,
+            void* yb = nullptr,  // yb: optional bf16 copy of y
+            bool xb16 = false);
+// dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu);
+// dx (fp32) and dxb (bf16) are each optional, at least one is required
+void bn_bwd(const void* x, const float* dy, const float* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st,
-            void* dxb = nullptr);  // dxb: optional bf16 copy of dx
+            float* dx, float* dres, hipStream_t st, void* dxb = nullptr, bool xb16 = false);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);

@@ -765,8 +765,11 @@ static inline bool conv_fwd_direct_ok(const ConvShape& s) {
 // 3-channel stem); the per-element gather engine above covers the rest
 // (LeNet-5's 3- and 6-channel layers, thin FC layers).
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-              bool relu, float* ws, hipStream_t st, bool bf16, const void* xb, const void* wtb) {
-  if (bf16 && conv_fwd_bf16_ok(s)) return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb, wtb);
+              bool relu, float* ws, hipStream_t st, bool bf16, const void* xb, const void* wtb,
+              void* yb) {
+  if (bf16 && conv_fwd_bf16_ok(s))
+    return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb, wtb, yb);
+  if (yb) throw std::runtime_error("conv_fwd: bf16 output needs the bf16 conv family");
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
   if (conv_fwd_direct_ok(s)) {
     const long long total = (long long)s.N * s.OH * s.OW * s.K;
@@ -808,7 +811,9 @@ void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* d
                    const void* wtb) {
   if (bf16 && conv_bwd_data_bf16_ok(s))
     return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb, addend, wtb);
-  if (conv_bwd_data_tiled_ok(s)) return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend);
+  if (conv_bwd_data_tiled_ok(s))
+    return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend, dyb);
+  if (!dy) throw std::runtime_error("conv_bwd_data: this shape needs the fp32 dY");
   if (addend) throw std::runtime_error("conv_bwd_data: no gradient-join epilogue for this shape");
   if (s.C < 32 && (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX && (s.K == 8 || s.K == 16)) {
     const int b = grid1d((long long)s.N * s.H * s.W * s.C);

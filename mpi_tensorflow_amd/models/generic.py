@@ -166,7 +166,9 @@ class ResNet18(GenericModel):
             return Fn.batchnorm(h, P[nm + "_g"], P[nm + "_b"], rm, rv, training, relu, res,
                                 res_join=res_join)
 
-        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3)
+        # every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
+        # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise
+        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True)
         h = BN(h, "bn1", True)
         h = Fn.maxpool(h, 3, 2, 1)
         join = x.is_cuda and training and torch.is_grad_enabled()
@@ -175,11 +177,13 @@ class ResNet18(GenericModel):
             # conv1 dgrad epilogue (Fn.GradJoin); the shortcut runs after c2
             # so its backward comes first
             j = Fn.GradJoin() if join else None
-            o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final")
+            o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final",
+                          out_bf16=True)
             o = BN(o, name + "n1", True)
-            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1)
+            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True)
             if down:
-                sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash")
+                sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash",
+                               out_bf16=True)
                 h = BN(o, name + "n2", True, res=BN(sc, name + "nd", False))
             else:
                 h = BN(o, name + "n2", True, res=h, res_join=j)

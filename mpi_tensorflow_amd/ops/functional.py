@@ -133,6 +133,8 @@ def _attach_bf16(t: torch.Tensor, tb: torch.Tensor) -> None:
 
 
 def _bf16_copy(t: torch.Tensor, s) -> torch.Tensor:
+    if t.dtype == torch.bfloat16:  # already bf16 (a bf16-input BatchNorm's dX)
+        return t.contiguous()
     a = getattr(t, "_mta_bf16", None)
     if a is not None and a[1] == t._version and a[2] == t.data_ptr() and t.is_contiguous():
         return a[0]
@@ -181,10 +183,9 @@ class GradJoin:
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None, wtb=None,
-                wtb_d=None):
+                wtb_d=None, out_bf16=False):
         C = native()
         x = x.contiguous()
-        y = _empty((shape.N, shape.OH, shape.OW, shape.K), x)
         ctx.bf16 = _CONV_BF16
         s = stream_handle()
         # bf16 family: the conv reads a bf16 copy of its input (half the
@@ -192,8 +193,11 @@ class _ConvFn(torch.autograd.Function):
         xb = None
         if ctx.bf16 and C.ops.conv_bf16_ok(shape):
             xb = _bf16_copy(x, s)
-        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), ptr(y), relu, ptr(ws), s, ctx.bf16,
-                       ptr(xb), ptr(wtb))
+        # out_bf16: the output is stored as bf16 (it feeds a bf16-input BatchNorm)
+        oshape = (shape.N, shape.OH, shape.OW, shape.K)
+        y = torch.empty(oshape, dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
+        C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), 0 if out_bf16 else ptr(y), relu, ptr(ws), s,
+                       ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0)
         ctx.save_for_backward(x, w, y, xb)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
@@ -206,6 +210,24 @@ class _ConvFn(torch.autograd.Function):
         x, w, y, xb = ctx.saved_tensors
         s = stream_handle()
         dy = dy.contiguous()
+        if dy.dtype == torch.bfloat16:  # from a bf16-input BatchNorm: the bf16 kernels only
+            dyb = dy
+            C.ops.conv_bwd_filter(ctx.shape, ptr(x), 0, ptr(ctx.ws), ptr(ctx.gw), s, True,
+                                  ptr(xb), ptr(dyb))
+            _grad_done(ctx.gw)
+            dx = None
+            if ctx.needs_input_grad[0]:
+                sh = ctx.shape
+                dx = _empty((sh.N, sh.H, sh.W, sh.C), x)
+                add = ctx.join.take() if ctx.role == "final" else None
+                C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
+                                    ptr(add), ptr(ctx.wtb_d))
+                if ctx.role == "stash":
+                    ctx.join.stash(dx)
+                    dx = None
+                elif ctx.role == "final" and add is None:
+                    ctx.join.out = dx
+            return dx, None, None, None, None, None, None, None, None, None, None, None, None
         if ctx.relu:
             dym = torch.empty_like(dy)
             C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
@@ -232,7 +254,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = None
             elif ctx.role == "final" and add is None:
                 ctx.join.out = dx
-        return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvIm2colFn(torch.autograd.Function):
@@ -245,7 +267,7 @@ class _ConvIm2colFn(torch.autograd.Function):
     stem)."""
 
     @staticmethod
-    def forward(ctx, x, w, shape, gw, ws, kp):
+    def forward(ctx, x, w, shape, gw, ws, kp, out_bf16=False):
         C = native()
         x = x.contiguous()
         sh = shape
@@ -258,8 +280,10 @@ class _ConvIm2colFn(torch.autograd.Function):
         wpad.view(kp, sh.K)[:sh.R * seg].view(sh.R, seg, sh.K)[:, :sc].copy_(
             w.reshape(sh.R, sc, sh.K))
         s1 = C.ops.ConvShape(sh.N, sh.OH, sh.OW, kp, sh.K, 1, 1, 1, 0)
-        y = _empty((sh.N, sh.OH, sh.OW, sh.K), x)
-        C.ops.conv_fwd(s1, 0, ptr(wpad), 0, ptr(y), False, ptr(ws), s, True, ptr(col))
+        y = torch.empty((sh.N, sh.OH, sh.OW, sh.K),
+                        dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
+        C.ops.conv_fwd(s1, 0, ptr(wpad), 0, 0 if out_bf16 else ptr(y), False, ptr(ws), s, True,
+                       ptr(col), 0, ptr(y) if out_bf16 else 0)
         ctx.save_for_backward(col)
         ctx.s1, ctx.R, ctx.sc, ctx.seg, ctx.gw, ctx.ws = s1, sh.R, sc, seg, gw, ws
         return y
@@ -277,7 +301,7 @@ class _ConvIm2colFn(torch.autograd.Function):
         ctx.gw.view(ctx.R, ctx.sc, s1.K).copy_(
             gpad[:ctx.R * ctx.seg].view(ctx.R, ctx.seg, s1.K)[:, :ctx.sc])
         _grad_done(ctx.gw)
-        return None, None, None, None, None, None
+        return None, None, None, None, None, None, None
 
 
 def _im2col_kp(sh, x: torch.Tensor, has_bias: bool, relu: bool) -> int:
@@ -323,20 +347,25 @@ _WS = ConvWorkspace()
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: int = 0,
            relu: bool = False, join: Optional[GradJoin] = None,
-           join_role: Optional[str] = None) -> torch.Tensor:
+           join_role: Optional[str] = None, out_bf16: bool = False) -> torch.Tensor:
     """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K].  join / join_role
     ("stash" | "final"): fuse the gradient sum at x with another branch (see
-    GradJoin); GPU only, ignored on the CPU path."""
+    GradJoin).  out_bf16: store the output as bf16 when the bf16 conv family
+    runs it (no bias / ReLU epilogue) - for a conv whose only consumer is
+    `batchnorm`, which reads bf16 input.  Both are GPU only, ignored on the
+    CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
     if x.is_cuda:
         C = native()
         sh = C.ops.ConvShape(N, H, W, Cin, K, R, S, stride, pad)
         kp = _im2col_kp(sh, x, b is not None, relu)
+        ob = bool(out_bf16 and _CONV_BF16 and b is None and not relu)
         if kp:
             s1 = C.ops.ConvShape(N, sh.OH, sh.OW, kp, K, 1, 1, 1, 0)
             ws = _WS.get(max(C.ops.conv_ws_floats(s1, False), 4), x.device)
-            return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp)
+            return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob)
+        ob = ob and C.ops.conv_bf16_ok(sh)
         nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
                   C.ops.chan_reduce_ws_floats(N * sh.OH * sh.OW, K), 4)
         ws = _WS.get(nws, x.device)
@@ -345,7 +374,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
                              None if b is None else b.grad_view, ws, join, join_role, w.wtb,
-                             w.wtb_d)
+                             w.wtb_d, ob)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y
@@ -403,7 +432,8 @@ class _BNFn(torch.autograd.Function):
         x = x.contiguous()
         Cc = x.shape[-1]
         rows = x.numel() // Cc
-        y = torch.empty_like(x)
+        xb16 = x.dtype == torch.bfloat16  # a bf16-output conv's activations
+        y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         mean = torch.empty(Cc, device=x.device)
         rstd = torch.empty(Cc, device=x.device)
         ws = _WS.get(max(C.ops.chan_reduce_ws_floats(rows, Cc), 4), x.device)
@@ -411,7 +441,7 @@ class _BNFn(torch.autograd.Function):
         # batch statistics, running-stat update and the fused apply, on device
         C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(y), ptr(mean), ptr(rstd),
                      ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle(),
-                     ptr(yb))
+                     ptr(yb), xb16)
         if yb is not None:
             _attach_bf16(y, yb)
         ctx.save_for_backward(x, y, mean, rstd, g)
@@ -427,13 +457,21 @@ class _BNFn(torch.autograd.Function):
         dy = dy.contiguous()
         Cc = x.shape[-1]
         rows = x.numel() // Cc
-        dx = torch.empty_like(dy)
+        xb16 = x.dtype == torch.bfloat16
         dres = torch.empty_like(dy) if ctx.has_res else None
-        dxb = _bf16_out(dx)
+        if xb16:
+            # the gradient of a bf16 input is bf16 (autograd's dtype contract):
+            # only the bf16 dX is written - the producing conv's backward reads
+            # nothing else
+            dx = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+            dxf, dxb = None, dx
+        else:
+            dx = torch.empty_like(dy)
+            dxf, dxb = dx, _bf16_out(dx)
         C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
-                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dx), ptr(dres), stream_handle(),
-                     ptr(dxb))
-        if dxb is not None:
+                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dxf), ptr(dres), stream_handle(),
+                     ptr(dxb), xb16)
+        if dxf is not None and dxb is not None:
             _attach_bf16(dx, dxb)
         _grad_done(ctx.gg, ctx.gb)
         if dres is not None and ctx.res_join is not None:
@@ -455,11 +493,11 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
             return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
                                rvar, momentum, eps, True, res_join)
         C = native()
-        y = torch.empty_like(x)
+        y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         Cc = x.shape[-1]
         C.ops.bn_fwd(ptr(x.contiguous()), x.numel() // Cc, Cc, ptr(g.value), ptr(b.value),
                      ptr(res), ptr(y), 0, 0, 0, eps, momentum, relu, False, ptr(rmean),
-                     ptr(rvar), stream_handle(), 0)
+                     ptr(rvar), stream_handle(), 0, x.dtype == torch.bfloat16)
         return y
     xn = x.permute(0, 3, 1, 2)
     y = F.batch_norm(xn, rmean, rvar, g.value, b.value, training, momentum, eps).permute(0, 2, 3, 1)

@@ -452,3 +452,74 @@ def test_bn_single_launch_reduction_repeatable(cuda_dev):
     yr.backward(dy.cpu().double().permute(0, 3, 1, 2))
     assert _rel(outs[0][0].cpu(), yr.detach().permute(0, 2, 3, 1)) < 1e-5
     assert _rel(outs[0][1].cpu(), xr.grad.permute(0, 2, 3, 1)) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,Cin,K,R,stride,pad", [
+    (4, 14, 64, 64, 3, 1, 1),     # halo conv, unsplit
+    (4, 7, 512, 512, 3, 1, 1),    # halo conv, split-K: bf16 written by the slab reduction
+    (2, 14, 64, 128, 3, 2, 1),    # generic bf16 forward; stride-2 dgrad from bf16 dY (tiled)
+    (2, 14, 64, 128, 1, 2, 0),    # 1x1 stride-2 downsample
+    (2, 20, 3, 64, 7, 2, 3),      # stem: bf16 im2col route
+])
+def test_conv_bf16_output_and_bf16_grad(cuda_dev, N, H, Cin, K, R, stride, pad):
+    """bf16-stored conv output (out_bf16, the ResNet bf16 path) and the
+    backward fed a bf16 dY (what a bf16-input BatchNorm returns) vs fp32 torch."""
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, H, H, Cin, generator=g)
+    w = torch.randn(R, R, Cin, K, generator=g) * 0.1
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, OH, OH, K, generator=g)
+    xr = x.clone().requires_grad_(Cin % 4 == 0)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), stride=stride,
+                  padding=pad).permute(0, 2, 3, 1)
+    yr.backward(dy.to(torch.bfloat16).float())
+    xg = x.to(cuda_dev).requires_grad_(Cin % 4 == 0)
+    wp = _param(w.to(cuda_dev))
+    Fn.set_conv_bf16(True)
+    try:
+        yg = Fn.conv2d(xg, wp, None, stride, pad, False, out_bf16=True)
+        assert yg.dtype == torch.bfloat16
+        yg.backward(dy.to(cuda_dev).to(torch.bfloat16))
+    finally:
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    assert _rel(yg.float().cpu(), yr.detach()) < 1e-2
+    assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-2
+    if Cin % 4 == 0:
+        assert _rel(xg.grad.cpu(), xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
+def test_batchnorm_bf16_input(cuda_dev, relu, res):
+    """BN over a bf16 input (a bf16-output conv's activations): statistics,
+    apply and backward read the bf16 tensor; dX comes back bf16.  Reference:
+    fp32 torch on the same bf16-rounded input."""
+    g = torch.Generator().manual_seed(2)
+    x = (torch.randn(8, 10, 10, 64, generator=g) * 2 + 0.5).to(torch.bfloat16)
+    r = torch.randn(8, 10, 10, 64, generator=g)
+    gam = torch.rand(64, generator=g) + 0.5
+    bet = torch.randn(64, generator=g)
+    dy = torch.randn(8, 10, 10, 64, generator=g)
+    xr = x.float().requires_grad_(True)
+    yr = F.batch_norm(xr.permute(0, 3, 1, 2), None, None, gam, bet, True, 0.1, 1e-5).permute(0, 2, 3, 1)
+    if res:
+        yr = yr + r
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(dy)
+    xg = x.to(cuda_dev).requires_grad_(True)
+    gp, bp = _param(gam.to(cuda_dev)), _param(bet.to(cuda_dev))
+    rm, rv = torch.zeros(64, device=cuda_dev), torch.ones(64, device=cuda_dev)
+    yg = Fn.batchnorm(xg, gp, bp, rm, rv, True, relu, r.to(cuda_dev) if res else None)
+    assert yg.dtype == torch.float32
+    yg.backward(dy.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert xg.grad.dtype == torch.bfloat16
+    assert _rel(yg.cpu(), yr.detach()) < 1e-5
+    assert _rel(xg.grad.float().cpu(), xr.grad) < 1e-2  # bf16 rounding of dX
+    assert _rel(gp.grad_view.cpu(), gam.grad if gam.grad is not None else
+                (dy * (yr > 0 if relu else torch.ones_like(yr)) *
+                 ((xr - xr.mean((0, 1, 2))) / (xr.var((0, 1, 2), unbiased=False) + 1e-5).sqrt())
+                 ).sum((0, 1, 2)).detach()) < 1e-4
+    assert torch.allclose(rm.cpu(), 0.1 * x.float().mean(dim=(0, 1, 2)), atol=1e-5)
