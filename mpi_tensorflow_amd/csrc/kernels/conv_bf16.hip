@@ -214,7 +214,10 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps,
                                                  const float* __restrict__ addend,
-                                                 __bf16* __restrict__ yb) {
+                                                 __bf16* __restrict__ yb, int ex2) {
+  // ex2 (unsplit): the 1x1 stride-2 backward-data - rows are dY pixels
+  // (n, a, b), written to dX pixel (2a, 2b) of the 2x-sized output with the
+  // other three pixels of its 2x2 block zero (plus addend everywhere)
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int STAGE = (BM + BN) * LDK;  // bf16 elements
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
@@ -260,6 +263,27 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
       if (more) ld.store(nxt, nxt + BM * LDK);
       __syncthreads();
     }
+  }
+  if (ex2) {
+    const size_t K = s.K, W2 = 2 * (size_t)s.OW;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (BN / 2) + 32 * j + r;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q, lane);
+          if (m >= M) continue;
+          const int b = m % s.OW, t = m / s.OW;  // t = n * OH + a
+          const size_t o = ((size_t)(2 * t) * W2 + 2 * b) * K + co;  // (n, 2a, 2b)
+          const size_t o2[4] = {o, o + K, o + W2 * K, o + W2 * K + K};
+          const float v[4] = {acc[i][j][q], 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[o2[e]] = addend ? v[e] + addend[o2[e]] : v[e];
+        }
+    }
+    return;
   }
   y += (size_t)blockIdx.y * M * s.K;
 #pragma unroll
@@ -774,9 +798,9 @@ static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 1
 template <class XT>
 static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const float* bias,
                    float* y, bool relu, float* ws, hipStream_t st,
-                   const float* addend = nullptr, __bf16* yb = nullptr) {
+                   const float* addend = nullptr, __bf16* yb = nullptr, int ex2 = 0) {
   const long long M = (long long)s.N * s.OH * s.OW;
-  const Plan p = plan(s, bias != nullptr || relu);
+  const Plan p = plan(s, bias != nullptr || relu || ex2);  // ex2: never split
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const float* add = p.z > 1 ? nullptr : addend;  // split-K: added by the slab reduction
@@ -784,10 +808,10 @@ static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const floa
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
-    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
-    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
-    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
   }
 #undef GRID
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
@@ -1139,9 +1163,16 @@ static void wgrad3(const ConvShape& s, const __bf16* xb, const __bf16* dyb, floa
 
 bool conv_fwd_bf16_ok(const ConvShape& s) { return s.C % 64 == 0 && s.K % 64 == 0; }
 bool conv_bwd_filter_bf16_ok(const ConvShape& s) { return s.C % 64 == 0 && s.K % 64 == 0; }
+// 1x1, stride 2, no padding, even input: dX = dY W^T on the even pixels, zero elsewhere
+static bool dgrad_1x1s2(const ConvShape& s) {
+  return s.R == 1 && s.S == 1 && s.stride == 2 && s.pad == 0 && s.H == 2 * s.OH &&
+         s.W == 2 * s.OW;
+}
 bool conv_bwd_data_bf16_ok(const ConvShape& s) {
-  return s.C % 64 == 0 && s.K % 64 == 0 && s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 &&
-         s.OH == s.H + 2 * s.pad - s.R + 1 && s.OW == s.W + 2 * s.pad - s.S + 1;
+  if (s.C % 64 != 0 || s.K % 64 != 0) return false;
+  return dgrad_1x1s2(s) ||
+         (s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 &&
+          s.OH == s.H + 2 * s.pad - s.R + 1 && s.OW == s.W + 2 * s.pad - s.S + 1);
 }
 
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
@@ -1260,6 +1291,17 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
     __bf16* wc = reinterpret_cast<__bf16*>(ws);
     convert(s, w, 1, wc, st);
     wt = wc;
+  }
+  if (dgrad_1x1s2(s)) {  // a 1x1 GEMM over the dY pixels, 2x2-expanding epilogue
+    ConvShape d = dgrad_shape(s);
+    d.H = d.OH = s.OH;
+    d.W = d.OW = s.OW;
+    if (dyb)
+      launch(d, reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st, addend,
+             nullptr, 1);
+    else
+      launch(d, dy, wt, nullptr, dx, false, ws, st, addend, nullptr, 1);
+    return;
   }
   if (dyb && conv3_ok(dgrad_shape(s)))
     launch3(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend);

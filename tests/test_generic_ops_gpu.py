@@ -374,6 +374,7 @@ def test_batchnorm_large_mean_channels(cuda_dev):
     (4, 14, 64, 64, 3, 1, 1, True),  # bf16 family, one K slab
     (4, 7, 512, 512, 3, 1, 1, True),  # bf16 family, split-K slab reduction
     (4, 14, 64, 128, 3, 2, 1, True),  # stride 2: tiled family
+    (4, 14, 128, 64, 1, 2, 0, True),  # 1x1 stride 2: GEMM with the 2x2-expanding epilogue
     (4, 14, 64, 64, 3, 1, 1, False),  # fp32 tiled
     (2, 28, 128, 128, 3, 2, 1, False),
 ])
