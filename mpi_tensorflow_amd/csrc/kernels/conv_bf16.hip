@@ -515,6 +515,162 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
   }
 }
 
+// ------------------------------- 3x3 stride-2 backward-data (halo form) ----
+// dX of a 3x3 / stride 2 / pad 1 conv on an even input: output pixel
+// (2a + py, 2b + px) takes only the taps of its parity class -
+//   py = 0: kh = 1 reading dY row a;  py = 1: kh = 0 reading row a + 1 and
+//   kh = 2 reading row a  (likewise px / kw / columns)
+// - so a block owns 128 dY-grid pixels (n, a, b) x 64 input channels and
+// keeps FOUR accumulator sets, one per class: each of the 9 taps is one
+// 128 x 64 x 64 MFMA step into its class, reading the dY halo (the tile's
+// stacked rows plus one below) at a per-lane (+1 row / +1 column) shift.
+// Same staging as conv3_kernel: halo and weight ring by LDS-DMA, swizzled
+// 128-byte rows, zero row for shifts past the image; weights in the
+// stride-1 dgrad layout (taps reversed, [tap'][ci][co]).  Replaces the
+// phase-split tiled kernel on these layers (45-56 us at B = 32).
+template <int BM, int BN, int RB>
+__global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16* __restrict__ dy,
+                                                      const __bf16* __restrict__ wt,
+                                                      float* __restrict__ dx, int cps,
+                                                      const float* __restrict__ addend) {
+  using h3::ROWB;
+  using h3::HCAP;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int GB = BN / 32;
+  constexpr int HB = (HCAP + 1) * ROWB;
+  constexpr int BSZ = BN * ROWB;
+  static_assert(RB >= 3 && RB <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[HB + RB * BSZ];
+  const int OH = s.OH, OW = s.OW;
+  const int M = s.N * OH * OW;  // dY-grid pixels
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;  // n: input channel ci
+  const int nch = s.K / BK;  // reduction over output channels co
+  const int cc0 = blockIdx.y * cps, cc1 = min(nch, cc0 + cps);
+  const int g_first = m0 / OW, g_last = (min(m0 + BM, M) - 1) / OW;
+  const long long hbase = (long long)g_first * OW;  // global dY pixel of halo row 0
+  const int npix = (g_last - g_first + 2) * OW;
+  const int nins = (npix + 7) >> 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5, lr = lane >> 3;
+  if (tid < 8) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  int gl[TM], bs[TM], as[TM];
+  bool mv[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / 2) + 32 * i + r;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : m0;
+    const int g = mm / OW;
+    bs[i] = mm - g * OW;
+    as[i] = g % OH;
+    gl[i] = g - g_first;
+  }
+  const __bf16* bsrc[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = wave * (BN / 4) + 8 * j + lr;
+    bsrc[j] = wt + (size_t)(n0 + row) * s.K + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  auto issue_b = [&](int tap, int cc, int slot) {  // original tap (kh, kw) = (tap / 3, tap % 3)
+    const size_t o = (size_t)(8 - tap) * s.C * s.K + (size_t)cc * BK;
+    char* dst = smem + HB + slot * BSZ + wave * (BN / 4) * ROWB;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) h3::glds(bsrc[j] + o, dst + 8 * j * ROWB);
+  };
+  auto issue_halo = [&](int cc) {
+    for (int ins = wave; ins < nins; ins += 4) {
+      const int p = 8 * ins + lr;
+      const long long gp = hbase + p;
+      const bool ok = p < npix && gp < M;
+      const void* src = ok ? (const void*)(dy + gp * s.K + (size_t)cc * BK +
+                                           8 * ((lane & 7) ^ ((p >> 1) & 7)))
+                           : (const void*)h3::g_zero;
+      h3::glds(src, smem + ins * 8 * ROWB);
+    }
+  };
+  f32x16 acc[4][TM][TN];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[c][i][j] = zero16();
+  for (int cc = cc0; cc < cc1; ++cc) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_halo(cc);
+#pragma unroll
+    for (int t = 0; t < RB - 1; ++t) issue_b(t, cc, t);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ahead = min(RB - 2, 8 - t);
+      if (ahead >= 2)
+        h3::wait_vm<2 * GB>();
+      else if (ahead == 1)
+        h3::wait_vm<GB>();
+      else
+        h3::wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + RB - 1 < 9) issue_b(t + RB - 1, cc, (t + RB - 1) % RB);
+      const int kh = t / 3, kw = t - 3 * kh;
+      const int cls = (kh != 1 ? 2 : 0) + (kw != 1 ? 1 : 0);  // (py, px)
+      const int dh = kh == 0 ? 1 : 0, dw = kw == 0 ? 1 : 0;
+      int hrow[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool ok = mv[i] && as[i] + dh < OH && bs[i] + dw < OW;
+        hrow[i] = ok ? (gl[i] + dh) * OW + bs[i] + dw : HCAP;
+      }
+      const char* B = smem + HB + (t % RB) * BSZ;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int c = 2 * ks + h;
+        bfx8 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const bfx8*>(smem + hrow[i] * ROWB +
+                                                ((c ^ ((hrow[i] >> 1) & 7)) << 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int R = wn * (BN / 2) + 32 * j + r;
+          b[j] = *reinterpret_cast<const bfx8*>(B + R * ROWB + ((c ^ ((R >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[cls][i][j] =
+                __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[cls][i][j], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: grid pixel m = (n, a, b) -> dX pixels (n, 2a + py, 2b + px)
+  dx += (size_t)blockIdx.y * s.N * s.H * s.W * s.C;
+  const size_t C = s.C, W = s.W;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int ci = n0 + wn * (BN / 2) + 32 * j + r;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q, lane);
+        if (m >= M) continue;
+        const int b = m % OW, g = m / OW;  // g = n * OH + a
+        const size_t o = ((size_t)(2 * g) * W + 2 * b) * C + ci;  // (n, 2a, 2b)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const size_t oc = o + (c >> 1) * W * C + (c & 1) * C;
+          const float v = acc[c][i][j][q];
+          dx[oc] = addend ? v + addend[oc] : v;
+        }
+      }
+    }
+}
+
 // ----------------------------------------------------- backward-filter ----
 // dW[tap][ci][co] = sum_pix X[pix shifted by tap][ci] dY[pix][co].  GEMM
 // M = (tap, ci), N = co, reduction over output pixels; block = (128-row M
@@ -852,6 +1008,40 @@ static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
 }
 
+// 3x3 / stride 2 / pad 1 dgrad on an even input (the halo form above)
+static bool dgrad3s2_ok(const ConvShape& s) {
+  return s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && s.H == 2 * s.OH &&
+         s.W == 2 * s.OW && s.C % 64 == 0 && s.K % 64 == 0 &&
+         ((128 + s.OW - 2) / s.OW + 2) * s.OW <= h3::HCAP &&
+         (long long)s.N * s.H * s.W * s.C < (1LL << 31);
+}
+// split-K over co chunks up to one block per CU (measured: splitting only
+// below 128 blocks - fewer 4x-sized dX slabs - was no faster, 2.70 vs 2.69 ms)
+static inline P3 plan3s2(const ConvShape& s) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const long long blocks = (long long)cdiv(M, 128) * (s.C / 64);
+  const int nch = s.K / BK;
+  int z = 1;
+  if (blocks < 256) {
+    z = cdiv(256, blocks);
+    if (z > nch) z = nch;
+  }
+  const int cps = cdiv(nch, z);
+  return {cdiv(nch, cps), cps};
+}
+static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, float* dx,
+                      float* ws, hipStream_t st, const float* addend) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const P3 p = plan3s2(s);
+  float* slabs = ws + wt_floats(s);
+  float* out = p.z > 1 ? slabs : dx;
+  const dim3 grid(cdiv(M, 128) * (s.C / 64), p.z);
+  dgrad3s2_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, dy, wt, out, p.cps,
+                                                   p.z > 1 ? nullptr : addend);
+  if (p.z > 1)
+    slab_reduce(slabs, p.z, (long long)s.N * s.H * s.W * s.C / 4, dx, st, addend);
+}
+
 // wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
 // at least 4 K tiles per slice, at most 64 slices
 struct WgPlan {
@@ -1170,7 +1360,7 @@ static bool dgrad_1x1s2(const ConvShape& s) {
 }
 bool conv_bwd_data_bf16_ok(const ConvShape& s) {
   if (s.C % 64 != 0 || s.K % 64 != 0) return false;
-  return dgrad_1x1s2(s) ||
+  return dgrad_1x1s2(s) || cbf::dgrad3s2_ok(s) ||
          (s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 &&
           s.OH == s.H + 2 * s.pad - s.R + 1 && s.OW == s.W + 2 * s.pad - s.S + 1);
 }
@@ -1192,6 +1382,10 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
   if (conv_bwd_data_bf16_ok(s)) {
     const ConvShape d = dgrad_shape(s);
     n = std::max(n, wt_floats(d) + slab_floats(d, false));
+    if (dgrad3s2_ok(s)) {
+      const P3 q = plan3s2(s);
+      if (q.z > 1) n = std::max(n, wt_floats(s) + (long long)q.z * s.N * s.H * s.W * s.C);
+    }
   }
   if (conv_bwd_filter_bf16_ok(s)) {
     const WgPlan p = wg_plan(s);
@@ -1291,6 +1485,10 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
     __bf16* wc = reinterpret_cast<__bf16*>(ws);
     convert(s, w, 1, wc, st);
     wt = wc;
+  }
+  if (dgrad3s2_ok(s)) {
+    if (dyb) return launch3s2(s, reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend);
+    return conv_bwd_data_tiled(s, dy, w, dx, ws, st, true, addend);  // fp32 dY only
   }
   if (dgrad_1x1s2(s)) {  // a 1x1 GEMM over the dY pixels, 2x2-expanding epilogue
     ConvShape d = dgrad_shape(s);
