@@ -252,14 +252,15 @@ PYBIND11_MODULE(_C, m) {
   g.def("bn_bwd", [](uintptr_t x, uintptr_t dy, uintptr_t y, uintptr_t mean, uintptr_t rstd,
                      uintptr_t gm, long long rows, int C, bool relu, uintptr_t ws, uintptr_t dg,
                      uintptr_t db, uintptr_t dx, uintptr_t dres, uintptr_t st, uintptr_t dxb,
-                     bool x_bf16) {
-    gops::bn_bwd(P<const void>(x), P<const float>(dy), P<const float>(y), P<const float>(mean),
+                     bool x_bf16, bool y_bf16) {
+    gops::bn_bwd(P<const void>(x), P<const float>(dy), P<const void>(y), P<const float>(mean),
                  P<const float>(rstd), P<const float>(gm), rows, C, relu, P<float>(ws), P<float>(dg),
-                 P<float>(db), P<float>(dx), P<float>(dres), S(st), P<void>(dxb), x_bf16);
+                 P<float>(db), P<float>(dx), P<float>(dres), S(st), P<void>(dxb), x_bf16, y_bf16);
     check_launch();
   }, py::arg("x"), py::arg("dy"), py::arg("y"), py::arg("mean"), py::arg("rstd"), py::arg("g"),
      py::arg("rows"), py::arg("C"), py::arg("relu"), py::arg("ws"), py::arg("dg"), py::arg("db"),
-     py::arg("dx"), py::arg("dres"), py::arg("st"), py::arg("dxb") = 0, py::arg("x_bf16") = false);
+     py::arg("dx"), py::arg("dres"), py::arg("st"), py::arg("dxb") = 0, py::arg("x_bf16") = false,
+     py::arg("y_bf16") = false);
   g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {
     gops::maxpool_fwd(p, P<const float>(x), P<float>(y), P<int>(arg), S(st));
     check_launch();

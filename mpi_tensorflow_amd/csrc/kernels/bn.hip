@@ -120,10 +120,11 @@ __device__ __forceinline__ void fold_rows(float4 (*red)[PT], int cq, int RP, int
 // (<= 256) and the last block's sum of them is short.
 constexpr int PT = 1024;
 
-template <int MODE, bool XB>
+// XB: x is bf16; YB: the ReLU-mask tensor y is the bf16 twin of the output
+template <int MODE, bool XB, bool YB>
 __global__ __launch_bounds__(PT) void partial_kernel(const void* __restrict__ a,
                                                      const float* __restrict__ b,
-                                                     const float* __restrict__ yv,
+                                                     const void* __restrict__ yv,
                                                      const void* __restrict__ mean,
                                                      const float* __restrict__ rstd, int relu,
                                                      long long rows, int C, int rows_per_block,
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(PT) void partial_kernel(const void* __restrict__ a,
       } else {  // a = x, b = dy, yv = y (relu mask)
         float4 d = ld4(b + o);
         if (relu) {
-          const float4 yy = ld4(yv + o);
+          const float4 yy = ldx<YB>(yv, o);
           d.x = yy.x > 0.f ? d.x : 0.f;
           d.y = yy.y > 0.f ? d.y : 0.f;
           d.z = yy.z > 0.f ? d.z : 0.f;
@@ -271,16 +272,16 @@ __global__ __launch_bounds__(256) void apply_kernel(const void* __restrict__ x,
     if (relu) {
       o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
     }
-    *reinterpret_cast<float4*>(y + 4 * i) = o;
+    if (y) *reinterpret_cast<float4*>(y + 4 * i) = o;  // null: the bf16 twin only
     if (yb) yb[i] = pack4(o);
   }
 }
 
 // dx = g rstd (dy' - s1/rows - xhat s2/rows); dres = dy' (residual branch).
 // dx (fp32) and dxb (bf16) are each optional.
-template <bool XB>
+template <bool XB, bool YB>
 __global__ __launch_bounds__(256) void bwd_apply_kernel(
-    const void* __restrict__ x, const float* __restrict__ dy, const float* __restrict__ y,
+    const void* __restrict__ x, const float* __restrict__ dy, const void* __restrict__ y,
     const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
     const float* __restrict__ s1, const float* __restrict__ s2, float* __restrict__ dx,
     float* __restrict__ dres, long long n4, int C, long long rows, int relu,
@@ -292,7 +293,7 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
     const int c = (int)(i % cq) * 4;
     float4 d = ld4(dy + 4 * i);
     if (relu) {
-      const float4 yy = ld4(y + 4 * i);
+      const float4 yy = ldx<YB>(y, 4 * i);
       d.x = yy.x > 0.f ? d.x : 0.f;
       d.y = yy.y > 0.f ? d.y : 0.f;
       d.z = yy.z > 0.f ? d.z : 0.f;
@@ -340,31 +341,35 @@ long long chan_reduce_ws_floats(long long rows, int C) {
   return chan_reduce_ok(C) ? (long long)bn::nblocks(rows, C) * 2 * C : 0;
 }
 
-template <bool XB>
-static void run_partials_t(int mode, const void* a, const float* b, const float* y,
+template <bool XB, bool YB>
+static void run_partials_t(int mode, const void* a, const float* b, const void* y,
                            const void* mean, const float* rstd, int relu, long long rows, int C,
                            float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
   const int rpb = (int)((rows + nb - 1) / nb);
   switch (mode) {
     case bn::SUM_SQ:
-      bn::partial_kernel<bn::SUM_SQ, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_SQ, XB, YB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     case bn::SUM_PROD:
-      bn::partial_kernel<bn::SUM_PROD, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::SUM_PROD, XB, YB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
       break;
     default:
-      bn::partial_kernel<bn::BN_BWD, XB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
+      bn::partial_kernel<bn::BN_BWD, XB, YB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
   }
   bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, fin);
 }
 
-static void run_partials(int mode, const void* a, bool ab16, const float* b, const float* y,
-                         const void* mean, const float* rstd, int relu, long long rows, int C,
-                         float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
-  if (ab16)
-    run_partials_t<true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+static void run_partials(int mode, const void* a, bool ab16, const float* b, const void* y,
+                         bool yb16, const void* mean, const float* rstd, int relu, long long rows,
+                         int C, float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
+  if (ab16 && yb16)
+    run_partials_t<true, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+  else if (ab16)
+    run_partials_t<true, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+  else if (yb16)
+    run_partials_t<false, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
   else
-    run_partials_t<false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+    run_partials_t<false, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
 }
 
 static bn::Fin sums(float* s1, float* s2) {
@@ -376,7 +381,8 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
   if (!chan_reduce_ok(C)) throw std::runtime_error("chan_reduce: unsupported channel count");
   const int nb = bn::nblocks(rows, C);
   if (C % 4 == 0 && C <= 1024) {
-    run_partials(mode, a, false, b, nullptr, nullptr, nullptr, 0, rows, C, ws, nb, sums(s1, s2), st);
+    run_partials(mode, a, false, b, nullptr, false, nullptr, nullptr, 0, rows, C, ws, nb,
+                 sums(s1, s2), st);
   } else {
     const int rpb = (int)((rows + nb - 1) / nb);
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
@@ -395,7 +401,8 @@ void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b
     const int nb = bn::nblocks(rows, C);
     // shift K = row 0 of x (passed as the partials' `mean`)
     const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x, xb16 ? 1 : 0};
-    run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, x, nullptr, 0, rows, C, ws, nb, fin, st);
+    run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, false, x, nullptr, 0, rows, C, ws, nb, fin,
+                 st);
     if (xb16)
       bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
                                                                  relu ? 1 : 0, 0, eps, ybv);
@@ -412,23 +419,31 @@ void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b
   }
 }
 
-void bn_bwd(const void* x, const float* dy, const float* y, const float* mean, const float* rstd,
+void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st, void* dxb, bool xb16) {
+            float* dx, float* dres, hipStream_t st, void* dxb, bool xb16, bool yb16) {
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
   if (!dx && !dxb) throw std::runtime_error("bn_bwd: no dx output");
   const int nb = bn::nblocks(rows, C);
   // db = sum dy', dg = sum dy' xhat
-  run_partials(bn::BN_BWD, x, xb16, dy, y, mean, rstd, relu ? 1 : 0, rows, C, ws, nb, sums(db, dg),
-               st);
+  run_partials(bn::BN_BWD, x, xb16, dy, y, yb16, mean, rstd, relu ? 1 : 0, rows, C, ws, nb,
+               sums(db, dg), st);
   const long long n4 = rows * C / 4;
   uint2* dxbv = reinterpret_cast<uint2*>(dxb);
-  if (xb16)
-    bn::bwd_apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(
-        x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0, dxbv);
+  const int rl = relu ? 1 : 0;
+  const int gr = bn::grid_elems(n4);
+#define BWD_APPLY(XB_, YB_)                                                               \
+  bn::bwd_apply_kernel<XB_, YB_><<<gr, 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx, dres, \
+                                                     n4, C, rows, rl, dxbv)
+  if (xb16 && yb16)
+    BWD_APPLY(true, true);
+  else if (xb16)
+    BWD_APPLY(true, false);
+  else if (yb16)
+    BWD_APPLY(false, true);
   else
-    bn::bwd_apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(
-        x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0, dxbv);
+    BWD_APPLY(false, false);
+#undef BWD_APPLY
 }
 
 }  // namespace gops

@@ -982,19 +982,23 @@ static bool conv3_ok(const ConvShape& s) {
 }
 // 64-channel output tiles; split-K over channel chunks up to one block per CU
 struct P3 {
-  int z, cps;
+  int z, cps, bm;
 };
+// 128-pixel tiles when they fill the chip; otherwise (the small-M deep
+// layers) 64-pixel tiles, split-K over channel chunks only below 128 blocks
+// (split-K slabs cost a ~7 us reduction launch per conv)
 static inline P3 plan3(const ConvShape& s) {
   const long long M = (long long)s.N * s.H * s.W;
-  const long long blocks = (long long)cdiv(M, 128) * (s.K / 64);
   const int nch = s.C / BK;
+  if ((long long)cdiv(M, 128) * (s.K / 64) >= 256) return {1, nch, 128};
+  const long long blocks = (long long)cdiv(M, 64) * (s.K / 64);
   int z = 1;
-  if (blocks < 256) {
+  if (blocks < 128) {
     z = cdiv(256, blocks);
     if (z > nch) z = nch;
   }
   const int cps = cdiv(nch, z);
-  return {cdiv(nch, cps), cps};
+  return {cdiv(nch, cps), cps, 64};
 }
 static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
                     hipStream_t st, const float* addend, __bf16* yb = nullptr) {
@@ -1002,9 +1006,13 @@ static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float
   const P3 p = plan3(s);
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
-  const dim3 grid(cdiv(M, 128) * (s.K / 64), p.z);
-  conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, p.z > 1 ? nullptr : addend,
-                                                p.z > 1 ? nullptr : yb);
+  const dim3 grid(cdiv(M, p.bm) * (s.K / 64), p.z);
+  const float* add = p.z > 1 ? nullptr : addend;
+  __bf16* ob = p.z > 1 ? nullptr : yb;
+  if (p.bm == 128)
+    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob);
+  else
+    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob);
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
 }
 
@@ -1027,7 +1035,7 @@ static inline P3 plan3s2(const ConvShape& s) {
     if (z > nch) z = nch;
   }
   const int cps = cdiv(nch, z);
-  return {cdiv(nch, cps), cps};
+  return {cdiv(nch, cps), cps, 128};
 }
 static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, float* dx,
                       float* ws, hipStream_t st, const float* addend) {

@@ -91,17 +91,20 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 // training: batch statistics -> mean / rstd, running stats updated in place
 // (momentum, unbiased var); eval: normalise with rmean / rvar.  y = BN(x)
 // (+ res) (ReLU).
-// x: fp32, or bf16 when xb16 (the ResNet bf16 path's conv outputs)
+// x: fp32, or bf16 when xb16 (the ResNet bf16 path's conv outputs); y may be
+// null when yb is given (only the bf16 twin is written)
 void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
             float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
             void* yb = nullptr,  // yb: optional bf16 copy of y
             bool xb16 = false);
 // dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu);
-// dx (fp32) and dxb (bf16) are each optional, at least one is required
-void bn_bwd(const void* x, const float* dy, const float* y, const float* mean, const float* rstd,
+// dx (fp32) and dxb (bf16) are each optional, at least one is required;
+// y (the ReLU mask) is the fp32 output, or its bf16 twin when yb16
+void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, const float* rstd,
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
-            float* dx, float* dres, hipStream_t st, void* dxb = nullptr, bool xb16 = false);
+            float* dx, float* dres, hipStream_t st, void* dxb = nullptr, bool xb16 = false,
+            bool yb16 = false);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);

@@ -161,10 +161,10 @@ class ResNet18(GenericModel):
         return d
 
     def forward(self, P, bn, x, training):
-        def BN(h, nm, relu, res=None, res_join=None):
+        def BN(h, nm, relu, res=None, res_join=None, twin_only=False):
             rm, rv = bn[nm]
             return Fn.batchnorm(h, P[nm + "_g"], P[nm + "_b"], rm, rv, training, relu, res,
-                                res_join=res_join)
+                                res_join=res_join, twin_only=twin_only)
 
         # every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
         # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise
@@ -179,7 +179,7 @@ class ResNet18(GenericModel):
             j = Fn.GradJoin() if join else None
             o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final",
                           out_bf16=True)
-            o = BN(o, name + "n1", True)
+            o = BN(o, name + "n1", True, twin_only=True)  # only conv c2 reads it
             o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True)
             if down:
                 sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash",

@@ -427,7 +427,7 @@ def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) ->
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, b, res, relu, gg, gb, rmean, rvar, momentum, eps, training,
-                res_join=None):
+                res_join=None, twin_only=False):
         C = native()
         x = x.contiguous()
         Cc = x.shape[-1]
@@ -438,13 +438,18 @@ class _BNFn(torch.autograd.Function):
         rstd = torch.empty(Cc, device=x.device)
         ws = _WS.get(max(C.ops.chan_reduce_ws_floats(rows, Cc), 4), x.device)
         yb = _bf16_out(y)
+        # twin_only: the only consumer is a bf16 conv, so only the bf16 twin is
+        # written (y's fp32 storage stays unwritten; the twin is attached)
+        yf = None if (twin_only and yb is not None) else y
         # batch statistics, running-stat update and the fused apply, on device
-        C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(y), ptr(mean), ptr(rstd),
+        C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(yf), ptr(mean), ptr(rstd),
                      ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle(),
                      ptr(yb), xb16)
         if yb is not None:
             _attach_bf16(y, yb)
-        ctx.save_for_backward(x, y, mean, rstd, g)
+        # the backward's ReLU mask reads the bf16 twin when there is one (same signs)
+        ctx.yb16 = yb is not None
+        ctx.save_for_backward(x, yb if yb is not None else y, mean, rstd, g)
         ctx.relu, ctx.gg, ctx.gb, ctx.has_res = relu, gg, gb, res is not None
         ctx.ws = ws
         ctx.res_join = res_join
@@ -470,28 +475,30 @@ class _BNFn(torch.autograd.Function):
             dxf, dxb = dx, _bf16_out(dx)
         C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
                      ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dxf), ptr(dres), stream_handle(),
-                     ptr(dxb), xb16)
+                     ptr(dxb), xb16, ctx.yb16)
         if dxf is not None and dxb is not None:
             _attach_bf16(dx, dxb)
         _grad_done(ctx.gg, ctx.gb)
         if dres is not None and ctx.res_join is not None:
             ctx.res_join.stash(dres)
             dres = None
-        return dx, None, None, dres, None, None, None, None, None, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
 
 
 def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: torch.Tensor,
               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None,
               momentum: float = 0.1, eps: float = 1e-5,
-              res_join: Optional[GradJoin] = None) -> torch.Tensor:
+              res_join: Optional[GradJoin] = None, twin_only: bool = False) -> torch.Tensor:
     """BatchNorm over N,H,W of an NHWC tensor, optional fused residual + ReLU.
     res_join: the residual's gradient is stashed there (GradJoin) instead of
-    returned to autograd (GPU training only)."""
+    returned to autograd.  twin_only: the output's only consumer is a bf16
+    conv - write just its bf16 twin (bf16 conv mode; the returned fp32 tensor
+    is not written).  Both GPU training only."""
     if x.is_cuda:
         res = None if residual is None else residual.contiguous()
         if training:
             return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
-                               rvar, momentum, eps, True, res_join)
+                               rvar, momentum, eps, True, res_join, twin_only)
         C = native()
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         Cc = x.shape[-1]

@@ -524,3 +524,31 @@ def test_batchnorm_bf16_input(cuda_dev, relu, res):
                  ((xr - xr.mean((0, 1, 2))) / (xr.var((0, 1, 2), unbiased=False) + 1e-5).sqrt())
                  ).sum((0, 1, 2)).detach()) < 1e-4
     assert torch.allclose(rm.cpu(), 0.1 * x.float().mean(dim=(0, 1, 2)), atol=1e-5)
+
+
+def test_bn_twin_only_feeds_conv_identically(cuda_dev):
+    """batchnorm(twin_only=True) writes only the bf16 twin of its output; a
+    bf16 conv reading it gives bit-identical outputs and gradients to the
+    full fp32 + twin version (and the ReLU mask comes from the twin)."""
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(4, 12, 12, 64, generator=g).to(torch.bfloat16).to(cuda_dev)
+    w = (torch.randn(3, 3, 64, 64, generator=g) * 0.1).to(cuda_dev)
+    gam, bet = (torch.rand(64, generator=g) + 0.5).to(cuda_dev), torch.randn(64, generator=g).to(cuda_dev)
+    dy = torch.randn(4, 12, 12, 64, generator=g).to(torch.bfloat16).to(cuda_dev)
+    out = []
+    Fn.set_conv_bf16(True)
+    try:
+        for twin in (False, True):
+            xi = x.clone().requires_grad_(True)
+            gp, bp, wp = _param(gam), _param(bet), _param(w)
+            rm, rv = torch.zeros(64, device=cuda_dev), torch.ones(64, device=cuda_dev)
+            h = Fn.batchnorm(xi, gp, bp, rm, rv, True, True, twin_only=twin)
+            y = Fn.conv2d(h, wp, None, 1, 1, False, out_bf16=True)
+            y.backward(dy)
+            out.append((y.detach().clone(), xi.grad.clone(), wp.grad_view.clone(),
+                        gp.grad_view.clone(), bp.grad_view.clone()))
+    finally:
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    for a_, b_ in zip(*out):
+        assert torch.equal(a_, b_)
