@@ -214,6 +214,15 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
      py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0, py::arg("wtb") = 0);
+  g.def("stem_weight_bf16", [](uintptr_t w, int R, int sc, int seg, int kp, int K, uintptr_t out,
+                               uintptr_t st) {
+    gops::stem_weight_bf16(P<const float>(w), R, sc, seg, kp, K, P<void>(out), S(st));
+    check_launch();
+  });
+  g.def("stem_wgrad", [](uintptr_t gpad, int R, int sc, int seg, int K, uintptr_t gw, uintptr_t st) {
+    gops::stem_wgrad(P<const float>(gpad), R, sc, seg, K, P<float>(gw), S(st));
+    check_launch();
+  });
   g.def("wcvt_blocks", &gops::wcvt_blocks);
   g.def("wcvt_batch", [](uintptr_t jobs, int njobs, long long nblocks, uintptr_t st) {
     gops::wcvt_batch(P<const long long>(jobs), njobs, nblocks, S(st));

@@ -956,6 +956,41 @@ void linear_bwd(const float* x, const float* w, const float* y, const float* dy,
                                                   bw, bb);
 }
 
+// Stem (im2col route, ops/functional.py _ConvIm2colFn): HWIO fp32
+// [R][S][C][K] -> the 1x1 conv's pre-laid-out bf16 forward weight [K][kp] in
+// the im2col's k order (k = kh * seg + kw * C + ci, zero-padded to seg per tap
+// row and to kp overall), and the 1x1 conv's filter gradient [kp][K] back to
+// HWIO.  (They were a torch.zeros + strided copy_ each way: ATen kernels.)
+__global__ __launch_bounds__(256) void stem_wt_kernel(const float* __restrict__ w, int R, int sc,
+                                                      int seg, int kp, int K,
+                                                      __bf16* __restrict__ out) {
+  const int n = K * kp;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int co = i / kp, k = i - co * kp, kh = k / seg, j = k - kh * seg;
+    out[i] = (__bf16)((kh < R && j < sc) ? w[((size_t)kh * sc + j) * K + co] : 0.f);
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_wgrad_kernel(const float* __restrict__ gpad, int R,
+                                                         int sc, int seg, int K,
+                                                         float* __restrict__ gw) {
+  const int n = R * sc * K;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int co = i % K, t = i / K, kh = t / sc, j = t - kh * sc;
+    gw[i] = gpad[((size_t)kh * seg + j) * K + co];
+  }
+}
+
+void stem_weight_bf16(const float* w, int R, int sc, int seg, int kp, int K, void* out,
+                      hipStream_t st) {
+  stem_wt_kernel<<<grid1d((long long)K * kp), 256, 0, st>>>(w, R, sc, seg, kp, K,
+                                                            reinterpret_cast<__bf16*>(out));
+}
+
+void stem_wgrad(const float* gpad, int R, int sc, int seg, int K, float* gw, hipStream_t st) {
+  stem_wgrad_kernel<<<grid1d((long long)R * sc * K), 256, 0, st>>>(gpad, R, sc, seg, K, gw);
+}
+
 void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st) {
   relu_bwd_kernel<<<grid1d(n), 256, 0, st>>>(dy, y, dx, n);
 }

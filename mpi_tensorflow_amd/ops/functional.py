@@ -275,15 +275,15 @@ class _ConvIm2colFn(torch.autograd.Function):
         s = stream_handle()
         col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
         C.ops.im2col_bf16(sh, ptr(x), kp, ptr(col), s)
-        # weights in the im2col's k order: tap row kh at kh * seg, (kw, ci) inside
-        wpad = torch.zeros((1, 1, kp, sh.K), device=x.device, dtype=torch.float32)
-        wpad.view(kp, sh.K)[:sh.R * seg].view(sh.R, seg, sh.K)[:, :sc].copy_(
-            w.reshape(sh.R, sc, sh.K))
+        # weights in the im2col's k order (tap row kh at kh * seg, (kw, ci)
+        # inside), written straight as the 1x1 conv's bf16 [K][kp] layout
+        wtb = torch.empty(sh.K * kp, dtype=torch.bfloat16, device=x.device)
+        C.ops.stem_weight_bf16(ptr(w), sh.R, sc, seg, kp, sh.K, ptr(wtb), s)
         s1 = C.ops.ConvShape(sh.N, sh.OH, sh.OW, kp, sh.K, 1, 1, 1, 0)
         y = torch.empty((sh.N, sh.OH, sh.OW, sh.K),
                         dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
-        C.ops.conv_fwd(s1, 0, ptr(wpad), 0, 0 if out_bf16 else ptr(y), False, ptr(ws), s, True,
-                       ptr(col), 0, ptr(y) if out_bf16 else 0)
+        C.ops.conv_fwd(s1, 0, 0, 0, 0 if out_bf16 else ptr(y), False, ptr(ws), s, True,
+                       ptr(col), ptr(wtb), ptr(y) if out_bf16 else 0)
         ctx.save_for_backward(col)
         ctx.s1, ctx.R, ctx.sc, ctx.seg, ctx.gw, ctx.ws = s1, sh.R, sc, seg, gw, ws
         return y
@@ -298,8 +298,7 @@ class _ConvIm2colFn(torch.autograd.Function):
         dyb = _bf16_copy(dy, s)
         gpad = torch.empty((s1.C, s1.K), device=dy.device, dtype=torch.float32)
         C.ops.conv_bwd_filter(s1, 0, 0, ptr(ctx.ws), ptr(gpad), s, True, ptr(col), ptr(dyb))
-        ctx.gw.view(ctx.R, ctx.sc, s1.K).copy_(
-            gpad[:ctx.R * ctx.seg].view(ctx.R, ctx.seg, s1.K)[:, :ctx.sc])
+        C.ops.stem_wgrad(ptr(gpad), ctx.R, ctx.sc, ctx.seg, s1.K, ptr(ctx.gw), s)
         _grad_done(ctx.gw)
         return None, None, None, None, None, None, None
 

@@ -25,3 +25,15 @@ def cuda_dev():
 
     require_native()  # GPU tests must run the native path, never a fallback
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _reset_conv_mode():
+    """Engines set the process-wide conv operand mode (Fn.set_conv_bf16);
+    restore fp32 after every test so later tests start from the default."""
+    yield
+    try:
+        from mpi_tensorflow_amd.ops import functional as Fn
+    except Exception:  # noqa: BLE001 - CPU-only collection without the package deps
+        return
+    Fn.set_conv_bf16(False)
