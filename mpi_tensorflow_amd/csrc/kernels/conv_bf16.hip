@@ -492,12 +492,14 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
           if (full || mb + rr < M) pb[(size_t)rr * K] = (__bf16)acc[i][j][q];
         }
       } else if (full && addend) {
+        // all 16 addend loads first, then the stores (interleaved, hipcc waited
+        // vmcnt(0) per element: 16 serial round trips)
         const float* ap = addend + (size_t)mb * K + co;
+        float av[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const size_t o = (size_t)((q & 3) + 8 * (q >> 2)) * K;
-          p[o] = acc[i][j][q] + ap[o];
-        }
+        for (int q = 0; q < 16; ++q) av[q] = ap[(size_t)((q & 3) + 8 * (q >> 2)) * K];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[(size_t)((q & 3) + 8 * (q >> 2)) * K] = acc[i][j][q] + av[q];
       } else if (full) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) p[(size_t)((q & 3) + 8 * (q >> 2)) * K] = acc[i][j][q];
@@ -647,7 +649,10 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
       }
     }
   }
-  // epilogue: grid pixel m = (n, a, b) -> dX pixels (n, 2a + py, 2b + px)
+  // epilogue: grid pixel m = (n, a, b) -> dX pixels (n, 2a + py, 2b + px);
+  // the addend (the gradient join of a downsample block) is loaded for a whole
+  // row group before any store: interleaved, hipcc waited vmcnt(0) per element
+  // (64 serial round trips a lane; 162 us instead of ~50 at B = 128)
   dx += (size_t)blockIdx.y * s.N * s.H * s.W * s.C;
   const size_t C = s.C, W = s.W;
 #pragma unroll
@@ -656,16 +661,29 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
     for (int j = 0; j < TN; ++j) {
       const int ci = n0 + wn * (BN / 2) + 32 * j + r;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q, lane);
-        if (m >= M) continue;
-        const int b = m % OW, g = m / OW;  // g = n * OH + a
-        const size_t o = ((size_t)(2 * g) * W + 2 * b) * C + ci;  // (n, 2a, 2b)
+      for (int q4 = 0; q4 < 16; q4 += 4) {
+        size_t o[4];
+        bool ok[4];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const size_t oc = o + (c >> 1) * W * C + (c & 1) * C;
-          const float v = acc[c][i][j][q];
-          dx[oc] = addend ? v + addend[oc] : v;
+        for (int u = 0; u < 4; ++u) {
+          const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q4 + u, lane);
+          ok[u] = m < M;
+          const int mm = ok[u] ? m : 0;
+          const int b = mm % OW, g = mm / OW;  // g = n * OH + a
+          o[u] = ((size_t)(2 * g) * W + 2 * b) * C + ci;  // (n, 2a, 2b)
+        }
+        float av[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            av[u][c] = (addend && ok[u]) ? addend[o[u] + (c >> 1) * W * C + (c & 1) * C] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (!ok[u]) continue;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            dx[o[u] + (c >> 1) * W * C + (c & 1) * C] = acc[c][i][j][q4 + u] + av[u][c];
         }
       }
     }
@@ -1027,7 +1045,7 @@ static bool dgrad3s2_ok(const ConvShape& s) {
 // below 128 blocks - fewer 4x-sized dX slabs - was no faster, 2.70 vs 2.69 ms)
 static inline P3 plan3s2(const ConvShape& s) {
   const long long M = (long long)s.N * s.OH * s.OW;
-  const long long blocks = (long long)cdiv(M, 128) * (s.C / 64);
+  const long long blocks = (long long)cdiv(M, 64) * (s.C / 64);
   const int nch = s.K / BK;
   int z = 1;
   if (blocks < 256) {
@@ -1035,7 +1053,7 @@ static inline P3 plan3s2(const ConvShape& s) {
     if (z > nch) z = nch;
   }
   const int cps = cdiv(nch, z);
-  return {cdiv(nch, cps), cps, 128};
+  return {cdiv(nch, cps), cps, 64};
 }
 static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, float* dx,
                       float* ws, hipStream_t st, const float* addend) {
@@ -1043,9 +1061,11 @@ static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, fl
   const P3 p = plan3s2(s);
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : dx;
-  const dim3 grid(cdiv(M, 128) * (s.C / 64), p.z);
-  dgrad3s2_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, dy, wt, out, p.cps,
-                                                   p.z > 1 ? nullptr : addend);
+  // 64-pixel tiles: with four accumulator classes a 128-pixel tile needed 272
+  // registers a lane (one wave per SIMD) and ran 10x slower per tile
+  const dim3 grid(cdiv(M, 64) * (s.C / 64), p.z);
+  dgrad3s2_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, dy, wt, out, p.cps,
+                                                  p.z > 1 ? nullptr : addend);
   if (p.z > 1)
     slab_reduce(slabs, p.z, (long long)s.N * s.H * s.W * s.C / 4, dx, st, addend);
 }

@@ -555,3 +555,37 @@ def test_bn_twin_only_feeds_conv_identically(cuda_dev):
     torch.cuda.synchronize()
     for a_, b_ in zip(*out):
         assert torch.equal(a_, b_)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_resnet18_resume_restores_eval_gpu(cuda_dev, tmp_path, dtype):
+    """GPU resume: ResNet-18 trained a few (graph-replayed) steps, saved with its
+    BN running statistics, restored into a fresh engine: eval logits and error
+    identical to before the save, and training continues identically."""
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils import checkpoint as ck
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 48, shape=(32, 32, 3))
+    cfg = C.TrainConfig(model="resnet18", batch_size=8, dtype=dtype, graph=True,
+                        graph_steps=2).validate()
+    eng = GenericEngine(cfg, x, y, cuda_dev)
+    eng.train(5)
+    torch.cuda.synchronize()
+    err0 = eng.evaluate(x[:16], y[:16])
+    p = str(tmp_path / "r.npz")
+    ck.save(p, eng.layout, eng.params, eng.mom, eng.step, meta={"model": "resnet18"},
+            extra=eng.extra_state())
+    e2 = GenericEngine(C.TrainConfig(model="resnet18", batch_size=8, dtype=dtype, graph=True,
+                                     graph_steps=2, seed=7).validate(), x, y, cuda_dev)
+    step, _ = ck.load(p, e2.layout, e2.params, e2.mom, extra=e2.extra_state(),
+                      expect={"model": "resnet18"})
+    e2.set_step(step)
+    assert step == eng.step
+    for k in eng.bn:
+        assert torch.equal(eng.bn[k][0], e2.bn[k][0]) and torch.equal(eng.bn[k][1], e2.bn[k][1])
+    assert e2.evaluate(x[:16], y[:16]) == err0
+    eng.train(2)
+    e2.train(2)
+    torch.cuda.synchronize()
+    assert torch.equal(eng.params.detach(), e2.params.detach())
