@@ -371,6 +371,8 @@ __device__ __forceinline__ void data_body(const ConvShape& s, const DT* __restri
   mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
   dx += (size_t)blockIdx.z * s.N * s.H * s.W * s.C;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+  // addend loads of 4 rows are issued before their stores (interleaved, hipcc
+  // waited vmcnt(0) per element)
 #pragma unroll
   for (int j = 0; j < G::TN; ++j) {
     const int ci = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
@@ -378,15 +380,24 @@ __device__ __forceinline__ void data_body(const ConvShape& s, const DT* __restri
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
-        if (m >= M) continue;
-        const int jx = m % PW, t = m / PW, jy = t % PH, n = t / PH;
-        const int iy = jy * sd + py, ix = jx * sd + px;
-        if (iy < s.H && ix < s.W) {
-          const size_t o = (((size_t)n * s.H + iy) * s.W + ix) * s.C + ci;
-          dx[o] = addend ? acc[i][j][r] + addend[o] : acc[i][j][r];
+      for (int r4 = 0; r4 < 16; r4 += 4) {
+        size_t o[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r4 + u, lane);
+          const int mm = m < M ? m : 0;
+          const int jx = mm % PW, t = mm / PW, jy = t % PH, n = t / PH;
+          const int iy = jy * sd + py, ix = jx * sd + px;
+          ok[u] = m < M && iy < s.H && ix < s.W;
+          o[u] = (((size_t)n * s.H + iy) * s.W + ix) * s.C + ci;
         }
+        float av[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) av[u] = (addend && ok[u]) ? addend[o[u]] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (ok[u]) dx[o[u]] = acc[i][j][r4 + u] + av[u];
       }
   }
 }
