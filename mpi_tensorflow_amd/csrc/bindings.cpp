@@ -223,6 +223,10 @@ PYBIND11_MODULE(_C, m) {
     gops::stem_wgrad(P<const float>(gpad), R, sc, seg, K, P<float>(gw), S(st));
     check_launch();
   });
+  g.def("softmax_rows", [](uintptr_t x, uintptr_t y, int M, int N, uintptr_t st) {
+    gops::softmax_rows(P<const float>(x), P<float>(y), M, N, S(st));
+    check_launch();
+  });
   g.def("wcvt_blocks", &gops::wcvt_blocks);
   g.def("wcvt_batch", [](uintptr_t jobs, int njobs, long long nblocks, uintptr_t st) {
     gops::wcvt_batch(P<const long long>(jobs), njobs, nblocks, S(st));

@@ -112,6 +112,7 @@ void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t s
 void xent(const float* logits, const int* labels, int B, int C, float* loss_rows, float* dlogits,
           int* correct, hipStream_t st);
 void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st);
+void softmax_rows(const float* x, float* y, int M, int N, hipStream_t st);
 // stem im2col route: HWIO weight -> bf16 [K][kp] (im2col k order), and the
 // [kp][K] filter gradient back to HWIO
 void stem_weight_bf16(const float* w, int R, int sc, int seg, int kp, int K, void* out,

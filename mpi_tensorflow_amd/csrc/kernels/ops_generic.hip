@@ -991,6 +991,27 @@ void stem_wgrad(const float* gpad, int R, int sc, int seg, int K, float* gw, hip
   stem_wgrad_kernel<<<grid1d((long long)R * sc * K), 256, 0, st>>>(gpad, R, sc, seg, K, gw);
 }
 
+// Row softmax (the reference's train_prediction / eval_prediction heads,
+// /root/reference/mpipy.py:67-68): one wave per row, max-subtracted.
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ x,
+                                                          float* __restrict__ y, int M, int N) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * N;
+  float mx = -INFINITY;
+  for (int j = lane; j < N; j += 64) mx = fmaxf(mx, xr[j]);
+  mx = wave_max(mx);
+  float s = 0.f;
+  for (int j = lane; j < N; j += 64) s += __expf(xr[j] - mx);
+  s = wave_sum(s);
+  const float inv = 1.f / s;
+  for (int j = lane; j < N; j += 64) y[(size_t)row * N + j] = __expf(xr[j] - mx) * inv;
+}
+
+void softmax_rows(const float* x, float* y, int M, int N, hipStream_t st) {
+  if (M > 0) softmax_rows_kernel<<<(M + 3) / 4, 256, 0, st>>>(x, y, M, N);
+}
+
 void relu_bwd(const float* dy, const float* y, float* dx, long long n, hipStream_t st) {
   relu_bwd_kernel<<<grid1d(n), 256, 0, st>>>(dy, y, dx, n);
 }

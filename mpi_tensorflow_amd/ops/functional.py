@@ -512,6 +512,17 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
     return F.relu(y) if relu else y
 
 
+def softmax(logits: torch.Tensor) -> torch.Tensor:
+    """Row softmax of [M, N] logits (no autograd): the prediction heads.
+    Native kernel on GPU, torch on the CPU oracle path."""
+    if not logits.is_cuda:
+        return torch.softmax(logits.float(), dim=1)
+    x = logits.contiguous().float()
+    y = torch.empty_like(x)
+    native().ops.softmax_rows(ptr(x), ptr(y), x.shape[0], x.shape[1], stream_handle())
+    return y
+
+
 # ---------------------------------------------------------------- pooling --
 class _MaxPoolFn(torch.autograd.Function):
     @staticmethod

@@ -271,15 +271,21 @@ class GenericEngine:
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
-    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 256, dropout: bool = False):
+    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 256, dropout: bool = False,
+                 return_logits: bool = False):
         n = int(x.shape[0])
+        outs = []
         if not self.on_gpu:
             wrong = 0
             for a in range(0, n, chunk):
                 xb = torch.from_numpy(np.ascontiguousarray(x[a:a + chunk], np.float32))
-                pred = self.model.forward(self.P, self.bn, xb, False).argmax(1).numpy()
+                lg = self.model.forward(self.P, self.bn, xb, False)
+                if return_logits:
+                    outs.append(lg)
+                pred = lg.argmax(1).numpy()
                 wrong += int((pred != y[a:a + chunk]).sum())
-            return 100.0 * wrong / max(1, n)
+            err = 100.0 * wrong / max(1, n)
+            return (err, torch.cat(outs)) if return_logits else err
         # GPU: the test set is uploaded once and stays resident; the xent
         # kernel's argmax counter accumulates the correct predictions on the
         # device, so the whole evaluation ends in ONE 4-byte read
@@ -296,10 +302,13 @@ class GenericEngine:
         for a in range(0, n, chunk):
             xb, yb = xd[a:a + chunk], yd[a:a + chunk]
             logits = self.model.forward(self.P, self.bn, xb, False).contiguous()
+            if return_logits:
+                outs.append(logits)
             m, k = logits.shape
             rows = torch.empty(m, device=self.device)
             self._C.ops.xent(ptr(logits), ptr(yb), m, k, ptr(rows), 0, ptr(correct), s)
-        return 100.0 * (n - int(correct.item())) / max(1, n)
+        err = 100.0 * (n - int(correct.item())) / max(1, n)
+        return (err, torch.cat(outs)) if return_logits else err
 
 
 def make_image_engine(cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,

@@ -151,17 +151,25 @@ class TorchMnistEngine(MnistEngineBase):
         return self.last_loss + self.l2_value()
 
     @torch.no_grad()
-    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 2000, dropout: bool = False):
+    def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 2000, dropout: bool = False,
+                 return_logits: bool = False):
         views = self.param_views()
         wrong = 0
+        outs = []
         for a in range(0, x.shape[0], chunk):
             xb = torch.from_numpy(x[a:a + chunk]).to(self.device)
             mask = None
             if dropout:
                 mask = self.dropout_mask(self.step, xb.shape[0], rng.EVAL_SALT)
-            pred = M.forward(views, xb, mask, self.cfg.dropout_keep).argmax(1).cpu().numpy()
+            lg = M.forward(views, xb, mask, self.cfg.dropout_keep)
+            if return_logits:
+                outs.append(lg)
+            pred = lg.argmax(1).cpu().numpy()
             wrong += int((pred != y[a:a + chunk]).sum())
-        return 100.0 * wrong / max(1, x.shape[0])
+        err = 100.0 * wrong / max(1, x.shape[0])
+        if return_logits:
+            return err, (torch.cat(outs) if outs else torch.empty(0, 10, device=self.device))
+        return err
 
 
 class NativeMnistEngine(MnistEngineBase):

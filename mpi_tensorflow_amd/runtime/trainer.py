@@ -23,6 +23,7 @@ import dataclasses
 import time
 from typing import Dict, Optional
 
+import numpy as np
 import torch
 
 from .. import config as C
@@ -34,6 +35,8 @@ from ..utils import checkpoint as ckpt_mod
 from ..utils.data import (data_exist_here, load_mnist_shard, local_train_rows, mnist_files_present,
                           steps_per_run, synthetic_image_shard)
 from ..utils.logging import MetricsWriter, emit, progress_line, start_line
+from ..ops import functional as Fn
+from ..utils.data import batch_offset
 from ..utils.profiling import SegmentTimer
 
 
@@ -148,6 +151,23 @@ class Trainer:
     def evaluate(self, dropout: Optional[bool] = None) -> float:
         d = self.cfg.eval_dropout if dropout is None else dropout
         return self.engine.evaluate(self.shard.test_x, self.shard.test_y, dropout=d)
+
+    def eval_prediction(self, x: np.ndarray, dropout: Optional[bool] = None) -> torch.Tensor:
+        """`eval_prediction = softmax(model(eval_data))` of the reference
+        (/root/reference/mpipy.py:68): class probabilities [n, 10] (dropout
+        per --eval-dropout, as the reference's shared graph applies it)."""
+        d = self.cfg.eval_dropout if dropout is None else dropout
+        n = int(x.shape[0])
+        _, logits = self.engine.evaluate(x, np.zeros(n, np.int64), dropout=d, return_logits=True)
+        return Fn.softmax(logits)
+
+    def train_prediction(self) -> torch.Tensor:
+        """`train_prediction = softmax(logits)` of the reference's training graph
+        (/root/reference/mpipy.py:67): probabilities for the current training
+        batch (rows at the step's batch offset, dropout on as in training)."""
+        sh = self.shard
+        off = batch_offset(self.engine.step, sh.train_x.shape[0], self.cfg.batch_size)
+        return self.eval_prediction(sh.train_x[off:off + self.cfg.batch_size], dropout=True)
 
     def check_replicas(self, step: int) -> None:
         """All ranks must hold bit-identical weights under per-step gradient

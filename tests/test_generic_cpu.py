@@ -165,3 +165,23 @@ def test_lenet_dp_gloo_matches_serial(tmp_path):
 def test_make_model_unknown():
     with pytest.raises(KeyError):
         make_model("vgg")
+
+
+@pytest.mark.parametrize("model", ["mnist_cnn", "lenet5"])
+def test_prediction_heads_cpu(model):
+    """train_prediction / eval_prediction (reference mpipy.py:67-68): softmax
+    probabilities whose argmax reproduces evaluate()'s error."""
+    from mpi_tensorflow_amd.runtime.trainer import Trainer
+
+    cfg = C.TrainConfig(model=model, device="cpu", max_steps=5, eval_every=0, quiet=True,
+                        synthetic=True).validate()
+    tr = Trainer(cfg)
+    tr.run()
+    x, y = tr.shard.test_x[:200], tr.shard.test_y[:200]
+    p = tr.eval_prediction(x, dropout=False)
+    assert p.shape == (200, 10)
+    assert torch.allclose(p.sum(1), torch.ones(200, dtype=p.dtype), atol=1e-5)
+    err = 100.0 * float((p.argmax(1).cpu().numpy() != y).sum()) / 200
+    assert abs(err - tr.engine.evaluate(x, y, dropout=False)) < 1e-9
+    tp = tr.train_prediction()
+    assert tp.shape == (cfg.batch_size, 10) and torch.isfinite(tp).all()

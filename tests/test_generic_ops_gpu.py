@@ -589,3 +589,11 @@ def test_resnet18_resume_restores_eval_gpu(cuda_dev, tmp_path, dtype):
     e2.train(2)
     torch.cuda.synchronize()
     assert torch.equal(eng.params.detach(), e2.params.detach())
+
+
+def test_softmax_rows_native(cuda_dev):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(37, 10, generator=g) * 5
+    y = Fn.softmax(x.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert _rel(y.cpu(), torch.softmax(x, 1)) < 1e-6
