@@ -225,7 +225,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": a.dtype,
+            "dtype": getattr(getattr(eng, "cfg", None), "dtype", a.dtype),  # effective
             "data": data_desc,
             "config": {
                 "model": model_desc,

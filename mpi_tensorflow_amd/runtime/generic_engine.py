@@ -24,6 +24,8 @@ On CPU the same model runs through the PyTorch oracle ops.
 
 from __future__ import annotations
 
+import dataclasses
+
 from typing import Optional
 
 import numpy as np
@@ -314,11 +316,20 @@ class GenericEngine:
 def make_image_engine(cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
                       device: torch.device, rank: int = 0, world: int = 1,
                       comm: Optional[DeviceComm] = None, force_sync: bool = False):
-    """Engine for the extra image models: LeNet-5 in fp32 on a GPU runs the
-    fused two-launch executor (runtime/lenet_engine.py); everything else
-    (ResNet-18, LeNet-5 bf16, the CPU oracle) runs the op-by-op engine."""
-    if cfg.model == "lenet5" and device.type == "cuda" and cfg.dtype == "fp32":
+    """Engine for the extra image models: LeNet-5 on a GPU runs the fused
+    two-launch executor (runtime/lenet_engine.py); everything else (ResNet-18,
+    the CPU oracle) runs the op-by-op engine.  LeNet-5 has no bf16 variant:
+    its 3- and 6-channel convs and its FCs are VALU work whatever the operand
+    type (the op-by-op engine's "bf16" LeNet ran the same fp32 math 6x
+    slower), so --dtype bf16 runs the fp32 executor, says so, and the
+    engine's `dtype` reports fp32."""
+    if cfg.model == "lenet5" and device.type == "cuda":
         from .lenet_engine import NativeLenetEngine
 
+        if cfg.dtype != "fp32":
+            if rank == 0:
+                print("[lenet5] --dtype bf16: LeNet-5's layers are VALU-bound at any operand "
+                      "type; running the fp32 fused executor", flush=True)
+            cfg = dataclasses.replace(cfg, dtype="fp32")
         return NativeLenetEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)
     return GenericEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)

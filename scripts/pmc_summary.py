@@ -1,23 +1,30 @@
-"""Per-kernel averages of rocprofv3 --pmc CSV output (one dispatch = one row
-per counter).  python scripts/pmc_summary.py <dir-with-*_counter_collection.csv>"""
-import csv
+"""Per-kernel, per-grid averages of rocprofv3 --pmc results (rocpd SQLite,
+`counters_collection`), SQ counters also per wave.
+    python scripts/pmc_summary.py gpurun_out/pmc1 [gpurun_out/pmc2 ...] [--match conv3]"""
 import glob
+import sqlite3
 import sys
 from collections import defaultdict
 
-for d in sys.argv[1:]:
-    f = glob.glob(d + "/*counter_collection.csv")[0]
-    agg = defaultdict(lambda: defaultdict(float))
-    disp = defaultdict(set)
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0][-38:]
-        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[k].add(r["Dispatch_Id"])
-    names = sorted({c for v in agg.values() for c in v})
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+match = sys.argv[sys.argv.index("--match") + 1] if "--match" in sys.argv else ""
+for d in args:
+    if d == match:
+        continue
+    db = glob.glob(d + "/*.db")[0]
+    con = sqlite3.connect(db)
+    rows = con.execute("select kernel_name, grid_size, counter_name, value from counters_collection")
+    agg = defaultdict(lambda: defaultdict(list))
+    for name, grid, cn, v in rows:
+        if match in name:
+            agg[(name.split("(")[0][-60:], grid)][cn].append(v)
     print(d)
-    print(f"{'kernel':38s} " + " ".join(f"{n[-14:]:>14s}" for n in names))
-    for k, v in agg.items():
-        n = len(disp[k])
-        if n < 5:
-            continue
-        print(f"{k:38s} " + " ".join(f"{v[c] / n:14.0f}" for c in names))
+    for (name, grid), cs in sorted(agg.items()):
+        waves = cs.get("SQ_WAVES")
+        w = sum(waves) / len(waves) if waves else None
+        vals = []
+        for cn, vs in sorted(cs.items()):
+            m = sum(vs) / len(vs)
+            per_wave = f"/wave {m / w:,.0f}" if (w and cn.startswith("SQ_") and cn != "SQ_WAVES") else ""
+            vals.append(f"{cn}={m:,.0f}{per_wave}")
+        print(f"  {name} grid={grid}: " + "; ".join(vals))
