@@ -461,6 +461,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("stream"), py::arg("comm") = nullptr, py::arg("comm_stream") = 0,
            py::arg("comm2") = nullptr)
       .def("set_schedule", &MnistExecutor::set_schedule)
+      .def("set_fc_sgd_rounds", &MnistExecutor::set_fc_sgd_rounds)
       .def_property_readonly("schedule", &MnistExecutor::schedule)
       .def("sharded_ok", &MnistExecutor::sharded_ok)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })

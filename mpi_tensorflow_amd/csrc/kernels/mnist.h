@@ -5,6 +5,27 @@
 #include <stdint.h>
 
 namespace mnist {
+// world-1 FC-bucket momentum SGD run as extra blocks of a conv2 bwd-data launch
+// (mnist_shared.h fc_sgd_role): flat [0, n) floats, L2 on all of it, device lr
+struct FcSgdArgs {
+  float* w;
+  const float* g;
+  float* m;
+  long long n;
+  float l2, momentum;
+  const float* lr;
+  int rounds;  // FC_SGD_UNROLL-float4 rounds per thread (sets the block count)
+};
+// conv1 filter-grad role appended to a conv2 filter-gradient launch (its input
+// dA1m must be final: the conv2 bwd-data launch ran before)
+struct C1FilterArgs {
+  const float* data;
+  const long long* step;
+  int n_local;
+  const float* da1m;
+  const uint8_t* idx1;
+  float* part1;
+};
 // out_pad (optional): zero-bordered NHWC copy [batch][18][18][32] of the pooled
 // output (its border is never written: allocate it zeroed)
 void launch_conv1_fwd(const float* data, const long long* step, int n_local, int batch,
@@ -43,11 +64,11 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
 int conv2_filter_splits(int batch);
 // a1p: the zero-bordered NHWC pooled conv1 output [batch][18][18][32]
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
-                             hipStream_t s);
+                             hipStream_t s, const C1FilterArgs* c1 = nullptr);
 // L2-direct bwd-data (the one the executor uses): dy2t from launch_fc1_bwd,
 // w2t from launch_conv2_fwd; batch % 8 == 0
 void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
-                              float* da1m, hipStream_t s);
+                              float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr);
 
 
 int conv1_filter_blocks(int batch);
@@ -61,7 +82,7 @@ void launch_grad_finalize(const float* part2, int ngroups, const float* part1, i
 void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s);
+                         const float* lr, long long* step, hipStream_t s, bool fc_done = false);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

@@ -831,11 +831,17 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_l2_kernel(const float* __r
                                                                 const float* __restrict__ w2t,
                                                                 const float* __restrict__ a1,
                                                                 int batch,
-                                                                float* __restrict__ da1m) {
+                                                                float* __restrict__ da1m,
+                                                                const FcSgd sgd) {
   __shared__ float red[2][16][64];
+  const int nconv = gridDim.x - sgd.nblk;
+  if ((int)blockIdx.x >= nconv) {
+    fc_sgd_role(sgd, blockIdx.x - nconv);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int mtiles = batch * 49 / 8;
-  const int mt_raw = xcd_remap(blockIdx.x, gridDim.x) * 2 + (wave & 1), kk = wave >> 1;
+  const int mt_raw = xcd_remap(blockIdx.x, nconv) * 2 + (wave & 1), kk = wave >> 1;
   const int mt = min(mt_raw, mtiles - 1);
   const int m = mt * 32 + r, n = m / 196, p = m % 196, y = p / 14, x = p % 14;
   // padded source pixel of tap (kh, kw): (y + 4 - kh, x + 4 - kw)
@@ -869,75 +875,23 @@ __global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(int batch,
                                                               const float* __restrict__ a1p,
                                                               const float* __restrict__ dy2,
                                                               float* __restrict__ part2,
-                                                              float* __restrict__ part_db2) {
-  __shared__ float smem[3 * 2 * 16 * 64];
+                                                              float* __restrict__ part_db2,
+                                                              int nc2, const C1Filter c1) {
+  constexpr int SM = 3 * 2 * 16 * 64 > C1F_SMEM ? 3 * 2 * 16 * 64 : C1F_SMEM;
+  __shared__ float smem[SM];
+  if ((int)blockIdx.x >= nc2) {  // conv1 filter-grad role (its dA1 is final)
+    conv1_filter_unit<512>(blockIdx.x - nc2, batch, c1, smem);
+    return;
+  }
   conv2_bwd_filter_v3<DEPTH, CENTRE_ONLY>(blockIdx.x, batch, a1p, dy2, part2, part_db2, smem);
 }
 
 // ------------------------------------------------------ conv1 bwd filter ----
-// Sparse: each pooled gradient reaches exactly one pre-pool pixel (its argmax),
-// so dW1[t][co] = sum over pooled (n,py,px) of dA1m * x[argmax pixel + tap].
-// Block = (image, pair of pooled rows); thread = (co, position group).  All of
-// a thread's (gradient, argmax) pairs are loaded up front (one latency round).
-constexpr int C1F_SPLIT = 7;                    // pooled-row pairs per image
-constexpr int C1F_POS = 28;                     // pooled positions per block
-constexpr int C1F_PER_T = (C1F_POS + 7) / 8;    // positions per thread (4)
-
-__global__ __launch_bounds__(256) void conv1_bwd_filter_kernel(
-    const float* __restrict__ data, const long long* step_ptr, int n_local, int batch,
-    const float* __restrict__ da1m, const uint8_t* __restrict__ idx1, float* __restrict__ part1) {
-  __shared__ float xs[8 * 32];  // rows 4*pair-2 .. 4*pair+5 of the padded image
-  __shared__ float red[8][26 * 32 + 1];
-  const int n = blockIdx.x / C1F_SPLIT, pair = blockIdx.x % C1F_SPLIT;
-  const long long off = batch_offset_dev(step_ptr, n_local, batch);
-  const float* x = data + (off + n) * 784;
-  const int tid = threadIdx.x, co = tid & 31, grp = tid >> 5;
-  const int y0 = 4 * pair - 2;  // first image row held in xs
-  {
-    const int yy = y0 + tid / 32, xx = tid % 32 - 2;
-    xs[tid] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
-  }
-  float v[C1F_PER_T];
-  int q[C1F_PER_T];
-#pragma unroll
-  for (int j = 0; j < C1F_PER_T; ++j) {
-    const int p = grp + 8 * j;
-    v[j] = 0.f;
-    q[j] = 0;
-    if (p < C1F_POS) {
-      const int py = 2 * pair + p / 14, px = p % 14;
-      const int e = ((n * 14 + py) * 14 + px) * 32 + co;
-      v[j] = da1m[e];
-      q[j] = idx1[e];
-    }
-  }
-  __syncthreads();
-  float acc[26];
-#pragma unroll
-  for (int t = 0; t < 26; ++t) acc[t] = 0.f;
-#pragma unroll
-  for (int j = 0; j < C1F_PER_T; ++j) {
-    const int p = grp + 8 * j;
-    if (p < C1F_POS && v[j] != 0.f) {
-      const int py = 2 * pair + p / 14, px = p % 14;
-      const int ly = 2 * py + (q[j] >> 1) - y0 - 2;  // row in xs of tap kh = 0
-      const int lx = 2 * px + (q[j] & 1);            // col in xs (padded by 2) of kw = 0
-#pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
-#pragma unroll
-        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += v[j] * xs[(ly + kh) * 32 + lx + kw];
-      acc[25] += v[j];
-    }
-  }
-#pragma unroll
-  for (int t = 0; t < 26; ++t) red[grp][t * 32 + co] = acc[t];
-  __syncthreads();
-  for (int i = tid; i < 26 * 32; i += 256) {
-    float s = 0.f;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) s += red[g][i];
-    part1[(size_t)blockIdx.x * 832 + i] = s;
-  }
+// standalone 256-thread form of mnist_shared.h conv1_filter_unit (the executor
+// runs it as a role of the conv2 filter-gradient launch)
+__global__ __launch_bounds__(256) void conv1_bwd_filter_kernel(int batch, const C1Filter c) {
+  __shared__ float smem[C1F_SMEM];
+  conv1_filter_unit<256>(blockIdx.x, batch, c, smem);
 }
 
 // ------------------------------------------------------------ finalize ----
@@ -1080,27 +1034,47 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }
 
 
+FcSgd fc_sgd_args(const FcSgdArgs* a) {
+  FcSgd r{};
+  if (a == nullptr || a->n == 0) return r;
+  if (a->n % 4) throw std::runtime_error("fc_sgd: FC bucket not a multiple of 4 floats");
+  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0};
+  const long long per_blk = 256LL * FC_SGD_UNROLL * a->rounds;
+  r.nblk = (int)((r.n4 + per_blk - 1) / per_blk);
+  return r;
+}
+
 void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
-                              float* da1m, hipStream_t s) {
+                              float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd) {
   if (batch % 8 != 0) throw std::runtime_error("conv2_bwd_data_l2: batch % 8 != 0");
   const int mtiles = batch * 49 / 8;
-  conv2_bwd_data_l2_kernel<<<cdiv(mtiles, 2), 256, 0, s>>>(dy2t, w2t, a1, batch, da1m);
+  const FcSgd sg = fc_sgd_args(fc_sgd);
+  conv2_bwd_data_l2_kernel<<<cdiv(mtiles, 2) + sg.nblk, 256, 0, s>>>(dy2t, w2t, a1, batch, da1m,
+                                                                     sg);
 }
 
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
-                             hipStream_t s) {
+                             hipStream_t s, const C1FilterArgs* c1) {
   const int G = conv2_filter_splits(batch);
   float* db = part2 + (size_t)G * 51200;
-  conv2_bwd_filter_kernel<3, true><<<25 * G, 512, 0, s>>>(batch, a1p, dy2, part2, db);
+  const C1Filter c = c1_args(c1);
+  const int n1 = c.part1 ? conv1_filter_blocks(batch) : 0;
+  conv2_bwd_filter_kernel<3, true><<<25 * G + n1, 512, 0, s>>>(batch, a1p, dy2, part2, db, 25 * G,
+                                                                c);
 }
 
 int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }
 
+C1Filter c1_args(const C1FilterArgs* a) {
+  if (a == nullptr) return C1Filter{};
+  return C1Filter{a->data, a->step, a->n_local, a->da1m, a->idx1, a->part1};
+}
+
 void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
                              const float* da1m, const uint8_t* idx1, float* part1,
                              hipStream_t s) {
-  conv1_bwd_filter_kernel<<<conv1_filter_blocks(batch), 256, 0, s>>>(data, step, n_local, batch,
-                                                                     da1m, idx1, part1);
+  conv1_bwd_filter_kernel<<<conv1_filter_blocks(batch), 256, 0, s>>>(
+      batch, C1Filter{data, step, n_local, da1m, idx1, part1});
 }
 
 // ----------------------------------------------- world-1 SGD + finalize ----
@@ -1137,22 +1111,6 @@ __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, 
   const float mv = mu * *m + g;
   *m = mv;
   *w -= lr * mv;
-}
-
-__device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc, float lr,
-                                     float mu) {
-  gv.x += lc * wv.x;
-  gv.y += lc * wv.y;
-  gv.z += lc * wv.z;
-  gv.w += lc * wv.w;
-  mv.x = mu * mv.x + gv.x;
-  mv.y = mu * mv.y + gv.y;
-  mv.z = mu * mv.z + gv.z;
-  mv.w = mu * mv.w + gv.w;
-  wv.x -= lr * mv.x;
-  wv.y -= lr * mv.y;
-  wv.z -= lr * mv.z;
-  wv.w -= lr * mv.w;
 }
 
 __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
@@ -1232,12 +1190,13 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
 void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s) {
+                         const float* lr, long long* step, hipStream_t s, bool fc_done) {
   if (fc_end % 4 || off_w2 % 4 || l2_end != fc_end)
     throw std::runtime_error("sgd_finalize: misaligned flat segments / L2 prefix != FC bucket");
   const long long n4 = fc_end / 4;
   long long b = (n4 + 255) / 256;
-  const int fc_blocks = (int)(b < 2048 ? b : 2048);  // as the flat SGD
+  // fc_done: the FC bucket was updated by the conv2 bwd-data launch's SGD role
+  const int fc_blocks = fc_done ? 0 : (int)(b < 2048 ? b : 2048);  // as the flat SGD
   SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
                part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
                fc_blocks};

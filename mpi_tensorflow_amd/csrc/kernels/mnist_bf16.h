@@ -29,6 +29,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mnist.h"
+
 namespace mnist16 {
 // fp32 master weights -> the four bf16 shadows
 void launch_shadows(const float* w1, const float* w2, uint16_t* w1b, uint16_t* w1t,
@@ -50,10 +52,12 @@ void launch_fc1_bwd(const uint16_t* a2, const uint16_t* a2t, const uint8_t* idx2
                     float* g_w4, float* g_b4, uint16_t* dy2p, uint16_t* dy2t, hipStream_t s);
 // conv2 bwd-data with the ReLU1 mask: da1m fp32 [B][14][14][32]
 void launch_conv2_bwd_data(const uint16_t* dy2p, const uint16_t* w2b, const uint16_t* a1p,
-                           int batch, float* da1m, hipStream_t s);
+                           int batch, float* da1m, hipStream_t s,
+                           const mnist::FcSgdArgs* fc_sgd = nullptr);
 // conv2 bwd-filter partial slabs part2[G][800][64] + db2 partials [4G][64]
 int conv2_filter_groups(int batch);
 void launch_conv2_bwd_filter(const uint16_t* a1t, const uint16_t* dy2t, int batch, float* part2,
-                             hipStream_t s);
+                             hipStream_t s,
+                             const mnist::C1FilterArgs* c1 = nullptr);
 size_t part2_floats(int batch);
 }  // namespace mnist16

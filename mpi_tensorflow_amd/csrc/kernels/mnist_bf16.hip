@@ -272,8 +272,13 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
 __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restrict__ dy2p,
                                                              const bf* __restrict__ w2b,
                                                              const bf* __restrict__ a1p, int batch,
-                                                             float* __restrict__ da1m) {
+                                                             float* __restrict__ da1m,
+                                                             const mnist::FcSgd sgd) {
   __shared__ float red[2][16][64];
+  if ((int)blockIdx.x >= (int)gridDim.x - sgd.nblk) {  // world-1 FC SGD role (mnist_shared.h)
+    mnist::fc_sgd_role(sgd, blockIdx.x - (gridDim.x - sgd.nblk));
+    return;
+  }
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int mtiles = batch * 196 / 32;
   const int mt_raw = blockIdx.x * 2 + (wave & 1), kk = wave >> 1;
@@ -320,8 +325,15 @@ constexpr int C2F_IMG = 8;
 __global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(const bf* __restrict__ a1t,
                                                                const bf* __restrict__ dy2t,
                                                                int batch, float* __restrict__ part2,
-                                                               float* __restrict__ part_db2) {
-  __shared__ float red[3][2][16][64];
+                                                               float* __restrict__ part_db2,
+                                                               int nc2, const mnist::C1Filter c1f) {
+  constexpr int SM = 3 * 2 * 16 * 64 > mnist::C1F_SMEM ? 3 * 2 * 16 * 64 : mnist::C1F_SMEM;
+  __shared__ float smem[SM];
+  if ((int)blockIdx.x >= nc2) {  // conv1 filter-grad role (mnist_shared.h)
+    mnist::conv1_filter_unit<512>(blockIdx.x - nc2, batch, c1f, smem);
+    return;
+  }
+  auto red = reinterpret_cast<float(*)[2][16][64]>(smem);
   const int ngroups = (batch + C2F_IMG - 1) / C2F_IMG;
   const int bid = blockIdx.x;
   int t, g;
@@ -431,20 +443,24 @@ void launch_fc1_bwd(const uint16_t* a2p, const uint16_t* a2t, const uint8_t* idx
 }
 
 void launch_conv2_bwd_data(const uint16_t* dy2p, const uint16_t* w2b, const uint16_t* a1p,
-                           int batch, float* da1m, hipStream_t s) {
+                           int batch, float* da1m, hipStream_t s,
+                           const mnist::FcSgdArgs* fc_sgd) {
   if (batch % 8 != 0) throw std::runtime_error("mnist16 conv2_bwd_data: batch % 8 != 0");
   const int mtiles = batch * 196 / 32;
-  conv2_bwd_data_kernel<<<cdiv(mtiles, 2), 256, 0, s>>>(C16(dy2p), C16(w2b), C16(a1p), batch,
-                                                        da1m);
+  const mnist::FcSgd sg = mnist::fc_sgd_args(fc_sgd);
+  conv2_bwd_data_kernel<<<cdiv(mtiles, 2) + sg.nblk, 256, 0, s>>>(C16(dy2p), C16(w2b), C16(a1p),
+                                                                  batch, da1m, sg);
 }
 
 int conv2_filter_groups(int batch) { return cdiv(batch, C2F_IMG); }
 
 void launch_conv2_bwd_filter(const uint16_t* a1t, const uint16_t* dy2t, int batch, float* part2,
-                             hipStream_t s) {
+                             hipStream_t s, const mnist::C1FilterArgs* c1) {
   const int G = conv2_filter_groups(batch);
-  conv2_bwd_filter_kernel<<<25 * G, 512, 0, s>>>(C16(a1t), C16(dy2t), batch, part2,
-                                                 part2 + (size_t)G * 51200);
+  const mnist::C1Filter c = mnist::c1_args(c1);
+  const int n1 = c.part1 ? mnist::conv1_filter_blocks(batch) : 0;
+  conv2_bwd_filter_kernel<<<25 * G + n1, 512, 0, s>>>(C16(a1t), C16(dy2t), batch, part2,
+                                                      part2 + (size_t)G * 51200, 25 * G, c);
 }
 
 size_t part2_floats(int batch) { return (size_t)conv2_filter_groups(batch) * (51200 + 256); }

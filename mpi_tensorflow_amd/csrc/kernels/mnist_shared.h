@@ -2,6 +2,7 @@
 // (mnist_bf16.hip) MNIST kernel sets.
 #pragma once
 #include "common.h"
+#include "mnist.h"
 
 namespace mnist {
 
@@ -67,6 +68,158 @@ __device__ inline void fc1_small_grads(int blk, const float* hd, const float* dh
   }
 }
 
+// ------------------------------------------------ conv1 filter gradient ----
+// Sparse: each pooled gradient reaches exactly one pre-pool pixel (its argmax),
+// so dW1[t][co] = sum over pooled (n,py,px) of dA1m * x[argmax pixel + tap]
+// (reference mpipy.py:155-157 conv1, B7).  Unit = (image, pair of pooled
+// rows) -> one 832-float partial row part1[unit] (800 weights + 32 biases);
+// thread = (co, position group), NT / 32 groups.  All of a thread's
+// (gradient, argmax) pairs are loaded up front (one latency round); the two
+// groups of a wave are combined by a lane shuffle, the NT / 64 wave partials
+// in a fixed order through LDS.  Run as its own 256-thread kernel or as the
+// 512-thread role blocks appended to the conv2 filter-gradient launch.
+constexpr int C1F_SPLIT = 7;                    // pooled-row pairs per image
+constexpr int C1F_POS = 28;                     // pooled positions per unit
+constexpr int C1F_SMEM = 8 * 32 + 8 * (26 * 32 + 1);  // floats (NT <= 512)
+
+struct C1Filter {  // conv1 filter-grad role arguments (part1 == nullptr: off)
+  const float* data;
+  const long long* step;
+  int n_local;
+  const float* da1m;
+  const uint8_t* idx1;
+  float* part1;
+};
+
+C1Filter c1_args(const C1FilterArgs* a);  // host (mnist.hip)
+int conv1_filter_blocks(int batch);
+
+template <int NT>
+__device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c, float* smem) {
+  constexpr int NG = NT / 32, PER_T = (C1F_POS + NG - 1) / NG, NW = NT / 64;
+  static_assert(NW <= 8, "C1F_SMEM sized for 8 waves");
+  float* xs = smem;                // rows 4*pair-2 .. 4*pair+5 of the padded image
+  float* red = smem + 8 * 32;      // [NW][26 * 32 + 1]
+  const int n = unit / C1F_SPLIT, pair = unit % C1F_SPLIT;
+  const long long off = batch_offset_dev(c.step, c.n_local, batch);
+  const float* x = c.data + (off + n) * 784;
+  const int tid = threadIdx.x, co = tid & 31, grp = tid >> 5, wave = tid >> 6;
+  const int y0 = 4 * pair - 2;  // first image row held in xs
+  if (tid < 256) {
+    const int yy = y0 + tid / 32, xx = tid % 32 - 2;
+    xs[tid] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
+  }
+  float v[PER_T];
+  int q[PER_T];
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int p = grp + NG * j;
+    v[j] = 0.f;
+    q[j] = 0;
+    if (p < C1F_POS) {
+      const int py = 2 * pair + p / 14, px = p % 14;
+      const int e = ((n * 14 + py) * 14 + px) * 32 + co;
+      v[j] = c.da1m[e];
+      q[j] = c.idx1[e];
+    }
+  }
+  __syncthreads();
+  float acc[26];
+#pragma unroll
+  for (int t = 0; t < 26; ++t) acc[t] = 0.f;
+#pragma unroll
+  for (int j = 0; j < PER_T; ++j) {
+    const int p = grp + NG * j;
+    if (p < C1F_POS && v[j] != 0.f) {
+      const int py = 2 * pair + p / 14, px = p % 14;
+      const int ly = 2 * py + (q[j] >> 1) - y0 - 2;  // row in xs of tap kh = 0
+      const int lx = 2 * px + (q[j] & 1);            // col in xs (padded by 2) of kw = 0
+#pragma unroll
+      for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += v[j] * xs[(ly + kh) * 32 + lx + kw];
+      acc[25] += v[j];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 26; ++t) acc[t] += __shfl_xor(acc[t], 32, 64);
+  if ((tid & 32) == 0) {
+#pragma unroll
+    for (int t = 0; t < 26; ++t) red[wave * (26 * 32 + 1) + t * 32 + co] = acc[t];
+  }
+  __syncthreads();
+  for (int i = tid; i < 26 * 32; i += NT) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) s += red[w * (26 * 32 + 1) + i];
+    c.part1[(size_t)unit * 832 + i] = s;
+  }
+}
+
+// momentum SGD on 4 floats: g += lc * w (L2); m = mu m + g; w -= lr m
+__device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc, float lr,
+                                     float mu) {
+  gv.x += lc * wv.x;
+  gv.y += lc * wv.y;
+  gv.z += lc * wv.z;
+  gv.w += lc * wv.w;
+  mv.x = mu * mv.x + gv.x;
+  mv.y = mu * mv.y + gv.y;
+  mv.z = mu * mv.z + gv.z;
+  mv.w = mu * mv.w + gv.w;
+  wv.x -= lr * mv.x;
+  wv.y -= lr * mv.y;
+  wv.z -= lr * mv.z;
+  wv.w -= lr * mv.w;
+}
+
+// ---------------------------------------------- world-1 FC SGD role ----
+// Single-rank step: every FC gradient is final when fc1 backward ends, so the
+// momentum SGD of the FC bucket (flat [0, n4) float4s, all of it under the L2
+// term, reference mpipy.py:58-65) runs as extra blocks of the conv2 bwd-data
+// launch that follows.  That kernel is MFMA / vector-L1 bound on 196 blocks
+// and leaves ~60 CUs idle, which these HBM-streaming blocks fill; the SGD
+// launch at the end of the step then only finishes the conv parameters.
+struct FcSgd {
+  float* w;
+  const float* g;
+  float* m;
+  long long n4;  // float4s; 0 = role off
+  float l2, mu;
+  const float* lr;
+  int nblk;  // extra blocks appended to the grid
+};
+constexpr int FC_SGD_UNROLL = 4;
+FcSgd fc_sgd_args(const FcSgdArgs* a);  // host: role off when a == nullptr (mnist.hip)
+
+__device__ inline void fc_sgd_role(const FcSgd& a, int blk) {
+  float4* W4 = reinterpret_cast<float4*>(a.w);
+  float4* M4 = reinterpret_cast<float4*>(a.m);
+  const float4* G4 = reinterpret_cast<const float4*>(a.g);
+  const float lr = *a.lr;
+  const long long stride = (long long)a.nblk * 256;
+  // U float4s per thread per round, every load of a round in flight together
+  for (long long i0 = (long long)blk * 256 + threadIdx.x; i0 < a.n4;
+       i0 += stride * FC_SGD_UNROLL) {
+    float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
+      const long long i = min(i0 + u * stride, a.n4 - 1);
+      wv[u] = W4[i];
+      gv[u] = G4[i];
+      mv[u] = M4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
+      const long long i = i0 + u * stride;
+      if (i < a.n4) {
+        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
+        W4[i] = wv[u];
+        M4[i] = mv[u];
+      }
+    }
+  }
+}
 
 // ------------------------------------------------------- bf16 shadows ----
 // bf16 engine: the MFMA operand copies of the fp32 master weights (layouts in

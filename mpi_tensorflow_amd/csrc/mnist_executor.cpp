@@ -38,8 +38,9 @@ MnistExecutor::~MnistExecutor() {
 // running concurrently.  Independent work is therefore merged into single
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
-void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize) {
-  if (p_.bf16) return enqueue_fwd_bwd_bf16(s, finalize);
+void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
+                                    const mnist::FcSgdArgs* fc_sgd) {
+  if (p_.bf16) return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd);
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -64,12 +65,13 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize) {
                         P<float>(p.dy2t), s);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
-                                  P<const float>(p.a1), B, P<float>(p.da1m), s);
+                                  P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
+  // conv1 filter grad (needs dA1 from bwd-data) as role blocks of this launch
+  const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
+                               P<const float>(p.da1m), P<const uint8_t>(p.idx1),
+                               P<float>(p.part1)};
   mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
-                                 P<float>(p.part2), s);
-  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
-                                 P<const float>(p.da1m), P<const uint8_t>(p.idx1),
-                                 P<float>(p.part1), s);
+                                 P<float>(p.part2), s, &c1);
   if (finalize)
     mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
                                 P<const float>(p.part1), mnist::conv1_filter_blocks(B),
@@ -80,7 +82,8 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize) {
 // weight shadows from the fp32 master weights, conv1 (K = 25, tiny) stays on
 // fp32 MFMA and writes bf16 images, the conv1 filter grad / fc2 head / slab
 // reductions / SGD stay fp32.
-void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize) {
+void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
+                                         const mnist::FcSgdArgs* fc_sgd) {
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -112,12 +115,12 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize) {
                           P<U16>(p.dy2t), s);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   mnist16::launch_conv2_bwd_data(P<const U16>(p.dy2p), P<const U16>(p.w2b), P<const U16>(p.a1p), B,
-                                 P<float>(p.da1m), s);
+                                 P<float>(p.da1m), s, fc_sgd);
+  const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
+                               P<const float>(p.da1m), P<const uint8_t>(p.idx1),
+                               P<float>(p.part1)};
   mnist16::launch_conv2_bwd_filter(P<const U16>(p.a1t), P<const U16>(p.dy2t), B,
-                                   P<float>(p.part2), s);
-  mnist::launch_conv1_bwd_filter(P<const float>(p.train_x), step, p.n_local, B,
-                                 P<const float>(p.da1m), P<const uint8_t>(p.idx1),
-                                 P<float>(p.part1), s);
+                                   P<float>(p.part2), s, &c1);
   if (finalize)
     mnist::launch_grad_finalize(P<const float>(p.part2), mnist16::conv2_filter_groups(B),
                                 P<const float>(p.part1), mnist::conv1_filter_blocks(B),
@@ -177,12 +180,17 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
     const MnistPtrs& p = p_;
     wait_fc_params(s);
-    enqueue_fwd_bwd(s, /*finalize=*/false);  // the slab sums run inside the SGD launch
+    // the FC bucket's SGD rides in the conv2 bwd-data launch (its grads are final
+    // after fc1 backward); the slab sums + conv SGD run in the last launch
+    const mnist::FcSgdArgs fc{P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
+                              p.bucket1, p.l2, p.momentum, P<const float>(p.lr), fc_sgd_rounds_};
+    const bool fused = fc_sgd_rounds_ > 0 && p.l2_end == p.bucket1;
+    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr);
     mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
                                p.bucket1, p.l2_end, (int)p.off_w2, (int)p.off_b2, (int)p.off_w1,
                                (int)p.off_b1, P<const float>(p.part2), conv2_groups(),
                                P<const float>(p.part1), mnist::conv1_filter_blocks(p.batch), p.l2,
-                               p.momentum, P<const float>(p.lr), P<long long>(p.step), s);
+                               p.momentum, P<const float>(p.lr), P<long long>(p.step), s, fused);
     return;
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {

@@ -56,6 +56,10 @@ struct MnistPtrs {
   int world = 1;
 };
 
+namespace mnist {
+struct FcSgdArgs;
+}
+
 class MnistExecutor {
  public:
   explicit MnistExecutor(const MnistPtrs& p);
@@ -100,18 +104,26 @@ class MnistExecutor {
                          float keep_prob, uint32_t drop_key, hipStream_t s);
 
   const MnistPtrs& ptrs() const { return p_; }
+  // single-rank step: rounds of FC_SGD_UNROLL float4s per thread of the FC SGD
+  // role appended to the conv2 bwd-data launch (sets its block count); 0 runs
+  // the FC SGD in the final SGD launch instead
+  void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? 0 : r; }
 
  private:
   // finalize = false: leave the conv filter grads as slabs (the world-1 SGD
   // launch reduces them itself)
-  void enqueue_fwd_bwd(hipStream_t s, bool finalize = true);
+  // fc_sgd (single rank): FC-bucket SGD appended to the conv2 bwd-data launch
+  void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
+                       const mnist::FcSgdArgs* fc_sgd = nullptr);
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void wait_fc_params(hipStream_t s);
   int sched_ = SCHED_BUCKETS;
   bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on
-  void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true);
+  void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,
+                            const mnist::FcSgdArgs* fc_sgd = nullptr);
+  int fc_sgd_rounds_ = 2;
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;
