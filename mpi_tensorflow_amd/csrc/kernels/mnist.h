@@ -15,6 +15,10 @@ struct FcSgdArgs {
   float l2, momentum;
   const float* lr;
   int rounds;  // FC_SGD_UNROLL-float4 rounds per thread (sets the block count)
+  // bf16 engine: also write the fc1 weight's bf16 shadows (w1 = its float offset)
+  uint16_t* w1b = nullptr;
+  uint16_t* w1t = nullptr;
+  long long w1 = 0;
 };
 // conv1 filter-grad role appended to a conv2 filter-gradient launch (its input
 // dA1m must be final: the conv2 bwd-data launch ran before)

@@ -114,8 +114,8 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void conv_pool_fwd_kernel(
   constexpr int SM = CF::SMEM_FLOATS > SHADOW_SMEM_FLOATS ? CF::SMEM_FLOATS : SHADOW_SMEM_FLOATS;
   __shared__ float smem[SM];
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
-  if (bid >= conv_blocks) {
-    shadow_block(bid - conv_blocks, sh, smem);
+  if (bid >= conv_blocks) {  // sh.w1b == nullptr: conv2 shadows only (the SGD wrote fc1's)
+    shadow_block(bid - conv_blocks + (sh.w1b ? 0 : SHADOW_W1_BLOCKS), sh, smem);
     return;
   }
   const long long off = batch_offset_dev(step_ptr, n_local, batch);
@@ -836,7 +836,7 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_l2_kernel(const float* __r
   __shared__ float red[2][16][64];
   const int nconv = gridDim.x - sgd.nblk;
   if ((int)blockIdx.x >= nconv) {
-    fc_sgd_role(sgd, blockIdx.x - nconv);
+    fc_sgd_role(sgd, blockIdx.x - nconv, nullptr);  // fp32: no shadows
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
@@ -973,7 +973,8 @@ void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local
   const int mt = cdiv(M, 32 * C1_WM), nt = 32 / (32 * C1_WN);
   auto B16 = [](uint16_t* p) { return reinterpret_cast<__bf16*>(p); };
   const ShadowPtrs sh{w3, w2, B16(w1b), B16(w1t), B16(w2tb), B16(w2b)};
-  const int extra = w1b ? SHADOW_BLOCKS : 0;
+  const int extra = (w2tb ? SHADOW_W2_BLOCKS : 0) + (w1b ? SHADOW_W1_BLOCKS : 0);
+  if (w1b && !w2tb) throw std::runtime_error("conv1_fwd_bf16: fc1 shadows without conv2 shadows");
   conv_pool_fwd_kernel<Conv1, C1_WM, C1_WN, C1_WK>
       <<<mt * nt + extra, 64 * C1_WM * C1_WN * C1_WK, 0, s>>>(
           data, step, n_local, batch, w, b, nullptr, argmax, B16(a1p), B16(a1t), ld_batch, nullptr,
@@ -1038,8 +1039,18 @@ FcSgd fc_sgd_args(const FcSgdArgs* a) {
   FcSgd r{};
   if (a == nullptr || a->n == 0) return r;
   if (a->n % 4) throw std::runtime_error("fc_sgd: FC bucket not a multiple of 4 floats");
-  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0};
+  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0};
   const long long per_blk = 256LL * FC_SGD_UNROLL * a->rounds;
+  if (a->w1b) {
+    if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
+      throw std::runtime_error("fc_sgd: fc1 weight misaligned or outside the FC bucket");
+    r.w1b = reinterpret_cast<__bf16*>(a->w1b);
+    r.w1t = reinterpret_cast<__bf16*>(a->w1t);
+    r.w1_off4 = a->w1 / 4;
+    const long long rest = r.n4 - W1_F4;
+    r.nblk = SHADOW_W1_BLOCKS + (int)((rest + per_blk - 1) / per_blk);
+    return r;
+  }
   r.nblk = (int)((r.n4 + per_blk - 1) / per_blk);
   return r;
 }

@@ -274,11 +274,13 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restric
                                                              const bf* __restrict__ a1p, int batch,
                                                              float* __restrict__ da1m,
                                                              const mnist::FcSgd sgd) {
-  __shared__ float red[2][16][64];
+  constexpr int SM = mnist::SHADOW_SMEM_FLOATS > 2 * 16 * 64 ? mnist::SHADOW_SMEM_FLOATS : 2 * 16 * 64;
+  __shared__ float smem[SM];
   if ((int)blockIdx.x >= (int)gridDim.x - sgd.nblk) {  // world-1 FC SGD role (mnist_shared.h)
-    mnist::fc_sgd_role(sgd, blockIdx.x - (gridDim.x - sgd.nblk));
+    mnist::fc_sgd_role(sgd, blockIdx.x - (gridDim.x - sgd.nblk), smem);
     return;
   }
+  auto red = reinterpret_cast<float(*)[16][64]>(smem);
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int mtiles = batch * 196 / 32;
   const int mt_raw = blockIdx.x * 2 + (wave & 1), kk = wave >> 1;

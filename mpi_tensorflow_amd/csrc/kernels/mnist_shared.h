@@ -173,54 +173,6 @@ __device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc
   wv.w -= lr * mv.w;
 }
 
-// ---------------------------------------------- world-1 FC SGD role ----
-// Single-rank step: every FC gradient is final when fc1 backward ends, so the
-// momentum SGD of the FC bucket (flat [0, n4) float4s, all of it under the L2
-// term, reference mpipy.py:58-65) runs as extra blocks of the conv2 bwd-data
-// launch that follows.  That kernel is MFMA / vector-L1 bound on 196 blocks
-// and leaves ~60 CUs idle, which these HBM-streaming blocks fill; the SGD
-// launch at the end of the step then only finishes the conv parameters.
-struct FcSgd {
-  float* w;
-  const float* g;
-  float* m;
-  long long n4;  // float4s; 0 = role off
-  float l2, mu;
-  const float* lr;
-  int nblk;  // extra blocks appended to the grid
-};
-constexpr int FC_SGD_UNROLL = 4;
-FcSgd fc_sgd_args(const FcSgdArgs* a);  // host: role off when a == nullptr (mnist.hip)
-
-__device__ inline void fc_sgd_role(const FcSgd& a, int blk) {
-  float4* W4 = reinterpret_cast<float4*>(a.w);
-  float4* M4 = reinterpret_cast<float4*>(a.m);
-  const float4* G4 = reinterpret_cast<const float4*>(a.g);
-  const float lr = *a.lr;
-  const long long stride = (long long)a.nblk * 256;
-  // U float4s per thread per round, every load of a round in flight together
-  for (long long i0 = (long long)blk * 256 + threadIdx.x; i0 < a.n4;
-       i0 += stride * FC_SGD_UNROLL) {
-    float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];
-#pragma unroll
-    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
-      const long long i = min(i0 + u * stride, a.n4 - 1);
-      wv[u] = W4[i];
-      gv[u] = G4[i];
-      mv[u] = M4[i];
-    }
-#pragma unroll
-    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
-      const long long i = i0 + u * stride;
-      if (i < a.n4) {
-        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
-        W4[i] = wv[u];
-        M4[i] = mv[u];
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------- bf16 shadows ----
 // bf16 engine: the MFMA operand copies of the fp32 master weights (layouts in
 // mnist_bf16.h), re-derived at the start of every step.  Blocks [0, 392): one
@@ -287,6 +239,114 @@ __device__ inline void shadow_block(int L, const ShadowPtrs sp, float* tile) {
     const int t = idx >> 11, ci = (idx >> 6) & 31, co = idx & 63;
     sp.w2t[((t * 2 + (ci >> 4)) * 64 + co) * 16 + (ci & 15)] = v;
     sp.w2b[((t * 4 + (co >> 4)) * 32 + ci) * 16 + (co & 15)] = v;
+  }
+}
+
+// ---------------------------------------------- world-1 FC SGD role ----
+// Single-rank step: every FC gradient is final when fc1 backward ends, so the
+// momentum SGD of the FC bucket (flat [0, n4) float4s, all of it under the L2
+// term, reference mpipy.py:58-65) runs as extra blocks of the conv2 bwd-data
+// launch that follows.  That kernel is MFMA / vector-L1 bound on 196 blocks
+// and leaves ~60 CUs idle, which these HBM-streaming blocks fill; the SGD
+// launch at the end of the step then only finishes the conv parameters.
+struct FcSgd {
+  float* w;
+  const float* g;
+  float* m;
+  long long n4;  // float4s; 0 = role off
+  float l2, mu;
+  const float* lr;
+  int nblk;  // extra blocks appended to the grid
+  // bf16 engine, single rank: the fc1 weight's bf16 MFMA shadows (layouts of
+  // shadow_block below) are written by the same threads that update it, so
+  // the next step's conv1 launch only re-derives the small conv2 shadows.
+  // fc1 weight = float4s [w1_off4, w1_off4 + W1_F4) of the bucket, updated in
+  // SHADOW_W1_BLOCKS 64 x 64 tiles (LDS transpose for w1t); the other blocks
+  // stream the rest of the bucket.
+  __bf16* w1b;
+  __bf16* w1t;
+  long long w1_off4;
+};
+constexpr int FC_SGD_UNROLL = 4;
+constexpr long long W1_F4 = (long long)FC1_IN * FC1_OUT / 4;
+FcSgd fc_sgd_args(const FcSgdArgs* a);  // host: role off when a == nullptr (mnist.hip)
+
+// one 64 x 64 tile of the fc1 weight: momentum SGD + both bf16 shadows
+__device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* tile) {
+  const int tid = threadIdx.x;
+  const int i0 = (L % (FC1_IN / 64)) * 64, j0 = (L / (FC1_IN / 64)) * 64;
+  const int row = tid >> 2, ck = tid & 3;
+  const size_t e0 = (size_t)a.w1_off4 * 4 + (size_t)(i0 + row) * FC1_OUT + j0 + 16 * ck;
+  float4* W4 = reinterpret_cast<float4*>(a.w + e0);
+  float4* M4 = reinterpret_cast<float4*>(a.m + e0);
+  const float4* G4 = reinterpret_cast<const float4*>(a.g + e0);
+  float4 wv[4], gv[4], mv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    wv[u] = W4[u];
+    gv[u] = G4[u];
+    mv[u] = M4[u];
+  }
+  float v[16];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
+    W4[u] = wv[u];
+    M4[u] = mv[u];
+    v[4 * u] = wv[u].x;
+    v[4 * u + 1] = wv[u].y;
+    v[4 * u + 2] = wv[u].z;
+    v[4 * u + 3] = wv[u].w;
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) tile[row * 65 + 16 * ck + e] = v[e];
+  shadow_store16(a.w1b + ((size_t)((j0 >> 4) + ck) * FC1_IN + i0 + row) * 16, v);
+  __syncthreads();
+  const int col = tid >> 2;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) v[e] = tile[(16 * ck + e) * 65 + col];
+  shadow_store16(a.w1t + ((size_t)((i0 >> 4) + ck) * FC1_OUT + j0 + col) * 16, v);
+}
+
+// blk: index among the role's blocks; tile: >= 64 x 65 floats of LDS when
+// a.w1b is set (256-thread blocks)
+__device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile) {
+  float4* W4 = reinterpret_cast<float4*>(a.w);
+  float4* M4 = reinterpret_cast<float4*>(a.m);
+  const float4* G4 = reinterpret_cast<const float4*>(a.g);
+  const float lr = *a.lr;
+  long long n4 = a.n4;
+  int nb = a.nblk;
+  if (a.w1b) {
+    if (blk < SHADOW_W1_BLOCKS) {
+      fc_sgd_w1_tile(a, blk, lr, tile);
+      return;
+    }
+    blk -= SHADOW_W1_BLOCKS;
+    nb -= SHADOW_W1_BLOCKS;
+    n4 -= W1_F4;  // the rest of the bucket, the fc1 weight's float4s skipped
+  }
+  const long long stride = (long long)nb * 256;
+  auto at = [&](long long f) { return (a.w1b && f >= a.w1_off4) ? f + W1_F4 : f; };
+  // U float4s per thread per round, every load of a round in flight together
+  for (long long i0 = (long long)blk * 256 + threadIdx.x; i0 < n4; i0 += stride * FC_SGD_UNROLL) {
+    float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];
+#pragma unroll
+    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
+      const long long i = at(min(i0 + u * stride, n4 - 1));
+      wv[u] = W4[i];
+      gv[u] = G4[i];
+      mv[u] = M4[i];
+    }
+#pragma unroll
+    for (int u = 0; u < FC_SGD_UNROLL; ++u) {
+      if (i0 + u * stride < n4) {
+        const long long i = at(i0 + u * stride);
+        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
+        W4[i] = wv[u];
+        M4[i] = mv[u];
+      }
+    }
   }
 }
 

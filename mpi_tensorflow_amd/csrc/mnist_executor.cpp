@@ -94,10 +94,12 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
   // the conv1 launch also re-derives the bf16 weight shadows (block role):
   // measured as fast as having the SGD write them (which needs a refresh
   // after any outside change of the weights), and always correct
+  // (fc_sgd->w1b: the previous step's SGD already wrote the fc1 shadows)
+  const bool w1_done = fc_sgd != nullptr && fc_sgd->w1b != nullptr;
   mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
                                W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1), B,
-                               s, W + p.off_w3, W + p.off_w2, P<U16>(p.w1b), P<U16>(p.w1t),
-                               P<U16>(p.w2tb), P<U16>(p.w2b));
+                               s, W + p.off_w3, W + p.off_w2, w1_done ? nullptr : P<U16>(p.w1b),
+                               P<U16>(p.w1t), P<U16>(p.w2tb), P<U16>(p.w2b));
   mnist16::launch_conv2_fwd(P<const U16>(p.a1p), B, P<const U16>(p.w2tb), W + p.off_b2,
                             P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2), s);
   mnist16::launch_fc1_fwd_train(P<const U16>(p.a2h), P<const U16>(p.w1t), B, P<float>(p.fc1_part),
@@ -154,6 +156,13 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
                              bump_step ? P<long long>(p.step) : nullptr, s);
 }
 
+void MnistExecutor::refresh_shadows(hipStream_t s) {
+  if (!p_.bf16) return;
+  const float* W = P<const float>(p_.params);
+  mnist16::launch_shadows(W + p_.off_w3, W + p_.off_w2, P<uint16_t>(p_.w1b), P<uint16_t>(p_.w1t),
+                          P<uint16_t>(p_.w2tb), P<uint16_t>(p_.w2b), s);
+}
+
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
@@ -182,8 +191,13 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
     wait_fc_params(s);
     // the FC bucket's SGD rides in the conv2 bwd-data launch (its grads are final
     // after fc1 backward); the slab sums + conv SGD run in the last launch
-    const mnist::FcSgdArgs fc{P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
-                              p.bucket1, p.l2, p.momentum, P<const float>(p.lr), fc_sgd_rounds_};
+    mnist::FcSgdArgs fc{P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
+                        p.bucket1, p.l2, p.momentum, P<const float>(p.lr), fc_sgd_rounds_};
+    if (p.bf16 && p.world == 1) {  // the SGD also writes the fc1 bf16 shadows (see refresh_shadows)
+      fc.w1b = P<uint16_t>(p.w1b);
+      fc.w1t = P<uint16_t>(p.w1t);
+      fc.w1 = p.off_w3;
+    }
     const bool fused = fc_sgd_rounds_ > 0 && p.l2_end == p.bucket1;
     enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr);
     mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),

@@ -108,6 +108,13 @@ class MnistExecutor {
   // role appended to the conv2 bwd-data launch (sets its block count); 0 runs
   // the FC SGD in the final SGD launch instead
   void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? 0 : r; }
+  // bf16 engine: re-derive every bf16 weight shadow from the fp32 master
+  // weights.  A single-rank bf16 step writes the fc1 shadows from its SGD and
+  // the next step relies on them, so the caller refreshes them once before a
+  // run of steps (the engine does so at the start of every train() call):
+  // any change to the weights between runs (init, checkpoint load, ...) is
+  // picked up there.
+  void refresh_shadows(hipStream_t s);
 
  private:
   // finalize = false: leave the conv filter grads as slabs (the world-1 SGD

@@ -392,6 +392,10 @@ class NativeMnistEngine(MnistEngineBase):
     def train(self, k: int) -> None:
         if k <= 0:
             return
+        # bf16: the single-rank step's SGD writes the fc1 weight shadows the next
+        # step reads, so re-derive them from the master weights before a run of
+        # steps (picks up any change made to the weights since the last run)
+        self.exe.refresh_shadows(stream_handle())
         if not self._tuned and k >= self.tune_steps():
             k -= self.tune_schedule()
         done = 0
