@@ -52,6 +52,8 @@ def parse(argv=None):
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded", "split"))
+    ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),
+                    help="wire dtype of the gradient all-reduce (bf16: half the xGMI bytes)")
     ap.add_argument("--comm-emulate", default=None, metavar="LAT_US,BUSBW_GBPS[,N[,BLOCKS]]",
                     help="1 GPU: replace the collectives by timing stand-ins of an N-rank ring "
                          "(default N=8, 32 workgroups) to measure sync/compute overlap")
@@ -132,7 +134,8 @@ def main(argv=None) -> int:
         a.batch_size = 32 if a.model == "resnet18" else 64
     cfg = C.TrainConfig(model=a.model, batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
                         graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend,
-                        sync_schedule=a.sync_schedule).validate()
+                        sync_schedule=a.sync_schedule,
+                        grad_comm_dtype=a.grad_comm_dtype).validate()
     comm = make_comm(di, device) if (N > 1 and a.sync == "grad") else None
     force = bool((a.force_sync or a.comm_emulate) and N == 1 and device.type == "cuda")
     if force and a.comm_emulate:
@@ -241,6 +244,7 @@ def main(argv=None) -> int:
                 "ranks": N,
                 "rccl_nranks": rccl_nranks,
                 "sync_schedule": getattr(eng, "sync_schedule", "n/a"),
+                "grad_comm_dtype": a.grad_comm_dtype,
                 "sync_tune_us_per_step": getattr(eng, "tune_log", {}) or None,
                 "sync_tune_steps": tune_steps,
                 "graph_steps": (a.graph_steps if not a.no_graph else 0),

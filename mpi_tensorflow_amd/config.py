@@ -83,6 +83,10 @@ class TrainConfig:
     sync: str = "grad"
     sync_every: int = SYNC_EVERY
     sync_schedule: str = "auto"
+    # dtype of the gradient collectives: fp32 (the reference's MPI Gather of
+    # fp32 tensors) or bf16 (half the bytes over xGMI; the sum is rounded to
+    # bf16 on the wire, the update stays fp32)
+    grad_comm_dtype: str = "fp32"
     # evaluate (and print the reference log line) every N steps; the
     # reference evaluates every step (Q9) but prints every 50
     eval_every: int = SYNC_EVERY
@@ -125,6 +129,8 @@ class TrainConfig:
         if self.sync_schedule not in SYNC_SCHEDULES:
             raise ValueError(f"unknown sync schedule {self.sync_schedule!r}; "
                              f"choose from {SYNC_SCHEDULES}")
+        if self.grad_comm_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"unknown grad comm dtype {self.grad_comm_dtype!r}")
         if self.dtype not in DTYPES:
             raise ValueError(f"unknown dtype {self.dtype!r}; choose from {DTYPES}")
         if self.backend not in ("auto", "native", "torch"):
@@ -173,6 +179,8 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--sync-every", type=int, default=d.sync_every)
     p.add_argument("--sync-schedule", default=d.sync_schedule, choices=SYNC_SCHEDULES,
                    help="native MNIST grad-sync schedule (auto / buckets / sharded FC update)")
+    p.add_argument("--grad-comm-dtype", default=d.grad_comm_dtype, choices=("fp32", "bf16"),
+                   help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--eval-every", type=int, default=d.eval_every,
                    help="0 disables periodic eval")
     p.add_argument("--data-dir", default=d.data_dir)

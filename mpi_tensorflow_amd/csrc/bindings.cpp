@@ -160,6 +160,14 @@ PYBIND11_MODULE(_C, m) {
                                P<long long>(step_ptr), S(s));
     check_launch();
   });
+  o.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t s) {
+    optim::launch_to_bf16(P<const float>(x), P<uint16_t>(y), n, S(s));
+    check_launch();
+  });
+  o.def("from_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t s) {
+    optim::launch_from_bf16(P<const uint16_t>(x), P<float>(y), n, S(s));
+    check_launch();
+  });
   o.def("scale", [](uintptr_t x, long long n, float a, uintptr_t s) {
     optim::launch_scale(P<float>(x), n, a, S(s));
     check_launch();
@@ -339,7 +347,7 @@ PYBIND11_MODULE(_C, m) {
                   RW(off_b2) RW(off_w1) RW(off_b1) RW(step) RW(lr) RW(correct) RW(a1) RW(idx1)
                       RW(a2) RW(idx2) RW(fc1_part) RW(hd) RW(dh) RW(dlog) RW(loss_rows) RW(dy2)
                           RW(da1m) RW(part2) RW(part1) RW(w2t) RW(a1pf) RW(keep_prob) RW(base_lr) RW(lr_decay)
-                              RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16)
+                              RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16) RW(grad_bf16) RW(gb16)
                                   RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
                                       RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b);
 #undef RW
@@ -408,7 +416,7 @@ PYBIND11_MODULE(_C, m) {
 #define RWL(f) .def_readwrite(#f, &LenetPtrs::f)
           RWL(train_x) RWL(train_y) RWL(n_local) RWL(batch) RWL(params) RWL(grads) RWL(mom)
               RWL(total) RWL(off) RWL(step) RWL(lr) RWL(correct) RWL(acts) RWL(deltas) RWL(convp)
-                  RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum);
+                  RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum) RWL(grad_bf16) RWL(gb16);
 #undef RWL
   m.def("lenet_buffer_floats", [](int batch) {
     return py::make_tuple(lenet::acts_floats(batch), lenet::deltas_floats(batch),

@@ -101,4 +101,7 @@ void launch_sgd_momentum(float* w, const float* g, float* mom, long long n, long
                          float l2, float momentum, float gscale, const float* lr_ptr,
                          float lr_const, long long* step_ptr, hipStream_t s);
 void launch_scale(float* x, long long n, float a, hipStream_t s);
+// bf16 gradient wire: bucket copies around a collective (n % 4 == 0, 16-B aligned)
+void launch_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
+void launch_from_bf16(const uint16_t* x, float* y, long long n, hipStream_t s);
 }  // namespace optim

@@ -7,6 +7,8 @@
 //   w  -= lr * acc
 // lr comes from the device (written by the fc head from the device step
 // counter), so the kernel is graph-replayable; one thread bumps the step.
+#include <stdexcept>
+
 #include "common.h"
 #include "mnist.h"
 
@@ -51,6 +53,28 @@ __global__ __launch_bounds__(256) void scale_kernel(float4* __restrict__ x, long
   }
 }
 
+// bf16 gradient wire (--grad-comm-dtype bf16): fp32 <-> bf16 copies of a
+// gradient bucket around its collective (round to nearest even)
+__global__ __launch_bounds__(256) void to_bf16_kernel(const float4* __restrict__ x,
+                                                     uint2* __restrict__ y, long long n4) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = x[i];
+    __bf16 b[4] = {(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+    y[i] = __builtin_bit_cast(uint2, b);
+  }
+}
+
+__global__ __launch_bounds__(256) void from_bf16_kernel(const uint2* __restrict__ x,
+                                                       float4* __restrict__ y, long long n4) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const uint2 u = x[i];
+    y[i] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                       __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+  }
+}
+
 static inline int grid_for(long long n4) {
   long long b = (n4 + 255) / 256;
   return (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
@@ -64,6 +88,18 @@ void launch_sgd_momentum(float* w, const float* g, float* mom, long long n, long
       reinterpret_cast<float4*>(w), reinterpret_cast<const float4*>(g),
       reinterpret_cast<float4*>(mom), n4, l2_end / 4, l2, momentum, gscale, lr_ptr, lr_const,
       step_ptr);
+}
+
+void launch_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s) {
+  if (n % 4) throw std::runtime_error("to_bf16: n % 4 != 0");
+  to_bf16_kernel<<<grid_for(n / 4), 256, 0, s>>>(reinterpret_cast<const float4*>(x),
+                                                 reinterpret_cast<uint2*>(y), n / 4);
+}
+
+void launch_from_bf16(const uint16_t* x, float* y, long long n, hipStream_t s) {
+  if (n % 4) throw std::runtime_error("from_bf16: n % 4 != 0");
+  from_bf16_kernel<<<grid_for(n / 4), 256, 0, s>>>(reinterpret_cast<const uint2*>(x),
+                                                   reinterpret_cast<float4*>(y), n / 4);
 }
 
 void launch_scale(float* x, long long n, float a, hipStream_t s) {

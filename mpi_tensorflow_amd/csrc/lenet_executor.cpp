@@ -50,7 +50,14 @@ void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
                        p_.momentum, P<const float>(p_.lr), P<long long>(p_.step), apply, s);
   if (apply) return;
   float* G = P<float>(p_.grads);
-  comm->all_reduce(G, G, (size_t)p_.total, 7 /*ncclFloat32*/, 0 /*ncclSum*/, s);
+  if (p_.grad_bf16) {
+    uint16_t* B = P<uint16_t>(p_.gb16);
+    optim::launch_to_bf16(G, B, p_.total, s);
+    comm->all_reduce(B, B, (size_t)p_.total, 9 /*ncclBfloat16*/, 0 /*ncclSum*/, s);
+    optim::launch_from_bf16(B, G, p_.total, s);
+  } else {
+    comm->all_reduce(G, G, (size_t)p_.total, 7 /*ncclFloat32*/, 0 /*ncclSum*/, s);
+  }
   optim::launch_sgd_momentum(P<float>(p_.params), G, P<float>(p_.mom), p_.total, 0, 0.f,
                              p_.momentum, 1.0f / (float)comm->size(), P<const float>(p_.lr), 0.f,
                              P<long long>(p_.step), s);

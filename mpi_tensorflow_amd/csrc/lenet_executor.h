@@ -26,6 +26,10 @@ struct LenetPtrs {
   uintptr_t step = 0, lr = 0, correct = 0;
   uintptr_t acts = 0, deltas = 0, convp = 0, loss_rows = 0;
   float base_lr = 0.01f, lr_decay = 0.95f, momentum = 0.9f;
+  // --grad-comm-dtype bf16: the all-reduce runs on a bf16 copy (gb16, total
+  // elements) of the grads
+  int grad_bf16 = 0;
+  uintptr_t gb16 = 0;
 };
 
 class LenetExecutor {

@@ -156,6 +156,18 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
                              bump_step ? P<long long>(p.step) : nullptr, s);
 }
 
+void MnistExecutor::reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs) {
+  float* G = P<float>(p_.grads) + lo;
+  if (!p_.grad_bf16) {
+    comm->all_reduce(G, G, (size_t)n, ncclFloat32, ncclSum, cs);
+    return;
+  }
+  uint16_t* B = P<uint16_t>(p_.gb16) + lo;
+  optim::launch_to_bf16(G, B, n, cs);
+  comm->all_reduce(B, B, (size_t)n, ncclBfloat16, ncclSum, cs);
+  optim::launch_from_bf16(B, G, n, cs);
+}
+
 void MnistExecutor::refresh_shadows(hipStream_t s) {
   if (!p_.bf16) return;
   const float* W = P<const float>(p_.params);
@@ -223,13 +235,12 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1 backward is done;
   // it overlaps the conv backward still running on the compute stream
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
-  comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
+  reduce_bucket(comm, 0, p.bucket1, cs);
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   // bucket 2 (conv grads) after the slab reduction, same ordered stream
   HIP_CHECK(hipEventRecord(ev_fin_, s));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
-  comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
-                   ncclSum, cs);
+  reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
   HIP_CHECK(hipEventRecord(ev_done_, cs));
   // FC update while bucket 2 is in flight, then the conv update
   HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
@@ -257,12 +268,18 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
   const long long chunk = p.bucket1 / n, lo = chunk * comm->rank();
   enqueue_fwd_bwd(s);
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
-  comm->reduce_scatter(G, G + lo, (size_t)chunk, ncclFloat32, ncclSum, cs);
+  if (p.grad_bf16) {  // bf16 wire: the shard comes back to fp32 before its SGD
+    uint16_t* Gb = P<uint16_t>(p.gb16);
+    optim::launch_to_bf16(G, Gb, p.bucket1, cs);
+    comm->reduce_scatter(Gb, Gb + lo, (size_t)chunk, ncclBfloat16, ncclSum, cs);
+    optim::launch_from_bf16(Gb + lo, G + lo, chunk, cs);
+  } else {
+    comm->reduce_scatter(G, G + lo, (size_t)chunk, ncclFloat32, ncclSum, cs);
+  }
   sgd_range(cs, lo, lo + chunk, gscale, false);
   HIP_CHECK(hipEventRecord(ev_fin_, s));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
-  comm->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
-                   ncclSum, cs);
+  reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
   HIP_CHECK(hipEventRecord(ev_done_, cs));
   comm->all_gather(W + lo, W, (size_t)chunk, ncclFloat32, cs);
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
@@ -280,16 +297,14 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
 void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_t cs,
                                      Collective* comm2) {
   const MnistPtrs& p = p_;
-  float* G = P<float>(p.grads);
   const float gscale = 1.0f / (float)comm->size();
   enqueue_fwd_bwd(s);
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
-  comm->all_reduce(G, G, (size_t)p.bucket1, ncclFloat32, ncclSum, cs);
+  reduce_bucket(comm, 0, p.bucket1, cs);
   sgd_range(cs, 0, p.bucket1, gscale, false);
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   fc_pending_ = true;
-  comm2->all_reduce(G + p.bucket1, G + p.bucket1, (size_t)(p.total - p.bucket1), ncclFloat32,
-                    ncclSum, s);
+  reduce_bucket(comm2, p.bucket1, p.total - p.bucket1, s);
   sgd_range(s, p.bucket1, p.total, gscale, true);
 }
 

@@ -54,6 +54,11 @@ struct MnistPtrs {
   float keep_prob = 0.5f, base_lr = 0.01f, lr_decay = 0.95f, l2 = 5e-4f, momentum = 0.9f;
   uint32_t seed = 1, rank = 0;
   int world = 1;
+  // gradient wire dtype of the collectives (--grad-comm-dtype): 0 = fp32 (the
+  // reference's), 1 = bf16 (half the bytes over xGMI; gb16 = a bf16 staging
+  // buffer of `total` elements)
+  int grad_bf16 = 0;
+  uintptr_t gb16 = 0;
 };
 
 namespace mnist {
@@ -126,6 +131,8 @@ class MnistExecutor {
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void wait_fc_params(hipStream_t s);
+  // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
+  void reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs);
   int sched_ = SCHED_BUCKETS;
   bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on
   void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,

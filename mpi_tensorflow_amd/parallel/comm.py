@@ -182,26 +182,30 @@ class HostStagedComm(DeviceComm):
         self.bases = []
         self._c = native().PyComm(di.world, di.rank, self._callback)
 
-    def _view(self, p: int, count: int) -> torch.Tensor:
+    def _view(self, p: int, count: int, dtype=torch.float32) -> torch.Tensor:
+        es = torch.empty((), dtype=dtype).element_size()
         for b in self.bases:
+            if b.dtype != dtype:
+                continue
             off = p - b.data_ptr()
-            if 0 <= off and off + 4 * count <= 4 * b.numel():
-                return b.view(-1)[off // 4: off // 4 + count]
+            if 0 <= off and off + es * count <= es * b.numel():
+                return b.view(-1)[off // es: off // es + count]
         raise ValueError("HostStagedComm: pointer outside the registered tensors")
 
     def _callback(self, op: str, send: int, recv: int, count: int, dtype: int) -> None:
-        if dtype != NCCL_FLOAT32:
-            raise ValueError("HostStagedComm handles float32 only")
+        if dtype not in (NCCL_FLOAT32, NCCL_BF16):
+            raise ValueError("HostStagedComm handles float32 / bfloat16 only")
+        dt = torch.float32 if dtype == NCCL_FLOAT32 else torch.bfloat16
         torch.cuda.synchronize()
         n = self.size
-        if op == "all_reduce":
-            t = self._view(send, count).cpu()
+        if op == "all_reduce":  # bf16: summed in fp32 on the host, rounded back
+            t = self._view(send, count, dt).cpu().float()
             dist.all_reduce(t)
-            self._view(recv, count).copy_(t)
+            self._view(recv, count, dt).copy_(t.to(dt))
         elif op == "reduce_scatter":
-            t = self._view(send, count * n).cpu()
+            t = self._view(send, count * n, dt).cpu().float()
             dist.all_reduce(t)
-            self._view(recv, count).copy_(t[self.rank * count:(self.rank + 1) * count])
+            self._view(recv, count, dt).copy_(t[self.rank * count:(self.rank + 1) * count].to(dt))
         elif op == "all_gather":
             t = self._view(send, count).cpu()
             parts = [torch.empty_like(t) for _ in range(n)]
@@ -225,6 +229,35 @@ class HostStagedComm(DeviceComm):
 
     def duplicate(self):
         return self  # synchronous host staging: one object serves both streams
+
+
+def all_reduce_grads_(comm: DeviceComm, t: torch.Tensor, wire: str = "fp32", stream=None,
+                      stage: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum-all-reduce of a gradient tensor over the `wire` dtype
+    (TrainConfig.grad_comm_dtype).  bf16 on a GPU: the native conversion
+    kernels fill `stage` (a bf16 tensor of t's size), the collective runs on
+    it and the sum comes back to fp32; on the CPU (gloo) the same rounding is
+    emulated (inputs and the sum rounded to bf16)."""
+    if wire == "fp32":
+        if stream is None:
+            return comm.all_reduce_(t)
+        return comm.all_reduce_(t, stream=stream)
+    if t.is_cuda:
+        if stage is None or stage.dtype != torch.bfloat16 or stage.numel() != t.numel():
+            raise ValueError("bf16 gradient wire needs a bf16 staging tensor of the bucket's size")
+        C = native()
+        sh = stream_handle(stream)
+        C.optim.to_bf16(ptr(t), ptr(stage), t.numel(), sh)
+        if stream is None:
+            comm.all_reduce_(stage)
+        else:
+            comm.all_reduce_(stage, stream=stream)
+        C.optim.from_bf16(ptr(stage), ptr(t), t.numel(), sh)
+        return t
+    b = t.to(torch.bfloat16).float()
+    comm.all_reduce_(b)
+    t.copy_(b.to(torch.bfloat16).float())
+    return t
 
 
 class TorchDeviceComm(DeviceComm):

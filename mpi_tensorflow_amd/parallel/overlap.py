@@ -32,17 +32,22 @@ from typing import Dict, List, Optional
 
 import torch
 
-from .comm import DeviceComm
+from .comm import DeviceComm, all_reduce_grads_
 from .flat import FlatLayout
 
 
 class BucketedAllReduce:
     def __init__(self, layout: FlatLayout, grads: torch.Tensor, comm: DeviceComm,
-                 device: torch.device):
+                 device: torch.device, wire: str = "fp32"):
         self.comm = comm
         self.grads = grads
+        self.wire = wire  # gradient wire dtype (TrainConfig.grad_comm_dtype)
         ranges = layout.buckets()  # [(lo, hi)] per bucket id, in flat order
         self.slices: List[torch.Tensor] = [grads[lo:hi] for lo, hi in ranges]
+        self.stage: List[Optional[torch.Tensor]] = [None] * len(ranges)
+        if wire == "bf16":  # bf16 staging per bucket (native conversions around the collective)
+            st = torch.zeros(grads.numel(), dtype=torch.bfloat16, device=device)
+            self.stage = [st[lo:hi] for lo, hi in ranges]
         views = layout.views(grads)
         self.bucket_of: Dict[int, int] = {}
         self.size = [0] * len(ranges)
@@ -64,13 +69,15 @@ class BucketedAllReduce:
         self.launched[b] = True
         self.order.append(b)
         if len(self.slices) == 1:  # one bucket: no overlap to gain, no cross-queue hop
-            self.comm.all_reduce_(self.slices[b], stream=torch.cuda.current_stream())
+            all_reduce_grads_(self.comm, self.slices[b], self.wire,
+                              stream=torch.cuda.current_stream(), stage=self.stage[b])
             return
         ev = self.events[b]
         ev.record(torch.cuda.current_stream())
         self.stream.wait_event(ev)
         with torch.cuda.stream(self.stream):
-            self.comm.all_reduce_(self.slices[b], stream=self.stream)
+            all_reduce_grads_(self.comm, self.slices[b], self.wire, stream=self.stream,
+                              stage=self.stage[b])
 
     def grad_ready(self, grad_view: Optional[torch.Tensor]) -> None:
         if grad_view is None:

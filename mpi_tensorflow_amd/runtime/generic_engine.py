@@ -35,7 +35,7 @@ from .. import config as C
 from ..models.generic import make_model
 from ..ops import functional as Fn
 from ..ops import native, ptr, stream_handle
-from ..parallel.comm import DeviceComm
+from ..parallel.comm import DeviceComm, all_reduce_grads_
 from ..parallel.overlap import BucketedAllReduce
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
@@ -85,7 +85,8 @@ class GenericEngine:
             if self.grad_sync:
                 if comm.native_handle is None:
                     raise RuntimeError("GPU grad sync needs the native RCCL communicator")
-                self.bucketer = BucketedAllReduce(self.layout, self.grads, comm, device)
+                self.bucketer = BucketedAllReduce(self.layout, self.grads, comm, device,
+                                                  wire=cfg.grad_comm_dtype)
                 comm.all_reduce_(self.grads)  # connection setup outside any capture
                 torch.cuda.synchronize(device)
             h, w, c = train_x.shape[1:]
@@ -190,7 +191,7 @@ class GenericEngine:
             self.grads.copy_(self.params.grad)
             self.loss_buf.copy_(loss.detach())
             if self.grad_sync:
-                self.comm.all_reduce_(self.grads)
+                all_reduce_grads_(self.comm, self.grads, self.cfg.grad_comm_dtype)
                 self.grads.mul_(1.0 / self.world)
             self.mom.mul_(self.cfg.momentum).add_(self.grads)
             self.params.sub_(self.lr() * self.mom)

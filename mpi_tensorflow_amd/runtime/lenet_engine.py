@@ -87,6 +87,12 @@ class NativeLenetEngine:
         p.acts, p.deltas, p.convp = ptr(self.acts), ptr(self.deltas), ptr(self.convp)
         p.loss_rows = ptr(self.loss_rows)
         p.base_lr, p.lr_decay, p.momentum = cfg.base_lr, cfg.lr_decay, cfg.momentum
+        self.gb16 = None  # bf16 gradient wire staging (--grad-comm-dtype bf16)
+        if cfg.grad_comm_dtype == "bf16" and self.grad_sync:
+            if self.layout.total % 4:
+                raise RuntimeError("bf16 gradient wire needs a flat buffer of 4k floats")
+            self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)
+            p.grad_bf16, p.gb16 = 1, ptr(self.gb16)
         self.ptrs = p
         self.exe = C_.LenetExecutor(p)
         self._native_comm = None
@@ -95,7 +101,7 @@ class NativeLenetEngine:
             if self._native_comm is None:
                 raise RuntimeError("GPU grad sync needs the native RCCL communicator")
             if getattr(comm, "kind", "") == "host-staged":  # test comm: eager only
-                comm.bases = [self.grads]
+                comm.bases = [self.grads] + ([self.gb16] if self.gb16 is not None else [])
             # connection setup of the collective, outside any capture
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())

@@ -32,7 +32,7 @@ import torch
 from .. import config as C
 from ..models import mnist_cnn as M
 from ..ops import native, ptr, stream_handle
-from ..parallel.comm import DeviceComm
+from ..parallel.comm import DeviceComm, all_reduce_grads_
 from ..utils import rng
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
@@ -137,7 +137,7 @@ class TorchMnistEngine(MnistEngineBase):
             self.forward_backward(self.step)
             gscale = 1.0
             if self.grad_sync:
-                self.comm.all_reduce_(self.grads)
+                all_reduce_grads_(self.comm, self.grads, self.cfg.grad_comm_dtype)
                 gscale = 1.0 / self.world
             lr = self.lr(self.step)
             _, l2_end = self.layout.l2_range()
@@ -251,6 +251,10 @@ class NativeMnistEngine(MnistEngineBase):
         p.l2, p.momentum = cfg.l2, cfg.momentum
         p.seed, p.rank, p.world = cfg.seed, self.drop_rank, world
         p.bf16 = 1 if self.bf16 else 0
+        self.gb16 = None  # bf16 gradient wire staging (--grad-comm-dtype bf16)
+        if cfg.grad_comm_dtype == "bf16" and world > 1:
+            self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)
+            p.grad_bf16, p.gb16 = 1, ptr(self.gb16)
         self.ptrs = p
         self.exe = C_.MnistExecutor(p)
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
@@ -264,7 +268,8 @@ class NativeMnistEngine(MnistEngineBase):
         if self.grad_sync:
             self.exe.set_schedule(self._pick_schedule(cfg.sync_schedule, self._native_comm.size))
         if getattr(self.comm, "kind", "") == "host-staged":  # test comm: eager only
-            self.comm.bases = [self.grads, self.params, self.mom]
+            self.comm.bases = [self.grads, self.params, self.mom] + (
+                [self.gb16] if self.gb16 is not None else [])
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self.use_graph = cfg.graph and getattr(self.comm, "kind", "") != "host-staged"
         self.graph_steps = max(1, cfg.graph_steps)

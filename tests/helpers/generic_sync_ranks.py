@@ -7,7 +7,10 @@ forward/backward on the same kernels, grads summed, one SGD with gscale 1/N)
 and the params must be bit-identical; all ranks must hold the same params.
 MODEL "lenet5-native" runs the fused LeNet-5 executor (runtime/lenet_engine.py)
 instead, whose single flat-gradient all-reduce goes through the same comm.
-Launch: torchrun --nproc-per-node 2 ... generic_sync_ranks.py MODEL STEPS BATCH"""
+WIRE "bf16" (optional 4th argument) uses the bf16 gradient wire
+(--grad-comm-dtype bf16); the serial emulation then sums bf16(grad_r) and
+rounds the sum to bf16.
+Launch: torchrun --nproc-per-node 2 ... generic_sync_ranks.py MODEL STEPS BATCH [WIRE]"""
 import sys
 
 import numpy as np
@@ -37,10 +40,11 @@ def main():
     Eng = NativeLenetEngine if fused else GenericEngine
     steps = int(sys.argv[2])
     B = int(sys.argv[3])
+    wire = sys.argv[4] if len(sys.argv) > 4 else "fp32"
     rows = 4 * B
     di = D.init("cuda")
     dev = torch.device("cuda")
-    cfg = C.TrainConfig(model=model, batch_size=B, graph=False).validate()
+    cfg = C.TrainConfig(model=model, batch_size=B, graph=False, grad_comm_dtype=wire).validate()
     x, y = shard(model, di.rank, rows, cfg.seed)
     eng = Eng(cfg, x, y, dev, di.rank, di.world, HostStagedComm(di))
     assert eng.grad_sync
@@ -64,8 +68,12 @@ def main():
                     e.forward_backward_only()
                 else:
                     e.forward_backward_gpu()
-            for e in engs[1:]:
-                lead.grads.add_(e.grads)
+            if wire == "bf16":
+                gs = sum(e.grads.to(torch.bfloat16).float() for e in engs)
+                lead.grads.copy_(gs.to(torch.bfloat16).float())
+            else:
+                for e in engs[1:]:
+                    lead.grads.add_(e.grads)
             if fused:  # the flat SGD the executor runs after its all-reduce
                 native().optim.sgd_momentum(ptr(lead.params), ptr(lead.grads), ptr(lead.mom),
                                             lead.layout.total, 0, 0.0, cfg.momentum,
@@ -78,8 +86,8 @@ def main():
         d = (p - q).abs().max().item()
         assert torch.equal(p, q), f"serial emulation differs by {d}"
         assert np.isfinite(p.numpy()).all()
-        print(f"GENERIC_SYNC_OK model={sys.argv[1]} world={di.world} buckets={nb} steps={steps}",
-              flush=True)
+        print(f"GENERIC_SYNC_OK model={sys.argv[1]} world={di.world} buckets={nb} steps={steps} "
+              f"wire={wire}", flush=True)
     D.barrier()
     D.shutdown()
 

@@ -9,7 +9,10 @@ cross-rank data), and checks
   * switching schedules mid-run (buckets -> sharded -> buckets, what the
     startup autotune does) keeps the replicas identical to a buckets-only run
     (the FC momentum shards are gathered before leaving the sharded schedule);
-  * every rank holds the same params (replica consistency).
+  * every rank holds the same params (replica consistency);
+  * with the bf16 gradient wire (--grad-comm-dtype bf16) buckets and sharded
+    agree bit for bit and equal the serial emulation with the sum formed as
+    bf16(sum of bf16(grad_r)).
 Launch: torchrun --nproc-per-node 2 --master-addr 127.0.0.1 tests/helpers/native_sync_ranks.py"""
 import sys
 
@@ -31,8 +34,9 @@ def _shard(rank, world, seed):
     return sh.train_x[:ROWS], sh.train_y[:ROWS]
 
 
-def make(schedule, dtype, di):
-    cfg = C.TrainConfig(sync_schedule=schedule, dtype=dtype, graph=False).validate()
+def make(schedule, dtype, di, wire="fp32"):
+    cfg = C.TrainConfig(sync_schedule=schedule, dtype=dtype, graph=False,
+                        grad_comm_dtype=wire).validate()
     x, y = _shard(di.rank, di.world, cfg.seed)
     comm = HostStagedComm(di)
     eng = NativeMnistEngine(cfg, x, y, torch.device("cuda"), di.rank, di.world, comm)
@@ -47,8 +51,8 @@ def finish(eng):
     return eng.params.cpu(), eng.mom.cpu()
 
 
-def run(schedule, dtype, steps, di):
-    eng = make(schedule, dtype, di)
+def run(schedule, dtype, steps, di, wire="fp32"):
+    eng = make(schedule, dtype, di, wire)
     eng.train(steps)
     return finish(eng)
 
@@ -66,7 +70,7 @@ def run_switching(dtype, steps, di):
     return finish(eng)
 
 
-def serial(dtype, steps, world):
+def serial(dtype, steps, world, wire="fp32"):
     """One process plays every rank: same kernels, summed grads, one SGD."""
     C_ = native()
     cfg = C.TrainConfig(dtype=dtype, graph=False).validate()
@@ -85,9 +89,11 @@ def serial(dtype, steps, world):
                 e.params.copy_(lead.params)
                 e.step_dev.copy_(lead.step_dev)
             e.forward_backward_only()
-        gsum.copy_(engs[0].grads)
+        rnd = (lambda t: t.to(torch.bfloat16).float()) if wire == "bf16" else (lambda t: t)
+        gsum.copy_(rnd(engs[0].grads))
         for e in engs[1:]:
-            gsum.add_(e.grads)
+            gsum.add_(rnd(e.grads))
+        gsum.copy_(rnd(gsum))
         # lead.lr_dev was written by its head kernel from the device step
         C_.optim.sgd_momentum(ptr(lead.params), ptr(gsum), ptr(lead.mom), lead.layout.total, hi,
                               cfg.l2, cfg.momentum, 1.0 / world, ptr(lead.lr_dev), 0.0,
@@ -116,7 +122,19 @@ def main():
         p1, m1 = serial(dtype, steps, di.world)
         assert torch.equal(pb, p1), f"serial emulation: params differ: {(pb - p1).abs().max().item()}"
         assert torch.equal(mb, m1), f"serial emulation: momentum differs: {(mb - m1).abs().max().item()}"
-        print(f"NATIVE_SYNC_OK world={di.world} steps={steps} dtype={dtype}", flush=True)
+    # bf16 gradient wire
+    pbb, mbb = run("buckets", dtype, steps, di, "bf16")
+    psb, msb = run("sharded", dtype, steps, di, "bf16")
+    assert torch.equal(pbb, psb) and torch.equal(mbb, msb), "bf16 wire: sharded != buckets"
+    assert not torch.equal(pbb, pb), "bf16 wire left the update unchanged"
+    if di.rank == 0:
+        p2, m2 = serial(dtype, steps, di.world, "bf16")
+        assert torch.equal(pbb, p2), f"bf16 wire vs serial: params differ: {(pbb - p2).abs().max().item()}"
+        assert torch.equal(mbb, m2), f"bf16 wire vs serial: momentum differs: {(mbb - m2).abs().max().item()}"
+        rel = ((pbb - pb).norm() / pb.norm()).item()
+        assert rel < 1e-2, f"bf16 wire drifted from fp32: rel {rel}"
+        print(f"NATIVE_SYNC_OK world={di.world} steps={steps} dtype={dtype} bf16-wire-rel={rel:.2e}",
+              flush=True)
     D.barrier()
     D.shutdown()
 

@@ -34,7 +34,7 @@ def _env(rank, world, port):
         os.environ.pop(k, None)
 
 
-def _worker_grad_sync(rank, world, port, out_dir, steps):
+def _worker_grad_sync(rank, world, port, out_dir, steps, wire="fp32"):
     torch.set_num_threads(2)
     _env(rank, world, port)
     from mpi_tensorflow_amd import config as C
@@ -46,7 +46,7 @@ def _worker_grad_sync(rank, world, port, out_dir, steps):
     di = D.init("cpu")
     comm = make_comm(di, torch.device("cpu"))
     x, y = synthetic_rows("train", rank * 512, (rank + 1) * 512)
-    cfg = C.TrainConfig(device="cpu").validate()
+    cfg = C.TrainConfig(device="cpu", grad_comm_dtype=wire).validate()
     eng = TorchMnistEngine(cfg, x, y, torch.device("cpu"), rank, world, comm)
     eng.train(steps)
     np.save(os.path.join(out_dir, f"p{rank}.npy"), eng.params.numpy())
@@ -54,9 +54,14 @@ def _worker_grad_sync(rank, world, port, out_dir, steps):
 
 
 @pytest.mark.slow
-def test_grad_allreduce_keeps_replicas_identical_and_matches_serial(tmp_path):
+@pytest.mark.parametrize("wire", ["fp32", "bf16"])
+def test_grad_allreduce_keeps_replicas_identical_and_matches_serial(tmp_path, wire):
+    """Per-step gradient all-reduce over gloo (fp32, or the bf16 gradient wire
+    of --grad-comm-dtype: every rank's grads and their sum rounded to bf16)
+    vs a serial emulation."""
     world, steps, port = 2, 3, _free_port()
-    mp.spawn(_worker_grad_sync, args=(world, port, str(tmp_path), steps), nprocs=world, join=True)
+    mp.spawn(_worker_grad_sync, args=(world, port, str(tmp_path), steps, wire), nprocs=world,
+             join=True)
     p0 = np.load(tmp_path / "p0.npy")
     p1 = np.load(tmp_path / "p1.npy")
     assert np.array_equal(p0, p1), "replicas diverged under per-step gradient all-reduce"
@@ -73,13 +78,14 @@ def test_grad_allreduce_keeps_replicas_identical_and_matches_serial(tmp_path):
         engs.append(TorchMnistEngine(cfg, x, y, torch.device("cpu"), r, world, None))
     lead = engs[0]
     _, l2_end = lead.layout.l2_range()
+    rnd = (lambda t: t.to(torch.bfloat16).float()) if wire == "bf16" else (lambda t: t)
     for s in range(steps):
         gsum = torch.zeros_like(lead.grads)
         for e in engs:
             e.params.copy_(lead.params)
             e.forward_backward(s)
-            gsum += e.grads
-        g = gsum / world
+            gsum += rnd(e.grads)
+        g = rnd(gsum) / world
         g[:l2_end] += cfg.l2 * lead.params[:l2_end]
         lead.mom.mul_(cfg.momentum).add_(g)
         lead.params.sub_(lead.lr(s) * lead.mom)

@@ -34,16 +34,19 @@ def test_sharded_schedule_matches_buckets_two_ranks(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,steps,batch", [("lenet5", 5, 64), ("resnet18", 3, 4),
-                                               ("lenet5-native", 6, 64)])
-def test_generic_bucketed_allreduce_matches_serial_two_ranks(model, steps, batch):
+@pytest.mark.parametrize("model,steps,batch,wire", [("lenet5", 5, 64, "fp32"),
+                                                    ("resnet18", 3, 4, "fp32"),
+                                                    ("lenet5-native", 6, 64, "fp32"),
+                                                    ("lenet5", 5, 64, "bf16"),
+                                                    ("lenet5-native", 6, 64, "bf16")])
+def test_generic_bucketed_allreduce_matches_serial_two_ranks(model, steps, batch, wire):
     """Backward-overlapped bucketed all-reduce (parallel/overlap.py) with real
     cross-rank sums vs a serial averaged-gradient emulation: bit-identical."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "helpers", "generic_sync_ranks.py"), model, str(steps),
-           str(batch)]
+           str(batch), wire]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
-    assert f"GENERIC_SYNC_OK model={model} world=2" in r.stdout
+    assert f"GENERIC_SYNC_OK model={model} world=2" in r.stdout and f"wire={wire}" in r.stdout
