@@ -1435,6 +1435,7 @@ long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue) {
 __global__ __launch_bounds__(256) void im2col_bf16_kernel(ConvShape s, const float* __restrict__ x,
                                                           int kp, int seg, uint4* __restrict__ col) {
   const int kq = kp / 8, sq = seg / 8, sc = s.S * s.C;
+  const long long nx = (long long)s.N * s.H * s.W * s.C;
   const int total = s.N * s.OH * s.OW * kq;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int m = i / kq, c = i - m * kq;
@@ -1446,9 +1447,20 @@ __global__ __launch_bounds__(256) void im2col_bf16_kernel(ConvShape s, const flo
     if (kh < s.R && iy >= 0 && iy < s.H) {
       const int jlo = max(0, -ix0) * s.C, jhi = min(sc, (s.W - ix0) * s.C);
       const long long rowbase = ((long long)(n * s.H + iy) * s.W + ix0) * s.C;
+      const long long e0 = rowbase + j0;
+      if (e0 >= 0 && e0 + 8 <= nx) {
+        // two 16-byte loads at 4-byte alignment (full speed on gfx950), then
+        // the run is masked to the in-image part [jlo, jhi) of the segment
+        const float4 a = *reinterpret_cast<const float4*>(x + e0);
+        const float4 b = *reinterpret_cast<const float4*>(x + e0 + 4);
+        const float r[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j0 + j >= jlo && j0 + j < jhi) v[j] = x[rowbase + j0 + j];
+        for (int j = 0; j < 8; ++j) v[j] = (j0 + j >= jlo && j0 + j < jhi) ? r[j] : 0.f;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j0 + j >= jlo && j0 + j < jhi) v[j] = x[rowbase + j0 + j];
+      }
     }
     col[i] = cbf::pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
   }
