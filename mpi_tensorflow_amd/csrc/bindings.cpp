@@ -286,6 +286,17 @@ PYBIND11_MODULE(_C, m) {
     gops::maxpool_fwd(p, P<const float>(x), P<float>(y), P<int>(arg), S(st));
     check_launch();
   });
+  g.def("maxpool_b16_ok", &gops::maxpool_b16_ok);
+  g.def("maxpool_fwd_b16", [](const gops::PoolShape& p, uintptr_t xb, uintptr_t y, uintptr_t yb,
+                              uintptr_t arg, uintptr_t st) {
+    gops::maxpool_fwd_b16(p, P<const void>(xb), P<float>(y), P<void>(yb), P<uint8_t>(arg), S(st));
+    check_launch();
+  });
+  g.def("maxpool_bwd_b8", [](const gops::PoolShape& p, uintptr_t dy, uintptr_t arg, uintptr_t dx,
+                             uintptr_t st) {
+    gops::maxpool_bwd_b8(p, P<const float>(dy), P<const uint8_t>(arg), P<float>(dx), S(st));
+    check_launch();
+  });
   g.def("maxpool_bwd", [](const gops::PoolShape& p, uintptr_t dy, uintptr_t arg, uintptr_t dx, uintptr_t st) {
     gops::maxpool_bwd(p, P<const float>(dy), P<const int>(arg), P<float>(dx), S(st));
     check_launch();

@@ -107,6 +107,13 @@ void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, co
             bool yb16 = false);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
+// bf16-twin form: xb = bf16 input, y (fp32) / yb (bf16) outputs each optional,
+// arg = window-relative tap (uint8); C % 4 == 0, k * k < 255
+bool maxpool_b16_ok(const PoolShape& p);
+void maxpool_fwd_b16(const PoolShape& p, const void* xb, float* y, void* yb, uint8_t* arg,
+                     hipStream_t st);
+void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, float* dx,
+                    hipStream_t st);
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st);
 void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t st);
 void xent(const float* logits, const int* labels, int B, int C, float* loss_rows, float* dlogits,

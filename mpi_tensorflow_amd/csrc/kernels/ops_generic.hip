@@ -433,6 +433,88 @@ __global__ __launch_bounds__(256) void maxpool_bwd4_kernel(PoolShape p, const fl
   }
 }
 
+// bf16-twin form (ResNet stem in bf16 conv mode): x is the bf16 twin of the
+// BatchNorm output (whose fp32 storage is then never written), the argmax is
+// the window-relative tap (uint8: kh * k + kw, 255 = empty window) instead of
+// an int32 pixel index, and the output gets its own bf16 twin for the next
+// conv.  Per step at B=32 this drops the BN's 102 MB fp32 store, half of the
+// pool's input bytes, 3/4 of its argmax bytes and a to_bf16 pass.
+__device__ __forceinline__ float4 bf4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
+__global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const uint2* __restrict__ x,
+                                                            float4* __restrict__ y,
+                                                            uint2* __restrict__ yb,
+                                                            uchar4* __restrict__ arg) {
+  const int C4 = p.C / 4;
+  const int n = p.N * p.OH * p.OW * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    int t = i / C4;
+    const int ox = t % p.OW;
+    t /= p.OW;
+    const int oy = t % p.OH, nn = t / p.OH;
+    float4 b = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    uchar4 bi = make_uchar4(255, 255, 255, 255);
+    for (int kh = 0; kh < p.k; ++kh) {
+      const int iy = oy * p.stride - p.pad + kh;
+      if (iy < 0 || iy >= p.H) continue;
+      for (int kw = 0; kw < p.k; ++kw) {
+        const int ix = ox * p.stride - p.pad + kw;
+        if (ix < 0 || ix >= p.W) continue;
+        const float4 v = bf4(x[((nn * p.H + iy) * p.W + ix) * C4 + c4]);
+        const unsigned char r = (unsigned char)(kh * p.k + kw);
+        if (v.x > b.x) { b.x = v.x; bi.x = r; }
+        if (v.y > b.y) { b.y = v.y; bi.y = r; }
+        if (v.z > b.z) { b.z = v.z; bi.z = r; }
+        if (v.w > b.w) { b.w = v.w; bi.w = r; }
+      }
+    }
+    if (y) y[i] = b;
+    if (yb) {  // the maxima are bf16 values already: exact
+      __bf16 h[4] = {(__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      yb[i] = __builtin_bit_cast(uint2, h);
+    }
+    arg[i] = bi;
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd4b_kernel(PoolShape p, const float4* __restrict__ dy,
+                                                            const uchar4* __restrict__ arg,
+                                                            float4* __restrict__ dx) {
+  const int C4 = p.C / 4;
+  const int n = p.N * p.H * p.W * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    const int pix = i / C4;
+    const int ix = pix % p.W, t = pix / p.W;
+    const int iy = t % p.H, nn = t / p.H;
+    const int oy0 = max(0, (iy + p.pad - p.k + p.stride) / p.stride);
+    const int oy1 = min(p.OH - 1, (iy + p.pad) / p.stride);
+    const int ox0 = max(0, (ix + p.pad - p.k + p.stride) / p.stride);
+    const int ox1 = min(p.OW - 1, (ix + p.pad) / p.stride);
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int oy = oy0; oy <= oy1; ++oy)
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int o = ((nn * p.OH + oy) * p.OW + ox) * C4 + c4;
+        // this pixel's tap index inside window (oy, ox)
+        const unsigned char r =
+            (unsigned char)((iy - (oy * p.stride - p.pad)) * p.k + (ix - (ox * p.stride - p.pad)));
+        const uchar4 a = arg[o];
+        if (a.x == r || a.y == r || a.z == r || a.w == r) {
+          const float4 d = dy[o];
+          if (a.x == r) g.x += d.x;
+          if (a.y == r) g.y += d.y;
+          if (a.z == r) g.z += d.z;
+          if (a.w == r) g.w += d.w;
+        }
+      }
+    dx[i] = g;
+  }
+}
+
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x,
                                                           float* __restrict__ y, int N, int HW,
                                                           int C) {
@@ -921,6 +1003,26 @@ void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx,
                                                        reinterpret_cast<float4*>(dx));
   else
     maxpool_bwd_kernel<<<grid1d(n), 256, 0, st>>>(p, dy, arg, dx);
+}
+
+bool maxpool_b16_ok(const PoolShape& p) { return pool_vec4(p) && p.k * p.k < 255; }
+
+void maxpool_fwd_b16(const PoolShape& p, const void* xb, float* y, void* yb, uint8_t* arg,
+                     hipStream_t st) {
+  if (!maxpool_b16_ok(p)) throw std::runtime_error("maxpool_fwd_b16: unsupported shape");
+  const long long n = (long long)p.N * p.OH * p.OW * p.C;
+  maxpool_fwd4b_kernel<<<grid1d(n / 4), 256, 0, st>>>(
+      p, reinterpret_cast<const uint2*>(xb), reinterpret_cast<float4*>(y),
+      reinterpret_cast<uint2*>(yb), reinterpret_cast<uchar4*>(arg));
+}
+
+void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, float* dx,
+                    hipStream_t st) {
+  if (!maxpool_b16_ok(p)) throw std::runtime_error("maxpool_bwd_b8: unsupported shape");
+  const long long n = (long long)p.N * p.H * p.W * p.C;
+  maxpool_bwd4b_kernel<<<grid1d(n / 4), 256, 0, st>>>(p, reinterpret_cast<const float4*>(dy),
+                                                      reinterpret_cast<const uchar4*>(arg),
+                                                      reinterpret_cast<float4*>(dx));
 }
 
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st) {

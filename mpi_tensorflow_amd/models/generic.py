@@ -169,7 +169,7 @@ class ResNet18(GenericModel):
         # every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
         # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise
         h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True)
-        h = BN(h, "bn1", True)
+        h = BN(h, "bn1", True, twin_only=True)  # the pool reads its bf16 twin
         h = Fn.maxpool(h, 3, 2, 1)
         join = x.is_cuda and training and torch.is_grad_enabled()
         for name, cin, c, s, down in self._blocks():

@@ -132,6 +132,14 @@ def _attach_bf16(t: torch.Tensor, tb: torch.Tensor) -> None:
     t._mta_bf16 = (tb, t._version, t.data_ptr())
 
 
+def _bf16_twin(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """The attached bf16 copy of t if it is still valid, else None."""
+    a = getattr(t, "_mta_bf16", None)
+    if a is not None and a[1] == t._version and a[2] == t.data_ptr() and t.is_contiguous():
+        return a[0]
+    return None
+
+
 def _bf16_copy(t: torch.Tensor, s) -> torch.Tensor:
     if t.dtype == torch.bfloat16:  # already bf16 (a bf16-input BatchNorm's dX)
         return t.contiguous()
@@ -532,8 +540,20 @@ class _MaxPoolFn(torch.autograd.Function):
         N, H, W, Cc = x.shape
         sh = C.ops.PoolShape(N, H, W, Cc, k, stride, pad)
         y = _empty((N, sh.OH, sh.OW, Cc), x)
-        arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.int32, device=x.device)
-        C.ops.maxpool_fwd(sh, ptr(x), ptr(y), ptr(arg), stream_handle())
+        s = stream_handle()
+        xb = _bf16_twin(x)
+        ctx.b8 = xb is not None and C.ops.maxpool_b16_ok(sh)
+        if ctx.b8:
+            # bf16 conv mode: pool the producer's bf16 twin (a twin-only BN
+            # output), uint8 window-relative argmax, bf16 twin of the output
+            arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.uint8, device=x.device)
+            yb = _bf16_out(y)
+            C.ops.maxpool_fwd_b16(sh, ptr(xb), ptr(y), ptr(yb), ptr(arg), s)
+            if yb is not None:
+                _attach_bf16(y, yb)
+        else:
+            arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.int32, device=x.device)
+            C.ops.maxpool_fwd(sh, ptr(x), ptr(y), ptr(arg), s)
         ctx.save_for_backward(arg)
         ctx.sh, ctx.xshape = sh, x.shape
         return y
@@ -543,7 +563,10 @@ class _MaxPoolFn(torch.autograd.Function):
         C = native()
         (arg,) = ctx.saved_tensors
         dx = _empty(ctx.xshape, dy)
-        C.ops.maxpool_bwd(ctx.sh, ptr(dy.contiguous()), ptr(arg), ptr(dx), stream_handle())
+        if ctx.b8:
+            C.ops.maxpool_bwd_b8(ctx.sh, ptr(dy.contiguous()), ptr(arg), ptr(dx), stream_handle())
+        else:
+            C.ops.maxpool_bwd(ctx.sh, ptr(dy.contiguous()), ptr(arg), ptr(dx), stream_handle())
         return dx, None, None, None
 
 

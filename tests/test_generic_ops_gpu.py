@@ -119,6 +119,34 @@ def test_maxpool(cuda_dev, k, stride, pad, H, C):
     assert _rel(xg.grad.cpu(), xr.grad) < 1e-6
 
 
+@pytest.mark.parametrize("C", [16, 64])
+def test_maxpool_bf16_twin(cuda_dev, C):
+    """bf16 conv mode: the pool reads the input's attached bf16 twin (a
+    twin-only BN output, whose fp32 storage is garbage here on purpose),
+    records uint8 window taps and gives its output a bf16 twin; values and
+    gradients equal torch's pool of the bf16-rounded input."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 15, 15, C, generator=g)
+    xb = x.to(torch.bfloat16)
+    xr = xb.float().clone().requires_grad_(True)
+    yr = F.max_pool2d(xr.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy)
+    xg = torch.full(x.shape, float("nan"), device=cuda_dev).requires_grad_(True)
+    Fn._attach_bf16(xg, xb.to(cuda_dev))
+    Fn.set_conv_bf16(True)
+    yg = Fn.maxpool(xg, 3, 2, 1)
+    yg.backward(dy.to(cuda_dev))
+    torch.cuda.synchronize()
+    assert torch.equal(yg.detach().cpu(), yr.detach())
+    assert _rel(xg.grad.cpu(), xr.grad) < 1e-6
+    tw = Fn._bf16_twin(yg)
+    if C % 64 == 0:
+        assert tw is not None and torch.equal(tw.float().cpu(), yr.detach())
+    else:
+        assert tw is None
+
+
 def test_avgpool_and_xent(cuda_dev):
     g = torch.Generator().manual_seed(3)
     x = torch.randn(4, 7, 7, 33, generator=g)
