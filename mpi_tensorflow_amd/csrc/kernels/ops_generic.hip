@@ -444,11 +444,20 @@ __device__ __forceinline__ float4 bf4(uint2 u) {
                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
 
+// KK / SS / PP / CC4: compile-time window, stride, pad and C/4 (the ResNet
+// stem's 3 / 2 / 1 / 16; 0 = read from p): the index math is then multiplies
+// and shifts instead of integer divides
+template <int KK, int SS, int PP, int CC4>
 __global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const uint2* __restrict__ x,
                                                             float4* __restrict__ y,
                                                             uint2* __restrict__ yb,
                                                             uchar4* __restrict__ arg) {
-  const int C4 = p.C / 4;
+  if constexpr (KK > 0) {
+    p.k = KK;
+    p.stride = SS;
+    p.pad = PP;
+  }
+  const int C4 = CC4 > 0 ? CC4 : p.C / 4;
   const int n = p.N * p.OH * p.OW * C4;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int c4 = i % C4;
@@ -481,10 +490,16 @@ __global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const u
   }
 }
 
+template <int KK, int SS, int PP, int CC4>
 __global__ __launch_bounds__(256) void maxpool_bwd4b_kernel(PoolShape p, const float4* __restrict__ dy,
                                                             const uchar4* __restrict__ arg,
                                                             float4* __restrict__ dx) {
-  const int C4 = p.C / 4;
+  if constexpr (KK > 0) {
+    p.k = KK;
+    p.stride = SS;
+    p.pad = PP;
+  }
+  const int C4 = CC4 > 0 ? CC4 : p.C / 4;
   const int n = p.N * p.H * p.W * C4;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int c4 = i % C4;
@@ -515,9 +530,37 @@ __global__ __launch_bounds__(256) void maxpool_bwd4b_kernel(PoolShape p, const f
   }
 }
 
+// block = (image n, 32 channels) x 8 pixel groups; the group partials are
+// summed through LDS in a fixed order (ResNet-18 head: 512 blocks instead of
+// 64 threads-per-channel blocks walking 49 dependent loads, 13 -> ~3 us)
 __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restrict__ x,
                                                           float* __restrict__ y, int N, int HW,
                                                           int C) {
+  __shared__ float red[8][33];
+  const int cb = C / 32, n = blockIdx.x / cb, c0 = (blockIdx.x % cb) * 32;
+  const int cl = threadIdx.x & 31, g = threadIdx.x >> 5, c = c0 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  const float* xp = x + (size_t)n * HW * C + c;
+  int p = g;
+  for (; p + 8 < HW; p += 16) {
+    s0 += xp[(size_t)p * C];
+    s1 += xp[(size_t)(p + 8) * C];
+  }
+  if (p < HW) s0 += xp[(size_t)p * C];
+  red[g][cl] = s0 + s1;
+  __syncthreads();
+  if (g == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t += red[j][cl];
+    y[(size_t)n * C + c] = t / (float)HW;
+  }
+}
+
+// C % 32 != 0 fallback: thread per (n, c)
+__global__ __launch_bounds__(256) void avgpool_fwd1_kernel(const float* __restrict__ x,
+                                                           float* __restrict__ y, int N, int HW,
+                                                           int C) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= N * C) return;
   const int n = i / C, c = i % C;
@@ -529,13 +572,11 @@ __global__ __launch_bounds__(256) void avgpool_fwd_kernel(const float* __restric
 __global__ __launch_bounds__(256) void avgpool_bwd_kernel(const float* __restrict__ dy,
                                                           float* __restrict__ dx, int N, int HW,
                                                           int C) {
-  const long long n = (long long)N * HW * C;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int c = (int)(i % C);
-    const int nn = (int)(i / ((long long)HW * C));
-    dx[i] = dy[nn * C + c] / (float)HW;
-  }
+  const int n = N * HW * C;  // host checks < 2^31: 32-bit index math
+  const int stride = gridDim.x * blockDim.x, hwc = HW * C;
+  const float inv = 1.f / (float)HW;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    dx[i] = dy[(i / hwc) * C + i % C] * inv;
 }
 
 // ----------------------------------------------------- softmax xent ----
@@ -1011,25 +1052,38 @@ void maxpool_fwd_b16(const PoolShape& p, const void* xb, float* y, void* yb, uin
                      hipStream_t st) {
   if (!maxpool_b16_ok(p)) throw std::runtime_error("maxpool_fwd_b16: unsupported shape");
   const long long n = (long long)p.N * p.OH * p.OW * p.C;
-  maxpool_fwd4b_kernel<<<grid1d(n / 4), 256, 0, st>>>(
-      p, reinterpret_cast<const uint2*>(xb), reinterpret_cast<float4*>(y),
-      reinterpret_cast<uint2*>(yb), reinterpret_cast<uchar4*>(arg));
+  const auto X = reinterpret_cast<const uint2*>(xb);
+  const auto Y = reinterpret_cast<float4*>(y);
+  const auto YB = reinterpret_cast<uint2*>(yb);
+  const auto A = reinterpret_cast<uchar4*>(arg);
+  if (p.k == 3 && p.stride == 2 && p.pad == 1 && p.C == 64)  // the ResNet stem pool
+    maxpool_fwd4b_kernel<3, 2, 1, 16><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, YB, A);
+  else
+    maxpool_fwd4b_kernel<0, 0, 0, 0><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, YB, A);
 }
 
 void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, float* dx,
                     hipStream_t st) {
   if (!maxpool_b16_ok(p)) throw std::runtime_error("maxpool_bwd_b8: unsupported shape");
   const long long n = (long long)p.N * p.H * p.W * p.C;
-  maxpool_bwd4b_kernel<<<grid1d(n / 4), 256, 0, st>>>(p, reinterpret_cast<const float4*>(dy),
-                                                      reinterpret_cast<const uchar4*>(arg),
-                                                      reinterpret_cast<float4*>(dx));
+  const auto D = reinterpret_cast<const float4*>(dy);
+  const auto A = reinterpret_cast<const uchar4*>(arg);
+  const auto DX = reinterpret_cast<float4*>(dx);
+  if (p.k == 3 && p.stride == 2 && p.pad == 1 && p.C == 64)
+    maxpool_bwd4b_kernel<3, 2, 1, 16><<<grid1d(n / 4), 256, 0, st>>>(p, D, A, DX);
+  else
+    maxpool_bwd4b_kernel<0, 0, 0, 0><<<grid1d(n / 4), 256, 0, st>>>(p, D, A, DX);
 }
 
 void avgpool_fwd(const float* x, float* y, int N, int HW, int C, hipStream_t st) {
-  avgpool_fwd_kernel<<<(N * C + 255) / 256, 256, 0, st>>>(x, y, N, HW, C);
+  if (C % 32 == 0)
+    avgpool_fwd_kernel<<<N * (C / 32), 256, 0, st>>>(x, y, N, HW, C);
+  else
+    avgpool_fwd1_kernel<<<(N * C + 255) / 256, 256, 0, st>>>(x, y, N, HW, C);
 }
 
 void avgpool_bwd(const float* dy, float* dx, int N, int HW, int C, hipStream_t st) {
+  if ((long long)N * HW * C >= (1LL << 31)) throw std::runtime_error("avgpool_bwd: too large");
   avgpool_bwd_kernel<<<grid1d((long long)N * HW * C), 256, 0, st>>>(dy, dx, N, HW, C);
 }
 

@@ -149,12 +149,13 @@ def test_maxpool_bf16_twin(cuda_dev, C):
 
 def test_avgpool_and_xent(cuda_dev):
     g = torch.Generator().manual_seed(3)
-    x = torch.randn(4, 7, 7, 33, generator=g)
-    xg = x.to(cuda_dev).requires_grad_(True)
-    y = Fn.global_avgpool(xg)
-    y.sum().backward()
-    assert _rel(y.cpu(), x.mean(dim=(1, 2))) < 1e-6
-    assert torch.allclose(xg.grad.cpu(), torch.full_like(x, 1 / 49.0))
+    for C in (33, 512):  # per-(n, c) fallback, 32-channel x 8-group blocks
+        x = torch.randn(4, 7, 7, C, generator=g)
+        xg = x.to(cuda_dev).requires_grad_(True)
+        y = Fn.global_avgpool(xg)
+        y.sum().backward()
+        assert _rel(y.cpu(), x.mean(dim=(1, 2))) < 1e-6
+        assert torch.allclose(xg.grad.cpu(), torch.full_like(x, 1 / 49.0))
     logits = torch.randn(9, 13, generator=g)
     lab = torch.randint(0, 13, (9,), generator=g)
     lr_ = logits.clone().requires_grad_(True)
