@@ -201,6 +201,18 @@ PYBIND11_MODULE(_C, m) {
     gops::im2col_bf16(s, P<const float>(x), kp, P<void>(col), S(st));
     check_launch();
   });
+  g.def("conv_fwd_stem_bf16", [](const gops::ConvShape& s1, const gops::ConvShape& si,
+                                 uintptr_t x, uintptr_t wtb, uintptr_t yb, uintptr_t st) {
+    gops::conv_fwd_stem_bf16(s1, si, P<const float>(x), P<const void>(wtb), P<void>(yb), S(st));
+    check_launch();
+  });
+  g.def("conv_bwd_filter_stem_bf16",
+        [](const gops::ConvShape& s1, const gops::ConvShape& si, uintptr_t x, uintptr_t dyb,
+           uintptr_t ws, uintptr_t dw, uintptr_t st) {
+          gops::conv_bwd_filter_stem_bf16(s1, si, P<const float>(x), P<const void>(dyb),
+                                          P<float>(ws), P<float>(dw), S(st));
+          check_launch();
+        });
   g.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
     gops::to_bf16(P<const float>(x), P<void>(y), n, S(st));
     check_launch();

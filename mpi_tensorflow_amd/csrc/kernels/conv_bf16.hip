@@ -146,7 +146,8 @@ struct Loader {
   float4 ra[XB ? 1 : AR][2];
   uint4 rab[XB ? AR : 1];
   uint4 rb[BR];
-  __device__ Loader(const ConvShape& s_, const XT* x, const __bf16* wt_, int m0, int n0)
+  __device__ Loader(const ConvShape& s_, const ConvShape&, const XT* x, const __bf16* wt_, int m0,
+                    int n0)
       : s(s_), wt(wt_) {
     cchunks = s.C / BK;
     const int tid = threadIdx.x, c8 = tid & 7;
@@ -208,13 +209,116 @@ struct Loader {
   }
 };
 
-template <int BM, int BN, class XT>
+// Implicit im2col for a thin-input strided conv (the ResNet stem, 7x7 / s2 /
+// 3 channels), replacing the materialised bf16 im2col (154 MB written and
+// read twice per step at B = 32): s is the 1x1 GEMM shape over kp = K-dim
+// channels, si the image conv.  The k order is per tap row (kh * seg + kw * C
+// + ci, seg = S*C rounded up to 8, zero beyond R * seg) as in
+// im2col_bf16_kernel: a thread's 8 consecutive k of one tap row are ONE run of
+// 8 consecutive image floats (NHWC), fetched as two unaligned 16-byte loads
+// and masked to the in-image part.
+struct StemGeo {
+  int seg, sc;  // padded and real tap-row length (S * C)
+  long long nx;  // image elements
+  __device__ StemGeo(const ConvShape& si)
+      : seg((si.S * si.C + 7) / 8 * 8), sc(si.S * si.C),
+        nx((long long)si.N * si.H * si.W * si.C) {}
+  // 8 (or 4) consecutive k from k0 (within one tap row) of output pixel
+  // (n, iy0 = oy*stride - pad, ix0) of image x
+  template <int E>
+  __device__ __forceinline__ void fetch(const ConvShape& si, const float* x, int n, int iy0,
+                                        int ix0, int k0, bool pix_ok, float* v) const {
+    const int kh = k0 / seg, j0 = k0 - kh * seg;
+    const int iy = iy0 + kh;
+#pragma unroll
+    for (int j = 0; j < E; ++j) v[j] = 0.f;
+    if (!pix_ok || kh >= si.R || iy < 0 || iy >= si.H) return;
+    const int jlo = max(0, -ix0) * si.C, jhi = min(sc, (si.W - ix0) * si.C);
+    const long long e0 = (((long long)n * si.H + iy) * si.W + ix0) * si.C + j0;
+    if (e0 >= 0 && e0 + E <= nx) {
+      float r[E];
+#pragma unroll
+      for (int u = 0; u < E / 4; ++u) {
+        const float4 f = *reinterpret_cast<const float4*>(x + e0 + 4 * u);
+        r[4 * u] = f.x;
+        r[4 * u + 1] = f.y;
+        r[4 * u + 2] = f.z;
+        r[4 * u + 3] = f.w;
+      }
+#pragma unroll
+      for (int j = 0; j < E; ++j) v[j] = (j0 + j >= jlo && j0 + j < jhi) ? r[j] : 0.f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < E; ++j)
+        if (j0 + j >= jlo && j0 + j < jhi) v[j] = x[e0 + j];
+    }
+  }
+};
+
+template <int BM, int BN>
+struct StemLoader {
+  static constexpr int AR = BM * BK / 8 / NT;
+  static constexpr int BR = BN * BK / 8 / NT;
+  ConvShape s, si;
+  StemGeo g;
+  const float* x;
+  const __bf16* wt;
+  int nimg[AR], iy0[AR], ix0[AR];
+  bool av[AR];
+  const __bf16* bbase[BR];
+  uint4 rab[AR];
+  uint4 rb[BR];
+  __device__ StemLoader(const ConvShape& s_, const ConvShape& si_, const float* x_,
+                        const __bf16* wt_, int m0, int n0)
+      : s(s_), si(si_), g(si_), x(x_), wt(wt_) {
+    const int tid = threadIdx.x, c8 = tid & 7;
+    const int M = s.N * s.OH * s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + (NT / 8) * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH;
+      nimg[i] = t / s.OH;
+      iy0[i] = oy * si.stride - si.pad;
+      ix0[i] = ox * si.stride - si.pad;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = min(n0 + (tid >> 3) + (NT / 8) * i, s.K - 1);
+      bbase[i] = wt + (size_t)n * s.C + 8 * c8;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int k0 = kt * BK + 8 * (threadIdx.x & 7);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      float v[8];
+      g.fetch<8>(si, x, nimg[i], iy0[i], ix0[i], k0, av[i], v);
+      rab[i] = pack8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]));
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const uint4*>(bbase[i] + kt * BK);
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x, c8 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rab[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[i];
+  }
+};
+
+template <int BM, int BN, class XT, class LD = Loader<BM, BN, XT>>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restrict__ x,
                                                  const __bf16* __restrict__ wt,
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps,
                                                  const float* __restrict__ addend,
-                                                 __bf16* __restrict__ yb, int ex2) {
+                                                 __bf16* __restrict__ yb, int ex2,
+                                                 const ConvShape si) {
   // ex2 (unsplit): the 1x1 stride-2 backward-data - rows are dY pixels
   // (n, a, b), written to dX pixel (2a, 2b) of the 2x-sized output with the
   // other three pixels of its 2x2 block zero (plus addend everywhere)
@@ -229,7 +333,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
   const int nk = min(kps, nk_all - kb);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
   const int r = lane & 31, h = lane >> 5;
-  Loader<BM, BN, XT> ld(s, x, wt, m0, n0);
+  LD ld(s, si, x, wt, m0, n0);
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -714,8 +818,10 @@ struct WgLoader {
   // A rows are the flattened (tap, ci) index m = tap * C + ci: a 128-row tile
   // spans two taps of a 64-channel layer, so the dY tile it multiplies is
   // fetched once for both (C % 64 == 0: a channel quad never straddles taps)
-  __device__ WgLoader(const ConvShape& s_, const T* x_, const T* dy_, int m0, int n0,
-                      int pix0_, int npix_)
+  using TX = T;
+  using TD = T;
+  __device__ WgLoader(const ConvShape& s_, const ConvShape&, const T* x_, const T* dy_, int m0,
+                      int n0, int pix0_, int npix_)
       : s(s_), x(x_), dy(dy_), pix0(pix0_), npix(npix_) {
     const int m = m0 + 4 * (threadIdx.x % GA);
     mv = m < s.R * s.S * s.C;
@@ -791,11 +897,77 @@ struct WgLoader {
   }
 };
 
-template <int BM, int BN, bool XB>
+// Stem filter gradient over the implicit im2col (see StemLoader): A rows are
+// the kp k-indices, each thread fetches 4 consecutive k (one image run) for
+// PA pixels straight from the fp32 image; B = the bf16 dY as in WgLoader.
+template <int BM, int BN>
+struct StemWgLoader {
+  using TX = float;
+  using TD = __bf16;
+  using LA = WgLoader<BM, BN, false>;  // fp32 A vectors (float4 = 4 k)
+  using LB = WgLoader<BM, BN, true>;   // bf16 B vectors (uint2 = 4 channels)
+  static constexpr int GA = LA::GA, GB = LB::GB, PA = LA::PA, PB = LB::PB;
+  ConvShape s, si;
+  StemGeo g;
+  const float* x;
+  const __bf16* dy;
+  int pix0, npix, ka0, cb;
+  bool mv;
+  float4 ra[PA];
+  uint2 rb[PB];
+  __device__ StemWgLoader(const ConvShape& s_, const ConvShape& si_, const float* x_,
+                          const __bf16* dy_, int m0, int n0, int pix0_, int npix_)
+      : s(s_), si(si_), g(si_), x(x_), dy(dy_), pix0(pix0_), npix(npix_) {
+    ka0 = m0 + 4 * (threadIdx.x % GA);  // this thread's 4 k (a quad never straddles tap rows)
+    mv = ka0 < s.C;
+    cb = n0 + 4 * (threadIdx.x % GB);
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tid = threadIdx.x;
+    {
+      const int p = pix0 + kt * BK + PA * (tid / GA);
+      const int pc = min(p, npix - 1);
+      int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
+#pragma unroll
+      for (int q = 0; q < PA; ++q) {
+        float v[4];
+        g.fetch<4>(si, x, n, oy * si.stride - si.pad, ox * si.stride - si.pad, ka0,
+                   mv && p + q < npix, v);
+        ra[q] = make_float4(v[0], v[1], v[2], v[3]);
+        if (++ox == s.OW) {
+          ox = 0;
+          if (++oy == s.OH) {
+            oy = 0;
+            n = min(n + 1, s.N - 1);
+          }
+        }
+      }
+    }
+    {
+      const int p = pix0 + kt * BK + PB * (tid / GB);
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        const uint2 v = *reinterpret_cast<const uint2*>(dy + (size_t)min(p + q, npix - 1) * s.K + cb);
+        rb[q] = sel(p + q < npix, v);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x;
+    const int ra0 = 4 * (tid % GA), ka = PA * (tid / GA);
+    const int rb0 = 4 * (tid % GB), kb = PB * (tid / GB);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      LA::template put_col<PA>(As + (ra0 + c) * LDK + ka, ra, c);
+      LB::template put_col<PB>(Bs + (rb0 + c) * LDK + kb, rb, c);
+    }
+  }
+};
+
+template <int BM, int BN, bool XB, class LD = WgLoader<BM, BN, XB>>
 __global__ __launch_bounds__(NT) void wgrad_kernel(
-    ConvShape s, const typename WgLoader<BM, BN, XB>::T* __restrict__ x,
-    const typename WgLoader<BM, BN, XB>::T* __restrict__ dy, float* __restrict__ part,
-    int kchunk) {
+    ConvShape s, const typename LD::TX* __restrict__ x, const typename LD::TD* __restrict__ dy,
+    float* __restrict__ part, int kchunk, const ConvShape si) {
   constexpr int TM = BM / 64, TN = BN / 64;
   constexpr int STAGE = (BM + BN) * LDK;
   __shared__ __attribute__((aligned(16))) __bf16 smem[2 * STAGE];
@@ -809,7 +981,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(
   const int nk = min(kchunk, (npix - pix0 + BK - 1) / BK);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
   const int r = lane & 31, h = lane >> 5;
-  WgLoader<BM, BN, XB> ld(s, x, dy, m0, n0, pix0, npix);
+  LD ld(s, si, x, dy, m0, n0, pix0, npix);
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -982,10 +1154,10 @@ static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const floa
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
-    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
-    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
-    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
   }
 #undef GRID
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
@@ -1565,24 +1737,72 @@ void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, f
     const __bf16* xh = reinterpret_cast<const __bf16*>(xb);
     const __bf16* dh = reinterpret_cast<const __bf16*>(dyb);
     if (p.bm == 128 && p.bn == 128)
-      wgrad_kernel<128, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+      wgrad_kernel<128, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk, s);
     else if (p.bm == 128)
-      wgrad_kernel<128, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+      wgrad_kernel<128, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk, s);
     else if (p.bn == 128)
-      wgrad_kernel<64, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+      wgrad_kernel<64, 128, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk, s);
     else
-      wgrad_kernel<64, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk);
+      wgrad_kernel<64, 64, true><<<blocks, NT, 0, st>>>(s, xh, dh, out, p.kchunk, s);
   } else {
     if (p.bm == 128 && p.bn == 128)
-      wgrad_kernel<128, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+      wgrad_kernel<128, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk, s);
     else if (p.bm == 128)
-      wgrad_kernel<128, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+      wgrad_kernel<128, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk, s);
     else if (p.bn == 128)
-      wgrad_kernel<64, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+      wgrad_kernel<64, 128, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk, s);
     else
-      wgrad_kernel<64, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk);
+      wgrad_kernel<64, 64, false><<<blocks, NT, 0, st>>>(s, x, dy, out, p.kchunk, s);
   }
   if (p.z > 1) slab_reduce(ws, p.z, (long long)s.R * s.S * s.C * s.K / 4, dw, st);
+}
+
+// ---- stem over the implicit im2col (StemLoader / StemWgLoader) ----------
+// s1: the 1x1 GEMM shape over kp channels (kp % 64 == 0, >= R * seg), si the
+// image conv (C * S <= seg, fp32 NHWC image x)
+static void stem_check(const ConvShape& s1, const ConvShape& si) {
+  const int seg = (si.S * si.C + 7) / 8 * 8;
+  if (s1.C % 64 || s1.C < si.R * seg || s1.K % 64 || s1.R != 1 || s1.S != 1 ||
+      s1.N != si.N || s1.OH != si.OH || s1.OW != si.OW ||
+      (long long)si.N * si.H * si.W * si.C >= (1LL << 31) ||
+      (long long)s1.N * s1.OH * s1.OW >= (1LL << 31))
+    throw std::runtime_error("stem conv: inconsistent shapes");
+}
+
+void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x, const void* wtb,
+                        void* yb, hipStream_t st) {
+  using namespace cbf;
+  stem_check(s1, si);
+  const long long M = (long long)s1.N * s1.OH * s1.OW;
+  // 128 x 64 tiles: M = 401 K pixels at B = 32 (3136 blocks), no split
+  fwd_kernel<128, 64, float, StemLoader<128, 64>>
+      <<<dim3(cdiv(M, 128) * (s1.K / 64), 1), NT, 0, st>>>(
+          s1, x, reinterpret_cast<const __bf16*>(wtb), nullptr, nullptr, 0, s1.C / BK, nullptr,
+          reinterpret_cast<__bf16*>(yb), 0, si);
+}
+
+void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,
+                               const void* dyb, float* ws, float* dw, hipStream_t st) {
+  using namespace cbf;
+  stem_check(s1, si);
+  const WgPlan p = wg_plan(s1);
+  if (p.z > 1 && !ws) throw std::runtime_error("stem wgrad: split-K needs a workspace");
+  float* out = p.z > 1 ? ws : dw;
+  const int blocks = cdiv((long long)s1.C, p.bm) * (s1.K / p.bn) * p.z;
+  const __bf16* d = reinterpret_cast<const __bf16*>(dyb);
+#define STEM_WG(BM_, BN_)                                                                 \
+  wgrad_kernel<BM_, BN_, true, StemWgLoader<BM_, BN_>><<<blocks, NT, 0, st>>>(s1, x, d, out, \
+                                                                             p.kchunk, si)
+  if (p.bm == 128 && p.bn == 128)
+    STEM_WG(128, 128);
+  else if (p.bm == 128)
+    STEM_WG(128, 64);
+  else if (p.bn == 128)
+    STEM_WG(64, 128);
+  else
+    STEM_WG(64, 64);
+#undef STEM_WG
+  if (p.z > 1) slab_reduce(ws, p.z, (long long)s1.C * s1.K / 4, dw, st);
 }
 
 }  // namespace gops

@@ -46,6 +46,13 @@ bool conv_bwd_data_bf16_ok(const ConvShape& s);
 long long conv_bf16_ws_floats(const ConvShape& s, bool fwd_epilogue);
 void to_bf16(const float* x, void* y, long long n, hipStream_t st);
 void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStream_t st);
+// the stem conv over its implicit im2col (no column matrix): s1 = the 1x1
+// GEMM shape over kp channels, si = the image conv, x = fp32 NHWC image,
+// wtb = stem_weight_bf16 layout; yb = bf16 output; dw = padded [kp][K] grad
+void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x, const void* wtb,
+                        void* yb, hipStream_t st);
+void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,
+                               const void* dyb, float* ws, float* dw, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr,
                    const void* wtb = nullptr, void* yb = nullptr);

@@ -281,8 +281,6 @@ class _ConvIm2colFn(torch.autograd.Function):
         sh = shape
         sc, seg = sh.S * sh.C, _im2col_seg(sh)
         s = stream_handle()
-        col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
-        C.ops.im2col_bf16(sh, ptr(x), kp, ptr(col), s)
         # weights in the im2col's k order (tap row kh at kh * seg, (kw, ci)
         # inside), written straight as the 1x1 conv's bf16 [K][kp] layout
         wtb = torch.empty(sh.K * kp, dtype=torch.bfloat16, device=x.device)
@@ -290,22 +288,35 @@ class _ConvIm2colFn(torch.autograd.Function):
         s1 = C.ops.ConvShape(sh.N, sh.OH, sh.OW, kp, sh.K, 1, 1, 1, 0)
         y = torch.empty((sh.N, sh.OH, sh.OW, sh.K),
                         dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
-        C.ops.conv_fwd(s1, 0, 0, 0, 0 if out_bf16 else ptr(y), False, ptr(ws), s, True,
-                       ptr(col), ptr(wtb), ptr(y) if out_bf16 else 0)
-        ctx.save_for_backward(col)
-        ctx.s1, ctx.R, ctx.sc, ctx.seg, ctx.gw, ctx.ws = s1, sh.R, sc, seg, gw, ws
+        # bf16 output (ResNet stem): the GEMM loaders gather the im2col on the fly
+        # from the image (conv_bf16.hip StemLoader / StemWgLoader); else the
+        # column matrix is materialised
+        ctx.implicit = bool(out_bf16)
+        if ctx.implicit:
+            C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s)
+            ctx.save_for_backward(x)
+        else:
+            col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
+            C.ops.im2col_bf16(sh, ptr(x), kp, ptr(col), s)
+            C.ops.conv_fwd(s1, 0, 0, 0, ptr(y), False, ptr(ws), s, True, ptr(col), ptr(wtb), 0)
+            ctx.save_for_backward(col)
+        ctx.s1, ctx.si, ctx.R, ctx.sc, ctx.seg, ctx.gw, ctx.ws = s1, sh, sh.R, sc, seg, gw, ws
         return y
 
     @staticmethod
     def backward(ctx, dy):
         C = native()
-        (col,) = ctx.saved_tensors
+        (src,) = ctx.saved_tensors
         s1 = ctx.s1
         s = stream_handle()
         dy = dy.contiguous()
         dyb = _bf16_copy(dy, s)
         gpad = torch.empty((s1.C, s1.K), device=dy.device, dtype=torch.float32)
-        C.ops.conv_bwd_filter(s1, 0, 0, ptr(ctx.ws), ptr(gpad), s, True, ptr(col), ptr(dyb))
+        if ctx.implicit:
+            C.ops.conv_bwd_filter_stem_bf16(s1, ctx.si, ptr(src), ptr(dyb), ptr(ctx.ws), ptr(gpad),
+                                            s)
+        else:
+            C.ops.conv_bwd_filter(s1, 0, 0, ptr(ctx.ws), ptr(gpad), s, True, ptr(src), ptr(dyb))
         C.ops.stem_wgrad(ptr(gpad), ctx.R, ctx.sc, ctx.seg, s1.K, ptr(ctx.gw), s)
         _grad_done(ctx.gw)
         return None, None, None, None, None, None, None

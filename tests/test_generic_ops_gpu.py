@@ -303,11 +303,15 @@ def test_trainer_eval_between_graph_replays(cuda_dev):
     assert s.final_test_error_global < 50.0, s
 
 
+@pytest.mark.parametrize("out_bf16", [False, True])
 @pytest.mark.parametrize("R,st,pad,K,kp", [(7, 2, 3, 64, 192), (5, 1, 2, 128, 128)])
-def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp):
+def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp, out_bf16):
     """bf16 mode: a thin-input conv whose input needs no gradient (ResNet stem,
-    7x7 s2, 3 -> 64) runs as a bf16 im2col + 1x1 conv on the bf16 family;
-    output and filter gradient vs fp32 torch within bf16 operand rounding."""
+    7x7 s2, 3 -> 64) runs as a 1x1 conv over its bf16 im2col on the bf16
+    family - materialised (fp32 output), or gathered on the fly from the image
+    by the GEMM loaders (bf16 output, the ResNet path); output and filter
+    gradient vs fp32 torch within bf16 operand rounding, and the on-the-fly
+    filter gradient bit-identical to the materialised one."""
     from mpi_tensorflow_amd.ops import native
 
     g = torch.Generator().manual_seed(11)
@@ -324,13 +328,20 @@ def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp):
     Fn.set_conv_bf16(True)
     try:
         assert Fn._im2col_kp(sh, xg, False, False) == kp
-        yg = Fn.conv2d(xg, wp, None, st, pad, False)
-        yg.backward(dy.to(cuda_dev))
+        grads = []
+        for ob in sorted({False, out_bf16}):
+            wp.grad_view.zero_()
+            yg = Fn.conv2d(xg, wp, None, st, pad, False, out_bf16=ob)
+            assert yg.dtype == (torch.bfloat16 if ob else torch.float32)
+            yg.backward(dy.to(cuda_dev).to(yg.dtype))
+            torch.cuda.synchronize()
+            grads.append(wp.grad_view.detach().clone())
     finally:
         Fn.set_conv_bf16(False)
-    torch.cuda.synchronize()
-    assert _rel(yg.detach().cpu(), yr.detach()) < 1e-2
+    assert _rel(yg.detach().float().cpu(), yr.detach()) < 1e-2
     assert _rel(wp.grad_view.cpu(), wr.grad) < 1e-2
+    if out_bf16:  # same bf16 operands, same plan: the sums are identical
+        assert torch.equal(grads[0], grads[1])
 
 
 def test_bn_bf16_twin_feeds_conv(cuda_dev):
