@@ -65,7 +65,7 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
 # "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
 # compute stream over a second communicator
-SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split")
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors")
 DTYPES = ("fp32", "bf16")
 
 
@@ -178,7 +178,8 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--sync", default=d.sync, choices=SYNC_MODES)
     p.add_argument("--sync-every", type=int, default=d.sync_every)
     p.add_argument("--sync-schedule", default=d.sync_schedule, choices=SYNC_SCHEDULES,
-                   help="native MNIST grad-sync schedule (auto / buckets / sharded FC update)")
+                   help="native MNIST grad-sync schedule (auto / buckets / sharded FC update / "
+                        "factors: all-gather the FC gradient factors, fp32)")
     p.add_argument("--grad-comm-dtype", default=d.grad_comm_dtype, choices=("fp32", "bf16"),
                    help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--eval-every", type=int, default=d.eval_every,

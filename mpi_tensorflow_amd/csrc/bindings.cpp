@@ -372,7 +372,8 @@ PYBIND11_MODULE(_C, m) {
                           RW(da1m) RW(part2) RW(part1) RW(w2t) RW(a1pf) RW(keep_prob) RW(base_lr) RW(lr_decay)
                               RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16) RW(grad_bf16) RW(gb16)
                                   RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
-                                      RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b);
+                                      RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b) RW(a2_all)
+                                          RW(dh_all) RW(hd_all) RW(dlog_all) RW(fac_ranks);
 #undef RW
 
   py::class_<Collective>(m, "Collective")
@@ -496,6 +497,7 @@ PYBIND11_MODULE(_C, m) {
       .def("refresh_shadows", [](MnistExecutor& e, uintptr_t s) { e.refresh_shadows(S(s)); })
       .def_property_readonly("schedule", &MnistExecutor::schedule)
       .def("sharded_ok", &MnistExecutor::sharded_ok)
+      .def("factors_ok", &MnistExecutor::factors_ok)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
       .def("gather_optimizer_state",
            [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs) {
@@ -524,6 +526,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_BUCKETS") = (int)MnistExecutor::SCHED_BUCKETS;
   m.attr("MnistExecutor").attr("SCHED_SHARDED_FC") = (int)MnistExecutor::SCHED_SHARDED_FC;
   m.attr("MnistExecutor").attr("SCHED_SPLIT") = (int)MnistExecutor::SCHED_SPLIT;
+  m.attr("MnistExecutor").attr("SCHED_FACTORS") = (int)MnistExecutor::SCHED_FACTORS;
 
   // ----------------------------------------------------------------- IDX
   m.def("idx_header", [](const std::string& path) {

@@ -39,22 +39,27 @@ double EmuComm::gather_us(size_t full_bytes) const {
   return lat_us_ + (n - 1) / n * (double)full_bytes / (busbw_ * 1e3);
 }
 
+double EmuComm::lat_once() {
+  if (!in_group_) return lat_us_;
+  return grouped_++ == 0 ? lat_us_ : 0.0;
+}
+
 void EmuComm::occupy(void* buf, size_t bytes, double us, hipStream_t s) {
   commemu::launch_occupy(buf, bytes, us, blocks_, s);
 }
 
 void EmuComm::all_reduce(const void*, void* recv, size_t count, int dtype, int, hipStream_t s) {
   const size_t b = count * dtype_bytes(dtype);
-  occupy(recv, b, all_reduce_us(b), s);
+  occupy(recv, b, all_reduce_us(b) - lat_us_ + lat_once(), s);
 }
 
 void EmuComm::all_gather(const void*, void* recv, size_t send_count, int dtype, hipStream_t s) {
   const size_t b = send_count * dtype_bytes(dtype) * (size_t)nranks_;
-  occupy(recv, b, gather_us(b), s);
+  occupy(recv, b, gather_us(b) - lat_us_ + lat_once(), s);
 }
 
 void EmuComm::reduce_scatter(const void* send, void*, size_t recv_count, int dtype, int,
                              hipStream_t s) {
   const size_t b = recv_count * dtype_bytes(dtype) * (size_t)nranks_;
-  occupy(const_cast<void*>(send), b, gather_us(b), s);
+  occupy(const_cast<void*>(send), b, gather_us(b) - lat_us_ + lat_once(), s);
 }

@@ -30,6 +30,11 @@ class Collective {
                           hipStream_t s) = 0;
   virtual void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                               hipStream_t s) = 0;
+  // Collectives issued between group_start() and group_end() form ONE fused
+  // operation (ncclGroupStart / ncclGroupEnd): one launch and one latency for
+  // several buffers.  Implementations without grouping run them one by one.
+  virtual void group_start() {}
+  virtual void group_end() {}
 };
 
 // Ring cost model (rccl-tests conventions): an all-reduce of S bytes takes
@@ -46,13 +51,19 @@ class EmuComm : public Collective {
                   hipStream_t s) override;
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                       hipStream_t s) override;
+  // grouped ops pay the latency term once (the first op of the group)
+  void group_start() override { grouped_ = 0; in_group_ = true; }
+  void group_end() override { in_group_ = false; }
   double all_reduce_us(size_t bytes) const;
   double gather_us(size_t full_bytes) const;  // reduce-scatter / all-gather
 
  private:
   void occupy(void* buf, size_t bytes, double us, hipStream_t s);
+  double lat_once();  // lat_us_, or 0 after the first op of a group
   int nranks_, rank_, blocks_;
   double lat_us_, busbw_;
+  bool in_group_ = false;
+  int grouped_ = 0;
 };
 
 size_t dtype_bytes(int dtype);

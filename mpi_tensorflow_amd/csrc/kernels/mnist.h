@@ -64,7 +64,13 @@ void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
                     float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
-                    int roles = 7);  // roles: bit 0 dX, bit 1 dW1, bit 2 small grads (profiling)
+                    int roles = 7);  // roles: bit 0 dX, bit 1 dW1, bit 2 small grads
+                                     // (roles == 1: a dX-only grid, SCHED_FACTORS)
+// FC weight / bias grads over `rows` gathered rows (rank-major a2 [rows][3136],
+// dh / hd [rows][512], dlog [rows][10]); SCHED_FACTORS
+void launch_fc1_bwd_weights(const float* a2, const float* dh, const float* hd, const float* dlog,
+                            int rows, float* g_w3, float* g_b3, float* g_w4, float* g_b4,
+                            hipStream_t s);
 int conv2_filter_splits(int batch);
 // a1p: the zero-bordered NHWC pooled conv1 output [batch][18][18][32]
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,

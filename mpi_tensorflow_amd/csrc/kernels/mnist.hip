@@ -543,6 +543,24 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   }
 }
 
+// FC weight gradients from GATHERED factors (SCHED_FACTORS): dW1 = A^T DH,
+// dW2 = HD^T DLOG, db1 = sum DH, db2 = sum DLOG over the rows of every rank
+// (rows = N x batch, rank-major; the rank's own slot written in place by its
+// forward / head kernels, the rest by one grouped all-gather).  Same dW / small
+// block roles as fc1_bwd_kernel with K = rows, so the result is the exact
+// global sum, formed in one fixed order identically on every rank.
+__global__ __launch_bounds__(256) void fc1_bwd_weights_kernel(
+    const float* __restrict__ a2, const float* __restrict__ dh, const float* __restrict__ hd,
+    const float* __restrict__ dlog, int rows, float* __restrict__ g_w3, float* __restrict__ g_b3,
+    float* __restrict__ g_w4, float* __restrict__ g_b4) {
+  __shared__ float smem[4 * (NCLS + 1) * 64];
+  const int L = xcd_remap(blockIdx.x, gridDim.x);
+  if (L < FC1BWD_DW_BLOCKS)
+    fc1_bwd_dw(L, a2, dh, rows, g_w3);
+  else
+    fc1_small_grads(L - FC1BWD_DW_BLOCKS, hd, dh, dlog, rows, g_w4, g_b4, g_b3, smem);
+}
+
 // ------------------------------------------ conv2: dedicated MFMA kernels ----
 // The three conv2 products are the bulk of the step's FLOPs (3 x 1.28 GFLOP at
 // B = 64).  They bypass the generic gather engine:
@@ -1027,9 +1045,18 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                     int roles) {
   if (batch <= 0 || batch % 32 != 0) throw std::runtime_error("fc1_bwd: batch % 32 != 0");
   const int n_dx = (batch / 32) * (FC1_IN / 32);
-  fc1_bwd_kernel<<<n_dx + FC1BWD_DW_BLOCKS + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
+  const int grid = roles == 1 ? n_dx : n_dx + FC1BWD_DW_BLOCKS + SMALL_BLOCKS;
+  fc1_bwd_kernel<<<grid, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
                                                             g_w3, g_b3, g_w4, g_b4, dy2, dy2t,
                                                             roles);
+}
+
+void launch_fc1_bwd_weights(const float* a2, const float* dh, const float* hd, const float* dlog,
+                            int rows, float* g_w3, float* g_b3, float* g_w4, float* g_b4,
+                            hipStream_t s) {
+  if (rows <= 0 || rows % 32 != 0) throw std::runtime_error("fc1_bwd_weights: rows % 32 != 0");
+  fc1_bwd_weights_kernel<<<FC1BWD_DW_BLOCKS + SMALL_BLOCKS, 256, 0, s>>>(
+      a2, dh, hd, dlog, rows, g_w3, g_b3, g_w4, g_b4);
 }
 
 int conv2_filter_splits(int batch) { return cdiv(batch, C2F_GROUPS_IMG); }

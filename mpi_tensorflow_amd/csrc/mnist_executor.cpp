@@ -7,6 +7,9 @@
 #include "kernels/mnist.h"
 #include "kernels/mnist_bf16.h"
 
+// FC factor row widths (models/mnist_cnn.py: 7*7*64 -> 512 -> 10)
+constexpr size_t kFc1In = 3136, kFc1Out = 512, kNcls = 10;
+
 template <class T>
 static inline T* P(uintptr_t v) {
   return reinterpret_cast<T*>(v);
@@ -22,12 +25,12 @@ MnistExecutor::MnistExecutor(const MnistPtrs& p) : p_(p) {
         "MnistExecutor: flat segments must be multiples of 4 floats with the L2 prefix in bucket 1");
   // (hipEventDisableSystemFence / hipEventReleaseToDevice on these events
   // changed nothing in graph replay: captured edges do not use the flags)
-  for (hipEvent_t* e : {&ev_dw_, &ev_b1_, &ev_fin_, &ev_done_})
+  for (hipEvent_t* e : {&ev_dw_, &ev_b1_, &ev_fin_, &ev_done_, &ev_fac_})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
 
 MnistExecutor::~MnistExecutor() {
-  for (hipEvent_t e : {ev_dw_, ev_b1_, ev_fin_, ev_done_})
+  for (hipEvent_t e : {ev_dw_, ev_b1_, ev_fin_, ev_done_, ev_fac_})
     if (e) (void)hipEventDestroy(e);
 }
 
@@ -39,8 +42,11 @@ MnistExecutor::~MnistExecutor() {
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
-                                    const mnist::FcSgdArgs* fc_sgd) {
-  if (p_.bf16) return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd);
+                                    const mnist::FcSgdArgs* fc_sgd, bool factors) {
+  if (p_.bf16) {
+    if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
+    return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd);
+  }
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -58,11 +64,12 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                               p.keep_prob, p.seed, p.rank, p.base_lr, p.lr_decay, P<float>(p.hd),
                               P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
                               P<float>(p.lr), P<int>(p.correct), s);
+  if (factors) HIP_CHECK(hipEventRecord(ev_fac_, s));
   // backward: fc1 dX (+pool2/ReLU2 scatter) | dW1 | fc2 grads, one launch
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
                         P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
-                        P<float>(p.dy2t), s);
+                        P<float>(p.dy2t), s, factors ? 1 : 7);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
                                   P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
@@ -176,7 +183,8 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 }
 
 void MnistExecutor::set_schedule(int sched) {
-  if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT)
+  if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
+      sched != SCHED_FACTORS)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -185,6 +193,11 @@ void MnistExecutor::set_schedule(int sched) {
 
 bool MnistExecutor::sharded_ok(int nranks) const {
   return nranks > 1 && p_.bucket1 % (4LL * nranks) == 0;
+}
+
+bool MnistExecutor::factors_ok(int nranks) const {
+  return nranks > 1 && nranks == p_.fac_ranks && !p_.bf16 && p_.a2_all && p_.dh_all &&
+         p_.hd_all && p_.dlog_all;
 }
 
 void MnistExecutor::wait_fc_params(hipStream_t s) {
@@ -221,6 +234,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
     train_step_sharded(s, comm, cs);
+    return;
+  }
+  if (sched_ == SCHED_FACTORS && factors_ok(comm->size())) {
+    train_step_factors(s, comm, cs);
     return;
   }
   if (sched_ == SCHED_SPLIT && comm2 != nullptr && comm2->size() == comm->size()) {
@@ -306,6 +323,57 @@ void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_
   fc_pending_ = true;
   reduce_bucket(comm2, p.bucket1, p.total - p.bucket1, s);
   sgd_range(s, p.bucket1, p.total, gscale, true);
+}
+
+// Factor schedule (sufficient-factor exchange).  The FC gradients of a batch
+// are products of per-row factors: dW1 = a2^T dh (rank B), dW2 = hd^T dlog,
+// db1 = sum dh, db2 = sum dlog.  Instead of all-reducing the 6.45 MB FC
+// gradient (ring: 2 (N-1)/N x 6.45 MB sent per rank), every rank all-gathers
+// the factors of all ranks (B x 4170 floats = 1.07 MB per rank at B = 64;
+// (N-1)/N x N x 1.07 MB sent per rank: 6x fewer bytes at N = 2, 3.4x at 4,
+// 1.7x at 8) and forms the global FC gradients itself with K = N x B.  All
+// ranks compute the same sums in the same order, so the replicas stay
+// bit-identical.
+//   compute stream: fwd, head (-> ev_fac_), fc1 dX, conv bwd, slab reduction
+//                   (-> ev_fin_), wait ev_b1_ -> FC weight grads over the
+//                   gathered rows, wait ev_done_ -> SGD of every parameter
+//   comm stream:    wait ev_fac_ -> grouped all-gather of the factors
+//                   (-> ev_b1_), wait ev_fin_ -> all-reduce conv grads
+//                   (-> ev_done_)
+// The gather runs under the whole conv backward; the latency-bound conv
+// all-reduce runs under the FC weight-gradient GEMM.  The factor slots are
+// rewritten only by the next step's forward / head, after this step's GEMM.
+void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStream_t cs) {
+  const MnistPtrs& p = p_;
+  float* G = P<float>(p.grads);
+  const int n = comm->size(), r = comm->rank();
+  const size_t B = (size_t)p.batch;
+  const float gscale = 1.0f / (float)n;
+  enqueue_fwd_bwd(s, /*finalize=*/true, nullptr, /*factors=*/true);
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fac_, 0));
+  float* a2 = P<float>(p.a2_all);
+  float* dh = P<float>(p.dh_all);
+  float* hd = P<float>(p.hd_all);
+  float* dl = P<float>(p.dlog_all);
+  comm->group_start();
+  comm->all_gather(a2 + r * B * kFc1In, a2, B * kFc1In, ncclFloat32, cs);
+  comm->all_gather(dh + r * B * kFc1Out, dh, B * kFc1Out, ncclFloat32, cs);
+  comm->all_gather(hd + r * B * kFc1Out, hd, B * kFc1Out, ncclFloat32, cs);
+  comm->all_gather(dl + r * B * kNcls, dl, B * kNcls, ncclFloat32, cs);
+  comm->group_end();
+  HIP_CHECK(hipEventRecord(ev_b1_, cs));
+  HIP_CHECK(hipEventRecord(ev_fin_, s));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
+  reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
+  HIP_CHECK(hipEventRecord(ev_done_, cs));
+  // (an FC momentum SGD applied in the GEMM epilogue instead of this SGD pass
+  // measured slower: 146 -> 155 us at N = 2, 191 -> 204 us at N = 8 against
+  // the emulated ring, docs/PERF_NOTES.md)
+  HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
+  mnist::launch_fc1_bwd_weights(a2, dh, hd, dl, n * p.batch, G + p.off_w3, G + p.off_b3,
+                                G + p.off_w4, G + p.off_b4, s);
+  HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  sgd_range(s, 0, p.total, gscale, true);
 }
 
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {

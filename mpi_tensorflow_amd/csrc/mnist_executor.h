@@ -59,6 +59,11 @@ struct MnistPtrs {
   // buffer of `total` elements)
   int grad_bf16 = 0;
   uintptr_t gb16 = 0;
+  // SCHED_FACTORS (fp32, world > 1): rank-major gathered FC factors of all
+  // ranks, [world * batch] rows each (a2 [.][3136], dh / hd [.][512], dlog
+  // [.][10]); a2 / dh / hd / dlog above point at this rank's slot in them
+  uintptr_t a2_all = 0, dh_all = 0, hd_all = 0, dlog_all = 0;
+  int fac_ranks = 0;  // communicator size the factor buffers were sized for
 };
 
 namespace mnist {
@@ -85,10 +90,17 @@ class MnistExecutor {
   //   SCHED_SPLIT      - FC all-reduce + FC SGD on the comm stream, conv
   //                      all-reduce on the compute stream via comm2 (one
   //                      fork + one join per step, see train_step_split).
-  static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2;
+  //   SCHED_FACTORS    - all-gather the FC layers' gradient FACTORS (a2, dh,
+  //                      hd, dlog: 1.07 MB per rank at B = 64) instead of
+  //                      all-reducing the 6.45 MB FC gradient, then form the
+  //                      global FC gradients on every rank (see
+  //                      train_step_factors).
+  static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
+                       SCHED_FACTORS = 3;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
+  bool factors_ok(int nranks) const;
   // Makes stream s wait for any collective still in flight from the last
   // step (call at the end of every captured / eager run of steps).
   void join(hipStream_t s);
@@ -125,11 +137,15 @@ class MnistExecutor {
   // finalize = false: leave the conv filter grads as slabs (the world-1 SGD
   // launch reduces them itself)
   // fc_sgd (single rank): FC-bucket SGD appended to the conv2 bwd-data launch
+  // factors: record ev_fac_ once the FC factors are written (after the head)
+  // and compute only dX in fc1 backward (the FC weight grads come from the
+  // gathered factors)
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
-                       const mnist::FcSgdArgs* fc_sgd = nullptr);
+                       const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false);
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
+  void train_step_factors(hipStream_t s, Collective* comm, hipStream_t cs);
   void wait_fc_params(hipStream_t s);
   // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
   void reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs);
@@ -143,5 +159,7 @@ class MnistExecutor {
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;
   // ev_fin_: conv grads final (bucket 2 may start); ev_done_: bucket 2 reduced.
   // Sharded schedule: ev_b1_ = FC params gathered
-  hipEvent_t ev_dw_ = nullptr, ev_b1_ = nullptr, ev_fin_ = nullptr, ev_done_ = nullptr;
+  // ev_fac_: FC factors written (SCHED_FACTORS all-gather may start)
+  hipEvent_t ev_dw_ = nullptr, ev_b1_ = nullptr, ev_fin_ = nullptr, ev_done_ = nullptr,
+             ev_fac_ = nullptr;
 };

@@ -43,8 +43,8 @@ class RcclComm : public Collective {
                   hipStream_t s) override;
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                       hipStream_t s) override;
-  void group_start();
-  void group_end();
+  void group_start() override;
+  void group_end() override;
   void destroy();
   // failure detection: ncclResult_t of the communicator's asynchronous state
   // (0 = ok, 7 = in progress), abort (idempotent, thread safe), rank count as

@@ -38,8 +38,8 @@ from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
 # sync_schedule="auto": the single-communicator gradient-sync schedules
-# (buckets / sharded, csrc/mnist_executor.h) are timed on real training steps
-# (bit-identical under every schedule) and the fastest is kept; all ranks take
+# (buckets / sharded / factors (fp32), csrc/mnist_executor.h) are timed on real
+# training steps and the fastest is kept; all ranks take
 # the decision from the same (max-over-ranks) timings.  The two-communicator
 # "split" schedule (fastest against the comm-emulated 8-rank ring,
 # docs/PERF_NOTES.md) issues collectives on two RCCL communicators from two
@@ -216,6 +216,22 @@ class NativeMnistEngine(MnistEngineBase):
             a1pf=torch.zeros(B * 18 * 18 * 32, **f32),
         )
         self.bf16 = cfg.dtype == "bf16"
+        self.fac = None
+        hcomm = comm.native_handle if (self.grad_sync and comm is not None) else None
+        nfac = hcomm.size if hcomm is not None else 1
+        if nfac > 1 and not self.bf16:
+            # SCHED_FACTORS: rank-major gathered FC factors; this rank's forward /
+            # head kernels write their slot in place (csrc/mnist_executor.cpp
+            # train_step_factors).  Sized by the communicator (an emulated
+            # N-rank comm on one GPU gets N slots, rank 0's filled).
+            crank = hcomm.rank
+            self.fac = dict(a2=torch.zeros(nfac * B * M.FC1_IN, **f32),
+                            dh=torch.zeros(nfac * B * M.FC1_OUT, **f32),
+                            hd=torch.zeros(nfac * B * M.FC1_OUT, **f32),
+                            dlog=torch.zeros(nfac * B * 10, **f32))
+            for name, t in self.fac.items():
+                n = t.numel() // nfac
+                self.bufs[name] = t[crank * n:(crank + 1) * n]
         if self.bf16:
             # bf16 activation images (zero borders are never written) and
             # weight shadows; layouts in csrc/kernels/mnist_bf16.h
@@ -255,6 +271,10 @@ class NativeMnistEngine(MnistEngineBase):
         if cfg.grad_comm_dtype == "bf16" and world > 1:
             self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)
             p.grad_bf16, p.gb16 = 1, ptr(self.gb16)
+        if self.fac is not None:
+            p.a2_all, p.dh_all = ptr(self.fac["a2"]), ptr(self.fac["dh"])
+            p.hd_all, p.dlog_all = ptr(self.fac["hd"]), ptr(self.fac["dlog"])
+            p.fac_ranks = nfac
         self.ptrs = p
         self.exe = C_.MnistExecutor(p)
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
@@ -269,12 +289,14 @@ class NativeMnistEngine(MnistEngineBase):
             self.exe.set_schedule(self._pick_schedule(cfg.sync_schedule, self._native_comm.size))
         if getattr(self.comm, "kind", "") == "host-staged":  # test comm: eager only
             self.comm.bases = [self.grads, self.params, self.mom] + (
-                [self.gb16] if self.gb16 is not None else [])
+                [self.gb16] if self.gb16 is not None else []) + (
+                list(self.fac.values()) if self.fac is not None else [])
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self.use_graph = cfg.graph and getattr(self.comm, "kind", "") != "host-staged"
         self.graph_steps = max(1, cfg.graph_steps)
         self._tuned = not (self.grad_sync and cfg.sync_schedule == "auto" and self.use_graph
-                           and self.exe.sharded_ok(self._native_comm.size))
+                           and (self.exe.sharded_ok(self._native_comm.size)
+                                or self.exe.factors_ok(self._native_comm.size)))
         self.tune_log: Dict[str, float] = {}
         self._eval_ws = None
         if self.grad_sync:  # connection setup of every collective used, outside any capture
@@ -284,6 +306,10 @@ class NativeMnistEngine(MnistEngineBase):
                 chunk = self.ptrs.bucket1 // c.size
                 c.reduce_scatter(g, g + 4 * chunk * c.rank, chunk, 7, 0, hs)
                 c.all_gather(g + 4 * chunk * c.rank, g, chunk, 7, hs)
+            if self.exe.factors_ok(c.size):  # factor all-gathers, in place
+                for t in self.fac.values():
+                    k = t.numel() // c.size
+                    c.all_gather(ptr(t) + 4 * k * c.rank, ptr(t), k, 7, hs)
             if self._native_comm2 is not None:
                 self._native_comm2.all_reduce(g, g, n, 7, 0, hs)
             torch.cuda.synchronize(dev)
@@ -300,6 +326,8 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_SHARDED_FC
         if name == "split" and self._native_comm2 is not None:
             return E.SCHED_SPLIT
+        if name == "factors" and self.exe.factors_ok(nranks):
+            return E.SCHED_FACTORS
         return E.SCHED_BUCKETS  # "auto" until tuned
 
     def _set_schedule(self, sched: int) -> None:
@@ -317,8 +345,8 @@ class NativeMnistEngine(MnistEngineBase):
         if not self.grad_sync:
             return "none"
         E = self._C.MnistExecutor
-        return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split"}.get(self.exe.schedule,
-                                                                          "buckets")
+        return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
+                E.SCHED_FACTORS: "factors"}.get(self.exe.schedule, "buckets")
 
     def sync_optimizer_state(self) -> None:
         if self.grad_sync:
@@ -354,7 +382,11 @@ class NativeMnistEngine(MnistEngineBase):
         return g
 
     def tune_steps(self) -> int:
-        return 0 if self._tuned else 2 * (1 + TUNE_REPLAYS) * self.graph_steps
+        if self._tuned:
+            return 0
+        n = self._native_comm.size
+        cands = 1 + int(self.exe.sharded_ok(n)) + int(self.exe.factors_ok(n))
+        return cands * (1 + TUNE_REPLAYS) * self.graph_steps
 
     def tune_schedule(self) -> int:
         """Times TUNE_REPLAYS graph replays of each sync schedule (after one
@@ -367,7 +399,12 @@ class NativeMnistEngine(MnistEngineBase):
         G = self.graph_steps
         steps = 0
         best = None
-        cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SHARDED_FC, "sharded")]
+        n = self._native_comm.size
+        cands = [(E.SCHED_BUCKETS, "buckets")]
+        if self.exe.sharded_ok(n):
+            cands.append((E.SCHED_SHARDED_FC, "sharded"))
+        if self.exe.factors_ok(n):
+            cands.append((E.SCHED_FACTORS, "factors"))
         for sched, name in cands:
             self._set_schedule(sched)
             g = self._graph(G)

@@ -12,7 +12,11 @@ cross-rank data), and checks
   * every rank holds the same params (replica consistency);
   * with the bf16 gradient wire (--grad-comm-dtype bf16) buckets and sharded
     agree bit for bit and equal the serial emulation with the sum formed as
-    bf16(sum of bf16(grad_r)).
+    bf16(sum of bf16(grad_r));
+  * fp32: the factor schedule (all-gathered FC gradient factors, global FC
+    gradients formed on every rank) keeps the replicas bit-identical and
+    matches buckets to fp32 rounding (its FC sums run in another order), also
+    when switched in and out mid-run.
 Launch: torchrun --nproc-per-node 2 --master-addr 127.0.0.1 tests/helpers/native_sync_ranks.py"""
 import sys
 
@@ -70,6 +74,33 @@ def run_switching(dtype, steps, di):
     return finish(eng)
 
 
+def run_factors_switching(steps, di):
+    eng = make("auto", "fp32", di)
+    E = native().MnistExecutor
+    k = steps // 3
+    eng.train(k)
+    eng._set_schedule(E.SCHED_FACTORS)
+    assert eng.sync_schedule == "factors"
+    eng.train(k)
+    eng._set_schedule(E.SCHED_BUCKETS)
+    eng.train(steps - 2 * k)
+    return finish(eng)
+
+
+def check_factors(pb, mb, steps, di):
+    out = []
+    for tag, (pf, mf) in (("factors", run("factors", "fp32", steps, di)),
+                          ("factors-switching", run_factors_switching(steps, di))):
+        ref = pf.clone()
+        dist.broadcast(ref, 0)
+        assert torch.equal(ref, pf), f"{tag}: replicas diverged"
+        dp = (pf - pb).abs().max().item() / pb.abs().max().item()
+        dm = (mf - mb).abs().max().item() / mb.abs().max().item()
+        assert dp < 1e-5 and dm < 1e-4, f"{tag} vs buckets: rel params {dp:.2e}, momentum {dm:.2e}"
+        out.append(dp)
+    return max(out)
+
+
 def serial(dtype, steps, world, wire="fp32"):
     """One process plays every rank: same kernels, summed grads, one SGD."""
     C_ = native()
@@ -111,6 +142,7 @@ def main():
         ps, ms = run(sched, dtype, steps, di)
         assert torch.equal(pb, ps), f"{sched}: params differ: {(pb - ps).abs().max().item()}"
         assert torch.equal(mb, ms), f"{sched}: momentum differs: {(mb - ms).abs().max().item()}"
+    fac_rel = check_factors(pb, mb, steps, di) if dtype == "fp32" else 0.0
     pw, mw = run_switching(dtype, steps, di)
     assert torch.equal(pb, pw), f"switching: params differ: {(pb - pw).abs().max().item()}"
     assert torch.equal(mb, mw), f"switching: momentum differs: {(mb - mw).abs().max().item()}"
@@ -133,8 +165,8 @@ def main():
         assert torch.equal(mbb, m2), f"bf16 wire vs serial: momentum differs: {(mbb - m2).abs().max().item()}"
         rel = ((pbb - pb).norm() / pb.norm()).item()
         assert rel < 1e-2, f"bf16 wire drifted from fp32: rel {rel}"
-        print(f"NATIVE_SYNC_OK world={di.world} steps={steps} dtype={dtype} bf16-wire-rel={rel:.2e}",
-              flush=True)
+        print(f"NATIVE_SYNC_OK world={di.world} steps={steps} dtype={dtype} bf16-wire-rel={rel:.2e} "
+              f"factors-rel={fac_rel:.2e}", flush=True)
     D.barrier()
     D.shutdown()
 

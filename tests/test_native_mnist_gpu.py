@@ -207,8 +207,9 @@ def test_native_rccl_comm_and_graph_capture(cuda_dev, data):
 def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     """Startup autotune of the gradient-sync schedule (runtime/mnist_engine.py:
     tune_schedule) against an emulated 8-rank ring (csrc/collective.h EmuComm):
-    both schedules are captured and timed, the faster one is kept, and the
-    tuning steps are real steps (step counter advances)."""
+    every single-communicator schedule (buckets, sharded, factors) is
+    captured and timed, the fastest is kept, and the tuning steps are real
+    steps (step counter advances)."""
     from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
 
     x, y = data
@@ -218,10 +219,10 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     assert eng.sync_schedule == "buckets"  # default until tuned
     assert eng.comm2 is None  # auto never builds the two-communicator schedule
     n = eng.tune_schedule()
-    assert n == 2 * 3 * 5 and eng.step == n
+    assert n == 3 * 3 * 5 and eng.step == n and n == 3 * 3 * 5
     assert int(eng.step_dev.item()) == n
     log = eng.tune_log
-    assert set(log) == {"buckets", "sharded"}
+    assert set(log) == {"buckets", "sharded", "factors"}
     assert eng.sync_schedule == min(log, key=log.get)
     eng.train(7)
     torch.cuda.synchronize()
