@@ -124,9 +124,10 @@ def prewarm(eng, x, y, ms: float) -> float:
     if ms <= 0:
         return 0.0
     n = min(2000, int(x.shape[0]))
+    xs, ys = x[:n], y[:n]  # one object: engines that keep the eval set resident upload it once
     t0 = time.perf_counter()
     while 1000.0 * (time.perf_counter() - t0) < ms:
-        eng.evaluate(x[:n], y[:n])
+        eng.evaluate(xs, ys)
     return round(1000.0 * (time.perf_counter() - t0), 1)
 
 
