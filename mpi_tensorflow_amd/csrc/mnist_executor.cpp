@@ -367,8 +367,8 @@ void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStrea
   reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
   HIP_CHECK(hipEventRecord(ev_done_, cs));
   // (an FC momentum SGD applied in the GEMM epilogue instead of this SGD pass
-  // measured slower: 146 -> 155 us at N = 2, 191 -> 204 us at N = 8 against
-  // the emulated ring, docs/PERF_NOTES.md)
+  // measured slower with per-element update chains and neutral with all
+  // loads batched first, docs/PERF_NOTES.md)
   HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
   mnist::launch_fc1_bwd_weights(a2, dh, hd, dl, n * p.batch, G + p.off_w3, G + p.off_b3,
                                 G + p.off_w4, G + p.off_b4, s);
