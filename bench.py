@@ -222,6 +222,18 @@ def main(argv=None) -> int:
                 eng.train(max(0, steps_per_run(eng.n_local, cfg.epochs, a.batch_size) - eng.step))
                 sync()
         err = D.allreduce_sum_host(eng.evaluate(test_x, test_y)) / N
+    # replica consistency (N > 1, per-step gradient sync): every rank must hold
+    # bit-identical weights after the run; a mismatch means a lost or corrupted
+    # collective, and the run fails loudly (outside the timing)
+    replicas = None
+    if N > 1 and a.sync == "grad" and getattr(eng, "params", None) is not None:
+        from mpi_tensorflow_amd.parallel.sync import replica_checksum
+
+        if hasattr(eng, "sync_optimizer_state"):
+            eng.sync_optimizer_state()
+        sync()
+        c = replica_checksum(eng.params)
+        replicas = D.allreduce_max_host(c) == -D.allreduce_max_host(-c)
     images = N * a.batch_size * a.steps
     value = images / dt
     if a.model == "mnist_cnn":
@@ -270,6 +282,7 @@ def main(argv=None) -> int:
                 "sync_tune_steps": tune_steps,
                 "graph_steps": (a.graph_steps if not a.no_graph else 0),
                 "prewarm_ms": prewarm_ms,
+                "replicas_identical": replicas,
             },
             "final_test_accuracy": None if err != err else round(100.0 - err, 3),
             "test_eval_after_steps": int(eng.step),
@@ -280,6 +293,10 @@ def main(argv=None) -> int:
     D.barrier()
     wd.stop()
     D.shutdown()
+    if replicas is False:
+        print("error: the ranks' weights differ after the run (replica checksum mismatch)",
+              file=sys.stderr)
+        return 4
     return 0
 
 

@@ -358,7 +358,10 @@ class NativeMnistEngine(MnistEngineBase):
         cs = stream_handle(self.comm_stream) if self.comm_stream is not None else 0
         self.exe.train_step(stream_handle(), self._native_comm, cs, self._native_comm2)
 
-    def _graph(self, n: int) -> Optional[torch.cuda.CUDAGraph]:
+    def _graph(self, n: int, sticky: bool = True) -> Optional[torch.cuda.CUDAGraph]:
+        """Captured graph of n steps under the current schedule.  A failed
+        capture switches the engine to eager launches (sticky) or, while the
+        schedules are being tuned, only drops that candidate."""
         key = (self.exe.schedule, n)
         g = self._graphs.get(key)
         if g is None:
@@ -373,9 +376,10 @@ class NativeMnistEngine(MnistEngineBase):
             except RuntimeError as e:
                 # e.g. a collective library build that cannot be captured:
                 # keep training with eager launches instead of failing the run
-                print(f"[rank {self.rank}] hipGraph capture failed ({e}); using eager launches",
+                print(f"[rank {self.rank}] hipGraph capture failed ({e}); "
+                      + ("using eager launches" if sticky else "skipping this schedule"),
                       flush=True)
-                self.use_graph = False
+                self.use_graph = self.use_graph and not sticky
                 torch.cuda.synchronize(self.device)
                 return None
             self._graphs[key] = g
@@ -407,10 +411,15 @@ class NativeMnistEngine(MnistEngineBase):
             cands.append((E.SCHED_FACTORS, "factors"))
         for sched, name in cands:
             self._set_schedule(sched)
-            g = self._graph(G)
-            if g is None:  # capture unavailable: keep the default schedule
-                self._set_schedule(E.SCHED_BUCKETS)
-                break
+            g = self._graph(G, sticky=(sched == E.SCHED_BUCKETS))
+            # the decision must be collective: a candidate any rank could not
+            # capture is dropped on every rank
+            ok = D.allreduce_max_host(0.0 if g is not None else 1.0) == 0.0
+            if not ok:
+                if sched == E.SCHED_BUCKETS:  # no graphs at all: keep buckets, eager
+                    break
+                self.tune_log[name] = None
+                continue
             g.replay()
             torch.cuda.synchronize(self.device)
             t0 = torch.cuda.Event(enable_timing=True)
@@ -425,8 +434,7 @@ class NativeMnistEngine(MnistEngineBase):
             self.tune_log[name] = round(us, 2)
             if best is None or us < best[0]:
                 best = (us, sched)
-        if best is not None:
-            self._set_schedule(best[1])
+        self._set_schedule(best[1] if best is not None else E.SCHED_BUCKETS)
         self._tuned = True
         self.step += steps
         return steps

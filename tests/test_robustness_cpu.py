@@ -118,6 +118,7 @@ def test_bench_spawns_ranks_without_launcher():
     j = json.loads(lines[0])
     assert j["n_gpus"] == 2 and j["config"]["parallelism"] == "dp2"
     assert j["config"]["ranks"] == 2 and j["config"]["global_batch"] == 128
+    assert j["config"]["replicas_identical"] is True  # post-run weight checksum over ranks
 
 
 @pytest.mark.slow
