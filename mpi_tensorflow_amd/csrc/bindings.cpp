@@ -72,6 +72,22 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   }, py::arg("data"), py::arg("step"), py::arg("n_local"), py::arg("batch"), py::arg("w"),
      py::arg("b"), py::arg("out"), py::arg("argmax"), py::arg("stream"), py::arg("out_pad") = 0);
+  k.def("conv12_fwd", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
+                         uintptr_t b1, uintptr_t a1, uintptr_t a1pf, uintptr_t idx1, uintptr_t w2,
+                         uintptr_t b2, uintptr_t a2, uintptr_t idx2, uintptr_t w2t, uintptr_t s) {
+    mnist::C12In c;
+    c.data = P<const float>(data);
+    c.step = P<const long long>(step);
+    c.n_local = n_local;
+    c.w1 = P<const float>(w1);
+    c.b1 = P<const float>(b1);
+    c.a1 = P<float>(a1);
+    c.a1pf = P<float>(a1pf);
+    c.idx1 = P<uint8_t>(idx1);
+    mnist::launch_conv12_fwd(c, batch, P<const float>(w2), P<const float>(b2), P<float>(a2),
+                             P<uint8_t>(idx2), P<float>(w2t), S(s));
+    check_launch();
+  });
   k.def("conv2_fwd", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t b, uintptr_t out,
                         uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
     mnist::launch_conv2_fwd(P<const float>(a1), batch, P<const float>(w), P<const float>(b),

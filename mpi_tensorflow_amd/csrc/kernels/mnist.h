@@ -44,6 +44,22 @@ void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local
                            const float* w3 = nullptr, const float* w2 = nullptr,
                            uint16_t* w1b = nullptr, uint16_t* w1t = nullptr,
                            uint16_t* w2tb = nullptr, uint16_t* w2b = nullptr);
+// Train forward of conv1 + conv2 in ONE launch (fp32): every conv2 block
+// computes the pooled conv1 rows of its input halo itself (~2x recompute of the
+// 25-tap conv1) and writes the rows it owns to a1 / a1pf / idx1 (the layouts
+// of launch_conv1_fwd); data rows at the device-step batch offset.
+struct C12In {
+  const float* data = nullptr;
+  const long long* step = nullptr;
+  int n_local = 0;
+  const float* w1 = nullptr;
+  const float* b1 = nullptr;
+  float* a1 = nullptr;
+  float* a1pf = nullptr;
+  uint8_t* idx1 = nullptr;
+};
+void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float* b2, float* a2,
+                       uint8_t* idx2, float* w2t, hipStream_t s);
 // w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s);

@@ -585,12 +585,101 @@ constexpr int C2_XS_ROWS = 8, C2_XS_COLS = 18;
 // come from the LDS halo tile, B (weights, L2 resident) one tap ahead in
 // registers.  Also writes W2T[t][co][ci] for bwd-data when w2t != nullptr.
 constexpr int C2_XS = C2_XS_ROWS * C2_XS_COLS * 33;
+// FUSED: the input image rows of the block (8 pg - 6 .. 8 pg + 13, columns
+// -2 .. 30, zero outside the 28 x 28 image)
+constexpr int C12_IMG_ROWS = 20, C12_IMG_LD = 33;
 
+// conv1 of the fused train forward (launch_conv12_fwd): the block computes the
+// pooled conv1 rows its conv2 halo needs (a1 rows 4 pg - 2 .. 4 pg + 5, ~2x
+// recompute of a 25-tap conv) straight into the halo tile, and writes the rows
+// it owns (4 pg .. 4 pg + 3) to a1 / a1pf / idx1 for the backward pass.  Same
+// GEMM view as conv_pool_fwd_kernel: M = pre-pool pixels (window, quadrant),
+// N = 32 channels, K = 25 taps (-> 32), one 32 x 32 MFMA tile per 8 windows.
+__device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int n, int pg,
+                                                float* __restrict__ xs, float* __restrict__ img) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long off = batch_offset_dev(c1.step, c1.n_local, batch);
+  const float* xin = c1.data + (off + n) * 784;
+  const int iy0 = 8 * pg - 6;
+  constexpr int NIMG = C12_IMG_ROWS * C12_IMG_LD;  // 660
+  float iv[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = tid + 256 * j;
+    const int r = i / C12_IMG_LD, c = i % C12_IMG_LD, iy = iy0 + r, ix = c - 2;
+    const bool ok = i < NIMG && iy >= 0 && iy < 28 && ix >= 0 && ix < 28;
+    const float v = xin[min(max(iy, 0), 27) * 28 + min(max(ix, 0), 27)];
+    iv[j] = ok ? v : 0.f;
+  }
+  const int co = lane & 31, kh2 = lane >> 5;
+  float wb[16];
+#pragma unroll
+  for (int st = 0; st < 16; ++st) {
+    const int k = 2 * st + kh2;
+    const float v = c1.w1[min(k, 24) * 32 + co];
+    wb[st] = k < 25 ? v : 0.f;
+  }
+  const float bias = c1.b1[co];
+  for (int i = tid; i < C2_XS; i += 256) xs[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = tid + 256 * j;
+    if (i < NIMG) img[i] = iv[j];
+  }
+  __syncthreads();
+  const int y0 = 4 * pg - 2;  // a1 row of halo row 0
+  const int ya = max(y0, 0), yb = min(y0 + C2_XS_ROWS, 14);
+  const int nwin = (yb - ya) * 14, ntile = (nwin + 7) / 8;
+  for (int t = wave; t < ntile; t += 4) {
+    const int m = lane & 31, wi = t * 8 + (m >> 2), q = m & 3;
+    const bool vw = wi < nwin;
+    const int wic = vw ? wi : 0;
+    const int py = 2 * (ya + wic / 14) + (q >> 1), px = 2 * (wic % 14) + (q & 1);
+    const float* ib = img + (py - 2 - iy0) * C12_IMG_LD + px;  // + kh * LD + kw
+    // one accumulator chain in K order, like conv_pool_fwd_kernel (same sums)
+    f32x16 acc = zero16();
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int k = 2 * st + kh2, kc = min(k, 24);
+      const float a = ib[(kc / 5) * C12_IMG_LD + kc % 5];
+      acc = mfma32x32x2((vw && k < 25) ? a : 0.f, wb[st], acc);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int wj = t * 8 + 2 * g + (lane >> 5);
+      float v = acc[4 * g];
+      int qq = 0;
+#pragma unroll
+      for (int j = 1; j < 4; ++j) {
+        if (acc[4 * g + j] > v) {  // strict: first max wins (TF MaxPool order)
+          v = acc[4 * g + j];
+          qq = j;
+        }
+      }
+      if (wj < nwin) {
+        const int y = ya + wj / 14, x = wj % 14;
+        const float o = fmaxf(v + bias, 0.f);
+        xs[((y - y0) * C2_XS_COLS + x + 2) * 33 + co] = o;
+        if (y >= 4 * pg && y < 4 * pg + 4) {  // rows this block owns
+          const size_t pi = ((size_t)(n * 14 + y) * 14 + x) * 32 + co;
+          c1.a1[pi] = o;
+          c1.idx1[pi] = (uint8_t)qq;
+          c1.a1pf[((size_t)(n * 18 + y + 2) * 18 + x + 2) * 32 + co] = o;
+        }
+      }
+    }
+  }
+}
+
+// FUSED (train): conv1 is computed into the halo tile (conv1_into_halo)
+// instead of a separate conv1 launch staging a1 through global memory.
+template <bool FUSED>
 __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ b2, float* __restrict__ out, uint8_t* __restrict__ argmax,
-    float* __restrict__ w2t) {
+    float* __restrict__ w2t, const C12In c1) {
   __shared__ float xs[C2_XS];
+  __shared__ float img[FUSED ? C12_IMG_ROWS * C12_IMG_LD : 1];
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (w2t) {  // 51200 floats over all blocks
@@ -599,7 +688,9 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
       w2t[i] = w2[(t * 32 + ci) * 64 + co];
     }
   }
-  {  // stage the halo tile: all loads in flight first, then the LDS writes
+  if constexpr (FUSED) {
+    conv1_into_halo(c1, batch, n, pg, xs, img);
+  } else {  // stage the halo tile: all loads in flight first, then the LDS writes
     constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 32 / 256;  // 18
     float sv[NS];
 #pragma unroll
@@ -1001,7 +1092,14 @@ void launch_conv1_fwd_bf16(const float* data, const long long* step, int n_local
 
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s) {
-  conv2_fwd_v3_kernel<<<batch * 4, 256, 0, s>>>(a1, batch, w, b, out, argmax, w2t);
+  conv2_fwd_v3_kernel<false><<<batch * 4, 256, 0, s>>>(a1, batch, w, b, out, argmax, w2t, C12In{});
+}
+
+void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float* b2, float* a2,
+                       uint8_t* idx2, float* w2t, hipStream_t s) {
+  if (!c1.data || !c1.w1 || !c1.b1 || !c1.a1 || !c1.a1pf || !c1.idx1)
+    throw std::runtime_error("conv12_fwd: missing conv1 operand");
+  conv2_fwd_v3_kernel<true><<<batch * 4, 256, 0, s>>>(nullptr, batch, w2, b2, a2, idx2, w2t, c1);
 }
 
 int fc1_train_splits() { return FC1_SPLITS; }

@@ -53,10 +53,19 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   const long long* step = P<const long long>(p.step);
   const int B = p.batch;
   // forward
-  mnist::launch_conv1_fwd(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
-                          W + p.off_b1, P<float>(p.a1), P<uint8_t>(p.idx1), s, P<float>(p.a1pf));
-  mnist::launch_conv2_fwd(P<const float>(p.a1), B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
-                          P<uint8_t>(p.idx2), P<float>(p.w2t), s);
+  // conv1 is recomputed inside the conv2 blocks (one launch, ~3 us less than a
+  // separate conv1 launch staging a1 through memory: 108.2 -> 105.0 us/step)
+  mnist::C12In cf;
+  cf.data = P<const float>(p.train_x);
+  cf.step = step;
+  cf.n_local = p.n_local;
+  cf.w1 = W + p.off_w1;
+  cf.b1 = W + p.off_b1;
+  cf.a1 = P<float>(p.a1);
+  cf.a1pf = P<float>(p.a1pf);
+  cf.idx1 = P<uint8_t>(p.idx1);
+  mnist::launch_conv12_fwd(cf, B, W + p.off_w2, W + p.off_b2, P<float>(p.a2), P<uint8_t>(p.idx2),
+                           P<float>(p.w2t), s);
   wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
   mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
   mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,

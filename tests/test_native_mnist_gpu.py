@@ -70,6 +70,48 @@ def test_conv_pool_forward_matches_oracle(cuda_dev, data):
     assert torch.equal(i1[pos], code[pos])
 
 
+@pytest.mark.parametrize("step", [0, 3])
+def test_fused_conv12_forward_matches_oracle(cuda_dev, data, step):
+    """Train forward of conv1 + conv2 in one launch (conv1 recomputed into each
+    conv2 block's halo): a1 / zero-bordered a1pf / idx1 / a2 / idx2 vs torch on
+    the batch rows at the device-step offset."""
+    Cn = native()
+    x, _ = data
+    B, n_local = 64, 512
+    xd = torch.from_numpy(x[:n_local]).to(cuda_dev)
+    g = torch.Generator().manual_seed(5)
+    w1 = (torch.randn(5, 5, 1, 32, generator=g) * 0.2).to(cuda_dev)
+    b1 = (torch.randn(32, generator=g) * 0.1).to(cuda_dev)
+    w2 = (torch.randn(5, 5, 32, 64, generator=g) * 0.05).to(cuda_dev)
+    b2 = (torch.randn(64, generator=g) * 0.1).to(cuda_dev)
+    a1 = torch.empty(B, 14, 14, 32, device=cuda_dev)
+    a1pf = torch.zeros(B, 18, 18, 32, device=cuda_dev)
+    i1 = torch.empty(B, 14, 14, 32, dtype=torch.uint8, device=cuda_dev)
+    a2 = torch.empty(B, 7, 7, 64, device=cuda_dev)
+    i2 = torch.empty(B, 7, 7, 64, dtype=torch.uint8, device=cuda_dev)
+    w2t = torch.empty(25 * 64 * 32, device=cuda_dev)
+    st = torch.tensor([step], dtype=torch.int64, device=cuda_dev)
+    Cn.mnist.conv12_fwd(ptr(xd), ptr(st), n_local, B, ptr(w1), ptr(b1), ptr(a1), ptr(a1pf),
+                        ptr(i1), ptr(w2), ptr(b2), ptr(a2), ptr(i2), ptr(w2t), stream_handle())
+    torch.cuda.synchronize()
+    off = (step * B) % (n_local - B)
+    xn = xd[off:off + B].permute(0, 3, 1, 2)
+    z1 = F.conv2d(xn, w1.permute(3, 2, 0, 1), b1, padding=2)
+    r1, ri1 = F.max_pool2d(F.relu(z1), 2, 2, return_indices=True)
+    z2 = F.conv2d(r1, w2.permute(3, 2, 0, 1), b2, padding=2)
+    r2, ri2 = F.max_pool2d(F.relu(z2), 2, 2, return_indices=True)
+    r1h = r1.permute(0, 2, 3, 1)
+    assert _rel(a1, r1h) < 1e-5
+    assert torch.equal(a1pf[:, 2:16, 2:16], a1)
+    assert float(a1pf[:, :2].abs().sum() + a1pf[:, 16:].abs().sum()) == 0.0  # border untouched
+    assert _rel(a2, r2.permute(0, 2, 3, 1)) < 1e-5
+    assert torch.equal(w2t.view(25, 64, 32), w2.view(25, 32, 64).transpose(1, 2))
+    for idx, ri, r, w in ((i1, ri1, r1h, 28), (i2, ri2, r2.permute(0, 2, 3, 1), 14)):
+        code = (((ri // w) % 2) * 2 + (ri % w) % 2).permute(0, 2, 3, 1).to(torch.uint8)
+        pos = r > 0
+        assert torch.equal(idx[pos], code[pos])
+
+
 @pytest.mark.parametrize("batch", [64, 96, 128])
 def test_forward_backward_grads_match_oracle(cuda_dev, data, batch):
     """All grads of one native step vs the fp32 PyTorch oracle; batch 96
