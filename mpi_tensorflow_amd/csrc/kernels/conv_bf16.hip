@@ -99,8 +99,18 @@ __global__ __launch_bounds__(256) void wcvt_batch_kernel(const long long* __rest
                                                          int njobs) {
   __shared__ float t[32][33];
   const int b = blockIdx.x;
+  // job of this block: the first blocks ascend with j, so the jobs starting at
+  // or before b are a prefix; every lane tests one job (one load round per 64
+  // jobs instead of a dependent load chain through the table)
   int j = 0;
-  while (j + 1 < njobs && jobs[8 * (j + 1) + 6] <= b) ++j;
+  for (int base = 0; base < njobs; base += 64) {
+    const int jj = base + (int)(threadIdx.x & 63);
+    const bool le = jj < njobs && jobs[8 * min(jj, njobs - 1) + 6] <= b;
+    const int cnt = __popcll(__ballot(le));
+    j = base + cnt - 1;
+    if (cnt < 64) break;
+  }
+  j = max(j, 0);
   const long long* J = jobs + 8 * j;
   const float* w = reinterpret_cast<const float*>(J[0]);
   __bf16* out = reinterpret_cast<__bf16*>(J[1]);
