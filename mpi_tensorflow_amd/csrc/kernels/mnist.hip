@@ -630,20 +630,15 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
   const int y0 = 4 * pg - 2;  // a1 row of halo row 0
   const int ya = max(y0, 0), yb = min(y0 + C2_XS_ROWS, 14);
   const int nwin = (yb - ya) * 14, ntile = (nwin + 7) / 8;
-  for (int t = wave; t < ntile; t += 4) {
+  // A-operand base of tile t for this lane (vw: the lane's window exists)
+  auto tile_base = [&](int t, bool& vw) {
     const int m = lane & 31, wi = t * 8 + (m >> 2), q = m & 3;
-    const bool vw = wi < nwin;
+    vw = wi < nwin;
     const int wic = vw ? wi : 0;
     const int py = 2 * (ya + wic / 14) + (q >> 1), px = 2 * (wic % 14) + (q & 1);
-    const float* ib = img + (py - 2 - iy0) * C12_IMG_LD + px;  // + kh * LD + kw
-    // one accumulator chain in K order, like conv_pool_fwd_kernel (same sums)
-    f32x16 acc = zero16();
-#pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const int k = 2 * st + kh2, kc = min(k, 24);
-      const float a = ib[(kc / 5) * C12_IMG_LD + kc % 5];
-      acc = mfma32x32x2((vw && k < 25) ? a : 0.f, wb[st], acc);
-    }
+    return img + (py - 2 - iy0) * C12_IMG_LD + px;  // + kh * LD + kw
+  };
+  auto epilogue = [&](int t, const f32x16& acc) {
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int wj = t * 8 + 2 * g + (lane >> 5);
@@ -668,6 +663,25 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
         }
       }
     }
+  };
+  // tiles t and t + 4 of this wave as two interleaved accumulator chains:
+  // consecutive MFMAs are independent, and each tile's sum keeps the K order of
+  // the standalone conv1 kernel (same results)
+  for (int t = wave; t < ntile; t += 8) {
+    const bool two = t + 4 < ntile;
+    bool v0, v1;
+    const float* ib0 = tile_base(t, v0);
+    const float* ib1 = tile_base(two ? t + 4 : t, v1);
+    f32x16 acc0 = zero16(), acc1 = zero16();
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const int k = 2 * st + kh2, kc = min(k, 24), o = (kc / 5) * C12_IMG_LD + kc % 5;
+      const float a0 = ib0[o], a1v = ib1[o];
+      acc0 = mfma32x32x2((v0 && k < 25) ? a0 : 0.f, wb[st], acc0);
+      acc1 = mfma32x32x2((v1 && k < 25) ? a1v : 0.f, wb[st], acc1);
+    }
+    epilogue(t, acc0);
+    if (two) epilogue(t + 4, acc1);
   }
 }
 
