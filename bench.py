@@ -19,7 +19,12 @@ Each rank runs W untimed steps, then EXACTLY K timed steps bracketed by a
 barrier + device synchronize on both sides; the slowest rank's time is
 used; rank 0 prints one JSON line.  Every timed step is a full training
 step (forward, backward, all-reduce, SGD update); eval is outside the
-timed region.
+timed region.  Before the W warm-up steps, --prewarm-ms (default 100) of
+forward-only test-set passes bring the GPU out of its idle clock state
+(no training state changes; reported as prewarm_ms).  With N > 1 the
+sync schedule is autotuned first (real training steps, reported), and
+after the run every rank's weights are checksummed: replicas that differ
+fail the run (replicas_identical in the JSON).
 """
 
 from __future__ import annotations
