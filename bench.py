@@ -57,6 +57,8 @@ def parse(argv=None):
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded", "split", "factors"))
+    ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "torch"),
+                    help="device communicator (auto: RCCL, or shared memory when ranks share GPUs)")
     ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),
                     help="wire dtype of the gradient all-reduce (bf16: half the xGMI bytes)")
     ap.add_argument("--comm-emulate", default=None, metavar="LAT_US,BUSBW_GBPS[,N[,BLOCKS]]",
@@ -84,13 +86,36 @@ def _free_port() -> int:
     return port
 
 
+def gpu_count_sysfs() -> int:
+    """GPUs visible to this process, counted from the KFD topology in sysfs
+    (nodes with SIMDs) and the *_VISIBLE_DEVICES masks: no HIP call, so the
+    spawning parent can never initialise the GPU runtime.  -1 if unknown."""
+    import glob
+
+    n = 0
+    try:
+        for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            with open(f) as fh:
+                for line in fh:
+                    k, _, v = line.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+    except (OSError, ValueError):
+        return -1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(n: int, argv) -> int:
     """Starts n rank processes of this script (no torchrun / mpirun in the
-    environment).  The parent never initialises the GPU (it only counts
-    devices), so the children are fresh processes, not re-execs.  Rank 0's
+    environment).  The parent makes no HIP call at all (GPUs are counted from
+    sysfs), so the children are fresh processes, not re-execs.  Rank 0's
     stdout (the JSON line) is inherited; the first failing rank makes the
     parent stop the others and return its exit code."""
-    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    ndev = gpu_count_sysfs()
     if 0 < ndev < n:
         print(f"error: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
         return 2
@@ -139,12 +164,9 @@ def prewarm(eng, x, y, ms: float) -> float:
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
-    from mpi_tensorflow_amd import config as C
     from mpi_tensorflow_amd.parallel import dist as D
-    from mpi_tensorflow_amd.parallel.comm import make_comm
     from mpi_tensorflow_amd.parallel.watchdog import make_watchdog
-    from mpi_tensorflow_amd.runtime.mnist_engine import make_engine
-    from mpi_tensorflow_amd.utils.data import load_mnist_shard
+    from mpi_tensorflow_amd.utils.faults import maybe_fail
 
     if a.gpus > 1 and D.discover().launcher == "none":
         return launch_ranks(a.gpus, argv)
@@ -155,56 +177,89 @@ def main(argv=None) -> int:
     device = D.resolve_device("auto")
     di = D.init(str(device))
     N = di.world
+    maybe_fail("after_init", di.rank)
+    # the watchdog exists before the communicator: start-up collectives
+    # (communicator init, the engines' connection setup) are guarded too
+    wd = make_watchdog([], a.collective_timeout_s, di.rank, N)
+    try:
+        return run(a, di, device, wd)
+    finally:
+        wd.stop()
+
+
+def run(a, di, device, wd) -> int:
+    from mpi_tensorflow_amd import config as C
+    from mpi_tensorflow_amd.parallel import dist as D
+    from mpi_tensorflow_amd.parallel.comm import make_comm
+    from mpi_tensorflow_amd.parallel.watchdog import run_in_chunks
+    from mpi_tensorflow_amd.runtime.mnist_engine import make_engine
+    from mpi_tensorflow_amd.runtime.trainer import comm_capacity_bytes
+    from mpi_tensorflow_amd.utils.data import load_mnist_shard
+    from mpi_tensorflow_amd.utils.faults import maybe_fail
+
+    N = di.world
     if a.batch_size is None:
         a.batch_size = 32 if a.model == "resnet18" else 64
     cfg = C.TrainConfig(model=a.model, batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
                         graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend,
-                        sync_schedule=a.sync_schedule,
-                        grad_comm_dtype=a.grad_comm_dtype).validate()
-    comm = make_comm(di, device) if (N > 1 and a.sync == "grad") else None
+                        sync_schedule=a.sync_schedule, comm=a.comm,
+                        grad_comm_dtype=a.grad_comm_dtype,
+                        collective_timeout_s=a.collective_timeout_s).validate()
     force = bool((a.force_sync or a.comm_emulate) and N == 1 and device.type == "cuda")
-    if force and a.comm_emulate:
-        from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
-        f = [float(v) for v in a.comm_emulate.split(",")]
-        comm = EmulatedDeviceComm(int(f[2]) if len(f) > 2 else 8, f[0], f[1],
-                                  int(f[3]) if len(f) > 3 else 32)
-    elif force:
-        from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
-        comm = RcclDeviceComm(di)
-    if a.model == "mnist_cnn":
-        shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
-        eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
-                          force_sync=force)
-        test_x, test_y = shard.test_x, shard.test_y
-    else:
-        from mpi_tensorflow_amd.models.generic import model_input_shape
-        from mpi_tensorflow_amd.runtime.generic_engine import make_image_engine
-        from mpi_tensorflow_amd.utils.data import synthetic_images_torch
+    with wd.guard("start-up (communicator, engine)"):
+        maybe_fail("before_comm", di.rank)
+        comm = None
+        if N > 1 and a.sync == "grad":
+            comm = make_comm(di, device, a.comm, shm_capacity=comm_capacity_bytes(cfg),
+                             timeout_s=a.collective_timeout_s)
+        if force and a.comm_emulate:
+            from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
+            f = [float(v) for v in a.comm_emulate.split(",")]
+            comm = EmulatedDeviceComm(int(f[2]) if len(f) > 2 else 8, f[0], f[1],
+                                      int(f[3]) if len(f) > 3 else 32)
+        elif force:
+            from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
+            comm = RcclDeviceComm(di)
+        wd.add(comm)
+        maybe_fail("after_comm", di.rank)
+        if a.model == "mnist_cnn":
+            shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
+            eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
+                              force_sync=force)
+            test_x, test_y = shard.test_x, shard.test_y
+        else:
+            from mpi_tensorflow_amd.models.generic import model_input_shape
+            from mpi_tensorflow_amd.runtime.generic_engine import make_image_engine
+            from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
-        shape = model_input_shape(a.model)
-        rows = max(4 * a.batch_size, 8192 if a.model == "lenet5" else 4 * a.batch_size)
-        tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
-        ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
-                                        start=di.rank * rows)
-        eng = make_image_engine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
-                                force_sync=force)
-        test_x, test_y = ex.numpy(), ey.numpy()
+            shape = model_input_shape(a.model)
+            rows = max(4 * a.batch_size, 8192 if a.model == "lenet5" else 4 * a.batch_size)
+            tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
+            ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
+                                            start=di.rank * rows)
+            eng = make_image_engine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
+                                    force_sync=force)
+            test_x, test_y = ex.numpy(), ey.numpy()
+        wd.add(getattr(eng, "comm2", None))
 
     def sync():
         if device.type == "cuda":
             torch.cuda.synchronize()
 
-    wd = make_watchdog([comm, getattr(eng, "comm2", None)], a.collective_timeout_s, di.rank, N)
     # startup autotune of the gradient-sync schedule (N > 1, native MNIST
-    # engine): real training steps, before the warm-up, outside the timing
-    with wd.guard("sync-schedule autotune"):
+    # engine): trial steps that are discarded (params / momentum / step are
+    # restored), before the warm-up, outside the timing
+    with wd.guard("sync-schedule autotune and capture"):
         tune_steps = eng.tune_schedule() if hasattr(eng, "tune_schedule") else 0
         if hasattr(eng, "capture"):
             eng.capture(a.warmup)
             eng.capture(a.steps)
         prewarm_ms = prewarm(eng, test_x, test_y, a.prewarm_ms if device.type == "cuda" else 0.0)
-        eng.train(a.warmup)
         sync()
+    maybe_fail("before_train", di.rank)
+    chunks = {}
+    run_in_chunks(wd, eng.train, sync, a.warmup, "warm-up steps",
+                  granule=getattr(eng, "graph_steps", 1), state=chunks)
     D.barrier()
     sync()
     with wd.guard(f"timed steps ({a.steps})"):  # arming is two attribute writes
@@ -223,22 +278,22 @@ def main(argv=None) -> int:
         if a.model == "mnist_cnn":
             from mpi_tensorflow_amd.utils.data import steps_per_run
 
-            with wd.guard("accuracy run"):
-                eng.train(max(0, steps_per_run(eng.n_local, cfg.epochs, a.batch_size) - eng.step))
-                sync()
+            run_in_chunks(wd, eng.train, sync,
+                          max(0, steps_per_run(eng.n_local, cfg.epochs, a.batch_size) - eng.step),
+                          "accuracy-run steps", first_step=eng.step,
+                          granule=getattr(eng, "graph_steps", 1), state=chunks)
         err = D.allreduce_sum_host(eng.evaluate(test_x, test_y)) / N
     # replica consistency (N > 1, per-step gradient sync): every rank must hold
     # bit-identical weights after the run; a mismatch means a lost or corrupted
     # collective, and the run fails loudly (outside the timing)
     replicas = None
     if N > 1 and a.sync == "grad" and getattr(eng, "params", None) is not None:
-        from mpi_tensorflow_amd.parallel.sync import replica_checksum
+        from mpi_tensorflow_amd.parallel.sync import replicas_identical
 
         if hasattr(eng, "sync_optimizer_state"):
             eng.sync_optimizer_state()
         sync()
-        c = replica_checksum(eng.params)
-        replicas = D.allreduce_max_host(c) == -D.allreduce_max_host(-c)
+        replicas = replicas_identical(eng.params) and replicas_identical(eng.mom)
     images = N * a.batch_size * a.steps
     value = images / dt
     if a.model == "mnist_cnn":
@@ -275,7 +330,7 @@ def main(argv=None) -> int:
                 "seq_len": None,
                 "image": image,
                 "parallelism": f"dp{N}",
-                "sync": ("per-step gradient all-reduce (RCCL)" if (N > 1 or force)
+                "sync": ("per-step gradient all-reduce" if (N > 1 or force)
                          else "none (1 rank)"),
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
@@ -296,7 +351,6 @@ def main(argv=None) -> int:
         print(json.dumps(out))
         sys.stdout.flush()
     D.barrier()
-    wd.stop()
     D.shutdown()
     if replicas is False:
         print("error: the ranks' weights differ after the run (replica checksum mismatch)",

@@ -66,6 +66,11 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
 # compute stream over a second communicator
 SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors")
+# device communicator (world > 1): "auto" = native RCCL when every rank has a
+# GPU of its own, the shared-memory host-staged communicator when ranks share
+# GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",
+# "shm" and "torch" (torch.distributed) force one
+COMMS = ("auto", "rccl", "shm", "torch")
 DTYPES = ("fp32", "bf16")
 
 
@@ -87,6 +92,12 @@ class TrainConfig:
     # fp32 tensors) or bf16 (half the bytes over xGMI; the sum is rounded to
     # bf16 on the wire, the update stays fp32)
     grad_comm_dtype: str = "fp32"
+    comm: str = "auto"
+    # restrict sync_schedule="auto" to the schedules whose updates are bit
+    # identical to the bucketed all-reduce (the factor schedule sums the FC
+    # gradients in another order, so an auto run that picked it is only
+    # reproducible by naming it; the chosen schedule is logged either way)
+    deterministic: bool = False
     # evaluate (and print the reference log line) every N steps; the
     # reference evaluates every step (Q9) but prints every 50
     eval_every: int = SYNC_EVERY
@@ -131,6 +142,8 @@ class TrainConfig:
                              f"choose from {SYNC_SCHEDULES}")
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError(f"unknown grad comm dtype {self.grad_comm_dtype!r}")
+        if self.comm not in COMMS:
+            raise ValueError(f"unknown comm {self.comm!r}; choose from {COMMS}")
         if self.dtype not in DTYPES:
             raise ValueError(f"unknown dtype {self.dtype!r}; choose from {DTYPES}")
         if self.backend not in ("auto", "native", "torch"):
@@ -182,6 +195,11 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
                         "factors: all-gather the FC gradient factors, fp32)")
     p.add_argument("--grad-comm-dtype", default=d.grad_comm_dtype, choices=("fp32", "bf16"),
                    help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
+    p.add_argument("--comm", default=d.comm, choices=COMMS,
+                   help="device communicator: RCCL over xGMI (one GPU per rank), shm (host-"
+                        "staged shared memory, ranks may share a GPU) or torch.distributed")
+    p.add_argument("--deterministic", action="store_true",
+                   help="sync-schedule auto-tune picks only bit-identical schedules")
     p.add_argument("--eval-every", type=int, default=d.eval_every,
                    help="0 disables periodic eval")
     p.add_argument("--data-dir", default=d.data_dir)

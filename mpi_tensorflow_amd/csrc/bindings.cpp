@@ -17,6 +17,7 @@
 #include "lenet_executor.h"
 #include "mnist_executor.h"
 #include "rccl_comm.h"
+#include "shm_comm.h"
 
 namespace py = pybind11;
 
@@ -182,6 +183,10 @@ PYBIND11_MODULE(_C, m) {
   });
   o.def("from_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t s) {
     optim::launch_from_bf16(P<const uint16_t>(x), P<float>(y), n, S(s));
+    check_launch();
+  });
+  o.def("hash_words", [](uintptr_t x, long long n, uintptr_t out, uintptr_t s) {
+    optim::launch_hash_words(P<const uint32_t>(x), n, P<unsigned long long>(out), S(s));
     check_launch();
   });
   o.def("scale", [](uintptr_t x, long long n, float a, uintptr_t s) {
@@ -414,6 +419,35 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<PyComm, Collective>(m, "PyComm")
       .def(py::init<int, int, py::function>(), py::arg("nranks"), py::arg("rank"), py::arg("fn"));
+
+  py::class_<ShmComm, Collective>(m, "ShmComm")
+      .def(py::init<const std::string&, bool, int, int, size_t, double, bool>(), py::arg("path"),
+           py::arg("create"), py::arg("nranks"), py::arg("rank"), py::arg("capacity"),
+           py::arg("timeout_s"), py::arg("pinned") = true)
+      .def("run_host",
+           [](ShmComm& c, int kind, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              int root) { c.run_host(kind, P<void>(send), P<void>(recv), count, dtype, op, root); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("broadcast",
+           [](ShmComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int root,
+              uintptr_t s) { c.broadcast(P<void>(send), P<void>(recv), count, dtype, root, S(s)); })
+      .def("reduce",
+           [](ShmComm& c, uintptr_t send, uintptr_t recv, size_t count, int dtype, int op,
+              int root, uintptr_t s) {
+             c.reduce(P<void>(send), P<void>(recv), count, dtype, op, root, S(s));
+           })
+      .def("async_error", &ShmComm::async_error)
+      .def("error_message", &ShmComm::error_message)
+      .def("abort", &ShmComm::abort)
+      .def("unlink_path", &ShmComm::unlink_path)
+      .def_property_readonly("capacity", &ShmComm::capacity)
+      .def_property_readonly("completed", &ShmComm::completed)
+      .def_property_readonly("host_progress", &ShmComm::host_progress);
+  m.attr("ShmComm").attr("AR") = (int)ShmComm::AR;
+  m.attr("ShmComm").attr("AG") = (int)ShmComm::AG;
+  m.attr("ShmComm").attr("RS") = (int)ShmComm::RS;
+  m.attr("ShmComm").attr("BC") = (int)ShmComm::BC;
+  m.attr("ShmComm").attr("RD") = (int)ShmComm::RD;
 
   py::class_<RcclComm, Collective>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank) {

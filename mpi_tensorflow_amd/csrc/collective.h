@@ -1,8 +1,11 @@
 // Device-collective interface of the step executors.
 //
 // The executors issue their gradient / parameter collectives through this
-// interface, on a HIP stream, inside the captured step.  Two implementations:
+// interface, on a HIP stream, inside the captured step.  Three implementations:
 //   RcclComm (rccl_comm.h) - RCCL over xGMI, the production path;
+//   ShmComm  (shm_comm.h)  - host-staged exchange through shared memory for
+//                            ranks that share a GPU (capturable: D2H copy,
+//                            host function, H2D copy);
 //   EmuComm  (below)       - a timing stand-in for an N-rank communicator on
 //                            ONE GPU, used to measure how a comm schedule
 //                            overlaps with the compute stream before the
@@ -35,6 +38,11 @@ class Collective {
   // several buffers.  Implementations without grouping run them one by one.
   virtual void group_start() {}
   virtual void group_end() {}
+  // True when the collectives make progress in blocking host functions
+  // (ShmComm): the collectives of two such communicators must then be
+  // reached in the same order on every rank, so a schedule that would run
+  // them concurrently on two streams orders them instead.
+  virtual bool host_progress() const { return false; }
 };
 
 // Ring cost model (rccl-tests conventions): an all-reduce of S bytes takes

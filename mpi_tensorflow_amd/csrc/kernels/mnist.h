@@ -126,4 +126,6 @@ void launch_scale(float* x, long long n, float a, hipStream_t s);
 // bf16 gradient wire: bucket copies around a collective (n % 4 == 0, 16-B aligned)
 void launch_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 void launch_from_bf16(const uint16_t* x, float* y, long long n, hipStream_t s);
+// *out = replica fingerprint of n raw 32-bit words (sgd.hip hash_words_kernel)
+void launch_hash_words(const uint32_t* x, long long n, unsigned long long* out, hipStream_t s);
 }  // namespace optim

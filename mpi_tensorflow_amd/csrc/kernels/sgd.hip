@@ -75,6 +75,33 @@ __global__ __launch_bounds__(256) void from_bf16_kernel(const uint2* __restrict_
   }
 }
 
+// Replica fingerprint: sum over i (mod 2^64) of splitmix64((i << 32) | word_i)
+// of the raw 32-bit words.  Position-keyed and bitwise, so any differing bit,
+// sign flip or permutation changes it; integer addition makes the sum
+// independent of the reduction order (one number per rank, compared across
+// ranks; parallel/sync.py:replica_hash has the identical host version).
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void hash_words_kernel(const uint32_t* __restrict__ x,
+                                                        long long n,
+                                                        unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[4];
+  unsigned long long acc = 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    acc += splitmix64(((unsigned long long)i << 32) | x[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);
+}
+
 static inline int grid_for(long long n4) {
   long long b = (n4 + 255) / 256;
   return (int)(b > 2048 ? 2048 : (b < 1 ? 1 : b));
@@ -100,6 +127,11 @@ void launch_from_bf16(const uint16_t* x, float* y, long long n, hipStream_t s) {
   if (n % 4) throw std::runtime_error("from_bf16: n % 4 != 0");
   from_bf16_kernel<<<grid_for(n / 4), 256, 0, s>>>(reinterpret_cast<const uint2*>(x),
                                                    reinterpret_cast<float4*>(y), n / 4);
+}
+
+void launch_hash_words(const uint32_t* x, long long n, unsigned long long* out, hipStream_t s) {
+  HIP_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned long long), s));
+  hash_words_kernel<<<grid_for(n / 4 + 1), 256, 0, s>>>(x, n, out);
 }
 
 void launch_scale(float* x, long long n, float a, hipStream_t s) {

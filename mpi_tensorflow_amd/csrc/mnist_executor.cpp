@@ -330,6 +330,9 @@ void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_
   sgd_range(cs, 0, p.bucket1, gscale, false);
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   fc_pending_ = true;
+  // host-progress communicators block a runtime thread per exchange: every
+  // rank must reach the FC exchange before the conv exchange (collective.h)
+  if (comm->host_progress() || comm2->host_progress()) wait_fc_params(s);
   reduce_bucket(comm2, p.bucket1, p.total - p.bucket1, s);
   sgd_range(s, p.bucket1, p.total, gscale, true);
 }

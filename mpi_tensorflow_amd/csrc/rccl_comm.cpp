@@ -2,6 +2,7 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <stdexcept>
@@ -109,6 +110,7 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::destroy() {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   ncclComm_t c = comm_.exchange(nullptr);
   if (c) check(g_api.commDestroy(c), "CommDestroy");
 }
@@ -120,6 +122,9 @@ void RcclComm::destroy() {
 // when a peer died or a collective overran its deadline.  Abort makes the
 // in-flight RCCL kernels exit, so the stuck synchronize returns.
 int RcclComm::async_error() const {
+  // never blocks the watchdog: a busy communicator reads as "in progress"
+  std::unique_lock<std::timed_mutex> lk(mu_, std::try_to_lock);
+  if (!lk.owns_lock()) return (int)ncclInProgress;
   ncclComm_t c = comm_.load();
   if (!c) return aborted_.load() ? (int)ncclRemoteError : (int)ncclSuccess;
   ncclResult_t e = ncclSuccess;
@@ -128,14 +133,17 @@ int RcclComm::async_error() const {
 }
 
 void RcclComm::abort() {
+  aborted_.store(true);
+  // a host call stuck inside RCCL must not keep the watchdog from exiting:
+  // after 3 s the process ends without the abort (its exit frees the GPU)
+  std::unique_lock<std::timed_mutex> lk(mu_, std::chrono::seconds(3));
+  if (!lk.owns_lock()) return;
   ncclComm_t c = comm_.exchange(nullptr);
-  if (c) {
-    aborted_.store(true);
-    (void)g_api.commAbort(c);
-  }
+  if (c) (void)g_api.commAbort(c);
 }
 
 int RcclComm::comm_count() const {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   ncclComm_t c = comm_.load();
   if (!c) throw std::runtime_error("RCCL communicator was destroyed or aborted");
   int n = 0;
@@ -156,28 +164,33 @@ ncclComm_t RcclComm::live() const {
 
 void RcclComm::all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
                           hipStream_t s) {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   check(g_api.allReduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, live(), s),
         "AllReduce");
 }
 
 void RcclComm::broadcast(const void* send, void* recv, size_t count, int dtype, int root,
                          hipStream_t s) {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   check(g_api.broadcast(send, recv, count, (ncclDataType_t)dtype, root, live(), s), "Broadcast");
 }
 
 void RcclComm::reduce(const void* send, void* recv, size_t count, int dtype, int op, int root,
                       hipStream_t s) {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   check(g_api.reduce(send, recv, count, (ncclDataType_t)dtype, (ncclRedOp_t)op, root, live(), s),
         "Reduce");
 }
 
 void RcclComm::all_gather(const void* send, void* recv, size_t send_count, int dtype,
                           hipStream_t s) {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   check(g_api.allGather(send, recv, send_count, (ncclDataType_t)dtype, live(), s), "AllGather");
 }
 
 void RcclComm::reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                               hipStream_t s) {
+  std::lock_guard<std::timed_mutex> lk(mu_);
   check(g_api.reduceScatter(send, recv, recv_count, (ncclDataType_t)dtype, (ncclRedOp_t)op, live(),
                             s),
         "ReduceScatter");

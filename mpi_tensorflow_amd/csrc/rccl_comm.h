@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -56,6 +57,12 @@ class RcclComm : public Collective {
 
  private:
   ncclComm_t live() const;
+  // Serialises every host call on the communicator against abort() /
+  // destroy() from the watchdog thread: a collective never runs on a handle
+  // that another thread is aborting or freeing.  abort() waits at most a few
+  // seconds for it (the watchdog must still reach its exit), async_error()
+  // not at all.
+  mutable std::timed_mutex mu_;
   std::atomic<ncclComm_t> comm_{nullptr};
   std::atomic<bool> aborted_{false};
   int nranks_ = 0, rank_ = 0;

@@ -11,6 +11,12 @@ Replaces the reference's host-staged, blocking mpi4py collectives
 * `TorchDeviceComm` - `torch.distributed` collectives (gloo for CPU tensors,
   an RCCL `nccl` group for GPU tensors).  Used for the CPU/gloo config and as
   the fallback if the native communicator cannot be created.
+* `ShmDeviceComm` - the native `_C.ShmComm`: host-staged collectives through
+  a shared-memory segment for ranks that share a GPU (the reference runs
+  every rank on /GPU:0, quirk Q13; RCCL refuses two ranks on one device).
+  Each collective is a D2H copy, a host function and an H2D copy on the
+  caller's stream, so it too is captured into the step's hipGraph and the
+  executors' captured sync schedules run unchanged.
 * world size 1 -> no communicator at all.
 
 ncclDataType / ncclRedOp enum values follow rccl.h.
@@ -19,6 +25,8 @@ ncclDataType / ncclRedOp enum values follow rccl.h.
 from __future__ import annotations
 
 import os
+import tempfile
+import uuid
 from typing import Optional
 
 import torch
@@ -166,6 +174,102 @@ class EmulatedDeviceComm(DeviceComm):
         return EmulatedDeviceComm(*self._args)
 
 
+DEFAULT_SHM_CAPACITY = 64 << 20  # bytes per rank and collective
+
+
+class ShmDeviceComm(DeviceComm):
+    """Shared-memory communicator (csrc/shm_comm.h) of the ranks on this
+    node.  Rank 0 creates the segment (in /dev/shm when it has room, else in
+    the temp directory), the others map it, then the file is unlinked (the
+    mappings stay: nothing is left behind).  Creation is voted over gloo, so
+    a rank that fails makes every rank raise instead of hanging.
+    `capacity` bounds the bytes one rank contributes to one collective."""
+
+    kind = "host-shm"
+
+    def __init__(self, di: DistInfo, capacity: int = DEFAULT_SHM_CAPACITY,
+                 timeout_s: float = 300.0):
+        C = native()
+        n = di.world
+        cap = int(capacity)
+        need = (n + 2) * cap + (1 << 20)
+        path = None
+        if di.rank == 0:
+            d = "/dev/shm"
+            try:
+                st = os.statvfs(d)
+                if st.f_bavail * st.f_frsize < 2 * need:
+                    d = tempfile.gettempdir()
+            except OSError:
+                d = tempfile.gettempdir()
+            path = os.path.join(d, f"mta-comm-{os.getpid()}-{uuid.uuid4().hex[:12]}")
+        objs = [path]
+        if n > 1:
+            dist.broadcast_object_list(objs, src=0)
+        path = objs[0]
+        self._c = None
+        err = None
+        if di.rank == 0:
+            try:
+                self._c = C.ShmComm(path, True, n, 0, cap, float(timeout_s))
+            except Exception as e:  # noqa: BLE001 - reported after the vote
+                err = e
+        if not _all_ranks_ok(err is None, n):
+            raise RuntimeError(f"shared-memory communicator unavailable (rank 0: {err!r})")
+        if di.rank != 0:
+            try:
+                self._c = C.ShmComm(path, False, n, di.rank, cap, float(timeout_s))
+            except Exception as e:  # noqa: BLE001
+                err = e
+        ok = _all_ranks_ok(err is None, n)
+        if di.rank == 0:
+            self._c.unlink_path()
+        if not ok:
+            raise RuntimeError(f"shared-memory communicator unavailable (here: {err!r})")
+        self.rank, self.size = di.rank, n
+        self._di, self._cap, self._timeout = di, cap, timeout_s
+        self.path = path
+
+    @property
+    def nranks(self) -> int:
+        return self.size
+
+    def duplicate(self):
+        return ShmDeviceComm(self._di, self._cap, self._timeout)
+
+    def _check(self, t: torch.Tensor):
+        if not t.is_cuda or not t.is_contiguous() or t.dtype not in _DT:
+            raise ValueError("shm comm needs a contiguous CUDA tensor of a supported dtype")
+
+    def all_reduce_(self, t, stream=None):
+        self._check(t)
+        self._c.all_reduce(ptr(t), ptr(t), t.numel(), _DT[t.dtype], NCCL_SUM, stream_handle(stream))
+        return t
+
+    def broadcast_(self, t, root=0, stream=None):
+        self._check(t)
+        self._c.broadcast(ptr(t), ptr(t), t.numel(), _DT[t.dtype], root, stream_handle(stream))
+        return t
+
+    def reduce_(self, t, root=0, stream=None):
+        self._check(t)
+        self._c.reduce(ptr(t), ptr(t), t.numel(), _DT[t.dtype], NCCL_SUM, root,
+                       stream_handle(stream))
+        return t
+
+    def all_gather(self, out, inp, stream=None):
+        self._check(out)
+        self._check(inp)
+        if out.numel() != inp.numel() * self.size:
+            raise ValueError("all_gather output must be world_size x input")
+        self._c.all_gather(ptr(inp), ptr(out), inp.numel(), _DT[inp.dtype], stream_handle(stream))
+        return out
+
+    @property
+    def native_handle(self):
+        return self._c
+
+
 class HostStagedComm(DeviceComm):
     """Test communicator: the native executors call back into Python for
     every collective, which synchronizes the device, stages the slice through
@@ -298,10 +402,25 @@ def _all_ranks_ok(ok: bool, world: int) -> bool:
     return bool(t.item())
 
 
-def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto") -> Optional[DeviceComm]:
-    """Communicator for `device`, or None at world size 1."""
+def ranks_share_gpus(di: DistInfo) -> bool:
+    """True when this node runs more ranks than it has GPUs (each rank binds
+    local_rank % device_count, parallel/dist.py), so RCCL cannot be used.
+    Decided from environment data only, identically on every rank."""
+    ndev = torch.cuda.device_count()  # does not initialise HIP on this image
+    return ndev > 0 and di.local_world > ndev
+
+
+def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto",
+              shm_capacity: int = DEFAULT_SHM_CAPACITY,
+              timeout_s: float = 300.0) -> Optional[DeviceComm]:
+    """Communicator for `device`, or None at world size 1.  prefer: auto |
+    rccl (alias native) | shm | torch (TrainConfig.comm)."""
     if di.world <= 1:
         return None
+    if device.type == "cuda" and (prefer == "shm" or (prefer == "auto" and ranks_share_gpus(di))):
+        return ShmDeviceComm(di, shm_capacity, timeout_s)
+    if prefer == "rccl":
+        prefer = "native"
     if device.type == "cuda" and prefer in ("auto", "native"):
         try:  # every rank takes the same branch: RcclDeviceComm votes first
             return RcclDeviceComm(di)

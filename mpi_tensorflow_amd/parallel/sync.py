@@ -22,6 +22,7 @@ from __future__ import annotations
 
 from typing import Iterable
 
+import numpy as np
 import torch
 
 from .comm import DeviceComm
@@ -50,6 +51,48 @@ def average_params_root_only(comm: DeviceComm, layout: FlatLayout, params: torch
             v.copy_(buf.view(v.shape) / comm.size)
 
 
-def replica_checksum(params: torch.Tensor) -> float:
-    """Cheap cross-replica consistency probe (sum of |w| in float64)."""
-    return float(params.detach().double().abs().sum().item())
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64_np(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def replica_hash(t: torch.Tensor) -> int:
+    """Bitwise replica fingerprint of a 32-bit tensor: sum over i (mod 2^64)
+    of splitmix64((i << 32) | raw_word_i).  Sensitive to every bit, to sign
+    flips and to permutations (position-keyed), exact (integer arithmetic).
+    GPU tensors hash on the device (csrc/kernels/sgd.hip hash_words_kernel,
+    one 8-byte read back); CPU tensors hash here with the same function."""
+    x = t.detach().contiguous().view(-1)
+    if x.element_size() != 4:
+        raise ValueError("replica_hash hashes 32-bit words")
+    if x.is_cuda:
+        from ..ops import native, ptr, stream_handle
+
+        out = torch.empty(1, dtype=torch.int64, device=x.device)
+        native().optim.hash_words(ptr(x), x.numel(), ptr(out), stream_handle())
+        return int(out.item()) & _M64
+    w = x.view(torch.int32).numpy().view(np.uint32).astype(np.uint64)
+    i = np.arange(w.size, dtype=np.uint64)
+    h = _splitmix64_np((i << np.uint64(32)) | w)
+    with np.errstate(over="ignore"):
+        return int(np.sum(h, dtype=np.uint64)) & _M64
+
+
+def replicas_identical(t: torch.Tensor) -> bool:
+    """True iff every rank's tensor hashes identically (gloo host group)."""
+    import torch.distributed as dist
+
+    h = replica_hash(t)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() <= 1:
+        return True
+    v = torch.tensor([h - (1 << 64) if h >= (1 << 63) else h], dtype=torch.int64)
+    lo, hi = v.clone(), v.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(lo.item() == hi.item())

@@ -21,8 +21,17 @@ job" semantics:
   bench.py's own spawner - then tears down the remaining ranks).
 
 Communicators are any objects with `async_error() -> int` and `abort()`
-(the native `_C.RcclComm`, or a fake in the CPU tests); others are ignored
-and only the deadline applies (gloo, emulated and host-staged comms).
+(the native `_C.RcclComm` and `_C.ShmComm`, or a fake in the CPU tests);
+others are ignored and only the deadline applies (gloo, emulated and
+host-staged comms).  The watchdog exists BEFORE the communicators: start-up
+(communicator creation, the engines' connection-setup collectives) runs
+under a deadline too, and communicators are registered with `add()` as they
+appear.
+
+The deadline is a heartbeat, not a budget for a whole run: `run_in_chunks`
+splits a long run of training steps into chunks, each armed on its own and
+sized from the measured step time to a fraction of the deadline, so a slow
+but progressing run is never declared hung.
 """
 
 from __future__ import annotations
@@ -58,6 +67,18 @@ class CollectiveWatchdog:
         self._thread = threading.Thread(target=self._run, name="collective-watchdog", daemon=True)
         self._thread.start()
 
+    def add(self, comm) -> None:
+        """Registers a communicator created after the watchdog (DeviceComm
+        wrappers are unwrapped to their native handle)."""
+        if comm is None:
+            return
+        h = getattr(comm, "native_handle", None)
+        c = h if h is not None else comm
+        if hasattr(c, "async_error") and hasattr(c, "abort"):
+            with self._lock:
+                if all(c is not o for o in self.comms):
+                    self.comms.append(c)
+
     # ---------------------------------------------------------------- arming
     def arm(self, what: str, timeout_s: Optional[float] = None) -> None:
         with self._lock:
@@ -84,13 +105,18 @@ class CollectiveWatchdog:
 
     # ---------------------------------------------------------------- thread
     def _check_async(self) -> Optional[str]:
-        for c in self.comms:
+        with self._lock:
+            comms = list(self.comms)
+        for c in comms:
             try:
                 e = int(c.async_error())
             except Exception as ex:  # a broken communicator is itself fatal
                 return f"async-error query failed ({ex})"
             if e not in (NCCL_SUCCESS, NCCL_IN_PROGRESS):
-                msg = self._describe(e) if self._describe else ""
+                if hasattr(c, "error_message"):  # shared-memory communicator
+                    msg = c.error_message()
+                else:
+                    msg = self._describe(e) if self._describe else ""
                 return f"RCCL asynchronous error {e}{' (' + msg + ')' if msg else ''}"
         return None
 
@@ -110,7 +136,9 @@ class CollectiveWatchdog:
         print(f"[rank {self.rank}] collective watchdog: {reason} during {what}; "
               f"aborting {len(self.comms)} communicator(s) and exiting with {EXIT_CODE}",
               file=sys.stderr, flush=True)
-        for c in self.comms:
+        with self._lock:
+            comms = list(self.comms)
+        for c in comms:
             try:
                 c.abort()
             except Exception:
@@ -127,6 +155,10 @@ class NullWatchdog:
 
     comms: List = []
     fired = None
+    timeout_s = float("inf")
+
+    def add(self, comm):
+        pass
 
     def arm(self, what, timeout_s=None):
         pass
@@ -139,6 +171,37 @@ class NullWatchdog:
 
     def stop(self):
         pass
+
+
+def run_in_chunks(wd, train: Callable[[int], None], sync: Callable[[], None], k: int,
+                  label: str, first_step: int = 0, granule: int = 1,
+                  state: Optional[dict] = None) -> None:
+    """Runs train(k) as consecutive train(n) + sync() chunks, each guarded by
+    its own deadline (a heartbeat).  The chunk length is a multiple of
+    `granule` (the engine's captured-graph length) sized so a chunk takes
+    about a quarter of the deadline at the step time measured so far
+    (`state["step_s"]`, carried across calls).  A hang is still caught
+    within one deadline; a long healthy run is never mistaken for one."""
+    st = state if state is not None else {}
+    g = max(1, int(granule))
+    budget = getattr(wd, "timeout_s", float("inf"))
+    done = 0
+    while done < k:
+        step_s = st.get("step_s")
+        if budget == float("inf"):  # nothing watches: one chunk
+            n = k - done
+        elif step_s is None:  # first chunk measures the step time
+            n = g
+        else:
+            n = max(g, int(0.25 * budget / max(step_s, 1e-9)) // g * g)
+        n = min(n, k - done)
+        s0 = first_step + done
+        t0 = time.monotonic()
+        with wd.guard(f"{label} {s0}..{s0 + n - 1}"):
+            train(n)
+            sync()
+        st["step_s"] = (time.monotonic() - t0) / n
+        done += n
 
 
 def make_watchdog(comms: Iterable, timeout_s: float, rank: int, world: int):

@@ -298,6 +298,7 @@ class NativeMnistEngine(MnistEngineBase):
                            and (self.exe.sharded_ok(self._native_comm.size)
                                 or self.exe.factors_ok(self._native_comm.size)))
         self.tune_log: Dict[str, float] = {}
+        self.tune_steps_run = 0
         self._eval_ws = None
         if self.grad_sync:  # connection setup of every collective used, outside any capture
             c, g, n, hs = self._native_comm, ptr(self.grads), lay.total, stream_handle()
@@ -385,17 +386,32 @@ class NativeMnistEngine(MnistEngineBase):
             self._graphs[key] = g
         return g
 
+    def _tune_candidates(self):
+        E = self._C.MnistExecutor
+        n = self._native_comm.size
+        cands = [(E.SCHED_BUCKETS, "buckets")]
+        if self.exe.sharded_ok(n):
+            cands.append((E.SCHED_SHARDED_FC, "sharded"))
+        # the factor schedule forms the FC gradients in another summation
+        # order: under --deterministic auto keeps to the bit-identical ones
+        if self.exe.factors_ok(n) and not self.cfg.deterministic:
+            cands.append((E.SCHED_FACTORS, "factors"))
+        return cands
+
     def tune_steps(self) -> int:
+        """Training steps tune_schedule() runs (and then discards)."""
         if self._tuned:
             return 0
-        n = self._native_comm.size
-        cands = 1 + int(self.exe.sharded_ok(n)) + int(self.exe.factors_ok(n))
-        return cands * (1 + TUNE_REPLAYS) * self.graph_steps
+        return len(self._tune_candidates()) * (1 + TUNE_REPLAYS) * self.graph_steps
 
     def tune_schedule(self) -> int:
         """Times TUNE_REPLAYS graph replays of each sync schedule (after one
-        untimed replay each) and keeps the faster; returns the number of
-        training steps it ran.  Collective over the ranks."""
+        untimed replay each) and keeps the fastest.  Side-effect free: the
+        params, momentum and device step are snapshotted first and restored
+        afterwards, so training continues exactly where it was (the trial
+        steps do not count towards `step`).  Collective over the ranks: all
+        ranks decide from the same max-over-ranks timings.  Returns the
+        number of trial steps run."""
         if self._tuned:
             return 0
         from ..parallel import dist as D
@@ -403,13 +419,9 @@ class NativeMnistEngine(MnistEngineBase):
         G = self.graph_steps
         steps = 0
         best = None
-        n = self._native_comm.size
-        cands = [(E.SCHED_BUCKETS, "buckets")]
-        if self.exe.sharded_ok(n):
-            cands.append((E.SCHED_SHARDED_FC, "sharded"))
-        if self.exe.factors_ok(n):
-            cands.append((E.SCHED_FACTORS, "factors"))
-        for sched, name in cands:
+        self.exe.join(stream_handle())
+        snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
+        for sched, name in self._tune_candidates():
             self._set_schedule(sched)
             g = self._graph(G, sticky=(sched == E.SCHED_BUCKETS))
             # the decision must be collective: a candidate any rank could not
@@ -435,19 +447,24 @@ class NativeMnistEngine(MnistEngineBase):
             if best is None or us < best[0]:
                 best = (us, sched)
         self._set_schedule(best[1] if best is not None else E.SCHED_BUCKETS)
+        self.exe.join(stream_handle())
+        self.params.copy_(snap[0])
+        self.mom.copy_(snap[1])
+        self.step_dev.copy_(snap[2])
+        torch.cuda.synchronize(self.device)
         self._tuned = True
-        self.step += steps
+        self.tune_steps_run = steps
         return steps
 
     def train(self, k: int) -> None:
         if k <= 0:
             return
+        if not self._tuned:  # side-effect free: restores the state it trained
+            self.tune_schedule()
         # bf16: the single-rank step's SGD writes the fc1 weight shadows the next
         # step reads, so re-derive them from the master weights before a run of
         # steps (picks up any change made to the weights since the last run)
         self.exe.refresh_shadows(stream_handle())
-        if not self._tuned and k >= self.tune_steps():
-            k -= self.tune_schedule()
         done = 0
         if self.use_graph:
             G = self.graph_steps

@@ -29,15 +29,31 @@ import torch
 from .. import config as C
 from ..parallel import dist as D
 from ..parallel.comm import make_comm
-from ..parallel.watchdog import make_watchdog
-from ..parallel.sync import average_params, average_params_root_only, replica_checksum
+from ..parallel.watchdog import make_watchdog, run_in_chunks
+from ..parallel.sync import average_params, average_params_root_only, replicas_identical
 from ..utils import checkpoint as ckpt_mod
 from ..utils.data import (data_exist_here, load_mnist_shard, local_train_rows, mnist_files_present,
                           steps_per_run, synthetic_image_shard)
 from ..utils.logging import MetricsWriter, emit, progress_line, start_line
 from ..ops import functional as Fn
 from ..utils.data import batch_offset
+from ..utils.faults import maybe_fail
 from ..utils.profiling import SegmentTimer
+
+
+def comm_capacity_bytes(cfg: C.TrainConfig) -> int:
+    """Largest per-rank contribution of one collective of this model's step
+    (the whole flat fp32 gradient / parameter buffer), rounded up to 1 MiB:
+    the capacity a shared-memory communicator needs."""
+    if cfg.model == "mnist_cnn":
+        from ..models import mnist_cnn as M
+
+        total = M.layout().total
+    else:
+        from ..models.generic import make_model
+
+        total = make_model(cfg.model).layout.total
+    return ((4 * total + (1 << 20) - 1) >> 20) << 20
 
 
 @dataclasses.dataclass
@@ -59,6 +75,7 @@ class RunSummary:
     engine: str
     comm: str
     synthetic: bool
+    sync_schedule: str = "n/a"
 
     def as_dict(self) -> Dict:
         return dataclasses.asdict(self)
@@ -70,17 +87,31 @@ class Trainer:
         self.device = D.resolve_device(cfg.device)
         self.di = di or D.init(str(self.device), timeout_s=cfg.collective_timeout_s)
         self.rank, self.world = self.di.rank, self.di.world
-        self._prepare_data()
-        self.comm = make_comm(self.di, self.device) if self.world > 1 else None
-        self.engine = self._make_engine()
+        maybe_fail("after_init", self.rank)
+        # the watchdog exists before any communicator: a peer that dies during
+        # start-up (communicator init, the engines' connection-setup
+        # collectives) ends every rank within the deadline instead of hanging
+        self.watchdog = make_watchdog([], cfg.collective_timeout_s, self.rank, self.world)
+        self._chunk_state: Dict = {}
+        with self.watchdog.guard("start-up (data, communicator, engine)"):
+            self._prepare_data()
+            maybe_fail("before_comm", self.rank)
+            self.comm = None
+            if self.world > 1:
+                self.comm = make_comm(self.di, self.device, cfg.comm,
+                                      shm_capacity=comm_capacity_bytes(cfg),
+                                      timeout_s=cfg.collective_timeout_s)
+            self.watchdog.add(self.comm)
+            maybe_fail("after_comm", self.rank)
+            self.engine = self._make_engine()
+            self.watchdog.add(getattr(self.engine, "comm2", None))
+            self._sync()
         if cfg.resume:
             step, _ = ckpt_mod.load(cfg.resume, self.engine.layout, self.engine.params,
                                     self.engine.mom, extra=self.engine.extra_state(),
                                     expect={"model": cfg.model, "world": self.world})
             self.engine.set_step(step)
         self.metrics = MetricsWriter(cfg.metrics_jsonl, self.rank)
-        self.watchdog = make_watchdog([self.comm, getattr(self.engine, "comm2", None)],
-                                      cfg.collective_timeout_s, self.rank, self.world)
 
     # ------------------------------------------------------------------ data
     def _prepare_data(self):
@@ -174,15 +205,30 @@ class Trainer:
         all-reduce; a mismatch means a lost / corrupted collective."""
         if self.world <= 1 or self.cfg.sync != "grad":
             return
-        c = replica_checksum(self.engine.params)
-        hi = D.allreduce_max_host(c)
-        lo = -D.allreduce_max_host(-c)
-        if hi != lo:
-            raise RuntimeError(f"replicas diverged at step {step}: checksum range [{lo}, {hi}]")
+        if not replicas_identical(self.engine.params):
+            raise RuntimeError(f"replicas diverged at step {step}: the bitwise weight "
+                               f"fingerprints differ between ranks")
+
+    def sync_schedule(self) -> str:
+        return getattr(self.engine, "sync_schedule", "n/a")
 
     def run(self) -> RunSummary:
+        try:
+            return self._run()
+        finally:
+            self.watchdog.stop()
+
+    def _run(self) -> RunSummary:
         cfg, eng = self.cfg, self.engine
         emit(start_line(self.rank), cfg.quiet)
+        # the gradient-sync schedule is chosen once, before training, exactly as
+        # bench.py does (the trial steps are discarded: params, momentum and
+        # step are restored), so mpipy and bench train with the same schedule
+        if hasattr(eng, "tune_schedule"):
+            with self.watchdog.guard("sync-schedule autotune"):
+                eng.tune_schedule()
+                self._sync()
+        maybe_fail("before_train", self.rank)
         steps = self.total_steps()
         s = eng.step
         train_t = 0.0
@@ -196,11 +242,10 @@ class Trainer:
             k = nxt - s + 1
             self._sync()
             t0 = time.perf_counter()
-            with self.watchdog.guard(f"train steps {s}..{s + k - 1}"):
-                timer.start()
-                eng.train(k)
-                timer.stop(k)
-                self._sync()
+            timer.start()
+            run_in_chunks(self.watchdog, eng.train, self._sync, k, "train steps", first_step=s,
+                          granule=getattr(eng, "graph_steps", 1), state=self._chunk_state)
+            timer.stop(k)
             timer.collect()
             train_t += time.perf_counter() - t0
             trained += k
@@ -216,6 +261,7 @@ class Trainer:
                 if last % (cfg.sync_every if cfg.reference_quirks else ev) == 0:
                     emit(progress_line(self.rank, last, err), cfg.quiet)
                     self.metrics.write(step=last, test_error=err, loss=eng.loss_value(),
+                                       sync_schedule=self.sync_schedule(),
                                        lr=eng.lr(last), train_seconds=train_t,
                                        device_step_ms=timer.step_ms(),
                                        images_per_sec=trained * cfg.batch_size / max(train_t, 1e-9))
@@ -250,18 +296,19 @@ class Trainer:
             final_test_error_local=final_err, final_test_error_global=100.0 * wrong_g / max(n_g, 1),
             final_loss=eng.loss_value(), final_lr=eng.lr(max(0, s - 1)),
             device_step_ms=timer.step_ms(), engine=eng.kind,
-            comm=getattr(self.comm, "kind", "none"), synthetic=self.shard.synthetic)
+            comm=getattr(self.comm, "kind", "none"), synthetic=self.shard.synthetic,
+            sync_schedule=self.sync_schedule())
         self.metrics.write(final=True, **summary.as_dict())
         if cfg.ckpt:
             self.save_checkpoint(cfg.ckpt)
         self.metrics.close()
-        self.watchdog.stop()
         return summary
 
     def save_checkpoint(self, path: str) -> None:
         self.engine.sync_optimizer_state()  # sharded FC momentum -> whole buffer
         if self.rank == 0:
             ckpt_mod.save(path, self.engine.layout, self.engine.params, self.engine.mom,
-                          self.engine.step, meta={"model": self.cfg.model, "world": self.world},
+                          self.engine.step, meta={"model": self.cfg.model, "world": self.world,
+                                                  "sync_schedule": self.sync_schedule()},
                           extra=self.engine.extra_state())
         D.barrier()

@@ -208,3 +208,82 @@ def test_lenet5_resume_then_param_avg_two_ranks(tmp_path):
                        "--resume", ck, "--check-replicas"])
     summ = json.loads([l for l in out.splitlines() if l.startswith('{"summary"')][-1])["summary"]
     assert summ["world"] == 2 and summ["steps"] == 21
+
+
+# ------------------------------------------------- heartbeat + start-up faults
+def test_run_in_chunks_slow_but_progressing_run_is_not_killed():
+    """A run far longer than the deadline, but progressing, is chunked into
+    separately armed regions and never declared hung (the old
+    trainer armed one deadline around a whole segment)."""
+    from mpi_tensorflow_amd.parallel.watchdog import run_in_chunks
+
+    codes = []
+    wd = CollectiveWatchdog([FakeComm()], timeout_s=0.4, poll_s=0.01, exit_fn=codes.append)
+    sizes = []
+
+    def train(n):
+        sizes.append(n)
+        time.sleep(0.02 * n)
+
+    t0 = time.monotonic()
+    run_in_chunks(wd, train, lambda: None, 90, "train steps", granule=2)
+    dt = time.monotonic() - t0
+    wd.stop()
+    assert dt > 1.5 and not codes and wd.fired is None, (dt, codes, wd.fired)
+    assert sum(sizes) == 90 and sizes[0] == 2
+    assert all(n % 2 == 0 for n in sizes[:-1]) and max(sizes) * 0.02 < 0.4
+
+
+def test_run_in_chunks_still_catches_a_hang():
+    from mpi_tensorflow_amd.parallel.watchdog import run_in_chunks
+
+    codes = []
+    wd = CollectiveWatchdog([FakeComm()], timeout_s=0.3, poll_s=0.01, exit_fn=codes.append)
+    state = {"step_s": 0.001}
+
+    def train(n):
+        time.sleep(1.0)  # one chunk that never finishes in time
+
+    run_in_chunks(wd, train, lambda: None, 10, "train steps", state=state)
+    assert codes == [EXIT_CODE] and "deadline" in wd.fired
+
+
+def _spawn_ranks(world, args, extra_env):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT, RANK=str(r),
+                   WORLD_SIZE=str(world), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **extra_env)
+        procs.append(subprocess.Popen([sys.executable, "mpipy.py"] + args, cwd=ROOT, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    return procs
+
+
+@pytest.mark.parametrize("mode", ["exit", "hang"])
+def test_peer_failure_during_startup_ends_every_rank(mode):
+    """Rank 1 dies (or hangs) right after the communicator is created, inside
+    the start-up region: every rank must exit non-zero within the deadline
+    (the watchdog exists before the communicator and guards start-up)."""
+    timeout = 8.0
+    t0 = time.monotonic()
+    procs = _spawn_ranks(2, ["--device", "cpu", "--max-steps", "30", "--eval-every", "0",
+                             "--quiet", "--collective-timeout-s", str(timeout)],
+                         {"MTA_FAULT": f"1:after_comm:{mode}"})
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=120)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise AssertionError("a rank hung after its peer failed")
+        outs.append((p.returncode, out))
+    dt = time.monotonic() - t0
+    assert all(rc != 0 for rc, _ in outs), outs
+    assert "MTA_FAULT" in outs[1][1]
+    if mode == "exit":
+        assert outs[1][0] == 99
+    else:
+        assert outs[1][0] == EXIT_CODE and "collective watchdog" in outs[1][1], outs[1]
+    assert dt < 60, dt
