@@ -109,14 +109,14 @@ def gpu_count_sysfs() -> int:
     return n
 
 
-def launch_ranks(n: int, argv) -> int:
+def launch_ranks(n: int, argv, share_gpus: bool = False) -> int:
     """Starts n rank processes of this script (no torchrun / mpirun in the
     environment).  The parent makes no HIP call at all (GPUs are counted from
     sysfs), so the children are fresh processes, not re-execs.  Rank 0's
     stdout (the JSON line) is inherited; the first failing rank makes the
     parent stop the others and return its exit code."""
     ndev = gpu_count_sysfs()
-    if 0 < ndev < n:
+    if 0 < ndev < n and not share_gpus:
         print(f"error: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
         return 2
     port = _free_port()
@@ -169,7 +169,8 @@ def main(argv=None) -> int:
     from mpi_tensorflow_amd.utils.faults import maybe_fail
 
     if a.gpus > 1 and D.discover().launcher == "none":
-        return launch_ranks(a.gpus, argv)
+        # --comm shm: ranks may share GPUs (rank r binds GPU r % count)
+        return launch_ranks(a.gpus, argv, share_gpus=a.comm == "shm")
     if D.discover().world != a.gpus:
         print(f"error: --gpus {a.gpus} but the launcher started {D.discover().world} rank(s)",
               file=sys.stderr)
@@ -305,9 +306,9 @@ def run(a, di, device, wd) -> int:
     else:
         model_desc = "resnet18 (BasicBlock [2,2,2,2], BatchNorm, 10 classes)"
         image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, class-conditional; random-init weights)"
-    rccl_nranks = comm.nranks if hasattr(comm, "nranks") else None
-    if rccl_nranks is not None and rccl_nranks != N:
-        print(f"error: RCCL communicator has {rccl_nranks} ranks, expected {N}", file=sys.stderr)
+    comm_nranks = comm.nranks if hasattr(comm, "nranks") else None  # as the library reports it
+    if comm_nranks is not None and comm_nranks != N:
+        print(f"error: the communicator has {comm_nranks} ranks, expected {N}", file=sys.stderr)
         return 3
     if di.rank == 0:
         out = {
@@ -335,7 +336,7 @@ def run(a, di, device, wd) -> int:
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
                 "ranks": N,
-                "rccl_nranks": rccl_nranks,
+                "comm_nranks": comm_nranks,
                 "sync_schedule": getattr(eng, "sync_schedule", "n/a"),
                 "grad_comm_dtype": a.grad_comm_dtype,
                 "sync_tune_us_per_step": getattr(eng, "tune_log", {}) or None,

@@ -38,6 +38,7 @@ from ..ops import native, ptr, stream_handle
 from ..parallel.comm import DeviceComm, all_reduce_grads_
 from ..parallel.overlap import BucketedAllReduce
 from ..utils.data import batch_offset
+from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
 
 
@@ -77,8 +78,10 @@ class GenericEngine:
         self.use_graph = cfg.graph and self.on_gpu
         self.graph_steps = max(1, cfg.graph_steps)
         self._graphs = {}
+        self._graph_loss = {}
         self._warm = False
         self.loss_buf = torch.zeros((), device=device)
+        self._eval_x = DeviceArrayCache()
         self.bucketer = None
         if self.on_gpu:
             self._C = native()
@@ -211,6 +214,9 @@ class GenericEngine:
                 torch.cuda.synchronize(self.device)
                 return None
             self._graphs[n] = g
+            # the loss tensor of the LAST step in this graph: its storage
+            # belongs to the graph and is rewritten by every replay
+            self._graph_loss[n] = self._loss_t
         return g
 
     def _warmup(self, k: int) -> int:
@@ -262,11 +268,13 @@ class GenericEngine:
             if g is not None:
                 for _ in range(full):
                     g.replay()
+                self._loss_t = self._graph_loss[G]
             else:
                 rem = left
             gr = self._graphs.get(rem) if (rem and self.use_graph) else None
             if gr is not None:  # remainder graph pre-captured by capture()
                 gr.replay()
+                self._loss_t = self._graph_loss[rem]
             else:
                 for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
                     self._step_gpu()
@@ -293,11 +301,8 @@ class GenericEngine:
         # kernel's argmax counter accumulates the correct predictions on the
         # device, so the whole evaluation ends in ONE 4-byte read
         Fn.set_conv_bf16(self.bf16)
-        key = (id(x), n)
-        if getattr(self, "_eval_cache", (None,))[0] != key:
-            self._eval_cache = (key, torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(self.device),
-                                torch.from_numpy(np.asarray(y).astype(np.int32)).to(self.device))
-        _, xd, yd = self._eval_cache
+        xd = self._eval_x.get(x, self.device)
+        yd = torch.from_numpy(np.asarray(y).astype(np.int32)).to(self.device)
         correct = torch.zeros(1, dtype=torch.int32, device=self.device)
         s = stream_handle()
         if self.wcache is not None:

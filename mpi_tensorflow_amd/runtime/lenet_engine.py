@@ -23,6 +23,7 @@ from .. import config as C
 from ..models.generic import make_model
 from ..ops import native, ptr, stream_handle
 from ..parallel.comm import DeviceComm
+from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
 
 _OFFSETS = (("c1w", "c1_w"), ("c1b", "c1_b"), ("c2w", "c2_w"), ("c2b", "c2_b"), ("f1w", "f1_w"),
@@ -58,6 +59,7 @@ class NativeLenetEngine:
         self.grads = torch.zeros(self.layout.total, device=dev)
         self.mom = torch.zeros(self.layout.total, device=dev)
         self.bn: Dict = {}
+        self._eval_x = DeviceArrayCache()
         self.train_x = torch.from_numpy(np.ascontiguousarray(train_x, np.float32)).to(dev)
         self.train_y = torch.from_numpy(np.asarray(train_y).astype(np.int32)).to(dev)
         self.step = 0
@@ -191,12 +193,8 @@ class NativeLenetEngine:
     def evaluate(self, x: np.ndarray, y: np.ndarray, chunk: int = 4096, dropout: bool = False,
                  return_logits: bool = False):
         n = int(x.shape[0])
-        key = (id(x), n)
-        if getattr(self, "_eval_cache", (None,))[0] != key:
-            self._eval_cache = (key,
-                                torch.from_numpy(np.ascontiguousarray(x, np.float32)).to(self.device),
-                                torch.from_numpy(np.asarray(y).astype(np.int32)).to(self.device))
-        _, xd, yd = self._eval_cache
+        xd = self._eval_x.get(x, self.device)
+        yd = torch.from_numpy(np.asarray(y).astype(np.int32)).to(self.device)
         errors = torch.zeros(1, dtype=torch.int32, device=self.device)
         logits = torch.empty(n, 10, device=self.device) if return_logits else None
         s = stream_handle()
