@@ -234,13 +234,18 @@ def run(a, di, device, wd) -> int:
             from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
             shape = model_input_shape(a.model)
-            rows = max(4 * a.batch_size, 8192 if a.model == "lenet5" else 4 * a.batch_size)
-            tx, ty = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
-            ex, ey = synthetic_images_torch(min(rows, 1024), shape, seed=cfg.seed, split="test",
-                                            start=di.rank * rows)
-            eng = make_image_engine(cfg, tx.numpy(), ty.numpy(), device, di.rank, N, comm,
-                                    force_sync=force)
-            test_x, test_y = ex.numpy(), ey.numpy()
+            if a.model == "lenet5":  # the Trainer's task (utils/data.py v2 design)
+                from mpi_tensorflow_amd.utils.data import synthetic_image_shard
+
+                sh = synthetic_image_shard(di.rank, N, 8192, 2048, shape, seed=cfg.seed)
+                tx, ty, test_x, test_y = sh.train_x, sh.train_y, sh.test_x, sh.test_y
+            else:
+                rows = max(4 * a.batch_size, 256)
+                txt, tyt = synthetic_images_torch(rows, shape, seed=cfg.seed, start=di.rank * rows)
+                ext, eyt = synthetic_images_torch(256, shape, seed=cfg.seed, split="test",
+                                                  start=di.rank * 256)
+                tx, ty, test_x, test_y = txt.numpy(), tyt.numpy(), ext.numpy(), eyt.numpy()
+            eng = make_image_engine(cfg, tx, ty, device, di.rank, N, comm, force_sync=force)
         wd.add(getattr(eng, "comm2", None))
 
     def sync():
@@ -302,10 +307,10 @@ def run(a, di, device, wd) -> int:
         image, data_desc = "28x28x1", "synthetic (MNIST-shaped 28x28x1, class-conditional; random-init weights)"
     elif a.model == "lenet5":
         model_desc = "lenet5 (conv5x5x6-pool-conv5x5x16-pool-fc120-fc84-fc10)"
-        image, data_desc = "32x32x3", "synthetic (CIFAR-shaped 32x32x3, class-conditional; random-init weights)"
+        image, data_desc = "32x32x3", "synthetic (CIFAR-shaped 32x32x3, shared-template task v2; random-init weights)"
     else:
         model_desc = "resnet18 (BasicBlock [2,2,2,2], BatchNorm, 10 classes)"
-        image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, class-conditional; random-init weights)"
+        image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, shared-template task v2; random-init weights)"
     comm_nranks = comm.nranks if hasattr(comm, "nranks") else None  # as the library reports it
     if comm_nranks is not None and comm_nranks != N:
         print(f"error: the communicator has {comm_nranks} ranks, expected {N}", file=sys.stderr)

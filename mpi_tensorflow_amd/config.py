@@ -93,6 +93,10 @@ class TrainConfig:
     # bf16 on the wire, the update stays fp32)
     grad_comm_dtype: str = "fp32"
     comm: str = "auto"
+    # fp32 MNIST conv2 algorithm on the native engine: "winograd" (F(2x2,5x5),
+    # kernels/wino.h; 2.8x fewer MFMAs, fp32 arithmetic throughout, ~1e-6
+    # relative error) or "direct" (25-tap implicit GEMM)
+    conv_algo: str = "winograd"
     # restrict sync_schedule="auto" to the schedules whose updates are bit
     # identical to the bucketed all-reduce (the factor schedule sums the FC
     # gradients in another order, so an auto run that picked it is only
@@ -142,6 +146,8 @@ class TrainConfig:
                              f"choose from {SYNC_SCHEDULES}")
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError(f"unknown grad comm dtype {self.grad_comm_dtype!r}")
+        if self.conv_algo not in ("winograd", "direct"):
+            raise ValueError(f"unknown conv algo {self.conv_algo!r}")
         if self.comm not in COMMS:
             raise ValueError(f"unknown comm {self.comm!r}; choose from {COMMS}")
         if self.dtype not in DTYPES:
@@ -198,6 +204,8 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--comm", default=d.comm, choices=COMMS,
                    help="device communicator: RCCL over xGMI (one GPU per rank), shm (host-"
                         "staged shared memory, ranks may share a GPU) or torch.distributed")
+    p.add_argument("--conv-algo", default=d.conv_algo, choices=("winograd", "direct"),
+                   help="fp32 MNIST conv2 algorithm of the native engine")
     p.add_argument("--deterministic", action="store_true",
                    help="sync-schedule auto-tune picks only bit-identical schedules")
     p.add_argument("--eval-every", type=int, default=d.eval_every,

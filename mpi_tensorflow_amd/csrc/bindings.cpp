@@ -89,16 +89,55 @@ PYBIND11_MODULE(_C, m) {
                              P<uint8_t>(idx2), P<float>(w2t), S(s));
     check_launch();
   });
+  k.def("conv12_fwd_wino", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
+                              uintptr_t b1, uintptr_t a1, uintptr_t a1pf, uintptr_t idx1,
+                              uintptr_t w2, uintptr_t U, uintptr_t b2, uintptr_t a2, uintptr_t idx2,
+                              uintptr_t w2t, uintptr_t s) {
+    mnist::C12In c;
+    c.data = P<const float>(data);
+    c.step = P<const long long>(step);
+    c.n_local = n_local;
+    c.w1 = P<const float>(w1);
+    c.b1 = P<const float>(b1);
+    c.a1 = P<float>(a1);
+    c.a1pf = P<float>(a1pf);
+    c.idx1 = P<uint8_t>(idx1);
+    mnist::launch_conv12_fwd_wino(c, batch, P<const float>(w2), P<const float>(U),
+                                  P<const float>(b2), P<float>(a2), P<uint8_t>(idx2),
+                                  P<float>(w2t), S(s));
+    check_launch();
+  });
   k.def("conv2_fwd", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t b, uintptr_t out,
                         uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
     mnist::launch_conv2_fwd(P<const float>(a1), batch, P<const float>(w), P<const float>(b),
                             P<float>(out), P<uint8_t>(argmax), P<float>(w2t), S(s));
     check_launch();
   });
+  k.def("conv2_wino_weights", [](uintptr_t w2, uintptr_t U, uintptr_t Ud, uintptr_t s) {
+    mnist::launch_conv2_wino_weights(P<const float>(w2), P<float>(U), P<float>(Ud), S(s));
+    check_launch();
+  });
+  k.def("conv2_fwd_wino", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t U, uintptr_t b,
+                             uintptr_t out, uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
+    mnist::launch_conv2_fwd_wino(P<const float>(a1), batch, P<const float>(w), P<const float>(U),
+                                 P<const float>(b), P<float>(out), P<uint8_t>(argmax),
+                                 P<float>(w2t), S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd_data_wino", [](uintptr_t dy2t, uintptr_t Ud, uintptr_t a1, int batch,
+                                  uintptr_t da1m, uintptr_t s) {
+    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2t), P<const float>(Ud), P<const float>(a1),
+                                      batch, P<float>(da1m), S(s));
+    check_launch();
+  });
   k.def("fc1_train_splits", &mnist::fc1_train_splits);
   k.def("conv2_filter_splits", &mnist::conv2_filter_splits);
-  k.def("conv1_filter_blocks", &mnist::conv1_filter_blocks);
+  k.def("conv1_filter_blocks", [](int batch, int split) {
+    return mnist::conv1_filter_blocks(batch, split);
+  }, py::arg("batch"), py::arg("split") = 7);
+  k.def("conv2_wino_filter_groups", &mnist::conv2_wino_filter_groups);
   k.def("part2_floats", &mnist::part2_floats);
+  k.def("part2_floats_wino", &mnist::part2_floats_wino);
   k.def("part1_floats", &mnist::part1_floats);
   k.def("fc1_part_floats", &mnist::fc1_part_floats);
   k.def("part2_floats_bf16", &mnist16::part2_floats);
@@ -151,6 +190,18 @@ PYBIND11_MODULE(_C, m) {
   k.def("conv2_bwd_filter", [](uintptr_t a1p, uintptr_t dy2, int batch, uintptr_t part2, uintptr_t s) {
     mnist::launch_conv2_bwd_filter(P<const float>(a1p), P<const float>(dy2), batch, P<float>(part2),
                                    S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd_filter_wino", [](uintptr_t a1p, uintptr_t dy2, int batch, uintptr_t part2,
+                                    uintptr_t s) {
+    mnist::launch_conv2_bwd_filter_wino(P<const float>(a1p), P<const float>(dy2), batch,
+                                        P<float>(part2), S(s));
+    check_launch();
+  });
+  k.def("conv2_bwd_filter_wino_prof", [](uintptr_t a1p, uintptr_t dy2, int batch, uintptr_t part2,
+                                         uintptr_t prof, uintptr_t s) {
+    mnist::launch_conv2_bwd_filter_wino_prof(P<const float>(a1p), P<const float>(dy2), batch,
+                                             P<float>(part2), P<unsigned long long>(prof), S(s));
     check_launch();
   });
   k.def("conv1_bwd_filter", [](uintptr_t data, uintptr_t step, int n_local, int batch,
@@ -394,7 +445,8 @@ PYBIND11_MODULE(_C, m) {
                               RW(l2) RW(momentum) RW(seed) RW(rank) RW(world) RW(bf16) RW(grad_bf16) RW(gb16)
                                   RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
                                       RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b) RW(a2_all)
-                                          RW(dh_all) RW(hd_all) RW(dlog_all) RW(fac_ranks);
+                                          RW(dh_all) RW(hd_all) RW(dlog_all) RW(fac_ranks)
+                                              RW(wino) RW(wino_u) RW(wino_ud);
 #undef RW
 
   py::class_<Collective>(m, "Collective")

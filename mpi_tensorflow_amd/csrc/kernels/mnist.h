@@ -63,6 +63,17 @@ void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float*
 // w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s);
+// Winograd F(2x2,5x5) conv2 (wino.h): transformed filters U [36][32][64] and,
+// when Ud != nullptr, Ud [36][64][32] of the rotated filter (bwd-data)
+void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t s);
+void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
+                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s);
+void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
+                           const float* b, float* out, uint8_t* argmax, float* w2t, hipStream_t s);
+// Winograd bwd-data: dy2t as for launch_conv2_bwd_data_l2, Ud from
+// launch_conv2_wino_weights; da1m = dA1 masked by a1 > 0
+void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
+                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
@@ -91,24 +102,39 @@ int conv2_filter_splits(int batch);
 // a1p: the zero-bordered NHWC pooled conv1 output [batch][18][18][32]
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
                              hipStream_t s, const C1FilterArgs* c1 = nullptr);
+// Winograd conv2 filter gradient: tap slabs part2 [groups of 2 images][800][64]
+// + db2 partials [4 groups][64], the layout of launch_conv2_bwd_filter with
+// conv2_wino_filter_groups(B) groups.  c1: the conv1 filter grad as
+// whole-image role blocks (conv1_filter_blocks(B, 1) partial rows).
+int conv2_wino_filter_groups(int batch);
+size_t part2_floats_wino(int batch);
+void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch, float* part2,
+                                  hipStream_t s, const C1FilterArgs* c1 = nullptr);
+// phase timing of the above (s_memtime per wave, [blocks][waves][5]); labs only
+void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,
+                                       float* part2, unsigned long long* prof, hipStream_t s);
 // L2-direct bwd-data (the one the executor uses): dy2t from launch_fc1_bwd,
 // w2t from launch_conv2_fwd; batch % 8 == 0
 void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* a1, int batch,
                               float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr);
 
 
-int conv1_filter_blocks(int batch);
+// conv1 filter-grad units: batch * split (split 7: pooled-row pairs, the
+// default; split 1: whole images, the Winograd conv2 filter launch's roles)
+int conv1_filter_blocks(int batch, int split = 7);
 void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s);
 // world-1 step: grad_finalize fused into the momentum SGD (FC bucket from the
 // flat grads [0, fc_end) with L2 on all of it, conv grads straight from the
-// slabs); bumps *step
+// slabs); bumps *step.  wino_u / wino_ud (optional): also writes the Winograd
+// transforms of the updated conv2 filters (launch_conv2_wino_weights layouts)
 void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s, bool fc_done = false);
+                         const float* lr, long long* step, hipStream_t s, bool fc_done = false,
+                         float* wino_u = nullptr, float* wino_ud = nullptr);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

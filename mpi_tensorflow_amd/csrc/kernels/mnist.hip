@@ -30,6 +30,7 @@
 #include "gemm_core.h"
 #include "mnist.h"
 #include "mnist_shared.h"
+#include "wino.h"
 
 namespace mnist {
 
@@ -451,10 +452,6 @@ __device__ __forceinline__ void fc1_bwd_dx(int L, const float* __restrict__ a2,
 #pragma unroll
   for (int k = 0; k < 16; ++k) TA[k * 64 + lane] = c0[k] + c1[k];
   __syncthreads();
-  if (dy2 == nullptr) {  // profiling variant (roles bit 3): no scatter epilogue
-    if (smem[lane] == 12345.f) smem[64 + lane] = 0.f;
-    return;
-  }
   const int co = fi & 63, pp = fi >> 6, py = pp / 7, px = pp % 7;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -527,14 +524,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   const int role = L < n_dx ? 0 : (L < n_dx + FC1BWD_DW_BLOCKS ? 1 : 2);
   if (!((roles >> role) & 1)) return;
   if (L < n_dx) {
-    if (roles & 8) {  // profiling: dX without the scatter epilogue
-      fc1_bwd_dx(L, a2, idx2, dh, w1, batch, nullptr, nullptr, smem);
-      return;
-    }
-    if (roles & 16) {  // profiling: dX without the channel-major dY2t copy
-      fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, nullptr, smem);
-      return;
-    }
     fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, dy2t, smem);
   } else if (L < n_dx + FC1BWD_DW_BLOCKS) {
     fc1_bwd_dw(L - n_dx, a2, dh, batch, g_w3);
@@ -595,6 +584,8 @@ constexpr int C12_IMG_ROWS = 20, C12_IMG_LD = 33;
 // it owns (4 pg .. 4 pg + 3) to a1 / a1pf / idx1 for the backward pass.  Same
 // GEMM view as conv_pool_fwd_kernel: M = pre-pool pixels (window, quadrant),
 // N = 32 channels, K = 25 taps (-> 32), one 32 x 32 MFMA tile per 8 windows.
+// NT: block size (256 or 512); the conv1 MFMA tiles run on waves 0-3 only
+template <int NT = 256>
 __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int n, int pg,
                                                 float* __restrict__ xs, float* __restrict__ img) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -602,10 +593,11 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
   const float* xin = c1.data + (off + n) * 784;
   const int iy0 = 8 * pg - 6;
   constexpr int NIMG = C12_IMG_ROWS * C12_IMG_LD;  // 660
-  float iv[3];
+  constexpr int NJ = (NIMG + NT - 1) / NT;
+  float iv[NJ];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int i = tid + 256 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int i = tid + NT * j;
     const int r = i / C12_IMG_LD, c = i % C12_IMG_LD, iy = iy0 + r, ix = c - 2;
     const bool ok = i < NIMG && iy >= 0 && iy < 28 && ix >= 0 && ix < 28;
     const float v = xin[min(max(iy, 0), 27) * 28 + min(max(ix, 0), 27)];
@@ -620,13 +612,14 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
     wb[st] = k < 25 ? v : 0.f;
   }
   const float bias = c1.b1[co];
-  for (int i = tid; i < C2_XS; i += 256) xs[i] = 0.f;
+  for (int i = tid; i < C2_XS; i += NT) xs[i] = 0.f;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int i = tid + 256 * j;
+  for (int j = 0; j < NJ; ++j) {
+    const int i = tid + NT * j;
     if (i < NIMG) img[i] = iv[j];
   }
   __syncthreads();
+  if (wave >= 4) return;  // the tile loop below is laid out for 4 waves
   const int y0 = 4 * pg - 2;  // a1 row of halo row 0
   const int ya = max(y0, 0), yb = min(y0 + C2_XS_ROWS, 14);
   const int nwin = (yb - ya) * 14, ntile = (nwin + 7) / 8;
@@ -792,6 +785,639 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
   }
 }
 
+
+// ------------------------------------- conv2 forward, Winograd F(2x2,5x5) ----
+// Transformed filters (wino.h), stored in MFMA fragment order so that one
+// 16x16x4 B fragment is 256 contiguous bytes and a point's fragments sit at
+// small immediate offsets from one base (p = 6 a + b):
+//   U  (forward, K = ci, N = co):  [p][s = ci/4][q = co/16][ci%4][co%16]
+//   Ud (bwd-data, rotated filter, K = co, N = ci): [p][s = co/4][q = ci/16][co%4][ci%16]
+// One thread per (ci, co); both written from the same 25 loads.
+__host__ __device__ __forceinline__ int wino_u_index(int p, int ci, int co) {
+  return (((p * 8 + (ci >> 2)) * 4 + (co >> 4)) * 4 + (ci & 3)) * 16 + (co & 15);
+}
+__host__ __device__ __forceinline__ int wino_ud_index(int p, int ci, int co) {
+  return (((p * 16 + (co >> 2)) * 2 + (ci >> 4)) * 4 + (co & 3)) * 16 + (ci & 15);
+}
+__global__ __launch_bounds__(256) void conv2_wino_weights_kernel(const float* __restrict__ w2,
+                                                                 float* __restrict__ U,
+                                                                 float* __restrict__ Ud) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // ci * 64 + co
+  if (i >= 2048) return;
+  const int ci = i >> 6, co = i & 63;
+  float g[25], r[25], u[36];
+#pragma unroll
+  for (int t = 0; t < 25; ++t) g[t] = w2[t * 2048 + i];  // HWIO (t, ci, co)
+  wino::filter_tile(g, u);
+#pragma unroll
+  for (int p = 0; p < 36; ++p) U[wino_u_index(p, ci, co)] = u[p];
+  if (Ud) {
+#pragma unroll
+    for (int t = 0; t < 25; ++t) r[t] = g[24 - t];
+    wino::filter_tile(r, u);
+#pragma unroll
+    for (int p = 0; p < 36; ++p) Ud[wino_ud_index(p, ci, co)] = u[p];
+  }
+}
+
+// Output-transform weights per point: kWinoCoef[p][i * 2 + j]
+struct WinoCoef {
+  float c[36][4];
+};
+__host__ __device__ constexpr WinoCoef make_wino_coef() {
+  WinoCoef w{};
+  for (int p = 0; p < 36; ++p)
+    for (int o = 0; o < 4; ++o) w.c[p][o] = wino::out_coef(p / 6, p % 6, o >> 1, o & 1);
+  return w;
+}
+__constant__ WinoCoef kWinoCoef = make_wino_coef();
+
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// conv2 forward + bias + ReLU + 2x2 maxpool (+argmax) by Winograd F(2x2,5x5).
+// Block = (image, pair of pooled rows) as conv2_fwd_v3_kernel: 14 pool
+// windows = 14 Winograd tiles (M padded to 16).  Phases:
+//   1. a1 halo tile in LDS (FUSED: conv1 recomputed into it, conv1_into_halo)
+//   2. input transform: V[p][ci][tile] (36 x 32 x 16 floats) in LDS
+//   3. 36 batched products [16 tiles x 32 ci] x [32 ci x 64 co] on
+//      v_mfma_f32_16x16x4_f32; wave w owns points w, w+4, ..., each folded
+//      into the four 2x2 outputs right after its 8 k-steps (the output
+//      transform is linear), B = U[p] straight from L2, one point ahead
+//   4. the four waves' partial outputs summed through LDS in wave order,
+//      then bias + ReLU + pool + argmax per (tile, co)
+// FLOP per image: 36 x 49 x 32 x 64 x 2 = 7.2 M (direct: 20.1 M).
+constexpr int WV_FLOATS = 36 * 32 * 16;  // V image; reused for the cross-wave sums
+
+// 512 threads = 8 waves, two per SIMD: the transform runs one item per thread
+// and each SIMD interleaves two waves' MFMA streams (waves 0-3 own 5 points,
+// waves 4-7 own 4).  B fragments of the next point are loaded into the other
+// of two register sets while the current point's MFMAs run.
+constexpr int WNT = 512, WNW = WNT / 64;
+
+// one point's 32 MFMAs (8 k-steps x 4 co quarters), folded into the outputs
+__device__ __forceinline__ void wino_fwd_point(int p, const float* __restrict__ V, int lane,
+                                               const float (&b)[32], f32x4 (&y)[4][4]) {
+  float av[8];
+  const float* vp = V + p * 512 + lane;  // (p * 32 + 4 s + kq) * 16 + r16
+#pragma unroll
+  for (int s = 0; s < 8; ++s) av[s] = vp[s * 64];
+  f32x4 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(av[s], b[s * 4 + q], acc[q]);
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const float c = kWinoCoef.c[p][o];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[o][q] += c * acc[q];
+  }
+}
+
+// ub = U + lane offset; fragment (s, q) of point p is the 64 floats at
+// (32 p + 4 s + q) * 64: one base per point, immediate offsets
+__device__ __forceinline__ void wino_fwd_loadb(int p, const float* __restrict__ ub,
+                                               float (&b)[32]) {
+  const float* bp = ub + p * 2048;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) b[j] = bp[j * 64];
+}
+
+// halo image rows: the 8 of the block's windows + 6 zero rows that the two
+// padding tiles (14, 15) transform (zeros in, zeros out: no selects)
+constexpr int WX_ROWS = C2_XS_ROWS + 6, WX_FLOATS = WX_ROWS * C2_XS_COLS * 33;
+
+template <bool FUSED>
+__global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
+    const float* __restrict__ a1, int batch, const float* __restrict__ w2,
+    const float* __restrict__ U, const float* __restrict__ b2, float* __restrict__ out,
+    uint8_t* __restrict__ argmax, float* __restrict__ w2t, const C12In c1) {
+  __shared__ float xs[WX_FLOATS];
+  __shared__ float img[FUSED ? C12_IMG_ROWS * C12_IMG_LD : 1];
+  __shared__ float V[WV_FLOATS];
+  const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform in an SGPR: the point index p, its output-transform weights
+  // (scalar loads) and the fragment bases are then scalar
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (w2t) {  // W2T[t][co][ci] for the direct bwd-data kernel: 51200 floats over all blocks
+    for (int i = blockIdx.x * WNT + tid; i < 51200; i += gridDim.x * WNT) {
+      const int ci = i & 31, co = (i >> 5) & 63, t = i >> 11;
+      w2t[i] = w2[(t * 32 + ci) * 64 + co];
+    }
+  }
+  for (int i = C2_XS + tid; i < WX_FLOATS; i += WNT) xs[i] = 0.f;
+  if constexpr (FUSED) {
+    conv1_into_halo<WNT>(c1, batch, n, pg, xs, img);
+  } else {
+    constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 32 / WNT;  // 9
+    float sv[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + WNT * j;
+      const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
+      const int y = 2 * pr0 - 2 + r, x = c - 2;
+      const bool ok = y >= 0 && y < 14 && x >= 0 && x < 14;
+      const float v = a1[((n * 14 + min(max(y, 0), 13)) * 14 + min(max(x, 0), 13)) * 32 + ci];
+      sv[j] = ok ? v : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int i = tid + WNT * j;
+      const int ci = i & 31, c = (i >> 5) % C2_XS_COLS, r = (i >> 5) / C2_XS_COLS;
+      xs[(r * C2_XS_COLS + c) * 33 + ci] = sv[j];
+    }
+  }
+  __syncthreads();
+  // 2. input transform, one (ci, tile) item per thread.  Tile t = (pooled row
+  // 2 pg + t / 7, col t % 7): its 6x6 window starts at halo row 2 (t / 7),
+  // halo col 2 (t % 7).  Tiles 14, 15 are zero.
+  {
+    const int t = tid & 15, ci = tid >> 4;
+    float d[36], v[36];
+    const int r0 = t < 14 ? 2 * (t / 7) : C2_XS_ROWS, c0 = t < 14 ? 2 * (t % 7) : 0;
+    const float* src = xs + (r0 * C2_XS_COLS + c0) * 33 + ci;
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+      for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[(yy * C2_XS_COLS + xx) * 33];
+    wino::input_tile(d, v);
+    float* vp = V + ci * 16 + t;
+#pragma unroll
+    for (int p = 0; p < 36; ++p) vp[p * 512] = v[p];
+  }
+  __syncthreads();
+  // 3. batched products.  16x16x4 fragment maps: A lane l = V[tile l & 15][ci
+  // 4 s + l >> 4]; B lane l = U[ci 4 s + l >> 4][co 16 q + l & 15]; C lane l,
+  // reg j = (tile 4 (l >> 4) + j, co 16 q + l & 15).
+  f32x4 y[4][4];  // [output i*2+j][co quarter]
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) y[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* ub = U + lane;  // kq * 16 + r16
+  // points wave, wave + 8, ... (5 for waves 0-3, 4 for waves 4-7), fully
+  // unrolled with two register sets: the B fragments of point i + 1 are
+  // issued before point i's MFMAs (sched barriers keep that order)
+  // The next point's loads are unconditional (clamped index): a load under a
+  // branch makes the waitcnt pass count for the path without it, and every
+  // MFMA of the point would then wait for the prefetch.
+  float bA[32], bB[32];
+  wino_fwd_loadb(wave, ub, bA);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int p = wave + WNW * i;
+    float(&cur)[32] = (i & 1) ? bB : bA;
+    float(&nxt)[32] = (i & 1) ? bA : bB;
+    if (i < 4) wino_fwd_loadb(min(p + WNW, 35), ub, nxt);
+    __builtin_amdgcn_sched_barrier(0);
+    if (p < 36) wino_fwd_point(p, V, lane, cur, y);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // 4. cross-wave sums in a fixed order: waves 4-7 hand their partials to
+  // waves 0-3 (slot = wave & 3), which add them and publish the pair sums
+  __syncthreads();  // every wave is done reading V
+  float* R = V;     // [slot][o][q][reg][lane] = 4 x 4 x 4 x 4 x 64 floats
+  const int slot = wave & 3;
+  auto rix = [&](int sl, int o, int q, int j) { return (((sl * 4 + o) * 4 + q) * 4 + j) * 64; };
+  if (wave >= 4) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[rix(slot, o, q, j) + lane] = y[o][q][j];
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float* r = R + rix(slot, o, q, j) + lane;
+          *r = y[o][q][j] + *r;
+        }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 1024 / WNT; ++e) {
+    const int item = tid + WNT * e, co = item & 63, t = item >> 6;  // (tile, co)
+    if (t >= 14) continue;
+    const int q = co >> 4, l = (t >> 2) * 16 + (co & 15), j = t & 3;
+    float v[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
+      v[o] = sum;
+    }
+    float m = v[0];
+    int qq = 0;
+#pragma unroll
+    for (int o = 1; o < 4; ++o) {
+      if (v[o] > m) {  // strict: first max wins (TF MaxPool order)
+        m = v[o];
+        qq = o;
+      }
+    }
+    const int pr = pr0 + t / 7, pc = t % 7;
+    if (pr < 7) {
+      const int oi = ((n * 7 + pr) * 7 + pc) * 64 + co;
+      out[oi] = fmaxf(m + b2[co], 0.f);
+      if (argmax) argmax[oi] = (uint8_t)qq;
+    }
+  }
+}
+
+// ------------------------------------ conv2 bwd-data, Winograd F(2x2,5x5) ----
+// dA1 = dY2 (x) rot180(W2) with the channel roles swapped: the forward form
+// on the zero-bordered channel-major dY2 image dy2t [n][64][18][MNIST32_T_LD]
+// (written by fc1 backward) with the filters Ud [36][64][32].  Block = (image,
+// pair of 2x2-tile rows) = 14 tiles (M 16), N = 32 input channels of conv2,
+// K = 64 in two halves of 32 (the transformed image V is 72 KB per half).
+// Epilogue: the ReLU1 mask (a1 > 0), NHWC da1m.  Optional FC SGD role blocks
+// (single rank) as in conv2_bwd_data_l2_kernel.
+__device__ __forceinline__ void wino_bwd_point(int p, const float* __restrict__ V, int lane,
+                                               const float (&b)[16], f32x4 (&y)[4][2]) {
+  float av[8];
+  const float* vp = V + p * 512 + lane;
+#pragma unroll
+  for (int s = 0; s < 8; ++s) av[s] = vp[s * 64];
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) acc[q] = mfma16x16x4(av[s], b[s * 2 + q], acc[q]);
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const float c = kWinoCoef.c[p][o];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) y[o][q] += c * acc[q];
+  }
+}
+
+// ub = Ud + lane offset + this K half; fragment (s, q) of point p at
+// ((16 p + s) * 2 + q) * 64
+__device__ __forceinline__ void wino_bwd_loadb(int p, const float* __restrict__ ub,
+                                               float (&b)[16]) {
+  const float* bp = ub + p * 2048;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) b[j] = bp[j * 64];
+}
+
+__global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
+    const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
+    int batch, float* __restrict__ da1m, const FcSgd sgd) {
+  __shared__ float V[WV_FLOATS];
+  const int nconv = gridDim.x - sgd.nblk / 2;
+  if ((int)blockIdx.x >= nconv) {  // 512-thread blocks: two 256-thread role units
+    fc_sgd_role(sgd, 2 * (blockIdx.x - nconv) + (threadIdx.x >> 8), nullptr, threadIdx.x & 255);
+    return;
+  }
+  const int n = blockIdx.x >> 2, pg = blockIdx.x & 3;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave-uniform in an SGPR: the point index p, its output-transform weights
+  // (scalar loads) and the fragment bases are then scalar
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  f32x4 y[4][2];
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) y[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int half = 0; half < 2; ++half) {
+    {  // input transform of channels 32 half .. 32 half + 31 straight from L2
+      const int t = tid & 15, c = tid >> 4;
+      const int tr = 2 * pg + t / 7, tc = t % 7;
+      const bool ok = t < 14 && tr < 7;
+      const float* src = dy2t + ((size_t)(n * 64 + 32 * half + c) * 18 + 2 * (ok ? tr : 0)) *
+                                    MNIST32_T_LD + 2 * (ok ? tc : 0);
+      float d[36], v[36];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[yy * MNIST32_T_LD + xx];
+      wino::input_tile(d, v);
+#pragma unroll
+      for (int p = 0; p < 36; ++p) V[(p * 32 + c) * 16 + t] = ok ? v[p] : 0.f;
+    }
+    __syncthreads();
+    const float* ub = Ud + half * 1024 + lane;  // s in [8 half, 8 half + 8)
+    float bA[16], bB[16];
+    wino_bwd_loadb(wave, ub, bA);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {  // unconditional clamped prefetch, as in the forward
+      const int p = wave + WNW * i;
+      float(&cur)[16] = (i & 1) ? bB : bA;
+      float(&nxt)[16] = (i & 1) ? bA : bB;
+      if (i < 4) wino_bwd_loadb(min(p + WNW, 35), ub, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      if (p < 36) wino_bwd_point(p, V, lane, cur, y);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();  // V is rewritten by the next half / the reduction
+  }
+  float* R = V;  // [slot][o][q][reg][lane] = 4 x 4 x 2 x 4 x 64 floats
+  const int slot = wave & 3;
+  auto rix = [&](int sl, int o, int q, int j) { return (((sl * 4 + o) * 2 + q) * 4 + j) * 64; };
+  if (wave >= 4) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) R[rix(slot, o, q, j) + lane] = y[o][q][j];
+  }
+  __syncthreads();
+  if (wave < 4) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float* r = R + rix(slot, o, q, j) + lane;
+          *r = y[o][q][j] + *r;
+        }
+  }
+  __syncthreads();
+  {
+    const int ci = tid & 31, t = tid >> 5;
+    const int tr = 2 * pg + t / 7, tc = t % 7;
+    if (t < 14 && tr < 7) {
+      const int q = ci >> 4, l = (t >> 2) * 16 + (ci & 15), j = t & 3;
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        float sum = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
+        const size_t oi =
+            ((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci;
+        da1m[oi] = a1[oi] > 0.f ? sum : 0.f;
+      }
+    }
+  }
+}
+
+// ------------------------------------------ Winograd conv2 bwd-filter ----
+// dW2 = G^T [ sum_tiles V (.) (AT^T dY AT) ] G per (ci, co) - the gradient of
+// the forward transform in wino.h: for each of the 36 points p = (a, b) the
+// product M_p[ci][co] = sum_tiles V_p[tile][ci] dY'_p[tile][co] is a GEMM
+// over the tiles (2.78x fewer MFMAs than the 25-tap form), dY' = AT^T dY AT of
+// the tile's 2x2 pre-pool gradient (dy2).  Block = (group of 2 images, 16 ci,
+// 16 co) and all 36 points, so the output transform runs in-block and the
+// partials are ordinary tap slabs part2[g][t][ci][co] (grad_finalize /
+// sgd_finalize unchanged).  12 waves = (point row a, half of the tile rows):
+// three per SIMD, so each SIMD's matrix pipe interleaves three MFMA streams
+// (6 waves, one per row, measured 19-28 K cycles in the main loop: 1.5 waves
+// per SIMD left the pipe idle behind each wave's LDS -> VALU -> MFMA chain):
+//   1. the group's a1 (16 ci, zero border) and dY2 (16 co) slices -> LDS, one
+//      round of float4 loads
+//   2. the MFMA k index runs over tiles as (row set m, column tx, quad kq):
+//      lane quad kq walks tile row 4 m + kq from tx = 0 to 6 (the wave's half:
+//      row sets 2 h, 2 h + 1), so the column
+//      transform slides - each step reads only the 2 new columns (5 nonzero
+//      BT rows, one ds_read_b64 each) - then the row transform gives the 6
+//      points' V, two ds_read_b64 give the 2x2 dY -> dY' (row a), and 6
+//      v_mfma_f32_16x16x4_f32 run (points (a, 0..5)); 14 k-steps, no
+//      staging buffers and no barriers in the loop.  The compiler pairs the
+//      b64 reads into ds_read2_b64 (16-lane bank groups, 32 banks): a row of
+//      18 floats per channel puts the 16 channels' pairs on distinct banks
+//      (a 20-float row measured 1,446 conflict cycles per wave)
+//   3. S_ah[kw] = sum_b G[b][kw] M_h[a][b] per wave -> LDS, then dW[kh][kw] =
+//      sum_a G[a][kh] (S_a0 + S_a1)[kw] (no FMA contraction) -> part2; the ci-tile-0
+//      blocks also write the group's db2 partial
+// The conv1 filter grad runs as whole-image role blocks after the conv2
+// blocks.
+constexpr int WF_IMG = 2, WF_ROWS = 7 * WF_IMG, WF_SETS = (WF_ROWS + 3) / 4;
+constexpr int WF_NT = 768;
+constexpr int WF_XLD = 18;                        // floats per (image row, ci)
+constexpr int WF_XS = WF_IMG * 18 * 16 * WF_XLD;  // [img][row][ci][col]
+constexpr int WF_DLD = 18;                        // floats per (dY row, co): 14 + 4
+constexpr int WF_DS = WF_IMG * 14 * 16 * WF_DLD;  // [img][row][co][col]
+constexpr int WF_SMEM = WF_XS + WF_DS;
+static_assert(6 * 2 * 5 * 4 * 64 <= WF_SMEM, "S_ah reduction reuses the slices");
+
+template <int A>
+__device__ __forceinline__ void wino_wgrad_row(const float* __restrict__ xs,
+                                               const float* __restrict__ dys, int nimg,
+                                               int lane, int half, f32x4 (&acc)[6]) {
+  const int kq = lane >> 4, ch = lane & 15;
+  constexpr float al0 = wino::kAT[0][A], al1 = wino::kAT[1][A];
+#pragma unroll 1
+  for (int m = half * (WF_SETS / 2); m < (half + 1) * (WF_SETS / 2); ++m) {
+    const int R = 4 * m + kq, Rc = min(R, WF_ROWS - 1);
+    const int img = Rc / 7, ty = Rc - 7 * img;
+    const bool ok = R < WF_ROWS && img < nimg;  // pad rows: dY' = 0
+    const float* xrow = xs + ((img * 18 + 2 * ty) * 16 + ch) * WF_XLD;
+    const float* drow = dys + ((img * 14 + 2 * ty) * 16 + ch) * WF_DLD;
+    // column pair pc of the window: t[c] = sum_i BT[A][i] x[2 ty + i][2 pc + c]
+    auto colpair = [&](int pc, float& c0, float& c1) {
+      c0 = 0.f;
+      c1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        if (wino::kBT[A][i] == 0.f) continue;
+        const float2 x = *reinterpret_cast<const float2*>(xrow + i * 16 * WF_XLD + 2 * pc);
+        c0 += wino::kBT[A][i] * x.x;
+        c1 += wino::kBT[A][i] * x.y;
+      }
+    };
+    float t[6];
+    colpair(0, t[0], t[1]);
+    colpair(1, t[2], t[3]);
+#pragma unroll
+    for (int tx = 0; tx < 7; ++tx) {
+      if (tx > 0) {
+        t[0] = t[2];
+        t[1] = t[3];
+        t[2] = t[4];
+        t[3] = t[5];
+      }
+      colpair(tx + 2, t[4], t[5]);
+      float v[6];
+      wino::bt6<1, 1>(t, v);
+      const int ds = 2 * tx;
+      const float2 d0 = *reinterpret_cast<const float2*>(drow + ds);
+      const float2 d1 = *reinterpret_cast<const float2*>(drow + 16 * WF_DLD + ds);
+      float r0 = al0 * d0.x + al1 * d1.x, r1 = al0 * d0.y + al1 * d1.y;
+      r0 = ok ? r0 : 0.f;
+      r1 = ok ? r1 : 0.f;
+      const float u[6] = {r0, r0 + r1, r0 - r1, r0 + 2.f * r1, r0 - 0.5f * r1, r1};
+#pragma unroll
+      for (int b = 0; b < 6; ++b) acc[b] = mfma16x16x4(v[b], u[b], acc[b]);
+    }
+  }
+}
+
+// PROF: per-wave s_memtime stamps at the phase boundaries -> prof[block][wave][5]
+// (scripts/wino_lab.py --phases; never used by the executor)
+template <bool PROF>
+__global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
+    int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter c1,
+    unsigned long long* __restrict__ prof) {
+  unsigned long long stamp[5];
+  if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
+  constexpr int SM = WF_SMEM > c1f_smem<1, WF_NT / 64>() ? WF_SMEM : c1f_smem<1, WF_NT / 64>();
+  __shared__ float smem[SM];
+  if ((int)blockIdx.x >= nwg) {  // conv1 filter-grad role (its dA1 is final)
+    conv1_filter_unit<WF_NT, 1>(blockIdx.x - nwg, batch, c1, smem);
+    return;
+  }
+  // XCD-aware: the 8 (ci, co) tiles of an image group share one XCD's L2
+  const int ngroups = nwg / 8, bid = blockIdx.x;
+  int g, sub;
+  if (ngroups % 8 == 0) {
+    const int x = bid & 7, idx = bid >> 3;
+    g = x + 8 * (idx >> 3);
+    sub = idx & 7;
+  } else {
+    g = bid >> 3;
+    sub = bid & 7;
+  }
+  const int ci_t = sub & 1, co_t = sub >> 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int arow = wave % 6, half = wave / 6;
+  const int n0 = g * WF_IMG, nimg = min(WF_IMG, batch - n0);
+  float* xs = smem;
+  float* dys = smem + WF_XS;
+  // 1. slices -> LDS (every load issued before the first store)
+  {
+    constexpr int NX = WF_IMG * 324 * 4, ND = WF_IMG * 196 * 4;  // float4s
+    constexpr int PX = (NX + WF_NT - 1) / WF_NT, PD = (ND + WF_NT - 1) / WF_NT;
+    float4 vx[PX], vd[PD];
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int i = min(tid + j * WF_NT, NX - 1), pix = i >> 2, img = pix / 324;
+      const int n = min(n0 + img, batch - 1);  // clamped: images past the batch are masked
+      vx[j] = *reinterpret_cast<const float4*>(
+          a1p + ((size_t)n * 324 + (pix - 324 * img)) * 32 + ci_t * 16 + 4 * (i & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      const int i = min(tid + j * WF_NT, ND - 1), pix = i >> 2, img = pix / 196;
+      const int n = min(n0 + img, batch - 1);
+      vd[j] = *reinterpret_cast<const float4*>(
+          dy2 + ((size_t)n * 196 + (pix - 196 * img)) * 64 + co_t * 16 + 4 * (i & 3));
+    }
+#pragma unroll
+    for (int j = 0; j < PX; ++j) {
+      const int i = tid + j * WF_NT;
+      if (i < NX) {
+        const int pix = i >> 2, img = pix / 324, pp = pix - 324 * img, row = pp / 18;
+        const int col = pp - 18 * row, c0 = 4 * (i & 3);
+        float* d = xs + ((img * 18 + row) * 16 + c0) * WF_XLD + col;
+        d[0] = vx[j].x;
+        d[WF_XLD] = vx[j].y;
+        d[2 * WF_XLD] = vx[j].z;
+        d[3 * WF_XLD] = vx[j].w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      const int i = tid + j * WF_NT;
+      if (i < ND) {
+        const int pix = i >> 2, img = pix / 196, pp = pix - 196 * img, row = pp / 14;
+        const int col = pp - 14 * row, c0 = 4 * (i & 3);
+        float* d = dys + ((img * 14 + row) * 16 + c0) * WF_DLD + col;
+        d[0] = vd[j].x;
+        d[WF_DLD] = vd[j].y;
+        d[2 * WF_DLD] = vd[j].z;
+        d[3 * WF_DLD] = vd[j].w;
+      }
+    }
+  }
+  __syncthreads();
+  if constexpr (PROF) stamp[1] = __builtin_amdgcn_s_memtime();
+  // 2. the wave's point row
+  f32x4 acc[6];
+#pragma unroll
+  for (int b = 0; b < 6; ++b) acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  switch (arow) {
+    case 0: wino_wgrad_row<0>(xs, dys, nimg, lane, half, acc); break;
+    case 1: wino_wgrad_row<1>(xs, dys, nimg, lane, half, acc); break;
+    case 2: wino_wgrad_row<2>(xs, dys, nimg, lane, half, acc); break;
+    case 3: wino_wgrad_row<3>(xs, dys, nimg, lane, half, acc); break;
+    case 4: wino_wgrad_row<4>(xs, dys, nimg, lane, half, acc); break;
+    default: wino_wgrad_row<5>(xs, dys, nimg, lane, half, acc); break;
+  }
+  if constexpr (PROF) stamp[2] = __builtin_amdgcn_s_memtime();
+  float db = 0.f;  // db2 partial: thread (co, dY row stripe), ci-tile-0 blocks
+  if (ci_t == 0 && tid < 256) {
+    const int co = tid & 15;
+    for (int L = tid >> 4; L < nimg * 14; L += 16) {
+      const float* dl = dys + (L * 16 + co) * WF_DLD;
+#pragma unroll
+      for (int x = 0; x < 14; ++x) db += dl[x];
+    }
+  }
+  float* dbr = smem + 6 * 2 * 5 * 4 * 64;  // db2 stripes [16][16], after red
+  __syncthreads();  // the slices are reused below
+  // 3. S_ah[kw] = sum_b G[b][kw] M_h[a][b]   (this wave's a, h)
+  float* red = smem;  // [a][h][kw][j][lane]
+  {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float sv = 0.f;
+#pragma unroll
+        for (int b = 0; b < 6; ++b)
+          if (wino::kG[b][kw] != 0.f) sv += wino::kG[b][kw] * acc[b][j];
+        red[(((arow * 2 + half) * 5 + kw) * 4 + j) * 64 + lane] = sv;
+      }
+  }
+  if (ci_t == 0 && tid < 256) dbr[tid] = db;
+  __syncthreads();
+  if constexpr (PROF) stamp[3] = __builtin_amdgcn_s_memtime();
+  if (tid < 256) {  // dW[kh][kw] = sum_a G[a][kh] S_a[kw] for element (j, lane')
+#pragma clang fp contract(off)
+    const int j = tid >> 6, l = tid & 63;
+    float S[6][5];
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+        S[a][kw] = red[(((a * 2) * 5 + kw) * 4 + j) * 64 + l] +
+                   red[(((a * 2 + 1) * 5 + kw) * 4 + j) * 64 + l];
+    const int ci = ci_t * 16 + 4 * (l >> 4) + j, co = co_t * 16 + (l & 15);
+    float* out = part2 + (size_t)g * 51200 + ci * 64 + co;
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        float sv = 0.f;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+          if (wino::kG[a][kh] != 0.f) sv += wino::kG[a][kh] * S[a][kw];
+        out[(kh * 5 + kw) * 2048] = sv;
+      }
+  }
+  if (ci_t == 0 && tid < 16) {  // db2: one row per group (rows 4 g + 1..3 zero)
+    float sv = 0.f;
+#pragma unroll
+    for (int st = 0; st < 16; ++st) sv += dbr[st * 16 + tid];
+    const int co = co_t * 16 + tid;
+    part_db2[(g * 4) * 64 + co] = sv;
+#pragma unroll
+    for (int r = 1; r < 4; ++r) part_db2[(g * 4 + r) * 64 + co] = 0.f;
+  }
+  if constexpr (PROF) {
+    stamp[4] = __builtin_amdgcn_s_memtime();
+    if (lane == 0)
+      for (int k = 0; k < 5; ++k) prof[((size_t)blockIdx.x * (WF_NT / 64) + wave) * 5 + k] = stamp[k];
+  }
+}
 
 // conv2 bwd-filter: dW2[t][ci][co] = sum_pix a1[pix shifted by tap t][ci] dY2[pix][co].
 // Block = (tap, group of 4 images); 8 waves = 2 (N: co halves) x 4 (one image
@@ -1116,6 +1742,25 @@ void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float*
   conv2_fwd_v3_kernel<true><<<batch * 4, 256, 0, s>>>(nullptr, batch, w2, b2, a2, idx2, w2t, c1);
 }
 
+void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t s) {
+  conv2_wino_weights_kernel<<<2048 / 256, 256, 0, s>>>(w2, U, Ud);
+}
+
+void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
+                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s) {
+  if (!c1.data || !c1.w1 || !c1.b1 || !c1.a1 || !c1.a1pf || !c1.idx1 || !U)
+    throw std::runtime_error("conv12_fwd_wino: missing operand");
+  conv2_fwd_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2, w2t,
+                                                        c1);
+}
+
+void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
+                           const float* b, float* out, uint8_t* argmax, float* w2t,
+                           hipStream_t s) {
+  conv2_fwd_wino_kernel<false><<<batch * 4, WNT, 0, s>>>(a1, batch, w2, U, b, out, argmax, w2t,
+                                                         C12In{});
+}
+
 int fc1_train_splits() { return FC1_SPLITS; }
 
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part,
@@ -1203,6 +1848,16 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
                                                                      sg);
 }
 
+void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
+                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd) {
+  FcSgd sg = fc_sgd_args(fc_sgd);
+  // the SGD role works in 256-thread units: two per 512-thread block
+  const int role_blocks = (sg.nblk + 1) / 2;
+  sg.nblk = 2 * role_blocks;
+  conv2_bwd_data_wino_kernel<<<batch * 4 + role_blocks, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m,
+                                                                     sg);
+}
+
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
                              hipStream_t s, const C1FilterArgs* c1) {
   const int G = conv2_filter_splits(batch);
@@ -1213,7 +1868,36 @@ void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, floa
                                                                 c);
 }
 
-int conv1_filter_blocks(int batch) { return batch * C1F_SPLIT; }
+int conv1_filter_blocks(int batch, int split) {
+  if (split != C1F_SPLIT && split != 1) throw std::runtime_error("conv1 filter split: 1 or 7");
+  return batch * split;
+}
+
+int conv2_wino_filter_groups(int batch) { return cdiv(batch, WF_IMG); }
+size_t part2_floats_wino(int batch) {
+  return (size_t)conv2_wino_filter_groups(batch) * (51200 + 256);
+}
+
+void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch, float* part2,
+                                  hipStream_t s, const C1FilterArgs* c1) {
+  const int G = conv2_wino_filter_groups(batch);
+  const C1Filter c = c1_args(c1);
+  const int n1 = c.part1 ? conv1_filter_blocks(batch, 1) : 0;
+  // MTA_WF_PAD (bytes of extra dynamic LDS): placement experiments only
+  static const int pad = [] {
+    const char* e = getenv("MTA_WF_PAD");
+    return e ? atoi(e) : 0;
+  }();
+  conv2_bwd_filter_wino_kernel<false><<<8 * G + n1, WF_NT, pad, s>>>(
+      batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, c, nullptr);
+}
+
+void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,
+                                       float* part2, unsigned long long* prof, hipStream_t s) {
+  const int G = conv2_wino_filter_groups(batch);
+  conv2_bwd_filter_wino_kernel<true><<<8 * G, WF_NT, 0, s>>>(
+      batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, C1Filter{}, prof);
+}
 
 C1Filter c1_args(const C1FilterArgs* a) {
   if (a == nullptr) return C1Filter{};
@@ -1255,12 +1939,110 @@ struct SgdFinArgs {
   const float* lr;
   long long* step;
   int fc_blocks;
+  // Winograd conv2 (optional): the updated conv2 filters' transforms for the
+  // NEXT step's forward (U) and bwd-data (Ud), layouts of wino_u_index
+  float* U;
+  float* Ud;
 };
 
 __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, float mu) {
   const float mv = mu * *m + g;
   *m = mv;
   *w -= lr * mv;
+}
+
+// conv2 weights of ONE input channel ci (25 taps x 64 co): slab sums + SGD,
+// then the Winograd transforms of the updated 5x5 filters (U and Ud).  Thread
+// (co4 = tid & 15, tg = tid >> 4) updates taps tg and tg + 16; each slab sum
+// runs in the same order as the 50-block path.
+__device__ void sgd_conv2_wino(const SgdFinArgs& a, int ci, float lr) {
+  __shared__ float wl[25 * 64];
+  const int tid = threadIdx.x, co4 = tid & 15, tg = tid >> 4;
+  for (int t = tg; t < 25; t += 16) {
+    const int i = (t * 32 + ci) * 16 + co4;  // float4 index in the HWIO block
+    const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 8 <= a.ngroups; z += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sv.x += v[u].x;
+        sv.y += v[u].y;
+        sv.z += v[u].z;
+        sv.w += v[u].w;
+      }
+    }
+    for (; z < a.ngroups; ++z) {
+      const float4 v = p2[(size_t)z * 12800];
+      sv.x += v.x;
+      sv.y += v.y;
+      sv.z += v.z;
+      sv.w += v.w;
+    }
+    float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
+    float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
+    float4 wv = *wp, mv = *mp;
+    sgd4(wv, mv, sv, 0.f, lr, a.momentum);
+    *wp = wv;
+    *mp = mv;
+    *reinterpret_cast<float4*>(wl + t * 64 + 4 * co4) = wv;
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int co = tid & 63;
+    float g[25], u[36];
+    if (tid < 64) {
+#pragma unroll
+      for (int t = 0; t < 25; ++t) g[t] = wl[t * 64 + co];
+      wino::filter_tile(g, u);
+#pragma unroll
+      for (int p = 0; p < 36; ++p) a.U[wino_u_index(p, ci, co)] = u[p];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 64 + co];
+      wino::filter_tile(g, u);
+#pragma unroll
+      for (int p = 0; p < 36; ++p) a.Ud[wino_ud_index(p, ci, co)] = u[p];
+    }
+  }
+}
+
+// conv2 weights: 51200 floats = 50 blocks x 256 threads x float4, each summed
+// over the image-group slabs in order
+__device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
+  const int tid = threadIdx.x;
+  const int i = blk * 256 + tid;
+  const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 8 <= a.ngroups; z += 8) {  // 8 slab loads in flight, summed in order
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s.x += v[u].x;
+      s.y += v[u].y;
+      s.z += v[u].z;
+      s.w += v[u].w;
+    }
+  }
+  for (; z < a.ngroups; ++z) {
+    const float4 v = p2[(size_t)z * 12800];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
+  float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
+  float4 wv = *wp, mv = *mp;
+  sgd4(wv, mv, s, 0.f, lr, a.momentum);
+  *wp = wv;
+  *mp = mv;
 }
 
 __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
@@ -1282,39 +2064,15 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
     return;
   }
   blk -= a.fc_blocks;
-  if (blk < 50) {  // conv2 weights: 51200 floats = 50 blocks x 256 threads x float4
-    const int i = blk * 256 + tid;
-    const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    int z = 0;
-    for (; z + 8 <= a.ngroups; z += 8) {  // 8 slab loads in flight, summed in order
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        s.x += v[u].x;
-        s.y += v[u].y;
-        s.z += v[u].z;
-        s.w += v[u].w;
-      }
-    }
-    for (; z < a.ngroups; ++z) {
-      const float4 v = p2[(size_t)z * 12800];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
-    float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
-    float4 wv = *wp, mv = *mp;
-    sgd4(wv, mv, s, 0.f, lr, a.momentum);
-    *wp = wv;
-    *mp = mv;
+  const int nconv2 = a.U ? 32 : 50;
+  if (blk < nconv2) {
+    if (a.U)
+      sgd_conv2_wino(a, blk, lr);
+    else
+      sgd_conv2_flat(a, blk, lr);
     return;
   }
-  blk -= 50;
+  blk -= nconv2;
   const int lane = tid & 63;
   if (blk < 16) {  // conv2 bias: one wave per channel
     const int co = blk * 4 + (tid >> 6);
@@ -1340,17 +2098,21 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
 void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s, bool fc_done) {
+                         const float* lr, long long* step, hipStream_t s, bool fc_done,
+                         float* wino_u, float* wino_ud) {
   if (fc_end % 4 || off_w2 % 4 || l2_end != fc_end)
     throw std::runtime_error("sgd_finalize: misaligned flat segments / L2 prefix != FC bucket");
+  if ((wino_u == nullptr) != (wino_ud == nullptr))
+    throw std::runtime_error("sgd_finalize: Winograd filters need both U and Ud");
   const long long n4 = fc_end / 4;
   long long b = (n4 + 255) / 256;
   // fc_done: the FC bucket was updated by the conv2 bwd-data launch's SGD role
   const int fc_blocks = fc_done ? 0 : (int)(b < 2048 ? b : 2048);  // as the flat SGD
   SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
                part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
-               fc_blocks};
-  sgd_finalize_kernel<<<fc_blocks + 50 + 16 + cdiv(832, 4), 256, 0, s>>>(a);
+               fc_blocks, wino_u, wino_ud};
+  const int conv2_blocks = wino_u ? 32 : 50;
+  sgd_finalize_kernel<<<fc_blocks + conv2_blocks + 16 + cdiv(832, 4), 256, 0, s>>>(a);
 }
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,

@@ -71,16 +71,21 @@ __device__ inline void fc1_small_grads(int blk, const float* hd, const float* dh
 // ------------------------------------------------ conv1 filter gradient ----
 // Sparse: each pooled gradient reaches exactly one pre-pool pixel (its argmax),
 // so dW1[t][co] = sum over pooled (n,py,px) of dA1m * x[argmax pixel + tap]
-// (reference mpipy.py:155-157 conv1, B7).  Unit = (image, pair of pooled
-// rows) -> one 832-float partial row part1[unit] (800 weights + 32 biases);
-// thread = (co, position group), NT / 32 groups.  All of a thread's
+// (reference mpipy.py:155-157 conv1, B7).  Unit = (image, band of 14 / SPLIT
+// pooled rows) -> one 832-float partial row part1[unit] (800 weights + 32
+// biases); thread = (co, position group), NT / 32 groups.  All of a thread's
 // (gradient, argmax) pairs are loaded up front (one latency round); the two
 // groups of a wave are combined by a lane shuffle, the NT / 64 wave partials
 // in a fixed order through LDS.  Run as its own 256-thread kernel or as the
-// 512-thread role blocks appended to the conv2 filter-gradient launch.
-constexpr int C1F_SPLIT = 7;                    // pooled-row pairs per image
-constexpr int C1F_POS = 28;                     // pooled positions per unit
-constexpr int C1F_SMEM = 8 * 32 + 8 * (26 * 32 + 1);  // floats (NT <= 512)
+// 512-thread role blocks appended to a conv2 filter-gradient launch: SPLIT = 7
+// (pairs of pooled rows) where the conv2 part fills the chip, SPLIT = 1 (whole
+// images: batch units) where the conv2 part leaves batch CUs free (Winograd).
+constexpr int C1F_SPLIT = 7;  // default: pooled-row pairs per image (mnist.h)
+template <int SPLIT, int NW = 8>
+constexpr int c1f_smem() {  // floats for NW waves: image rows + wave partials
+  return (2 * (14 / SPLIT) + 4) * 32 + NW * (26 * 32 + 1);
+}
+constexpr int C1F_SMEM = c1f_smem<C1F_SPLIT>();
 
 struct C1Filter {  // conv1 filter-grad role arguments (part1 == nullptr: off)
   const float* data;
@@ -92,22 +97,22 @@ struct C1Filter {  // conv1 filter-grad role arguments (part1 == nullptr: off)
 };
 
 C1Filter c1_args(const C1FilterArgs* a);  // host (mnist.hip)
-int conv1_filter_blocks(int batch);
 
-template <int NT>
+template <int NT, int SPLIT = C1F_SPLIT>
 __device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c, float* smem) {
-  constexpr int NG = NT / 32, PER_T = (C1F_POS + NG - 1) / NG, NW = NT / 64;
-  static_assert(NW <= 8, "C1F_SMEM sized for 8 waves");
-  float* xs = smem;                // rows 4*pair-2 .. 4*pair+5 of the padded image
-  float* red = smem + 8 * 32;      // [NW][26 * 32 + 1]
-  const int n = unit / C1F_SPLIT, pair = unit % C1F_SPLIT;
+  static_assert(14 % SPLIT == 0, "SPLIT divides the 14 pooled rows");
+  constexpr int PR = 14 / SPLIT, POS = PR * 14, XR = 2 * PR + 4;
+  constexpr int NG = NT / 32, PER_T = (POS + NG - 1) / NG, NW = NT / 64;  // smem: c1f_smem<SPLIT, NW>
+  float* xs = smem;            // rows 2*PR*band-2 .. +XR-1 of the padded image
+  float* red = smem + XR * 32;  // [NW][26 * 32 + 1]
+  const int n = unit / SPLIT, band = unit % SPLIT;
   const long long off = batch_offset_dev(c.step, c.n_local, batch);
   const float* x = c.data + (off + n) * 784;
   const int tid = threadIdx.x, co = tid & 31, grp = tid >> 5, wave = tid >> 6;
-  const int y0 = 4 * pair - 2;  // first image row held in xs
-  if (tid < 256) {
-    const int yy = y0 + tid / 32, xx = tid % 32 - 2;
-    xs[tid] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
+  const int y0 = 2 * PR * band - 2;  // first image row held in xs
+  for (int i = tid; i < XR * 32; i += NT) {
+    const int yy = y0 + i / 32, xx = i % 32 - 2;
+    xs[i] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
   }
   float v[PER_T];
   int q[PER_T];
@@ -116,8 +121,8 @@ __device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c,
     const int p = grp + NG * j;
     v[j] = 0.f;
     q[j] = 0;
-    if (p < C1F_POS) {
-      const int py = 2 * pair + p / 14, px = p % 14;
+    if (p < POS) {
+      const int py = PR * band + p / 14, px = p % 14;
       const int e = ((n * 14 + py) * 14 + px) * 32 + co;
       v[j] = c.da1m[e];
       q[j] = c.idx1[e];
@@ -130,8 +135,8 @@ __device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c,
 #pragma unroll
   for (int j = 0; j < PER_T; ++j) {
     const int p = grp + NG * j;
-    if (p < C1F_POS && v[j] != 0.f) {
-      const int py = 2 * pair + p / 14, px = p % 14;
+    if (p < POS && v[j] != 0.f) {
+      const int py = PR * band + p / 14, px = p % 14;
       const int ly = 2 * py + (q[j] >> 1) - y0 - 2;  // row in xs of tap kh = 0
       const int lx = 2 * px + (q[j] & 1);            // col in xs (padded by 2) of kw = 0
 #pragma unroll
@@ -310,7 +315,10 @@ __device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* ti
 
 // blk: index among the role's blocks; tile: >= 64 x 65 floats of LDS when
 // a.w1b is set (256-thread blocks)
-__device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile) {
+// tid: the thread's index in its 256-thread unit (a 512-thread block runs two
+// units; the shadow path (a.w1b) needs 256-thread blocks)
+__device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile,
+                                   int tid = (int)threadIdx.x) {
   float4* W4 = reinterpret_cast<float4*>(a.w);
   float4* M4 = reinterpret_cast<float4*>(a.m);
   const float4* G4 = reinterpret_cast<const float4*>(a.g);
@@ -329,7 +337,7 @@ __device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile) {
   const long long stride = (long long)nb * 256;
   auto at = [&](long long f) { return (a.w1b && f >= a.w1_off4) ? f + W1_F4 : f; };
   // U float4s per thread per round, every load of a round in flight together
-  for (long long i0 = (long long)blk * 256 + threadIdx.x; i0 < n4; i0 += stride * FC_SGD_UNROLL) {
+  for (long long i0 = (long long)blk * 256 + tid; i0 < n4; i0 += stride * FC_SGD_UNROLL) {
     float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];
 #pragma unroll
     for (int u = 0; u < FC_SGD_UNROLL; ++u) {

@@ -42,7 +42,8 @@ MnistExecutor::~MnistExecutor() {
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
-                                    const mnist::FcSgdArgs* fc_sgd, bool factors) {
+                                    const mnist::FcSgdArgs* fc_sgd, bool factors,
+                                    bool wino_fresh) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
     return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd);
@@ -64,8 +65,17 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   cf.a1 = P<float>(p.a1);
   cf.a1pf = P<float>(p.a1pf);
   cf.idx1 = P<uint8_t>(p.idx1);
-  mnist::launch_conv12_fwd(cf, B, W + p.off_w2, W + p.off_b2, P<float>(p.a2), P<uint8_t>(p.idx2),
-                           P<float>(p.w2t), s);
+  if (p.wino) {
+    // transformed filters of this step's weights (forward U, bwd-data Ud);
+    // the single-rank step's SGD already wrote them (wino_fresh)
+    if (!wino_fresh)
+      mnist::launch_conv2_wino_weights(W + p.off_w2, P<float>(p.wino_u), P<float>(p.wino_ud), s);
+    mnist::launch_conv12_fwd_wino(cf, B, W + p.off_w2, P<const float>(p.wino_u), W + p.off_b2,
+                                  P<float>(p.a2), P<uint8_t>(p.idx2), nullptr, s);
+  } else {
+    mnist::launch_conv12_fwd(cf, B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
+                             P<uint8_t>(p.idx2), P<float>(p.w2t), s);
+  }
   wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
   mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
   mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
@@ -80,18 +90,26 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
                         P<float>(p.dy2t), s, factors ? 1 : 7);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
-  mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
-                                  P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
+  if (p.wino)
+    mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
+                                      P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
+  else
+    mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
+                                    P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
   // conv1 filter grad (needs dA1 from bwd-data) as role blocks of this launch
   const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
                                P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                P<float>(p.part1)};
-  mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
-                                 P<float>(p.part2), s, &c1);
+  if (p.wino)
+    mnist::launch_conv2_bwd_filter_wino(P<const float>(p.a1pf), P<const float>(p.dy2), B,
+                                        P<float>(p.part2), s, &c1);
+  else
+    mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
+                                   P<float>(p.part2), s, &c1);
   if (finalize)
-    mnist::launch_grad_finalize(P<const float>(p.part2), mnist::conv2_filter_splits(B),
-                                P<const float>(p.part1), mnist::conv1_filter_blocks(B),
-                                G + p.off_w2, G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
+    mnist::launch_grad_finalize(P<const float>(p.part2), conv2_groups(), P<const float>(p.part1),
+                                conv1_blocks(), G + p.off_w2, G + p.off_b2, G + p.off_w1,
+                                G + p.off_b1, s);
 }
 
 // bf16 step: same kernel boundaries; the first launch re-derives the bf16
@@ -146,7 +164,14 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
 }
 
 int MnistExecutor::conv2_groups() const {
-  return p_.bf16 ? mnist16::conv2_filter_groups(p_.batch) : mnist::conv2_filter_splits(p_.batch);
+  if (p_.bf16) return mnist16::conv2_filter_groups(p_.batch);
+  return p_.wino ? mnist::conv2_wino_filter_groups(p_.batch)
+                 : mnist::conv2_filter_splits(p_.batch);
+}
+
+// the Winograd filter launch runs the conv1 filter grad as whole-image units
+int MnistExecutor::conv1_blocks() const {
+  return mnist::conv1_filter_blocks(p_.batch, (p_.wino && !p_.bf16) ? 1 : 7);
 }
 
 void MnistExecutor::forward_backward(hipStream_t s) {
@@ -185,6 +210,10 @@ void MnistExecutor::reduce_bucket(Collective* comm, long long lo, long long n, h
 }
 
 void MnistExecutor::refresh_shadows(hipStream_t s) {
+  if (p_.wino) {
+    const float* W = P<const float>(p_.params);
+    mnist::launch_conv2_wino_weights(W + p_.off_w2, P<float>(p_.wino_u), P<float>(p_.wino_ud), s);
+  }
   if (!p_.bf16) return;
   const float* W = P<const float>(p_.params);
   mnist16::launch_shadows(W + p_.off_w3, W + p_.off_w2, P<uint16_t>(p_.w1b), P<uint16_t>(p_.w1t),
@@ -233,12 +262,17 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
       fc.w1 = p.off_w3;
     }
     const bool fused = fc_sgd_rounds_ > 0 && p.l2_end == p.bucket1;
-    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr);
+    // Winograd: the filter transforms come from the previous step's SGD (or
+    // refresh_shadows() before the first step of a run) and are rewritten by
+    // this step's SGD for the next one
+    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr, false, /*wino_fresh=*/true);
     mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
                                p.bucket1, p.l2_end, (int)p.off_w2, (int)p.off_b2, (int)p.off_w1,
                                (int)p.off_b1, P<const float>(p.part2), conv2_groups(),
-                               P<const float>(p.part1), mnist::conv1_filter_blocks(p.batch), p.l2,
-                               p.momentum, P<const float>(p.lr), P<long long>(p.step), s, fused);
+                               P<const float>(p.part1), conv1_blocks(), p.l2, p.momentum,
+                               P<const float>(p.lr), P<long long>(p.step), s, fused,
+                               p.wino ? P<float>(p.wino_u) : nullptr,
+                               p.wino ? P<float>(p.wino_ud) : nullptr);
     return;
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {

@@ -64,6 +64,10 @@ struct MnistPtrs {
   // [.][10]); a2 / dh / hd / dlog above point at this rank's slot in them
   uintptr_t a2_all = 0, dh_all = 0, hd_all = 0, dlog_all = 0;
   int fac_ranks = 0;  // communicator size the factor buffers were sized for
+  // fp32 conv2 by Winograd F(2x2,5x5) (kernels/wino.h): transformed filters
+  // wino_u [36][32][64] (forward) and wino_ud [36][64][32] (bwd-data)
+  int wino = 0;
+  uintptr_t wino_u = 0, wino_ud = 0;
 };
 
 namespace mnist {
@@ -125,8 +129,9 @@ class MnistExecutor {
   // role appended to the conv2 bwd-data launch (sets its block count); 0 runs
   // the FC SGD in the final SGD launch instead
   void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? 0 : r; }
-  // bf16 engine: re-derive every bf16 weight shadow from the fp32 master
-  // weights.  A single-rank bf16 step writes the fc1 shadows from its SGD and
+  // Re-derives every weight copy the step kernels read from the fp32 master
+  // weights: the Winograd filter transforms (fp32, wino) and the bf16
+  // shadows (bf16 engine).  A single-rank bf16 step writes the fc1 shadows from its SGD and
   // the next step relies on them, so the caller refreshes them once before a
   // run of steps (the engine does so at the start of every train() call):
   // any change to the weights between runs (init, checkpoint load, ...) is
@@ -140,8 +145,13 @@ class MnistExecutor {
   // factors: record ev_fac_ once the FC factors are written (after the head)
   // and compute only dX in fc1 backward (the FC weight grads come from the
   // gathered factors)
+  // wino_fresh: the Winograd filter transforms are already current (the
+  // single-rank step writes them from its SGD); otherwise they are derived
+  // from the weights by a launch at the start of the step
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
-                       const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false);
+                       const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
+                       bool wino_fresh = false);
+  int conv1_blocks() const;
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);

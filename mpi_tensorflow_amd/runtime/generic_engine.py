@@ -8,7 +8,8 @@ per-step gradient all-reduce of the flat grad buffer.
 With cfg.dtype == "bf16" the convolutions run their MFMAs on bf16 operands
 (bf16 copies of activations / output gradients and re-laid bf16 weights,
 csrc/kernels/conv_bf16.hip; fp32 accumulation); the stored activations,
-BatchNorm, linear layers (fp32 library GEMMs), gradients and the optimizer
+BatchNorm, the native fp32 linear layers (gops::linear_fwd / linear_bwd),
+gradients and the optimizer
 stay fp32.
 
 On GPU one training step is: batch gather from the device-resident shard at

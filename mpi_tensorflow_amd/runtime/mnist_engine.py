@@ -216,6 +216,12 @@ class NativeMnistEngine(MnistEngineBase):
             a1pf=torch.zeros(B * 18 * 18 * 32, **f32),
         )
         self.bf16 = cfg.dtype == "bf16"
+        self.wino = (not self.bf16) and cfg.conv_algo == "winograd"
+        if self.wino:  # Winograd-transformed conv2 filters (csrc/kernels/wino.h)
+            self.bufs.update(wino_u=torch.empty(36 * 32 * 64, **f32),
+                             wino_ud=torch.empty(36 * 64 * 32, **f32),
+                             # the filter gradient's point slabs replace the 25-tap ones
+                             part2=torch.empty(k.part2_floats_wino(B), **f32))
         self.fac = None
         hcomm = comm.native_handle if (self.grad_sync and comm is not None) else None
         nfac = hcomm.size if hcomm is not None else 1
@@ -267,6 +273,7 @@ class NativeMnistEngine(MnistEngineBase):
         p.l2, p.momentum = cfg.l2, cfg.momentum
         p.seed, p.rank, p.world = cfg.seed, self.drop_rank, world
         p.bf16 = 1 if self.bf16 else 0
+        p.wino = 1 if self.wino else 0
         self.gb16 = None  # bf16 gradient wire staging (--grad-comm-dtype bf16)
         if cfg.grad_comm_dtype == "bf16" and world > 1:
             self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)

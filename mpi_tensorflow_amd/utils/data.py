@@ -297,26 +297,64 @@ def synthetic_image_shard(rank: int, world: int, rows_per_rank: int, test_per_ra
 
 
 def synthetic_images_torch(n: int, shape: Tuple[int, int, int], classes: int = 10,
-                           seed: int = C.SEED, start: int = 0, device="cpu", split: str = "train"):
-    """Large-image synthetic data (ResNet-18 at 224x224x3) generated with torch
-    on the target device: class prototypes (a coarse random field upsampled
-    16x) + per-image noise, values in [-0.5, 0.5], NHWC float32, int64 labels.
-    Deterministic in (seed, split, start); rows [start, start+n).  Train and
-    test splits share the class prototypes (same seed) and differ in labels
-    and noise."""
+                           seed: int = C.SEED, start: int = 0, device="cpu", split: str = "train",
+                           noise: float = 0.35):
+    """Large-image synthetic task (ResNet-18 at 224x224x3), generated with
+    torch: the v2 design of `_synthetic_chunk` scaled to the image size, so
+    the final accuracy is informative (it is not separable at a glance):
+      * a pool of 16 smooth colour templates (coarse random fields at 1/16 of
+        the resolution, bilinear upsampled, tanh-squashed) SHARED by the
+        classes: class c is a fixed set of 3 pool templates;
+      * each of the class's templates present with prob. 0.8 (at least one),
+        weight U(0.45, 1), independent circular shift of up to h/14 px;
+      * a distractor template of another class with prob. 0.6;
+      * random gain / bias and Gaussian pixel noise (`noise`).
+    Values in [-0.5, 0.5], NHWC float32, int64 labels.  Deterministic in
+    (seed, split, start): rows [start, start + n)."""
     import torch
 
     h, w, c = shape
+    pool_n, per = _POOL, _PER_CLASS
     g = torch.Generator(device="cpu").manual_seed(seed * 1000003 + 17)
     ch, cw = max(2, h // 16), max(2, w // 16)
-    protos = torch.randn(classes, c, ch, cw, generator=g)
-    protos = torch.nn.functional.interpolate(protos, size=(h, w), mode="bilinear",
-                                             align_corners=False)
+    coarse = torch.randn(pool_n, c, ch, cw, generator=g)
+    tpl = torch.tanh(2.0 * torch.nn.functional.interpolate(coarse, size=(h, w), mode="bilinear",
+                                                           align_corners=False))
+    codes = torch.from_numpy(_class_codes(seed, classes))
     salt = {"train": 0, "test": 1 << 40, "val": 2 << 40}[split]
     gl = torch.Generator(device="cpu").manual_seed(seed * 7919 + start + salt)
     labels = torch.randint(0, classes, (n,), generator=gl)
+    keep = torch.rand(n, per, generator=gl) < 0.8
+    keep[torch.arange(n), torch.randint(0, per, (n,), generator=gl)] = True
+    wts = torch.where(keep, 0.45 + 0.55 * torch.rand(n, per, generator=gl), torch.zeros(()))
+    other = (labels + torch.randint(1, classes, (n,), generator=gl)) % classes
+    dist = codes[other, torch.randint(0, per, (n,), generator=gl)]
+    dw = torch.where(torch.rand(n, generator=gl) < 0.6, 0.3 + 0.4 * torch.rand(n, generator=gl),
+                     torch.zeros(()))
+    smax = max(2, h // 14)
+    shifts = torch.randint(-smax, smax + 1, (n, per + 1, 2), generator=gl)
+    gain = 0.5 + 0.5 * torch.rand(n, 1, 1, 1, generator=gl)
+    bias = -0.05 + 0.2 * torch.rand(n, 1, 1, 1, generator=gl)
     gn = torch.Generator(device=device).manual_seed(seed * 104729 + start + salt)
-    x = protos.to(device)[labels.to(device)] * 0.25
-    x = x + 0.15 * torch.randn(x.shape, generator=gn, device=device)
-    x = x.clamp_(-0.5, 0.5).permute(0, 2, 3, 1).contiguous()
+    tpl = tpl.to(device)
+    ar_h = torch.arange(h, device=device)
+    ar_w = torch.arange(w, device=device)
+    x = torch.empty(n, h, w, c, device=device)
+    for a in range(0, n, 64):  # chunks keep the gathers small
+        b = min(n, a + 64)
+        m = b - a
+        img = torch.zeros(m, c, h, w, device=device)
+        srcs = [(codes[labels[a:b], j], wts[a:b, j]) for j in range(per)] + [(dist[a:b], dw[a:b])]
+        for j, (ids, wt) in enumerate(srcs):
+            sy = shifts[a:b, j, 0].to(device)
+            sx = shifts[a:b, j, 1].to(device)
+            yi = (ar_h[None, :] - sy[:, None]) % h  # circular shift, per sample
+            xi = (ar_w[None, :] - sx[:, None]) % w
+            t = tpl[ids.to(device)]  # [m, c, h, w]
+            t = t.gather(2, yi[:, None, :, None].expand(m, c, h, w))
+            t = t.gather(3, xi[:, None, None, :].expand(m, c, h, w))
+            img += wt.to(device)[:, None, None, None] * t
+        img = gain[a:b].to(device) * img + bias[a:b].to(device)
+        img = img + noise * torch.randn(img.shape, generator=gn, device=device)
+        x[a:b] = (0.25 * img).clamp_(-0.5, 0.5).permute(0, 2, 3, 1)
     return x, labels

@@ -37,6 +37,12 @@ def main():
                                          W("conv1_bias"), ptr(b["a1"]), ptr(b["idx1"]), s, ptr(b["a1pf"])),
         "conv2_fwd": lambda: k.conv2_fwd(ptr(b["a1"]), B, W("conv2_weight"), W("conv2_bias"), ptr(b["a2"]),
                                          ptr(b["idx2"]), ptr(b["w2t"]), s),
+        "conv2_wino_w": lambda: k.conv2_wino_weights(W("conv2_weight"), ptr(b["wino_u"]), 0, s),
+        "conv2_fwd_wino": lambda: k.conv2_fwd_wino(ptr(b["a1"]), B, W("conv2_weight"), ptr(b["wino_u"]),
+                                                   W("conv2_bias"), ptr(b["a2"]), ptr(b["idx2"]),
+                                                   ptr(b["w2t"]), s),
+        "conv2_bwd_data_wino": lambda: k.conv2_bwd_data_wino(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]),
+                                                             B, ptr(b["da1m"]), s),
         "fc1_fwd": lambda: k.fc1_fwd_train(ptr(b["a2"]), W("fc1_weight"), B, ptr(b["fc1_part"]), s),
         "fc_head": lambda: k.fc_head_train(ptr(b["fc1_part"]), W("fc1_bias"), W("fc2_weight"), W("fc2_bias"),
                                            ptr(e.train_y), e.n_local, ptr(e.step_dev), B, 0.5, 1, 0, 0.01, 0.95,
@@ -53,14 +59,6 @@ def main():
                                          ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
                                          G("fc1_bias"), G("fc2_weight"), G("fc2_bias"), ptr(b["dy2"]),
                                          ptr(b["dy2t"]), s, 2),
-        "fc1_bwd[dX-noepi]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
-                                              ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
-                                              G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
-                                              ptr(b["dy2"]), ptr(b["dy2t"]), s, 1 | 8),
-        "fc1_bwd[dX-nody2t]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
-                                               ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
-                                               G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
-                                               ptr(b["dy2"]), ptr(b["dy2t"]), s, 1 | 16),
         "fc1_bwd[none]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
                                            ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
                                            G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
@@ -72,6 +70,12 @@ def main():
         "conv2_bwd_data": lambda: k.conv2_bwd_data_l2(ptr(b["dy2t"]), ptr(b["w2t"]), ptr(b["a1"]), B,
                                                       ptr(b["da1m"]), s),
         "conv2_bwd_filter": lambda: k.conv2_bwd_filter(ptr(b["a1pf"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
+        "conv2_bwd_filter_wino": lambda: k.conv2_bwd_filter_wino(ptr(b["a1pf"]), ptr(b["dy2"]), B,
+                                                                  ptr(b["part2"]), s),
+        "grad_finalize_wino": lambda: k.grad_finalize(ptr(b["part2"]), k.conv2_wino_filter_groups(B),
+                                                      ptr(b["part1"]), k.conv1_filter_blocks(B, 1),
+                                                      G("conv2_weight"), G("conv2_bias"),
+                                                      G("conv1_weight"), G("conv1_bias"), s),
         "conv1_bwd_filter": lambda: k.conv1_bwd_filter(ptr(e.train_x), ptr(e.step_dev), e.n_local, B,
                                                        ptr(b["da1m"]), ptr(b["idx1"]), ptr(b["part1"]), s),
         "grad_finalize": lambda: k.grad_finalize(ptr(b["part2"]), k.conv2_filter_splits(B), ptr(b["part1"]),
@@ -120,6 +124,21 @@ def main():
     e1.record()
     e1.synchronize()
     print(f"step (graph replay): {e0.elapsed_time(e1) * 1000.0 / 500:.2f} us")
+    # where the single-rank FC momentum SGD runs: role blocks of the conv2
+    # bwd-data launch (rounds > 0) or the final SGD launch (rounds = 0)
+    for rounds in (0, 2):
+        e.exe.set_fc_sgd_rounds(rounds)
+        e._graphs.clear()
+        e.capture(50)
+        e.train(50)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e.train(500)
+        e1.record()
+        e1.synchronize()
+        print(f"step (graph replay, fc_sgd_rounds={rounds}): "
+              f"{e0.elapsed_time(e1) * 1000.0 / 500:.2f} us")
 
 
 if __name__ == "__main__":

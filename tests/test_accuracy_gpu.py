@@ -44,3 +44,72 @@ def test_native_full_run_matches_oracle_accuracy(cuda_dev, shard, oracle_err, dt
     err = eng.evaluate(shard.test_x, shard.test_y)
     print(f"native {dtype}: final test error {err:.2f}% (oracle {oracle_err:.2f}%) after {steps} steps")
     assert abs(err - oracle_err) <= TOL_POINTS
+
+
+# ---------------------------------------------------------------- LeNet-5
+LENET_TOL_POINTS = 1.0
+
+
+def test_lenet5_native_full_run_matches_oracle_accuracy(cuda_dev):
+    """LeNet-5 (BASELINE config 4) on the v2 CIFAR-shaped task: the native
+    fused executor's full run (2 epochs of the 8192-row shard, 256 steps at
+    B = 64) must end within 1 point of the fp32 PyTorch oracle's (generic
+    engine on the CPU, same data and init).  The oracle must land in 70-95 %,
+    i.e. the task is not separable at a glance."""
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.runtime.lenet_engine import NativeLenetEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_image_shard
+
+    sh = synthetic_image_shard(0, 1, 8192, 2048, (32, 32, 3))
+    cfg = C.TrainConfig(model="lenet5", batch_size=64, graph_steps=16).validate()
+    steps = steps_per_run(sh.train_x.shape[0], cfg.epochs, cfg.batch_size)
+    ref = GenericEngine(C.TrainConfig(model="lenet5", batch_size=64, device="cpu").validate(),
+                        sh.train_x, sh.train_y, torch.device("cpu"))
+    ref.train(steps)
+    acc_ref = 100.0 - ref.evaluate(sh.test_x, sh.test_y)
+    nat = NativeLenetEngine(cfg, sh.train_x, sh.train_y, cuda_dev)
+    nat.train(steps)
+    torch.cuda.synchronize()
+    acc = 100.0 - nat.evaluate(sh.test_x, sh.test_y)
+    print(f"lenet5: native {acc:.2f}% vs CPU oracle {acc_ref:.2f}% after {steps} steps")
+    assert 70.0 < acc_ref < 95.0, "LeNet-5 task too easy / too hard to carry information"
+    assert abs(acc - acc_ref) <= LENET_TOL_POINTS
+
+
+# -------------------------------------------------------------- ResNet-18
+RESNET_STEPS = 200
+RESNET_CURVE_TOL = 0.12  # max |mean loss| gap per 25-step window, fp32 vs bf16
+
+
+def test_resnet18_bf16_tracks_fp32_loss_curve(cuda_dev):
+    """ResNet-18 (BASELINE config 5) on the v2 224x224x3 task: the native bf16
+    MFMA engine's loss curve over 200 steps must track the native fp32
+    engine's (same data, init and batch order) within RESNET_CURVE_TOL per
+    25-step window, both must learn, and the held-out accuracy must be
+    informative (below 100 %)."""
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_images_torch
+
+    tx, ty = synthetic_images_torch(1024, (224, 224, 3), device=cuda_dev)
+    ex, ey = synthetic_images_torch(256, (224, 224, 3), device=cuda_dev, split="test")
+    tx, ty, ex, ey = tx.cpu().numpy(), ty.numpy(), ex.cpu().numpy(), ey.numpy()
+    curves, accs = {}, {}
+    for dt in ("fp32", "bf16"):
+        cfg = C.TrainConfig(model="resnet18", batch_size=16, dtype=dt, graph_steps=25).validate()
+        e = GenericEngine(cfg, tx, ty, cuda_dev)
+        windows = []
+        for _ in range(RESNET_STEPS // 25):
+            losses = []
+            for _ in range(5):
+                e.train(5)
+                losses.append(e.loss_value())
+            windows.append(sum(losses) / len(losses))
+        curves[dt] = windows
+        accs[dt] = 100.0 - e.evaluate(ex, ey)
+    gap = max(abs(a - b) for a, b in zip(curves["fp32"], curves["bf16"]))
+    print(f"resnet18: fp32 curve {[round(v, 3) for v in curves['fp32']]}, bf16 curve "
+          f"{[round(v, 3) for v in curves['bf16']]}, max window gap {gap:.3f}; acc fp32 "
+          f"{accs['fp32']:.1f}% bf16 {accs['bf16']:.1f}%")
+    assert curves["fp32"][-1] < 0.8 * curves["fp32"][0], "fp32 did not learn"
+    assert gap <= RESNET_CURVE_TOL
+    assert accs["fp32"] < 100.0 and accs["bf16"] < 100.0

@@ -250,8 +250,8 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     """Startup autotune of the gradient-sync schedule (runtime/mnist_engine.py:
     tune_schedule) against an emulated 8-rank ring (csrc/collective.h EmuComm):
     every single-communicator schedule (buckets, sharded, factors) is
-    captured and timed, the fastest is kept, and the tuning steps are real
-    steps (step counter advances)."""
+    captured and timed, the fastest is kept, and the trial steps are
+    discarded: params, momentum and the step counter are restored."""
     from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
 
     x, y = data
@@ -260,9 +260,10 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     eng = NativeMnistEngine(cfg, x, y, cuda_dev, comm=comm, force_sync=True)
     assert eng.sync_schedule == "buckets"  # default until tuned
     assert eng.comm2 is None  # auto never builds the two-communicator schedule
+    p0 = eng.params.clone()
     n = eng.tune_schedule()
-    assert n == 3 * 3 * 5 and eng.step == n and n == 3 * 3 * 5
-    assert int(eng.step_dev.item()) == n
+    assert n == 3 * 3 * 5 and eng.step == 0 and int(eng.step_dev.item()) == 0
+    assert torch.equal(eng.params, p0)
     log = eng.tune_log
     assert set(log) == {"buckets", "sharded", "factors"}
     assert eng.sync_schedule == min(log, key=log.get)
