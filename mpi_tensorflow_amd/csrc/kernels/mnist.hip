@@ -1072,9 +1072,13 @@ __device__ __forceinline__ void wino_bwd_loadb(int p, const float* __restrict__ 
   for (int j = 0; j < 16; ++j) b[j] = bp[j * 64];
 }
 
+// c1.part1 != nullptr: each block also computes the conv1 filter-gradient
+// partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
+// values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
+// no second pass over dA1 and no role blocks in the filter-gradient launch.
 __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
     const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
-    int batch, float* __restrict__ da1m, const FcSgd sgd) {
+    int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1) {
   __shared__ float V[WV_FLOATS];
   const int nconv = gridDim.x - sgd.nblk / 2;
   if ((int)blockIdx.x >= nconv) {  // 512-thread blocks: two 256-thread role units
@@ -1147,22 +1151,77 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
           *r = y[o][q][j] + *r;
         }
   }
+  // conv1 band: the padded input rows 8 pg - 2 .. 8 pg + 9 (x 32 columns)
+  // staged next to R while the sums are read; argmax codes loaded early
+  constexpr int C1X = 12 * 32;
+  float* xs1 = V + 4 * 4 * 2 * 4 * 64;
+  float* red1 = xs1 + C1X;  // [7 waves][26 * 32 + 1]
+  const bool do_c1 = c1.part1 != nullptr;
+  const int ci = tid & 31, t = tid >> 5;
+  const int tr = 2 * pg + t / 7, tc = t % 7;
+  const bool own = t < 14 && tr < 7;
+  int q1[4] = {0, 0, 0, 0};
+  if (do_c1) {
+    const long long off = batch_offset_dev(c1.step, c1.n_local, batch);
+    const float* x = c1.data + (off + n) * 784;
+    const int y0 = 8 * pg - 2;
+    if (tid < C1X) {
+      const int yy = y0 + tid / 32, xx = tid % 32 - 2;
+      xs1[tid] = (yy >= 0 && yy < 28 && xx >= 0 && xx < 28) ? x[yy * 28 + xx] : 0.f;
+    }
+    if (own) {
+#pragma unroll
+      for (int o = 0; o < 4; ++o)
+        q1[o] = c1.idx1[((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci];
+    }
+  }
   __syncthreads();
-  {
-    const int ci = tid & 31, t = tid >> 5;
-    const int tr = 2 * pg + t / 7, tc = t % 7;
-    if (t < 14 && tr < 7) {
-      const int q = ci >> 4, l = (t >> 2) * 16 + (ci & 15), j = t & 3;
+  float g1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (own) {
+    const int q = ci >> 4, l = (t >> 2) * 16 + (ci & 15), j = t & 3;
 #pragma unroll
-      for (int o = 0; o < 4; ++o) {
-        float sum = 0.f;
+    for (int o = 0; o < 4; ++o) {
+      float sum = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
-        const size_t oi =
-            ((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci;
-        da1m[oi] = a1[oi] > 0.f ? sum : 0.f;
+      for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
+      const size_t oi =
+          ((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci;
+      g1[o] = a1[oi] > 0.f ? sum : 0.f;
+      da1m[oi] = g1[o];
+    }
+  }
+  if (!do_c1) return;
+  // dW1[t][ci] += dA1 * x[argmax pixel + tap] over the thread's 4 positions
+  float acc[26];
+#pragma unroll
+  for (int k = 0; k < 26; ++k) acc[k] = 0.f;
+  if (own) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      if (g1[o] != 0.f) {
+        const int py = 2 * tr + (o >> 1), px = 2 * tc + (o & 1);
+        const int ly = 2 * py + (q1[o] >> 1) - 8 * pg;  // xs1 row of tap kh = 0
+        const int lx = 2 * px + (q1[o] & 1);            // xs1 col of tap kw = 0
+#pragma unroll
+        for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+          for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += g1[o] * xs1[(ly + kh) * 32 + lx + kw];
+        acc[25] += g1[o];
       }
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], 32, 64);  // tiles 2w, 2w + 1
+  if (wave < 7 && (tid & 32) == 0) {
+#pragma unroll
+    for (int k = 0; k < 26; ++k) red1[wave * (26 * 32 + 1) + k * 32 + ci] = acc[k];
+  }
+  __syncthreads();
+  for (int i = tid; i < 26 * 32; i += WNT) {
+    float sv = 0.f;
+#pragma unroll
+    for (int w = 0; w < 7; ++w) sv += red1[w * (26 * 32 + 1) + i];
+    c1.part1[(size_t)(n * 4 + pg) * 832 + i] = sv;
   }
 }
 
@@ -1849,13 +1908,14 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
 }
 
 void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
-                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd) {
+                                float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd,
+                                const C1FilterArgs* c1) {
   FcSgd sg = fc_sgd_args(fc_sgd);
   // the SGD role works in 256-thread units: two per 512-thread block
   const int role_blocks = (sg.nblk + 1) / 2;
   sg.nblk = 2 * role_blocks;
   conv2_bwd_data_wino_kernel<<<batch * 4 + role_blocks, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m,
-                                                                     sg);
+                                                                     sg, c1_args(c1));
 }
 
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
@@ -1869,7 +1929,8 @@ void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, floa
 }
 
 int conv1_filter_blocks(int batch, int split) {
-  if (split != C1F_SPLIT && split != 1) throw std::runtime_error("conv1 filter split: 1 or 7");
+  if (split != C1F_SPLIT && split != 1 && split != 4)
+    throw std::runtime_error("conv1 filter split: 1, 4 (Winograd bwd-data bands) or 7");
   return batch * split;
 }
 

@@ -90,19 +90,20 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
                         P<float>(p.dy2t), s, factors ? 1 : 7);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
-  if (p.wino)
-    mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
-                                      P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
-  else
-    mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
-                                    P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
-  // conv1 filter grad (needs dA1 from bwd-data) as role blocks of this launch
+  // conv1 filter grad: Winograd - in the bwd-data blocks' epilogue, from the
+  // dA1 values they produce; direct - role blocks of the filter-grad launch
   const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
                                P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                P<float>(p.part1)};
   if (p.wino)
+    mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
+                                      P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd, &c1);
+  else
+    mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
+                                    P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
+  if (p.wino)
     mnist::launch_conv2_bwd_filter_wino(P<const float>(p.a1pf), P<const float>(p.dy2), B,
-                                        P<float>(p.part2), s, &c1);
+                                        P<float>(p.part2), s);
   else
     mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
                                    P<float>(p.part2), s, &c1);
@@ -169,9 +170,9 @@ int MnistExecutor::conv2_groups() const {
                  : mnist::conv2_filter_splits(p_.batch);
 }
 
-// the Winograd filter launch runs the conv1 filter grad as whole-image units
+// the Winograd bwd-data blocks produce one conv1 partial per band of 4 a1 rows
 int MnistExecutor::conv1_blocks() const {
-  return mnist::conv1_filter_blocks(p_.batch, (p_.wino && !p_.bf16) ? 1 : 7);
+  return mnist::conv1_filter_blocks(p_.batch, (p_.wino && !p_.bf16) ? 4 : 7);
 }
 
 void MnistExecutor::forward_backward(hipStream_t s) {
