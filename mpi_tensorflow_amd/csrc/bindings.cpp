@@ -274,10 +274,16 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("conv_fwd_stem_bf16", [](const gops::ConvShape& s1, const gops::ConvShape& si,
-                                 uintptr_t x, uintptr_t wtb, uintptr_t yb, uintptr_t st) {
-    gops::conv_fwd_stem_bf16(s1, si, P<const float>(x), P<const void>(wtb), P<void>(yb), S(st));
+                                 uintptr_t x, uintptr_t wtb, uintptr_t yb, uintptr_t st,
+                                 uintptr_t stats_part, int stats_rows, uintptr_t stats_shift) {
+    const gops::ConvStats cs{P<float>(stats_part), stats_rows, P<const float>(stats_shift)};
+    gops::conv_fwd_stem_bf16(s1, si, P<const float>(x), P<const void>(wtb), P<void>(yb), S(st),
+                             &cs);
     check_launch();
-  });
+  }, py::arg("s1"), py::arg("si"), py::arg("x"), py::arg("wtb"), py::arg("yb"), py::arg("st"),
+     py::arg("stats_part") = 0, py::arg("stats_rows") = 0, py::arg("stats_shift") = 0);
+  g.def("conv_fwd_stats_rows", &gops::conv_fwd_stats_rows);
+  g.def("conv_fwd_stem_stats_rows", &gops::conv_fwd_stem_stats_rows);
   g.def("conv_bwd_filter_stem_bf16",
         [](const gops::ConvShape& s1, const gops::ConvShape& si, uintptr_t x, uintptr_t dyb,
            uintptr_t ws, uintptr_t dw, uintptr_t st) {
@@ -291,13 +297,17 @@ PYBIND11_MODULE(_C, m) {
   });
   g.def("conv_fwd", [](const gops::ConvShape& s, uintptr_t x, uintptr_t w, uintptr_t b, uintptr_t y,
                        bool relu, uintptr_t ws, uintptr_t st, bool bf16, uintptr_t xb,
-                       uintptr_t wtb, uintptr_t yb) {
+                       uintptr_t wtb, uintptr_t yb, uintptr_t stats_part, int stats_rows,
+                       uintptr_t stats_shift) {
+    const gops::ConvStats cs{P<float>(stats_part), stats_rows, P<const float>(stats_shift)};
     gops::conv_fwd(s, P<const float>(x), P<const float>(w), P<const float>(b), P<float>(y), relu,
-                   P<float>(ws), S(st), bf16, P<const void>(xb), P<const void>(wtb), P<void>(yb));
+                   P<float>(ws), S(st), bf16, P<const void>(xb), P<const void>(wtb), P<void>(yb),
+                   &cs);
     check_launch();
   }, py::arg("s"), py::arg("x"), py::arg("w"), py::arg("b"), py::arg("y"), py::arg("relu"),
      py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0, py::arg("wtb") = 0,
-     py::arg("yb") = 0);
+     py::arg("yb") = 0, py::arg("stats_part") = 0, py::arg("stats_rows") = 0,
+     py::arg("stats_shift") = 0);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
                             uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend,
                             uintptr_t wtb) {
@@ -337,6 +347,17 @@ PYBIND11_MODULE(_C, m) {
                       int mode, uintptr_t ws, uintptr_t st) {
     gops::colsum2(P<const float>(a), P<const float>(b), rows, C, P<float>(s1), P<float>(s2), mode,
                   P<float>(ws), S(st));
+    check_launch();
+  });
+  g.def("bn_fwd_partials", [](uintptr_t part, int nrows, uintptr_t shift, uintptr_t x, long long rows,
+                              int C, uintptr_t gm, uintptr_t bt, uintptr_t res, uintptr_t y,
+                              uintptr_t mean, uintptr_t rstd, float eps, float momentum, bool relu,
+                              uintptr_t rmean, uintptr_t rvar, uintptr_t st, uintptr_t yb,
+                              bool x_bf16) {
+    gops::bn_fwd_partials(P<const float>(part), nrows, P<const float>(shift), P<const void>(x), rows, C,
+                          P<const float>(gm), P<const float>(bt), P<const float>(res), P<float>(y),
+                          P<float>(mean), P<float>(rstd), eps, momentum, relu, P<float>(rmean),
+                          P<float>(rvar), S(st), P<void>(yb), x_bf16);
     check_launch();
   });
   g.def("chan_reduce_ok", &gops::chan_reduce_ok);

@@ -223,20 +223,38 @@ __global__ __launch_bounds__(256) void partial1_kernel(const float* __restrict__
   }
 }
 
-// Pass 2: one wave per channel sums its nb contiguous partials (fixed order),
-// lane 0 applies the epilogue.
+// Pass 2: one block per channel sums its nb contiguous partials (fixed
+// order: thread strides, then the waves in order), thread 0 applies the
+// epilogue.  (One wave per channel ran 6.2 us on the ~1.5 K partial rows a
+// conv epilogue writes for ResNet-18 layer 1; one block per channel keeps
+// every load of a thread independent and 4x as many in flight.)
+// grp64: the conv-epilogue layout [2][C / 64][nb][64] (a row of 64 channels
+// per producing wave: coalesced writes), else channel-major [2][C][nb]
 __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__ part, int nb,
-                                                       int C, long long rows, Fin fin) {
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (c >= C) return;
+                                                       int C, long long rows, Fin fin,
+                                                       int grp64) {
+  __shared__ float red[2][4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = grp64 ? (size_t)(c >> 6) * nb * 64 + (c & 63) : (size_t)c * nb;
+  const size_t step = grp64 ? 64 : 1, half = (size_t)C * nb;
+  const float* pa = part + base;
+  const float* pb = part + half + base;
   float a = 0.f, b = 0.f;
-  for (int k = lane; k < nb; k += 64) {
-    a += part[(size_t)c * nb + k];
-    b += part[(size_t)(C + c) * nb + k];
+#pragma unroll 4
+  for (int k = tid; k < nb; k += 256) {
+    a += pa[k * step];
+    b += pb[k * step];
   }
   a = wave_sum(a);
   b = wave_sum(b);
-  if (lane == 0) fin_channel(fin, c, a, b, rows);
+  if (lane == 0) {
+    red[0][wave] = a;
+    red[1][wave] = b;
+  }
+  __syncthreads();
+  if (tid == 0)
+    fin_channel(fin, c, (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]),
+                (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]), rows);
 }
 
 // y = (x - mean) rstd g + b (+ res) (relu); eval: mean / var from running stats
@@ -356,7 +374,7 @@ static void run_partials_t(int mode, const void* a, const float* b, const void* 
     default:
       bn::partial_kernel<bn::BN_BWD, XB, YB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
   }
-  bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, fin);
+  bn::finalize_kernel<<<C, 256, 0, st>>>(ws, nb, C, rows, fin, 0);
 }
 
 static void run_partials(int mode, const void* a, bool ab16, const float* b, const void* y,
@@ -386,7 +404,7 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
   } else {
     const int rpb = (int)((rows + nb - 1) / nb);
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
-    bn::finalize_kernel<<<(C + 3) / 4, 256, 0, st>>>(ws, nb, C, rows, sums(s1, s2));
+    bn::finalize_kernel<<<C, 256, 0, st>>>(ws, nb, C, rows, sums(s1, s2), 0);
   }
 }
 
@@ -417,6 +435,25 @@ void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b
       bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
                                                                   C, relu ? 1 : 0, 1, eps, ybv);
   }
+}
+
+void bn_fwd_partials(const float* part, int P, const float* shift, const void* x, long long rows,
+                     int C, const float* g, const float* b, const float* res, float* y, float* mean,
+                     float* rstd, float eps, float momentum, bool relu, float* rmean, float* rvar,
+                     hipStream_t st, void* yb, bool xb16) {
+  if (C % 64 != 0 || C > 1024 || P < 1 || !part || !shift || shift != rmean)
+    throw std::runtime_error("bn_fwd_partials: needs C % 64 == 0, C <= 1024, shift == rmean");
+  const long long n4 = rows * C / 4;
+  uint2* ybv = reinterpret_cast<uint2*>(yb);
+  // fp32 shift (the running mean, read by fin_channel before its update)
+  const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, shift, 0};
+  bn::finalize_kernel<<<C, 256, 0, st>>>(part, P, C, rows, fin, 1);
+  if (xb16)
+    bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
+                                                               relu ? 1 : 0, 0, eps, ybv);
+  else
+    bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
+                                                                relu ? 1 : 0, 0, eps, ybv);
 }
 
 void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, const float* rstd,

@@ -321,6 +321,26 @@ struct StemLoader {
   }
 };
 
+// BatchNorm statistics in a bf16-output epilogue (ConvStats): lane (r, h) of
+// a wave holds column r of its 32-row tiles; after its own rows are summed
+// the two half-waves combine, and lanes h == 0 write the wave's partial row
+// prow.  Table layout [2][K / 64][P][64]: the 32 lanes store 128 contiguous
+// bytes (a channel-major table made every lane's store its own cache line:
+// +3.6 us per halo conv); every (channel, prow) is written exactly once.
+__device__ __forceinline__ size_t stats_index(int co, int prow, int P) {
+  return ((size_t)(co >> 6) * P + prow) * 64 + (co & 63);
+}
+__device__ __forceinline__ void stats_store(const ConvStats& cs, int K, int co, int prow, int h,
+                                            float s1, float s2) {
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if (h == 0) {
+    const size_t i = stats_index(co, prow, cs.P);
+    cs.part[i] = s1;
+    cs.part[(size_t)K * cs.P + i] = s2;
+  }
+}
+
 template <int BM, int BN, class XT, class LD = Loader<BM, BN, XT>>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restrict__ x,
                                                  const __bf16* __restrict__ wt,
@@ -328,7 +348,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
                                                  float* __restrict__ y, int relu, int kps,
                                                  const float* __restrict__ addend,
                                                  __bf16* __restrict__ yb, int ex2,
-                                                 const ConvShape si) {
+                                                 const ConvShape si, const ConvStats cs) {
   // ex2 (unsplit): the 1x1 stride-2 backward-data - rows are dY pixels
   // (n, a, b), written to dX pixel (2a, 2b) of the 2x-sized output with the
   // other three pixels of its 2x2 block zero (plus addend everywhere)
@@ -344,6 +364,13 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
   const int r = lane & 31, h = lane >> 5;
   LD ld(s, si, x, wt, m0, n0);
+  // BatchNorm shift of this lane's output columns, loaded before the main
+  // loop: an epilogue load issued after the first stores would make the
+  // compiler wait for those stores (vmcnt counts both) before the next ones
+  float kcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    kcol[j] = (yb && cs.part) ? cs.shift[n0 + wn * (BN / 2) + 32 * j + r] : 0.f;
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -400,10 +427,13 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
     return;
   }
   y += (size_t)blockIdx.y * M * s.K;
+  const bool st = yb && cs.part;
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int co = n0 + wn * (BN / 2) + 32 * j + r;
     const float bv = bias ? bias[co] : 0.f;
+    const float kc = kcol[j];
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -413,11 +443,17 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
         float v = acc[i][j][q] + bv;
         if (relu) v = fmaxf(v, 0.f);
         if (addend) v += addend[(size_t)m * s.K + co];  // gradient junction (dX accumulate)
-        if (yb)  // bf16 output (unsplit only): the conv feeds a bf16-input BatchNorm
-          yb[(size_t)m * s.K + co] = (__bf16)v;
-        else
+        if (yb) {  // bf16 output (unsplit only): the conv feeds a bf16-input BatchNorm
+          const __bf16 hv = (__bf16)v;
+          yb[(size_t)m * s.K + co] = hv;
+          const float d = (float)hv - kc;
+          s1 += d;
+          s2 += d * d;
+        } else {
           y[(size_t)m * s.K + co] = v;
+        }
       }
+    if (st) stats_store(cs, s.K, co, (bid % mt) * 2 + wm, h, s1, s2);
   }
 }
 
@@ -469,7 +505,7 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
                                                    const __bf16* __restrict__ wt,
                                                    float* __restrict__ y, int cps,
                                                    const float* __restrict__ addend,
-                                                   __bf16* __restrict__ yb) {
+                                                   __bf16* __restrict__ yb, const ConvStats cs) {
   using h3::ROWB;
   using h3::HCAP;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -528,6 +564,11 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
       h3::glds(src, smem + ins * 8 * ROWB);
     }
   };
+  // BatchNorm shift of this lane's output columns (loaded up front, see fwd_kernel)
+  float kcol[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    kcol[j] = (yb && cs.part) ? cs.shift[n0 + wn * (BN / 2) + 32 * j + r] : 0.f;
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -590,6 +631,10 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
   // once per tile (per element they were ~40 % of the kernel's instructions)
   y += (size_t)blockIdx.y * M * s.K;
   const size_t K = s.K;
+  const bool st = yb && cs.part;
+  float ss1[TN], ss2[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) ss1[j] = ss2[j] = 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
@@ -600,10 +645,17 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
       float* p = y + (size_t)mb * K + co;
       if (yb) {  // bf16 output (unsplit, no addend): feeds a bf16-input BatchNorm
         __bf16* pb = yb + (size_t)mb * K + co;
+        const float kc = kcol[j];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int rr = (q & 3) + 8 * (q >> 2);
-          if (full || mb + rr < M) pb[(size_t)rr * K] = (__bf16)acc[i][j][q];
+          if (full || mb + rr < M) {
+            const __bf16 hv = (__bf16)acc[i][j][q];
+            pb[(size_t)rr * K] = hv;
+            const float d = (float)hv - kc;
+            ss1[j] += d;
+            ss2[j] += d * d;
+          }
         }
       } else if (full && addend) {
         // all 16 addend loads first, then the stores (interleaved, hipcc waited
@@ -628,6 +680,11 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
         }
       }
     }
+  }
+  if (st) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      stats_store(cs, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
   }
 }
 
@@ -1040,12 +1097,19 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(
   }
 }
 
+// cs (with outb): BatchNorm statistics of the bf16 outputs, one partial row
+// per block (C channels, 256 % (C / 4) == 0: a thread keeps one channel quad)
 __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict__ part, int nz,
                                                         long long zs, long long n4,
                                                         float4* __restrict__ out,
                                                         const float4* __restrict__ addend,
-                                                        uint2* __restrict__ outb) {
+                                                        uint2* __restrict__ outb,
+                                                        const ConvStats cs, int C) {
   const long long stride = (long long)gridDim.x * blockDim.x;
+  const bool st = outb && cs.part;
+  const int cq = C >> 2, tid = threadIdx.x;
+  float4 kc = make_float4(0.f, 0.f, 0.f, 0.f), t1 = kc, t2 = kc;
+  if (st) kc = *reinterpret_cast<const float4*>(cs.shift + 4 * (tid % cq));
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
     for (int z = 1; z < nz; ++z) {
@@ -1065,8 +1129,30 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
     if (outb) {
       const __bf16 hv[4] = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w};
       outb[i] = __builtin_bit_cast(uint2, hv);
+      if (st) {
+        const float d[4] = {(float)hv[0] - kc.x, (float)hv[1] - kc.y, (float)hv[2] - kc.z,
+                            (float)hv[3] - kc.w};
+        t1.x += d[0]; t1.y += d[1]; t1.z += d[2]; t1.w += d[3];
+        t2.x += d[0] * d[0]; t2.y += d[1] * d[1]; t2.z += d[2] * d[2]; t2.w += d[3] * d[3];
+      }
     } else {
       out[i] = a;
+    }
+  }
+  if (st) {  // threads tid, tid + cq, ... share a channel quad: fixed-order sum
+    __shared__ float4 red[2][256];
+    red[0][tid] = t1;
+    red[1][tid] = t2;
+    __syncthreads();
+    if (tid < cq) {
+      float4 a = red[0][tid], b = red[1][tid];
+      for (int t = tid + cq; t < 256; t += cq) {
+        a.x += red[0][t].x; a.y += red[0][t].y; a.z += red[0][t].z; a.w += red[0][t].w;
+        b.x += red[1][t].x; b.y += red[1][t].y; b.z += red[1][t].z; b.w += red[1][t].w;
+      }
+      const size_t i = stats_index(4 * tid, blockIdx.x, cs.P);
+      *reinterpret_cast<float4*>(cs.part + i) = a;
+      *reinterpret_cast<float4*>(cs.part + (size_t)C * cs.P + i) = b;
     }
   }
 }
@@ -1097,20 +1183,31 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 // Deterministic sum of nz slabs of n4 float4s into out (fixed association
 // order for a given nz).
 // outb: bf16 output instead of out
-static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st,
-                        const float* addend = nullptr, __bf16* outb = nullptr) {
+// grid of slab_sum4 (also the partial rows of its BatchNorm statistics)
+static inline int slab_blocks(long long n4) {
   long long b = (n4 + 255) / 256;
-  if (b > 4096) b = 4096;
+  return (int)(b > 4096 ? 4096 : b);
+}
+static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st,
+                        const float* addend = nullptr, __bf16* outb = nullptr,
+                        const ConvStats* stats = nullptr, int C = 0) {
+  const long long b = slab_blocks(n4);
   int G = 1;
   if (b < 128 && nz >= 32) {
     G = 8;
     slab_fold4_kernel<<<dim3((int)b, cdiv(nz, G)), 256, 0, st>>>(reinterpret_cast<float4*>(slabs),
                                                                  nz, G, n4);
   }
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (!outb || C % 64 || 256 % (C / 4) || stats->P != b)
+      throw std::runtime_error("slab_reduce: BatchNorm statistics layout mismatch");
+    cs = *stats;
+  }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), cdiv(nz, G),
                                           n4 * G, n4, reinterpret_cast<float4*>(out),
                                           reinterpret_cast<const float4*>(addend),
-                                          reinterpret_cast<uint2*>(outb));
+                                          reinterpret_cast<uint2*>(outb), cs, C);
 }
 
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
@@ -1151,12 +1248,27 @@ static inline long long wt_elems(const ConvShape& s) { return (long long)s.R * s
 // bf16 weight copy at the front of the workspace, split-K slabs after it
 static inline long long wt_floats(const ConvShape& s) { return ((wt_elems(s) + 127) / 128) * 64; }
 
+// partial rows of the BatchNorm statistics the forward writes (plan-dependent)
+static int stats_rows(const ConvShape& s, bool epilogue) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const Plan p = plan(s, epilogue);
+  if (p.z > 1) return slab_blocks(M * s.K / 4);
+  return cdiv(M, tm(p.t)) * 2;
+}
+
 template <class XT>
 static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const float* bias,
                    float* y, bool relu, float* ws, hipStream_t st,
-                   const float* addend = nullptr, __bf16* yb = nullptr, int ex2 = 0) {
+                   const float* addend = nullptr, __bf16* yb = nullptr, int ex2 = 0,
+                   const ConvStats* stats = nullptr) {
   const long long M = (long long)s.N * s.OH * s.OW;
   const Plan p = plan(s, bias != nullptr || relu || ex2);  // ex2: never split
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (!yb || bias || relu || ex2 || stats->P != stats_rows(s, false))
+      throw std::runtime_error("conv fwd: BatchNorm statistics need a plain bf16-output conv");
+    if (p.z == 1) cs = *stats;
+  }
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const float* add = p.z > 1 ? nullptr : addend;  // split-K: added by the slab reduction
@@ -1164,13 +1276,13 @@ static void launch(const ConvShape& s, const XT* x, const __bf16* wt, const floa
   const int r = relu ? 1 : 0;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), p.z)
   switch (p.t) {
-    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
-    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
-    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
-    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s); break;
+    case T128x128: fwd_kernel<128, 128, XT><<<GRID(128, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s, cs); break;
+    case T128x64: fwd_kernel<128, 64, XT><<<GRID(128, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s, cs); break;
+    case T64x128: fwd_kernel<64, 128, XT><<<GRID(64, 128), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s, cs); break;
+    default: fwd_kernel<64, 64, XT><<<GRID(64, 64), NT, 0, st>>>(s, x, wt, bias, out, r, p.kps, add, ob, ex2, s, cs); break;
   }
 #undef GRID
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb, stats, s.K);
 }
 
 // halo conv: 3x3, stride 1, pad 1, C and K % 64 == 0, a 128-pixel tile's
@@ -1200,20 +1312,33 @@ static inline P3 plan3(const ConvShape& s) {
   const int cps = cdiv(nch, z);
   return {cdiv(nch, cps), cps, 64};
 }
-static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
-                    hipStream_t st, const float* addend, __bf16* yb = nullptr) {
+static int stats_rows3(const ConvShape& s) {
   const long long M = (long long)s.N * s.H * s.W;
   const P3 p = plan3(s);
+  if (p.z > 1) return slab_blocks(M * s.K / 4);
+  return cdiv(M, p.bm) * 2;
+}
+static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
+                    hipStream_t st, const float* addend, __bf16* yb = nullptr,
+                    const ConvStats* stats = nullptr) {
+  const long long M = (long long)s.N * s.H * s.W;
+  const P3 p = plan3(s);
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (!yb || addend || stats->P != stats_rows3(s))
+      throw std::runtime_error("conv3: BatchNorm statistics need a plain bf16-output conv");
+    if (p.z == 1) cs = *stats;
+  }
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const dim3 grid(cdiv(M, p.bm) * (s.K / 64), p.z);
   const float* add = p.z > 1 ? nullptr : addend;
   __bf16* ob = p.z > 1 ? nullptr : yb;
   if (p.bm == 128)
-    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob);
+    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs);
   else
-    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob);
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb);
+    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb, stats, s.K);
 }
 
 // 3x3 / stride 2 / pad 1 dgrad on an even input (the halo form above)
@@ -1678,9 +1803,20 @@ void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t
   cbf::wcvt_batch_kernel<<<(int)nblocks, 256, 0, st>>>(jobs, njobs);
 }
 
+int conv_fwd_stats_rows(const ConvShape& s) {
+  using namespace cbf;
+  if (!conv_fwd_bf16_ok(s)) throw std::runtime_error("conv_fwd_stats_rows: not a bf16-family conv");
+  return conv3_ok(s) ? stats_rows3(s) : stats_rows(s, false);
+}
+
+int conv_fwd_stem_stats_rows(const ConvShape& s1) {
+  using namespace cbf;
+  return cdiv((long long)s1.N * s1.OH * s1.OW, 128) * 2;
+}
+
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb, const void* wtb,
-                   void* yb) {
+                   void* yb, const ConvStats* stats) {
   using namespace cbf;
   if (!conv_fwd_bf16_ok(s) || !ws) throw std::runtime_error("conv_fwd_bf16: unsupported shape");
   const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
@@ -1690,12 +1826,15 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
     wt = wc;
   }
   __bf16* ob = reinterpret_cast<__bf16*>(yb);
+  // statistics rows are planned for the halo kernel whenever it takes the shape
+  if (stats && stats->part && conv3_ok(s) && !(xb && !bias && !relu))
+    throw std::runtime_error("conv_fwd_bf16: statistics need the bf16 input of a plain halo conv");
   if (xb && !bias && !relu && conv3_ok(s))
-    launch3(s, reinterpret_cast<const __bf16*>(xb), wt, y, ws, st, nullptr, ob);
+    launch3(s, reinterpret_cast<const __bf16*>(xb), wt, y, ws, st, nullptr, ob, stats);
   else if (xb)
-    launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st, nullptr, ob);
+    launch(s, reinterpret_cast<const __bf16*>(xb), wt, bias, y, relu, ws, st, nullptr, ob, 0, stats);
   else
-    launch(s, x, wt, bias, y, relu, ws, st, nullptr, ob);
+    launch(s, x, wt, bias, y, relu, ws, st, nullptr, ob, 0, stats);
 }
 
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
@@ -1780,15 +1919,21 @@ static void stem_check(const ConvShape& s1, const ConvShape& si) {
 }
 
 void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x, const void* wtb,
-                        void* yb, hipStream_t st) {
+                        void* yb, hipStream_t st, const ConvStats* stats) {
   using namespace cbf;
   stem_check(s1, si);
   const long long M = (long long)s1.N * s1.OH * s1.OW;
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (stats->P != conv_fwd_stem_stats_rows(s1))
+      throw std::runtime_error("stem conv: BatchNorm statistics layout mismatch");
+    cs = *stats;
+  }
   // 128 x 64 tiles: M = 401 K pixels at B = 32 (3136 blocks), no split
   fwd_kernel<128, 64, float, StemLoader<128, 64>>
       <<<dim3(cdiv(M, 128) * (s1.K / 64), 1), NT, 0, st>>>(
           s1, x, reinterpret_cast<const __bf16*>(wtb), nullptr, nullptr, 0, s1.C / BK, nullptr,
-          reinterpret_cast<__bf16*>(yb), 0, si);
+          reinterpret_cast<__bf16*>(yb), 0, si, cs);
 }
 
 void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,

@@ -24,9 +24,21 @@ struct PoolShape {
 // wtb (optional, bf16 family): the weights already laid out by wcvt_batch
 // (forward copy for conv_fwd, stride-1 dgrad copy for conv_bwd_data)
 // yb (optional, bf16 family only): write the output as bf16 there instead of y
+// BatchNorm statistics from a bf16-output conv (the bf16 family's epilogue,
+// or its split-K reduction): partial sums of (y - shift[c]) and
+// (y - shift[c])^2 over the output rows, part [2][K / 64][P][64] with P =
+// conv_fwd_stats_rows(s) (y = the bf16-rounded outputs the BatchNorm reads;
+// shift = the BatchNorm's running mean).  Consumed by bn_fwd_partials.
+struct ConvStats {
+  float* part = nullptr;
+  int P = 0;
+  const float* shift = nullptr;
+};
+int conv_fwd_stats_rows(const ConvShape& s);  // bf16 family, bf16 output, no bias / ReLU
+int conv_fwd_stem_stats_rows(const ConvShape& s1);
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
               bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr,
-              const void* wtb = nullptr, void* yb = nullptr);
+              const void* wtb = nullptr, void* yb = nullptr, const ConvStats* stats = nullptr);
 // addend (optional, bf16 / tiled families): a gradient that joins dX at this
 // tensor (a residual branch), added in the epilogue: dx = conv + addend
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
@@ -50,12 +62,13 @@ void im2col_bf16(const ConvShape& s, const float* x, int kp, void* col, hipStrea
 // GEMM shape over kp channels, si = the image conv, x = fp32 NHWC image,
 // wtb = stem_weight_bf16 layout; yb = bf16 output; dw = padded [kp][K] grad
 void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x, const void* wtb,
-                        void* yb, hipStream_t st);
+                        void* yb, hipStream_t st, const ConvStats* stats = nullptr);
 void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,
                                const void* dyb, float* ws, float* dw, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr,
-                   const void* wtb = nullptr, void* yb = nullptr);
+                   const void* wtb = nullptr, void* yb = nullptr,
+                   const ConvStats* stats = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                         hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr,
                         const void* wtb = nullptr);
@@ -105,6 +118,13 @@ void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b
             float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
             void* yb = nullptr,  // yb: optional bf16 copy of y
             bool xb16 = false);
+// training forward from the statistics a conv epilogue already wrote
+// (ConvStats part [2][C][P] of (x - shift), shift = rmean before the update):
+// finalize + apply only, no statistics pass over x
+void bn_fwd_partials(const float* part, int P, const float* shift, const void* x, long long rows,
+                     int C, const float* g, const float* b, const float* res, float* y, float* mean,
+                     float* rstd, float eps, float momentum, bool relu, float* rmean, float* rvar,
+                     hipStream_t st, void* yb = nullptr, bool xb16 = false);
 // dg = sum dy' xhat, db = sum dy', dx, and dres = dy' (dy' = dy [y > 0] if relu);
 // dx (fp32) and dxb (bf16) are each optional, at least one is required;
 // y (the ReLU mask) is the fp32 output, or its bf16 twin when yb16

@@ -889,10 +889,11 @@ static inline bool conv_fwd_direct_ok(const ConvShape& s) {
 // (LeNet-5's 3- and 6-channel layers, thin FC layers).
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
               bool relu, float* ws, hipStream_t st, bool bf16, const void* xb, const void* wtb,
-              void* yb) {
+              void* yb, const ConvStats* stats) {
   if (bf16 && conv_fwd_bf16_ok(s))
-    return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb, wtb, yb);
+    return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb, wtb, yb, stats);
   if (yb) throw std::runtime_error("conv_fwd: bf16 output needs the bf16 conv family");
+  if (stats && stats->part) throw std::runtime_error("conv_fwd: statistics need the bf16 family");
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
   if (conv_fwd_direct_ok(s)) {
     const long long total = (long long)s.N * s.OH * s.OW * s.K;

@@ -167,8 +167,13 @@ class ResNet18(GenericModel):
                                 res_join=res_join, twin_only=twin_only)
 
         # every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
-        # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise
-        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True)
+        # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise, and in
+        # training its epilogue also writes that BatchNorm's batch statistics
+        # (shifted by the running mean: Fn.conv2d bn_shift)
+        def sh(nm):
+            return bn[nm][0] if training else None
+
+        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True, bn_shift=sh("bn1"))
         h = BN(h, "bn1", True, twin_only=True)  # the pool reads its bf16 twin
         h = Fn.maxpool(h, 3, 2, 1)
         join = x.is_cuda and training and torch.is_grad_enabled()
@@ -178,12 +183,12 @@ class ResNet18(GenericModel):
             # so its backward comes first
             j = Fn.GradJoin() if join else None
             o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final",
-                          out_bf16=True)
+                          out_bf16=True, bn_shift=sh(name + "n1"))
             o = BN(o, name + "n1", True, twin_only=True)  # only conv c2 reads it
-            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True)
+            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True, bn_shift=sh(name + "n2"))
             if down:
                 sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash",
-                               out_bf16=True)
+                               out_bf16=True, bn_shift=sh(name + "nd"))
                 h = BN(o, name + "n2", True, res=BN(sc, name + "nd", False))
             else:
                 h = BN(o, name + "n2", True, res=h, res_join=j)

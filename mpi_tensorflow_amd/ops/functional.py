@@ -151,6 +151,21 @@ def _bf16_copy(t: torch.Tensor, s) -> torch.Tensor:
     return tb
 
 
+# BatchNorm statistics written by the producing conv's epilogue (bf16 conv
+# mode): the channel-major partial sums of (y - shift) / (y - shift)^2 with
+# shift = the consuming BatchNorm's running mean, attached to the conv output
+# like the bf16 twins (valid while the tensor is unmodified).
+def _attach_bnstats(t: torch.Tensor, part: torch.Tensor, rows: int, shift: torch.Tensor) -> None:
+    t._mta_bnstats = (part, rows, shift, t._version, t.data_ptr())
+
+
+def _bnstats(t: torch.Tensor, rmean: torch.Tensor):
+    a = getattr(t, "_mta_bnstats", None)
+    if a is not None and a[2] is rmean and a[3] == t._version and a[4] == t.data_ptr():
+        return a[0], a[1]
+    return None
+
+
 def _bf16_out(like: torch.Tensor) -> Optional[torch.Tensor]:
     """A bf16 twin for a BN output when a bf16 conv can consume it."""
     if not _CONV_BF16 or like.shape[-1] % 64 != 0:
@@ -191,7 +206,7 @@ class GradJoin:
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None, wtb=None,
-                wtb_d=None, out_bf16=False):
+                wtb_d=None, out_bf16=False, bn_shift=None):
         C = native()
         x = x.contiguous()
         ctx.bf16 = _CONV_BF16
@@ -204,8 +219,15 @@ class _ConvFn(torch.autograd.Function):
         # out_bf16: the output is stored as bf16 (it feeds a bf16-input BatchNorm)
         oshape = (shape.N, shape.OH, shape.OW, shape.K)
         y = torch.empty(oshape, dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
+        part, rows = None, 0
+        if out_bf16 and bn_shift is not None:  # the consuming BatchNorm's statistics
+            rows = C.ops.conv_fwd_stats_rows(shape)
+            part = torch.empty(2 * shape.K * rows, dtype=torch.float32, device=x.device)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), 0 if out_bf16 else ptr(y), relu, ptr(ws), s,
-                       ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0)
+                       ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0, ptr(part), rows,
+                       ptr(bn_shift) if part is not None else 0)
+        if part is not None:
+            _attach_bnstats(y, part, rows, bn_shift)
         ctx.save_for_backward(x, w, y, xb)
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
@@ -235,7 +257,7 @@ class _ConvFn(torch.autograd.Function):
                     dx = None
                 elif ctx.role == "final" and add is None:
                     ctx.join.out = dx
-            return dx, None, None, None, None, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None, None, None, None, None
         if ctx.relu:
             dym = torch.empty_like(dy)
             C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
@@ -262,7 +284,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = None
             elif ctx.role == "final" and add is None:
                 ctx.join.out = dx
-        return dx, None, None, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvIm2colFn(torch.autograd.Function):
@@ -275,7 +297,7 @@ class _ConvIm2colFn(torch.autograd.Function):
     stem)."""
 
     @staticmethod
-    def forward(ctx, x, w, shape, gw, ws, kp, out_bf16=False):
+    def forward(ctx, x, w, shape, gw, ws, kp, out_bf16=False, bn_shift=None):
         C = native()
         x = x.contiguous()
         sh = shape
@@ -293,7 +315,14 @@ class _ConvIm2colFn(torch.autograd.Function):
         # column matrix is materialised
         ctx.implicit = bool(out_bf16)
         if ctx.implicit:
-            C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s)
+            part, rows = None, 0
+            if bn_shift is not None:  # the consuming BatchNorm's statistics
+                rows = C.ops.conv_fwd_stem_stats_rows(s1)
+                part = torch.empty(2 * sh.K * rows, dtype=torch.float32, device=x.device)
+            C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s, ptr(part), rows,
+                                     ptr(bn_shift) if part is not None else 0)
+            if part is not None:
+                _attach_bnstats(y, part, rows, bn_shift)
             ctx.save_for_backward(x)
         else:
             col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
@@ -319,7 +348,7 @@ class _ConvIm2colFn(torch.autograd.Function):
             C.ops.conv_bwd_filter(s1, 0, 0, ptr(ctx.ws), ptr(gpad), s, True, ptr(src), ptr(dyb))
         C.ops.stem_wgrad(ptr(gpad), ctx.R, ctx.sc, ctx.seg, s1.K, ptr(ctx.gw), s)
         _grad_done(ctx.gw)
-        return None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None
 
 
 def _im2col_kp(sh, x: torch.Tensor, has_bias: bool, relu: bool) -> int:
@@ -365,13 +394,16 @@ _WS = ConvWorkspace()
 
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: int = 0,
            relu: bool = False, join: Optional[GradJoin] = None,
-           join_role: Optional[str] = None, out_bf16: bool = False) -> torch.Tensor:
+           join_role: Optional[str] = None, out_bf16: bool = False,
+           bn_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K].  join / join_role
     ("stash" | "final"): fuse the gradient sum at x with another branch (see
     GradJoin).  out_bf16: store the output as bf16 when the bf16 conv family
     runs it (no bias / ReLU epilogue) - for a conv whose only consumer is
-    `batchnorm`, which reads bf16 input.  Both are GPU only, ignored on the
-    CPU path."""
+    `batchnorm`, which reads bf16 input.  bn_shift (training): that
+    BatchNorm's running mean - a bf16-output conv then also writes the batch
+    statistics in its epilogue (shifted by it) and the BatchNorm skips its
+    statistics pass.  All GPU only, ignored on the CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
     if x.is_cuda:
@@ -382,7 +414,8 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
         if kp:
             s1 = C.ops.ConvShape(N, sh.OH, sh.OW, kp, K, 1, 1, 1, 0)
             ws = _WS.get(max(C.ops.conv_ws_floats(s1, False), 4), x.device)
-            return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob)
+            return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob,
+                                       bn_shift if ob else None)
         ob = ob and C.ops.conv_bf16_ok(sh)
         nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
                   C.ops.chan_reduce_ws_floats(N * sh.OH * sh.OW, K), 4)
@@ -392,7 +425,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
                              None if b is None else b.grad_view, ws, join, join_role, w.wtb,
-                             w.wtb_d, ob)
+                             w.wtb_d, ob, bn_shift if ob else None)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y
@@ -459,10 +492,17 @@ class _BNFn(torch.autograd.Function):
         # twin_only: the only consumer is a bf16 conv, so only the bf16 twin is
         # written (y's fp32 storage stays unwritten; the twin is attached)
         yf = None if (twin_only and yb is not None) else y
-        # batch statistics, running-stat update and the fused apply, on device
-        C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(yf), ptr(mean), ptr(rstd),
-                     ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar), stream_handle(),
-                     ptr(yb), xb16)
+        # batch statistics, running-stat update and the fused apply, on device;
+        # the statistics come from the producing conv's epilogue when it wrote them
+        st = _bnstats(x, rmean)
+        if st is not None:
+            C.ops.bn_fwd_partials(ptr(st[0]), st[1], ptr(rmean), ptr(x), rows, Cc, ptr(g), ptr(b),
+                                  ptr(res), ptr(yf), ptr(mean), ptr(rstd), eps, momentum, relu,
+                                  ptr(rmean), ptr(rvar), stream_handle(), ptr(yb), xb16)
+        else:
+            C.ops.bn_fwd(ptr(x), rows, Cc, ptr(g), ptr(b), ptr(res), ptr(yf), ptr(mean), ptr(rstd),
+                         ptr(ws), eps, momentum, relu, True, ptr(rmean), ptr(rvar),
+                         stream_handle(), ptr(yb), xb16)
         if yb is not None:
             _attach_bf16(y, yb)
         # the backward's ReLU mask reads the bf16 twin when there is one (same signs)

@@ -48,12 +48,15 @@ class SegmentTimer:
         self._open = None
 
     def collect(self) -> None:
-        """Fold the closed segments (their end events have completed once
-        the caller has synchronised)."""
+        """Fold the closed segments (waits for their end events)."""
         for ev0, ev1, host, steps in self._done:
             self.host_s += host
             self.steps += steps
-            self.device_ms += ev0.elapsed_time(ev1) if self.cuda else host * 1e3
+            if self.cuda:
+                ev1.synchronize()  # recorded after the segment's last device sync
+                self.device_ms += ev0.elapsed_time(ev1)
+            else:
+                self.device_ms += host * 1e3
         self._done = []
 
     def step_ms(self) -> float:

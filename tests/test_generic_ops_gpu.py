@@ -534,6 +534,49 @@ def test_conv_bf16_output_and_bf16_grad(cuda_dev, N, H, Cin, K, R, stride, pad):
         assert _rel(xg.grad.cpu(), xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,Cin,K,R,stride,pad", [
+    (4, 14, 64, 64, 3, 1, 1),     # halo conv, unsplit: statistics in its epilogue
+    (4, 7, 512, 512, 3, 1, 1),    # halo conv, split-K: in the slab reduction
+    (2, 14, 64, 128, 3, 2, 1),    # generic bf16 forward epilogue
+    (2, 14, 64, 128, 1, 2, 0),    # 1x1 stride-2 downsample
+    (2, 20, 3, 64, 7, 2, 3),      # stem: implicit-im2col epilogue
+])
+def test_conv_epilogue_bn_statistics(cuda_dev, N, H, Cin, K, R, stride, pad):
+    """A bf16-output conv given the consuming BatchNorm's running mean
+    (bn_shift) writes the batch statistics in its epilogue and the BatchNorm
+    skips its own statistics pass: the BN output, the running statistics and
+    the gradients match the two-pass BatchNorm on the same conv output."""
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, H, H, Cin, generator=g).to(cuda_dev)
+    w = (torch.randn(R, R, Cin, K, generator=g) * 0.1).to(cuda_dev)
+    gam = (torch.rand(K, generator=g) + 0.5).to(cuda_dev)
+    bet = torch.randn(K, generator=g).to(cuda_dev)
+    rm0 = (torch.randn(K, generator=g) * 0.3).to(cuda_dev)  # a nonzero shift
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, OH, OH, K, generator=g).to(cuda_dev)
+    out = []
+    Fn.set_conv_bf16(True)
+    try:
+        for fused in (False, True):
+            xi = x.clone().requires_grad_(Cin % 4 == 0)
+            wp, gp, bp = _param(w), _param(gam), _param(bet)
+            rm, rv = rm0.clone(), torch.ones(K, device=cuda_dev)
+            y = Fn.conv2d(xi, wp, None, stride, pad, False, out_bf16=True,
+                          bn_shift=rm if fused else None)
+            assert (Fn._bnstats(y, rm) is not None) == fused
+            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True)
+            h.backward(dy)
+            out.append((h.detach().clone(), rm.clone(), rv.clone(), wp.grad_view.clone(),
+                        gp.grad_view.clone(), bp.grad_view.clone()))
+    finally:
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    (h0, m0, v0, gw0, gg0, gb0), (h1, m1, v1, gw1, gg1, gb1) = out
+    assert _rel(h1, h0) < 2e-5
+    assert _rel(m1, m0) < 1e-5 and _rel(v1, v0) < 1e-5
+    assert _rel(gw1, gw0) < 1e-4 and _rel(gg1, gg0) < 1e-4 and _rel(gb1, gb0) < 1e-5
+
+
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
 def test_batchnorm_bf16_input(cuda_dev, relu, res):
     """BN over a bf16 input (a bf16-output conv's activations): statistics,
