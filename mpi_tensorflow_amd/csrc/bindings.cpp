@@ -448,11 +448,15 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("gather_batch", [](uintptr_t data, uintptr_t labels, uintptr_t step, int n_local, int batch,
-                           long long row_elems, uintptr_t xb, uintptr_t yb, uintptr_t st) {
+                           long long row_elems, uintptr_t xb, uintptr_t yb, uintptr_t st,
+                           float lr_base, float lr_decay, uintptr_t lr_out) {
     gops::gather_batch(P<const float>(data), P<const int>(labels), P<const long long>(step), n_local,
-                       batch, row_elems, P<float>(xb), P<int>(yb), S(st));
+                       batch, row_elems, P<float>(xb), P<int>(yb), S(st), lr_base, lr_decay,
+                       P<float>(lr_out));
     check_launch();
-  });
+  }, py::arg("data"), py::arg("labels"), py::arg("step"), py::arg("n_local"), py::arg("batch"),
+     py::arg("row_elems"), py::arg("xb"), py::arg("yb"), py::arg("st"), py::arg("lr_base") = 0.f,
+     py::arg("lr_decay") = 1.f, py::arg("lr_out") = 0);
 
   // ------------------------------------------------------------ executor
   py::class_<MnistPtrs>(m, "MnistPtrs")

@@ -162,7 +162,9 @@ void linear_bwd(const float* x, const float* w, const float* y, const float* dy,
                 float* db, float* dx, int M, int K, int N, bool relu, hipStream_t st);
 void lr_from_step(const long long* step, int n_local, int batch, float base, float decay,
                   float* lr, hipStream_t st);
+// lr_out (optional): also writes the learning rate of that step (as lr_from_step)
 void gather_batch(const float* data, const int* labels, const long long* step, int n_local,
-                  int batch, long long row_elems, float* xb, int* yb, hipStream_t st);
+                  int batch, long long row_elems, float* xb, int* yb, hipStream_t st,
+                  float lr_base = 0.f, float lr_decay = 1.f, float* lr_out = nullptr);
 
 }  // namespace gops

@@ -736,13 +736,18 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(
 }
 
 // batch gather from a device-resident dataset at the device-step offset
+// lr_out (optional): also the step's learning rate of the reference schedule
+// (mpipy.py:59-64), so the SGD that follows needs no LR launch of its own
 __global__ __launch_bounds__(256) void gather_batch_kernel(const float* __restrict__ data,
                                                            const int* __restrict__ labels,
                                                            const long long* step, int n_local,
                                                            int batch, long long row_elems,
                                                            float* __restrict__ xb,
-                                                           int* __restrict__ yb) {
+                                                           int* __restrict__ yb, float lr_base,
+                                                           float lr_decay, float* lr_out) {
   const long long s = step ? *step : 0;
+  if (lr_out && blockIdx.x == 0 && threadIdx.x == 0)
+    lr_out[0] = lr_base * powf(lr_decay, (float)((s * batch) / n_local));
   const long long off = (s * batch) % (long long)(n_local - batch);
   const long long n = (long long)batch * row_elems;
   const long long stride = (long long)gridDim.x * blockDim.x;
@@ -1179,10 +1184,11 @@ void lr_from_step(const long long* step, int n_local, int batch, float base, flo
 }
 
 void gather_batch(const float* data, const int* labels, const long long* step, int n_local,
-                  int batch, long long row_elems, float* xb, int* yb, hipStream_t st) {
+                  int batch, long long row_elems, float* xb, int* yb, hipStream_t st,
+                  float lr_base, float lr_decay, float* lr_out) {
   if (row_elems % 4 != 0 || batch > 256) throw std::runtime_error("gather_batch: unsupported shape");
   gather_batch_kernel<<<grid1d((long long)batch * row_elems / 4), 256, 0, st>>>(
-      data, labels, step, n_local, batch, row_elems, xb, yb);
+      data, labels, step, n_local, batch, row_elems, xb, yb, lr_base, lr_decay, lr_out);
 }
 
 }  // namespace gops

@@ -83,7 +83,8 @@ class GenericModel:
                 raise ValueError(s.init)
 
     def make_bn_state(self, device) -> Dict[str, Tuple[torch.Tensor, torch.Tensor]]:
-        return {k: (torch.zeros(c, device=device), torch.ones(c, device=device))
+        # built on the host and copied (no device fill kernels)
+        return {k: (torch.zeros(c).to(device), torch.ones(c).to(device))
                 for k, c in self.bn_channels.items()}
 
 

@@ -62,8 +62,10 @@ class GenericEngine:
         host = torch.zeros(self.layout.total)
         self.model.init_params(host, cfg.seed)
         self.params = host.to(device).requires_grad_(True)
-        self.grads = torch.zeros(self.layout.total, device=device)
-        self.mom = torch.zeros(self.layout.total, device=device)
+        # zero state built on the host and copied: no device fill kernels (the
+        # profiles' only at::native launches were these start-up fills)
+        self.grads = torch.zeros(self.layout.total).to(device)
+        self.mom = torch.zeros(self.layout.total).to(device)
         pv = self.layout.views(self.params)
         gv = self.layout.views(self.grads)
         self.P = {s.name: Fn.Param(pv[s.name], gv[s.name]) for s in self.layout.specs}
@@ -81,7 +83,7 @@ class GenericEngine:
         self._graphs = {}
         self._graph_loss = {}
         self._warm = False
-        self.loss_buf = torch.zeros((), device=device)
+        self.loss_buf = torch.zeros(()).to(device)
         self._eval_x = DeviceArrayCache()
         self.bucketer = None
         if self.on_gpu:
@@ -96,9 +98,9 @@ class GenericEngine:
             h, w, c = train_x.shape[1:]
             self.xb = torch.empty(self.B, h, w, c, device=device)
             self.yb = torch.empty(self.B, dtype=torch.int32, device=device)
-            self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
-            self.lr_dev = torch.zeros(1, device=device)
-            self.seed = torch.ones((), device=device)  # backward seed, never written
+            self.step_dev = torch.zeros(1, dtype=torch.int64).to(device)
+            self.lr_dev = torch.zeros(1).to(device)
+            self.seed = torch.ones(()).to(device)  # backward seed, never written
             # bf16: all conv weight copies in one launch per step
             self.wcache = Fn.Bf16Weights(self.P, device) if self.bf16 else None
 
@@ -122,7 +124,7 @@ class GenericEngine:
     def set_step(self, step: int) -> None:
         self.step = int(step)
         if self.on_gpu:
-            self.step_dev.fill_(int(step))
+            self.step_dev.copy_(torch.tensor([int(step)], dtype=torch.int64))
 
     def loss_value(self) -> float:
         t = getattr(self, "_loss_t", None) if self.on_gpu else None
@@ -146,8 +148,11 @@ class GenericEngine:
         row = int(np.prod(self.xb.shape[1:]))
         if self.wcache is not None:
             self.wcache.refresh()
+        # the gather also writes this step's device LR (no separate LR launch)
         C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
-                            self.B, row, ptr(self.xb), ptr(self.yb), s)
+                            self.B, row, ptr(self.xb), ptr(self.yb), s, self.cfg.base_lr,
+                            self.cfg.lr_decay, ptr(self.lr_dev))
+        self._lr_fresh = True
         logits = self.model.forward(self.P, self.bn, self.xb, True)
         loss = Fn.cross_entropy(logits, self.yb)
         # keep the device scalar itself (no copy launch): under graph capture its
@@ -173,12 +178,15 @@ class GenericEngine:
         return gscale
 
     def update_gpu(self, gscale: float) -> None:
-        """Device LR from the device step, then the flat momentum SGD (which
-        bumps the device step)."""
+        """The flat momentum SGD (which bumps the device step) at the device LR
+        the step's batch gather wrote (or a separate LR launch when no gather
+        of this step ran since the last update)."""
         C_ = self._C
         s = stream_handle()
-        C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
-                            self.cfg.lr_decay, ptr(self.lr_dev), s)
+        if not getattr(self, "_lr_fresh", False):
+            C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
+                                self.cfg.lr_decay, ptr(self.lr_dev), s)
+        self._lr_fresh = False
         C_.optim.sgd_momentum(ptr(self.params), ptr(self.grads), ptr(self.mom), self.layout.total, 0,
                               0.0, self.cfg.momentum, gscale, ptr(self.lr_dev), 0.0,
                               ptr(self.step_dev), s)
