@@ -2012,24 +2012,26 @@ __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, 
   *w -= lr * mv;
 }
 
-// conv2 weights of ONE input channel ci (25 taps x 64 co): slab sums + SGD,
-// then the Winograd transforms of the updated 5x5 filters (U and Ud).  Thread
-// (co4 = tid & 15, tg = tid >> 4) updates taps tg and tg + 16; each slab sum
-// runs in the same order as the 50-block path.
-__device__ void sgd_conv2_wino(const SgdFinArgs& a, int ci, float lr) {
-  __shared__ float wl[25 * 64];
-  const int tid = threadIdx.x, co4 = tid & 15, tg = tid >> 4;
-  for (int t = tg; t < 25; t += 16) {
-    const int i = (t * 32 + ci) * 16 + co4;  // float4 index in the HWIO block
+// conv2 weights of one input channel ci and 16 output channels (block b: ci
+// = b / 4, co quarter b % 4; 25 taps x 4 float4s = 100 threads): slab sums in
+// group order (16 loads in flight), SGD, then the Winograd transforms of the
+// updated 5x5 filters (U and Ud).  128 blocks with short sums: with 32 blocks
+// of 2 taps x 32 groups a thread waited on 8 rounds of 8 loads (9.1 us SGD).
+__device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
+  __shared__ float wl[25 * 16];
+  const int tid = threadIdx.x, ci = blk >> 2, cq = blk & 3;
+  if (tid < 100) {
+    const int t = tid >> 2, c4 = tid & 3;
+    const int i = (t * 32 + ci) * 16 + cq * 4 + c4;  // float4 index in the HWIO block
     const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
     float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
     int z = 0;
-    for (; z + 8 <= a.ngroups; z += 8) {
-      float4 v[8];
+    for (; z + 16 <= a.ngroups; z += 16) {
+      float4 v[16];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+      for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < 16; ++u) {
         sv.x += v[u].x;
         sv.y += v[u].y;
         sv.z += v[u].z;
@@ -2049,21 +2051,21 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int ci, float lr) {
     sgd4(wv, mv, sv, 0.f, lr, a.momentum);
     *wp = wv;
     *mp = mv;
-    *reinterpret_cast<float4*>(wl + t * 64 + 4 * co4) = wv;
+    *reinterpret_cast<float4*>(wl + t * 16 + 4 * c4) = wv;
   }
   __syncthreads();
-  if (tid < 128) {
-    const int co = tid & 63;
+  if (tid < 32) {
+    const int cl = tid & 15, co = cq * 16 + cl;
     float g[25], u[36];
-    if (tid < 64) {
+    if (tid < 16) {
 #pragma unroll
-      for (int t = 0; t < 25; ++t) g[t] = wl[t * 64 + co];
+      for (int t = 0; t < 25; ++t) g[t] = wl[t * 16 + cl];
       wino::filter_tile(g, u);
 #pragma unroll
       for (int p = 0; p < 36; ++p) a.U[wino_u_index(p, ci, co)] = u[p];
     } else {
 #pragma unroll
-      for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 64 + co];
+      for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 16 + cl];
       wino::filter_tile(g, u);
 #pragma unroll
       for (int p = 0; p < 36; ++p) a.Ud[wino_ud_index(p, ci, co)] = u[p];
@@ -2125,7 +2127,7 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
     return;
   }
   blk -= a.fc_blocks;
-  const int nconv2 = a.U ? 32 : 50;
+  const int nconv2 = a.U ? 128 : 50;
   if (blk < nconv2) {
     if (a.U)
       sgd_conv2_wino(a, blk, lr);
@@ -2172,7 +2174,7 @@ void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end,
   SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
                part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
                fc_blocks, wino_u, wino_ud};
-  const int conv2_blocks = wino_u ? 32 : 50;
+  const int conv2_blocks = wino_u ? 128 : 50;
   sgd_finalize_kernel<<<fc_blocks + conv2_blocks + 16 + cdiv(832, 4), 256, 0, s>>>(a);
 }
 
