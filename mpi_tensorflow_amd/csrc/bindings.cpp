@@ -107,6 +107,44 @@ PYBIND11_MODULE(_C, m) {
                                   P<float>(w2t), S(s));
     check_launch();
   });
+  // bf16 engine forward pieces (tests): two-launch conv1 -> conv2 and the fused launch
+  k.def("conv1_fwd_bf16", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
+                             uintptr_t b1, uintptr_t a1p, uintptr_t a1t, uintptr_t idx1,
+                             uintptr_t s) {
+    mnist::launch_conv1_fwd_bf16(P<const float>(data), P<const long long>(step), n_local, batch,
+                                 P<const float>(w1), P<const float>(b1), P<uint16_t>(a1p),
+                                 P<uint16_t>(a1t), P<uint8_t>(idx1), batch, S(s));
+    check_launch();
+  });
+  k.def("conv2_fwd_bf16", [](uintptr_t a1p, int batch, uintptr_t w2tb, uintptr_t b2, uintptr_t a2p,
+                             uintptr_t a2t, uintptr_t idx2, uintptr_t s) {
+    mnist16::launch_conv2_fwd(P<const uint16_t>(a1p), batch, P<const uint16_t>(w2tb),
+                              P<const float>(b2), P<uint16_t>(a2p), P<uint16_t>(a2t),
+                              P<uint8_t>(idx2), S(s));
+    check_launch();
+  });
+  k.def("conv12_fwd_bf16", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
+                              uintptr_t b1, uintptr_t idx1, uintptr_t w2tb, uintptr_t b2,
+                              uintptr_t a1p, uintptr_t a1t, uintptr_t a2p, uintptr_t a2t,
+                              uintptr_t idx2, uintptr_t s) {
+    mnist::C12In c;
+    c.data = P<const float>(data);
+    c.step = P<const long long>(step);
+    c.n_local = n_local;
+    c.w1 = P<const float>(w1);
+    c.b1 = P<const float>(b1);
+    c.idx1 = P<uint8_t>(idx1);
+    mnist::launch_conv12_fwd_bf16(c, batch, P<const uint16_t>(w2tb), P<const float>(b2),
+                                  P<uint16_t>(a1p), P<uint16_t>(a1t), P<uint16_t>(a2p),
+                                  P<uint16_t>(a2t), P<uint8_t>(idx2), S(s));
+    check_launch();
+  });
+  k.def("shadows_bf16", [](uintptr_t w1, uintptr_t w2, uintptr_t w1b, uintptr_t w1t,
+                           uintptr_t w2tb, uintptr_t w2b, uintptr_t s) {
+    mnist16::launch_shadows(P<const float>(w1), P<const float>(w2), P<uint16_t>(w1b),
+                            P<uint16_t>(w1t), P<uint16_t>(w2tb), P<uint16_t>(w2b), S(s));
+    check_launch();
+  });
   k.def("conv2_fwd", [](uintptr_t a1, int batch, uintptr_t w, uintptr_t b, uintptr_t out,
                         uintptr_t argmax, uintptr_t w2t, uintptr_t s) {
     mnist::launch_conv2_fwd(P<const float>(a1), batch, P<const float>(w), P<const float>(b),
@@ -308,14 +346,22 @@ PYBIND11_MODULE(_C, m) {
      py::arg("ws"), py::arg("st"), py::arg("bf16") = false, py::arg("xb") = 0, py::arg("wtb") = 0,
      py::arg("yb") = 0, py::arg("stats_part") = 0, py::arg("stats_rows") = 0,
      py::arg("stats_shift") = 0);
+  g.def("conv_bwd_data_stats_rows", &gops::conv_bwd_data_stats_rows);
   g.def("conv_bwd_data", [](const gops::ConvShape& s, uintptr_t dy, uintptr_t w, uintptr_t dx,
                             uintptr_t ws, uintptr_t st, bool bf16, uintptr_t dyb, uintptr_t addend,
-                            uintptr_t wtb) {
+                            uintptr_t wtb, uintptr_t bstats_part, int bstats_rows, uintptr_t bn_x,
+                            uintptr_t bn_y, uintptr_t bn_mean, uintptr_t bn_rstd, bool bn_relu) {
+    const gops::BnBwdStats bb{P<float>(bstats_part), bstats_rows, P<const void>(bn_x),
+                              P<const void>(bn_y), P<const float>(bn_mean),
+                              P<const float>(bn_rstd), bn_relu ? 1 : 0};
     gops::conv_bwd_data(s, P<const float>(dy), P<const float>(w), P<float>(dx), P<float>(ws), S(st),
-                        bf16, P<const void>(dyb), P<const float>(addend), P<const void>(wtb));
+                        bf16, P<const void>(dyb), P<const float>(addend), P<const void>(wtb), &bb);
     check_launch();
   }, py::arg("s"), py::arg("dy"), py::arg("w"), py::arg("dx"), py::arg("ws"), py::arg("st"),
-     py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0, py::arg("wtb") = 0);
+     py::arg("bf16") = false, py::arg("dyb") = 0, py::arg("addend") = 0, py::arg("wtb") = 0,
+     py::arg("bstats_part") = 0, py::arg("bstats_rows") = 0, py::arg("bn_x") = 0,
+     py::arg("bn_y") = 0, py::arg("bn_mean") = 0, py::arg("bn_rstd") = 0,
+     py::arg("bn_relu") = false);
   g.def("stem_weight_bf16", [](uintptr_t w, int R, int sc, int seg, int kp, int K, uintptr_t out,
                                uintptr_t st) {
     gops::stem_weight_bf16(P<const float>(w), R, sc, seg, kp, K, P<void>(out), S(st));
@@ -387,6 +433,16 @@ PYBIND11_MODULE(_C, m) {
      py::arg("rows"), py::arg("C"), py::arg("relu"), py::arg("ws"), py::arg("dg"), py::arg("db"),
      py::arg("dx"), py::arg("dres"), py::arg("st"), py::arg("dxb") = 0, py::arg("x_bf16") = false,
      py::arg("y_bf16") = false);
+  g.def("bn_bwd_partials", [](uintptr_t part, int nrows, uintptr_t x, uintptr_t dy, uintptr_t y,
+                              uintptr_t mean, uintptr_t rstd, uintptr_t gm, long long rows, int C,
+                              bool relu, uintptr_t dg, uintptr_t db, uintptr_t dx, uintptr_t dres,
+                              uintptr_t st, uintptr_t dxb) {
+    gops::bn_bwd_partials(P<const float>(part), nrows, P<const void>(x), P<const float>(dy),
+                          P<const void>(y), P<const float>(mean), P<const float>(rstd),
+                          P<const float>(gm), rows, C, relu, P<float>(dg), P<float>(db), P<float>(dx),
+                          P<float>(dres), S(st), P<void>(dxb));
+    check_launch();
+  });
   g.def("maxpool_fwd", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg, uintptr_t st) {
     gops::maxpool_fwd(p, P<const float>(x), P<float>(y), P<int>(arg), S(st));
     check_launch();

@@ -483,4 +483,18 @@ void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, co
 #undef BWD_APPLY
 }
 
+void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, const void* y,
+                     const float* mean, const float* rstd, const float* g, long long rows, int C,
+                     bool relu, float* dg, float* db, float* dx, float* dres, hipStream_t st,
+                     void* dxb) {
+  if (C % 64 != 0 || C > 1024 || P < 1 || !part || (!dx && !dxb) || (relu && !y))
+    throw std::runtime_error("bn_bwd_partials: needs C % 64 == 0, C <= 1024, a dx output");
+  // the dgrad epilogue's rows [2][C / 64][P][64] -> db, dg
+  bn::finalize_kernel<<<C, 256, 0, st>>>(part, P, C, rows, sums(db, dg), 1);
+  const long long n4 = rows * C / 4;
+  bn::bwd_apply_kernel<true, true><<<bn::grid_elems(n4), 256, 0, st>>>(
+      x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0,
+      reinterpret_cast<uint2*>(dxb));
+}
+
 }  // namespace gops

@@ -341,6 +341,24 @@ __device__ __forceinline__ void stats_store(const ConvStats& cs, int K, int co, 
   }
 }
 
+// BatchNorm BACKWARD statistics in a dgrad epilogue (BnBwdStats): the fp32
+// dX value v at element e of channel co is the BatchNorm's dY; d = v [y > 0]
+// (relu), s1 += d, s2 += d (x - mean) rstd.  Same partial-row table and
+// store as the forward statistics (stats_store).
+__device__ __forceinline__ float bf16_at(const void* p, size_t e) {
+  return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(p)[e] << 16);
+}
+__device__ __forceinline__ void bnb_store(const BnBwdStats& bb, int C, int co, int prow, int h,
+                                          float s1, float s2) {
+  s1 += __shfl_xor(s1, 32, 64);
+  s2 += __shfl_xor(s2, 32, 64);
+  if (h == 0) {
+    const size_t i = stats_index(co, prow, bb.P);
+    bb.part[i] = s1;
+    bb.part[(size_t)C * bb.P + i] = s2;
+  }
+}
+
 template <int BM, int BN, class XT, class LD = Loader<BM, BN, XT>>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restrict__ x,
                                                  const __bf16* __restrict__ wt,
@@ -505,7 +523,8 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
                                                    const __bf16* __restrict__ wt,
                                                    float* __restrict__ y, int cps,
                                                    const float* __restrict__ addend,
-                                                   __bf16* __restrict__ yb, const ConvStats cs) {
+                                                   __bf16* __restrict__ yb, const ConvStats cs,
+                                                   const BnBwdStats bb) {
   using h3::ROWB;
   using h3::HCAP;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -564,11 +583,17 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
       h3::glds(src, smem + ins * 8 * ROWB);
     }
   };
-  // BatchNorm shift of this lane's output columns (loaded up front, see fwd_kernel)
-  float kcol[TN];
+  // BatchNorm shift of this lane's output columns (loaded up front, see
+  // fwd_kernel); dgrad feeding a BatchNorm backward: its mean / rstd
+  const bool bs = !yb && bb.part;
+  float kcol[TN], bmu[TN], brs[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
-    kcol[j] = (yb && cs.part) ? cs.shift[n0 + wn * (BN / 2) + 32 * j + r] : 0.f;
+  for (int j = 0; j < TN; ++j) {
+    const int co = n0 + wn * (BN / 2) + 32 * j + r;
+    kcol[j] = (yb && cs.part) ? cs.shift[co] : 0.f;
+    bmu[j] = bs ? bb.mean[co] : 0.f;
+    brs[j] = bs ? bb.rstd[co] : 0.f;
+  }
   f32x16 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -657,6 +682,28 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
             ss2[j] += d * d;
           }
         }
+      } else if (bs) {  // fp32 dX = a BatchNorm's dY: its backward sums too
+        const size_t e0 = (size_t)mb * K + co;
+        float av[16], xv[16], yv[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {  // every load before the first store
+          const int rr = (q & 3) + 8 * (q >> 2);
+          const size_t e = e0 + (size_t)((full || mb + rr < M) ? rr : 0) * K;
+          av[q] = addend ? addend[e] : 0.f;
+          xv[q] = bf16_at(bb.x, e);
+          yv[q] = bb.relu ? bf16_at(bb.y, e) : 1.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = (q & 3) + 8 * (q >> 2);
+          if (full || mb + rr < M) {
+            const float v = acc[i][j][q] + av[q];
+            p[(size_t)rr * K] = v;
+            const float d = yv[q] > 0.f ? v : 0.f;
+            ss1[j] += d;
+            ss2[j] += d * (xv[q] - bmu[j]) * brs[j];
+          }
+        }
       } else if (full && addend) {
         // all 16 addend loads first, then the stores (interleaved, hipcc waited
         // vmcnt(0) per element: 16 serial round trips)
@@ -686,6 +733,11 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
     for (int j = 0; j < TN; ++j)
       stats_store(cs, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
   }
+  if (bs) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bnb_store(bb, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
+  }
 }
 
 // ------------------------------- 3x3 stride-2 backward-data (halo form) ----
@@ -705,7 +757,8 @@ template <int BM, int BN, int RB>
 __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16* __restrict__ dy,
                                                       const __bf16* __restrict__ wt,
                                                       float* __restrict__ dx, int cps,
-                                                      const float* __restrict__ addend) {
+                                                      const float* __restrict__ addend,
+                                                      const BnBwdStats bb) {
   using h3::ROWB;
   using h3::HCAP;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -826,6 +879,16 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
   // (64 serial round trips a lane; 162 us instead of ~50 at B = 128)
   dx += (size_t)blockIdx.y * s.N * s.H * s.W * s.C;
   const size_t C = s.C, W = s.W;
+  // unsplit, dX = a BatchNorm's dY: its backward sums too (bnb_store)
+  const bool bst = bb.part != nullptr;
+  float bs1[TN], bs2[TN], bmu[TN], brs[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int ci = n0 + wn * (BN / 2) + 32 * j + r;
+    bs1[j] = bs2[j] = 0.f;
+    bmu[j] = bst ? bb.mean[ci] : 0.f;
+    brs[j] = bst ? bb.rstd[ci] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -849,15 +912,38 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
 #pragma unroll
           for (int c = 0; c < 4; ++c)
             av[u][c] = (addend && ok[u]) ? addend[o[u] + (c >> 1) * W * C + (c & 1) * C] : 0.f;
+        float xv[4][4], yv[4][4];
+        if (bst) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const size_t e = o[u] + (c >> 1) * W * C + (c & 1) * C;
+              xv[u][c] = bf16_at(bb.x, e);
+              yv[u][c] = bb.relu ? bf16_at(bb.y, e) : 1.f;
+            }
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (!ok[u]) continue;
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            dx[o[u] + (c >> 1) * W * C + (c & 1) * C] = acc[c][i][j][q4 + u] + av[u][c];
+          for (int c = 0; c < 4; ++c) {
+            const float v = acc[c][i][j][q4 + u] + av[u][c];
+            dx[o[u] + (c >> 1) * W * C + (c & 1) * C] = v;
+            if (bst) {
+              const float d = yv[u][c] > 0.f ? v : 0.f;
+              bs1[j] += d;
+              bs2[j] += d * (xv[u][c] - bmu[j]) * brs[j];
+            }
+          }
         }
       }
     }
+  if (bst) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bnb_store(bb, s.C, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, bs1[j], bs2[j]);
+  }
 }
 
 // ----------------------------------------------------- backward-filter ----
@@ -1104,12 +1190,18 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
                                                         float4* __restrict__ out,
                                                         const float4* __restrict__ addend,
                                                         uint2* __restrict__ outb,
-                                                        const ConvStats cs, int C) {
+                                                        const ConvStats cs, int C,
+                                                        const BnBwdStats bb) {
   const long long stride = (long long)gridDim.x * blockDim.x;
-  const bool st = outb && cs.part;
+  const bool bs = !outb && bb.part;  // fp32 dX = a BatchNorm's dY: its backward sums
+  const bool st = (outb && cs.part) || bs;
   const int cq = C >> 2, tid = threadIdx.x;
-  float4 kc = make_float4(0.f, 0.f, 0.f, 0.f), t1 = kc, t2 = kc;
-  if (st) kc = *reinterpret_cast<const float4*>(cs.shift + 4 * (tid % cq));
+  float4 kc = make_float4(0.f, 0.f, 0.f, 0.f), t1 = kc, t2 = kc, mu = kc, rs = kc;
+  if (outb && cs.part) kc = *reinterpret_cast<const float4*>(cs.shift + 4 * (tid % cq));
+  if (bs) {
+    mu = *reinterpret_cast<const float4*>(bb.mean + 4 * (tid % cq));
+    rs = *reinterpret_cast<const float4*>(bb.rstd + 4 * (tid % cq));
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 a = part[i];
     for (int z = 1; z < nz; ++z) {
@@ -1137,6 +1229,20 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
       }
     } else {
       out[i] = a;
+      if (bs) {
+        const float av[4] = {a.x, a.y, a.z, a.w};
+        const float mv[4] = {mu.x, mu.y, mu.z, mu.w}, rv[4] = {rs.x, rs.y, rs.z, rs.w};
+        float d[4], e[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float xv = bf16_at(bb.x, 4 * i + c);
+          const float yv = bb.relu ? bf16_at(bb.y, 4 * i + c) : 1.f;
+          d[c] = yv > 0.f ? av[c] : 0.f;
+          e[c] = d[c] * (xv - mv[c]) * rv[c];
+        }
+        t1.x += d[0]; t1.y += d[1]; t1.z += d[2]; t1.w += d[3];
+        t2.x += e[0]; t2.y += e[1]; t2.z += e[2]; t2.w += e[3];
+      }
     }
   }
   if (st) {  // threads tid, tid + cq, ... share a channel quad: fixed-order sum
@@ -1150,9 +1256,11 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
         a.x += red[0][t].x; a.y += red[0][t].y; a.z += red[0][t].z; a.w += red[0][t].w;
         b.x += red[1][t].x; b.y += red[1][t].y; b.z += red[1][t].z; b.w += red[1][t].w;
       }
-      const size_t i = stats_index(4 * tid, blockIdx.x, cs.P);
-      *reinterpret_cast<float4*>(cs.part + i) = a;
-      *reinterpret_cast<float4*>(cs.part + (size_t)C * cs.P + i) = b;
+      float* part = bs ? bb.part : cs.part;
+      const int P = bs ? bb.P : cs.P;
+      const size_t i = stats_index(4 * tid, blockIdx.x, P);
+      *reinterpret_cast<float4*>(part + i) = a;
+      *reinterpret_cast<float4*>(part + (size_t)C * P + i) = b;
     }
   }
 }
@@ -1190,7 +1298,8 @@ static inline int slab_blocks(long long n4) {
 }
 static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStream_t st,
                         const float* addend = nullptr, __bf16* outb = nullptr,
-                        const ConvStats* stats = nullptr, int C = 0) {
+                        const ConvStats* stats = nullptr, int C = 0,
+                        const BnBwdStats* bstats = nullptr) {
   const long long b = slab_blocks(n4);
   int G = 1;
   if (b < 128 && nz >= 32) {
@@ -1204,10 +1313,16 @@ static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStrea
       throw std::runtime_error("slab_reduce: BatchNorm statistics layout mismatch");
     cs = *stats;
   }
+  BnBwdStats bb;
+  if (bstats && bstats->part) {
+    if (outb || C % 64 || 256 % (C / 4) || bstats->P != b)
+      throw std::runtime_error("slab_reduce: BatchNorm backward statistics layout mismatch");
+    bb = *bstats;
+  }
   slab_sum4_kernel<<<(int)b, 256, 0, st>>>(reinterpret_cast<const float4*>(slabs), cdiv(nz, G),
                                           n4 * G, n4, reinterpret_cast<float4*>(out),
                                           reinterpret_cast<const float4*>(addend),
-                                          reinterpret_cast<uint2*>(outb), cs, C);
+                                          reinterpret_cast<uint2*>(outb), cs, C, bb);
 }
 
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
@@ -1320,7 +1435,7 @@ static int stats_rows3(const ConvShape& s) {
 }
 static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float* y, float* ws,
                     hipStream_t st, const float* addend, __bf16* yb = nullptr,
-                    const ConvStats* stats = nullptr) {
+                    const ConvStats* stats = nullptr, const BnBwdStats* bstats = nullptr) {
   const long long M = (long long)s.N * s.H * s.W;
   const P3 p = plan3(s);
   ConvStats cs;
@@ -1329,16 +1444,22 @@ static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float
       throw std::runtime_error("conv3: BatchNorm statistics need a plain bf16-output conv");
     if (p.z == 1) cs = *stats;
   }
+  BnBwdStats bb;
+  if (bstats && bstats->part) {
+    if (yb || bstats->P != stats_rows3(s))
+      throw std::runtime_error("conv3: BatchNorm backward statistics layout mismatch");
+    if (p.z == 1) bb = *bstats;
+  }
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : y;
   const dim3 grid(cdiv(M, p.bm) * (s.K / 64), p.z);
   const float* add = p.z > 1 ? nullptr : addend;
   __bf16* ob = p.z > 1 ? nullptr : yb;
   if (p.bm == 128)
-    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs);
+    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs, bb);
   else
-    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs);
-  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb, stats, s.K);
+    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs, bb);
+  if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb, stats, s.K, bstats);
 }
 
 // 3x3 / stride 2 / pad 1 dgrad on an even input (the halo form above)
@@ -1362,19 +1483,34 @@ static inline P3 plan3s2(const ConvShape& s) {
   const int cps = cdiv(nch, z);
   return {cdiv(nch, cps), cps, 64};
 }
-static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, float* dx,
-                      float* ws, hipStream_t st, const float* addend) {
+// partial rows of the BatchNorm backward statistics launch3s2 writes
+static int stats_rows3s2(const ConvShape& s) {
   const long long M = (long long)s.N * s.OH * s.OW;
   const P3 p = plan3s2(s);
+  if (p.z > 1) return slab_blocks((long long)s.N * s.H * s.W * s.C / 4);
+  return cdiv(M, 64) * 2;
+}
+static void launch3s2(const ConvShape& s, const __bf16* dy, const __bf16* wt, float* dx,
+                      float* ws, hipStream_t st, const float* addend,
+                      const BnBwdStats* bstats = nullptr) {
+  const long long M = (long long)s.N * s.OH * s.OW;
+  const P3 p = plan3s2(s);
+  BnBwdStats bb;
+  if (bstats && bstats->part) {
+    if (bstats->P != stats_rows3s2(s))
+      throw std::runtime_error("dgrad3s2: BatchNorm backward statistics layout mismatch");
+    if (p.z == 1) bb = *bstats;
+  }
   float* slabs = ws + wt_floats(s);
   float* out = p.z > 1 ? slabs : dx;
   // 64-pixel tiles: with four accumulator classes a 128-pixel tile needed 272
   // registers a lane (one wave per SIMD) and ran 10x slower per tile
   const dim3 grid(cdiv(M, 64) * (s.C / 64), p.z);
   dgrad3s2_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, dy, wt, out, p.cps,
-                                                  p.z > 1 ? nullptr : addend);
+                                                  p.z > 1 ? nullptr : addend, bb);
   if (p.z > 1)
-    slab_reduce(slabs, p.z, (long long)s.N * s.H * s.W * s.C / 4, dx, st, addend);
+    slab_reduce(slabs, p.z, (long long)s.N * s.H * s.W * s.C / 4, dx, st, addend, nullptr,
+                nullptr, s.C, bstats);
 }
 
 // wgrad: tile = (ci, co) per tap; pixel slices fill the chip (~1024 blocks),
@@ -1837,10 +1973,27 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
     launch(s, x, wt, bias, y, relu, ws, st, nullptr, ob, 0, stats);
 }
 
+// BatchNorm backward statistics rows of the dgrad of s (0: not available -
+// the dgrad kinds without the epilogue, or a channel count the slab pass
+// cannot keep one quad per thread of)
+int conv_bwd_data_stats_rows(const ConvShape& s) {
+  using namespace cbf;
+  if (!conv_bwd_data_bf16_ok(s) || s.C % 64 != 0 || 256 % (s.C / 4) != 0) return 0;
+  if (dgrad3s2_ok(s)) return stats_rows3s2(s);
+  if (dgrad_1x1s2(s)) return 0;
+  if (conv3_ok(dgrad_shape(s))) return stats_rows3(dgrad_shape(s));
+  return 0;
+}
+
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                        hipStream_t st, const void* dyb, const float* addend, const void* wtb) {
+                        hipStream_t st, const void* dyb, const float* addend, const void* wtb,
+                        const BnBwdStats* bstats) {
   using namespace cbf;
   if (!conv_bwd_data_bf16_ok(s) || !ws) throw std::runtime_error("conv_bwd_data_bf16: unsupported shape");
+  if (bstats && bstats->part &&
+      (!dyb || bstats->P != conv_bwd_data_stats_rows(s) || bstats->P == 0 || !bstats->x ||
+       !bstats->mean || !bstats->rstd || (bstats->relu && !bstats->y)))
+    throw std::runtime_error("conv_bwd_data_bf16: BatchNorm backward statistics not available here");
   const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
   if (!wt) {
     __bf16* wc = reinterpret_cast<__bf16*>(ws);
@@ -1848,7 +2001,8 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
     wt = wc;
   }
   if (dgrad3s2_ok(s)) {
-    if (dyb) return launch3s2(s, reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend);
+    if (dyb)
+      return launch3s2(s, reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend, bstats);
     return conv_bwd_data_tiled(s, dy, w, dx, ws, st, true, addend);  // fp32 dY only
   }
   if (dgrad_1x1s2(s)) {  // a 1x1 GEMM over the dY pixels, 2x2-expanding epilogue
@@ -1863,7 +2017,8 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
     return;
   }
   if (dyb && conv3_ok(dgrad_shape(s)))
-    launch3(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend);
+    launch3(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, dx, ws, st, addend, nullptr,
+            nullptr, bstats);
   else if (dyb)
     launch(dgrad_shape(s), reinterpret_cast<const __bf16*>(dyb), wt, nullptr, dx, false, ws, st,
            addend);

@@ -60,6 +60,13 @@ struct C12In {
 };
 void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float* b2, float* a2,
                        uint8_t* idx2, float* w2t, hipStream_t s);
+// bf16 engine: conv1 + conv2 (+bias, ReLU, pool, argmax) in one launch; conv1
+// owned rows to a1p / a1t / c1.idx1, conv2 to a2p / a2t / idx2 (mnist_bf16.h
+// layouts, ld_batch = batch); w2tb = the bf16 conv2 shadow [25][2][64][16],
+// already current (batch % 16 == 0)
+void launch_conv12_fwd_bf16(const C12In& c1, int batch, const uint16_t* w2tb, const float* b2,
+                            uint16_t* a1p, uint16_t* a1t, uint16_t* a2p, uint16_t* a2t,
+                            uint8_t* idx2, hipStream_t s);
 // w2t (optional): also writes the transposed weights W2T[t][co][ci] for bwd-data
 void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b, float* out,
                       uint8_t* argmax, float* w2t, hipStream_t s);
@@ -136,7 +143,8 @@ void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
                          const float* lr, long long* step, hipStream_t s, bool fc_done = false,
-                         float* wino_u = nullptr, float* wino_ud = nullptr);
+                         float* wino_u = nullptr, float* wino_ud = nullptr,
+                         uint16_t* w2tb = nullptr, uint16_t* w2b = nullptr);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

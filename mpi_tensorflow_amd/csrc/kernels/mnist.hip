@@ -585,9 +585,30 @@ constexpr int C12_IMG_ROWS = 20, C12_IMG_LD = 33;
 // GEMM view as conv_pool_fwd_kernel: M = pre-pool pixels (window, quadrant),
 // N = 32 channels, K = 25 taps (-> 32), one 32 x 32 MFMA tile per 8 windows.
 // NT: block size (256 or 512); the conv1 MFMA tiles run on waves 0-3 only
-template <int NT = 256>
-__device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int n, int pg,
-                                                float* __restrict__ xs, float* __restrict__ img) {
+// Sink: where the pooled conv1 values go - zero(tid, NT) clears the block's
+// halo tile, put(y, x, co, o, qq, own) stores a1 row y, column x (own: a row
+// this block writes out for the backward pass).
+struct HaloF32 {  // fp32 engines: the fp32 halo tile + a1 / idx1 / a1pf
+  const C12In& c1;
+  float* xs;
+  int n, y0;
+  __device__ __forceinline__ void zero(int tid, int nt) const {
+    for (int i = tid; i < C2_XS; i += nt) xs[i] = 0.f;
+  }
+  __device__ __forceinline__ void put(int y, int x, int co, float o, int qq, bool own) const {
+    xs[((y - y0) * C2_XS_COLS + x + 2) * 33 + co] = o;
+    if (own) {
+      const size_t pi = ((size_t)(n * 14 + y) * 14 + x) * 32 + co;
+      c1.a1[pi] = o;
+      c1.idx1[pi] = (uint8_t)qq;
+      c1.a1pf[((size_t)(n * 18 + y + 2) * 18 + x + 2) * 32 + co] = o;
+    }
+  }
+};
+
+template <int NT, class Sink>
+__device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, int n, int pg,
+                                                  float* __restrict__ img, const Sink& sink) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long off = batch_offset_dev(c1.step, c1.n_local, batch);
   const float* xin = c1.data + (off + n) * 784;
@@ -612,7 +633,7 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
     wb[st] = k < 25 ? v : 0.f;
   }
   const float bias = c1.b1[co];
-  for (int i = tid; i < C2_XS; i += NT) xs[i] = 0.f;
+  sink.zero(tid, NT);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int i = tid + NT * j;
@@ -646,14 +667,8 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
       }
       if (wj < nwin) {
         const int y = ya + wj / 14, x = wj % 14;
-        const float o = fmaxf(v + bias, 0.f);
-        xs[((y - y0) * C2_XS_COLS + x + 2) * 33 + co] = o;
-        if (y >= 4 * pg && y < 4 * pg + 4) {  // rows this block owns
-          const size_t pi = ((size_t)(n * 14 + y) * 14 + x) * 32 + co;
-          c1.a1[pi] = o;
-          c1.idx1[pi] = (uint8_t)qq;
-          c1.a1pf[((size_t)(n * 18 + y + 2) * 18 + x + 2) * 32 + co] = o;
-        }
+        // own: the rows this block writes out
+        sink.put(y, x, co, fmaxf(v + bias, 0.f), qq, y >= 4 * pg && y < 4 * pg + 4);
       }
     }
   };
@@ -676,6 +691,12 @@ __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int 
     epilogue(t, acc0);
     if (two) epilogue(t + 4, acc1);
   }
+}
+
+template <int NT = 256>
+__device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int n, int pg,
+                                                float* __restrict__ xs, float* __restrict__ img) {
+  conv1_into_halo_t<NT>(c1, batch, n, pg, img, HaloF32{c1, xs, n, 4 * pg - 2});
 }
 
 // FUSED (train): conv1 is computed into the halo tile (conv1_into_halo)
@@ -785,6 +806,115 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
   }
 }
 
+
+// ------------------------------ bf16 engine: conv1 + conv2 in ONE launch ----
+// The bf16 twin of conv2_fwd_v3_kernel<true> (BASELINE config 2): each block
+// (image, pair of pooled conv2 rows) recomputes the pooled conv1 rows of its
+// halo on fp32 MFMA (conv1_into_halo_t, the standalone conv1's K order) and
+// stores them bf16-rounded into a bf16 LDS halo; the rows it owns go out in
+// the bf16 engine's layouts (a1p / a1t / idx1, mnist_bf16.h).  conv2 then runs
+// on v_mfma_f32_32x32x16_bf16 with A fragments from that halo (one
+// ds_read_b128 per k-step) and B from the w2t shadow (which the previous
+// step's SGD wrote, or refresh_shadows), in the K order and with the two
+// accumulator chains of mnist16::conv2_fwd_kernel, so a2 / idx2 equal the
+// two-launch path's.  One launch and one a1 round trip through memory fewer.
+constexpr int XB_LD = 40;  // bf16 per halo pixel (32 channels + 8: 16-B aligned rows)
+constexpr int XB_ELEMS = C2_XS_ROWS * C2_XS_COLS * XB_LD;
+
+struct HaloB16 {
+  const C12In& c1;
+  __bf16* xb;
+  __bf16* a1p;  // [2][B][18][18][16]
+  __bf16* a1t;  // [B][18][32][MNIST16_T_LD]
+  int n, y0, batch;
+  __device__ __forceinline__ void zero(int tid, int nt) const {
+    uint4* z = reinterpret_cast<uint4*>(xb);
+    for (int i = tid; i < XB_ELEMS / 8; i += nt) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
+  __device__ __forceinline__ void put(int y, int x, int co, float o, int qq, bool own) const {
+    const __bf16 h = (__bf16)o;
+    xb[((y - y0) * C2_XS_COLS + x + 2) * XB_LD + co] = h;
+    if (own) {
+      c1.idx1[((size_t)(n * 14 + y) * 14 + x) * 32 + co] = (uint8_t)qq;
+      a1p[(((size_t)(co >> 4) * batch + n) * 18 + y + 2) * 18 * 16 + (x + 2) * 16 + (co & 15)] = h;
+      a1t[((size_t)(n * 18 + y + 2) * 32 + co) * MNIST16_T_LD + x + 2] = h;
+    }
+  }
+};
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__global__ __launch_bounds__(256) void conv12_fwd_bf16_kernel(
+    const C12In c1, int batch, const __bf16* __restrict__ w2t, const float* __restrict__ b2,
+    __bf16* __restrict__ a1p, __bf16* __restrict__ a1t, __bf16* __restrict__ a2p,
+    __bf16* __restrict__ a2t, uint8_t* __restrict__ idx2) {
+  __shared__ __attribute__((aligned(16))) __bf16 xb[XB_ELEMS];
+  __shared__ float img[C12_IMG_ROWS * C12_IMG_LD];
+  const int n = blockIdx.x >> 2, pg = blockIdx.x & 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  conv1_into_halo_t<256>(c1, batch, n, pg, img,
+                         HaloB16{c1, xb, a1p, a1t, n, 4 * pg - 2, batch});
+  // A rows of this wave: pre-pool pixel m = (window, quadrant) of the block's
+  // 14 windows (rows 56..63 of the second tile are padding, read pixel 0)
+  const int msub = wave & 1, nsub = wave >> 1;
+  const int m = msub * 32 + r, win = m >> 2, q = m & 3;
+  int ly = 0, lx = 0;
+  if (win < 14) {
+    ly = 2 * (win / 7) + (q >> 1);
+    lx = 2 * (win % 7) + (q & 1);
+  }
+  const __bf16* ap = xb + (ly * C2_XS_COLS + lx) * XB_LD + 8 * h;
+  const __bf16* bp = w2t + (nsub * 32 + r) * 16 + 8 * h;
+  constexpr int D = 5;
+  bf16x8 rb[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) rb[d] = *reinterpret_cast<const bf16x8*>(bp + d * 1024);
+  __syncthreads();  // the halo tile is complete
+  f32x16 acc0 = zero16(), acc1 = zero16();
+  // K-step ks = (tap t = ks / 2, channel half s = ks % 2), mnist16::kloop order
+#pragma unroll
+  for (int ks = 0; ks < 50; ks += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int k = ks + d, t = k >> 1, sh = k & 1, kh = t / 5, kw = t % 5;
+      const bf16x8 a =
+          *reinterpret_cast<const bf16x8*>(ap + (kh * C2_XS_COLS + kw) * XB_LD + 16 * sh);
+      const bf16x8 b = rb[d];
+      if (k + D < 50) rb[d] = *reinterpret_cast<const bf16x8*>(bp + (k + D) * 1024);
+      __builtin_amdgcn_sched_barrier(0);
+      if (d & 1)
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc1, 0, 0, 0);
+      else
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const int co = nsub * 32 + r;
+  const float bias = b2[co];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    float v = acc0[4 * g] + acc1[4 * g];
+    int qq = 0;
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const float u = acc0[4 * g + j] + acc1[4 * g + j];
+      if (u > v) {  // strict: first max wins (TF MaxPool order)
+        v = u;
+        qq = j;
+      }
+    }
+    const int w_ = msub * 8 + 2 * g + h;  // pooling window of registers 4g..4g+3
+    const int pr = 2 * pg + w_ / 7, pc = w_ % 7;
+    if (w_ < 14 && pr < 7) {
+      const int i = (pr * 7 + pc) * 64 + co;
+      const __bf16 out = (__bf16)fmaxf(v + bias, 0.f);
+      a2p[((size_t)(i >> 4) * batch + n) * 16 + (i & 15)] = out;
+      idx2[(size_t)n * FC1_IN + i] = (uint8_t)qq;
+      a2t[((size_t)(n >> 4) * FC1_IN + i) * 16 + (n & 15)] = out;
+    }
+  }
+}
 
 // ------------------------------------- conv2 forward, Winograd F(2x2,5x5) ----
 // Transformed filters (wino.h), stored in MFMA fragment order so that one
@@ -1801,6 +1931,18 @@ void launch_conv12_fwd(const C12In& c1, int batch, const float* w2, const float*
   conv2_fwd_v3_kernel<true><<<batch * 4, 256, 0, s>>>(nullptr, batch, w2, b2, a2, idx2, w2t, c1);
 }
 
+void launch_conv12_fwd_bf16(const C12In& c1, int batch, const uint16_t* w2tb, const float* b2,
+                            uint16_t* a1p, uint16_t* a1t, uint16_t* a2p, uint16_t* a2t,
+                            uint8_t* idx2, hipStream_t s) {
+  if (!c1.data || !c1.w1 || !c1.b1 || !c1.idx1 || !w2tb || !a1p || !a1t || !a2p || !a2t || !idx2)
+    throw std::runtime_error("conv12_fwd_bf16: missing operand");
+  if (batch % 16 != 0) throw std::runtime_error("conv12_fwd_bf16: batch % 16 != 0");
+  auto B16 = [](uint16_t* p) { return reinterpret_cast<__bf16*>(p); };
+  conv12_fwd_bf16_kernel<<<batch * 4, 256, 0, s>>>(
+      c1, batch, reinterpret_cast<const __bf16*>(w2tb), b2, B16(a1p), B16(a1t), B16(a2p),
+      B16(a2t), idx2);
+}
+
 void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t s) {
   conv2_wino_weights_kernel<<<2048 / 256, 256, 0, s>>>(w2, U, Ud);
 }
@@ -2004,6 +2146,10 @@ struct SgdFinArgs {
   // NEXT step's forward (U) and bwd-data (Ud), layouts of wino_u_index
   float* U;
   float* Ud;
+  // bf16 engine (optional): the updated conv2 weights' bf16 shadows w2t / w2b
+  // (mnist_bf16.h layouts) for the NEXT step's fused forward and bwd-data
+  __bf16* w2t;
+  __bf16* w2b;
 };
 
 __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, float mu) {
@@ -2106,6 +2252,19 @@ __device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
   sgd4(wv, mv, s, 0.f, lr, a.momentum);
   *wp = wv;
   *mp = mv;
+  if (a.w2t) {  // HWIO (t * 32 + ci) * 64 + co: 4 consecutive co
+    const int idx = 4 * i, t = idx >> 11, ci = (idx >> 6) & 31, co = idx & 63;
+    const float v[4] = {wv.x, wv.y, wv.z, wv.w};
+    __bf16 hb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      hb[e] = (__bf16)v[e];
+      a.w2t[((t * 2 + (ci >> 4)) * 64 + co + e) * 16 + (ci & 15)] = hb[e];
+    }
+    // w2b: the 4 co are consecutive within one 16-channel group (8-byte store)
+    *reinterpret_cast<uint2*>(a.w2b + ((t * 4 + (co >> 4)) * 32 + ci) * 16 + (co & 15)) =
+        __builtin_bit_cast(uint2, hb);
+  }
 }
 
 __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
@@ -2162,7 +2321,9 @@ void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end,
                          int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
                          int ngroups, const float* part1, int nblk1, float l2, float momentum,
                          const float* lr, long long* step, hipStream_t s, bool fc_done,
-                         float* wino_u, float* wino_ud) {
+                         float* wino_u, float* wino_ud, uint16_t* w2tb, uint16_t* w2b) {
+  if ((w2tb == nullptr) != (w2b == nullptr) || (w2tb && wino_u))
+    throw std::runtime_error("sgd_finalize: bf16 conv2 shadows need both layouts, no Winograd");
   if (fc_end % 4 || off_w2 % 4 || l2_end != fc_end)
     throw std::runtime_error("sgd_finalize: misaligned flat segments / L2 prefix != FC bucket");
   if ((wino_u == nullptr) != (wino_ud == nullptr))
@@ -2173,7 +2334,8 @@ void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end,
   const int fc_blocks = fc_done ? 0 : (int)(b < 2048 ? b : 2048);  // as the flat SGD
   SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
                part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
-               fc_blocks, wino_u, wino_ud};
+               fc_blocks, wino_u, wino_ud, reinterpret_cast<__bf16*>(w2tb),
+               reinterpret_cast<__bf16*>(w2b)};
   const int conv2_blocks = wino_u ? 128 : 50;
   sgd_finalize_kernel<<<fc_blocks + conv2_blocks + 16 + cdiv(832, 4), 256, 0, s>>>(a);
 }

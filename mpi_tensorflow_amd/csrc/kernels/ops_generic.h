@@ -34,6 +34,22 @@ struct ConvStats {
   int P = 0;
   const float* shift = nullptr;
 };
+// BatchNorm BACKWARD statistics from the dgrad that produces the BatchNorm's
+// dY (bf16 family, fp32 dX): with d = dX [y > 0] (relu) and xhat = (x - mean)
+// rstd, partial sums of d and d xhat over the rows, part [2][C / 64][P][64]
+// with P = conv_bwd_data_stats_rows(s) (0: this dgrad cannot write them).  x =
+// the BatchNorm's bf16 input, y = the bf16 twin of its output (ReLU mask).
+// Consumed by bn_bwd_partials.
+struct BnBwdStats {
+  float* part = nullptr;
+  int P = 0;
+  const void* x = nullptr;  // bf16
+  const void* y = nullptr;  // bf16 (relu only)
+  const float* mean = nullptr;
+  const float* rstd = nullptr;
+  int relu = 0;
+};
+int conv_bwd_data_stats_rows(const ConvShape& s);
 int conv_fwd_stats_rows(const ConvShape& s);  // bf16 family, bf16 output, no bias / ReLU
 int conv_fwd_stem_stats_rows(const ConvShape& s1);
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
@@ -43,7 +59,8 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
 // tensor (a residual branch), added in the epilogue: dx = conv + addend
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                    hipStream_t st, bool bf16 = false, const void* dyb = nullptr,
-                   const float* addend = nullptr, const void* wtb = nullptr);
+                   const float* addend = nullptr, const void* wtb = nullptr,
+                   const BnBwdStats* bstats = nullptr);
 bool conv_bwd_data_join_ok(const ConvShape& s, bool bf16);  // takes an addend
 int conv_filter_splits(const ConvShape& s);
 void conv_bwd_filter(const ConvShape& s, const float* x, const float* dy, float* ws, float* dw,
@@ -71,7 +88,7 @@ void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const flo
                    const ConvStats* stats = nullptr);
 void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                         hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr,
-                        const void* wtb = nullptr);
+                        const void* wtb = nullptr, const BnBwdStats* bstats = nullptr);
 // batched weight re-layout: jobs = device int64 [njobs][8] = {w, out, taps,
 // C, K, mode (0 forward, 1 stride-1 dgrad), first block, 0}, blocks of a job
 // = wcvt_blocks(taps, C, K), first blocks ascending
@@ -132,6 +149,13 @@ void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, co
             const float* g, long long rows, int C, bool relu, float* ws, float* dg, float* db,
             float* dx, float* dres, hipStream_t st, void* dxb = nullptr, bool xb16 = false,
             bool yb16 = false);
+// backward from the statistics the producing dgrad's epilogue already wrote
+// (BnBwdStats part, P rows): finalize + apply only, no statistics pass;
+// x bf16, y = the bf16 twin (relu)
+void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, const void* y,
+                     const float* mean, const float* rstd, const float* g, long long rows, int C,
+                     bool relu, float* dg, float* db, float* dx, float* dres, hipStream_t st,
+                     void* dxb);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 // bf16-twin form: xb = bf16 input, y (fp32) / yb (bf16) outputs each optional,

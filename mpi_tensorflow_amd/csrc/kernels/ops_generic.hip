@@ -937,9 +937,11 @@ bool conv_bwd_data_join_ok(const ConvShape& s, bool bf16) {
 
 void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                    hipStream_t st, bool bf16, const void* dyb, const float* addend,
-                   const void* wtb) {
+                   const void* wtb, const BnBwdStats* bstats) {
   if (bf16 && conv_bwd_data_bf16_ok(s))
-    return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb, addend, wtb);
+    return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb, addend, wtb, bstats);
+  if (bstats && bstats->part)
+    throw std::runtime_error("conv_bwd_data: BatchNorm backward statistics need the bf16 family");
   if (conv_bwd_data_tiled_ok(s))
     return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend, dyb);
   if (!dy) throw std::runtime_error("conv_bwd_data: this shape needs the fp32 dY");

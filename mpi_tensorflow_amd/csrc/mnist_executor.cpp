@@ -46,7 +46,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                                     bool wino_fresh) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
-    return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd);
+    return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, wino_fresh);
   }
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
@@ -118,7 +118,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
 // fp32 MFMA and writes bf16 images, the conv1 filter grad / fc2 head / slab
 // reductions / SGD stay fp32.
 void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
-                                         const mnist::FcSgdArgs* fc_sgd) {
+                                         const mnist::FcSgdArgs* fc_sgd, bool shadows_fresh) {
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
   float* G = P<float>(p.grads);
@@ -131,12 +131,28 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
   // after any outside change of the weights), and always correct
   // (fc_sgd->w1b: the previous step's SGD already wrote the fc1 shadows)
   const bool w1_done = fc_sgd != nullptr && fc_sgd->w1b != nullptr;
-  mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
-                               W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1), B,
-                               s, W + p.off_w3, W + p.off_w2, w1_done ? nullptr : P<U16>(p.w1b),
-                               P<U16>(p.w1t), P<U16>(p.w2tb), P<U16>(p.w2b));
-  mnist16::launch_conv2_fwd(P<const U16>(p.a1p), B, P<const U16>(p.w2tb), W + p.off_b2,
-                            P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2), s);
+  if (w1_done && shadows_fresh && B % 16 == 0) {
+    // single rank: every shadow is current (the previous step's SGD, or
+    // refresh_shadows), so conv1 runs inside the conv2 blocks (one launch)
+    mnist::C12In cf;
+    cf.data = P<const float>(p.train_x);
+    cf.step = step;
+    cf.n_local = p.n_local;
+    cf.w1 = W + p.off_w1;
+    cf.b1 = W + p.off_b1;
+    cf.idx1 = P<uint8_t>(p.idx1);
+    mnist::launch_conv12_fwd_bf16(cf, B, P<const U16>(p.w2tb), W + p.off_b2, P<U16>(p.a1p),
+                                  P<U16>(p.a1t), P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2),
+                                  s);
+  } else {
+    mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
+                                 W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1),
+                                 B, s, W + p.off_w3, W + p.off_w2,
+                                 w1_done ? nullptr : P<U16>(p.w1b), P<U16>(p.w1t), P<U16>(p.w2tb),
+                                 P<U16>(p.w2b));
+    mnist16::launch_conv2_fwd(P<const U16>(p.a1p), B, P<const U16>(p.w2tb), W + p.off_b2,
+                              P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2), s);
+  }
   mnist16::launch_fc1_fwd_train(P<const U16>(p.a2h), P<const U16>(p.w1t), B, P<float>(p.fc1_part),
                                 s);
   mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
@@ -273,7 +289,9 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                P<const float>(p.part1), conv1_blocks(), p.l2, p.momentum,
                                P<const float>(p.lr), P<long long>(p.step), s, fused,
                                p.wino ? P<float>(p.wino_u) : nullptr,
-                               p.wino ? P<float>(p.wino_ud) : nullptr);
+                               p.wino ? P<float>(p.wino_ud) : nullptr,
+                               (p.bf16 && fused) ? P<uint16_t>(p.w2tb) : nullptr,
+                               (p.bf16 && fused) ? P<uint16_t>(p.w2b) : nullptr);
     return;
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {

@@ -161,8 +161,9 @@ class MnistExecutor {
   void reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs);
   int sched_ = SCHED_BUCKETS;
   bool fc_pending_ = false;  // an FC all-gather was enqueued and not yet waited on
+  // shadows_fresh: every bf16 weight shadow is current (single-rank step)
   void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,
-                            const mnist::FcSgdArgs* fc_sgd = nullptr);
+                            const mnist::FcSgdArgs* fc_sgd = nullptr, bool shadows_fresh = false);
   int fc_sgd_rounds_ = 2;
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);

@@ -166,6 +166,40 @@ def _bnstats(t: torch.Tensor, rmean: torch.Tensor):
     return None
 
 
+# BatchNorm BACKWARD statistics written by the dgrad that produces the
+# BatchNorm's dY (bf16 conv mode).  The BatchNorm forward marks its output
+# with what that dgrad needs (its bf16 input x, the bf16 twin of its output
+# for the ReLU mask, mean, rstd); the consuming conv's backward passes it to
+# its dgrad, whose epilogue writes the partial table, attached to the dX it
+# returns; the BatchNorm backward then skips its statistics pass.
+BN_BWD_STATS = {"epilogue": 0, "pass": 0}  # BatchNorm backward counts by route
+_BNB_EPILOGUE = True
+
+
+def set_bn_bwd_epilogue(on: bool) -> None:
+    """Let dgrad epilogues write the BatchNorm backward statistics (default
+    on; off = the BatchNorm's own statistics pass, for A/B tests)."""
+    global _BNB_EPILOGUE
+    _BNB_EPILOGUE = bool(on)
+
+
+def _attach_bnbwd_src(y: torch.Tensor, x: torch.Tensor, yb: Optional[torch.Tensor],
+                      mean: torch.Tensor, rstd: torch.Tensor, relu: bool) -> None:
+    y._mta_bnbwd = (x, yb, mean, rstd, relu)
+
+
+def _attach_bnbwd_stats(dx: torch.Tensor, part: torch.Tensor, rows: int,
+                        mean: torch.Tensor) -> None:
+    dx._mta_bnbwdst = (part, rows, mean, dx._version, dx.data_ptr())
+
+
+def _bnbwd_stats(dy: torch.Tensor, mean: torch.Tensor):
+    a = getattr(dy, "_mta_bnbwdst", None)
+    if a is not None and a[2] is mean and a[3] == dy._version and a[4] == dy.data_ptr():
+        return a[0], a[1]
+    return None
+
+
 def _bf16_out(like: torch.Tensor) -> Optional[torch.Tensor]:
     """A bf16 twin for a BN output when a bf16 conv can consume it."""
     if not _CONV_BF16 or like.shape[-1] % 64 != 0:
@@ -229,6 +263,9 @@ class _ConvFn(torch.autograd.Function):
         if part is not None:
             _attach_bnstats(y, part, rows, bn_shift)
         ctx.save_for_backward(x, w, y, xb)
+        # x is a BatchNorm's output: the dgrad can write that BatchNorm's
+        # backward statistics (bf16 conv mode, bf16 BatchNorm input)
+        ctx.bnb = getattr(x, "_mta_bnbwd", None) if (ctx.bf16 and _BNB_EPILOGUE) else None
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
         ctx.join, ctx.role, ctx.wtb_d = join, role, wtb_d
@@ -250,8 +287,24 @@ class _ConvFn(torch.autograd.Function):
                 sh = ctx.shape
                 dx = _empty((sh.N, sh.H, sh.W, sh.C), x)
                 add = ctx.join.take() if ctx.role == "final" else None
-                C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
-                                    ptr(add), ptr(ctx.wtb_d))
+                # the BatchNorm statistics need the final dX: not for a stashed
+                # branch, nor a join whose other half is still to be added
+                bnb = ctx.bnb if (ctx.role is None or (ctx.role == "final" and add is not None)) \
+                    else None
+                part, prow = None, 0
+                if bnb is not None:
+                    prow = C.ops.conv_bwd_data_stats_rows(sh)
+                    if prow > 0:
+                        part = torch.empty(2 * sh.C * prow, dtype=torch.float32, device=dx.device)
+                if part is not None:
+                    bx, byb, bmean, brstd, brelu = bnb
+                    C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
+                                        ptr(add), ptr(ctx.wtb_d), ptr(part), prow, ptr(bx),
+                                        ptr(byb), ptr(bmean), ptr(brstd), brelu)
+                    _attach_bnbwd_stats(dx, part, prow, bmean)
+                else:
+                    C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
+                                        ptr(add), ptr(ctx.wtb_d))
                 if ctx.role == "stash":
                     ctx.join.stash(dx)
                     dx = None
@@ -505,6 +558,8 @@ class _BNFn(torch.autograd.Function):
                          stream_handle(), ptr(yb), xb16)
         if yb is not None:
             _attach_bf16(y, yb)
+        if xb16 and (yb is not None or not relu):
+            _attach_bnbwd_src(y, x, yb, mean, rstd, relu)
         # the backward's ReLU mask reads the bf16 twin when there is one (same signs)
         ctx.yb16 = yb is not None
         ctx.save_for_backward(x, yb if yb is not None else y, mean, rstd, g)
@@ -531,9 +586,17 @@ class _BNFn(torch.autograd.Function):
         else:
             dx = torch.empty_like(dy)
             dxf, dxb = dx, _bf16_out(dx)
-        C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc, ctx.relu,
-                     ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dxf), ptr(dres), stream_handle(),
-                     ptr(dxb), xb16, ctx.yb16)
+        st = _bnbwd_stats(dy, mean) if (xb16 and (ctx.yb16 or not ctx.relu)) else None
+        if st is not None:  # the dgrad producing dy wrote the sums (see above)
+            BN_BWD_STATS["epilogue"] += 1
+            C.ops.bn_bwd_partials(ptr(st[0]), st[1], ptr(x), ptr(dy), ptr(y), ptr(mean),
+                                  ptr(rstd), ptr(g), rows, Cc, ctx.relu, ptr(ctx.gg), ptr(ctx.gb),
+                                  ptr(dxf), ptr(dres), stream_handle(), ptr(dxb))
+        else:
+            BN_BWD_STATS["pass"] += 1
+            C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc,
+                         ctx.relu, ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dxf), ptr(dres),
+                         stream_handle(), ptr(dxb), xb16, ctx.yb16)
         if dxf is not None and dxb is not None:
             _attach_bf16(dx, dxb)
         _grad_done(ctx.gg, ctx.gb)

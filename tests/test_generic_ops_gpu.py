@@ -577,6 +577,49 @@ def test_conv_epilogue_bn_statistics(cuda_dev, N, H, Cin, K, R, stride, pad):
     assert _rel(gw1, gw0) < 1e-4 and _rel(gg1, gg0) < 1e-4 and _rel(gb1, gb0) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,Cin,K,stride,relu", [
+    (4, 14, 64, 64, 1, True),      # halo dgrad, unsplit: sums in its epilogue
+    (4, 7, 512, 512, 1, False),    # halo dgrad, split-K: in the slab reduction
+    (32, 56, 64, 128, 2, True),    # 3x3 stride-2 dgrad, unsplit
+    (2, 28, 64, 128, 2, True),     # 3x3 stride-2 dgrad, split-K
+])
+def test_dgrad_epilogue_bn_backward_statistics(cuda_dev, N, H, Cin, K, stride, relu):
+    """bf16 conv mode: the dgrad of a conv whose input is a BatchNorm output
+    writes that BatchNorm's backward sums (sum dY', sum dY' xhat) in its
+    epilogue (or its split-K reduction), and the BatchNorm backward skips its
+    statistics pass: dX, dgamma and dbeta match the two-pass BatchNorm."""
+    g = torch.Generator().manual_seed(31)
+    x = (torch.randn(N, H, H, Cin, generator=g) * 2 + 0.5).to(torch.bfloat16).to(cuda_dev)
+    w = (torch.randn(3, 3, Cin, K, generator=g) * 0.05).to(cuda_dev)
+    gam = (torch.rand(Cin, generator=g) + 0.5).to(cuda_dev)
+    bet = torch.randn(Cin, generator=g).to(cuda_dev)
+    OH = (H + 2 - 3) // stride + 1
+    dy = torch.randn(N, OH, OH, K, generator=g).to(torch.bfloat16).to(cuda_dev)
+    out = []
+    Fn.set_conv_bf16(True)
+    try:
+        for fused in (False, True):
+            Fn.set_bn_bwd_epilogue(fused)
+            n0 = Fn.BN_BWD_STATS["epilogue"]
+            xi = x.clone().requires_grad_(True)
+            gp, bp, wp = _param(gam), _param(bet), _param(w)
+            rm, rv = torch.zeros(Cin, device=cuda_dev), torch.ones(Cin, device=cuda_dev)
+            h = Fn.batchnorm(xi, gp, bp, rm, rv, True, relu)
+            y = Fn.conv2d(h, wp, None, stride, 1, False, out_bf16=True)
+            y.backward(dy)
+            assert Fn.BN_BWD_STATS["epilogue"] - n0 == (1 if fused else 0)
+            out.append((xi.grad.float().clone(), gp.grad_view.clone(), bp.grad_view.clone(),
+                        wp.grad_view.clone()))
+    finally:
+        Fn.set_bn_bwd_epilogue(True)
+        Fn.set_conv_bf16(False)
+    torch.cuda.synchronize()
+    (dx0, gg0, gb0, gw0), (dx1, gg1, gb1, gw1) = out
+    assert torch.equal(gw0, gw1)  # the filter gradient does not depend on the route
+    assert _rel(gb1, gb0) < 1e-5 and _rel(gg1, gg0) < 1e-4
+    assert _rel(dx1, dx0) < 4e-3  # dX is bf16: a few rounding flips
+
+
 @pytest.mark.parametrize("relu,res", [(False, False), (True, True)])
 def test_batchnorm_bf16_input(cuda_dev, relu, res):
     """BN over a bf16 input (a bf16-output conv's activations): statistics,

@@ -94,3 +94,60 @@ def test_bf16_learns_and_evaluates(cuda_dev, data):
     e_ref = ref.evaluate(tx, ty)
     assert e1 < e0 and e1 < 20.0, (e0, e1)  # v2 synthetic task: ~12 % after 150 steps
     assert abs(e1 - e_ref) <= 1.0, (e1, e_ref)  # bf16 vs fp32 inference, same weights
+
+
+def test_fused_conv12_bf16_equals_two_launches(cuda_dev):
+    """The single-rank bf16 step's fused forward (conv1 recomputed inside the
+    conv2 blocks, mnist.hip conv12_fwd_bf16_kernel) writes exactly what the
+    two-launch path (conv1 -> a1p -> conv2) writes: a1p / a1t / idx1 for the
+    backward and a2p / a2t / idx2, bit for bit, at a device-step batch
+    offset.  Then the conv2 output against fp32 torch on the bf16 operands."""
+    import torch.nn.functional as F
+
+    from mpi_tensorflow_amd.ops import native
+
+    k = native().mnist
+    B, n_local = 64, 256
+    g = torch.Generator().manual_seed(5)
+    data = (torch.rand(n_local, 28, 28, 1, generator=g) - 0.5).to(cuda_dev)
+    step = torch.tensor([3], dtype=torch.int64, device=cuda_dev)
+    w1 = (torch.randn(5, 5, 1, 32, generator=g) * 0.2).to(cuda_dev)
+    b1 = (torch.randn(32, generator=g) * 0.1).to(cuda_dev)
+    w2 = (torch.randn(5, 5, 32, 64, generator=g) * 0.05).to(cuda_dev)
+    b2 = (torch.randn(64, generator=g) * 0.1).to(cuda_dev)
+    w3 = torch.zeros(3136 * 512, device=cuda_dev)
+    u16 = dict(dtype=torch.int16, device=cuda_dev)
+    w1b, w1t = torch.zeros(3136 * 512, **u16), torch.zeros(3136 * 512, **u16)
+    w2tb, w2b = torch.zeros(51200, **u16), torch.zeros(51200, **u16)
+    s = torch.cuda.current_stream().cuda_stream
+    k.shadows_bf16(w3.data_ptr(), w2.data_ptr(), w1b.data_ptr(), w1t.data_ptr(), w2tb.data_ptr(),
+                   w2b.data_ptr(), s)
+    outs = []
+    for fused in (False, True):
+        a1p = torch.zeros(2 * B * 18 * 18 * 16, **u16)
+        a1t = torch.zeros(B * 18 * 32 * 24, **u16)
+        idx1 = torch.zeros(B * 14 * 14 * 32, dtype=torch.uint8, device=cuda_dev)
+        a2p = torch.zeros(196 * B * 16, **u16)
+        a2t = torch.zeros(B // 16 * 3136 * 16, **u16)
+        idx2 = torch.zeros(B * 3136, dtype=torch.uint8, device=cuda_dev)
+        P = [t.data_ptr() for t in (a1p, a1t, idx1, a2p, a2t, idx2)]
+        if fused:
+            k.conv12_fwd_bf16(data.data_ptr(), step.data_ptr(), n_local, B, w1.data_ptr(),
+                              b1.data_ptr(), P[2], w2tb.data_ptr(), b2.data_ptr(), P[0], P[1],
+                              P[3], P[4], P[5], s)
+        else:
+            k.conv1_fwd_bf16(data.data_ptr(), step.data_ptr(), n_local, B, w1.data_ptr(),
+                             b1.data_ptr(), P[0], P[1], P[2], s)
+            k.conv2_fwd_bf16(P[0], B, w2tb.data_ptr(), b2.data_ptr(), P[3], P[4], P[5], s)
+        outs.append((a1p, a1t, idx1, a2p, a2t, idx2))
+    torch.cuda.synchronize()
+    for name, a, b in zip(("a1p", "a1t", "idx1", "a2p", "a2t", "idx2"), *outs):
+        assert torch.equal(a, b), name
+    # a2 vs torch: conv2 of the bf16 pooled conv1 output with bf16 weights
+    a1p = outs[1][0].view(torch.bfloat16).view(2, B, 18, 18, 16)
+    a1 = torch.cat([a1p[0], a1p[1]], dim=-1)[:, 2:16, 2:16, :].float()  # [B,14,14,32]
+    w2r = w2.to(torch.bfloat16).float()
+    y = F.conv2d(a1.permute(0, 3, 1, 2), w2r.permute(3, 2, 0, 1), b2, padding=2)
+    ref = F.max_pool2d(F.relu(y), 2).permute(0, 2, 3, 1).reshape(B, 3136)  # (py, px, co)
+    a2 = outs[1][3].view(torch.bfloat16).view(196, B, 16).permute(1, 0, 2).reshape(B, 3136)
+    assert _nrel(a2.float(), ref) < 1e-2
