@@ -172,7 +172,7 @@ class ResNet18(GenericModel):
         # training its epilogue also writes that BatchNorm's batch statistics
         # (shifted by the running mean: Fn.conv2d bn_shift)
         def sh(nm):
-            return bn[nm][0] if training else None
+            return bn[nm][0] if (training and Fn.BN_FWD_EPILOGUE) else None
 
         h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True, bn_shift=sh("bn1"))
         h = BN(h, "bn1", True, twin_only=True)  # the pool reads its bf16 twin

@@ -22,6 +22,7 @@ the reference uses for its TF variables, /root/reference/mpipy.py:38-53).
 from __future__ import annotations
 
 import dataclasses
+import os
 from typing import Optional
 
 import torch
@@ -173,7 +174,10 @@ def _bnstats(t: torch.Tensor, rmean: torch.Tensor):
 # its dgrad, whose epilogue writes the partial table, attached to the dX it
 # returns; the BatchNorm backward then skips its statistics pass.
 BN_BWD_STATS = {"epilogue": 0, "pass": 0}  # BatchNorm backward counts by route
-_BNB_EPILOGUE = True
+# A/B switches for the BatchNorm statistics epilogues (labs / profiles):
+# MTA_BN_FWD_EPILOGUE=0 / MTA_BN_BWD_EPILOGUE=0 fall back to the statistics passes
+_BNB_EPILOGUE = os.environ.get("MTA_BN_BWD_EPILOGUE", "1") != "0"
+BN_FWD_EPILOGUE = os.environ.get("MTA_BN_FWD_EPILOGUE", "1") != "0"
 
 
 def set_bn_bwd_epilogue(on: bool) -> None:
