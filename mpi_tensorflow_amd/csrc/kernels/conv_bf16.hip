@@ -683,27 +683,53 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
           }
         }
       } else if (bs) {  // fp32 dX = a BatchNorm's dY: its backward sums too
+        // every operand load is unconditional (clamped row, y = x when there is
+        // no ReLU) and issued before the first store: a conditional load
+        // compiles to a branch and a vmcnt(0) wait per element
         const size_t e0 = (size_t)mb * K + co;
-        float av[16], xv[16], yv[16];
+        const uint16_t* xp = reinterpret_cast<const uint16_t*>(bb.x) + e0;
+        const uint16_t* yq = reinterpret_cast<const uint16_t*>(bb.y) + e0;
+        auto tile = [&](auto has_add, auto all_rows) {
+          uint32_t xr[16], yr[16];
+          float av[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {  // every load before the first store
-          const int rr = (q & 3) + 8 * (q >> 2);
-          const size_t e = e0 + (size_t)((full || mb + rr < M) ? rr : 0) * K;
-          av[q] = addend ? addend[e] : 0.f;
-          xv[q] = bf16_at(bb.x, e);
-          yv[q] = bb.relu ? bf16_at(bb.y, e) : 1.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-          const int rr = (q & 3) + 8 * (q >> 2);
-          if (full || mb + rr < M) {
-            const float v = acc[i][j][q] + av[q];
-            p[(size_t)rr * K] = v;
-            const float d = yv[q] > 0.f ? v : 0.f;
-            ss1[j] += d;
-            ss2[j] += d * (xv[q] - bmu[j]) * brs[j];
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            const size_t o = (size_t)((decltype(all_rows)::value || mb + rr < M) ? rr : 0) * K;
+            xr[q] = xp[o];
+            yr[q] = yq[o];
+            if constexpr (decltype(has_add)::value) av[q] = addend[e0 + o];
           }
-        }
+          // sums first, stores after: a load waited on after a store waits
+          // for the store too (vmcnt counts both)
+          const uint32_t one = bb.relu ? 0u : 0x3f80u;  // bf16 1.0: the mask is off
+          float vv[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            float v = acc[i][j][q];
+            if constexpr (decltype(has_add)::value) v += av[q];
+            vv[q] = v;
+            const uint32_t ym = one ? one : yr[q];
+            float d = __uint_as_float(ym << 16) > 0.f ? v : 0.f;
+            if (!(decltype(all_rows)::value || mb + rr < M)) d = 0.f;
+            ss1[j] += d;
+            ss2[j] += d * (__uint_as_float(xr[q] << 16) - bmu[j]) * brs[j];
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            if (decltype(all_rows)::value || mb + rr < M) p[(size_t)rr * K] = vv[q];
+          }
+        };
+        if (addend && full)
+          tile(std::true_type{}, std::true_type{});
+        else if (addend)
+          tile(std::true_type{}, std::false_type{});
+        else if (full)
+          tile(std::false_type{}, std::true_type{});
+        else
+          tile(std::false_type{}, std::false_type{});
       } else if (full && addend) {
         // all 16 addend loads first, then the stores (interleaved, hipcc waited
         // vmcnt(0) per element: 16 serial round trips)
@@ -920,7 +946,7 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
             for (int c = 0; c < 4; ++c) {
               const size_t e = o[u] + (c >> 1) * W * C + (c & 1) * C;
               xv[u][c] = bf16_at(bb.x, e);
-              yv[u][c] = bb.relu ? bf16_at(bb.y, e) : 1.f;
+              yv[u][c] = bf16_at(bb.y, e);  // y = x without a ReLU (host), mask unused
             }
         }
 #pragma unroll
@@ -931,7 +957,7 @@ __global__ __launch_bounds__(NT) void dgrad3s2_kernel(ConvShape s, const __bf16*
             const float v = acc[c][i][j][q4 + u] + av[u][c];
             dx[o[u] + (c >> 1) * W * C + (c & 1) * C] = v;
             if (bst) {
-              const float d = yv[u][c] > 0.f ? v : 0.f;
+              const float d = (!bb.relu || yv[u][c] > 0.f) ? v : 0.f;
               bs1[j] += d;
               bs2[j] += d * (xv[u][c] - bmu[j]) * brs[j];
             }
@@ -1232,13 +1258,18 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
       if (bs) {
         const float av[4] = {a.x, a.y, a.z, a.w};
         const float mv[4] = {mu.x, mu.y, mu.z, mu.w}, rv[4] = {rs.x, rs.y, rs.z, rs.w};
+        // 4 bf16 of x and of y (= x without a ReLU) as one 8-byte load each
+        const uint2 xu = reinterpret_cast<const uint2*>(bb.x)[i];
+        const uint2 yu = reinterpret_cast<const uint2*>(bb.y)[i];
+        const float xv[4] = {__uint_as_float(xu.x << 16), __uint_as_float(xu.x & 0xffff0000u),
+                             __uint_as_float(xu.y << 16), __uint_as_float(xu.y & 0xffff0000u)};
+        const float yv[4] = {__uint_as_float(yu.x << 16), __uint_as_float(yu.x & 0xffff0000u),
+                             __uint_as_float(yu.y << 16), __uint_as_float(yu.y & 0xffff0000u)};
         float d[4], e[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const float xv = bf16_at(bb.x, 4 * i + c);
-          const float yv = bb.relu ? bf16_at(bb.y, 4 * i + c) : 1.f;
-          d[c] = yv > 0.f ? av[c] : 0.f;
-          e[c] = d[c] * (xv - mv[c]) * rv[c];
+          d[c] = (!bb.relu || yv[c] > 0.f) ? av[c] : 0.f;
+          e[c] = d[c] * (xv[c] - mv[c]) * rv[c];
         }
         t1.x += d[0]; t1.y += d[1]; t1.z += d[2]; t1.w += d[3];
         t2.x += e[0]; t2.y += e[1]; t2.z += e[2]; t2.w += e[3];
@@ -1994,6 +2025,12 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
       (!dyb || bstats->P != conv_bwd_data_stats_rows(s) || bstats->P == 0 || !bstats->x ||
        !bstats->mean || !bstats->rstd || (bstats->relu && !bstats->y)))
     throw std::runtime_error("conv_bwd_data_bf16: BatchNorm backward statistics not available here");
+  BnBwdStats bsv;
+  if (bstats && bstats->part) {  // the kernels load y unconditionally: y = x without a ReLU
+    bsv = *bstats;
+    if (!bsv.relu) bsv.y = bsv.x;
+    bstats = &bsv;
+  }
   const __bf16* wt = reinterpret_cast<const __bf16*>(wtb);
   if (!wt) {
     __bf16* wc = reinterpret_cast<__bf16*>(ws);
