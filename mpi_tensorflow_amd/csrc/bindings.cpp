@@ -92,7 +92,7 @@ PYBIND11_MODULE(_C, m) {
   k.def("conv12_fwd_wino", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
                               uintptr_t b1, uintptr_t a1, uintptr_t a1pf, uintptr_t idx1,
                               uintptr_t w2, uintptr_t U, uintptr_t b2, uintptr_t a2, uintptr_t idx2,
-                              uintptr_t w2t, uintptr_t s) {
+                              uintptr_t w2t, uintptr_t s, uintptr_t prof) {
     mnist::C12In c;
     c.data = P<const float>(data);
     c.step = P<const long long>(step);
@@ -104,9 +104,9 @@ PYBIND11_MODULE(_C, m) {
     c.idx1 = P<uint8_t>(idx1);
     mnist::launch_conv12_fwd_wino(c, batch, P<const float>(w2), P<const float>(U),
                                   P<const float>(b2), P<float>(a2), P<uint8_t>(idx2),
-                                  P<float>(w2t), S(s));
+                                  P<float>(w2t), S(s), P<unsigned long long>(prof));
     check_launch();
-  });
+  }, py::arg("data"), py::arg("step"), py::arg("n_local"), py::arg("batch"), py::arg("w1"), py::arg("b1"), py::arg("a1"), py::arg("a1pf"), py::arg("idx1"), py::arg("w2"), py::arg("U"), py::arg("b2"), py::arg("a2"), py::arg("idx2"), py::arg("w2t"), py::arg("s"), py::arg("prof") = 0);
   // bf16 engine forward pieces (tests): two-launch conv1 -> conv2 and the fused launch
   k.def("conv1_fwd_bf16", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
                              uintptr_t b1, uintptr_t a1p, uintptr_t a1t, uintptr_t idx1,
@@ -166,6 +166,18 @@ PYBIND11_MODULE(_C, m) {
                                   uintptr_t da1m, uintptr_t s) {
     mnist::launch_conv2_bwd_data_wino(P<const float>(dy2t), P<const float>(Ud), P<const float>(a1),
                                       batch, P<float>(da1m), S(s));
+    check_launch();
+  });
+  // labs: with the conv1 filter-gradient epilogue and per-wave phase stamps
+  k.def("conv2_bwd_data_wino_prof", [](uintptr_t dy2t, uintptr_t Ud, uintptr_t a1, int batch,
+                                       uintptr_t da1m, uintptr_t data, uintptr_t step, int n_local,
+                                       uintptr_t idx1, uintptr_t part1, uintptr_t prof,
+                                       uintptr_t s) {
+    const mnist::C1FilterArgs c1{P<const float>(data), P<const long long>(step), n_local,
+                                 P<const float>(da1m), P<const uint8_t>(idx1), P<float>(part1)};
+    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2t), P<const float>(Ud), P<const float>(a1),
+                                      batch, P<float>(da1m), S(s), nullptr, &c1,
+                                      P<unsigned long long>(prof));
     check_launch();
   });
   k.def("fc1_train_splits", &mnist::fc1_train_splits);

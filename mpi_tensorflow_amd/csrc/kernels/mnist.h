@@ -73,15 +73,19 @@ void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b
 // Winograd F(2x2,5x5) conv2 (wino.h): transformed filters U [36][32][64] and,
 // when Ud != nullptr, Ud [36][64][32] of the rotated filter (bwd-data)
 void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t s);
+// prof (labs): per-wave phase stamps [blocks][8 waves][5] (s_memtime)
 void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
-                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s);
+                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s,
+                            unsigned long long* prof = nullptr);
 void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
                            const float* b, float* out, uint8_t* argmax, float* w2t, hipStream_t s);
 // Winograd bwd-data: dy2t as for launch_conv2_bwd_data_l2, Ud from
 // launch_conv2_wino_weights; da1m = dA1 masked by a1 > 0
+// prof (labs): per-wave phase stamps [blocks][8 waves][7] (s_memtime)
 void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr,
-                                const C1FilterArgs* c1 = nullptr);
+                                const C1FilterArgs* c1 = nullptr,
+                                unsigned long long* prof = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,

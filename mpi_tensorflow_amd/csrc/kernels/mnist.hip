@@ -1021,11 +1021,15 @@ __device__ __forceinline__ void wino_fwd_loadb(int p, const float* __restrict__ 
 // padding tiles (14, 15) transform (zeros in, zeros out: no selects)
 constexpr int WX_ROWS = C2_XS_ROWS + 6, WX_FLOATS = WX_ROWS * C2_XS_COLS * 33;
 
-template <bool FUSED>
+// PROF (labs): per-wave s_memtime at the phase boundaries -> prof[block][wave][5]
+template <bool FUSED, bool PROF = false>
 __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ U, const float* __restrict__ b2, float* __restrict__ out,
-    uint8_t* __restrict__ argmax, float* __restrict__ w2t, const C12In c1) {
+    uint8_t* __restrict__ argmax, float* __restrict__ w2t, const C12In c1,
+    unsigned long long* __restrict__ prof = nullptr) {
+  unsigned long long stamp[5];
+  if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
   __shared__ float xs[WX_FLOATS];
   __shared__ float img[FUSED ? C12_IMG_ROWS * C12_IMG_LD : 1];
   __shared__ float V[WV_FLOATS];
@@ -1063,6 +1067,7 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
     }
   }
   __syncthreads();
+  if constexpr (PROF) stamp[1] = __builtin_amdgcn_s_memtime();
   // 2. input transform, one (ci, tile) item per thread.  Tile t = (pooled row
   // 2 pg + t / 7, col t % 7): its 6x6 window starts at halo row 2 (t / 7),
   // halo col 2 (t % 7).  Tiles 14, 15 are zero.
@@ -1081,6 +1086,7 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
     for (int p = 0; p < 36; ++p) vp[p * 512] = v[p];
   }
   __syncthreads();
+  if constexpr (PROF) stamp[2] = __builtin_amdgcn_s_memtime();
   // 3. batched products.  16x16x4 fragment maps: A lane l = V[tile l & 15][ci
   // 4 s + l >> 4]; B lane l = U[ci 4 s + l >> 4][co 16 q + l & 15]; C lane l,
   // reg j = (tile 4 (l >> 4) + j, co 16 q + l & 15).
@@ -1110,6 +1116,7 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   }
   // 4. cross-wave sums in a fixed order: waves 4-7 hand their partials to
   // waves 0-3 (slot = wave & 3), which add them and publish the pair sums
+  if constexpr (PROF) stamp[3] = __builtin_amdgcn_s_memtime();
   __syncthreads();  // every wave is done reading V
   float* R = V;     // [slot][o][q][reg][lane] = 4 x 4 x 4 x 4 x 64 floats
   const int slot = wave & 3;
@@ -1164,6 +1171,11 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
       if (argmax) argmax[oi] = (uint8_t)qq;
     }
   }
+  if constexpr (PROF) {
+    stamp[4] = __builtin_amdgcn_s_memtime();
+    if ((tid & 63) == 0)
+      for (int k = 0; k < 5; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 5 + k] = stamp[k];
+  }
 }
 
 // ------------------------------------ conv2 bwd-data, Winograd F(2x2,5x5) ----
@@ -1206,9 +1218,15 @@ __device__ __forceinline__ void wino_bwd_loadb(int p, const float* __restrict__ 
 // partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
 // values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
 // no second pass over dA1 and no role blocks in the filter-gradient launch.
+template <bool PROF = false>
 __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
     const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
-    int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1) {
+    int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1,
+    unsigned long long* __restrict__ prof = nullptr) {
+  // PROF (labs): s_memtime per wave -> prof[block][wave][7]: start, half 0
+  // transform / products, half 1 transform / products, dA1 written, end
+  unsigned long long stamp[7];
+  if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
   __shared__ float V[WV_FLOATS];
   const int nconv = gridDim.x - sgd.nblk / 2;
   if ((int)blockIdx.x >= nconv) {  // 512-thread blocks: two 256-thread role units
@@ -1243,6 +1261,7 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
       for (int p = 0; p < 36; ++p) V[(p * 32 + c) * 16 + t] = ok ? v[p] : 0.f;
     }
     __syncthreads();
+    if constexpr (PROF) stamp[1 + 2 * half] = __builtin_amdgcn_s_memtime();
     const float* ub = Ud + half * 1024 + lane;  // s in [8 half, 8 half + 8)
     float bA[16], bB[16];
     wino_bwd_loadb(wave, ub, bA);
@@ -1256,6 +1275,7 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
       if (p < 36) wino_bwd_point(p, V, lane, cur, y);
       __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (PROF) stamp[2 + 2 * half] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // V is rewritten by the next half / the reduction
   }
   float* R = V;  // [slot][o][q][reg][lane] = 4 x 4 x 2 x 4 x 64 floats
@@ -1320,7 +1340,15 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
       da1m[oi] = g1[o];
     }
   }
-  if (!do_c1) return;
+  if constexpr (PROF) stamp[5] = __builtin_amdgcn_s_memtime();
+  if (!do_c1) {
+    if constexpr (PROF) {
+      stamp[6] = stamp[5];
+      if (lane == 0)
+        for (int k = 0; k < 7; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 7 + k] = stamp[k];
+    }
+    return;
+  }
   // dW1[t][ci] += dA1 * x[argmax pixel + tap] over the thread's 4 positions
   float acc[26];
 #pragma unroll
@@ -1352,6 +1380,11 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
 #pragma unroll
     for (int w = 0; w < 7; ++w) sv += red1[w * (26 * 32 + 1) + i];
     c1.part1[(size_t)(n * 4 + pg) * 832 + i] = sv;
+  }
+  if constexpr (PROF) {
+    stamp[6] = __builtin_amdgcn_s_memtime();
+    if (lane == 0)
+      for (int k = 0; k < 7; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 7 + k] = stamp[k];
   }
 }
 
@@ -1948,11 +1981,16 @@ void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t
 }
 
 void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
-                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s) {
+                            const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s,
+                            unsigned long long* prof) {
   if (!c1.data || !c1.w1 || !c1.b1 || !c1.a1 || !c1.a1pf || !c1.idx1 || !U)
     throw std::runtime_error("conv12_fwd_wino: missing operand");
-  conv2_fwd_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2, w2t,
-                                                        c1);
+  if (prof)
+    conv2_fwd_wino_kernel<true, true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2,
+                                                                w2t, c1, prof);
+  else
+    conv2_fwd_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2, w2t,
+                                                          c1);
 }
 
 void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
@@ -2051,13 +2089,17 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
 
 void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd,
-                                const C1FilterArgs* c1) {
+                                const C1FilterArgs* c1, unsigned long long* prof) {
   FcSgd sg = fc_sgd_args(fc_sgd);
   // the SGD role works in 256-thread units: two per 512-thread block
   const int role_blocks = (sg.nblk + 1) / 2;
   sg.nblk = 2 * role_blocks;
-  conv2_bwd_data_wino_kernel<<<batch * 4 + role_blocks, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m,
-                                                                     sg, c1_args(c1));
+  if (prof)
+    conv2_bwd_data_wino_kernel<true><<<batch * 4 + role_blocks, WNT, 0, s>>>(
+        dy2t, Ud, a1, batch, da1m, sg, c1_args(c1), prof);
+  else
+    conv2_bwd_data_wino_kernel<false><<<batch * 4 + role_blocks, WNT, 0, s>>>(
+        dy2t, Ud, a1, batch, da1m, sg, c1_args(c1));
 }
 
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,

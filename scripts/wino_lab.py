@@ -65,6 +65,33 @@ def main():
             print(f"  {nm:12s} {d[..., i].mean().item():9.0f} {d[..., i].max().item():9.0f}")
         print(f"  span (first start -> last end) {(t[..., 4].max() - t0).item():.0f} cycles; "
               f"block start spread {(t[..., 0].max() - t0).item():.0f}")
+    if a.phases:
+        nb, nw = B * 4, 8
+        W_ = lambda n: ptr(e.params) + 4 * lay.offsets[n]  # noqa: E731
+        pf = torch.zeros(nb * nw * 5, dtype=torch.int64, device=dev)
+        pb = torch.zeros(nb * nw * 7, dtype=torch.int64, device=dev)
+        part1 = torch.zeros(B * 4 * 832, device=dev)
+        for _ in range(5):
+            k.conv12_fwd_wino(ptr(e.train_x), ptr(e.step_dev), e.n_local, B, W_("conv1_weight"),
+                              W_("conv1_bias"), ptr(b["a1"]), ptr(b["a1pf"]), ptr(b["idx1"]),
+                              W_("conv2_weight"), ptr(b["wino_u"]), W_("conv2_bias"), ptr(b["a2"]),
+                              ptr(b["idx2"]), 0, s, ptr(pf))
+            k.conv2_bwd_data_wino_prof(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]), B,
+                                       ptr(b["da1m"]), ptr(e.train_x), ptr(e.step_dev), e.n_local,
+                                       ptr(b["idx1"]), ptr(part1), ptr(pb), s)
+        torch.cuda.synchronize()
+        for nm, t, names in (("conv12_fwd(wino)", pf.view(nb, nw, 5).double(),
+                              ["conv1 -> halo", "input transform", "products", "sums + epilogue"]),
+                             ("bwd_data(wino)+c1", pb.view(nb, nw, 7).double(),
+                              ["h0 transform", "h0 products", "h1 transform", "h1 products",
+                               "sums + dA1", "conv1 wgrad"])):
+            t0 = t[..., 0].min()
+            d = t[..., 1:] - t[..., :-1]
+            print(f"{nm} phases, cycles per wave: mean / max")
+            for i, ph in enumerate(names):
+                print(f"  {ph:16s} {d[..., i].mean().item():9.0f} {d[..., i].max().item():9.0f}")
+            print(f"  span (first start -> last end) {(t[..., -1].max() - t0).item():.0f} cycles; "
+                  f"block start spread {(t[..., 0].max() - t0).item():.0f}")
     for name, fn in ops.items():
         if a.only and a.only not in name:
             continue

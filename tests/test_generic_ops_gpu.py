@@ -723,3 +723,32 @@ def test_softmax_rows_native(cuda_dev):
     y = Fn.softmax(x.to(cuda_dev))
     torch.cuda.synchronize()
     assert _rel(y.cpu(), torch.softmax(x, 1)) < 1e-6
+
+
+@pytest.mark.parametrize("shape,B", [((32, 32, 3), 32), ((224, 224, 3), 8)])
+def test_resnet18_bn_backward_epilogue_matches_pass(cuda_dev, shape, B):
+    """ResNet-18 bf16: one forward + backward with the BatchNorm backward sums
+    written by the dgrad epilogues equals the same step with the BatchNorms'
+    own statistics passes, parameter by parameter (same operands; only the
+    summation order of the BN sums differs)."""
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 4 * B, shape=shape)
+    grads, counts = [], []
+    try:
+        for on in (False, True):
+            Fn.set_bn_bwd_epilogue(on)
+            eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=B, dtype="bf16",
+                                              graph=False).validate(), x, y, cuda_dev)
+            n0 = Fn.BN_BWD_STATS["epilogue"]
+            eng.forward_backward_gpu()
+            torch.cuda.synchronize()
+            counts.append(Fn.BN_BWD_STATS["epilogue"] - n0)
+            grads.append({k: v.clone() for k, v in eng.layout.views(eng.grads).items()})
+    finally:
+        Fn.set_bn_bwd_epilogue(True)
+    assert counts[0] == 0 and counts[1] >= 12, counts
+    errs = {k: _rel(grads[1][k], grads[0][k]) for k in grads[0]}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
+    assert worst[0][1] < 5e-3, worst
