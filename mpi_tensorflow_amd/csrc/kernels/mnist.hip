@@ -640,7 +640,7 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
     if (i < NIMG) img[i] = iv[j];
   }
   __syncthreads();
-  if (wave >= 4) return;  // the tile loop below is laid out for 4 waves
+  constexpr int NW = NT / 64;  // every wave runs conv1 tiles (pairs t, t + NW)
   const int y0 = 4 * pg - 2;  // a1 row of halo row 0
   const int ya = max(y0, 0), yb = min(y0 + C2_XS_ROWS, 14);
   const int nwin = (yb - ya) * 14, ntile = (nwin + 7) / 8;
@@ -672,14 +672,15 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
       }
     }
   };
-  // tiles t and t + 4 of this wave as two interleaved accumulator chains:
+  // tiles t and t + NW of this wave as two interleaved accumulator chains:
   // consecutive MFMAs are independent, and each tile's sum keeps the K order of
-  // the standalone conv1 kernel (same results)
-  for (int t = wave; t < ntile; t += 8) {
-    const bool two = t + 4 < ntile;
+  // the standalone conv1 kernel (same results).  With 8 waves (the Winograd
+  // forward's 512 threads) the 14 tiles take 2 per wave instead of 4.
+  for (int t = wave; t < ntile; t += 2 * NW) {
+    const bool two = t + NW < ntile;
     bool v0, v1;
     const float* ib0 = tile_base(t, v0);
-    const float* ib1 = tile_base(two ? t + 4 : t, v1);
+    const float* ib1 = tile_base(two ? t + NW : t, v1);
     f32x16 acc0 = zero16(), acc1 = zero16();
 #pragma unroll
     for (int st = 0; st < 16; ++st) {
@@ -689,7 +690,7 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
       acc1 = mfma32x32x2((v1 && k < 25) ? a1v : 0.f, wb[st], acc1);
     }
     epilogue(t, acc0);
-    if (two) epilogue(t + 4, acc1);
+    if (two) epilogue(t + NW, acc1);
   }
 }
 
@@ -972,50 +973,19 @@ __device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
 //   1. a1 halo tile in LDS (FUSED: conv1 recomputed into it, conv1_into_halo)
 //   2. input transform: V[p][ci][tile] (36 x 32 x 16 floats) in LDS
 //   3. 36 batched products [16 tiles x 32 ci] x [32 ci x 64 co] on
-//      v_mfma_f32_16x16x4_f32; wave w owns points w, w+4, ..., each folded
-//      into the four 2x2 outputs right after its 8 k-steps (the output
-//      transform is linear), B = U[p] straight from L2, one point ahead
-//   4. the four waves' partial outputs summed through LDS in wave order,
-//      then bias + ReLU + pool + argmax per (tile, co)
+//      v_mfma_f32_16x16x4_f32; wave = (co quarter, half of the points), each
+//      point folded into the four 2x2 outputs right after its 8 k-steps (the
+//      output transform is linear), B = U[p] straight from L2, one pair ahead
+//   4. the two halves' partial outputs summed through LDS, then bias + ReLU +
+//      pool + argmax from registers
 // FLOP per image: 36 x 49 x 32 x 64 x 2 = 7.2 M (direct: 20.1 M).
 constexpr int WV_FLOATS = 36 * 32 * 16;  // V image; reused for the cross-wave sums
 
 // 512 threads = 8 waves, two per SIMD: the transform runs one item per thread
-// and each SIMD interleaves two waves' MFMA streams (waves 0-3 own 5 points,
-// waves 4-7 own 4).  B fragments of the next point are loaded into the other
-// of two register sets while the current point's MFMAs run.
+// and each SIMD interleaves two waves' MFMA streams (wave = co quarter x half
+// of the 36 points).  B fragments of the next point pair are loaded into the
+// other of two register sets while the current pair's MFMAs run.
 constexpr int WNT = 512, WNW = WNT / 64;
-
-// one point's 32 MFMAs (8 k-steps x 4 co quarters), folded into the outputs
-__device__ __forceinline__ void wino_fwd_point(int p, const float* __restrict__ V, int lane,
-                                               const float (&b)[32], f32x4 (&y)[4][4]) {
-  float av[8];
-  const float* vp = V + p * 512 + lane;  // (p * 32 + 4 s + kq) * 16 + r16
-#pragma unroll
-  for (int s = 0; s < 8; ++s) av[s] = vp[s * 64];
-  f32x4 acc[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[q] = mfma16x16x4(av[s], b[s * 4 + q], acc[q]);
-#pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    const float c = kWinoCoef.c[p][o];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) y[o][q] += c * acc[q];
-  }
-}
-
-// ub = U + lane offset; fragment (s, q) of point p is the 64 floats at
-// (32 p + 4 s + q) * 64: one base per point, immediate offsets
-__device__ __forceinline__ void wino_fwd_loadb(int p, const float* __restrict__ ub,
-                                               float (&b)[32]) {
-  const float* bp = ub + p * 2048;
-#pragma unroll
-  for (int j = 0; j < 32; ++j) b[j] = bp[j * 64];
-}
 
 // halo image rows: the 8 of the block's windows + 6 zero rows that the two
 // padding tiles (14, 15) transform (zeros in, zeros out: no selects)
@@ -1090,85 +1060,90 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   // 3. batched products.  16x16x4 fragment maps: A lane l = V[tile l & 15][ci
   // 4 s + l >> 4]; B lane l = U[ci 4 s + l >> 4][co 16 q + l & 15]; C lane l,
   // reg j = (tile 4 (l >> 4) + j, co 16 q + l & 15).
-  f32x4 y[4][4];  // [output i*2+j][co quarter]
+  // Wave w owns co quarter q = w & 3 and the 18 points of half ph = w >> 2
+  // (144 MFMAs per wave, every wave the same), two points at a time as four
+  // accumulator chains (even / odd k-steps of each point); each point is
+  // folded into the four 2x2 outputs right after its 8 k-steps.  The two
+  // halves' partials meet once (LDS) and the ph = 0 waves finish bias, ReLU,
+  // pool and argmax straight from their registers: no (tile, co) re-read of
+  // all eight waves' partial outputs.
+  const int qw = wave & 3, ph = wave >> 2;
+  f32x4 y[4];  // [output i*2+j] for (tiles, co quarter qw)
 #pragma unroll
-  for (int o = 0; o < 4; ++o)
+  for (int o = 0; o < 4; ++o) y[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* ub = U + qw * 64 + lane;  // fragment (s, qw) of point p at (32 p + 4 s) * 64
+  auto loadb2 = [&](int p0, float(&b)[16]) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) y[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* ub = U + lane;  // kq * 16 + r16
-  // points wave, wave + 8, ... (5 for waves 0-3, 4 for waves 4-7), fully
-  // unrolled with two register sets: the B fragments of point i + 1 are
-  // issued before point i's MFMAs (sched barriers keep that order)
-  // The next point's loads are unconditional (clamped index): a load under a
-  // branch makes the waitcnt pass count for the path without it, and every
-  // MFMA of the point would then wait for the prefetch.
-  float bA[32], bB[32];
-  wino_fwd_loadb(wave, ub, bA);
+    for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
-    const int p = wave + WNW * i;
-    float(&cur)[32] = (i & 1) ? bB : bA;
-    float(&nxt)[32] = (i & 1) ? bA : bB;
-    if (i < 4) wino_fwd_loadb(min(p + WNW, 35), ub, nxt);
+      for (int k = 0; k < 8; ++k) b[pt * 8 + k] = ub[(32 * (p0 + pt) + 4 * k) * 64];
+  };
+  float bA[16], bB[16];
+  loadb2(18 * ph, bA);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int p0 = 18 * ph + 2 * i;
+    float(&cur)[16] = (i & 1) ? bB : bA;
+    float(&nxt)[16] = (i & 1) ? bA : bB;
+    if (i < 8) loadb2(p0 + 2, nxt);
     __builtin_amdgcn_sched_barrier(0);
-    if (p < 36) wino_fwd_point(p, V, lane, cur, y);
+    float av[16];
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) av[pt * 8 + k] = V[(p0 + pt) * 512 + k * 64 + lane];
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) acc[pt][0] = acc[pt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+        acc[pt][k & 1] = mfma16x16x4(av[pt * 8 + k], cur[pt * 8 + k], acc[pt][k & 1]);
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const f32x4 a = acc[pt][0] + acc[pt][1];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) y[o] += kWinoCoef.c[p0 + pt][o] * a;
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // 4. cross-wave sums in a fixed order: waves 4-7 hand their partials to
-  // waves 0-3 (slot = wave & 3), which add them and publish the pair sums
+  // 4. the two point halves' partials summed once (half 1 -> LDS -> half 0),
+  // then bias + ReLU + 2x2 pool + argmax from the half-0 waves' registers
   if constexpr (PROF) stamp[3] = __builtin_amdgcn_s_memtime();
   __syncthreads();  // every wave is done reading V
-  float* R = V;     // [slot][o][q][reg][lane] = 4 x 4 x 4 x 4 x 64 floats
-  const int slot = wave & 3;
-  auto rix = [&](int sl, int o, int q, int j) { return (((sl * 4 + o) * 4 + q) * 4 + j) * 64; };
-  if (wave >= 4) {
+  float* R = V;     // [qw][o][reg][lane]
+  if (ph == 1) {
 #pragma unroll
     for (int o = 0; o < 4; ++o)
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) R[rix(slot, o, q, j) + lane] = y[o][q][j];
+      for (int j = 0; j < 4; ++j) R[((qw * 4 + o) * 4 + j) * 64 + lane] = y[o][j];
   }
   __syncthreads();
-  if (wave < 4) {
+  if (ph == 0) {
+    const int co = 16 * qw + (lane & 15);
+    const float bias = b2[co];
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * (lane >> 4) + j;  // tile = pooling window of the block
+      float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int o = 0; o < 4; ++o) v[o] = y[o][j] + R[((qw * 4 + o) * 4 + j) * 64 + lane];
+      float m = v[0];
+      int qq = 0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float* r = R + rix(slot, o, q, j) + lane;
-          *r = y[o][q][j] + *r;
+      for (int o = 1; o < 4; ++o) {
+        if (v[o] > m) {  // strict: first max wins (TF MaxPool order)
+          m = v[o];
+          qq = o;
         }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < 1024 / WNT; ++e) {
-    const int item = tid + WNT * e, co = item & 63, t = item >> 6;  // (tile, co)
-    if (t >= 14) continue;
-    const int q = co >> 4, l = (t >> 2) * 16 + (co & 15), j = t & 3;
-    float v[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      float sum = 0.f;
-#pragma unroll
-      for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
-      v[o] = sum;
-    }
-    float m = v[0];
-    int qq = 0;
-#pragma unroll
-    for (int o = 1; o < 4; ++o) {
-      if (v[o] > m) {  // strict: first max wins (TF MaxPool order)
-        m = v[o];
-        qq = o;
       }
-    }
-    const int pr = pr0 + t / 7, pc = t % 7;
-    if (pr < 7) {
-      const int oi = ((n * 7 + pr) * 7 + pc) * 64 + co;
-      out[oi] = fmaxf(m + b2[co], 0.f);
-      if (argmax) argmax[oi] = (uint8_t)qq;
+      const int pr = pr0 + t / 7, pc = t % 7;
+      if (t < 14 && pr < 7) {
+        const int oi = ((n * 7 + pr) * 7 + pc) * 64 + co;
+        out[oi] = fmaxf(m + bias, 0.f);
+        if (argmax) argmax[oi] = (uint8_t)qq;
+      }
     }
   }
   if constexpr (PROF) {
@@ -1243,28 +1218,38 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   for (int o = 0; o < 4; ++o)
 #pragma unroll
     for (int q = 0; q < 2; ++q) y[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
+  // input windows of channels 32 half .. 32 half + 31 straight from L2 (one
+  // (tile, channel) item per thread); half 1's loads are issued before half
+  // 0's products so their latency hides under the MFMAs
+  const int it_t = tid & 15, it_c = tid >> 4;
+  const int it_tr = 2 * pg + it_t / 7, it_tc = it_t % 7;
+  const bool it_ok = it_t < 14 && it_tr < 7;
+  auto load_in = [&](int half, float (&d)[36]) {
+    const float* src = dy2t + ((size_t)(n * 64 + 32 * half + it_c) * 18 + 2 * (it_ok ? it_tr : 0)) *
+                                  MNIST32_T_LD + 2 * (it_ok ? it_tc : 0);
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+      for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[yy * MNIST32_T_LD + xx];
+  };
+  float din[36];
+  load_in(0, din);
+#pragma unroll
   for (int half = 0; half < 2; ++half) {
-    {  // input transform of channels 32 half .. 32 half + 31 straight from L2
-      const int t = tid & 15, c = tid >> 4;
-      const int tr = 2 * pg + t / 7, tc = t % 7;
-      const bool ok = t < 14 && tr < 7;
-      const float* src = dy2t + ((size_t)(n * 64 + 32 * half + c) * 18 + 2 * (ok ? tr : 0)) *
-                                    MNIST32_T_LD + 2 * (ok ? tc : 0);
-      float d[36], v[36];
+    {  // input transform
+      float v[36];
+      wino::input_tile(din, v);
 #pragma unroll
-      for (int yy = 0; yy < 6; ++yy)
-#pragma unroll
-        for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[yy * MNIST32_T_LD + xx];
-      wino::input_tile(d, v);
-#pragma unroll
-      for (int p = 0; p < 36; ++p) V[(p * 32 + c) * 16 + t] = ok ? v[p] : 0.f;
+      for (int p = 0; p < 36; ++p) V[(p * 32 + it_c) * 16 + it_t] = it_ok ? v[p] : 0.f;
     }
     __syncthreads();
     if constexpr (PROF) stamp[1 + 2 * half] = __builtin_amdgcn_s_memtime();
     const float* ub = Ud + half * 1024 + lane;  // s in [8 half, 8 half + 8)
     float bA[16], bB[16];
     wino_bwd_loadb(wave, ub, bA);
+    // half 1's inputs, in flight during half 0's products (loads return in
+    // order: issued after the first fragments, the first products do not wait)
+    if (half == 0) load_in(1, din);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {  // unconditional clamped prefetch, as in the forward
       const int p = wave + WNW * i;

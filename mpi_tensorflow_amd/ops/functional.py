@@ -591,6 +591,19 @@ class _BNFn(torch.autograd.Function):
             dx = torch.empty_like(dy)
             dxf, dxb = dx, _bf16_out(dx)
         st = _bnbwd_stats(dy, mean) if (xb16 and (ctx.yb16 or not ctx.relu)) else None
+        if st is not None and os.environ.get("MTA_BNB_CHECK") == "1":  # debug: vs the pass
+            db0 = torch.empty(Cc, device=x.device)
+            dg0 = torch.empty(Cc, device=x.device)
+            part, prow = st
+            C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc,
+                         ctx.relu, ptr(ctx.ws), ptr(dg0), ptr(db0), 0, 0, stream_handle(),
+                         ptr(torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)), xb16,
+                         ctx.yb16)
+            t = part.view(2, Cc // 64, prow, 64).sum(2).reshape(2, Cc)
+            e1 = ((t[0] - db0).norm() / db0.norm().clamp_min(1e-12)).item()
+            e2 = ((t[1] - dg0).norm() / dg0.norm().clamp_min(1e-12)).item()
+            print(f"BNB_CHECK rows={rows} C={Cc} relu={ctx.relu} P={prow} "
+                  f"db_err={e1:.2e} dg_err={e2:.2e}", flush=True)
         if st is not None:  # the dgrad producing dy wrote the sums (see above)
             BN_BWD_STATS["epilogue"] += 1
             C.ops.bn_bwd_partials(ptr(st[0]), st[1], ptr(x), ptr(dy), ptr(y), ptr(mean),

@@ -129,10 +129,14 @@ def test_forward_backward_grads_match_oracle(cuda_dev, data, batch):
         assert err < 2e-4, (s.name, err)
 
 
-def test_per_step_grads_along_native_trajectory(cuda_dev, data):
+@pytest.mark.parametrize("algo,max_ties", [("direct", 2), ("winograd", 4)])
+def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties):
     """Strict per-step check: at every step the native grads equal the oracle's
-    grads evaluated at the NATIVE parameters (no chaotic accumulation)."""
-    nat, ref = _engines(cuda_dev, data)
+    grads evaluated at the NATIVE parameters (no chaotic accumulation).  The
+    Winograd conv2 rounds differently from the oracle's direct sum (~1.4e-6
+    relative, docs/ACCURACY.md) so max-pool near-ties re-route a gradient
+    element somewhat more often than with the direct kernels."""
+    nat, ref = _engines(cuda_dev, data, conv_algo=algo)
     ties = 0
     for step in range(12):
         ref.params.copy_(nat.params)
@@ -152,7 +156,7 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data):
         if max(errs.values()) > 1e-4:
             ties += 1
         nat.train(1)
-    assert ties <= 2, ties
+    assert ties <= max_ties, ties
 
 
 def test_training_trajectory_matches_oracle(cuda_dev, data):

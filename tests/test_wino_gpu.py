@@ -118,6 +118,13 @@ def test_wino_fused_conv12_forward_matches_oracle(cuda_dev, step):
     r1 = F.max_pool2d(F.relu(z1), 2, 2)
     assert _rel(a1.double(), r1.permute(0, 2, 3, 1)) < 1e-5
     assert torch.equal(a1pf[:, 2:16, 2:16], a1)
+    # the fused conv1 (its tiles spread over all 8 waves) equals the standalone
+    # conv1 kernel bit for bit (each tile's K order is the same)
+    a1s = torch.empty_like(a1)
+    i1s = torch.empty_like(i1)
+    Cn.mnist.conv1_fwd(ptr(xd), ptr(st), n_local, B, ptr(w1), ptr(b1), ptr(a1s), ptr(i1s), s, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(a1s, a1) and torch.equal(i1s, i1)
     z2 = F.conv2d(a1.permute(0, 3, 1, 2).double(), w2.permute(3, 2, 0, 1).double(), b2.double(),
                   padding=2)
     r2 = F.max_pool2d(F.relu(z2), 2, 2)
