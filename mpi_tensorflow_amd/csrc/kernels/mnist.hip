@@ -1061,8 +1061,8 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   // 4 s + l >> 4]; B lane l = U[ci 4 s + l >> 4][co 16 q + l & 15]; C lane l,
   // reg j = (tile 4 (l >> 4) + j, co 16 q + l & 15).
   // Wave w owns co quarter q = w & 3 and the 18 points of half ph = w >> 2
-  // (144 MFMAs per wave, every wave the same), two points at a time as four
-  // accumulator chains (even / odd k-steps of each point); each point is
+  // (144 MFMAs per wave, every wave the same), two points at a time (one
+  // accumulator chain each, interleaved); each point is
   // folded into the four 2x2 outputs right after its 8 k-steps.  The two
   // halves' partials meet once (LDS) and the ph = 0 waves finish bias, ReLU,
   // pool and argmax straight from their registers: no (tile, co) re-read of
@@ -1092,20 +1092,19 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
     for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
       for (int k = 0; k < 8; ++k) av[pt * 8 + k] = V[(p0 + pt) * 512 + k * 64 + lane];
-    f32x4 acc[2][2];
+    // one accumulator chain per point (k order 0..7), the two points' MFMAs
+    // interleaved
+    f32x4 acc[2];
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) acc[pt][0] = acc[pt][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int pt = 0; pt < 2; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < 8; ++k)
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt)
-        acc[pt][k & 1] = mfma16x16x4(av[pt * 8 + k], cur[pt * 8 + k], acc[pt][k & 1]);
+      for (int pt = 0; pt < 2; ++pt) acc[pt] = mfma16x16x4(av[pt * 8 + k], cur[pt * 8 + k], acc[pt]);
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const f32x4 a = acc[pt][0] + acc[pt][1];
+    for (int pt = 0; pt < 2; ++pt)
 #pragma unroll
-      for (int o = 0; o < 4; ++o) y[o] += kWinoCoef.c[p0 + pt][o] * a;
-    }
+      for (int o = 0; o < 4; ++o) y[o] += kWinoCoef.c[p0 + pt][o] * acc[pt];
     __builtin_amdgcn_sched_barrier(0);
   }
   // 4. the two point halves' partials summed once (half 1 -> LDS -> half 0),
@@ -1159,36 +1158,11 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
 // (written by fc1 backward) with the filters Ud [36][64][32].  Block = (image,
 // pair of 2x2-tile rows) = 14 tiles (M 16), N = 32 input channels of conv2,
 // K = 64 in two halves of 32 (the transformed image V is 72 KB per half).
-// Epilogue: the ReLU1 mask (a1 > 0), NHWC da1m.  Optional FC SGD role blocks
-// (single rank) as in conv2_bwd_data_l2_kernel.
-__device__ __forceinline__ void wino_bwd_point(int p, const float* __restrict__ V, int lane,
-                                               const float (&b)[16], f32x4 (&y)[4][2]) {
-  float av[8];
-  const float* vp = V + p * 512 + lane;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) av[s] = vp[s * 64];
-  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int s = 0; s < 8; ++s)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) acc[q] = mfma16x16x4(av[s], b[s * 2 + q], acc[q]);
-#pragma unroll
-  for (int o = 0; o < 4; ++o) {
-    const float c = kWinoCoef.c[p][o];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) y[o][q] += c * acc[q];
-  }
-}
-
-// ub = Ud + lane offset + this K half; fragment (s, q) of point p at
-// ((16 p + s) * 2 + q) * 64
-__device__ __forceinline__ void wino_bwd_loadb(int p, const float* __restrict__ ub,
-                                               float (&b)[16]) {
-  const float* bp = ub + p * 2048;
-#pragma unroll
-  for (int j = 0; j < 16; ++j) b[j] = bp[j * 64];
-}
-
+// Waves = (ci half, quarter of the 36 points), each point's 8 k-steps per K
+// half folded into the 2x2 outputs at once; the four quarters' partials are
+// summed in order by the epilogue threads.  Half 1's input windows are loaded
+// under half 0's products.  Epilogue: the ReLU1 mask (a1 > 0), NHWC da1m.
+// Optional FC SGD role blocks (single rank) as in conv2_bwd_data_l2_kernel.
 // c1.part1 != nullptr: each block also computes the conv1 filter-gradient
 // partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
 // values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
@@ -1213,11 +1187,12 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   // wave-uniform in an SGPR: the point index p, its output-transform weights
   // (scalar loads) and the fragment bases are then scalar
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  f32x4 y[4][2];
+  // wave = (ci half qw = wave & 1, point quarter pq = wave >> 1: points 9 pq ..
+  // 9 pq + 8): 72 MFMAs per wave per K half, every wave the same
+  const int qw = wave & 1, pq = wave >> 1;
+  f32x4 y[4];
 #pragma unroll
-  for (int o = 0; o < 4; ++o)
-#pragma unroll
-    for (int q = 0; q < 2; ++q) y[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int o = 0; o < 4; ++o) y[o] = f32x4{0.f, 0.f, 0.f, 0.f};
   // input windows of channels 32 half .. 32 half + 31 straight from L2 (one
   // (tile, channel) item per thread); half 1's loads are issued before half
   // 0's products so their latency hides under the MFMAs
@@ -1244,52 +1219,60 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
     }
     __syncthreads();
     if constexpr (PROF) stamp[1 + 2 * half] = __builtin_amdgcn_s_memtime();
-    const float* ub = Ud + half * 1024 + lane;  // s in [8 half, 8 half + 8)
-    float bA[16], bB[16];
-    wino_bwd_loadb(wave, ub, bA);
+    // fragment (s, qw) of point p, s in [8 half, 8 half + 8): ub + p * 2048 + s * 128
+    const float* ub = Ud + half * 1024 + qw * 64 + lane;
+    auto loadb3 = [&](int p0, float(&b)[24]) {
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[pt * 8 + k] = ub[(p0 + pt) * 2048 + k * 128];
+    };
+    float bA[24], bB[24];
+    loadb3(9 * pq, bA);
     // half 1's inputs, in flight during half 0's products (loads return in
     // order: issued after the first fragments, the first products do not wait)
     if (half == 0) load_in(1, din);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {  // unconditional clamped prefetch, as in the forward
-      const int p = wave + WNW * i;
-      float(&cur)[16] = (i & 1) ? bB : bA;
-      float(&nxt)[16] = (i & 1) ? bA : bB;
-      if (i < 4) wino_bwd_loadb(min(p + WNW, 35), ub, nxt);
+    for (int i = 0; i < 3; ++i) {  // three points at a time
+      const int p0 = 9 * pq + 3 * i;
+      float(&cur)[24] = (i & 1) ? bB : bA;
+      float(&nxt)[24] = (i & 1) ? bA : bB;
+      if (i < 2) loadb3(p0 + 3, nxt);
       __builtin_amdgcn_sched_barrier(0);
-      if (p < 36) wino_bwd_point(p, V, lane, cur, y);
+      float av[24];
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) av[pt * 8 + k] = V[(p0 + pt) * 512 + k * 64 + lane];
+      f32x4 acc[3];  // one chain per point (k order), three interleaved
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) acc[pt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int pt = 0; pt < 3; ++pt)
+          acc[pt] = mfma16x16x4(av[pt * 8 + k], cur[pt * 8 + k], acc[pt]);
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+#pragma unroll
+        for (int o = 0; o < 4; ++o) y[o] += kWinoCoef.c[p0 + pt][o] * acc[pt];
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (PROF) stamp[2 + 2 * half] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // V is rewritten by the next half / the reduction
   }
-  float* R = V;  // [slot][o][q][reg][lane] = 4 x 4 x 2 x 4 x 64 floats
-  const int slot = wave & 3;
-  auto rix = [&](int sl, int o, int q, int j) { return (((sl * 4 + o) * 2 + q) * 4 + j) * 64; };
-  if (wave >= 4) {
+  // every wave's partial outputs -> R [qw][pq][o][reg][lane]; the epilogue
+  // threads sum the four point quarters in order
+  float* R = V;
+  auto rix = [&](int pq_, int o, int q, int j) { return (((q * 4 + pq_) * 4 + o) * 4 + j) * 64; };
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+  for (int o = 0; o < 4; ++o)
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) R[rix(slot, o, q, j) + lane] = y[o][q][j];
-  }
-  __syncthreads();
-  if (wave < 4) {
-#pragma unroll
-    for (int o = 0; o < 4; ++o)
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          float* r = R + rix(slot, o, q, j) + lane;
-          *r = y[o][q][j] + *r;
-        }
-  }
+    for (int j = 0; j < 4; ++j) R[rix(pq, o, qw, j) + lane] = y[o][j];
   // conv1 band: the padded input rows 8 pg - 2 .. 8 pg + 9 (x 32 columns)
   // staged next to R while the sums are read; argmax codes loaded early
   constexpr int C1X = 12 * 32;
-  float* xs1 = V + 4 * 4 * 2 * 4 * 64;
+  float* xs1 = V + 2 * 4 * 4 * 4 * 64;
   float* red1 = xs1 + C1X;  // [7 waves][26 * 32 + 1]
   const bool do_c1 = c1.part1 != nullptr;
   const int ci = tid & 31, t = tid >> 5;

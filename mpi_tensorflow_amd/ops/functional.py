@@ -306,6 +306,14 @@ class _ConvFn(torch.autograd.Function):
                                         ptr(add), ptr(ctx.wtb_d), ptr(part), prow, ptr(bx),
                                         ptr(byb), ptr(bmean), ptr(brstd), brelu)
                     _attach_bnbwd_stats(dx, part, prow, bmean)
+                    if os.environ.get("MTA_BNB_CHECK") == "1":  # debug: dX vs the plain dgrad
+                        dx2 = torch.empty_like(dx)
+                        C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx2), ptr(ctx.ws), s, True,
+                                            ptr(dyb), ptr(add), ptr(ctx.wtb_d))
+                        e = ((dx2 - dx).norm() / dx2.norm().clamp_min(1e-12)).item()
+                        print(f"BNB_CHECK dgrad N={sh.N} H={sh.H} C={sh.C} K={sh.K} "
+                              f"R={sh.R} s={sh.stride} add={add is not None} dx_err={e:.2e}",
+                              flush=True)
                 else:
                     C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
                                         ptr(add), ptr(ctx.wtb_d))
@@ -591,6 +599,8 @@ class _BNFn(torch.autograd.Function):
             dx = torch.empty_like(dy)
             dxf, dxb = dx, _bf16_out(dx)
         st = _bnbwd_stats(dy, mean) if (xb16 and (ctx.yb16 or not ctx.relu)) else None
+        if st is not None and os.environ.get("MTA_BNB_IGNORE") == "1":  # debug: pass anyway
+            st = None
         if st is not None and os.environ.get("MTA_BNB_CHECK") == "1":  # debug: vs the pass
             db0 = torch.empty(Cc, device=x.device)
             dg0 = torch.empty(Cc, device=x.device)

@@ -2,9 +2,9 @@
 vs plain PyTorch fp32, and of whole LeNet-5 / ResNet-18 training steps vs the
 CPU oracle path."""
 
-import numpy as np
 import os
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
