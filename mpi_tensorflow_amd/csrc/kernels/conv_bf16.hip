@@ -518,7 +518,11 @@ __device__ __forceinline__ void glds(const void* src, char* dst) {
 inline int halo_rows(const ConvShape& s, int bm) { return ((bm + s.W - 2) / s.W + 3) * s.W; }
 }  // namespace h3
 
-template <int BM, int BN, int RB>
+// EPI: the epilogue kind, one per instantiation (each keeps only its own
+// code): 0 fp32 output (+ addend), 1 bf16 output (+ the BatchNorm forward
+// statistics, ConvStats), 2 fp32 dX + the BatchNorm backward sums (BnBwdStats,
+// + addend)
+template <int BM, int BN, int RB, int EPI>
 __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __restrict__ x,
                                                    const __bf16* __restrict__ wt,
                                                    float* __restrict__ y, int cps,
@@ -585,14 +589,17 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
   };
   // BatchNorm shift of this lane's output columns (loaded up front, see
   // fwd_kernel); dgrad feeding a BatchNorm backward: its mean / rstd
-  const bool bs = !yb && bb.part;
+  constexpr bool bs = EPI == 2;
   float kcol[TN], bmu[TN], brs[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int co = n0 + wn * (BN / 2) + 32 * j + r;
-    kcol[j] = (yb && cs.part) ? cs.shift[co] : 0.f;
-    bmu[j] = bs ? bb.mean[co] : 0.f;
-    brs[j] = bs ? bb.rstd[co] : 0.f;
+    kcol[j] = bmu[j] = brs[j] = 0.f;
+    if constexpr (EPI == 1) kcol[j] = cs.part ? cs.shift[co] : 0.f;
+    if constexpr (EPI == 2) {
+      bmu[j] = bb.mean[co];
+      brs[j] = bb.rstd[co];
+    }
   }
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -656,10 +663,81 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
   // once per tile (per element they were ~40 % of the kernel's instructions)
   y += (size_t)blockIdx.y * M * s.K;
   const size_t K = s.K;
-  const bool st = yb && cs.part;
+  const bool st = EPI == 1 && cs.part;
   float ss1[TN], ss2[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) ss1[j] = ss2[j] = 0.f;
+  if constexpr (EPI == 2) {
+    // fp32 dX = a BatchNorm's dY, plus that BatchNorm's backward sums.  Every
+    // operand load of every tile (x, y = the ReLU mask source, addend) is
+    // issued first from clamped, always-valid rows, then one wait, the sums,
+    // and the stores last: a load issued after a store waits for that store
+    // too (vmcnt counts both), and a conditional load compiles to a branch
+    // plus a wait per element (each measured ~2x on the 128-pixel tiles)
+    auto epi2 = [&](auto has_add) {
+      constexpr bool ADD = decltype(has_add)::value;
+      uint32_t xr[TM][TN][16], yr[TM][TN][16];
+      float av[TM][TN][ADD ? 16 : 1];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int co = n0 + wn * (BN / 2) + 32 * j + r;
+          const size_t e0 = (size_t)mb * K + co;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            const size_t e = e0 + (size_t)(mb + rr < M ? rr : 0) * K;
+            xr[i][j][q] = reinterpret_cast<const uint16_t*>(bb.x)[e];
+            yr[i][j][q] = reinterpret_cast<const uint16_t*>(bb.y)[e];
+            if constexpr (ADD) av[i][j][q] = addend[e];
+          }
+        }
+      }
+      const uint32_t one = bb.relu ? 0u : 0x3f80u;  // bf16 1.0: no ReLU mask
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            float v = acc[i][j][q];
+            if constexpr (ADD) v += av[i][j][q];
+            acc[i][j][q] = v;
+            const uint32_t ym = one ? one : yr[i][j][q];
+            float d = __uint_as_float(ym << 16) > 0.f ? v : 0.f;
+            if (mb + rr >= M) d = 0.f;
+            ss1[j] += d;
+            ss2[j] += d * (__uint_as_float(xr[i][j][q] << 16) - bmu[j]) * brs[j];
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float* p = y + (size_t)mb * K + n0 + wn * (BN / 2) + 32 * j + r;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            const int rr = (q & 3) + 8 * (q >> 2);
+            if (mb + rr < M) p[(size_t)rr * K] = acc[i][j][q];
+          }
+        }
+      }
+    };
+    if (addend)
+      epi2(std::true_type{});
+    else
+      epi2(std::false_type{});
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bnb_store(bb, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
@@ -668,7 +746,7 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
     for (int j = 0; j < TN; ++j) {
       const int co = n0 + wn * (BN / 2) + 32 * j + r;
       float* p = y + (size_t)mb * K + co;
-      if (yb) {  // bf16 output (unsplit, no addend): feeds a bf16-input BatchNorm
+      if constexpr (EPI == 1) {  // bf16 output (unsplit, no addend): feeds a bf16-input BatchNorm
         __bf16* pb = yb + (size_t)mb * K + co;
         const float kc = kcol[j];
 #pragma unroll
@@ -682,54 +760,8 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
             ss2[j] += d * d;
           }
         }
-      } else if (bs) {  // fp32 dX = a BatchNorm's dY: its backward sums too
-        // every operand load is unconditional (clamped row, y = x when there is
-        // no ReLU) and issued before the first store: a conditional load
-        // compiles to a branch and a vmcnt(0) wait per element
-        const size_t e0 = (size_t)mb * K + co;
-        const uint16_t* xp = reinterpret_cast<const uint16_t*>(bb.x) + e0;
-        const uint16_t* yq = reinterpret_cast<const uint16_t*>(bb.y) + e0;
-        auto tile = [&](auto has_add, auto all_rows) {
-          uint32_t xr[16], yr[16];
-          float av[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int rr = (q & 3) + 8 * (q >> 2);
-            const size_t o = (size_t)((decltype(all_rows)::value || mb + rr < M) ? rr : 0) * K;
-            xr[q] = xp[o];
-            yr[q] = yq[o];
-            if constexpr (decltype(has_add)::value) av[q] = addend[e0 + o];
-          }
-          // sums first, stores after: a load waited on after a store waits
-          // for the store too (vmcnt counts both)
-          const uint32_t one = bb.relu ? 0u : 0x3f80u;  // bf16 1.0: the mask is off
-          float vv[16];
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int rr = (q & 3) + 8 * (q >> 2);
-            float v = acc[i][j][q];
-            if constexpr (decltype(has_add)::value) v += av[q];
-            vv[q] = v;
-            const uint32_t ym = one ? one : yr[q];
-            float d = __uint_as_float(ym << 16) > 0.f ? v : 0.f;
-            if (!(decltype(all_rows)::value || mb + rr < M)) d = 0.f;
-            ss1[j] += d;
-            ss2[j] += d * (__uint_as_float(xr[q] << 16) - bmu[j]) * brs[j];
-          }
-#pragma unroll
-          for (int q = 0; q < 16; ++q) {
-            const int rr = (q & 3) + 8 * (q >> 2);
-            if (decltype(all_rows)::value || mb + rr < M) p[(size_t)rr * K] = vv[q];
-          }
-        };
-        if (addend && full)
-          tile(std::true_type{}, std::true_type{});
-        else if (addend)
-          tile(std::true_type{}, std::false_type{});
-        else if (full)
-          tile(std::false_type{}, std::true_type{});
-        else
-          tile(std::false_type{}, std::false_type{});
+      } else if constexpr (EPI == 2) {
+        // (the whole EPI 2 epilogue runs above, before these per-tile loops)
       } else if (full && addend) {
         // all 16 addend loads first, then the stores (interleaved, hipcc waited
         // vmcnt(0) per element: 16 serial round trips)
@@ -758,11 +790,6 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       stats_store(cs, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
-  }
-  if (bs) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-      bnb_store(bb, s.K, n0 + wn * (BN / 2) + 32 * j + r, (bid % mt) * 2 + wm, h, ss1[j], ss2[j]);
   }
 }
 
@@ -1486,10 +1513,14 @@ static void launch3(const ConvShape& s, const __bf16* x, const __bf16* wt, float
   const dim3 grid(cdiv(M, p.bm) * (s.K / 64), p.z);
   const float* add = p.z > 1 ? nullptr : addend;
   __bf16* ob = p.z > 1 ? nullptr : yb;
-  if (p.bm == 128)
-    conv3_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs, bb);
-  else
-    conv3_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs, bb);
+  const int epi = ob ? 1 : (bb.part ? 2 : 0);
+#define C3(BM_, E_) conv3_kernel<BM_, 64, 4, E_><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add, ob, cs, bb)
+  if (p.bm == 128) {
+    if (epi == 1) C3(128, 1); else if (epi == 2) C3(128, 2); else C3(128, 0);
+  } else {
+    if (epi == 1) C3(64, 1); else if (epi == 2) C3(64, 2); else C3(64, 0);
+  }
+#undef C3
   if (p.z > 1) slab_reduce(slabs, p.z, M * s.K / 4, y, st, addend, yb, stats, s.K, bstats);
 }
 

