@@ -1279,6 +1279,14 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   const int tr = 2 * pg + t / 7, tc = t % 7;
   const bool own = t < 14 && tr < 7;
   int q1[4] = {0, 0, 0, 0};
+  // the ReLU1 mask operands, loaded before the barrier (a load issued after
+  // the dA1 stores below would wait for them: vmcnt counts both)
+  float a1v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (own) {
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+      a1v[o] = a1[((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci];
+  }
   if (do_c1) {
     const long long off = batch_offset_dev(c1.step, c1.n_local, batch);
     const float* x = c1.data + (off + n) * 784;
@@ -1304,7 +1312,7 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
       for (int w = 0; w < 4; ++w) sum += R[rix(w, o, q, j) + l];
       const size_t oi =
           ((size_t)(n * 14 + 2 * tr + (o >> 1)) * 14 + 2 * tc + (o & 1)) * 32 + ci;
-      g1[o] = a1[oi] > 0.f ? sum : 0.f;
+      g1[o] = a1v[o] > 0.f ? sum : 0.f;
       da1m[oi] = g1[o];
     }
   }
