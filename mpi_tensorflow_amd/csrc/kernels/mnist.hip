@@ -245,6 +245,10 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
   const long long off = batch_offset_dev(step_ptr, n_local, batch);
   const uint32_t key = dropout_key(seed, rank, (uint32_t)step, 0u);
   const float scale = 1.f / keep_prob;
+  // the label and fc2 bias used after the logit reduction: loaded now, not
+  // as a dependent round trip after the barrier
+  const int label = labels[off + row];
+  const float b4l = lane < NCLS ? b4[lane] : 0.f;
   // issue every slab load up front (one latency round, not 14)
   float ps[2][FC1_SPLITS];
 #pragma unroll
@@ -282,9 +286,8 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
   }
   __syncthreads();
   if (tid < 64) {
-    const int label = labels[off + row];
     float logit = -INFINITY;
-    if (lane < NCLS) logit = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] + b4[lane];
+    if (lane < NCLS) logit = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane] + b4l;
     const float mx = wave_max(logit);
     const float e = lane < NCLS ? __expf(logit - mx) : 0.f;
     const float se = wave_sum(e);
@@ -2218,22 +2221,39 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
     *reinterpret_cast<float4*>(wl + t * 16 + 4 * c4) = wv;
   }
   __syncthreads();
-  if (tid < 32) {
-    const int cl = tid & 15, co = cq * 16 + cl;
-    float g[25], u[36];
-    if (tid < 16) {
+  // the 2 x 36 x 16 transformed values of the block's filters (U and the
+  // rotated Ud), one per thread-iteration over all 256 threads: each is
+  // u[a][b] = sum_kw G[b][kw] (sum_kh G[a][kh] g[kh][kw]) in exactly
+  // wino::filter_tile's operation order (no FMA contraction, zero
+  // coefficients skipped), so it equals a fresh transform bit for bit
+  // (16 threads computing whole tiles left a ~1 us serial tail)
+  for (int it = tid; it < 2 * 36 * 16; it += 256) {
+#pragma clang fp contract(off)
+    const int rot = it >= 36 * 16, rem = it - rot * 36 * 16;
+    const int p = rem >> 4, cl = rem & 15, co = cq * 16 + cl;
+    const int ra = p / 6, rb = p - 6 * ra;
+    float t[5];
 #pragma unroll
-      for (int t = 0; t < 25; ++t) g[t] = wl[t * 16 + cl];
-      wino::filter_tile(g, u);
+    for (int kw = 0; kw < 5; ++kw) {
+      float acc = 0.f;
 #pragma unroll
-      for (int p = 0; p < 36; ++p) a.U[wino_u_index(p, ci, co)] = u[p];
-    } else {
-#pragma unroll
-      for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 16 + cl];
-      wino::filter_tile(g, u);
-#pragma unroll
-      for (int p = 0; p < 36; ++p) a.Ud[wino_ud_index(p, ci, co)] = u[p];
+      for (int kh = 0; kh < 5; ++kh) {
+        const float c = wino::kG[ra][kh];
+        const int tap = kh * 5 + kw;
+        if (c != 0.f) acc += c * wl[(rot ? 24 - tap : tap) * 16 + cl];
+      }
+      t[kw] = acc;
     }
+    float u = 0.f;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const float c = wino::kG[rb][kw];
+      if (c != 0.f) u += c * t[kw];
+    }
+    if (rot)
+      a.Ud[wino_ud_index(p, ci, co)] = u;
+    else
+      a.U[wino_u_index(p, ci, co)] = u;
   }
 }
 
