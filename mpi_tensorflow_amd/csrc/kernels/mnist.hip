@@ -2221,39 +2221,22 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
     *reinterpret_cast<float4*>(wl + t * 16 + 4 * c4) = wv;
   }
   __syncthreads();
-  // the 2 x 36 x 16 transformed values of the block's filters (U and the
-  // rotated Ud), one per thread-iteration over all 256 threads: each is
-  // u[a][b] = sum_kw G[b][kw] (sum_kh G[a][kh] g[kh][kw]) in exactly
-  // wino::filter_tile's operation order (no FMA contraction, zero
-  // coefficients skipped), so it equals a fresh transform bit for bit
-  // (16 threads computing whole tiles left a ~1 us serial tail)
-  for (int it = tid; it < 2 * 36 * 16; it += 256) {
-#pragma clang fp contract(off)
-    const int rot = it >= 36 * 16, rem = it - rot * 36 * 16;
-    const int p = rem >> 4, cl = rem & 15, co = cq * 16 + cl;
-    const int ra = p / 6, rb = p - 6 * ra;
-    float t[5];
+  if (tid < 32) {
+    const int cl = tid & 15, co = cq * 16 + cl;
+    float g[25], u[36];
+    if (tid < 16) {
 #pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      float acc = 0.f;
+      for (int t = 0; t < 25; ++t) g[t] = wl[t * 16 + cl];
+      wino::filter_tile(g, u);
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh) {
-        const float c = wino::kG[ra][kh];
-        const int tap = kh * 5 + kw;
-        if (c != 0.f) acc += c * wl[(rot ? 24 - tap : tap) * 16 + cl];
-      }
-      t[kw] = acc;
+      for (int p = 0; p < 36; ++p) a.U[wino_u_index(p, ci, co)] = u[p];
+    } else {
+#pragma unroll
+      for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 16 + cl];
+      wino::filter_tile(g, u);
+#pragma unroll
+      for (int p = 0; p < 36; ++p) a.Ud[wino_ud_index(p, ci, co)] = u[p];
     }
-    float u = 0.f;
-#pragma unroll
-    for (int kw = 0; kw < 5; ++kw) {
-      const float c = wino::kG[rb][kw];
-      if (c != 0.f) u += c * t[kw];
-    }
-    if (rot)
-      a.Ud[wino_ud_index(p, ci, co)] = u;
-    else
-      a.U[wino_u_index(p, ci, co)] = u;
   }
 }
 

@@ -213,17 +213,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const int mt = gw % bm, nt = gw / bm;
     const bf* ap = dh16 + (size_t)(mt * 32 + r) * 16 + 8 * h;
     const bf* bp = w1b + (size_t)(nt * 32 + r) * 16 + 8 * h;
-    const int i = nt * 32 + r;  // (py, px, co) flat
-    // epilogue operands (ReLU2 input, pool2 argmax) loaded before the MFMAs:
-    // loaded inside the store loop, each waited for the previous stores too
-    float a2v[16];
-    int q2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int n = mt * 32 + mfma32_row(k, lane);
-      a2v[k] = (float)a2p[((size_t)(i >> 4) * batch + n) * 16 + (i & 15)];
-      q2[k] = idx2[(size_t)n * FC1_IN + i];
-    }
     kloop<8>(
         FC1_OUT / 16,
         [&](int ks, bfx8& a, bfx8& b) {
@@ -231,14 +220,16 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
           b = ld8(bp + (size_t)ks * FC1_IN * 16);
         },
         c0, c1);
+    const int i = nt * 32 + r;  // (py, px, co) flat
     const int co = i & 63, pp = i >> 6, py = pp / 7, px = pp % 7;
     const size_t cplane = (size_t)(co >> 4) * batch * IMG + (co & 15);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int n = mt * 32 + mfma32_row(k, lane);
       float g = c0[k] + c1[k];
-      if (!(a2v[k] > 0.f)) g = 0.f;  // ReLU2 inactive at the argmax
-      const int q = q2[k];
+      const float a = (float)a2p[((size_t)(i >> 4) * batch + n) * 16 + (i & 15)];
+      if (!(a > 0.f)) g = 0.f;  // ReLU2 inactive at the argmax
+      const int q = idx2[(size_t)n * FC1_IN + i];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
@@ -298,17 +289,6 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restric
   const size_t cplane = (size_t)batch * IMG;
   const bf* ap = dy2p + 2 * kk * cplane + (size_t)n * IMG + ((y + 4) * 18 + x + 4) * 16 + 8 * h;
   const bf* bp = w2b + (2 * kk * 32 + r) * 16 + 8 * h;
-  // the ReLU1 mask operand, loaded before the MFMAs (kk == 0 waves finish)
-  float a1v[16];
-  if (kk == 0) {
-    const bf* a1c = a1p + (size_t)(r >> 4) * cplane + (r & 15);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int mm = mt * 32 + mfma32_row(k, lane);
-      const int nn = mm / 196, pq = mm % 196, yy = pq / 14, xx = pq % 14;
-      a1v[k] = (float)a1c[(size_t)nn * IMG + ((yy + 2) * 18 + xx + 2) * 16];
-    }
-  }
   f32x16 c0 = zero16(), c1 = zero16();
   kloop<5>(
       50,
@@ -324,11 +304,14 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restric
   }
   __syncthreads();
   if (kk == 1 || mt_raw >= mtiles) return;
+  const bf* a1c = a1p + (size_t)(r >> 4) * cplane + (r & 15);
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int mm = mt * 32 + mfma32_row(k, lane);
+    const int nn = mm / 196, pq = mm % 196, yy = pq / 14, xx = pq % 14;
     const float g = c0[k] + c1[k] + red[wave & 1][k][lane];
-    da1m[(size_t)mm * 32 + r] = a1v[k] > 0.f ? g : 0.f;
+    const float a = (float)a1c[(size_t)nn * IMG + ((yy + 2) * 18 + xx + 2) * 16];
+    da1m[(size_t)mm * 32 + r] = a > 0.f ? g : 0.f;
   }
 }
 

@@ -61,10 +61,19 @@ __device__ inline void fc1_small_grads(int blk, const float* hd, const float* dh
         g_b3[j] = v;
     }
   }
-  if (blk == 0 && tid < NCLS) {
-    float v = 0.f;
-    for (int n = 0; n < batch; ++n) v += dlog[n * NCLS + tid];
-    g_b4[tid] = v;
+  if (blk == 0 && tid < 64) {  // db4: rows strided over the wave, all loads in flight
+    float v[NCLS];
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) v[c] = 0.f;
+    for (int n = tid; n < batch; n += 64) {
+#pragma unroll
+      for (int c = 0; c < NCLS; ++c) v[c] += dlog[n * NCLS + c];
+    }
+#pragma unroll
+    for (int c = 0; c < NCLS; ++c) {
+      const float t = wave_sum(v[c]);
+      if (tid == 0) g_b4[c] = t;
+    }
   }
 }
 
