@@ -6,11 +6,13 @@ SGD (/root/reference/mpipy.py:59-66), batch offset (step*B) % (N-B), DP by
 per-step gradient all-reduce of the flat grad buffer.
 
 With cfg.dtype == "bf16" the convolutions run their MFMAs on bf16 operands
-(bf16 copies of activations / output gradients and re-laid bf16 weights,
-csrc/kernels/conv_bf16.hip; fp32 accumulation); the stored activations,
-BatchNorm, the native fp32 linear layers (gops::linear_fwd / linear_bwd),
-gradients and the optimizer
-stay fp32.
+(bf16 copies / twins of activations and output gradients, re-laid bf16
+weights, csrc/kernels/conv_bf16.hip; fp32 accumulation).  A conv whose only
+consumer is a BatchNorm stores its output in bf16 and writes that
+BatchNorm's batch statistics in its epilogue; the dgrad producing a
+BatchNorm's dY writes the BatchNorm's backward sums (ops/functional.py).
+BatchNorm math, the native fp32 linear layers (gops::linear_fwd /
+linear_bwd), gradients and the optimizer stay fp32.
 
 On GPU one training step is: batch gather from the device-resident shard at
 the device step offset -> forward/backward through the native NHWC kernels
