@@ -689,7 +689,6 @@ PYBIND11_MODULE(_C, m) {
            py::arg("comm2") = nullptr)
       .def("set_schedule", &MnistExecutor::set_schedule)
       .def("set_fc_sgd_rounds", &MnistExecutor::set_fc_sgd_rounds)
-      .def("set_fc1_sgd", &MnistExecutor::set_fc1_sgd)
       .def("refresh_shadows", [](MnistExecutor& e, uintptr_t s) { e.refresh_shadows(S(s)); })
       .def_property_readonly("schedule", &MnistExecutor::schedule)
       .def("sharded_ok", &MnistExecutor::sharded_ok)

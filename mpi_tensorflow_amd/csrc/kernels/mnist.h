@@ -19,9 +19,6 @@ struct FcSgdArgs {
   uint16_t* w1b = nullptr;
   uint16_t* w1t = nullptr;
   long long w1 = 0;
-  // fp32 single rank with launch_fc1_bwd_sgd: the fc1 weight (float offset w1)
-  // is already updated, the role streams the rest of the bucket only
-  bool skip_w1 = false;
 };
 // conv1 filter-grad role appended to a conv2 filter-gradient launch (its input
 // dA1m must be final: the conv2 bwd-data launch ran before)
@@ -108,13 +105,6 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                     float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
                     int roles = 7);  // roles: bit 0 dX, bit 1 dW1, bit 2 small grads
                                      // (roles == 1: a dX-only grid, SCHED_FACTORS)
-// single-rank fp32 step: fc1 backward with the fc1 weight's momentum SGD
-// folded in (W1 / its momentum updated in place, dW1 never stored); the FC
-// bias / fc2 grads go to g_b3 / g_w4 / g_b4 for the FC-SGD role (skip_w1)
-void launch_fc1_bwd_sgd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
-                        const float* dlog, int batch, float* w1, float* m1, const float* lr,
-                        float l2, float momentum, float* g_b3, float* g_w4, float* g_b4,
-                        float* dy2, float* dy2t, hipStream_t s);
 // FC weight / bias grads over `rows` gathered rows (rank-major a2 [rows][3136],
 // dh / hd [rows][512], dlog [rows][10]); SCHED_FACTORS
 void launch_fc1_bwd_weights(const float* a2, const float* dh, const float* hd, const float* dlog,

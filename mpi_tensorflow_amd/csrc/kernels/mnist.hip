@@ -535,175 +535,6 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
   }
 }
 
-// ------------------------------ fc1 backward + fc1 SGD, single rank ----
-// The fp32 single-rank step's fc1 backward with the fc1 weight update folded
-// in: block L owns fc1 input features f0 = 16 L .. f0 + 15 (rows of W1):
-//   1. dX[:, f0:f0+16] = dh W1[f0:f0+16, :]^T (K = 512 hidden), ReLU2 mask
-//      and the pool2 backward scatter into dy2 / dy2t (as fc1_bwd_dx);
-//   2. dW1[f0:f0+16, :] = a2[:, f0:f0+16]^T dh (K = batch), and straight
-//      into the momentum SGD of those W1 rows (g + l2 w; m = mu m + g;
-//      w -= lr m), so dW1 never goes through memory.
-// W1 rows f0 .. f0 + 15 are read (phase 1) and written (phase 2) by this block
-// only, a barrier apart: no other block of the launch touches them.  The FC
-// bias / fc2 grads stay the small-grads role blocks (their SGD: the FC-SGD
-// role of the next launch, which skips the fc1 weight).  v_mfma_f32_16x16x4_f32:
-// A lane l = A[row l & 15][k l >> 4], B lane l = B[k l >> 4][col l & 15], C
-// lane l reg i = C[row 4 (l >> 4) + i][col l & 15]; the dX K index of MFMA
-// step j in lane group kq is 16 (j >> 2) + 4 kq + (j & 3), so every A / B
-// operand load is one float4 per four steps.
-constexpr int FC1F_ROWS = 16;  // features per block
-constexpr int FC1F_BLOCKS = FC1_IN / FC1F_ROWS;  // 196
-
-struct Fc1Sgd {
-  float* w;        // W1 [3136][512] (params)
-  float* m;        // its momentum slot
-  const float* lr;
-  float l2, mu;
-};
-
-__device__ __forceinline__ void fc1f_dx(int L, const float* __restrict__ a2,
-                                        const uint8_t* __restrict__ idx2,
-                                        const float* __restrict__ dh,
-                                        const float* __restrict__ w1, int batch,
-                                        float* __restrict__ dy2, float* __restrict__ dy2t) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
-  const int f0 = L * FC1F_ROWS;
-  const float* bp = w1 + (size_t)(f0 + r) * FC1_OUT + 4 * kq;  // B[k][col r] = W1[f0 + r][k]
-  const int fi = f0 + r;  // this lane's C column: (py, px, co) flat feature
-  const int co = fi & 63, pp = fi >> 6, py = pp / 7, px = pp % 7;
-  for (int mt = wave; mt < batch / 16; mt += 4) {
-    const float* ap = dh + (size_t)(mt * 16 + r) * FC1_OUT + 4 * kq;  // A[row r][k] = dh[..][k]
-    // epilogue operands, after the first operand loads (loads return in order)
-    float4 a4[2][4], b4[2][4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a4[0][u] = *reinterpret_cast<const float4*>(ap + 16 * u);
-      b4[0][u] = *reinterpret_cast<const float4*>(bp + 16 * u);
-    }
-    float relu_in[4];
-    int qsel[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = mt * 16 + 4 * kq + i;
-      relu_in[i] = a2[(size_t)n * FC1_IN + fi];
-      qsel[i] = idx2[(size_t)n * FC1_IN + fi];
-    }
-    f32x4 acc[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // 8 chunks of 4 float4 (16 K per lane group): the next chunk's loads are
-    // issued before this chunk's 16 MFMAs (four accumulator chains)
-#pragma unroll
-    for (int ch = 0; ch < 8; ++ch) {
-      float4(&ca)[4] = a4[ch & 1];
-      float4(&cb)[4] = b4[ch & 1];
-      if (ch < 7) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a4[(ch + 1) & 1][u] = *reinterpret_cast<const float4*>(ap + 64 * (ch + 1) + 16 * u);
-          b4[(ch + 1) & 1][u] = *reinterpret_cast<const float4*>(bp + 64 * (ch + 1) + 16 * u);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        acc[0] = mfma16x16x4(ca[u].x, cb[u].x, acc[0]);
-        acc[1] = mfma16x16x4(ca[u].y, cb[u].y, acc[1]);
-        acc[2] = mfma16x16x4(ca[u].z, cb[u].z, acc[2]);
-        acc[3] = mfma16x16x4(ca[u].w, cb[u].w, acc[3]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    const f32x4 g4 = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = mt * 16 + 4 * kq + i;
-      float g = g4[i];
-      if (relu_in[i] <= 0.f) g = 0.f;  // ReLU2 inactive at the argmax
-#pragma unroll
-      for (int dy = 0; dy < 2; ++dy) {
-        const int y = 2 * py + dy, x = 2 * px;
-        const float v0 = (qsel[i] == 2 * dy) ? g : 0.f, v1 = (qsel[i] == 2 * dy + 1) ? g : 0.f;
-        dy2[((n * 14 + y) * 14 + x) * 64 + co] = v0;
-        dy2[((n * 14 + y) * 14 + x + 1) * 64 + co] = v1;
-        *reinterpret_cast<float2*>(dy2t + ((size_t)(n * 64 + co) * 18 + y + 2) * MNIST32_T_LD +
-                                   x + 2) = make_float2(v0, v1);
-      }
-    }
-  }
-}
-
-__device__ __forceinline__ void fc1f_dw_sgd(int L, const float* __restrict__ a2,
-                                            const float* __restrict__ dh, int batch,
-                                            const Fc1Sgd& u) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 15, kq = lane >> 4;
-  const int f0 = L * FC1F_ROWS;
-  const float lr = *u.lr;
-  // A[f][k = n] = a2[n][f0 + f]: lane (r, kq) holds rows n = 4 s + kq, s < batch / 4
-  constexpr int SMAX = 32;  // batch <= 128
-  float av[SMAX];
-#pragma unroll
-  for (int st = 0; st < SMAX; ++st) {
-    const int n = min(4 * st + kq, batch - 1);
-    av[st] = a2[(size_t)n * FC1_IN + f0 + r];
-  }
-  const int ns = batch / 4;
-  // 32 N tiles of 16 hidden units, wave w: tiles w, w + 4, ... as pairs (two chains)
-#pragma unroll 1
-  for (int t = wave; t < FC1_OUT / 16; t += 8) {
-    const int h0 = 16 * t, h1 = 16 * (t + 4);
-    // this pair's weights / momentum (C layout: row f = 4 kq + i, col h = r)
-    float wv[2][4], mv[2][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const size_t e = (size_t)(f0 + 4 * kq + i) * FC1_OUT + r;
-      wv[0][i] = u.w[e + h0];
-      mv[0][i] = u.m[e + h0];
-      wv[1][i] = u.w[e + h1];
-      mv[1][i] = u.m[e + h1];
-    }
-    f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int st = 0; st < SMAX; ++st) {
-      if (st < ns) {
-        const float* bp = dh + (size_t)(4 * st + kq) * FC1_OUT + r;
-        c0 = mfma16x16x4(av[st], bp[h0], c0);
-        c1 = mfma16x16x4(av[st], bp[h1], c1);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const f32x4 c = q ? c1 : c0;
-      const int hb = q ? h1 : h0;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float g = c[i] + u.l2 * wv[q][i];  // L2 on the whole FC bucket
-        const float mm = u.mu * mv[q][i] + g;
-        const float ww = wv[q][i] - lr * mm;
-        const size_t e = (size_t)(f0 + 4 * kq + i) * FC1_OUT + hb + r;
-        u.m[e] = mm;
-        u.w[e] = ww;
-      }
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void fc1_bwd_sgd_kernel(
-    const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
-    const float* __restrict__ hd, const float* __restrict__ dlog, int batch,
-    float* __restrict__ g_b3, float* __restrict__ g_w4, float* __restrict__ g_b4,
-    float* __restrict__ dy2, float* __restrict__ dy2t, const Fc1Sgd u) {
-  __shared__ float smem[4 * (NCLS + 1) * 64];
-  const int L = xcd_remap(blockIdx.x, gridDim.x);
-  if (L >= FC1F_BLOCKS) {
-    fc1_small_grads(L - FC1F_BLOCKS, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
-    return;
-  }
-  fc1f_dx(L, a2, idx2, dh, u.w, batch, dy2, dy2t);
-  __syncthreads();  // every wave is past its W1 reads before any W1 row is rewritten
-  fc1f_dw_sgd(L, a2, dh, batch, u);
-}
-
 // FC weight gradients from GATHERED factors (SCHED_FACTORS): dW1 = A^T DH,
 // dW2 = HD^T DLOG, db1 = sum DH, db2 = sum DLOG over the rows of every rank
 // (rows = N x batch, rank-major; the rank's own slot written in place by its
@@ -1135,6 +966,9 @@ __host__ __device__ constexpr WinoCoef make_wino_coef() {
 }
 __constant__ WinoCoef kWinoCoef = make_wino_coef();
 
+__device__ __forceinline__ f32x4 mfma16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
 
 // conv2 forward + bias + ReLU + 2x2 maxpool (+argmax) by Winograd F(2x2,5x5).
 // Block = (image, pair of pooled rows) as conv2_fwd_v3_kernel: 14 pool
@@ -2192,17 +2026,6 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                                                             roles);
 }
 
-void launch_fc1_bwd_sgd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
-                        const float* dlog, int batch, float* w1, float* m1, const float* lr,
-                        float l2, float momentum, float* g_b3, float* g_w4, float* g_b4,
-                        float* dy2, float* dy2t, hipStream_t s) {
-  if (batch <= 0 || batch % 16 != 0 || batch > 128)
-    throw std::runtime_error("fc1_bwd_sgd: batch % 16 != 0 or > 128");
-  const Fc1Sgd u{w1, m1, lr, l2, momentum};
-  fc1_bwd_sgd_kernel<<<FC1F_BLOCKS + SMALL_BLOCKS, 256, 0, s>>>(a2, idx2, dh, hd, dlog, batch, g_b3,
-                                                                g_w4, g_b4, dy2, dy2t, u);
-}
-
 void launch_fc1_bwd_weights(const float* a2, const float* dh, const float* hd, const float* dlog,
                             int rows, float* g_w3, float* g_b3, float* g_w4, float* g_b4,
                             hipStream_t s) {
@@ -2218,16 +2041,8 @@ FcSgd fc_sgd_args(const FcSgdArgs* a) {
   FcSgd r{};
   if (a == nullptr || a->n == 0) return r;
   if (a->n % 4) throw std::runtime_error("fc_sgd: FC bucket not a multiple of 4 floats");
-  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0, 0};
+  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0};
   const long long per_blk = 256LL * FC_SGD_UNROLL * a->rounds;
-  if (a->skip_w1 && !a->w1b) {
-    if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
-      throw std::runtime_error("fc_sgd: fc1 weight misaligned or outside the FC bucket");
-    r.skip_w1 = 1;
-    r.w1_off4 = a->w1 / 4;
-    r.nblk = (int)((r.n4 - W1_F4 + per_blk - 1) / per_blk);
-    return r;
-  }
   if (a->w1b) {
     if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
       throw std::runtime_error("fc_sgd: fc1 weight misaligned or outside the FC bucket");

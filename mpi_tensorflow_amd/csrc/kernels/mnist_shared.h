@@ -280,7 +280,6 @@ struct FcSgd {
   __bf16* w1b;
   __bf16* w1t;
   long long w1_off4;
-  int skip_w1;  // fc1 weight updated elsewhere (fc1_bwd_sgd_kernel): skip its float4s
 };
 constexpr int FC_SGD_UNROLL = 4;
 constexpr long long W1_F4 = (long long)FC1_IN * FC1_OUT / 4;
@@ -343,12 +342,9 @@ __device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile,
     blk -= SHADOW_W1_BLOCKS;
     nb -= SHADOW_W1_BLOCKS;
     n4 -= W1_F4;  // the rest of the bucket, the fc1 weight's float4s skipped
-  } else if (a.skip_w1) {
-    n4 -= W1_F4;
   }
   const long long stride = (long long)nb * 256;
-  const bool skip = a.w1b || a.skip_w1;
-  auto at = [&](long long f) { return (skip && f >= a.w1_off4) ? f + W1_F4 : f; };
+  auto at = [&](long long f) { return (a.w1b && f >= a.w1_off4) ? f + W1_F4 : f; };
   // U float4s per thread per round, every load of a round in flight together
   for (long long i0 = (long long)blk * 256 + tid; i0 < n4; i0 += stride * FC_SGD_UNROLL) {
     float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];

@@ -43,7 +43,7 @@ MnistExecutor::~MnistExecutor() {
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                                     const mnist::FcSgdArgs* fc_sgd, bool factors,
-                                    bool wino_fresh, bool fc1_sgd) {
+                                    bool wino_fresh) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
     return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, wino_fresh);
@@ -85,19 +85,10 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                               P<float>(p.lr), P<int>(p.correct), s);
   if (factors) HIP_CHECK(hipEventRecord(ev_fac_, s));
   // backward: fc1 dX (+pool2/ReLU2 scatter) | dW1 | fc2 grads, one launch
-  if (fc1_sgd && !factors && !finalize) {
-    // single rank: dW1 goes straight into the fc1 weight's momentum SGD
-    mnist::launch_fc1_bwd_sgd(P<const float>(p.a2), P<const uint8_t>(p.idx2),
-                              P<const float>(p.dh), P<const float>(p.hd), P<const float>(p.dlog),
-                              B, W + p.off_w3, P<float>(p.mom) + p.off_w3, P<const float>(p.lr),
-                              p.l2, p.momentum, G + p.off_b3, G + p.off_w4, G + p.off_b4,
-                              P<float>(p.dy2), P<float>(p.dy2t), s);
-  } else {
-    mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
-                          P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
-                          G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4,
-                          P<float>(p.dy2), P<float>(p.dy2t), s, factors ? 1 : 7);
-  }
+  mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
+                        P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
+                        G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
+                        P<float>(p.dy2t), s, factors ? 1 : 7);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   // conv1 filter grad: Winograd - in the bwd-data blocks' epilogue, from the
   // dA1 values they produce; direct - role blocks of the filter-grad launch
@@ -288,18 +279,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
       fc.w1 = p.off_w3;
     }
     const bool fused = fc_sgd_rounds_ > 0 && p.l2_end == p.bucket1;
-    // fp32: the fc1 weight's SGD inside the fc1 backward (the FC-SGD role
-    // then streams only the rest of the bucket)
-    const bool fc1f = fused && fc1_sgd_ && !p.bf16 && p.batch % 16 == 0 && p.batch <= 128;
-    if (fc1f) {
-      fc.skip_w1 = true;
-      fc.w1 = p.off_w3;
-    }
     // Winograd: the filter transforms come from the previous step's SGD (or
     // refresh_shadows() before the first step of a run) and are rewritten by
     // this step's SGD for the next one
-    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr, false, /*wino_fresh=*/true,
-                    fc1f);
+    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr, false, /*wino_fresh=*/true);
     mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
                                p.bucket1, p.l2_end, (int)p.off_w2, (int)p.off_b2, (int)p.off_w1,
                                (int)p.off_b1, P<const float>(p.part2), conv2_groups(),

@@ -129,8 +129,6 @@ class MnistExecutor {
   // role appended to the conv2 bwd-data launch (sets its block count); 0 runs
   // the FC SGD in the final SGD launch instead
   void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? 0 : r; }
-  // single-rank fp32 step: fold the fc1 weight's SGD into the fc1 backward
-  void set_fc1_sgd(bool on) { fc1_sgd_ = on; }
   // Re-derives every weight copy the step kernels read from the fp32 master
   // weights: the Winograd filter transforms (fp32, wino) and the bf16
   // shadows (bf16 engine).  A single-rank bf16 step writes the fc1 shadows from its SGD and
@@ -150,11 +148,9 @@ class MnistExecutor {
   // wino_fresh: the Winograd filter transforms are already current (the
   // single-rank step writes them from its SGD); otherwise they are derived
   // from the weights by a launch at the start of the step
-  // fc1_sgd (fp32 single rank): fc1 backward with the fc1 weight's SGD folded
-  // in (launch_fc1_bwd_sgd); fc_sgd must then skip the fc1 weight
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
                        const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
-                       bool wino_fresh = false, bool fc1_sgd = false);
+                       bool wino_fresh = false);
   int conv1_blocks() const;
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
@@ -169,7 +165,6 @@ class MnistExecutor {
   void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,
                             const mnist::FcSgdArgs* fc_sgd = nullptr, bool shadows_fresh = false);
   int fc_sgd_rounds_ = 2;
-  bool fc1_sgd_ = true;
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;

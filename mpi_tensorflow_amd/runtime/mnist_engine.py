@@ -24,7 +24,6 @@ body, `/root/reference/mpipy.py:79-85`, + optimizer `:59-66`):
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, Optional
 
 import numpy as np
@@ -285,9 +284,6 @@ class NativeMnistEngine(MnistEngineBase):
             p.fac_ranks = nfac
         self.ptrs = p
         self.exe = C_.MnistExecutor(p)
-        # single-rank fp32 step: the fc1 weight's SGD inside the fc1 backward
-        # (MTA_FC1_SGD=0: the separate FC-SGD role, for A/B)
-        self.exe.set_fc1_sgd(os.environ.get("MTA_FC1_SGD", "1") != "0")
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
         self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
         if self.grad_sync and self._native_comm is None:

@@ -66,6 +66,11 @@ def test_mnist_cnn_loss_wrt_params():
     flat = torch.zeros(lay.total, dtype=torch.float32)
     M.init_params(flat, lay, seed=1)
     views = {k: v.detach().to(D).clone().requires_grad_(True) for k, v in lay.views(flat).items()}
+    # fixed inputs: the directional step eps*d moves ~1e-4 of the conv
+    # pre-activations, so some draws put ReLU kinks inside the +-eps
+    # finite-difference window (a slope change there is an O(1) share of the
+    # difference); this draw has none on the checked directions
+    torch.manual_seed(2)
     x = torch.rand(2, 28, 28, 1, dtype=D) - 0.5
     y = torch.tensor([3, 7])
     mask = torch.rand(2, M.FC1_OUT) < 0.5

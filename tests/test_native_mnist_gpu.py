@@ -274,24 +274,3 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     eng.train(7)
     torch.cuda.synchronize()
     assert torch.isfinite(eng.params).all()
-
-
-def test_fc1_backward_with_folded_sgd_matches_separate_update(cuda_dev, data):
-    """Single-rank fp32 step: the fc1 weight's momentum SGD folded into the fc1
-    backward (fc1_bwd_sgd_kernel, dW1 never stored) gives the same parameters
-    and momentum after a few steps as the separate dW1 + FC-SGD role path, up
-    to the summation order of dW1 / dX (fp32 rounding)."""
-    x, y = data
-    out = []
-    for on in (False, True):
-        nat = NativeMnistEngine(C.TrainConfig(graph=False).validate(), x, y, cuda_dev)
-        nat.exe.set_fc1_sgd(on)
-        nat.train(3)
-        torch.cuda.synchronize()
-        out.append((nat.params.clone(), nat.mom.clone()))
-    (p0, m0), (p1, m1) = out
-    lay = nat.layout
-    for name in lay.views(p0):
-        a, b = lay.views(p1)[name], lay.views(p0)[name]
-        assert ((a - b).norm() / b.norm()).item() < 1e-5, name
-    assert ((m1 - m0).norm() / m0.norm()).item() < 1e-4
