@@ -684,11 +684,12 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int co = n0 + wn * (BN / 2) + 32 * j + r;
-          const size_t e0 = (size_t)mb * K + co;
 #pragma unroll
           for (int q = 0; q < 16; ++q) {
             const int rr = (q & 3) + 8 * (q >> 2);
-            const size_t e = e0 + (size_t)(mb + rr < M ? rr : 0) * K;
+            // rows past M (the last tile, whose 4-row group base mb may itself
+            // be past M) read row M - 1: in bounds, finite, and selected away
+            const size_t e = (size_t)min(mb + rr, M - 1) * K + co;
             xr[i][j][q] = reinterpret_cast<const uint16_t*>(bb.x)[e];
             yr[i][j][q] = reinterpret_cast<const uint16_t*>(bb.y)[e];
             if constexpr (ADD) av[i][j][q] = addend[e];
@@ -708,10 +709,11 @@ __global__ __launch_bounds__(NT) void conv3_kernel(ConvShape s, const __bf16* __
             if constexpr (ADD) v += av[i][j][q];
             acc[i][j][q] = v;
             const uint32_t ym = one ? one : yr[i][j][q];
-            float d = __uint_as_float(ym << 16) > 0.f ? v : 0.f;
-            if (mb + rr >= M) d = 0.f;
+            const bool in = mb + rr < M;
+            const float d = (in && __uint_as_float(ym << 16) > 0.f) ? v : 0.f;
+            const float dx = d * (__uint_as_float(xr[i][j][q] << 16) - bmu[j]) * brs[j];
             ss1[j] += d;
-            ss2[j] += d * (__uint_as_float(xr[i][j][q] << 16) - bmu[j]) * brs[j];
+            ss2[j] += in ? dx : 0.f;
           }
         }
       }

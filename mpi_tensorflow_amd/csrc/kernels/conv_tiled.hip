@@ -17,6 +17,7 @@
 // next tile's global loads in flight during the current tile's MFMAs;
 // XCD-aware block order.
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "ops_generic.h"
@@ -226,7 +227,94 @@ struct FwdLoader {
   }
 };
 
-template <int BM, int BN, int P>
+// Forward over the flattened (kh, kw, ci) reduction axis for channel counts
+// that are not a multiple of 32 (the 3-channel ResNet stem: 147 = 7x7x3, five
+// K tiles, the last zero-padded): each thread gathers 4 consecutive k of its
+// rows as scalars (the (kh, kw, ci) decode once per K tile, the pixel decode
+// once per thread); the weight rows are the HWIO rows kk, float4 along co.
+// Requires K % 4 == 0.
+template <int BM, int BN>
+struct FwdGatherLoader {
+  static constexpr int AR = BM * BK / 4 / NT;
+  static constexpr int BR = BN * BK / 4 / NT;
+  ConvShape s;
+  const float* x;
+  const float* w;
+  int n0, ktot;
+  const float* abase[AR];
+  int iy0[AR], ix0[AR];
+  bool av[AR];
+  float4 ra[AR], rb[BR];
+  bool bv[BR];
+  __device__ FwdGatherLoader(const ConvShape& s_, const float* x_, const float* w_, int m0,
+                             int n0_)
+      : s(s_), x(x_), w(w_), n0(n0_) {
+    ktot = s.R * s.S * s.C;
+    const int tid = threadIdx.x;
+    const int M = s.N * s.OH * s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + 32 * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+      abase[i] = x + (size_t)n * s.H * s.W * s.C;
+      iy0[i] = oy * s.stride - s.pad;
+      ix0[i] = ox * s.stride - s.pad;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) bv[i] = n0 + 4 * (tid % (BN / 4)) < s.K;
+  }
+  __device__ __forceinline__ void load(int kt) {
+    const int tid = threadIdx.x, kb = kt * BK + 4 * (tid & 7);
+    int dy[4], dx[4], ci[4];
+    bool kv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // (kh, kw, ci) of this thread's 4 k
+      const int kk = min(kb + u, ktot - 1);
+      kv[u] = kb + u < ktot;
+      const int tap = kk / s.C;
+      ci[u] = kk - tap * s.C;
+      dy[u] = tap / s.S;
+      dx[u] = tap - dy[u] * s.S;
+    }
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int iy = iy0[i] + dy[u], ix = ix0[i] + dx[u];
+        const bool ok = av[i] && kv[u] && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
+        // clamped pixel: the load is always in bounds, the value selected away
+        const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
+        const float e = abase[i][((size_t)iyc * s.W + ixc) * s.C + ci[u]];
+        v[u] = ok ? e : 0.f;
+      }
+      ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    const float* wb = w + min(n0 + 4 * (tid % (BN / 4)), s.K - 4);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = kt * BK + tid / (BN / 4) + (NT / (BN / 4)) * i;
+      const float4 e = *reinterpret_cast<const float4*>(wb + (size_t)min(k, ktot - 1) * s.K);
+      rb[i] = sel4(bv[i] && k < ktot, e);
+    }
+  }
+  template <int P>
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    const int tid = threadIdx.x, c4 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) Stage<P, BM>::put_k4(As, (tid >> 3) + 32 * i, 4 * c4, ra[i]);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int k = tid / (BN / 4) + (NT / (BN / 4)) * i;
+      Stage<P, BN>::put_r4(Bs, 4 * (tid % (BN / 4)), k, rb[i]);
+    }
+  }
+};
+
+// GATHER: FwdGatherLoader over the flattened reduction axis, else FwdLoader
+template <int BM, int BN, int P, bool GATHER = false>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ bias,
@@ -239,8 +327,10 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
   const int mt = (M + BM - 1) / BM;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
-  const int nk = s.R * s.S * (s.C / BK), kb = blockIdx.y * kps;
-  FwdLoader<BM, BN> ld(s, x, w, m0, n0);
+  const int nk = GATHER ? (s.R * s.S * s.C + BK - 1) / BK : s.R * s.S * (s.C / BK);
+  const int kb = blockIdx.y * kps;
+  using LD = typename std::conditional<GATHER, FwdGatherLoader<BM, BN>, FwdLoader<BM, BN>>::type;
+  LD ld(s, x, w, m0, n0);
   f32x16 acc[G::TM][G::TN];
   mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
   y += (size_t)blockIdx.y * M * s.K;
@@ -725,6 +815,11 @@ static inline Tile pick(long long M, int N) {
 }  // namespace tiled
 
 bool conv_fwd_tiled_ok(const ConvShape& s) { return s.C % 32 == 0 && s.K % 4 == 0; }
+// the gather-loader forward: thin inputs with a reduction axis of >= 2 K tiles
+// (the ResNet stem); smaller ones stay on the direct / gather engines
+bool conv_fwd_tiled_gather_ok(const ConvShape& s) {
+  return s.C % 32 != 0 && s.K % 4 == 0 && s.R * s.S * s.C >= 64;
+}
 bool conv_bwd_data_tiled_ok(const ConvShape& s) { return s.K % 32 == 0 && s.C % 4 == 0; }
 bool conv_bwd_filter_tiled_ok(const ConvShape& s) { return s.K % 4 == 0; }  // C % 4: vector path
 
@@ -748,7 +843,7 @@ static inline int ksplit(long long blocks, int nk) {
 static inline void fwd_plan(const ConvShape& s, bool epilogue, Tile& t, int& z, int& kps) {
   const long long M = (long long)s.N * s.OH * s.OW;
   t = pick(M, s.K);
-  const int nk = s.R * s.S * (s.C / BK);
+  const int nk = s.C % BK == 0 ? s.R * s.S * (s.C / BK) : cdiv(s.R * s.S * s.C, BK);
   z = epilogue ? 1 : ksplit((long long)cdiv(M, tile_m(t)) * cdiv(s.K, tile_n(t)), nk);
   kps = cdiv(nk, z);
 }
@@ -800,7 +895,14 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
   if (z > 1 && !ws) throw std::runtime_error("conv_fwd_tiled: split-K needs a workspace");
   float* out = z > 1 ? ws : y;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), z)
-  TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+  if (s.C % BK != 0) {  // gather loader (fp32 operands only)
+    if (bf16) throw std::runtime_error("conv_fwd_tiled: the gather forward is fp32");
+#define F32G F32, true
+    TILED_DISPATCH_P(F32G, t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+#undef F32G
+  } else {
+    TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+  }
 #undef GRID
   if (z > 1) slab_sum(ws, z, M * s.K, y, st);
 }

@@ -101,6 +101,7 @@ void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, f
 // LDS-tiled conv family (conv_tiled.hip), used by the launchers above for the
 // shapes it supports
 bool conv_fwd_tiled_ok(const ConvShape& s);
+bool conv_fwd_tiled_gather_ok(const ConvShape& s);  // fp32 tiled forward, flattened (kh, kw, ci)
 bool conv_bwd_data_tiled_ok(const ConvShape& s);
 bool conv_bwd_filter_tiled_ok(const ConvShape& s);
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,

@@ -912,6 +912,10 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
     }
     return;
   }
+  // thin-input convs too big for the direct kernel (the ResNet stem): fp32
+  // MFMA tiles over the flattened (kh, kw, ci) axis
+  if (!bf16 && conv_fwd_tiled_gather_ok(s))
+    return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, false);
   const int M = s.N * s.OH * s.OW;
   const int blocks = ((M + CFG_F::BM - 1) / CFG_F::BM) * ((s.K + CFG_F::BN - 1) / CFG_F::BN);
   conv_fwd_kernel<<<blocks, 256, 0, st>>>(s, x, w, bias, y, relu ? 1 : 0);
@@ -989,7 +993,8 @@ long long conv_ws_floats(const ConvShape& s, bool fwd_epilogue) {
     gather_data_plan(s, z, kchunk);
     if (z > 1) n = std::max(n, (long long)z * s.N * s.H * s.W * s.C);
   }
-  if (conv_fwd_tiled_ok(s)) n = std::max(n, conv_fwd_tiled_ws_floats(s, fwd_epilogue));
+  if (conv_fwd_tiled_ok(s) || conv_fwd_tiled_gather_ok(s))
+    n = std::max(n, conv_fwd_tiled_ws_floats(s, fwd_epilogue));
   if (conv_bwd_data_tiled_ok(s)) n = std::max(n, conv_bwd_data_tiled_ws_floats(s));
   return std::max(n, conv_bf16_ws_floats(s, fwd_epilogue));
 }

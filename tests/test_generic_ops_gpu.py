@@ -27,6 +27,10 @@ def _param(t):
     (4, 9, 7, 5, 6, 3, 1, 1, True, True),
     (4, 12, 12, 8, 16, 3, 2, 1, False, False),
     (2, 16, 16, 3, 64, 7, 2, 3, False, False),
+    # fp32 gather-loader tiled forward (flattened (kh, kw, ci) K tiles, last one
+    # partial): the stem with bias + ReLU and an M that is not a tile multiple
+    (3, 20, 18, 3, 64, 7, 2, 3, True, True),
+    (2, 15, 15, 5, 72, 5, 1, 2, False, False),   # K > 64: not a direct-kernel shape
     (3, 8, 8, 16, 32, 1, 2, 0, False, False),
     (5, 1, 1, 40, 70, 1, 1, 0, True, True),  # linear as a 1x1 conv
     # direct VALU forward (thin layers): the LeNet-5 conv shapes
@@ -618,6 +622,8 @@ def test_dgrad_epilogue_bn_backward_statistics(cuda_dev, N, H, Cin, K, stride, r
     torch.cuda.synchronize()
     (dx0, gg0, gb0, gw0), (dx1, gg1, gb1, gw1) = out
     assert torch.equal(gw0, gw1)  # the filter gradient does not depend on the route
+    nan = [bool(torch.isnan(t).any()) for t in (gg0, gb0, dx0, gg1, gb1, dx1)]
+    assert not any(nan), f"NaN in (gg0, gb0, dx0, gg1, gb1, dx1): {nan}"
     assert _rel(gb1, gb0) < 1e-5 and _rel(gg1, gg0) < 1e-4
     assert _rel(dx1, dx0) < 4e-3  # dX is bf16: a few rounding flips
 
