@@ -16,6 +16,8 @@
 // TMxTN 32x32 MFMA tiles; double-buffered LDS, one barrier per K tile, the
 // next tile's global loads in flight during the current tile's MFMAs;
 // XCD-aware block order.
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
@@ -792,8 +794,24 @@ static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b)
 
 // Block tile from the GEMM's M and N: 128-wide where the dimension allows it.
 enum Tile { T128x128, T128x64, T64x128, T64x64 };
-static inline Tile pick(long long M, int N) {
-  const bool bm = M >= 128 * 256, bn = N > 64;  // wide M tiles only with >= 256 blocks of them
+// 128-row tiles only with >= 256 blocks of them (bf16).  fp32 never: on the
+// ResNet-18 56x56 layers (M = 100352) 64-row tiles measured 116.4 -> 103.8 us
+// forward and 145.5 -> 129.0 us dgrad (the 128x64 grid, 784 blocks, overran
+// the 768 resident slots by 16).  MTA_TILED_M128 overrides both (experiments).
+static inline long long m128_min(bool bf16) {
+  static const long long v = [] {
+    const char* e = getenv("MTA_TILED_M128");
+    return e ? atoll(e) : -1LL;
+  }();
+  if (v >= 0) return v;
+  return bf16 ? 128LL * 256 : (1LL << 62);
+}
+static inline Tile pick(long long M, int N, bool bf16) {
+  static const bool n64 = [] {  // MTA_TILED_N64=1: fp32 64-column tiles (experiments)
+    const char* e = getenv("MTA_TILED_N64");
+    return e && e[0] == '1';
+  }();
+  const bool bm = M >= m128_min(bf16), bn = N > 64 && !(n64 && !bf16);
   if (bn) return bm ? T128x128 : T64x128;
   return bm ? T128x64 : T64x64;
 }
@@ -840,17 +858,18 @@ static inline int ksplit(long long blocks, int nk) {
   const int kps = cdiv(nk, z);
   return cdiv(nk, kps);
 }
-static inline void fwd_plan(const ConvShape& s, bool epilogue, Tile& t, int& z, int& kps) {
+static inline void fwd_plan(const ConvShape& s, bool epilogue, bool bf16, Tile& t, int& z,
+                            int& kps) {
   const long long M = (long long)s.N * s.OH * s.OW;
-  t = pick(M, s.K);
+  t = pick(M, s.K, bf16);
   const int nk = s.C % BK == 0 ? s.R * s.S * (s.C / BK) : cdiv(s.R * s.S * s.C, BK);
   z = epilogue ? 1 : ksplit((long long)cdiv(M, tile_m(t)) * cdiv(s.K, tile_n(t)), nk);
   kps = cdiv(nk, z);
 }
-static inline void data_plan(const ConvShape& s, Tile& t, int& z, int& kps) {
+static inline void data_plan(const ConvShape& s, bool bf16, Tile& t, int& z, int& kps) {
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
-  t = pick(Mph * sd * sd, s.C);
+  t = pick(Mph * sd * sd, s.C, bf16);
   const int ntap = cdiv(s.R, sd) * cdiv(s.S, sd);  // taps of the richest phase
   const int nk = ntap * (s.K / BK);
   z = ksplit((long long)cdiv(Mph, tile_m(t)) * cdiv(s.C, tile_n(t)) * sd * sd, nk);
@@ -871,18 +890,27 @@ static inline void slab_sum(const float* part, int z, long long n, float* out, h
 }
 }  // namespace tiled
 
+// workspace for either operand precision (the plans differ in tile shape)
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
-  tiled::Tile t;
-  int z, kps;
-  tiled::fwd_plan(s, epilogue, t, z, kps);
-  return z > 1 ? (long long)z * s.N * s.OH * s.OW * s.K : 0;
+  long long n = 0;
+  for (const bool b : {false, true}) {
+    tiled::Tile t;
+    int z, kps;
+    tiled::fwd_plan(s, epilogue, b, t, z, kps);
+    if (z > 1) n = std::max(n, (long long)z * s.N * s.OH * s.OW * s.K);
+  }
+  return n;
 }
 
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
-  tiled::Tile t;
-  int z, kps;
-  tiled::data_plan(s, t, z, kps);
-  return z > 1 ? (long long)z * s.N * s.H * s.W * s.C : 0;
+  long long n = 0;
+  for (const bool b : {false, true}) {
+    tiled::Tile t;
+    int z, kps;
+    tiled::data_plan(s, b, t, z, kps);
+    if (z > 1) n = std::max(n, (long long)z * s.N * s.H * s.W * s.C);
+  }
+  return n;
 }
 
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
@@ -891,7 +919,7 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
   const long long M = (long long)s.N * s.OH * s.OW;
   Tile t;
   int z, kps;
-  fwd_plan(s, bias != nullptr || relu, t, z, kps);
+  fwd_plan(s, bias != nullptr || relu, bf16, t, z, kps);
   if (z > 1 && !ws) throw std::runtime_error("conv_fwd_tiled: split-K needs a workspace");
   float* out = z > 1 ? ws : y;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), z)
@@ -914,7 +942,7 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
   Tile t;
   int z, kps;
-  data_plan(s, t, z, kps);
+  data_plan(s, bf16, t, z, kps);
   if (z > 1 && !ws) throw std::runtime_error("conv_bwd_data_tiled: split-K needs a workspace");
   float* out = z > 1 ? ws : dx;
   // phases no tap reaches (odd pixels of a 1x1 stride-2 conv) run zero K
@@ -932,7 +960,15 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
 
 namespace tiled {
 static inline Tile filter_tile(const ConvShape& s) {  // ci x co tiles
-  const bool bm = s.C >= 128, bn = s.K > 64;
+  // 64-wide ci tiles: ResNet-18 fp32 filter gradients 136 -> 122 (28x28), 112 -> 103
+  // (14x14), 116 -> 102 us (7x7), step 6.96 -> 6.78 ms; twice the tiles, so half
+  // the split-K slices (the bf16 models take the conv_bf16 filter kernels).
+  // MTA_TILED_WG64=0: 128-wide ci tiles from C >= 128 (the old plan)
+  static const bool wg64 = [] {
+    const char* e = getenv("MTA_TILED_WG64");
+    return !(e && e[0] == '0');
+  }();
+  const bool bm = s.C >= 128 && !wg64, bn = s.K > 64;
   return bm ? (bn ? T128x128 : T128x64) : (bn ? T64x128 : T64x64);
 }
 static inline int filter_blocks_per_split(const ConvShape& s) {
