@@ -806,12 +806,12 @@ static inline long long m128_min(bool bf16) {
   if (v >= 0) return v;
   return bf16 ? 128LL * 256 : (1LL << 62);
 }
-static inline Tile pick(long long M, int N, bool bf16) {
-  static const bool n64 = [] {  // MTA_TILED_N64=1: fp32 64-column tiles (experiments)
-    const char* e = getenv("MTA_TILED_N64");
-    return e && e[0] == '1';
-  }();
-  const bool bm = M >= m128_min(bf16), bn = N > 64 && !(n64 && !bf16);
+// narrow: 64-column tiles even for N > 64 (fp32 stride-2 dgrad and 1x1 stride-2
+// forward of ResNet-18: 99.0 -> 84.0 / 33.3 -> 20.0 us dgrad at 128 channels,
+// 98.0 -> 92.4 / 35.9 -> 29.1 at 256, 1x1 forward 14.4 -> 12.3 / 20.8 -> 17.0;
+// the stride-1 3x3 layers were slower with them, 95.7 -> 103.2 us forward)
+static inline Tile pick(long long M, int N, bool bf16, bool narrow = false) {
+  const bool bm = M >= m128_min(bf16), bn = N > 64 && !(narrow && !bf16);
   if (bn) return bm ? T128x128 : T64x128;
   return bm ? T128x64 : T64x64;
 }
@@ -861,7 +861,7 @@ static inline int ksplit(long long blocks, int nk) {
 static inline void fwd_plan(const ConvShape& s, bool epilogue, bool bf16, Tile& t, int& z,
                             int& kps) {
   const long long M = (long long)s.N * s.OH * s.OW;
-  t = pick(M, s.K, bf16);
+  t = pick(M, s.K, bf16, s.R == 1 && s.S == 1 && s.stride == 2);
   const int nk = s.C % BK == 0 ? s.R * s.S * (s.C / BK) : cdiv(s.R * s.S * s.C, BK);
   z = epilogue ? 1 : ksplit((long long)cdiv(M, tile_m(t)) * cdiv(s.K, tile_n(t)), nk);
   kps = cdiv(nk, z);
@@ -869,7 +869,7 @@ static inline void fwd_plan(const ConvShape& s, bool epilogue, bool bf16, Tile& 
 static inline void data_plan(const ConvShape& s, bool bf16, Tile& t, int& z, int& kps) {
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
-  t = pick(Mph * sd * sd, s.C, bf16);
+  t = pick(Mph * sd * sd, s.C, bf16, sd == 2);
   const int ntap = cdiv(s.R, sd) * cdiv(s.S, sd);  // taps of the richest phase
   const int nk = ntap * (s.K / BK);
   z = ksplit((long long)cdiv(Mph, tile_m(t)) * cdiv(s.C, tile_n(t)) * sd * sd, nk);
