@@ -845,13 +845,27 @@ namespace tiled {
 static inline int tile_m(Tile t) { return (t == T128x128 || t == T128x64) ? 128 : 64; }
 static inline int tile_n(Tile t) { return (t == T128x128 || t == T64x128) ? 128 : 64; }
 
+// split targets (blocks to aim for), overridable for plan experiments:
+// MTA_TILED_KSPLIT (forward / dgrad, default 1024), MTA_TILED_WGSPLIT (filter, 2048)
+static inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static inline int ksplit_target() {
+  static const int v = env_int("MTA_TILED_KSPLIT", 1024);
+  return v;
+}
+static inline int wgsplit_target() {
+  static const int v = env_int("MTA_TILED_WGSPLIT", 2048);
+  return v;
+}
 // split-K factor for a GEMM with `blocks` output tiles of nk K tiles each:
 // deep layers (few tiles, long K) get enough blocks to fill 256 CUs twice
 static inline int ksplit(long long blocks, int nk) {
   // measured (ResNet-18, B=32): filling the chip beats the extra slab traffic
   // (a 256-block / 8-slice cap cost +15 % step time in fp32 and bf16)
   if (blocks >= 512 || nk < 8) return 1;
-  int z = cdiv(1024, blocks);
+  int z = cdiv(ksplit_target(), blocks);
   if (z > nk / 4) z = nk / 4;
   if (z > 16) z = 16;
   if (z < 1) z = 1;
@@ -986,10 +1000,13 @@ int conv_filter_tiled_splits(const ConvShape& s) {
   const int tiles = vec ? filter_blocks_per_split(s) : cdiv(s.R * s.S * s.C, 64) * cdiv(s.K, 64);
   // aim for ~2048 blocks (measured: fewer, larger slices - 512 or 1024 blocks -
   // cost 4-20 % ResNet-18 step time despite the smaller slab traffic)
-  int z = cdiv(2048, tiles);
+  int z = cdiv(wgsplit_target(), tiles);
   if (z < 1) z = 1;
   if (z > ktiles) z = ktiles;
-  if (z > (vec ? 64 : 128)) z = vec ? 64 : 128;
+  // gather-path slice cap: the ResNet stem's filter gradient (3 tiles of 64 x 64,
+  // 12544 K tiles) went 271 -> 197 us from 128 to 256 slices (512: 196, 1024: 198)
+  static const int gcap = env_int("MTA_TILED_GCAP", 256);
+  if (z > (vec ? 64 : gcap)) z = vec ? 64 : gcap;
   const int kchunk = cdiv(ktiles, z);
   return cdiv(ktiles, kchunk);  // splits actually launched
 }
