@@ -317,6 +317,10 @@ PYBIND11_MODULE(_C, m) {
       }))
       .def_readonly("OH", &gops::PoolShape::OH).def_readonly("OW", &gops::PoolShape::OW);
   g.def("conv_bf16_ok", &gops::conv_fwd_bf16_ok);
+  // the fp32 tiled forward (its epilogue can write BatchNorm statistics)
+  g.def("conv_fwd_tiled_ok", [](const gops::ConvShape& s) {
+    return gops::conv_fwd_tiled_ok(s) || gops::conv_fwd_tiled_gather_ok(s);
+  });
   g.def("conv_bwd_data_join_ok", &gops::conv_bwd_data_join_ok);
   g.def("im2col_bf16", [](const gops::ConvShape& s, uintptr_t x, int kp, uintptr_t col,
                           uintptr_t st) {
@@ -332,7 +336,8 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   }, py::arg("s1"), py::arg("si"), py::arg("x"), py::arg("wtb"), py::arg("yb"), py::arg("st"),
      py::arg("stats_part") = 0, py::arg("stats_rows") = 0, py::arg("stats_shift") = 0);
-  g.def("conv_fwd_stats_rows", &gops::conv_fwd_stats_rows);
+  g.def("conv_fwd_stats_rows", &gops::conv_fwd_stats_rows, py::arg("shape"),
+        py::arg("bf16") = true);
   g.def("conv_fwd_stem_stats_rows", &gops::conv_fwd_stem_stats_rows);
   g.def("conv_bwd_filter_stem_bf16",
         [](const gops::ConvShape& s1, const gops::ConvShape& si, uintptr_t x, uintptr_t dyb,

@@ -2003,8 +2003,13 @@ void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t
   cbf::wcvt_batch_kernel<<<(int)nblocks, 256, 0, st>>>(jobs, njobs);
 }
 
-int conv_fwd_stats_rows(const ConvShape& s) {
+int conv_fwd_stats_rows(const ConvShape& s, bool bf16) {
   using namespace cbf;
+  if (!bf16) {
+    if (!conv_fwd_tiled_ok(s) && !conv_fwd_tiled_gather_ok(s))
+      throw std::runtime_error("conv_fwd_stats_rows: not a tiled-family conv");
+    return conv_fwd_tiled_stats_rows(s, false);
+  }
   if (!conv_fwd_bf16_ok(s)) throw std::runtime_error("conv_fwd_stats_rows: not a bf16-family conv");
   return conv3_ok(s) ? stats_rows3(s) : stats_rows(s, false);
 }

@@ -316,11 +316,16 @@ struct FwdGatherLoader {
 };
 
 // GATHER: FwdGatherLoader over the flattened reduction axis, else FwdLoader
+// cs (unsplit launches): the consuming BatchNorm's statistics of the stored
+// values, shifted by cs.shift, in the [2][K / 64][P][64] partial-row table of
+// the bf16 family (row (m tile, wm) per wave, P = 2 x m tiles); the two
+// half-waves combine their rows and lanes h == 0 store 32 contiguous floats
 template <int BM, int BN, int P, bool GATHER = false>
 __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __restrict__ x,
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ bias,
-                                                 float* __restrict__ y, int relu, int kps) {
+                                                 float* __restrict__ y, int relu, int kps,
+                                                 const ConvStats cs) {
   // split-K (gridDim.y > 1, no bias / ReLU): slice z of kps K tiles writes a
   // raw slab y + z * M * K, summed by slab_sum4 afterwards
   using G = Geo<BM, BN, P>;
@@ -337,21 +342,36 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
   mainloop<BM, BN, P>(ld, smem, kb, min(kps, nk - kb), acc);
   y += (size_t)blockIdx.y * M * s.K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave & 1, wn = wave >> 1;
+  const bool st = cs.part != nullptr;
 #pragma unroll
   for (int j = 0; j < G::TN; ++j) {
     const int co = n0 + wn * (BN / 2) + 32 * j + (lane & 31);
-    if (co >= s.K) continue;
-    const float b = bias ? bias[co] : 0.f;
+    const bool cok = co < s.K;
+    const float b = (bias && cok) ? bias[co] : 0.f;
+    const float kc = (st && cok) ? cs.shift[co] : 0.f;
+    float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < G::TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(r, lane);
-        if (m >= M) continue;
+        if (m >= M || !cok) continue;
         float v = acc[i][j][r] + b;
         if (relu) v = fmaxf(v, 0.f);
         y[(size_t)m * s.K + co] = v;
+        const float d = v - kc;
+        s1 += d;
+        s2 += d * d;
       }
+    if (st) {  // both half-waves hold the same column
+      s1 += __shfl_xor(s1, 32, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if ((lane >> 5) == 0 && cok) {
+        const size_t e = ((size_t)(co >> 6) * cs.P + (bid % mt) * 2 + wm) * 64 + (co & 63);
+        cs.part[e] = s1;
+        cs.part[(size_t)s.K * cs.P + e] = s2;
+      }
+    }
   }
 }
 
@@ -789,6 +809,49 @@ __global__ __launch_bounds__(256) void slab_sum4_kernel(const float4* __restrict
   }
 }
 
+// slab_sum4 for a split-K forward whose output feeds a BatchNorm: also the
+// shifted statistics of the summed values, one partial row per block in the
+// [2][C / 64][P][64] table (P = grid; 256 % (C / 4) == 0, so every thread
+// keeps one channel quad; threads sharing a quad are combined in a fixed order)
+__global__ __launch_bounds__(256) void slab_sum4_stats_kernel(const float4* __restrict__ part,
+                                                              int nz, long long n4,
+                                                              float4* __restrict__ out,
+                                                              const ConvStats cs, int C) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int cq = C >> 2, tid = threadIdx.x;
+  const float4 kc = *reinterpret_cast<const float4*>(cs.shift + 4 * (tid % cq));
+  float4 t1 = make_float4(0.f, 0.f, 0.f, 0.f), t2 = t1;
+  for (long long i = (long long)blockIdx.x * blockDim.x + tid; i < n4; i += stride) {
+    float4 a = part[i];
+    for (int z = 1; z < nz; ++z) {
+      const float4 b = part[z * n4 + i];
+      a.x += b.x;
+      a.y += b.y;
+      a.z += b.z;
+      a.w += b.w;
+    }
+    out[i] = a;
+    const float dx = a.x - kc.x, dy = a.y - kc.y, dz = a.z - kc.z, dw = a.w - kc.w;
+    t1.x += dx; t1.y += dy; t1.z += dz; t1.w += dw;
+    t2.x += dx * dx; t2.y += dy * dy; t2.z += dz * dz; t2.w += dw * dw;
+  }
+  __shared__ float4 red[2][256];
+  red[0][tid] = t1;
+  red[1][tid] = t2;
+  __syncthreads();
+  if (tid < cq) {
+    float4 a = red[0][tid], b = red[1][tid];
+    for (int t = tid + cq; t < 256; t += cq) {
+      a.x += red[0][t].x; a.y += red[0][t].y; a.z += red[0][t].z; a.w += red[0][t].w;
+      b.x += red[1][t].x; b.y += red[1][t].y; b.z += red[1][t].z; b.w += red[1][t].w;
+    }
+    const int co = 4 * tid;
+    const size_t e = ((size_t)(co >> 6) * cs.P + blockIdx.x) * 64 + (co & 63);
+    *reinterpret_cast<float4*>(cs.part + e) = a;
+    *reinterpret_cast<float4*>(cs.part + (size_t)C * cs.P + e) = b;
+  }
+}
+
 // ------------------------------------------------------------ dispatch ----
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
@@ -889,10 +952,13 @@ static inline void data_plan(const ConvShape& s, bool bf16, Tile& t, int& z, int
   z = ksplit((long long)cdiv(Mph, tile_m(t)) * cdiv(s.C, tile_n(t)) * sd * sd, nk);
   kps = cdiv(nk, z);
 }
+static inline long long slab_grid(long long n) {
+  const long long b = (n / 4 + 255) / 256;
+  return b > 4096 ? 4096 : b;
+}
 static inline void slab_sum(const float* part, int z, long long n, float* out, hipStream_t st,
                             const float* addend = nullptr) {
-  long long b = (n / 4 + 255) / 256;
-  if (b > 4096) b = 4096;
+  const long long b = slab_grid(n);
   if (b < 64 && z >= 16 && !addend) {  // deep, narrow stack: spread the slices over the block
     slab_sum4_deep_kernel<<<cdiv(n / 4, 64), 256, 0, st>>>(reinterpret_cast<const float4*>(part),
                                                             z, n / 4, reinterpret_cast<float4*>(out));
@@ -927,26 +993,49 @@ long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
   return n;
 }
 
+int conv_fwd_tiled_stats_rows(const ConvShape& s, bool bf16) {
+  using namespace tiled;
+  const long long M = (long long)s.N * s.OH * s.OW;
+  Tile t;
+  int z, kps;
+  fwd_plan(s, false, bf16, t, z, kps);
+  return z > 1 ? (int)slab_grid(M * s.K) : cdiv(M, tile_m(t)) * 2;
+}
+
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                    bool relu, float* ws, hipStream_t st, bool bf16) {
+                    bool relu, float* ws, hipStream_t st, bool bf16, const ConvStats* stats) {
   using namespace tiled;
   const long long M = (long long)s.N * s.OH * s.OW;
   Tile t;
   int z, kps;
   fwd_plan(s, bias != nullptr || relu, bf16, t, z, kps);
   if (z > 1 && !ws) throw std::runtime_error("conv_fwd_tiled: split-K needs a workspace");
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (bias || relu || s.K % 64 || 256 % (s.K / 4) ||
+        stats->P != conv_fwd_tiled_stats_rows(s, bf16))
+      throw std::runtime_error("conv_fwd_tiled: BatchNorm statistics layout mismatch");
+    if (z == 1) cs = *stats;
+  }
   float* out = z > 1 ? ws : y;
 #define GRID(BM_, BN_) dim3(cdiv(M, BM_) * cdiv(s.K, BN_), z)
   if (s.C % BK != 0) {  // gather loader (fp32 operands only)
     if (bf16) throw std::runtime_error("conv_fwd_tiled: the gather forward is fp32");
 #define F32G F32, true
-    TILED_DISPATCH_P(F32G, t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+    TILED_DISPATCH_P(F32G, t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs)
 #undef F32G
   } else {
-    TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps)
+    TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs)
   }
 #undef GRID
-  if (z > 1) slab_sum(ws, z, M * s.K, y, st);
+  if (z > 1) {
+    if (stats && stats->part)
+      slab_sum4_stats_kernel<<<(int)slab_grid(M * s.K), 256, 0, st>>>(
+          reinterpret_cast<const float4*>(ws), z, M * s.K / 4, reinterpret_cast<float4*>(y),
+          *stats, s.K);
+    else
+      slab_sum(ws, z, M * s.K, y, st);
+  }
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,

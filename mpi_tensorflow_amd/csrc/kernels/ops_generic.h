@@ -50,7 +50,8 @@ struct BnBwdStats {
   int relu = 0;
 };
 int conv_bwd_data_stats_rows(const ConvShape& s);
-int conv_fwd_stats_rows(const ConvShape& s);  // bf16 family, bf16 output, no bias / ReLU
+// bf16 = true: bf16 family, bf16 output; false: the fp32 tiled forward (no bias / ReLU)
+int conv_fwd_stats_rows(const ConvShape& s, bool bf16 = true);
 int conv_fwd_stem_stats_rows(const ConvShape& s1);
 void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
               bool relu, float* ws, hipStream_t st, bool bf16 = false, const void* xb = nullptr,
@@ -105,7 +106,10 @@ bool conv_fwd_tiled_gather_ok(const ConvShape& s);  // fp32 tiled forward, flatt
 bool conv_bwd_data_tiled_ok(const ConvShape& s);
 bool conv_bwd_filter_tiled_ok(const ConvShape& s);
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
-                    bool relu, float* ws, hipStream_t st, bool bf16);
+                    bool relu, float* ws, hipStream_t st, bool bf16,
+                    const ConvStats* stats = nullptr);
+// partial rows of the BatchNorm statistics the tiled forward writes (fp32 route)
+int conv_fwd_tiled_stats_rows(const ConvShape& s, bool bf16);
 // dy may be null when dyb (bf16 dY) is given
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                          hipStream_t st, bool bf16, const float* addend = nullptr,

@@ -898,7 +898,11 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
   if (bf16 && conv_fwd_bf16_ok(s))
     return conv_fwd_bf16(s, x, w, bias, y, relu, ws, st, xb, wtb, yb, stats);
   if (yb) throw std::runtime_error("conv_fwd: bf16 output needs the bf16 conv family");
-  if (stats && stats->part) throw std::runtime_error("conv_fwd: statistics need the bf16 family");
+  if (stats && stats->part) {  // fp32 route: the tiled forward's epilogue / slab reduction
+    if (bf16 || !(conv_fwd_tiled_ok(s) || conv_fwd_tiled_gather_ok(s)))
+      throw std::runtime_error("conv_fwd: BatchNorm statistics need the bf16 or fp32 tiled family");
+    return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, false, stats);
+  }
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
   if (conv_fwd_direct_ok(s)) {
     const long long total = (long long)s.N * s.OH * s.OW * s.K;

@@ -178,6 +178,19 @@ BN_BWD_STATS = {"epilogue": 0, "pass": 0}  # BatchNorm backward counts by route
 # MTA_BN_FWD_EPILOGUE=0 / MTA_BN_BWD_EPILOGUE=0 fall back to the statistics passes
 _BNB_EPILOGUE = os.environ.get("MTA_BN_BWD_EPILOGUE", "1") != "0"
 BN_FWD_EPILOGUE = os.environ.get("MTA_BN_FWD_EPILOGUE", "1") != "0"
+# fp32 conv mode: the tiled forward's epilogue / split-K reduction can write
+# them too.  Off by default (MTA_BN_FWD_F32=1 / set_bn_fwd_f32 turn it on):
+# ResNet-18 fp32 B=32 measured 6.655 / 6.666 ms on vs 6.641 / 6.646 off - the
+# 64-row fp32 tiles give P = 2 x M / 64 partial rows, and the finalize's
+# strided reads of that table cost what the skipped statistics pass saved
+_BN_FWD_F32 = os.environ.get("MTA_BN_FWD_F32", "0") == "1"
+
+
+def set_bn_fwd_f32(on: bool) -> None:
+    """fp32 conv mode: let the tiled forward write the consuming BatchNorm's
+    batch statistics (see _BN_FWD_F32)."""
+    global _BN_FWD_F32
+    _BN_FWD_F32 = bool(on)
 
 
 def set_bn_bwd_epilogue(on: bool) -> None:
@@ -258,8 +271,9 @@ class _ConvFn(torch.autograd.Function):
         oshape = (shape.N, shape.OH, shape.OW, shape.K)
         y = torch.empty(oshape, dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
         part, rows = None, 0
-        if out_bf16 and bn_shift is not None:  # the consuming BatchNorm's statistics
-            rows = C.ops.conv_fwd_stats_rows(shape)
+        if bn_shift is not None:  # the consuming BatchNorm's statistics
+            # bf16 output: the bf16 family; fp32: the tiled forward (conv2d checks)
+            rows = C.ops.conv_fwd_stats_rows(shape, bool(out_bf16))
             part = torch.empty(2 * shape.K * rows, dtype=torch.float32, device=x.device)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), 0 if out_bf16 else ptr(y), relu, ptr(ws), s,
                        ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0, ptr(part), rows,
@@ -466,9 +480,10 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
     GradJoin).  out_bf16: store the output as bf16 when the bf16 conv family
     runs it (no bias / ReLU epilogue) - for a conv whose only consumer is
     `batchnorm`, which reads bf16 input.  bn_shift (training): that
-    BatchNorm's running mean - a bf16-output conv then also writes the batch
-    statistics in its epilogue (shifted by it) and the BatchNorm skips its
-    statistics pass.  All GPU only, ignored on the CPU path."""
+    BatchNorm's running mean - a bf16-output conv (or, in fp32 conv mode, the
+    tiled fp32 forward) then also writes the batch statistics in its epilogue
+    (shifted by it) and the BatchNorm skips its statistics pass.  All GPU
+    only, ignored on the CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
     if x.is_cuda:
@@ -482,6 +497,10 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob,
                                        bn_shift if ob else None)
         ob = ob and C.ops.conv_bf16_ok(sh)
+        # fp32 conv mode: the tiled forward writes the statistics instead
+        st32 = bool(bn_shift is not None and not _CONV_BF16 and b is None and not relu and
+                    _BN_FWD_F32 and C.ops.conv_fwd_tiled_ok(sh) and K % 64 == 0 and
+                    256 % (K // 4) == 0)
         nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
                   C.ops.chan_reduce_ws_floats(N * sh.OH * sh.OW, K), 4)
         ws = _WS.get(nws, x.device)
@@ -490,7 +509,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
                              None if b is None else b.grad_view, ws, join, join_role, w.wtb,
-                             w.wtb_d, ob, bn_shift if ob else None)
+                             w.wtb_d, ob, bn_shift if (ob or st32) else None)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y

@@ -583,6 +583,48 @@ def test_conv_epilogue_bn_statistics(cuda_dev, N, H, Cin, K, R, stride, pad):
     assert _rel(gw1, gw0) < 1e-4 and _rel(gg1, gg0) < 1e-4 and _rel(gb1, gb0) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,Cin,K,R,stride,pad", [
+    (4, 14, 64, 64, 3, 1, 1),     # unsplit tiled forward: statistics in its epilogue
+    (2, 7, 256, 512, 3, 1, 1),    # split-K: in the slab reduction
+    (3, 9, 64, 128, 1, 2, 0),     # 1x1 stride-2 downsample, partial last tile
+    (2, 20, 3, 64, 7, 2, 3),      # stem: gather-loader forward
+])
+def test_conv_epilogue_bn_statistics_fp32(cuda_dev, N, H, Cin, K, R, stride, pad):
+    """fp32 conv mode: the tiled forward given the consuming BatchNorm's
+    running mean writes the batch statistics in its epilogue (or split-K
+    reduction) and the BatchNorm skips its statistics pass: output, running
+    statistics and gradients match the two-pass BatchNorm on the same conv."""
+    g = torch.Generator().manual_seed(19)
+    x = torch.randn(N, H, H, Cin, generator=g).to(cuda_dev)
+    w = (torch.randn(R, R, Cin, K, generator=g) * 0.1).to(cuda_dev)
+    gam = (torch.rand(K, generator=g) + 0.5).to(cuda_dev)
+    bet = torch.randn(K, generator=g).to(cuda_dev)
+    rm0 = (torch.randn(K, generator=g) * 0.3).to(cuda_dev)  # a nonzero shift
+    OH = (H + 2 * pad - R) // stride + 1
+    dy = torch.randn(N, OH, OH, K, generator=g).to(cuda_dev)
+    out = []
+    Fn.set_bn_fwd_f32(True)
+    try:
+        for fused in (False, True):
+            xi = x.clone().requires_grad_(Cin % 4 == 0)
+            wp, gp, bp = _param(w), _param(gam), _param(bet)
+            rm, rv = rm0.clone(), torch.ones(K, device=cuda_dev)
+            y = Fn.conv2d(xi, wp, None, stride, pad, False, bn_shift=rm if fused else None)
+            assert y.dtype == torch.float32
+            assert (Fn._bnstats(y, rm) is not None) == fused
+            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True)
+            h.backward(dy)
+            out.append((h.detach().clone(), rm.clone(), rv.clone(), wp.grad_view.clone(),
+                        gp.grad_view.clone(), bp.grad_view.clone()))
+    finally:
+        Fn.set_bn_fwd_f32(False)
+    torch.cuda.synchronize()
+    (h0, m0, v0, gw0, gg0, gb0), (h1, m1, v1, gw1, gg1, gb1) = out
+    assert _rel(h1, h0) < 1e-5
+    assert _rel(m1, m0) < 1e-6 and _rel(v1, v0) < 1e-5
+    assert _rel(gw1, gw0) < 1e-5 and _rel(gg1, gg0) < 1e-5 and _rel(gb1, gb0) < 1e-6
+
+
 @pytest.mark.parametrize("N,H,Cin,K,stride,relu", [
     (4, 14, 64, 64, 1, True),      # halo dgrad, unsplit: sums in its epilogue
     (4, 7, 512, 512, 1, False),    # halo dgrad, split-K: in the slab reduction
