@@ -325,7 +325,8 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
                                                  const float* __restrict__ w,
                                                  const float* __restrict__ bias,
                                                  float* __restrict__ y, int relu, int kps,
-                                                 const ConvStats cs) {
+                                                 const ConvStats cs,
+                                                 const float* __restrict__ addend) {
   // split-K (gridDim.y > 1, no bias / ReLU): slice z of kps K tiles writes a
   // raw slab y + z * M * K, summed by slab_sum4 afterwards
   using G = Geo<BM, BN, P>;
@@ -358,6 +359,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const float* __res
         if (m >= M || !cok) continue;
         float v = acc[i][j][r] + b;
         if (relu) v = fmaxf(v, 0.f);
+        if (addend) v += addend[(size_t)m * s.K + co];  // gradient join (dgrad as forward)
         y[(size_t)m * s.K + co] = v;
         const float d = v - kc;
         s1 += d;
@@ -852,6 +854,35 @@ __global__ __launch_bounds__(256) void slab_sum4_stats_kernel(const float4* __re
   }
 }
 
+// Stride-1 backward-data as a forward conv of dY (fp32): dX = conv(dY, W')
+// with pad R - 1 - pad and W'[kh][kw][co][ci] = W[R-1-kh][S-1-kw][ci][co].
+// The forward kernel's operands are both float4 rows into LDS; the dgrad
+// kernel stages W through 4 scalar LDS stores per float4 (its k = co is the
+// contiguous axis) and measured 119-129 us against 96-104 us forward on the
+// same ResNet-18 shapes.  One 32 x 32 LDS tile transpose per (tap, ci, co)
+// block: coalesced reads along co, coalesced writes along ci.
+__global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w,
+                                                    float* __restrict__ wt, int R, int S, int C,
+                                                    int K) {
+  __shared__ float t[32][33];
+  const int tap = blockIdx.z, ci0 = blockIdx.y * 32, co0 = blockIdx.x * 32;
+  const int kh = tap / S, kw = tap - kh * S;
+  const float* src = w + (size_t)((R - 1 - kh) * S + (S - 1 - kw)) * C * K;
+  float* dst = wt + (size_t)tap * K * C;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+#pragma unroll
+  for (int r = ty; r < 32; r += 8) {
+    const int ci = ci0 + r, co = co0 + tx;
+    t[r][tx] = (ci < C && co < K) ? src[(size_t)ci * K + co] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = ty; r < 32; r += 8) {
+    const int co = co0 + r, ci = ci0 + tx;
+    if (co < K && ci < C) dst[(size_t)co * C + ci] = t[tx][r];
+  }
+}
+
 // ------------------------------------------------------------ dispatch ----
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
@@ -970,6 +1001,25 @@ static inline void slab_sum(const float* part, int z, long long n, float* out, h
 }
 }  // namespace tiled
 
+// fp32 stride-1 dgrad through the forward kernel (see wflip_kernel): the
+// forward shape over dY and the floats of the flipped weight ahead of its
+// split-K workspace.  MTA_TILED_DGRAD_FWD=0: the phase-decomposed dgrad
+static bool dgrad_fwd_ok(const ConvShape& s) {
+  static const bool on = [] {
+    const char* e = getenv("MTA_TILED_DGRAD_FWD");
+    return !(e && e[0] == '0');
+  }();
+  return on && s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 && 2 * s.pad == s.R - 1 &&
+         s.K % tiled::BK == 0 && s.C % 4 == 0 && s.OH == s.H && s.OW == s.W;
+}
+static ConvShape dgrad_fwd_shape(const ConvShape& s) {
+  return ConvShape{s.N, s.OH, s.OW, s.K, s.C, s.R, s.S, 1, s.R - 1 - s.pad, s.H, s.W};
+}
+static long long dgrad_fwd_ws_floats(const ConvShape& s) {
+  const long long wf = ((long long)s.R * s.S * s.C * s.K + 3) / 4 * 4;
+  return wf + conv_fwd_tiled_ws_floats(dgrad_fwd_shape(s), false);
+}
+
 // workspace for either operand precision (the plans differ in tile shape)
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
   long long n = 0;
@@ -983,7 +1033,7 @@ long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
 }
 
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
-  long long n = 0;
+  long long n = dgrad_fwd_ok(s) ? dgrad_fwd_ws_floats(s) : 0;
   for (const bool b : {false, true}) {
     tiled::Tile t;
     int z, kps;
@@ -1002,8 +1052,20 @@ int conv_fwd_tiled_stats_rows(const ConvShape& s, bool bf16) {
   return z > 1 ? (int)slab_grid(M * s.K) : cdiv(M, tile_m(t)) * 2;
 }
 
+static void conv_fwd_tiled_impl(const ConvShape& s, const float* x, const float* w,
+                                const float* bias, float* y, bool relu, float* ws,
+                                hipStream_t st, bool bf16, const ConvStats* stats,
+                                const float* addend);
+
 void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                     bool relu, float* ws, hipStream_t st, bool bf16, const ConvStats* stats) {
+  conv_fwd_tiled_impl(s, x, w, bias, y, relu, ws, st, bf16, stats, nullptr);
+}
+
+static void conv_fwd_tiled_impl(const ConvShape& s, const float* x, const float* w,
+                                const float* bias, float* y, bool relu, float* ws,
+                                hipStream_t st, bool bf16, const ConvStats* stats,
+                                const float* addend) {
   using namespace tiled;
   const long long M = (long long)s.N * s.OH * s.OW;
   Tile t;
@@ -1022,25 +1084,38 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
   if (s.C % BK != 0) {  // gather loader (fp32 operands only)
     if (bf16) throw std::runtime_error("conv_fwd_tiled: the gather forward is fp32");
 #define F32G F32, true
-    TILED_DISPATCH_P(F32G, t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs)
+    TILED_DISPATCH_P(F32G, t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs,
+                     z > 1 ? nullptr : addend)
 #undef F32G
   } else {
-    TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs)
+    TILED_DISPATCH(t, fwd_kernel, GRID, s, x, w, bias, out, relu ? 1 : 0, kps, cs,
+                   z > 1 ? nullptr : addend)
   }
 #undef GRID
   if (z > 1) {
+    if (addend && stats && stats->part)
+      throw std::runtime_error("conv_fwd_tiled: statistics with an addend");
     if (stats && stats->part)
       slab_sum4_stats_kernel<<<(int)slab_grid(M * s.K), 256, 0, st>>>(
           reinterpret_cast<const float4*>(ws), z, M * s.K / 4, reinterpret_cast<float4*>(y),
           *stats, s.K);
     else
-      slab_sum(ws, z, M * s.K, y, st);
+      slab_sum(ws, z, M * s.K, y, st, addend);
   }
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                          hipStream_t st, bool bf16, const float* addend, const void* dyb) {
   using namespace tiled;
+  if (!bf16 && dy && ws && dgrad_fwd_ok(s)) {
+    const ConvShape f = dgrad_fwd_shape(s);
+    float* wt = ws;
+    float* fws = ws + ((long long)s.R * s.S * s.C * s.K + 3) / 4 * 4;
+    wflip_kernel<<<dim3(cdiv(s.K, 32), cdiv(s.C, 32), s.R * s.S), 256, 0, st>>>(w, wt, s.R, s.S,
+                                                                               s.C, s.K);
+    conv_fwd_tiled_impl(f, dy, wt, nullptr, dx, false, fws, st, false, nullptr, addend);
+    return;
+  }
   const int sd = s.stride;
   const long long Mph = (long long)s.N * ((s.H + sd - 1) / sd) * ((s.W + sd - 1) / sd);
   Tile t;
