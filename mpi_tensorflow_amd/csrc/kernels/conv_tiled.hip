@@ -1170,7 +1170,11 @@ int conv_filter_tiled_splits(const ConvShape& s) {
   // gather-path slice cap: the ResNet stem's filter gradient (3 tiles of 64 x 64,
   // 12544 K tiles) went 271 -> 197 us from 128 to 256 slices (512: 196, 1024: 198)
   static const int gcap = env_int("MTA_TILED_GCAP", 256);
-  if (z > (vec ? 64 : gcap)) z = vec ? 64 : gcap;
+  // vector-path slice cap (MTA_TILED_VCAP).  conv_lab fp32: the 56x56x64 filter
+  // gradient (9 tiles) 152.5 -> 129.0 -> 117.2 us at caps 64 -> 128 -> 256 (all
+  // layers 2120 -> 1984 / 2021 us); not yet verified in a full step, so 64 stays
+  static const int vcap = env_int("MTA_TILED_VCAP", 64);
+  if (z > (vec ? vcap : gcap)) z = vec ? vcap : gcap;
   const int kchunk = cdiv(ktiles, z);
   return cdiv(ktiles, kchunk);  // splits actually launched
 }
