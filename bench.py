@@ -169,8 +169,9 @@ def main(argv=None) -> int:
     from mpi_tensorflow_amd.utils.faults import maybe_fail
 
     if a.gpus > 1 and D.discover().launcher == "none":
-        # --comm shm: ranks may share GPUs (rank r binds GPU r % count)
-        return launch_ranks(a.gpus, argv, share_gpus=a.comm == "shm")
+        # --comm shm / auto: ranks may share GPUs (rank r binds GPU r % count;
+        # auto then picks the shared-memory communicator, parallel/comm.py)
+        return launch_ranks(a.gpus, argv, share_gpus=a.comm in ("shm", "auto"))
     if D.discover().world != a.gpus:
         print(f"error: --gpus {a.gpus} but the launcher started {D.discover().world} rank(s)",
               file=sys.stderr)

@@ -19,6 +19,7 @@ struct FcSgdArgs {
   uint16_t* w1b = nullptr;
   uint16_t* w1t = nullptr;
   long long w1 = 0;
+  float gscale = 1.f;  // world > 1: the grads are the rank sum (1 / ranks)
 };
 // conv1 filter-grad role appended to a conv2 filter-gradient launch (its input
 // dA1m must be final: the conv2 bwd-data launch ran before)
@@ -139,16 +140,39 @@ void launch_conv1_bwd_filter(const float* data, const long long* step, int n_loc
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s);
-// world-1 step: grad_finalize fused into the momentum SGD (FC bucket from the
-// flat grads [0, fc_end) with L2 on all of it, conv grads straight from the
-// slabs); bumps *step.  wino_u / wino_ud (optional): also writes the Winograd
-// transforms of the updated conv2 filters (launch_conv2_wino_weights layouts)
-void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
-                         int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
-                         int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s, bool fc_done = false,
-                         float* wino_u = nullptr, float* wino_ud = nullptr,
-                         uint16_t* w2tb = nullptr, uint16_t* w2b = nullptr);
+// The SGD launch that ends a train step (mnist.hip sgd_finalize_kernel):
+// momentum SGD of the FC bucket [0, fc_end) (optional; L2 on all of it) and
+// of the conv parameters (optional), whose grads are either summed from the
+// filter-gradient slabs (world 1: part2 / part1 set) or read from the flat
+// buffer (world > 1, after their all-reduce: part2 == nullptr).  Grads are
+// scaled by gscale (1 / ranks).  It also writes what the next step reads of
+// the updated weights: the Winograd transforms (wino_u / wino_ud), the bf16
+// conv2 shadows (w2tb / w2b) and, with the FC bucket, the bf16 fc1 shadows
+// (w1b / w1t; off_w1fc = the fc1 weight's float offset).  step: bumped once.
+struct SgdStepArgs {
+  float* w = nullptr;
+  const float* g = nullptr;
+  float* mom = nullptr;
+  float l2 = 0.f, momentum = 0.f, gscale = 1.f;
+  const float* lr = nullptr;
+  long long* step = nullptr;
+  long long fc_end = 0;
+  int fc_rounds = 2;
+  uint16_t* w1b = nullptr;
+  uint16_t* w1t = nullptr;
+  long long off_w1fc = 0;
+  bool conv = true;
+  int off_w2 = 0, off_b2 = 0, off_w1 = 0, off_b1 = 0;
+  const float* part2 = nullptr;
+  int ngroups = 0;
+  const float* part1 = nullptr;
+  int nblk1 = 0;
+  float* wino_u = nullptr;
+  float* wino_ud = nullptr;
+  uint16_t* w2tb = nullptr;
+  uint16_t* w2b = nullptr;
+};
+void launch_sgd_step(const SgdStepArgs& a, hipStream_t s);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

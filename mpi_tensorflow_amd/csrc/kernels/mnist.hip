@@ -2041,7 +2041,8 @@ FcSgd fc_sgd_args(const FcSgdArgs* a) {
   FcSgd r{};
   if (a == nullptr || a->n == 0) return r;
   if (a->n % 4) throw std::runtime_error("fc_sgd: FC bucket not a multiple of 4 floats");
-  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0};
+  r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0,
+            a->gscale};
   const long long per_blk = 256LL * FC_SGD_UNROLL * a->rounds;
   if (a->w1b) {
     if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
@@ -2135,34 +2136,39 @@ void launch_conv1_bwd_filter(const float* data, const long long* step, int n_loc
       batch, C1Filter{data, step, n_local, da1m, idx1, part1});
 }
 
-// ----------------------------------------------- world-1 SGD + finalize ----
-// Single-rank train step: the conv filter-grad slab reductions of
-// grad_finalize_kernel are fused into the momentum SGD (U1), which saves a
-// launch (a kernel boundary plus one dependent HBM round trip; 6.6 + 4.9 us
-// -> 9.4 us at B = 64).  With world > 1 the conv grads must be final in the
-// flat buffer BEFORE their all-reduce, so the executor keeps finalize + SGD
-// there.  (A variant that also wrote the bf16 weight shadows from the SGD
-// measured no faster than the shadow role of the conv1 launch: 13.7 us.)
-// Roles (blocks): [0, fc_blocks) grid-stride float4 over the FC bucket
-// [0, fc_end) (all of it L2-regularised); 50 blocks: conv2 weights, one
-// float4 per thread summed over the slabs; 16 blocks: conv2 bias, one wave
-// per channel; 208 blocks: conv1 weight + bias, one wave per output.  Each
-// conv element's sum runs in the same order as in grad_finalize_kernel.
+// ------------------------------------------------- SGD of the step ----
+// The last launch of a train step: momentum SGD (U1) of the parameters whose
+// gradients are final, plus the derived weights the NEXT step reads, so no
+// launch of its own re-derives them.
+//  * world 1: the conv filter-grad slab reductions of grad_finalize_kernel
+//    are fused into the SGD (a kernel boundary plus one dependent HBM round
+//    trip saved: 6.6 + 4.9 us -> 9.4 us at B = 64); the FC bucket was updated
+//    by the conv2 bwd-data launch's role blocks (fc.n4 == 0 here).
+//  * world > 1: the conv grads were finalized before their all-reduce, so
+//    the conv part reads the rank sums from the flat buffer (x 1/N); the FC
+//    bucket, when this launch owns it, runs fc_sgd_role (bf16: also the fc1
+//    weight's shadows, in 64 x 64 tiles).
+// Roles (blocks): [0, fc.nblk) FC bucket; then, when conv is on, 128
+// (Winograd: per (ci, co quarter), + the U / Ud transforms) or 50 (flat, +
+// the bf16 conv2 shadows) conv2-weight blocks, 16 conv2-bias blocks (one wave
+// per channel), 208 conv1 blocks (one wave per weight / bias).  Each slab sum
+// runs in the order of grad_finalize_kernel.
 struct SgdFinArgs {
+  FcSgd fc;  // FC bucket role (fc.n4 == 0: off)
   float* w;
   const float* g;
   float* mom;
-  long long fc_end4;
+  int conv;  // conv parameters updated by this launch
+  int flat;  // conv grads from g (world > 1) instead of the slabs
   int off_w2, off_b2, off_w1, off_b1;
   const float* part2;
   const float* part_db2;
   int ngroups;
   const float* part1;
   int nblk1;
-  float l2, momentum;
+  float momentum, gscale;
   const float* lr;
-  long long* step;
-  int fc_blocks;
+  long long* step;  // bumped once (nullptr: no bump)
   // Winograd conv2 (optional): the updated conv2 filters' transforms for the
   // NEXT step's forward (U) and bwd-data (Ud), layouts of wino_u_index
   float* U;
@@ -2179,43 +2185,51 @@ __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, 
   *w -= lr * mv;
 }
 
+// dW2 float4 i (HWIO order): slab sum in group order (16 loads in flight), or
+// the all-reduced flat gradient
+__device__ __forceinline__ float4 conv2_grad4(const SgdFinArgs& a, int i) {
+  if (a.flat) return reinterpret_cast<const float4*>(a.g + a.off_w2)[i];
+  const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
+  float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 16 <= a.ngroups; z += 16) {
+    float4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      sv.x += v[u].x;
+      sv.y += v[u].y;
+      sv.z += v[u].z;
+      sv.w += v[u].w;
+    }
+  }
+  for (; z < a.ngroups; ++z) {
+    const float4 v = p2[(size_t)z * 12800];
+    sv.x += v.x;
+    sv.y += v.y;
+    sv.z += v.z;
+    sv.w += v.w;
+  }
+  return sv;
+}
+
 // conv2 weights of one input channel ci and 16 output channels (block b: ci
-// = b / 4, co quarter b % 4; 25 taps x 4 float4s = 100 threads): slab sums in
-// group order (16 loads in flight), SGD, then the Winograd transforms of the
-// updated 5x5 filters (U and Ud).  128 blocks with short sums: with 32 blocks
-// of 2 taps x 32 groups a thread waited on 8 rounds of 8 loads (9.1 us SGD).
+// = b / 4, co quarter b % 4; 25 taps x 4 float4s = 100 threads): gradient,
+// SGD, then the Winograd transforms of the updated 5x5 filters (U and Ud).
+// 128 blocks with short sums: with 32 blocks of 2 taps x 32 groups a thread
+// waited on 8 rounds of 8 loads (9.1 us SGD).
 __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
   __shared__ float wl[25 * 16];
   const int tid = threadIdx.x, ci = blk >> 2, cq = blk & 3;
   if (tid < 100) {
     const int t = tid >> 2, c4 = tid & 3;
     const int i = (t * 32 + ci) * 16 + cq * 4 + c4;  // float4 index in the HWIO block
-    const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
-    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
-    int z = 0;
-    for (; z + 16 <= a.ngroups; z += 16) {
-      float4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        sv.x += v[u].x;
-        sv.y += v[u].y;
-        sv.z += v[u].z;
-        sv.w += v[u].w;
-      }
-    }
-    for (; z < a.ngroups; ++z) {
-      const float4 v = p2[(size_t)z * 12800];
-      sv.x += v.x;
-      sv.y += v.y;
-      sv.z += v.z;
-      sv.w += v.w;
-    }
+    const float4 sv = conv2_grad4(a, i);
     float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
     float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
     float4 wv = *wp, mv = *mp;
-    sgd4(wv, mv, sv, 0.f, lr, a.momentum);
+    sgd4(wv, mv, sv, 0.f, lr, a.momentum, a.gscale);
     *wp = wv;
     *mp = mv;
     *reinterpret_cast<float4*>(wl + t * 16 + 4 * c4) = wv;
@@ -2240,37 +2254,15 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
   }
 }
 
-// conv2 weights: 51200 floats = 50 blocks x 256 threads x float4, each summed
-// over the image-group slabs in order
+// conv2 weights: 51200 floats = 50 blocks x 256 threads x float4
 __device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
   const int tid = threadIdx.x;
   const int i = blk * 256 + tid;
-  const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
-  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-  int z = 0;
-  for (; z + 8 <= a.ngroups; z += 8) {  // 8 slab loads in flight, summed in order
-    float4 v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = p2[(size_t)(z + u) * 12800];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      s.x += v[u].x;
-      s.y += v[u].y;
-      s.z += v[u].z;
-      s.w += v[u].w;
-    }
-  }
-  for (; z < a.ngroups; ++z) {
-    const float4 v = p2[(size_t)z * 12800];
-    s.x += v.x;
-    s.y += v.y;
-    s.z += v.z;
-    s.w += v.w;
-  }
+  const float4 s = conv2_grad4(a, i);
   float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
   float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
   float4 wv = *wp, mv = *mp;
-  sgd4(wv, mv, s, 0.f, lr, a.momentum);
+  sgd4(wv, mv, s, 0.f, lr, a.momentum, a.gscale);
   *wp = wv;
   *mp = mv;
   if (a.w2t) {  // HWIO (t * 32 + ci) * 64 + co: 4 consecutive co
@@ -2289,24 +2281,16 @@ __device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
 }
 
 __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
+  __shared__ float tile[SHADOW_SMEM_FLOATS];  // fc1 shadow tiles (bf16, world > 1)
   const float lr = *a.lr;
   const int tid = threadIdx.x;
   int blk = blockIdx.x;
-  if (blk == 0 && tid == 0) *a.step += 1;
-  if (blk < a.fc_blocks) {
-    float4* W4 = reinterpret_cast<float4*>(a.w);
-    float4* M4 = reinterpret_cast<float4*>(a.mom);
-    const float4* G4 = reinterpret_cast<const float4*>(a.g);
-    const long long stride = (long long)a.fc_blocks * 256;
-    for (long long i = (long long)blk * 256 + tid; i < a.fc_end4; i += stride) {
-      float4 wv = W4[i], gv = G4[i], mv = M4[i];
-      sgd4(wv, mv, gv, a.l2, lr, a.momentum);
-      W4[i] = wv;
-      M4[i] = mv;
-    }
+  if (a.step && blk == 0 && tid == 0) *a.step += 1;
+  if (blk < a.fc.nblk) {
+    fc_sgd_role(a.fc, blk, tile);
     return;
   }
-  blk -= a.fc_blocks;
+  blk -= a.fc.nblk;
   const int nconv2 = a.U ? 128 : 50;
   if (blk < nconv2) {
     if (a.U)
@@ -2317,48 +2301,83 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
   }
   blk -= nconv2;
   const int lane = tid & 63;
+  // (gscale: the conv bias / conv1 grads go through the sgd4 expression form
+  // g * gs + 0 * w, as in optim::sgd_momentum_flat)
   if (blk < 16) {  // conv2 bias: one wave per channel
     const int co = blk * 4 + (tid >> 6);
     float s = 0.f;
-    for (int z = lane; z < 4 * a.ngroups; z += 64) s += a.part_db2[z * 64 + co];
-    s = wave_sum(s);
-    if (lane == 0) sgd_elem(a.w + a.off_b2 + co, a.mom + a.off_b2 + co, s, lr, a.momentum);
+    if (a.flat) {
+      s = a.g[a.off_b2 + co];
+    } else {
+      for (int z = lane; z < 4 * a.ngroups; z += 64) s += a.part_db2[z * 64 + co];
+      s = wave_sum(s);
+    }
+    if (lane == 0) {
+      float* w = a.w + a.off_b2 + co;
+      sgd_elem(w, a.mom + a.off_b2 + co, s * a.gscale + 0.f * *w, lr, a.momentum);
+    }
     return;
   }
   blk -= 16;
   const int o = blk * 4 + (tid >> 6);
   if (o >= 832) return;
+  const int off = o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800);
   float s = 0.f;
+  if (a.flat) {
+    s = a.g[off];
+  } else {
 #pragma unroll 8
-  for (int b = lane; b < a.nblk1; b += 64) s += a.part1[(size_t)b * 832 + o];
-  s = wave_sum(s);
-  if (lane == 0) {
-    const int off = o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800);
-    sgd_elem(a.w + off, a.mom + off, s, lr, a.momentum);
+    for (int b = lane; b < a.nblk1; b += 64) s += a.part1[(size_t)b * 832 + o];
+    s = wave_sum(s);
   }
+  if (lane == 0) sgd_elem(a.w + off, a.mom + off, s * a.gscale + 0.f * a.w[off], lr, a.momentum);
 }
 
-void launch_sgd_finalize(float* w, const float* g, float* mom, long long fc_end, long long l2_end,
-                         int off_w2, int off_b2, int off_w1, int off_b1, const float* part2,
-                         int ngroups, const float* part1, int nblk1, float l2, float momentum,
-                         const float* lr, long long* step, hipStream_t s, bool fc_done,
-                         float* wino_u, float* wino_ud, uint16_t* w2tb, uint16_t* w2b) {
-  if ((w2tb == nullptr) != (w2b == nullptr) || (w2tb && wino_u))
-    throw std::runtime_error("sgd_finalize: bf16 conv2 shadows need both layouts, no Winograd");
-  if (fc_end % 4 || off_w2 % 4 || l2_end != fc_end)
-    throw std::runtime_error("sgd_finalize: misaligned flat segments / L2 prefix != FC bucket");
-  if ((wino_u == nullptr) != (wino_ud == nullptr))
-    throw std::runtime_error("sgd_finalize: Winograd filters need both U and Ud");
-  const long long n4 = fc_end / 4;
-  long long b = (n4 + 255) / 256;
-  // fc_done: the FC bucket was updated by the conv2 bwd-data launch's SGD role
-  const int fc_blocks = fc_done ? 0 : (int)(b < 2048 ? b : 2048);  // as the flat SGD
-  SgdFinArgs a{w, g, mom, n4, off_w2, off_b2, off_w1, off_b1, part2,
-               part2 + (size_t)ngroups * 51200, ngroups, part1, nblk1, l2, momentum, lr, step,
-               fc_blocks, wino_u, wino_ud, reinterpret_cast<__bf16*>(w2tb),
-               reinterpret_cast<__bf16*>(w2b)};
-  const int conv2_blocks = wino_u ? 128 : 50;
-  sgd_finalize_kernel<<<fc_blocks + conv2_blocks + 16 + cdiv(832, 4), 256, 0, s>>>(a);
+void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
+  const SgdStepArgs& p = s_;
+  if ((p.w2tb == nullptr) != (p.w2b == nullptr) || (p.w2tb && p.wino_u))
+    throw std::runtime_error("sgd_step: bf16 conv2 shadows need both layouts, no Winograd");
+  if ((p.wino_u == nullptr) != (p.wino_ud == nullptr))
+    throw std::runtime_error("sgd_step: Winograd filters need both U and Ud");
+  if (p.off_w2 % 4 || p.fc_end % 4)
+    throw std::runtime_error("sgd_step: misaligned flat segments");
+  if (p.conv && p.part2 == nullptr && p.off_b1 != p.off_w1 + 800)
+    throw std::runtime_error("sgd_step: conv1 weight and bias must be adjacent");
+  SgdFinArgs a{};
+  if (p.fc_end > 0) {
+    FcSgdArgs f{p.w, p.g, p.mom, p.fc_end, p.l2, p.momentum, p.lr, p.fc_rounds};
+    f.w1b = p.w1b;
+    f.w1t = p.w1t;
+    f.w1 = p.off_w1fc;
+    f.gscale = p.gscale;
+    a.fc = fc_sgd_args(&f);
+  }
+  a.w = p.w;
+  a.g = p.g;
+  a.mom = p.mom;
+  a.conv = p.conv ? 1 : 0;
+  a.flat = p.part2 == nullptr ? 1 : 0;
+  a.off_w2 = p.off_w2;
+  a.off_b2 = p.off_b2;
+  a.off_w1 = p.off_w1;
+  a.off_b1 = p.off_b1;
+  a.part2 = p.part2;
+  a.part_db2 = p.part2 ? p.part2 + (size_t)p.ngroups * 51200 : nullptr;
+  a.ngroups = p.ngroups;
+  a.part1 = p.part1;
+  a.nblk1 = p.nblk1;
+  a.momentum = p.momentum;
+  a.gscale = p.gscale;
+  a.lr = p.lr;
+  a.step = p.step;
+  a.U = p.wino_u;
+  a.Ud = p.wino_ud;
+  a.w2t = reinterpret_cast<__bf16*>(p.w2tb);
+  a.w2b = reinterpret_cast<__bf16*>(p.w2b);
+  const int conv_blocks = p.conv ? (p.wino_u ? 128 : 50) + 16 + cdiv(832, 4) : 0;
+  const int grid = a.fc.nblk + conv_blocks;
+  if (grid == 0) throw std::runtime_error("sgd_step: nothing to update");
+  sgd_finalize_kernel<<<grid, 256, 0, s>>>(a);
 }
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,

@@ -170,13 +170,15 @@ __device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c,
   }
 }
 
-// momentum SGD on 4 floats: g += lc * w (L2); m = mu m + g; w -= lr m
+// momentum SGD on 4 floats: g = gs g + lc w (rank-sum scale 1/N, L2);
+// m = mu m + g; w -= lr m (the expression forms of optim::sgd_momentum_flat,
+// so every SGD path of the step rounds identically)
 __device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc, float lr,
-                                     float mu) {
-  gv.x += lc * wv.x;
-  gv.y += lc * wv.y;
-  gv.z += lc * wv.z;
-  gv.w += lc * wv.w;
+                                     float mu, float gs = 1.f) {
+  gv.x = gv.x * gs + lc * wv.x;
+  gv.y = gv.y * gs + lc * wv.y;
+  gv.z = gv.z * gs + lc * wv.z;
+  gv.w = gv.w * gs + lc * wv.w;
   mv.x = mu * mv.x + gv.x;
   mv.y = mu * mv.y + gv.y;
   mv.z = mu * mv.z + gv.z;
@@ -280,6 +282,7 @@ struct FcSgd {
   __bf16* w1b;
   __bf16* w1t;
   long long w1_off4;
+  float gs;  // gradient scale (1 / ranks: the bucket holds the rank sum)
 };
 constexpr int FC_SGD_UNROLL = 4;
 constexpr long long W1_F4 = (long long)FC1_IN * FC1_OUT / 4;
@@ -304,7 +307,7 @@ __device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* ti
   float v[16];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
-    sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
+    sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu, a.gs);
     W4[u] = wv[u];
     M4[u] = mv[u];
     v[4 * u] = wv[u].x;
@@ -359,7 +362,7 @@ __device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile,
     for (int u = 0; u < FC_SGD_UNROLL; ++u) {
       if (i0 + u * stride < n4) {
         const long long i = at(i0 + u * stride);
-        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu);
+        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.mu, a.gs);
         W4[i] = wv[u];
         M4[i] = mv[u];
       }

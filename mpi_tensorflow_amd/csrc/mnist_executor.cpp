@@ -42,11 +42,10 @@ MnistExecutor::~MnistExecutor() {
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
-                                    const mnist::FcSgdArgs* fc_sgd, bool factors,
-                                    bool wino_fresh) {
+                                    const mnist::FcSgdArgs* fc_sgd, bool factors, bool fresh) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
-    return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, wino_fresh);
+    return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, fresh);
   }
   const MnistPtrs& p = p_;
   float* W = P<float>(p.params);
@@ -67,8 +66,8 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   cf.idx1 = P<uint8_t>(p.idx1);
   if (p.wino) {
     // transformed filters of this step's weights (forward U, bwd-data Ud);
-    // the single-rank step's SGD already wrote them (wino_fresh)
-    if (!wino_fresh)
+    // the previous step's SGD launch already wrote them (fresh)
+    if (!fresh)
       mnist::launch_conv2_wino_weights(W + p.off_w2, P<float>(p.wino_u), P<float>(p.wino_ud), s);
     mnist::launch_conv12_fwd_wino(cf, B, W + p.off_w2, P<const float>(p.wino_u), W + p.off_b2,
                                   P<float>(p.a2), P<uint8_t>(p.idx2), nullptr, s);
@@ -125,15 +124,10 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
   const long long* step = P<const long long>(p.step);
   const int B = p.batch;
   using U16 = uint16_t;
-  wait_fc_params(s);  // the shadow role of the conv1 launch reads the FC weights
-  // the conv1 launch also re-derives the bf16 weight shadows (block role):
-  // measured as fast as having the SGD write them (which needs a refresh
-  // after any outside change of the weights), and always correct
-  // (fc_sgd->w1b: the previous step's SGD already wrote the fc1 shadows)
-  const bool w1_done = fc_sgd != nullptr && fc_sgd->w1b != nullptr;
-  if (w1_done && shadows_fresh && B % 16 == 0) {
-    // single rank: every shadow is current (the previous step's SGD, or
-    // refresh_shadows), so conv1 runs inside the conv2 blocks (one launch)
+  if (shadows_fresh && B % 16 == 0) {
+    // every shadow is current (the previous step's SGD launch, or
+    // refresh_shadows), so conv1 runs inside the conv2 blocks (one launch);
+    // the FC weights are first read by fc1 forward
     mnist::C12In cf;
     cf.data = P<const float>(p.train_x);
     cf.step = step;
@@ -144,7 +138,12 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
     mnist::launch_conv12_fwd_bf16(cf, B, P<const U16>(p.w2tb), W + p.off_b2, P<U16>(p.a1p),
                                   P<U16>(p.a1t), P<U16>(p.a2h), P<U16>(p.a2t), P<uint8_t>(p.idx2),
                                   s);
+    wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
   } else {
+    // the conv1 launch re-derives the bf16 weight shadows (block role) from the
+    // fp32 master weights, the FC ones included: wait for those first
+    wait_fc_params(s);
+    const bool w1_done = fc_sgd != nullptr && fc_sgd->w1b != nullptr;
     mnist::launch_conv1_fwd_bf16(P<const float>(p.train_x), step, p.n_local, B, W + p.off_w1,
                                  W + p.off_b1, P<U16>(p.a1p), P<U16>(p.a1t), P<uint8_t>(p.idx1),
                                  B, s, W + p.off_w3, W + p.off_w2,
@@ -214,6 +213,48 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
                              bump_step ? P<long long>(p.step) : nullptr, s);
 }
 
+// The fused SGD launch (kernels/mnist.h launch_sgd_step) over the flat grads
+// at world > 1 (rank sums, x gscale): fc - the FC bucket, conv - the conv
+// parameters (then it also bumps the step).  It writes the derived weights of
+// what it updates - Winograd transforms, bf16 conv2 shadows, with the FC
+// bucket the bf16 fc1 shadows - so the next step's forward takes them as
+// current instead of re-deriving them in a launch of its own.
+void MnistExecutor::sgd_step(hipStream_t s, float gscale, bool fc, bool conv) {
+  const MnistPtrs& p = p_;
+  mnist::SgdStepArgs a;
+  a.w = P<float>(p.params);
+  a.g = P<const float>(p.grads);
+  a.mom = P<float>(p.mom);
+  a.l2 = p.l2;
+  a.momentum = p.momentum;
+  a.gscale = gscale;
+  a.lr = P<const float>(p.lr);
+  a.step = conv ? P<long long>(p.step) : nullptr;
+  if (fc) {
+    a.fc_end = p.bucket1;
+    a.fc_rounds = 1;  // a launch of its own: twice the blocks of the in-launch role
+    if (p.bf16) {
+      a.w1b = P<uint16_t>(p.w1b);
+      a.w1t = P<uint16_t>(p.w1t);
+      a.off_w1fc = p.off_w3;
+    }
+  }
+  a.conv = conv;
+  a.off_w2 = (int)p.off_w2;
+  a.off_b2 = (int)p.off_b2;
+  a.off_w1 = (int)p.off_w1;
+  a.off_b1 = (int)p.off_b1;
+  if (conv && p.wino) {
+    a.wino_u = P<float>(p.wino_u);
+    a.wino_ud = P<float>(p.wino_ud);
+  }
+  if (conv && p.bf16) {
+    a.w2tb = P<uint16_t>(p.w2tb);
+    a.w2b = P<uint16_t>(p.w2b);
+  }
+  mnist::launch_sgd_step(a, s);
+}
+
 void MnistExecutor::reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs) {
   float* G = P<float>(p_.grads) + lo;
   if (!p_.grad_bf16) {
@@ -264,34 +305,63 @@ void MnistExecutor::wait_fc_params(hipStream_t s) {
 
 void MnistExecutor::join(hipStream_t s) { wait_fc_params(s); }
 
+bool MnistExecutor::fused_sgd_ok() const { return p_.l2_end == p_.bucket1; }
+
 void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                Collective* comm2) {
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
     const MnistPtrs& p = p_;
     wait_fc_params(s);
+    if (!fused_sgd_ok()) {  // (not the reference layout) plain launches
+      enqueue_fwd_bwd(s);
+      sgd_range(s, 0, p.total, 1.f, true);
+      return;
+    }
     // the FC bucket's SGD rides in the conv2 bwd-data launch (its grads are final
     // after fc1 backward); the slab sums + conv SGD run in the last launch
     mnist::FcSgdArgs fc{P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
                         p.bucket1, p.l2, p.momentum, P<const float>(p.lr), fc_sgd_rounds_};
-    if (p.bf16 && p.world == 1) {  // the SGD also writes the fc1 bf16 shadows (see refresh_shadows)
+    if (p.bf16) {  // the SGD also writes the fc1 bf16 shadows (see refresh_shadows)
       fc.w1b = P<uint16_t>(p.w1b);
       fc.w1t = P<uint16_t>(p.w1t);
       fc.w1 = p.off_w3;
     }
-    const bool fused = fc_sgd_rounds_ > 0 && p.l2_end == p.bucket1;
-    // Winograd: the filter transforms come from the previous step's SGD (or
-    // refresh_shadows() before the first step of a run) and are rewritten by
-    // this step's SGD for the next one
-    enqueue_fwd_bwd(s, /*finalize=*/false, fused ? &fc : nullptr, false, /*wino_fresh=*/true);
-    mnist::launch_sgd_finalize(P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
-                               p.bucket1, p.l2_end, (int)p.off_w2, (int)p.off_b2, (int)p.off_w1,
-                               (int)p.off_b1, P<const float>(p.part2), conv2_groups(),
-                               P<const float>(p.part1), conv1_blocks(), p.l2, p.momentum,
-                               P<const float>(p.lr), P<long long>(p.step), s, fused,
-                               p.wino ? P<float>(p.wino_u) : nullptr,
-                               p.wino ? P<float>(p.wino_ud) : nullptr,
-                               (p.bf16 && fused) ? P<uint16_t>(p.w2tb) : nullptr,
-                               (p.bf16 && fused) ? P<uint16_t>(p.w2b) : nullptr);
+    const bool role = fc_sgd_rounds_ > 0;
+    // the derived weights (Winograd transforms, bf16 shadows) come from the
+    // previous step's SGD (or refresh_shadows() before the first step of a
+    // run) and are rewritten by this step's SGD for the next one
+    enqueue_fwd_bwd(s, /*finalize=*/false, role ? &fc : nullptr, false, /*fresh=*/true);
+    mnist::SgdStepArgs a;
+    a.w = P<float>(p.params);
+    a.g = P<const float>(p.grads);
+    a.mom = P<float>(p.mom);
+    a.l2 = p.l2;
+    a.momentum = p.momentum;
+    a.lr = P<const float>(p.lr);
+    a.step = P<long long>(p.step);
+    if (!role) {  // the FC bucket in this launch (fc_sgd_rounds 0)
+      a.fc_end = p.bucket1;
+      a.w1b = fc.w1b;
+      a.w1t = fc.w1t;
+      a.off_w1fc = fc.w1;
+    }
+    a.off_w2 = (int)p.off_w2;
+    a.off_b2 = (int)p.off_b2;
+    a.off_w1 = (int)p.off_w1;
+    a.off_b1 = (int)p.off_b1;
+    a.part2 = P<const float>(p.part2);
+    a.ngroups = conv2_groups();
+    a.part1 = P<const float>(p.part1);
+    a.nblk1 = conv1_blocks();
+    if (p.wino) {
+      a.wino_u = P<float>(p.wino_u);
+      a.wino_ud = P<float>(p.wino_ud);
+    }
+    if (p.bf16) {
+      a.w2tb = P<uint16_t>(p.w2tb);
+      a.w2b = P<uint16_t>(p.w2b);
+    }
+    mnist::launch_sgd_step(a, s);
     return;
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
@@ -307,8 +377,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
     return;
   }
   const MnistPtrs& p = p_;
-  float* G = P<float>(p.grads);
-  enqueue_fwd_bwd(s);
+  const bool fused = fused_sgd_ok();
+  // fused: this step's single SGD launch writes the next step's derived
+  // weights, so the forward reads them as they are (one launch fewer)
+  enqueue_fwd_bwd(s, true, nullptr, false, fused);
   // size-1 comms are allowed (they exercise the capture path on one GPU)
   const float gscale = 1.0f / (float)comm->size();
   // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1 backward is done;
@@ -321,6 +393,14 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
   reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
   HIP_CHECK(hipEventRecord(ev_done_, cs));
+  if (fused) {
+    // ONE join: bucket 2 completes after bucket 1 on the ordered comm stream,
+    // and one SGD launch updates every parameter (a cross-queue wait costs
+    // ~10 us of idle queue in graph replay whether or not its event is done)
+    HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+    sgd_step(s, gscale, true, true);
+    return;
+  }
   // FC update while bucket 2 is in flight, then the conv update
   HIP_CHECK(hipStreamWaitEvent(s, ev_b1_, 0));
   sgd_range(s, 0, p.bucket1, gscale, false);
@@ -338,6 +418,8 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
 // but the FC momentum / SGD traffic drops by N and the all-gather half of the
 // FC collective overlaps the next forward instead of extending this step.
 // The FC momentum is sharded: gather_optimizer_state() before reading it.
+// bf16: the shard update cannot write the fc1 shadows (64 x 64 tiles), so the
+// next step's conv1 launch re-derives the shadows (fresh = false).
 void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs) {
   const MnistPtrs& p = p_;
   float* G = P<float>(p.grads);
@@ -345,7 +427,8 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
   const int n = comm->size();
   const float gscale = 1.0f / (float)n;
   const long long chunk = p.bucket1 / n, lo = chunk * comm->rank();
-  enqueue_fwd_bwd(s);
+  const bool fused = fused_sgd_ok();
+  enqueue_fwd_bwd(s, true, nullptr, false, fused && !p.bf16);
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
   if (p.grad_bf16) {  // bf16 wire: the shard comes back to fp32 before its SGD
     uint16_t* Gb = P<uint16_t>(p.gb16);
@@ -364,7 +447,10 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   fc_pending_ = true;
   HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
-  sgd_range(s, p.bucket1, p.total, gscale, true);
+  if (fused)
+    sgd_step(s, gscale, false, true);
+  else
+    sgd_range(s, p.bucket1, p.total, gscale, true);
 }
 
 // Split schedule: ONE fork and ONE join per step.  The FC all-reduce and the
@@ -377,17 +463,24 @@ void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_
                                      Collective* comm2) {
   const MnistPtrs& p = p_;
   const float gscale = 1.0f / (float)comm->size();
-  enqueue_fwd_bwd(s);
+  const bool fused = fused_sgd_ok();
+  enqueue_fwd_bwd(s, true, nullptr, false, fused);
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
   reduce_bucket(comm, 0, p.bucket1, cs);
-  sgd_range(cs, 0, p.bucket1, gscale, false);
+  if (fused)
+    sgd_step(cs, gscale, true, false);  // + the bf16 fc1 shadows
+  else
+    sgd_range(cs, 0, p.bucket1, gscale, false);
   HIP_CHECK(hipEventRecord(ev_b1_, cs));
   fc_pending_ = true;
   // host-progress communicators block a runtime thread per exchange: every
   // rank must reach the FC exchange before the conv exchange (collective.h)
   if (comm->host_progress() || comm2->host_progress()) wait_fc_params(s);
   reduce_bucket(comm2, p.bucket1, p.total - p.bucket1, s);
-  sgd_range(s, p.bucket1, p.total, gscale, true);
+  if (fused)
+    sgd_step(s, gscale, false, true);
+  else
+    sgd_range(s, p.bucket1, p.total, gscale, true);
 }
 
 // Factor schedule (sufficient-factor exchange).  The FC gradients of a batch
@@ -414,7 +507,8 @@ void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStrea
   const int n = comm->size(), r = comm->rank();
   const size_t B = (size_t)p.batch;
   const float gscale = 1.0f / (float)n;
-  enqueue_fwd_bwd(s, /*finalize=*/true, nullptr, /*factors=*/true);
+  const bool fused = fused_sgd_ok();
+  enqueue_fwd_bwd(s, /*finalize=*/true, nullptr, /*factors=*/true, fused);
   HIP_CHECK(hipStreamWaitEvent(cs, ev_fac_, 0));
   float* a2 = P<float>(p.a2_all);
   float* dh = P<float>(p.dh_all);
@@ -438,7 +532,10 @@ void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStrea
   mnist::launch_fc1_bwd_weights(a2, dh, hd, dl, n * p.batch, G + p.off_w3, G + p.off_b3,
                                 G + p.off_w4, G + p.off_b4, s);
   HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
-  sgd_range(s, 0, p.total, gscale, true);
+  if (fused)
+    sgd_step(s, gscale, true, true);
+  else
+    sgd_range(s, 0, p.total, gscale, true);
 }
 
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {

@@ -145,12 +145,18 @@ class MnistExecutor {
   // factors: record ev_fac_ once the FC factors are written (after the head)
   // and compute only dX in fc1 backward (the FC weight grads come from the
   // gathered factors)
-  // wino_fresh: the Winograd filter transforms are already current (the
-  // single-rank step writes them from its SGD); otherwise they are derived
-  // from the weights by a launch at the start of the step
+  // fresh: the derived weights (Winograd filter transforms; bf16 shadows) are
+  // already current - the previous step's SGD launch wrote them (sgd_step,
+  // launch_sgd_step); otherwise the step derives them from the weights first
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
                        const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
-                       bool wino_fresh = false);
+                       bool fresh = false);
+  // the fused SGD launch applies (L2 prefix == the FC bucket, as in the
+  // reference layout)
+  bool fused_sgd_ok() const;
+  // world > 1: the fused SGD launch over the all-reduced flat grads (FC
+  // bucket and / or conv parameters), writing the next step's derived weights
+  void sgd_step(hipStream_t s, float gscale, bool fc, bool conv);
   int conv1_blocks() const;
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);

@@ -243,12 +243,13 @@ bool ShmComm::barrier() {
 }
 
 void ShmComm::host_fn(void* arg) {
-  const Op* d = static_cast<const Op*>(arg);
+  Op* d = static_cast<Op*>(arg);
   try {
     d->comm->exchange(*d);
   } catch (...) {
     d->comm->fail(ncclInternalError, "exception in the host exchange");
   }
+  if (d->owned) delete d;  // an eager launch runs exactly once
 }
 
 // Runs on the HIP runtime's host-function thread, in stream order between
@@ -351,12 +352,21 @@ void ShmComm::enqueue(int kind, const void* send, void* recv, size_t count, int 
   if (!pinned_) throw std::runtime_error("ShmComm: a host-only communicator has no stream path");
   auto d = make_op(kind, send, recv, count, dtype, op, root);
   if (count == 0) return;
-  if (d->in_bytes)
-    HIP_CHECK(hipMemcpyAsync(send_stage_, send, d->in_bytes, hipMemcpyDeviceToHost, s));
-  HIP_CHECK(hipLaunchHostFunc(s, &ShmComm::host_fn, d.get()));
-  if (d->out_bytes)
-    HIP_CHECK(hipMemcpyAsync(recv, recv_stage_, d->out_bytes, hipMemcpyHostToDevice, s));
-  ops_.push_back(std::move(d));
+  // a captured op is replayed by every launch of its graph and lives as long
+  // as the communicator; an eager one is freed by its host function
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_CHECK(hipStreamIsCapturing(s, &cap));
+  d->owned = cap == hipStreamCaptureStatusNone;
+  const size_t in_bytes = d->in_bytes, out_bytes = d->out_bytes;
+  if (in_bytes) HIP_CHECK(hipMemcpyAsync(send_stage_, send, in_bytes, hipMemcpyDeviceToHost, s));
+  Op* raw = d.get();
+  if (d->owned)
+    d.release();  // from here on the host function owns it
+  else
+    ops_.push_back(std::move(d));
+  HIP_CHECK(hipLaunchHostFunc(s, &ShmComm::host_fn, raw));
+  if (out_bytes)
+    HIP_CHECK(hipMemcpyAsync(recv, recv_stage_, out_bytes, hipMemcpyHostToDevice, s));
 }
 
 void ShmComm::run_host(int kind, const void* send, void* recv, size_t count, int dtype, int op,

@@ -91,6 +91,7 @@ class ShmComm : public Collective {
     size_t count;     // elements: AR/RD/BC count, AG send count, RS recv count
     size_t in_bytes;  // bytes this rank contributes (0: none)
     size_t out_bytes; // bytes this rank receives (0: none)
+    bool owned = false;  // eager launch: the host function frees the op
   };
 
  private:
@@ -115,7 +116,7 @@ class ShmComm : public Collective {
   bool pinned_ = true;
   void* send_stage_ = nullptr;  // pinned, cap_ bytes
   void* recv_stage_ = nullptr;  // pinned, nranks_ * cap_ bytes
-  std::deque<std::unique_ptr<Op>> ops_;  // kept alive for captured graphs
+  std::deque<std::unique_ptr<Op>> ops_;  // ops of captured graphs (replayed later)
   unsigned long long seq_ = 0;           // host-function side sequence number
   std::atomic<int> err_{0};
   std::atomic<long long> done_{0};

@@ -405,22 +405,59 @@ def _all_ranks_ok(ok: bool, world: int) -> bool:
 def ranks_share_gpus(di: DistInfo) -> bool:
     """True when this node runs more ranks than it has GPUs (each rank binds
     local_rank % device_count, parallel/dist.py), so RCCL cannot be used.
-    Decided from environment data only, identically on every rank."""
+    Decided from environment data only (no collective)."""
     ndev = torch.cuda.device_count()  # does not initialise HIP on this image
     return ndev > 0 and di.local_world > ndev
+
+
+def _host_key() -> int:
+    import hashlib
+    import socket
+
+    h = hashlib.sha1(socket.gethostname().encode()).digest()
+    return int.from_bytes(h[:7], "little")  # fits an int64
+
+
+def _auto_vote(di: DistInfo) -> tuple:
+    """Collective (gloo) facts for comm="auto": (any rank shares its GPU,
+    every rank runs on one host).  Every rank takes the same decision, so no
+    rank enters a communicator whose set-up collectives the others skip."""
+    share = ranks_share_gpus(di)
+    if di.world <= 1 or not dist.is_initialized():
+        return share, True
+    key = _host_key()
+    t = torch.tensor([1 if share else 0, key, -key], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t[0].item()), int(t[1].item()) == -int(t[2].item())
 
 
 def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto",
               shm_capacity: int = DEFAULT_SHM_CAPACITY,
               timeout_s: float = 300.0) -> Optional[DeviceComm]:
     """Communicator for `device`, or None at world size 1.  prefer: auto |
-    rccl (alias native) | shm | torch (TrainConfig.comm)."""
+    rccl (alias native) | shm | torch (TrainConfig.comm).
+
+    auto on GPUs: native RCCL when every rank has a GPU of its own; when any
+    rank shares its GPU (more local ranks than GPUs: RCCL refuses two ranks
+    on one device) the shared-memory communicator if all ranks are on ONE
+    host (its segment is node-local), else torch.distributed.  The choice is
+    a gloo vote, and a failed shared-memory set-up falls back to
+    torch.distributed on every rank."""
     if di.world <= 1:
         return None
-    if device.type == "cuda" and (prefer == "shm" or (prefer == "auto" and ranks_share_gpus(di))):
-        return ShmDeviceComm(di, shm_capacity, timeout_s)
     if prefer == "rccl":
         prefer = "native"
+    if device.type == "cuda" and prefer == "shm":
+        return ShmDeviceComm(di, shm_capacity, timeout_s)
+    if device.type == "cuda" and prefer == "auto":
+        share, one_host = _auto_vote(di)
+        if share:
+            if one_host:
+                try:  # the constructor votes: every rank raises or none does
+                    return ShmDeviceComm(di, shm_capacity, timeout_s)
+                except RuntimeError as e:
+                    print(f"[rank {di.rank}] {e}; using torch.distributed", flush=True)
+            return TorchDeviceComm(di, device)
     if device.type == "cuda" and prefer in ("auto", "native"):
         try:  # every rank takes the same branch: RcclDeviceComm votes first
             return RcclDeviceComm(di)

@@ -42,13 +42,17 @@ from ..utils.profiling import SegmentTimer
 
 
 def comm_capacity_bytes(cfg: C.TrainConfig) -> int:
-    """Largest per-rank contribution of one collective of this model's step
-    (the whole flat fp32 gradient / parameter buffer), rounded up to 1 MiB:
-    the capacity a shared-memory communicator needs."""
+    """Largest per-rank contribution of one collective of this model's step,
+    rounded up to 1 MiB: the capacity a shared-memory communicator needs.
+    That is the whole flat fp32 gradient / parameter buffer, or for the MNIST
+    factor schedule (csrc/mnist_executor.cpp train_step_factors) one rank's
+    FC-factor slice a2 / dh / hd / dlog, B x (3136 + 2 x 512 + 10) floats,
+    when that is larger (B > ~400)."""
     if cfg.model == "mnist_cnn":
         from ..models import mnist_cnn as M
 
         total = M.layout().total
+        total = max(total, cfg.batch_size * (M.FC1_IN + 2 * M.FC1_OUT + 10))
     else:
         from ..models.generic import make_model
 
@@ -200,10 +204,11 @@ class Trainer:
         off = batch_offset(self.engine.step, sh.train_x.shape[0], self.cfg.batch_size)
         return self.eval_prediction(sh.train_x[off:off + self.cfg.batch_size], dropout=True)
 
-    def check_replicas(self, step: int) -> None:
+    def check_replicas(self, step: int, averaged: bool = False) -> None:
         """All ranks must hold bit-identical weights under per-step gradient
-        all-reduce; a mismatch means a lost / corrupted collective."""
-        if self.world <= 1 or self.cfg.sync != "grad":
+        all-reduce, and right after an all-ranks parameter average
+        (`averaged`); a mismatch means a lost / corrupted collective."""
+        if self.world <= 1 or (self.cfg.sync != "grad" and not averaged):
             return
         if not replicas_identical(self.engine.params):
             raise RuntimeError(f"replicas diverged at step {step}: the bitwise weight "
@@ -276,6 +281,8 @@ class Trainer:
                         average_params(self.comm, eng.params)
                     self._sync()
                 train_t += time.perf_counter() - t2
+                if cfg.check_replicas and not cfg.root_only_average:
+                    self.check_replicas(last, averaged=True)
             if cfg.ckpt and cfg.ckpt_every and last % cfg.ckpt_every == 0:
                 self.save_checkpoint(cfg.ckpt)
         if cfg.check_replicas:

@@ -129,8 +129,8 @@ def test_forward_backward_grads_match_oracle(cuda_dev, data, batch):
         assert err < 2e-4, (s.name, err)
 
 
-@pytest.mark.parametrize("algo,max_ties", [("direct", 2), ("winograd", 4)])
-def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties):
+@pytest.mark.parametrize("algo,max_ties,tie_err", [("direct", 2, 5e-3), ("winograd", 4, 1e-2)])
+def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties, tie_err):
     """Strict per-step check: at every step the native grads equal the oracle's
     grads evaluated at the NATIVE parameters (no chaotic accumulation).  The
     Winograd conv2 rounds differently from the oracle's direct sum (~1.4e-6
@@ -150,8 +150,9 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties):
         print(step, {k: f"{v:.1e}" for k, v in errs.items()})
         # a max-pool near-tie (fp32 summation order) can re-route a single
         # element of dY2 / dA1, which shifts the conv grads (never the FC
-        # grads) by ~1e-3 .. 5e-3; everything else must agree to fp32 rounding
-        assert max(errs.values()) < 1e-2, (step, errs)
+        # grads) by ~1e-3 .. 5e-3 (Winograd rounding: up to 1e-2); everything
+        # else must agree to fp32 rounding
+        assert max(errs.values()) < tie_err, (step, errs)
         assert max(v for k, v in errs.items() if k.startswith("fc")) < 1e-4, (step, errs)
         if max(errs.values()) > 1e-4:
             ties += 1
