@@ -322,6 +322,19 @@ PYBIND11_MODULE(_C, m) {
     return gops::conv_fwd_tiled_ok(s) || gops::conv_fwd_tiled_gather_ok(s);
   });
   g.def("conv_bwd_data_join_ok", &gops::conv_bwd_data_join_ok);
+  // tiled-family tile / split plan (labs only; production runs the defaults)
+  py::class_<gops::TiledPlan>(g, "TiledPlan")
+      .def(py::init<>())
+      .def_readwrite("m128_min_bf16", &gops::TiledPlan::m128_min_bf16)
+      .def_readwrite("m128_min_f32", &gops::TiledPlan::m128_min_f32)
+      .def_readwrite("ksplit_target", &gops::TiledPlan::ksplit_target)
+      .def_readwrite("wgsplit_target", &gops::TiledPlan::wgsplit_target)
+      .def_readwrite("gcap", &gops::TiledPlan::gcap)
+      .def_readwrite("vcap", &gops::TiledPlan::vcap)
+      .def_readwrite("dgrad_fwd", &gops::TiledPlan::dgrad_fwd)
+      .def_readwrite("wg64", &gops::TiledPlan::wg64);
+  g.def("get_tiled_plan", []() { return gops::tiled_plan(); });
+  g.def("set_tiled_plan", [](const gops::TiledPlan& p) { gops::tiled_plan() = p; });
   g.def("im2col_bf16", [](const gops::ConvShape& s, uintptr_t x, int kp, uintptr_t col,
                           uintptr_t st) {
     gops::im2col_bf16(s, P<const float>(x), kp, P<void>(col), S(st));

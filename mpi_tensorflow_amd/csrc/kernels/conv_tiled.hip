@@ -891,14 +891,9 @@ enum Tile { T128x128, T128x64, T64x128, T64x64 };
 // 128-row tiles only with >= 256 blocks of them (bf16).  fp32 never: on the
 // ResNet-18 56x56 layers (M = 100352) 64-row tiles measured 116.4 -> 103.8 us
 // forward and 145.5 -> 129.0 us dgrad (the 128x64 grid, 784 blocks, overran
-// the 768 resident slots by 16).  MTA_TILED_M128 overrides both (experiments).
+// the 768 resident slots by 16).  (TiledPlan m128_min_*)
 static inline long long m128_min(bool bf16) {
-  static const long long v = [] {
-    const char* e = getenv("MTA_TILED_M128");
-    return e ? atoll(e) : -1LL;
-  }();
-  if (v >= 0) return v;
-  return bf16 ? 128LL * 256 : (1LL << 62);
+  return bf16 ? tiled_plan().m128_min_bf16 : tiled_plan().m128_min_f32;
 }
 // narrow: 64-column tiles even for N > 64 (fp32 stride-2 dgrad and 1x1 stride-2
 // forward of ResNet-18: 99.0 -> 84.0 / 33.3 -> 20.0 us dgrad at 128 channels,
@@ -926,6 +921,11 @@ static inline Tile pick(long long M, int N, bool bf16, bool narrow = false) {
 
 }  // namespace tiled
 
+TiledPlan& tiled_plan() {
+  static TiledPlan plan;
+  return plan;
+}
+
 bool conv_fwd_tiled_ok(const ConvShape& s) { return s.C % 32 == 0 && s.K % 4 == 0; }
 // the gather-loader forward: thin inputs with a reduction axis of >= 2 K tiles
 // (the ResNet stem); smaller ones stay on the direct / gather engines
@@ -939,20 +939,10 @@ namespace tiled {
 static inline int tile_m(Tile t) { return (t == T128x128 || t == T128x64) ? 128 : 64; }
 static inline int tile_n(Tile t) { return (t == T128x128 || t == T64x128) ? 128 : 64; }
 
-// split targets (blocks to aim for), overridable for plan experiments:
-// MTA_TILED_KSPLIT (forward / dgrad, default 1024), MTA_TILED_WGSPLIT (filter, 2048)
-static inline int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-static inline int ksplit_target() {
-  static const int v = env_int("MTA_TILED_KSPLIT", 1024);
-  return v;
-}
-static inline int wgsplit_target() {
-  static const int v = env_int("MTA_TILED_WGSPLIT", 2048);
-  return v;
-}
+// split targets (blocks to aim for): TiledPlan ksplit_target (forward / dgrad)
+// and wgsplit_target (filter gradient)
+static inline int ksplit_target() { return tiled_plan().ksplit_target; }
+static inline int wgsplit_target() { return tiled_plan().wgsplit_target; }
 // split-K factor for a GEMM with `blocks` output tiles of nk K tiles each:
 // deep layers (few tiles, long K) get enough blocks to fill 256 CUs twice
 static inline int ksplit(long long blocks, int nk) {
@@ -1003,13 +993,9 @@ static inline void slab_sum(const float* part, int z, long long n, float* out, h
 
 // fp32 stride-1 dgrad through the forward kernel (see wflip_kernel): the
 // forward shape over dY and the floats of the flipped weight ahead of its
-// split-K workspace.  MTA_TILED_DGRAD_FWD=0: the phase-decomposed dgrad
+// split-K workspace.  TiledPlan dgrad_fwd = false: the phase-decomposed dgrad
 static bool dgrad_fwd_ok(const ConvShape& s) {
-  static const bool on = [] {
-    const char* e = getenv("MTA_TILED_DGRAD_FWD");
-    return !(e && e[0] == '0');
-  }();
-  return on && s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 && 2 * s.pad == s.R - 1 &&
+  return tiled_plan().dgrad_fwd && s.stride == 1 && s.R == s.S && s.pad <= s.R - 1 && 2 * s.pad == s.R - 1 &&
          s.K % tiled::BK == 0 && s.C % 4 == 0 && s.OH == s.H && s.OW == s.W;
 }
 static ConvShape dgrad_fwd_shape(const ConvShape& s) {
@@ -1141,12 +1127,8 @@ static inline Tile filter_tile(const ConvShape& s) {  // ci x co tiles
   // 64-wide ci tiles: ResNet-18 fp32 filter gradients 136 -> 122 (28x28), 112 -> 103
   // (14x14), 116 -> 102 us (7x7), step 6.96 -> 6.78 ms; twice the tiles, so half
   // the split-K slices (the bf16 models take the conv_bf16 filter kernels).
-  // MTA_TILED_WG64=0: 128-wide ci tiles from C >= 128 (the old plan)
-  static const bool wg64 = [] {
-    const char* e = getenv("MTA_TILED_WG64");
-    return !(e && e[0] == '0');
-  }();
-  const bool bm = s.C >= 128 && !wg64, bn = s.K > 64;
+  // TiledPlan wg64 = false: 128-wide ci tiles from C >= 128 (the old plan)
+  const bool bm = s.C >= 128 && !tiled_plan().wg64, bn = s.K > 64;
   return bm ? (bn ? T128x128 : T128x64) : (bn ? T64x128 : T64x64);
 }
 static inline int filter_blocks_per_split(const ConvShape& s) {
@@ -1169,11 +1151,11 @@ int conv_filter_tiled_splits(const ConvShape& s) {
   if (z > ktiles) z = ktiles;
   // gather-path slice cap: the ResNet stem's filter gradient (3 tiles of 64 x 64,
   // 12544 K tiles) went 271 -> 197 us from 128 to 256 slices (512: 196, 1024: 198)
-  static const int gcap = env_int("MTA_TILED_GCAP", 256);
-  // vector-path slice cap (MTA_TILED_VCAP).  conv_lab fp32: the 56x56x64 filter
+  const int gcap = tiled_plan().gcap;
+  // vector-path slice cap (TiledPlan vcap).  conv_lab fp32: the 56x56x64 filter
   // gradient (9 tiles) 152.5 -> 129.0 -> 117.2 us at caps 64 -> 128 -> 256 (all
   // layers 2120 -> 1984 / 2021 us); not yet verified in a full step, so 64 stays
-  static const int vcap = env_int("MTA_TILED_VCAP", 64);
+  const int vcap = tiled_plan().vcap;
   if (z > (vec ? vcap : gcap)) z = vec ? vcap : gcap;
   const int kchunk = cdiv(ktiles, z);
   return cdiv(ktiles, kchunk);  // splits actually launched

@@ -2108,12 +2108,7 @@ void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch,
   const int G = conv2_wino_filter_groups(batch);
   const C1Filter c = c1_args(c1);
   const int n1 = c.part1 ? conv1_filter_blocks(batch, 1) : 0;
-  // MTA_WF_PAD (bytes of extra dynamic LDS): placement experiments only
-  static const int pad = [] {
-    const char* e = getenv("MTA_WF_PAD");
-    return e ? atoi(e) : 0;
-  }();
-  conv2_bwd_filter_wino_kernel<false><<<8 * G + n1, WF_NT, pad, s>>>(
+  conv2_bwd_filter_wino_kernel<false><<<8 * G + n1, WF_NT, 0, s>>>(
       batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, c, nullptr);
 }
 

@@ -115,6 +115,20 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
                          hipStream_t st, bool bf16, const float* addend = nullptr,
                          const void* dyb = nullptr);
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
+// Tile / split plan of the tiled family.  Production runs the defaults (the
+// measured choices, docs/PERF_NOTES.md); labs (scripts/conv_lab.py) change
+// them through the binding before building workspaces, never per call.
+struct TiledPlan {
+  long long m128_min_bf16 = 128LL * 256;  // 128-row tiles from M >= this (bf16)
+  long long m128_min_f32 = 1LL << 62;     // fp32: never (64-row tiles measured faster)
+  int ksplit_target = 1024;               // forward / dgrad split-K: blocks to aim for
+  int wgsplit_target = 2048;              // filter gradient: blocks to aim for
+  int gcap = 256;                         // filter gradient slice cap, gather path
+  int vcap = 64;                          // filter gradient slice cap, vector path
+  bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
+  bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
+};
+TiledPlan& tiled_plan();
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
 int conv_filter_tiled_splits(const ConvShape& s);
 void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,

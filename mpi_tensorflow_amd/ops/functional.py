@@ -22,7 +22,6 @@ the reference uses for its TF variables, /root/reference/mpipy.py:38-53).
 from __future__ import annotations
 
 import dataclasses
-import os
 from typing import Optional
 
 import torch
@@ -173,17 +172,32 @@ def _bnstats(t: torch.Tensor, rmean: torch.Tensor):
 # for the ReLU mask, mean, rstd); the consuming conv's backward passes it to
 # its dgrad, whose epilogue writes the partial table, attached to the dX it
 # returns; the BatchNorm backward then skips its statistics pass.
-BN_BWD_STATS = {"epilogue": 0, "pass": 0}  # BatchNorm backward counts by route
-# A/B switches for the BatchNorm statistics epilogues (labs / profiles):
-# MTA_BN_FWD_EPILOGUE=0 / MTA_BN_BWD_EPILOGUE=0 fall back to the statistics passes
-_BNB_EPILOGUE = os.environ.get("MTA_BN_BWD_EPILOGUE", "1") != "0"
-BN_FWD_EPILOGUE = os.environ.get("MTA_BN_FWD_EPILOGUE", "1") != "0"
+# A/B switches of the BatchNorm statistics epilogues (set by tests and labs
+# through the setters below; production runs the defaults)
+_BNB_EPILOGUE = True
+BN_FWD_EPILOGUE = True
 # fp32 conv mode: the tiled forward's epilogue / split-K reduction can write
-# them too.  Off by default (MTA_BN_FWD_F32=1 / set_bn_fwd_f32 turn it on):
-# ResNet-18 fp32 B=32 measured 6.655 / 6.666 ms on vs 6.641 / 6.646 off - the
-# 64-row fp32 tiles give P = 2 x M / 64 partial rows, and the finalize's
-# strided reads of that table cost what the skipped statistics pass saved
-_BN_FWD_F32 = os.environ.get("MTA_BN_FWD_F32", "0") == "1"
+# them too.  Off by default (set_bn_fwd_f32 turns it on): ResNet-18 fp32 B=32
+# measured 6.655 / 6.666 ms on vs 6.641 / 6.646 off - the 64-row fp32 tiles
+# give P = 2 x M / 64 partial rows, and the finalize's strided reads of that
+# table cost what the skipped statistics pass saved
+_BN_FWD_F32 = False
+# observer of the BatchNorm backward route ("epilogue" | "pass"), for tests
+_BN_ROUTE_HOOK = None
+
+
+def set_bn_route_hook(fn) -> None:
+    """fn(route) is called by every BatchNorm backward with the statistics
+    route it took: "epilogue" (a dgrad wrote the sums) or "pass"."""
+    global _BN_ROUTE_HOOK
+    _BN_ROUTE_HOOK = fn
+
+
+def set_bn_fwd_epilogue(on: bool) -> None:
+    """Let bf16 conv epilogues write the BatchNorm forward statistics
+    (default on; off = the BatchNorm's own statistics pass)."""
+    global BN_FWD_EPILOGUE
+    BN_FWD_EPILOGUE = bool(on)
 
 
 def set_bn_fwd_f32(on: bool) -> None:
@@ -320,14 +334,6 @@ class _ConvFn(torch.autograd.Function):
                                         ptr(add), ptr(ctx.wtb_d), ptr(part), prow, ptr(bx),
                                         ptr(byb), ptr(bmean), ptr(brstd), brelu)
                     _attach_bnbwd_stats(dx, part, prow, bmean)
-                    if os.environ.get("MTA_BNB_CHECK") == "1":  # debug: dX vs the plain dgrad
-                        dx2 = torch.empty_like(dx)
-                        C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx2), ptr(ctx.ws), s, True,
-                                            ptr(dyb), ptr(add), ptr(ctx.wtb_d))
-                        e = ((dx2 - dx).norm() / dx2.norm().clamp_min(1e-12)).item()
-                        print(f"BNB_CHECK dgrad N={sh.N} H={sh.H} C={sh.C} K={sh.K} "
-                              f"R={sh.R} s={sh.stride} add={add is not None} dx_err={e:.2e}",
-                              flush=True)
                 else:
                     C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
                                         ptr(add), ptr(ctx.wtb_d))
@@ -618,28 +624,13 @@ class _BNFn(torch.autograd.Function):
             dx = torch.empty_like(dy)
             dxf, dxb = dx, _bf16_out(dx)
         st = _bnbwd_stats(dy, mean) if (xb16 and (ctx.yb16 or not ctx.relu)) else None
-        if st is not None and os.environ.get("MTA_BNB_IGNORE") == "1":  # debug: pass anyway
-            st = None
-        if st is not None and os.environ.get("MTA_BNB_CHECK") == "1":  # debug: vs the pass
-            db0 = torch.empty(Cc, device=x.device)
-            dg0 = torch.empty(Cc, device=x.device)
-            part, prow = st
-            C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc,
-                         ctx.relu, ptr(ctx.ws), ptr(dg0), ptr(db0), 0, 0, stream_handle(),
-                         ptr(torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)), xb16,
-                         ctx.yb16)
-            t = part.view(2, Cc // 64, prow, 64).sum(2).reshape(2, Cc)
-            e1 = ((t[0] - db0).norm() / db0.norm().clamp_min(1e-12)).item()
-            e2 = ((t[1] - dg0).norm() / dg0.norm().clamp_min(1e-12)).item()
-            print(f"BNB_CHECK rows={rows} C={Cc} relu={ctx.relu} P={prow} "
-                  f"db_err={e1:.2e} dg_err={e2:.2e}", flush=True)
+        if _BN_ROUTE_HOOK is not None:
+            _BN_ROUTE_HOOK("epilogue" if st is not None else "pass")
         if st is not None:  # the dgrad producing dy wrote the sums (see above)
-            BN_BWD_STATS["epilogue"] += 1
             C.ops.bn_bwd_partials(ptr(st[0]), st[1], ptr(x), ptr(dy), ptr(y), ptr(mean),
                                   ptr(rstd), ptr(g), rows, Cc, ctx.relu, ptr(ctx.gg), ptr(ctx.gb),
                                   ptr(dxf), ptr(dres), stream_handle(), ptr(dxb))
         else:
-            BN_BWD_STATS["pass"] += 1
             C.ops.bn_bwd(ptr(x), ptr(dy), ptr(y), ptr(mean), ptr(rstd), ptr(g), rows, Cc,
                          ctx.relu, ptr(ctx.ws), ptr(ctx.gg), ptr(ctx.gb), ptr(dxf), ptr(dres),
                          stream_handle(), ptr(dxb), xb16, ctx.yb16)

@@ -1,6 +1,9 @@
 """Times the generic conv ops (forward / backward-data / backward-filter) on
 every distinct ResNet-18 layer shape at batch B, per op and per layer.
-    python scripts/conv_lab.py [--batch 32] [--dtype bf16] [--reps 20]"""
+    python scripts/conv_lab.py [--batch 32] [--dtype bf16] [--reps 20]
+        [--plan vcap=128,ksplit_target=2048,...]
+--plan sets fields of the tiled family's TiledPlan (csrc/kernels/ops_generic.h)
+for this run only; production always runs the defaults."""
 import argparse
 import os
 import sys
@@ -29,9 +32,17 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--layers", default=None, help="comma list of shape-table rows to run")
     ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--plan", default="", help="TiledPlan overrides, k=v comma list")
     a = ap.parse_args()
     C = native()
     g = C.ops
+    if a.plan:
+        plan = g.get_tiled_plan()
+        for kv in a.plan.split(","):
+            k, v = kv.split("=")
+            cur = getattr(plan, k)
+            setattr(plan, k, (v not in ("0", "false")) if isinstance(cur, bool) else int(v))
+        g.set_tiled_plan(plan)
     bf16 = a.dtype == "bf16"
     dev = torch.device("cuda:0")
     s = stream_handle()

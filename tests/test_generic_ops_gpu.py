@@ -646,19 +646,22 @@ def test_dgrad_epilogue_bn_backward_statistics(cuda_dev, N, H, Cin, K, stride, r
     out = []
     Fn.set_conv_bf16(True)
     try:
+        routes = []
+        Fn.set_bn_route_hook(routes.append)
         for fused in (False, True):
             Fn.set_bn_bwd_epilogue(fused)
-            n0 = Fn.BN_BWD_STATS["epilogue"]
+            n0 = routes.count("epilogue")
             xi = x.clone().requires_grad_(True)
             gp, bp, wp = _param(gam), _param(bet), _param(w)
             rm, rv = torch.zeros(Cin, device=cuda_dev), torch.ones(Cin, device=cuda_dev)
             h = Fn.batchnorm(xi, gp, bp, rm, rv, True, relu)
             y = Fn.conv2d(h, wp, None, stride, 1, False, out_bf16=True)
             y.backward(dy)
-            assert Fn.BN_BWD_STATS["epilogue"] - n0 == (1 if fused else 0)
+            assert routes.count("epilogue") - n0 == (1 if fused else 0)
             out.append((xi.grad.float().clone(), gp.grad_view.clone(), bp.grad_view.clone(),
                         wp.grad_view.clone()))
     finally:
+        Fn.set_bn_route_hook(None)
         Fn.set_bn_bwd_epilogue(True)
         Fn.set_conv_bf16(False)
     torch.cuda.synchronize()
@@ -789,25 +792,27 @@ def test_resnet18_bn_backward_epilogue_matches_pass(cuda_dev, shape, B):
 
     x, y = synthetic_rows("train", 0, 4 * B, shape=shape)
     grads, counts = [], []
+    routes = []
+    Fn.set_bn_route_hook(routes.append)
     try:
         for on in ROUTES:
             Fn.set_bn_bwd_epilogue(on)
             eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=B, dtype="bf16",
                                               graph=False).validate(), x, y, cuda_dev)
-            n0 = Fn.BN_BWD_STATS["epilogue"]
+            n0 = routes.count("epilogue")
             eng.forward_backward_gpu()
             torch.cuda.synchronize()
-            counts.append(Fn.BN_BWD_STATS["epilogue"] - n0)
+            counts.append(routes.count("epilogue") - n0)
             grads.append({k: v.clone() for k, v in eng.layout.views(eng.grads).items()})
     finally:
+        Fn.set_bn_route_hook(None)
         Fn.set_bn_bwd_epilogue(True)
     assert all((c >= 12) == on for c, on in zip(counts, ROUTES)), counts
     errs = {k: _rel(grads[1][k], grads[0][k]) for k in grads[0]}
     # the head and the last block see the two routes' sums only through fp32
     # rounding (~1e-7); every BatchNorm further down the backward writes a bf16
     # dX, where such a difference flips the rounding of single elements (2^-8
-    # relative), so the gap grows layer by layer (~1e-2 at the stem,
-    # scripts/bnb_route_diff.py) without either route being wrong
+    # relative), so the gap grows layer by layer (~1e-2 at the stem) without either route being wrong
     head = {k: v for k, v in errs.items() if k.startswith(("fc_", "l4b1n2", "l4b1c2", "l4b1n1"))}
     assert max(head.values()) < 1e-5, head
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
