@@ -105,6 +105,26 @@ _GRAD_HOOK = None
 _UNIT_SEED = False
 
 
+# Oracle mode: every op takes its plain-PyTorch path (torch.nn.functional,
+# autograd) even for GPU tensors - the GPU-resident numerics reference of the
+# native kernels over whole training runs (GenericEngine oracle=True)
+_ORACLE = False
+
+
+class oracle_mode:
+    """Context manager: the ops run their PyTorch definitions on any device."""
+
+    def __enter__(self):
+        global _ORACLE
+        self._prev, _ORACLE = _ORACLE, True
+        return self
+
+    def __exit__(self, *exc):
+        global _ORACLE
+        _ORACLE = self._prev
+        return False
+
+
 def set_unit_loss_seed(on: bool) -> None:
     global _UNIT_SEED
     _UNIT_SEED = bool(on)
@@ -492,7 +512,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
     only, ignored on the CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
-    if x.is_cuda:
+    if x.is_cuda and not _ORACLE:
         C = native()
         sh = C.ops.ConvShape(N, H, W, Cin, K, R, S, stride, pad)
         kp = _im2col_kp(sh, x, b is not None, relu)
@@ -557,7 +577,7 @@ class _LinearFn(torch.autograd.Function):
 
 def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) -> torch.Tensor:
     """x [N,in], w [in,out] -> [N,out]."""
-    if x.is_cuda:
+    if x.is_cuda and not _ORACLE:
         return _LinearFn.apply(x, w.value, None if b is None else b.value, relu, w.grad_view,
                                None if b is None else b.grad_view)
     y = x @ w.value + (0 if b is None else b.value)
@@ -652,7 +672,7 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
     returned to autograd.  twin_only: the output's only consumer is a bf16
     conv - write just its bf16 twin (bf16 conv mode; the returned fp32 tensor
     is not written).  Both GPU training only."""
-    if x.is_cuda:
+    if x.is_cuda and not _ORACLE:
         res = None if residual is None else residual.contiguous()
         if training:
             return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
@@ -674,7 +694,7 @@ def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: to
 def softmax(logits: torch.Tensor) -> torch.Tensor:
     """Row softmax of [M, N] logits (no autograd): the prediction heads.
     Native kernel on GPU, torch on the CPU oracle path."""
-    if not logits.is_cuda:
+    if not logits.is_cuda or _ORACLE:
         return torch.softmax(logits.float(), dim=1)
     x = logits.contiguous().float()
     y = torch.empty_like(x)
@@ -722,7 +742,7 @@ class _MaxPoolFn(torch.autograd.Function):
 
 
 def maxpool(x: torch.Tensor, k: int, stride: int, pad: int = 0) -> torch.Tensor:
-    if x.is_cuda:
+    if x.is_cuda and not _ORACLE:
         return _MaxPoolFn.apply(x, k, stride, pad)
     return F.max_pool2d(x.permute(0, 3, 1, 2), k, stride, pad).permute(0, 2, 3, 1)
 
@@ -748,7 +768,7 @@ class _AvgPoolFn(torch.autograd.Function):
 
 
 def global_avgpool(x: torch.Tensor) -> torch.Tensor:
-    if x.is_cuda:
+    if x.is_cuda and not _ORACLE:
         return _AvgPoolFn.apply(x)
     return x.mean(dim=(1, 2))
 
@@ -781,6 +801,6 @@ class _XentFn(torch.autograd.Function):
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     """mean softmax cross-entropy; labels int32 on GPU."""
-    if logits.is_cuda:
+    if logits.is_cuda and not _ORACLE:
         return _XentFn.apply(logits, labels.to(torch.int32))
     return F.cross_entropy(logits, labels.long())

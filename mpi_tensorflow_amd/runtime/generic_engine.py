@@ -45,14 +45,30 @@ from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
 
 
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
 class GenericEngine:
     kind = "generic"
 
     def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
                  device: torch.device, rank: int = 0, world: int = 1,
-                 comm: Optional[DeviceComm] = None, force_sync: bool = False):
+                 comm: Optional[DeviceComm] = None, force_sync: bool = False,
+                 oracle: bool = False):
+        """oracle: run the model through the PyTorch ops (F.conv2d,
+        F.batch_norm, autograd) on `device` - a GPU-resident fp32 reference
+        run of the same init, data and batch order (ops/functional.py
+        oracle_mode); always fp32, eager, unsynced."""
         self.cfg, self.device, self.rank, self.world, self.comm = cfg, device, rank, world, comm
+        self.oracle = bool(oracle)
         self.bf16 = cfg.dtype == "bf16"
+        if self.oracle and (self.bf16 or world > 1):
+            raise ValueError("the oracle engine is fp32 and single-rank")
         if self.bf16 and device.type != "cuda":
             raise NotImplementedError("dtype bf16 needs the GPU kernels (bf16 MFMA convolutions)")
         self.model = make_model(cfg.model)
@@ -78,7 +94,7 @@ class GenericEngine:
         self.grad_sync = cfg.sync == "grad" and world > 1 and comm is not None
         if force_sync and comm is not None:  # exercise the collective path at world 1
             self.grad_sync = True
-        self.on_gpu = device.type == "cuda"
+        self.on_gpu = device.type == "cuda" and not self.oracle
         self.wcache = None
         self.use_graph = cfg.graph and self.on_gpu
         self.graph_steps = max(1, cfg.graph_steps)
@@ -264,9 +280,10 @@ class GenericEngine:
         if k <= 0:
             return
         if not self.on_gpu:
-            for _ in range(k):
-                self._step_cpu()
-                self.step += 1
+            with Fn.oracle_mode() if self.oracle else _null():
+                for _ in range(k):
+                    self._step_cpu()
+                    self.step += 1
             return
         left = k - self._warmup(k)
         if not self.use_graph:
@@ -299,13 +316,14 @@ class GenericEngine:
         outs = []
         if not self.on_gpu:
             wrong = 0
-            for a in range(0, n, chunk):
-                xb = torch.from_numpy(np.ascontiguousarray(x[a:a + chunk], np.float32))
-                lg = self.model.forward(self.P, self.bn, xb, False)
-                if return_logits:
-                    outs.append(lg)
-                pred = lg.argmax(1).numpy()
-                wrong += int((pred != y[a:a + chunk]).sum())
+            with Fn.oracle_mode() if self.oracle else _null():
+                for a in range(0, n, chunk):
+                    xb = torch.from_numpy(np.ascontiguousarray(x[a:a + chunk], np.float32))
+                    lg = self.model.forward(self.P, self.bn, xb.to(self.device), False)
+                    if return_logits:
+                        outs.append(lg)
+                    pred = lg.argmax(1).cpu().numpy()
+                    wrong += int((pred != y[a:a + chunk]).sum())
             err = 100.0 * wrong / max(1, n)
             return (err, torch.cat(outs)) if return_logits else err
         # GPU: the test set is uploaded once and stays resident; the xent

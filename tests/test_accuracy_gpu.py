@@ -117,3 +117,59 @@ def test_resnet18_bf16_tracks_fp32_loss_curve(cuda_dev):
     assert curves["fp32"][-1] < 0.8 * curves["fp32"][0], "fp32 did not learn"
     assert gap <= RESNET_CURVE_TOL
     assert accs["fp32"] < 100.0 and accs["bf16"] < 100.0
+
+
+# ------------------------------------------- ResNet-18 vs a PyTorch oracle
+RESNET_ORACLE_STEPS = 600
+RESNET_ORACLE_ROWS, RESNET_ORACLE_TEST = 4096, 1024
+# held-out accuracy gap to the oracle, points
+RESNET_ORACLE_TOL = {"fp32": 1.5, "bf16": 2.5}
+
+
+@pytest.fixture(scope="module")
+def resnet_task(cuda_dev):
+    from mpi_tensorflow_amd.utils.data import synthetic_images_torch
+
+    tx, ty = synthetic_images_torch(RESNET_ORACLE_ROWS, (224, 224, 3), device=cuda_dev)
+    ex, ey = synthetic_images_torch(RESNET_ORACLE_TEST, (224, 224, 3), device=cuda_dev,
+                                    split="test")
+    return tx.cpu().numpy(), ty.numpy(), ex.cpu().numpy(), ey.numpy()
+
+
+def _resnet_run(cuda_dev, task, dtype, oracle=False):
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+
+    tx, ty, ex, ey = task
+    cfg = C.TrainConfig(model="resnet18", batch_size=32, dtype=dtype, graph=not oracle,
+                        graph_steps=25).validate()
+    e = GenericEngine(cfg, tx, ty, cuda_dev, oracle=oracle)
+    e.train(RESNET_ORACLE_STEPS)
+    torch.cuda.synchronize()
+    acc = 100.0 - e.evaluate(ex, ey)
+    loss = e.loss_value()
+    del e
+    torch.cuda.empty_cache()
+    return acc, loss
+
+
+@pytest.fixture(scope="module")
+def resnet_oracle_acc(cuda_dev, resnet_task):
+    acc, loss = _resnet_run(cuda_dev, resnet_task, "fp32", oracle=True)
+    print(f"resnet18 torch oracle (F.conv2d / F.batch_norm autograd, fp32): held-out "
+          f"{acc:.2f}% after {RESNET_ORACLE_STEPS} steps, last loss {loss:.3f}")
+    assert 40.0 < acc < 99.0, "task too easy / too hard to carry information"
+    return acc
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_resnet18_native_matches_torch_oracle_accuracy(cuda_dev, resnet_task, resnet_oracle_acc,
+                                                       dtype):
+    """ResNet-18 (BASELINE config 5): the native engine (fp32 tiled MFMA or
+    bf16 MFMA convs, fused BatchNorm statistics, hipGraph replay) trained
+    RESNET_ORACLE_STEPS steps at B = 32 on the v2 224x224x3 task lands within
+    RESNET_ORACLE_TOL points of held-out accuracy of a PyTorch-op oracle of
+    the same model (same init, data and batch order) run on the same GPU."""
+    acc, loss = _resnet_run(cuda_dev, resnet_task, dtype)
+    print(f"resnet18 native {dtype}: held-out {acc:.2f}% (oracle {resnet_oracle_acc:.2f}%), "
+          f"last loss {loss:.3f}")
+    assert abs(acc - resnet_oracle_acc) <= RESNET_ORACLE_TOL[dtype]
