@@ -189,3 +189,34 @@ def test_mpipy_torchrun_grad_sync_replicas_identical(tmp_path, model):
     summ = json.loads([l for l in out.splitlines() if l.startswith('{"summary"')][-1])["summary"]
     assert summ["world"] == 2 and summ["steps"] == 41 and summ["model"] == model
     assert summ["device_step_ms"] > 0
+
+
+def _worker_auto_vote(rank, world, port, out_dir, local_world):
+    _env(rank, world, port)
+    os.environ["LOCAL_WORLD_SIZE"] = str(local_world)
+    from unittest import mock
+
+    from mpi_tensorflow_amd.parallel import comm as CM
+    from mpi_tensorflow_amd.parallel import dist as D
+
+    di = D.init("cpu")
+    # pretend rank 1 sees one GPU while this host runs 2 local ranks; rank 0
+    # sees no GPU: the vote must still give every rank the same answer
+    ndev = 1 if rank == 1 else 0
+    with mock.patch.object(CM.torch.cuda, "device_count", return_value=ndev):
+        share, one_host = CM._auto_vote(di)
+    with mock.patch.object(CM, "_host_key", return_value=1000 + rank):
+        _, split_hosts = CM._auto_vote(di)
+    np.save(os.path.join(out_dir, f"v{rank}.npy"), np.array([share, one_host, split_hosts]))
+    D.shutdown()
+
+
+def test_auto_comm_choice_is_a_collective_vote(tmp_path):
+    """comm=auto: whether any rank shares its GPU and whether all ranks run
+    on one host are decided by a gloo vote, identically on every rank (a
+    rank-local decision could send ranks into different communicators'
+    set-up collectives and hang them)."""
+    port = _free_port()
+    mp.spawn(_worker_auto_vote, args=(2, port, str(tmp_path), 2), nprocs=2, join=True)
+    v0, v1 = np.load(tmp_path / "v0.npy"), np.load(tmp_path / "v1.npy")
+    assert v0.tolist() == v1.tolist() == [True, True, False]
