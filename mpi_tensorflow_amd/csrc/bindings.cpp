@@ -406,6 +406,15 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("wcvt_blocks", &gops::wcvt_blocks);
+  g.def("sgd_wcvt", [](uintptr_t w, uintptr_t gr, uintptr_t mom, float momentum, float gscale,
+                       float l2, uintptr_t lr, uintptr_t step, uintptr_t jobs, int njobs,
+                       long long conv_blocks, uintptr_t ranges, int nranges,
+                       long long range_blocks, uintptr_t st) {
+    gops::sgd_wcvt(P<float>(w), P<const float>(gr), P<float>(mom), momentum, gscale, l2,
+                   P<const float>(lr), P<long long>(step), P<const long long>(jobs), njobs,
+                   conv_blocks, P<const long long>(ranges), nranges, range_blocks, S(st));
+    check_launch();
+  });
   g.def("wcvt_batch", [](uintptr_t jobs, int njobs, long long nblocks, uintptr_t st) {
     gops::wcvt_batch(P<const long long>(jobs), njobs, nblocks, S(st));
     check_launch();

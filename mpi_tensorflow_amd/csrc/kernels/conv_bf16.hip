@@ -138,6 +138,116 @@ __global__ __launch_bounds__(256) void wcvt_batch_kernel(const long long* __rest
   }
 }
 
+// The flat momentum SGD of a bf16-conv model in ONE launch that also writes
+// the bf16 MFMA layouts of the updated conv weights (wcvt_kernel modes 0 and
+// 1), so no per-step weight-conversion launch remains ("for bf16
+// configs it also writes the bf16 weight shadow").
+//  * blocks [0, conv_blocks): one 32 x 32 (ci, co) tile of one tap of a conv
+//    weight - SGD of its 1024 floats (rows along co: 128-B loads per
+//    half-wave), the bf16 result straight into the dgrad layout
+//    Wd[R*S-1-tap][ci][co] and, transposed through LDS, into the forward
+//    layout Wt[tap][co][ci];
+//  * the other blocks: the remaining flat ranges (BatchNorm, FC, ...),
+//    float4 grid-stride per range.
+// jobs[j] = {w offset (floats), fwd out, dgrad out, taps, C, K, first block,
+// 0}; ranges[r] = {lo4, hi4, first block, nblocks} (float4 units).  Same
+// arithmetic as optim::sgd_momentum_flat_kernel (bit-identical updates).
+struct SgdWcvtArgs {
+  float* w;
+  const float* g;
+  float* mom;
+  float momentum, gscale, l2;
+  const float* lr;
+  long long* step;
+  const long long* jobs;
+  int njobs, conv_blocks;
+  const long long* ranges;
+  int nranges;
+};
+
+// index of the entry whose first block (field `f` of an 8- / 4-wide int64
+// row) is the last one <= b: one ballot per 64 entries
+__device__ __forceinline__ int table_lookup(const long long* tab, int n, int width, int f,
+                                            long long b) {
+  int j = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int jj = base + (int)(threadIdx.x & 63);
+    const bool le = jj < n && tab[width * min(jj, n - 1) + f] <= b;
+    const int cnt = __popcll(__ballot(le));
+    j = base + cnt - 1;
+    if (cnt < 64) break;
+  }
+  return max(j, 0);
+}
+
+__global__ __launch_bounds__(256) void sgd_wcvt_kernel(const SgdWcvtArgs a) {
+  __shared__ float t[32][33];
+  const float lr = *a.lr;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  if (a.step && b == 0 && tid == 0) *a.step += 1;
+  if (b < a.conv_blocks) {
+    const long long* J = a.jobs + 8 * table_lookup(a.jobs, a.njobs, 8, 6, b);
+    const long long woff = J[0];
+    __bf16* out0 = reinterpret_cast<__bf16*>(J[1]);
+    __bf16* out1 = reinterpret_cast<__bf16*>(J[2]);
+    const int taps = (int)J[3], C = (int)J[4], K = (int)J[5];
+    const int lb = b - (int)J[6];
+    const int ct = C / 32, kt = K / 32;
+    const int tap = lb / (ct * kt), rem = lb % (ct * kt), c0 = (rem / kt) * 32, k0 = (rem % kt) * 32;
+    const int tx = tid & 31, ty = tid >> 5;
+    const size_t base = (size_t)woff + (size_t)tap * C * K;
+    float wv[4], gv[4], mv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // all loads of the tile in flight together
+      const size_t e = base + (size_t)(c0 + ty + 8 * i) * K + k0 + tx;
+      wv[i] = a.w[e];
+      gv[i] = a.g[e];
+      mv[i] = a.mom[e];
+    }
+    __bf16* d1 = out1 + (size_t)(taps - 1 - tap) * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const size_t o = (size_t)(c0 + ty + 8 * i) * K + k0 + tx;
+      const float ge = gv[i] * a.gscale + a.l2 * wv[i];
+      const float m = a.momentum * mv[i] + ge;
+      const float w = wv[i] - lr * m;
+      a.w[base + o] = w;
+      a.mom[base + o] = m;
+      t[ty + 8 * i][tx] = w;
+      d1[o] = (__bf16)w;
+    }
+    __syncthreads();
+    __bf16* d0 = out0 + (size_t)tap * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) d0[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = (__bf16)t[tx][ty + 8 * i];
+    return;
+  }
+  const long long rb = b - a.conv_blocks;
+  const long long* Rr = a.ranges + 4 * table_lookup(a.ranges, a.nranges, 4, 2, rb);
+  const long long lo4 = Rr[0], hi4 = Rr[1], nb = Rr[3];
+  float4* W4 = reinterpret_cast<float4*>(a.w);
+  float4* M4 = reinterpret_cast<float4*>(a.mom);
+  const float4* G4 = reinterpret_cast<const float4*>(a.g);
+  const long long stride = nb * 256;
+  for (long long i = lo4 + (rb - Rr[2]) * 256 + tid; i < hi4; i += stride) {
+    float4 wv = W4[i], gv = G4[i], mv = M4[i];
+    gv.x = gv.x * a.gscale + a.l2 * wv.x;
+    gv.y = gv.y * a.gscale + a.l2 * wv.y;
+    gv.z = gv.z * a.gscale + a.l2 * wv.z;
+    gv.w = gv.w * a.gscale + a.l2 * wv.w;
+    mv.x = a.momentum * mv.x + gv.x;
+    mv.y = a.momentum * mv.y + gv.y;
+    mv.z = a.momentum * mv.z + gv.z;
+    mv.w = a.momentum * mv.w + gv.w;
+    wv.x -= lr * mv.x;
+    wv.y -= lr * mv.y;
+    wv.z -= lr * mv.z;
+    wv.w -= lr * mv.w;
+    W4[i] = wv;
+    M4[i] = mv;
+  }
+}
+
 // Forward conv Y[m = (n, oy, ox)][co] = sum_{tap, ci} X[n, iy, ix, ci] Wt[tap][co][ci].
 // XT = __bf16: bf16 activation copy (16-byte loads); XT = float: fp32
 // activations converted while staged.
@@ -2001,6 +2111,19 @@ void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t
   if (njobs <= 0 || nblocks <= 0 || nblocks >= (1LL << 31))
     throw std::runtime_error("wcvt_batch: bad job table");
   cbf::wcvt_batch_kernel<<<(int)nblocks, 256, 0, st>>>(jobs, njobs);
+}
+
+void sgd_wcvt(float* w, const float* g, float* mom, float momentum, float gscale, float l2,
+              const float* lr, long long* step, const long long* jobs, int njobs,
+              long long conv_blocks, const long long* ranges, int nranges, long long range_blocks,
+              hipStream_t st) {
+  if (njobs < 0 || nranges < 0 || conv_blocks < 0 || range_blocks < 0 ||
+      conv_blocks + range_blocks <= 0 || conv_blocks + range_blocks >= (1LL << 31) ||
+      (njobs == 0) != (conv_blocks == 0) || (nranges == 0) != (range_blocks == 0))
+    throw std::runtime_error("sgd_wcvt: bad job / range table");
+  const cbf::SgdWcvtArgs a{w, g, mom, momentum, gscale, l2, lr, step, jobs, njobs,
+                           (int)conv_blocks, ranges, nranges};
+  cbf::sgd_wcvt_kernel<<<(int)(conv_blocks + range_blocks), 256, 0, st>>>(a);
 }
 
 int conv_fwd_stats_rows(const ConvShape& s, bool bf16) {

@@ -95,6 +95,17 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
 // = wcvt_blocks(taps, C, K), first blocks ascending
 long long wcvt_blocks(int taps, int C, int K);
 void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t st);
+// flat momentum SGD (optim::sgd_momentum_flat arithmetic, l2 on every
+// element) that also writes the bf16 layouts of the updated conv weights:
+// jobs = device int64 [njobs][8] = {w offset (floats), forward out, dgrad out,
+// taps, C, K, first block, 0} (wcvt_blocks(taps, C, K) blocks each, both
+// layouts per block); ranges = device int64 [nranges][4] = {lo4, hi4, first
+// block, blocks} of the other float4 ranges (first blocks ascending, counted
+// from conv_blocks); step (optional) is bumped once
+void sgd_wcvt(float* w, const float* g, float* mom, float momentum, float gscale, float l2,
+              const float* lr, long long* step, const long long* jobs, int njobs,
+              long long conv_blocks, const long long* ranges, int nranges, long long range_blocks,
+              hipStream_t st);
 bool conv_bwd_filter_bf16_ok(const ConvShape& s);
 void conv_bwd_filter_bf16(const ConvShape& s, const float* x, const float* dy, float* ws,
                           float* dw, hipStream_t st, const void* xb = nullptr,

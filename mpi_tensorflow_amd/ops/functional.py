@@ -46,36 +46,73 @@ class Param:
 class Bf16Weights:
     """bf16 re-laid copies of every MFMA-family conv weight (C, K % 64 == 0)
     of a model - the forward layout [tap][co][ci] and the stride-1 dgrad
-    layout (taps reversed) - in one buffer, refreshed by ONE wcvt_batch launch
-    that the engine issues ahead of each forward (after the previous update).
-    The conv ops then skip their per-call conversion (ResNet-18: 40 small
-    launches a step).  Param.wtb / wtb_d point into the buffer."""
+    layout (taps reversed) - in one buffer.  Param.wtb / wtb_d point into it.
 
-    def __init__(self, params, device: torch.device):
+    Kept current two ways: refresh() re-derives them all in ONE wcvt_batch
+    launch (start of a run of steps, evaluation: any weight change made
+    outside the step), and sgd() - the step's flat momentum SGD - writes them
+    from the updated weights in the same launch (gops::sgd_wcvt), so a
+    training step has no conversion launch of its own.  sgd() needs the flat
+    parameter buffer (`flat`) the Params are views of."""
+
+    def __init__(self, params, device: torch.device, flat: Optional[torch.Tensor] = None):
         C = native()
         eligible = [p for p in params.values()
                     if p.value.dim() == 4 and p.value.shape[2] % 64 == 0 and p.value.shape[3] % 64 == 0]
         self.buf = torch.empty(max(1, sum(2 * p.value.numel() for p in eligible)),
                                dtype=torch.bfloat16, device=device)
         rows, off, blocks = [], 0, 0
+        sgd_jobs, sblocks = [], 0
         for p in eligible:
             R, S, Ci, K = p.value.shape
             n = p.value.numel()
+            outs = []
             for mode in (0, 1):
                 out = self.buf[off:off + n]
                 off += n
+                outs.append(out)
                 rows.append([ptr(p.value), ptr(out), R * S, Ci, K, mode, blocks, 0])
                 blocks += C.ops.wcvt_blocks(R * S, Ci, K)
-                if mode == 0:
-                    p.wtb = out
-                else:
-                    p.wtb_d = out
+            p.wtb, p.wtb_d = outs
+            if flat is not None:
+                woff = (p.value.data_ptr() - flat.data_ptr()) // 4
+                sgd_jobs.append([woff, ptr(outs[0]), ptr(outs[1]), R * S, Ci, K, sblocks, 0])
+                sblocks += C.ops.wcvt_blocks(R * S, Ci, K)
         self.njobs, self.nblocks = len(rows), blocks
         self.jobs = torch.tensor(rows if rows else [[0] * 8], dtype=torch.int64, device=device)
+        self.flat = flat
+        if flat is not None:
+            # the float4 ranges of the flat buffer outside the eligible conv
+            # weights (segments are 4-float aligned, parallel/flat.py)
+            covered = sorted((j[0], j[0] + p.value.numel()) for j, p in zip(sgd_jobs, eligible))
+            ranges, lo, rb = [], 0, 0
+            for a, b in covered + [(flat.numel(), flat.numel())]:
+                if a > lo:
+                    assert lo % 4 == 0 and a % 4 == 0, "flat segments must be 4-float aligned"
+                    n4 = (a - lo) // 4
+                    nb = max(1, min(64, -(-n4 // 256)))
+                    ranges.append([lo // 4, a // 4, rb, nb])
+                    rb += nb
+                lo = max(lo, b)
+            self.sgd_njobs, self.sgd_conv_blocks = len(sgd_jobs), sblocks
+            self.sgd_jobs = torch.tensor(sgd_jobs if sgd_jobs else [[0] * 8], dtype=torch.int64,
+                                         device=device)
+            self.nranges, self.range_blocks = len(ranges), rb
+            self.ranges = torch.tensor(ranges if ranges else [[0] * 4], dtype=torch.int64,
+                                       device=device)
 
     def refresh(self) -> None:
         if self.njobs:
             native().ops.wcvt_batch(ptr(self.jobs), self.njobs, self.nblocks, stream_handle())
+
+    def sgd(self, grads: torch.Tensor, mom: torch.Tensor, momentum: float, gscale: float,
+            lr: torch.Tensor, step: Optional[torch.Tensor]) -> None:
+        """w = flat params: g' = gscale g; m = momentum m + g'; w -= lr m, and
+        the bf16 layouts of the updated conv weights (one launch)."""
+        native().ops.sgd_wcvt(ptr(self.flat), ptr(grads), ptr(mom), momentum, gscale, 0.0,
+                              ptr(lr), ptr(step), ptr(self.sgd_jobs), self.sgd_njobs,
+                              self.sgd_conv_blocks, ptr(self.ranges), self.nranges,
+                              self.range_blocks, stream_handle())
 
 
 def _empty(shape, like):

@@ -119,8 +119,10 @@ class GenericEngine:
             self.step_dev = torch.zeros(1, dtype=torch.int64).to(device)
             self.lr_dev = torch.zeros(1).to(device)
             self.seed = torch.ones(()).to(device)  # backward seed, never written
-            # bf16: all conv weight copies in one launch per step
-            self.wcache = Fn.Bf16Weights(self.P, device) if self.bf16 else None
+            # bf16: the conv weights' bf16 layouts, written by the step's SGD
+            # launch (Bf16Weights.sgd) and re-derived at the start of a run
+            self.wcache = Fn.Bf16Weights(self.P, device, flat=self.params) if self.bf16 else None
+            self._wfresh = False  # the bf16 layouts match the fp32 weights
 
     # ------------------------------------------------------------------ util
     def lr(self, step: Optional[int] = None) -> float:
@@ -164,8 +166,9 @@ class GenericEngine:
         Fn.set_conv_bf16(self.bf16)
         s = stream_handle()
         row = int(np.prod(self.xb.shape[1:]))
-        if self.wcache is not None:
+        if self.wcache is not None and not self._wfresh:
             self.wcache.refresh()
+            self._wfresh = True
         # the gather also writes this step's device LR (no separate LR launch)
         C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
                             self.B, row, ptr(self.xb), ptr(self.yb), s, self.cfg.base_lr,
@@ -205,6 +208,10 @@ class GenericEngine:
             C_.ops.lr_from_step(ptr(self.step_dev), self.n_local, self.B, self.cfg.base_lr,
                                 self.cfg.lr_decay, ptr(self.lr_dev), s)
         self._lr_fresh = False
+        if self.wcache is not None:  # + the bf16 layouts of the updated conv weights
+            self.wcache.sgd(self.grads, self.mom, self.cfg.momentum, gscale, self.lr_dev,
+                            self.step_dev)
+            return
         C_.optim.sgd_momentum(ptr(self.params), ptr(self.grads), ptr(self.mom), self.layout.total, 0,
                               0.0, self.cfg.momentum, gscale, ptr(self.lr_dev), 0.0,
                               ptr(self.step_dev), s)
@@ -285,6 +292,12 @@ class GenericEngine:
                     self._step_cpu()
                     self.step += 1
             return
+        if self.wcache is not None:
+            # the weights may have changed since the last step (init, checkpoint,
+            # parameter averaging): re-derive the bf16 layouts once; the steps'
+            # SGD launches keep them current from here on
+            self.wcache.refresh()
+            self._wfresh = True
         left = k - self._warmup(k)
         if not self.use_graph:
             for _ in range(left):

@@ -2,7 +2,6 @@
 vs plain PyTorch fp32, and of whole LeNet-5 / ResNet-18 training steps vs the
 CPU oracle path."""
 
-import os
 
 import numpy as np
 import pytest
@@ -778,7 +777,7 @@ def test_softmax_rows_native(cuda_dev):
     assert _rel(y.cpu(), torch.softmax(x, 1)) < 1e-6
 
 
-ROUTES = tuple(v == "1" for v in os.environ.get("MTA_BNB_ROUTES", "0,1").split(","))
+ROUTES = (False, True)
 
 
 @pytest.mark.parametrize("shape,B", [((32, 32, 3), 32), ((224, 224, 3), 8)])
@@ -817,3 +816,41 @@ def test_resnet18_bn_backward_epilogue_matches_pass(cuda_dev, shape, B):
     assert max(head.values()) < 1e-5, head
     worst = sorted(errs.items(), key=lambda kv: -kv[1])[:6]
     assert worst[0][1] < 3e-2, worst
+
+
+def test_sgd_writes_bf16_conv_layouts(cuda_dev):
+    """ResNet-18 bf16: the step's fused SGD (gops::sgd_wcvt) updates every
+    parameter bit-identically to the flat momentum SGD and writes the bf16
+    forward / dgrad layouts of the updated conv weights exactly as the
+    wcvt_batch re-derivation does (so no conversion launch is needed)."""
+    from mpi_tensorflow_amd.ops import native, ptr, stream_handle
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    x, y = synthetic_rows("train", 0, 16, shape=(32, 32, 3))
+    eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=8, dtype="bf16",
+                                      graph=False).validate(), x, y, cuda_dev)
+    g = torch.Generator(device="cpu").manual_seed(5)
+    grads = torch.randn(eng.layout.total, generator=g).to(cuda_dev)
+    mom = torch.randn(eng.layout.total, generator=g).to(cuda_dev)
+    lr = torch.tensor([0.0123], device=cuda_dev)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda_dev)
+    w0 = eng.params.detach().clone()
+    wc = eng.wcache
+    # reference: the flat SGD, then a full re-derivation of the layouts
+    m_ref = mom.clone()
+    native().optim.sgd_momentum(ptr(eng.params), ptr(grads), ptr(m_ref), eng.layout.total, 0, 0.0,
+                                0.9, 0.5, ptr(lr), 0.0, 0, stream_handle())
+    wc.refresh()
+    torch.cuda.synchronize()
+    w_ref, buf_ref = eng.params.detach().clone(), wc.buf.clone()
+    # fused
+    eng.params.data.copy_(w0)
+    wc.buf.zero_()
+    wc.sgd(grads, mom, 0.9, 0.5, lr, step)
+    torch.cuda.synchronize()
+    assert int(step.item()) == 1
+    assert torch.equal(eng.params.detach(), w_ref), "params differ from the flat SGD"
+    assert torch.equal(mom, m_ref), "momentum differs from the flat SGD"
+    assert torch.equal(wc.buf, buf_ref), "bf16 layouts differ from wcvt_batch"
+    assert wc.sgd_njobs > 0 and wc.nranges > 0
