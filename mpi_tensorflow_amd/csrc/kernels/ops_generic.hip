@@ -530,6 +530,59 @@ __global__ __launch_bounds__(256) void maxpool_bwd4b_kernel(PoolShape p, const f
   }
 }
 
+// The ResNet stem pool's backward (3x3, stride 2, pad 1, uint8 window taps):
+// a thread owns 8 channels (two float4) of one input pixel.  Its windows are
+// rows iy >> 1 and (odd iy) (iy + 1) >> 1, columns likewise; every candidate
+// window's taps and gradients are loaded up front, unconditionally from
+// clamped addresses (one latency round instead of a tap load -> gradient load
+// chain per window), and summed in the (oy, ox) order of maxpool_bwd4b_kernel
+// (bit-identical dX).
+template <int C4>
+__global__ __launch_bounds__(256) void maxpool_bwd_k3s2_kernel(PoolShape p,
+                                                               const float4* __restrict__ dy,
+                                                               const uint2* __restrict__ arg,
+                                                               float4* __restrict__ dx) {
+  static_assert(C4 % 2 == 0, "two float4 per thread");
+  constexpr int C8 = C4 / 2;
+  const int n = p.N * p.H * p.W * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    const int pix = i / C8;
+    const int ix = pix % p.W, t = pix / p.W;
+    const int iy = t % p.H, nn = t / p.H;
+    const int oy0 = iy >> 1, ox0 = ix >> 1;
+    const bool y2 = (iy & 1) && oy0 + 1 < p.OH, x2 = (ix & 1) && ox0 + 1 < p.OW;
+    uint2 a[4];
+    float4 d[4][2];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int oy = oy0 + ((w >> 1) & (int)y2), ox = ox0 + ((w & 1) & (int)x2);
+      const int o = ((nn * p.OH + oy) * p.OW + ox) * C8 + c8;
+      a[w] = arg[o];
+      d[w][0] = dy[2 * o];
+      d[w][1] = dy[2 * o + 1];
+    }
+    float4 g0 = make_float4(0.f, 0.f, 0.f, 0.f), g1 = g0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const bool live = ((w >> 1) == 0 || y2) && ((w & 1) == 0 || x2);
+      const int oy = oy0 + (w >> 1), ox = ox0 + (w & 1);
+      const unsigned r = live ? (unsigned)((iy - 2 * oy + 1) * 3 + (ix - 2 * ox + 1)) : 255u;
+      const uchar4 q0 = __builtin_bit_cast(uchar4, a[w].x), q1 = __builtin_bit_cast(uchar4, a[w].y);
+      if (q0.x == r) g0.x += d[w][0].x;
+      if (q0.y == r) g0.y += d[w][0].y;
+      if (q0.z == r) g0.z += d[w][0].z;
+      if (q0.w == r) g0.w += d[w][0].w;
+      if (q1.x == r) g1.x += d[w][1].x;
+      if (q1.y == r) g1.y += d[w][1].y;
+      if (q1.z == r) g1.z += d[w][1].z;
+      if (q1.w == r) g1.w += d[w][1].w;
+    }
+    dx[2 * i] = g0;
+    dx[2 * i + 1] = g1;
+  }
+}
+
 // block = (image n, 32 channels) x 8 pixel groups; the group partials are
 // summed through LDS in a fixed order (ResNet-18 head: 512 blocks instead of
 // 64 threads-per-channel blocks walking 49 dependent loads, 13 -> ~3 us)
@@ -1086,8 +1139,9 @@ void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, flo
   const auto D = reinterpret_cast<const float4*>(dy);
   const auto A = reinterpret_cast<const uchar4*>(arg);
   const auto DX = reinterpret_cast<float4*>(dx);
-  if (p.k == 3 && p.stride == 2 && p.pad == 1 && p.C == 64)
-    maxpool_bwd4b_kernel<3, 2, 1, 16><<<grid1d(n / 4), 256, 0, st>>>(p, D, A, DX);
+  if (p.k == 3 && p.stride == 2 && p.pad == 1 && p.C == 64)  // the ResNet stem pool
+    maxpool_bwd_k3s2_kernel<16><<<grid1d(n / 8), 256, 0, st>>>(
+        p, D, reinterpret_cast<const uint2*>(arg), DX);
   else
     maxpool_bwd4b_kernel<0, 0, 0, 0><<<grid1d(n / 4), 256, 0, st>>>(p, D, A, DX);
 }
