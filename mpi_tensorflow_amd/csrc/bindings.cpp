@@ -92,7 +92,7 @@ PYBIND11_MODULE(_C, m) {
   k.def("conv12_fwd_wino", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
                               uintptr_t b1, uintptr_t a1, uintptr_t a1pf, uintptr_t idx1,
                               uintptr_t w2, uintptr_t U, uintptr_t b2, uintptr_t a2, uintptr_t idx2,
-                              uintptr_t w2t, uintptr_t s, uintptr_t prof) {
+                              uintptr_t w2t, uintptr_t s, uintptr_t prof, uintptr_t a2t) {
     mnist::C12In c;
     c.data = P<const float>(data);
     c.step = P<const long long>(step);
@@ -104,9 +104,9 @@ PYBIND11_MODULE(_C, m) {
     c.idx1 = P<uint8_t>(idx1);
     mnist::launch_conv12_fwd_wino(c, batch, P<const float>(w2), P<const float>(U),
                                   P<const float>(b2), P<float>(a2), P<uint8_t>(idx2),
-                                  P<float>(w2t), S(s), P<unsigned long long>(prof));
+                                  P<float>(w2t), S(s), P<unsigned long long>(prof), P<float>(a2t));
     check_launch();
-  }, py::arg("data"), py::arg("step"), py::arg("n_local"), py::arg("batch"), py::arg("w1"), py::arg("b1"), py::arg("a1"), py::arg("a1pf"), py::arg("idx1"), py::arg("w2"), py::arg("U"), py::arg("b2"), py::arg("a2"), py::arg("idx2"), py::arg("w2t"), py::arg("s"), py::arg("prof") = 0);
+  }, py::arg("data"), py::arg("step"), py::arg("n_local"), py::arg("batch"), py::arg("w1"), py::arg("b1"), py::arg("a1"), py::arg("a1pf"), py::arg("idx1"), py::arg("w2"), py::arg("U"), py::arg("b2"), py::arg("a2"), py::arg("idx2"), py::arg("w2t"), py::arg("s"), py::arg("prof") = 0, py::arg("a2t") = 0);
   // bf16 engine forward pieces (tests): two-launch conv1 -> conv2 and the fused launch
   k.def("conv1_fwd_bf16", [](uintptr_t data, uintptr_t step, int n_local, int batch, uintptr_t w1,
                              uintptr_t b1, uintptr_t a1p, uintptr_t a1t, uintptr_t idx1,
@@ -196,6 +196,13 @@ PYBIND11_MODULE(_C, m) {
     mnist::launch_fc1_fwd_train(P<const float>(a2), P<const float>(w), batch, P<float>(part), S(s));
     check_launch();
   });
+  k.def("fc1_fwd_train_t", [](uintptr_t a2t, uintptr_t w, int batch, uintptr_t part,
+                              uintptr_t s) {
+    mnist::launch_fc1_fwd_train_t(P<const float>(a2t), P<const float>(w), batch, P<float>(part),
+                                  S(s));
+    check_launch();
+  });
+  k.def("fc1_train_t_splits", &mnist::fc1_train_t_splits);
   k.def("fc1_fwd_eval", [](uintptr_t a2, uintptr_t w, uintptr_t b, int M, uintptr_t h,
                            uint32_t key, float keep, uintptr_t s) {
     mnist::launch_fc1_fwd_eval(P<const float>(a2), P<const float>(w), P<const float>(b), M,
@@ -206,14 +213,20 @@ PYBIND11_MODULE(_C, m) {
         [](uintptr_t part, uintptr_t b3, uintptr_t w4, uintptr_t b4, uintptr_t labels, int n_local,
            uintptr_t step, int batch, float keep, uint32_t seed, uint32_t rank, float base_lr,
            float decay, uintptr_t hd, uintptr_t dh, uintptr_t dlog, uintptr_t loss_rows,
-           uintptr_t lr_out, uintptr_t correct, uintptr_t s) {
+           uintptr_t lr_out, uintptr_t correct, uintptr_t s, int splits) {
           mnist::launch_fc_head_train(P<const float>(part), P<const float>(b3), P<const float>(w4),
                                       P<const float>(b4), P<const int>(labels), n_local,
                                       P<const long long>(step), batch, keep, seed, rank, base_lr,
                                       decay, P<float>(hd), P<float>(dh), P<float>(dlog),
-                                      P<float>(loss_rows), P<float>(lr_out), P<int>(correct), S(s));
+                                      P<float>(loss_rows), P<float>(lr_out), P<int>(correct), S(s),
+                                      nullptr, nullptr, splits);
           check_launch();
-        });
+        },
+        py::arg("part"), py::arg("b3"), py::arg("w4"), py::arg("b4"), py::arg("labels"),
+        py::arg("n_local"), py::arg("step"), py::arg("batch"), py::arg("keep"), py::arg("seed"),
+        py::arg("rank"), py::arg("base_lr"), py::arg("decay"), py::arg("hd"), py::arg("dh"),
+        py::arg("dlog"), py::arg("loss_rows"), py::arg("lr_out"), py::arg("correct"), py::arg("s"),
+        py::arg("splits") = 14);
   k.def("fc_head_eval", [](uintptr_t h, uintptr_t w4, uintptr_t b4, uintptr_t labels, int M,
                            uintptr_t logits, uintptr_t errors, uintptr_t s) {
     mnist::launch_fc_head_eval(P<const float>(h), P<const float>(w4), P<const float>(b4),
@@ -566,7 +579,7 @@ PYBIND11_MODULE(_C, m) {
                                   RW(a1p) RW(a1t) RW(a2h) RW(a2t) RW(dy2p) RW(dy2t) RW(dh16)
                                       RW(dht16) RW(w1b) RW(w1t) RW(w2tb) RW(w2b) RW(a2_all)
                                           RW(dh_all) RW(hd_all) RW(dlog_all) RW(fac_ranks)
-                                              RW(wino) RW(wino_u) RW(wino_ud);
+                                              RW(wino) RW(wino_u) RW(wino_ud) RW(a2ft);
 #undef RW
 
   py::class_<Collective>(m, "Collective")

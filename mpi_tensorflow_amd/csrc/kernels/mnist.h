@@ -75,9 +75,10 @@ void launch_conv2_fwd(const float* a1, int batch, const float* w, const float* b
 // when Ud != nullptr, Ud [36][64][32] of the rotated filter (bwd-data)
 void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t s);
 // prof (labs): per-wave phase stamps [blocks][8 waves][5] (s_memtime)
+// a2t (optional): a2 also feature-major [3136][batch] (launch_fc1_fwd_train_t)
 void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
                             const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s,
-                            unsigned long long* prof = nullptr);
+                            unsigned long long* prof = nullptr, float* a2t = nullptr);
 void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
                            const float* b, float* out, uint8_t* argmax, float* w2t, hipStream_t s);
 // Winograd bwd-data: dy2t as for launch_conv2_bwd_data_l2, Ud from
@@ -89,6 +90,11 @@ void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float*
                                 unsigned long long* prof = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
+// fc1 train forward over the feature-major a2t [3136][batch] (batch % 32 ==
+// 0): fc1_train_t_splits() slabs, no LDS staging (mnist.hip fc1_fwd_t_kernel)
+int fc1_train_t_splits();
+void launch_fc1_fwd_train_t(const float* a2t, const float* w, int batch, float* part,
+                            hipStream_t s);
 void launch_fc1_fwd_eval(const float* a2, const float* w, const float* b, int M, float* h,
                          uint32_t key, float keep_prob, hipStream_t s);
 void launch_fc_head_train(const float* part, const float* b3, const float* w4, const float* b4,
@@ -96,7 +102,7 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
                           float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
                           float* lr_out, int* correct, hipStream_t s, uint16_t* dh16 = nullptr,
-                          uint16_t* dht16 = nullptr);
+                          uint16_t* dht16 = nullptr, int splits = 14);  // slabs in part
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
                          int M, float* logits, int* errors, hipStream_t s);
 // dY2 as NHWC dy2 [B][14][14][64] and channel-major zero-bordered dy2t

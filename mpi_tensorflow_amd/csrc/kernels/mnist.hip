@@ -224,11 +224,68 @@ __global__ __launch_bounds__(64 * WM * WN * WK) void fc1_fwd_kernel(
   }
 }
 
+// fc1 forward (train) over the feature-major a2t [3136][batch] that the
+// Winograd conv2 forward writes: both MFMA operands come straight from
+// L2 / MALL with lanes on their contiguous axis (a2t rows along the batch,
+// W1 rows along the 512 outputs: one 128-B line per half-wave load), so there
+// is no LDS staging, no transpose and no barrier before the products.
+// Block = (32 rows, 32 outputs, split of 3136 / FC1T_SPLITS features); its 4
+// waves take consecutive quarters of the split (49 k-steps each, every load
+// issued up front, two accumulator chains) and meet once in LDS; wave 0
+// writes the split's partial slab part[split][row][512] (the head sums them).
+constexpr int FC1T_SPLITS = 8;
+constexpr int FC1T_KW = FC1_IN / FC1T_SPLITS / 4;  // 98 features per wave
+static_assert(FC1T_KW % 2 == 0 && FC1_IN % (FC1T_SPLITS * 4) == 0, "fc1_fwd_t split");
+
+__global__ __launch_bounds__(256) void fc1_fwd_t_kernel(const float* __restrict__ a2t,
+                                                        const float* __restrict__ w,
+                                                        int batch, float* __restrict__ part) {
+  __shared__ float red[3][16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i = lane & 31, h = lane >> 5;
+  const int nt = blockIdx.x % (FC1_OUT / 32), bt = blockIdx.x / (FC1_OUT / 32);
+  const int z = blockIdx.y;
+  const int n0 = 32 * nt, b0 = 32 * bt;
+  const int kb = z * (FC1_IN / FC1T_SPLITS) + wave * FC1T_KW;
+  constexpr int ST = FC1T_KW / 2;  // 49 MFMA k-steps
+  const float* ap = a2t + (size_t)(kb + h) * batch + b0 + i;
+  const float* bp = w + (size_t)(kb + h) * FC1_OUT + n0 + i;
+  float av[ST], bv[ST];
+#pragma unroll
+  for (int t = 0; t < ST; ++t) {
+    av[t] = ap[(size_t)2 * t * batch];
+    bv[t] = bp[(size_t)2 * t * FC1_OUT];
+  }
+  f32x16 c0 = zero16(), c1 = zero16();
+#pragma unroll
+  for (int t = 0; t < ST; ++t) {
+    if (t & 1)
+      c1 = mfma32x32x2(av[t], bv[t], c1);
+    else
+      c0 = mfma32x32x2(av[t], bv[t], c0);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) c0[r] += c1[r];
+  if (wave > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave - 1][r][lane] = c0[r];
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float v = c0[r] + red[0][r][lane] + red[1][r][lane] + red[2][r][lane];
+      const int row = b0 + mfma32_row(r, lane);
+      part[((size_t)z * batch + row) * FC1_OUT + n0 + i] = v;
+    }
+  }
+}
+
 // -------------------------------------------------------------- fc head ----
 // One workgroup per batch row: reduce fc1 split-K slabs, bias, ReLU, dropout,
 // fc2 (512x10, too thin for MFMA: VALU dot products), softmax cross-entropy
 // forward AND backward (dlogits = (softmax - onehot) / B), then
 // dhidden = dlogits W2^T through the dropout and ReLU masks.
+template <int NS>  // split-K slabs of the fc1 forward (FC1_SPLITS, FC1T_SPLITS)
 __global__ __launch_bounds__(256) void fc_head_train_kernel(
     const float* __restrict__ part, const float* __restrict__ b3, const float* __restrict__ w4,
     const float* __restrict__ b4, const int* __restrict__ labels, int n_local,
@@ -250,11 +307,11 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
   const int label = labels[off + row];
   const float b4l = lane < NCLS ? b4[lane] : 0.f;
   // issue every slab load up front (one latency round, not 14)
-  float ps[2][FC1_SPLITS];
+  float ps[2][NS];
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int q = 0; q < FC1_SPLITS; ++q)
+    for (int q = 0; q < NS; ++q)
       ps[u][q] = part[((size_t)q * batch + row) * FC1_OUT + tid + 256 * u];
   float w4r[2][NCLS];
 #pragma unroll
@@ -271,7 +328,7 @@ __global__ __launch_bounds__(256) void fc_head_train_kernel(
     const int j = tid + 256 * u;
     float s = b3[j];
 #pragma unroll
-    for (int q = 0; q < FC1_SPLITS; ++q) s += ps[u][q];
+    for (int q = 0; q < NS; ++q) s += ps[u][q];
     z[u] = s;
     const float h = fmaxf(s, 0.f);
     kp[u] = dropout_keep(key, (uint32_t)(row * FC1_OUT + j), keep_prob);
@@ -1000,7 +1057,9 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
     const float* __restrict__ a1, int batch, const float* __restrict__ w2,
     const float* __restrict__ U, const float* __restrict__ b2, float* __restrict__ out,
     uint8_t* __restrict__ argmax, float* __restrict__ w2t, const C12In c1,
-    unsigned long long* __restrict__ prof = nullptr) {
+    unsigned long long* __restrict__ prof = nullptr, float* __restrict__ out_t = nullptr) {
+  // out_t (optional): the pooled output also feature-major, a2t [3136][batch]
+  // (the fc1 forward's MFMA operand, fc1_fwd_t_kernel)
   unsigned long long stamp[5];
   if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
   __shared__ float xs[WX_FLOATS];
@@ -1142,9 +1201,12 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
       }
       const int pr = pr0 + t / 7, pc = t % 7;
       if (t < 14 && pr < 7) {
-        const int oi = ((n * 7 + pr) * 7 + pc) * 64 + co;
-        out[oi] = fmaxf(m + bias, 0.f);
+        const int fi = (pr * 7 + pc) * 64 + co;
+        const int oi = n * FC1_IN + fi;
+        const float o = fmaxf(m + bias, 0.f);
+        out[oi] = o;
         if (argmax) argmax[oi] = (uint8_t)qq;
+        if (out_t) out_t[(size_t)fi * batch + n] = o;
       }
     }
   }
@@ -1961,15 +2023,15 @@ void launch_conv2_wino_weights(const float* w2, float* U, float* Ud, hipStream_t
 
 void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const float* U,
                             const float* b2, float* a2, uint8_t* idx2, float* w2t, hipStream_t s,
-                            unsigned long long* prof) {
+                            unsigned long long* prof, float* a2t) {
   if (!c1.data || !c1.w1 || !c1.b1 || !c1.a1 || !c1.a1pf || !c1.idx1 || !U)
     throw std::runtime_error("conv12_fwd_wino: missing operand");
   if (prof)
     conv2_fwd_wino_kernel<true, true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2,
-                                                                w2t, c1, prof);
+                                                                w2t, c1, prof, a2t);
   else
     conv2_fwd_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(nullptr, batch, w2, U, b2, a2, idx2, w2t,
-                                                          c1);
+                                                          c1, nullptr, a2t);
 }
 
 void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
@@ -1980,6 +2042,7 @@ void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const fl
 }
 
 int fc1_train_splits() { return FC1_SPLITS; }
+int fc1_train_t_splits() { return FC1T_SPLITS; }
 
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part,
                           hipStream_t s) {
@@ -2001,12 +2064,27 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           float keep_prob, uint32_t seed, uint32_t rank, float base_lr,
                           float lr_decay, float* hd, float* dh, float* dlog, float* loss_rows,
                           float* lr_out, int* correct, hipStream_t s, uint16_t* dh16,
-                          uint16_t* dht16) {
-  fc_head_train_kernel<<<batch, 256, 0, s>>>(part, b3, w4, b4, labels, n_local, step, batch,
-                                             keep_prob, seed, rank, base_lr, lr_decay, hd, dh,
-                                             dlog, loss_rows, lr_out, correct,
-                                             reinterpret_cast<__bf16*>(dh16),
-                                             reinterpret_cast<__bf16*>(dht16));
+                          uint16_t* dht16, int splits) {
+#define HEAD(NS_)                                                                              \
+  fc_head_train_kernel<NS_><<<batch, 256, 0, s>>>(part, b3, w4, b4, labels, n_local, step, batch, \
+                                                  keep_prob, seed, rank, base_lr, lr_decay, hd, dh, \
+                                                  dlog, loss_rows, lr_out, correct,              \
+                                                  reinterpret_cast<__bf16*>(dh16),               \
+                                                  reinterpret_cast<__bf16*>(dht16))
+  if (splits == FC1T_SPLITS)
+    HEAD(FC1T_SPLITS);
+  else if (splits == FC1_SPLITS)
+    HEAD(FC1_SPLITS);
+  else
+    throw std::runtime_error("fc_head_train: unsupported slab count");
+#undef HEAD
+}
+
+void launch_fc1_fwd_train_t(const float* a2t, const float* w, int batch, float* part,
+                            hipStream_t s) {
+  if (batch <= 0 || batch % 32) throw std::runtime_error("fc1_fwd_t: batch % 32 != 0");
+  fc1_fwd_t_kernel<<<dim3((FC1_OUT / 32) * (batch / 32), FC1T_SPLITS), 256, 0, s>>>(a2t, w, batch,
+                                                                                   part);
 }
 
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,

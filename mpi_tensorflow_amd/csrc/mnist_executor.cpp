@@ -70,18 +70,24 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
     if (!fresh)
       mnist::launch_conv2_wino_weights(W + p.off_w2, P<float>(p.wino_u), P<float>(p.wino_ud), s);
     mnist::launch_conv12_fwd_wino(cf, B, W + p.off_w2, P<const float>(p.wino_u), W + p.off_b2,
-                                  P<float>(p.a2), P<uint8_t>(p.idx2), nullptr, s);
+                                  P<float>(p.a2), P<uint8_t>(p.idx2), nullptr, s, nullptr,
+                                  P<float>(p.a2ft));
   } else {
     mnist::launch_conv12_fwd(cf, B, W + p.off_w2, W + p.off_b2, P<float>(p.a2),
                              P<uint8_t>(p.idx2), P<float>(p.w2t), s);
   }
   wait_fc_params(s);  // sharded FC update of the previous step (all-gather in flight)
-  mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
+  const bool fc1_t = p.wino && p.a2ft != 0;
+  if (fc1_t)
+    mnist::launch_fc1_fwd_train_t(P<const float>(p.a2ft), W + p.off_w3, B, P<float>(p.fc1_part), s);
+  else
+    mnist::launch_fc1_fwd_train(P<const float>(p.a2), W + p.off_w3, B, P<float>(p.fc1_part), s);
   mnist::launch_fc_head_train(P<const float>(p.fc1_part), W + p.off_b3, W + p.off_w4,
                               W + p.off_b4, P<const int>(p.train_y), p.n_local, step, B,
                               p.keep_prob, p.seed, p.rank, p.base_lr, p.lr_decay, P<float>(p.hd),
                               P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
-                              P<float>(p.lr), P<int>(p.correct), s);
+                              P<float>(p.lr), P<int>(p.correct), s, nullptr, nullptr,
+                              fc1_t ? mnist::fc1_train_t_splits() : mnist::fc1_train_splits());
   if (factors) HIP_CHECK(hipEventRecord(ev_fac_, s));
   // backward: fc1 dX (+pool2/ReLU2 scatter) | dW1 | fc2 grads, one launch
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),

@@ -68,6 +68,9 @@ struct MnistPtrs {
   // wino_u [36][32][64] (forward) and wino_ud [36][64][32] (bwd-data)
   int wino = 0;
   uintptr_t wino_u = 0, wino_ud = 0;
+  // fp32 Winograd step (optional): a2 also feature-major [3136][batch], written
+  // by the conv2 forward for the LDS-free fc1 forward (0: the LDS-staged one)
+  uintptr_t a2ft = 0;
 };
 
 namespace mnist {

@@ -275,3 +275,36 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     eng.train(7)
     torch.cuda.synchronize()
     assert torch.isfinite(eng.params).all()
+
+
+@pytest.mark.parametrize("batch", [64, 96])
+def test_fc1_forward_feature_major_matches_staged(cuda_dev, batch):
+    """fc1 train forward over the feature-major a2t copy (LDS-free operands,
+    8 split-K slabs) vs the LDS-staged kernel (14 slabs) and an fp64 matmul,
+    with asymmetric data; and the Winograd conv2 forward's a2t equals the
+    transpose of its a2 bit for bit."""
+    Cn = native()
+    k = Cn.mnist
+    g = torch.Generator().manual_seed(21)
+    a2 = torch.relu(torch.randn(batch, M.FC1_IN, generator=g)) * torch.rand(M.FC1_IN, generator=g)
+    w = torch.randn(M.FC1_IN, M.FC1_OUT, generator=g) * 0.05 + 0.01
+    a2d, a2td, wd = a2.to(cuda_dev), a2.t().contiguous().to(cuda_dev), w.to(cuda_dev)
+    p_t = torch.full((k.fc1_part_floats(batch),), float("nan"), device=cuda_dev)
+    p_s = torch.full_like(p_t, float("nan"))
+    s = stream_handle()
+    k.fc1_fwd_train_t(ptr(a2td), ptr(wd), batch, ptr(p_t), s)
+    k.fc1_fwd_train(ptr(a2d), ptr(wd), batch, ptr(p_s), s)
+    torch.cuda.synchronize()
+    zt, zs = k.fc1_train_t_splits(), k.fc1_train_splits()
+    ht = p_t[:zt * batch * M.FC1_OUT].view(zt, batch, M.FC1_OUT).sum(0).double().cpu()
+    hs = p_s[:zs * batch * M.FC1_OUT].view(zs, batch, M.FC1_OUT).sum(0).double().cpu()
+    ref = a2.double() @ w.double()
+    assert torch.isfinite(ht).all()
+    assert _rel(ht, ref) < 1e-6 and _rel(hs, ref) < 1e-6
+    # the conv2 forward's feature-major copy
+    x, y = synthetic_rows("train", 0, 4 * batch)
+    e = NativeMnistEngine(C.TrainConfig(batch_size=batch, graph=False).validate(), x, y, cuda_dev)
+    e.forward_backward_only()
+    torch.cuda.synchronize()
+    a2n = e.bufs["a2"].view(batch, M.FC1_IN)
+    assert torch.equal(e.bufs["a2ft"].view(M.FC1_IN, batch), a2n.t())
