@@ -120,7 +120,14 @@ __global__ __launch_bounds__(256) void wcvt_batch_kernel(const long long* __rest
   const int tap = lb / (ct * kt), rem = lb % (ct * kt), c0 = (rem / kt) * 32, k0 = (rem % kt) * 32;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const float* src = w + (size_t)tap * C * K;
-  if (mode == 0) {
+  if (mode == 2) {  // fp32 stride-1 dgrad weights: flipped taps, ci / co transposed
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t[ty + 8 * i][tx] = src[(size_t)(c0 + ty + 8 * i) * K + k0 + tx];
+    __syncthreads();
+    float* dst = reinterpret_cast<float*>(J[1]) + (size_t)(taps - 1 - tap) * C * K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dst[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = t[tx][ty + 8 * i];
+  } else if (mode == 0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) t[ty + 8 * i][tx] = src[(size_t)(c0 + ty + 8 * i) * K + k0 + tx];
     __syncthreads();
@@ -150,8 +157,11 @@ __global__ __launch_bounds__(256) void wcvt_batch_kernel(const long long* __rest
 //  * the other blocks: the remaining flat ranges (BatchNorm, FC, ...),
 //    float4 grid-stride per range.
 // jobs[j] = {w offset (floats), fwd out, dgrad out, taps, C, K, first block,
-// 0}; ranges[r] = {lo4, hi4, first block, nblocks} (float4 units).  Same
-// arithmetic as optim::sgd_momentum_flat_kernel (bit-identical updates).
+// kind}; kind 0: the bf16 forward / dgrad layouts; kind 1 (fp32 model): the
+// fp32 stride-1 dgrad weights, flipped and transposed (wflip_kernel's
+// layout) into `fwd out`.  ranges[r] = {lo4, hi4, first block, nblocks}
+// (float4 units).  Same arithmetic as optim::sgd_momentum_flat_kernel
+// (bit-identical updates).
 struct SgdWcvtArgs {
   float* w;
   const float* g;
@@ -192,6 +202,7 @@ __global__ __launch_bounds__(256) void sgd_wcvt_kernel(const SgdWcvtArgs a) {
     __bf16* out1 = reinterpret_cast<__bf16*>(J[2]);
     const int taps = (int)J[3], C = (int)J[4], K = (int)J[5];
     const int lb = b - (int)J[6];
+    const bool f32flip = J[7] == 1;
     const int ct = C / 32, kt = K / 32;
     const int tap = lb / (ct * kt), rem = lb % (ct * kt), c0 = (rem / kt) * 32, k0 = (rem % kt) * 32;
     const int tx = tid & 31, ty = tid >> 5;
@@ -214,9 +225,15 @@ __global__ __launch_bounds__(256) void sgd_wcvt_kernel(const SgdWcvtArgs a) {
       a.w[base + o] = w;
       a.mom[base + o] = m;
       t[ty + 8 * i][tx] = w;
-      d1[o] = (__bf16)w;
+      if (!f32flip) d1[o] = (__bf16)w;
     }
     __syncthreads();
+    if (f32flip) {
+      float* df = reinterpret_cast<float*>(out0) + (size_t)(taps - 1 - tap) * C * K;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) df[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = t[tx][ty + 8 * i];
+      return;
+    }
     __bf16* d0 = out0 + (size_t)tap * C * K;
 #pragma unroll
     for (int i = 0; i < 4; ++i) d0[(size_t)(k0 + ty + 8 * i) * C + c0 + tx] = (__bf16)t[tx][ty + 8 * i];

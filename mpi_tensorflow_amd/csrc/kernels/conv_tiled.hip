@@ -1091,14 +1091,18 @@ static void conv_fwd_tiled_impl(const ConvShape& s, const float* x, const float*
 }
 
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
-                         hipStream_t st, bool bf16, const float* addend, const void* dyb) {
+                         hipStream_t st, bool bf16, const float* addend, const void* dyb,
+                         const float* wflip) {
   using namespace tiled;
   if (!bf16 && dy && ws && dgrad_fwd_ok(s)) {
     const ConvShape f = dgrad_fwd_shape(s);
-    float* wt = ws;
     float* fws = ws + ((long long)s.R * s.S * s.C * s.K + 3) / 4 * 4;
-    wflip_kernel<<<dim3(cdiv(s.K, 32), cdiv(s.C, 32), s.R * s.S), 256, 0, st>>>(w, wt, s.R, s.S,
-                                                                               s.C, s.K);
+    const float* wt = wflip;  // kept current by the step's SGD (gops::sgd_wcvt)
+    if (!wt) {
+      wflip_kernel<<<dim3(cdiv(s.K, 32), cdiv(s.C, 32), s.R * s.S), 256, 0, st>>>(w, ws, s.R, s.S,
+                                                                                 s.C, s.K);
+      wt = ws;
+    }
     conv_fwd_tiled_impl(f, dy, wt, nullptr, dx, false, fws, st, false, nullptr, addend);
     return;
   }

@@ -91,15 +91,16 @@ void conv_bwd_data_bf16(const ConvShape& s, const float* dy, const float* w, flo
                         hipStream_t st, const void* dyb = nullptr, const float* addend = nullptr,
                         const void* wtb = nullptr, const BnBwdStats* bstats = nullptr);
 // batched weight re-layout: jobs = device int64 [njobs][8] = {w, out, taps,
-// C, K, mode (0 forward, 1 stride-1 dgrad), first block, 0}, blocks of a job
+// C, K, mode (0 bf16 forward, 1 bf16 stride-1 dgrad, 2 fp32 stride-1 dgrad:
+// flipped + ci / co transposed), first block, 0}, blocks of a job
 // = wcvt_blocks(taps, C, K), first blocks ascending
 long long wcvt_blocks(int taps, int C, int K);
 void wcvt_batch(const long long* jobs, int njobs, long long nblocks, hipStream_t st);
 // flat momentum SGD (optim::sgd_momentum_flat arithmetic, l2 on every
 // element) that also writes the bf16 layouts of the updated conv weights:
 // jobs = device int64 [njobs][8] = {w offset (floats), forward out, dgrad out,
-// taps, C, K, first block, 0} (wcvt_blocks(taps, C, K) blocks each, both
-// layouts per block); ranges = device int64 [nranges][4] = {lo4, hi4, first
+// taps, C, K, first block, kind} (wcvt_blocks(taps, C, K) blocks each; kind 0:
+// both bf16 layouts per block, kind 1: the fp32 flipped dgrad layout); ranges = device int64 [nranges][4] = {lo4, hi4, first
 // block, blocks} of the other float4 ranges (first blocks ascending, counted
 // from conv_blocks); step (optional) is bumped once
 void sgd_wcvt(float* w, const float* g, float* mom, float momentum, float gscale, float l2,
@@ -122,9 +123,12 @@ void conv_fwd_tiled(const ConvShape& s, const float* x, const float* w, const fl
 // partial rows of the BatchNorm statistics the tiled forward writes (fp32 route)
 int conv_fwd_tiled_stats_rows(const ConvShape& s, bool bf16);
 // dy may be null when dyb (bf16 dY) is given
+// wflip (optional, fp32 stride-1 dgrad): the weights already flipped and
+// ci / co-transposed, W'[kh][kw][co][ci] = W[R-1-kh][S-1-kw][ci][co]
+// (wcvt_batch mode 2 / sgd_wcvt fp32 jobs); else a wflip launch derives them
 void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, float* dx, float* ws,
                          hipStream_t st, bool bf16, const float* addend = nullptr,
-                         const void* dyb = nullptr);
+                         const void* dyb = nullptr, const float* wflip = nullptr);
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue);
 // Tile / split plan of the tiled family.  Production runs the defaults (the
 // measured choices, docs/PERF_NOTES.md); labs (scripts/conv_lab.py) change

@@ -1003,8 +1003,9 @@ void conv_bwd_data(const ConvShape& s, const float* dy, const float* w, float* d
     return conv_bwd_data_bf16(s, dy, w, dx, ws, st, dyb, addend, wtb, bstats);
   if (bstats && bstats->part)
     throw std::runtime_error("conv_bwd_data: BatchNorm backward statistics need the bf16 family");
-  if (conv_bwd_data_tiled_ok(s))
-    return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend, dyb);
+  if (conv_bwd_data_tiled_ok(s))  // fp32: wtb = the pre-flipped fp32 weights, when given
+    return conv_bwd_data_tiled(s, dy, w, dx, ws, st, bf16, addend, dyb,
+                               bf16 ? nullptr : static_cast<const float*>(wtb));
   if (!dy) throw std::runtime_error("conv_bwd_data: this shape needs the fp32 dY");
   if (addend) throw std::runtime_error("conv_bwd_data: no gradient-join epilogue for this shape");
   if (s.C < 32 && (long long)s.R * s.S * s.C * s.K <= DIRECT_W_MAX && (s.K == 8 || s.K == 16)) {

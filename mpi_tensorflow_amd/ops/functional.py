@@ -43,10 +43,16 @@ class Param:
     wtb_d: Optional[torch.Tensor] = None
 
 
-class Bf16Weights:
-    """bf16 re-laid copies of every MFMA-family conv weight (C, K % 64 == 0)
-    of a model - the forward layout [tap][co][ci] and the stride-1 dgrad
-    layout (taps reversed) - in one buffer.  Param.wtb / wtb_d point into it.
+class ConvWeightCopies:
+    """Re-laid copies of a model's conv weights that the conv kernels read
+    instead of the fp32 HWIO master weights, in one buffer.
+
+    kind "bf16" (bf16 conv mode): every MFMA-family conv weight (C, K % 64 ==
+    0) as the bf16 forward layout [tap][co][ci] (Param.wtb) and the bf16
+    stride-1 dgrad layout, taps reversed (Param.wtb_d).
+    kind "f32flip" (fp32 conv mode): every R x R (R > 1) conv weight with C, K
+    % 32 == 0 as the fp32 stride-1 dgrad weights, taps reversed and ci / co
+    transposed (Param.wtb_d; the tiled dgrad then skips its wflip launch).
 
     Kept current two ways: refresh() re-derives them all in ONE wcvt_batch
     launch (start of a run of steps, evaluation: any weight change made
@@ -55,28 +61,44 @@ class Bf16Weights:
     training step has no conversion launch of its own.  sgd() needs the flat
     parameter buffer (`flat`) the Params are views of."""
 
-    def __init__(self, params, device: torch.device, flat: Optional[torch.Tensor] = None):
+    def __init__(self, params, device: torch.device, flat: Optional[torch.Tensor] = None,
+                 kind: str = "bf16"):
         C = native()
-        eligible = [p for p in params.values()
-                    if p.value.dim() == 4 and p.value.shape[2] % 64 == 0 and p.value.shape[3] % 64 == 0]
-        self.buf = torch.empty(max(1, sum(2 * p.value.numel() for p in eligible)),
-                               dtype=torch.bfloat16, device=device)
+        if kind == "bf16":
+            eligible = [p for p in params.values() if p.value.dim() == 4
+                        and p.value.shape[2] % 64 == 0 and p.value.shape[3] % 64 == 0]
+            modes, dt = (0, 1), torch.bfloat16
+        elif kind == "f32flip":
+            eligible = [p for p in params.values() if p.value.dim() == 4
+                        and p.value.shape[0] == p.value.shape[1] and p.value.shape[0] > 1
+                        and p.value.shape[2] % 32 == 0 and p.value.shape[3] % 32 == 0]
+            modes, dt = (2,), torch.float32
+        else:
+            raise ValueError(kind)
+        self.kind = kind
+        self.buf = torch.empty(max(1, sum(len(modes) * p.value.numel() for p in eligible)),
+                               dtype=dt, device=device)
         rows, off, blocks = [], 0, 0
         sgd_jobs, sblocks = [], 0
         for p in eligible:
             R, S, Ci, K = p.value.shape
             n = p.value.numel()
             outs = []
-            for mode in (0, 1):
+            for mode in modes:
                 out = self.buf[off:off + n]
                 off += n
                 outs.append(out)
                 rows.append([ptr(p.value), ptr(out), R * S, Ci, K, mode, blocks, 0])
                 blocks += C.ops.wcvt_blocks(R * S, Ci, K)
-            p.wtb, p.wtb_d = outs
+            if kind == "bf16":
+                p.wtb, p.wtb_d = outs
+            else:
+                p.wtb_d = outs[0]
             if flat is not None:
                 woff = (p.value.data_ptr() - flat.data_ptr()) // 4
-                sgd_jobs.append([woff, ptr(outs[0]), ptr(outs[1]), R * S, Ci, K, sblocks, 0])
+                o1 = ptr(outs[1]) if len(outs) > 1 else 0
+                sgd_jobs.append([woff, ptr(outs[0]), o1, R * S, Ci, K, sblocks,
+                                 0 if kind == "bf16" else 1])
                 sblocks += C.ops.wcvt_blocks(R * S, Ci, K)
         self.njobs, self.nblocks = len(rows), blocks
         self.jobs = torch.tensor(rows if rows else [[0] * 8], dtype=torch.int64, device=device)
@@ -108,11 +130,14 @@ class Bf16Weights:
     def sgd(self, grads: torch.Tensor, mom: torch.Tensor, momentum: float, gscale: float,
             lr: torch.Tensor, step: Optional[torch.Tensor]) -> None:
         """w = flat params: g' = gscale g; m = momentum m + g'; w -= lr m, and
-        the bf16 layouts of the updated conv weights (one launch)."""
+        the copies of the updated conv weights (one launch)."""
         native().ops.sgd_wcvt(ptr(self.flat), ptr(grads), ptr(mom), momentum, gscale, 0.0,
                               ptr(lr), ptr(step), ptr(self.sgd_jobs), self.sgd_njobs,
                               self.sgd_conv_blocks, ptr(self.ranges), self.nranges,
                               self.range_blocks, stream_handle())
+
+
+Bf16Weights = ConvWeightCopies  # (the bf16 kind)
 
 
 def _empty(shape, like):

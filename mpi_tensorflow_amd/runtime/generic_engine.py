@@ -119,10 +119,14 @@ class GenericEngine:
             self.step_dev = torch.zeros(1, dtype=torch.int64).to(device)
             self.lr_dev = torch.zeros(1).to(device)
             self.seed = torch.ones(()).to(device)  # backward seed, never written
-            # bf16: the conv weights' bf16 layouts, written by the step's SGD
-            # launch (Bf16Weights.sgd) and re-derived at the start of a run
-            self.wcache = Fn.Bf16Weights(self.P, device, flat=self.params) if self.bf16 else None
-            self._wfresh = False  # the bf16 layouts match the fp32 weights
+            # the conv weights' re-laid copies (bf16 MFMA layouts; fp32: the
+            # flipped stride-1 dgrad weights), written by the step's SGD launch
+            # (ConvWeightCopies.sgd) and re-derived at the start of a run
+            self.wcache = Fn.ConvWeightCopies(self.P, device, flat=self.params,
+                                              kind="bf16" if self.bf16 else "f32flip")
+            if self.wcache.njobs == 0:  # (LeNet-5 etc.: nothing to keep)
+                self.wcache = None
+            self._wfresh = False  # the copies match the fp32 weights
 
     # ------------------------------------------------------------------ util
     def lr(self, step: Optional[int] = None) -> float:

@@ -818,17 +818,19 @@ def test_resnet18_bn_backward_epilogue_matches_pass(cuda_dev, shape, B):
     assert worst[0][1] < 3e-2, worst
 
 
-def test_sgd_writes_bf16_conv_layouts(cuda_dev):
-    """ResNet-18 bf16: the step's fused SGD (gops::sgd_wcvt) updates every
-    parameter bit-identically to the flat momentum SGD and writes the bf16
-    forward / dgrad layouts of the updated conv weights exactly as the
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_sgd_writes_conv_weight_copies(cuda_dev, dtype):
+    """ResNet-18: the step's fused SGD (gops::sgd_wcvt) updates every
+    parameter bit-identically to the flat momentum SGD and writes the conv
+    weights' re-laid copies - bf16: the MFMA forward / dgrad layouts; fp32:
+    the flipped, ci / co-transposed stride-1 dgrad weights - exactly as the
     wcvt_batch re-derivation does (so no conversion launch is needed)."""
     from mpi_tensorflow_amd.ops import native, ptr, stream_handle
     from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
     from mpi_tensorflow_amd.utils.data import synthetic_rows
 
     x, y = synthetic_rows("train", 0, 16, shape=(32, 32, 3))
-    eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=8, dtype="bf16",
+    eng = GenericEngine(C.TrainConfig(model="resnet18", batch_size=8, dtype=dtype,
                                       graph=False).validate(), x, y, cuda_dev)
     g = torch.Generator(device="cpu").manual_seed(5)
     grads = torch.randn(eng.layout.total, generator=g).to(cuda_dev)
@@ -837,13 +839,19 @@ def test_sgd_writes_bf16_conv_layouts(cuda_dev):
     step = torch.zeros(1, dtype=torch.int64, device=cuda_dev)
     w0 = eng.params.detach().clone()
     wc = eng.wcache
-    # reference: the flat SGD, then a full re-derivation of the layouts
+    assert wc is not None and wc.kind == ("bf16" if dtype == "bf16" else "f32flip")
+    # reference: the flat SGD, then a full re-derivation of the copies
     m_ref = mom.clone()
     native().optim.sgd_momentum(ptr(eng.params), ptr(grads), ptr(m_ref), eng.layout.total, 0, 0.0,
                                 0.9, 0.5, ptr(lr), 0.0, 0, stream_handle())
     wc.refresh()
     torch.cuda.synchronize()
     w_ref, buf_ref = eng.params.detach().clone(), wc.buf.clone()
+    if dtype == "fp32":  # the copy's layout: W'[kh][kw][co][ci] = W[R-1-kh][S-1-kw][ci][co]
+        p = eng.P["l1b0c2_w"]
+        R, S, Ci, K = p.value.shape
+        want = p.value.detach().flip(0).flip(1).permute(0, 1, 3, 2).contiguous()
+        assert torch.equal(p.wtb_d.view(R, S, K, Ci), want)
     # fused
     eng.params.data.copy_(w0)
     wc.buf.zero_()
@@ -852,5 +860,5 @@ def test_sgd_writes_bf16_conv_layouts(cuda_dev):
     assert int(step.item()) == 1
     assert torch.equal(eng.params.detach(), w_ref), "params differ from the flat SGD"
     assert torch.equal(mom, m_ref), "momentum differs from the flat SGD"
-    assert torch.equal(wc.buf, buf_ref), "bf16 layouts differ from wcvt_batch"
+    assert torch.equal(wc.buf, buf_ref), "weight copies differ from wcvt_batch"
     assert wc.sgd_njobs > 0 and wc.nranges > 0
