@@ -162,37 +162,55 @@ class ResNet18(GenericModel):
         return d
 
     def forward(self, P, bn, x, training):
+        # Every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
+        # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise.  In training
+        # each BatchNorm's statistics hand-offs are wired here, explicitly, by
+        # one Fn.BnLink: the producing conv writes the forward sums (bn_out),
+        # and the conv consuming the BatchNorm's output writes the backward sums
+        # from its dgrad (bn_in) - n1 -> c2 inside a block, a block's n2 -> the
+        # next block's c1 (whose dgrad also adds the shortcut's gradient, so its
+        # dX is the BatchNorm's whole dY).
+        links = {}
+
+        def link(nm):
+            if not (training and x.is_cuda):
+                return None
+            if nm not in links:
+                links[nm] = Fn.BnLink(bn[nm][0] if Fn.BN_FWD_EPILOGUE else None)
+            return links[nm]
+
+        def out_link(nm):  # the producing conv's forward statistics
+            lk = link(nm)
+            return lk if (lk is not None and lk.shift is not None) else None
+
         def BN(h, nm, relu, res=None, res_join=None, twin_only=False):
             rm, rv = bn[nm]
             return Fn.batchnorm(h, P[nm + "_g"], P[nm + "_b"], rm, rv, training, relu, res,
-                                res_join=res_join, twin_only=twin_only)
+                                res_join=res_join, twin_only=twin_only, link=link(nm))
 
-        # every conv feeds a BatchNorm: in bf16 mode its output is stored bf16
-        # (Fn.conv2d out_bf16; BN reads bf16 input), fp32 otherwise, and in
-        # training its epilogue also writes that BatchNorm's batch statistics
-        # (shifted by the running mean: Fn.conv2d bn_shift)
-        def sh(nm):
-            return bn[nm][0] if (training and Fn.BN_FWD_EPILOGUE) else None
-
-        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True, bn_shift=sh("bn1"))
+        h = Fn.conv2d(x, P["conv1_w"], None, 2, 3, out_bf16=True, bn_out=out_link("bn1"))
         h = BN(h, "bn1", True, twin_only=True)  # the pool reads its bf16 twin
         h = Fn.maxpool(h, 3, 2, 1)
         join = x.is_cuda and training and torch.is_grad_enabled()
+        h_bn = None  # the BatchNorm whose output h is (a block's n2)
         for name, cin, c, s, down in self._blocks():
             # the block input's two gradients (conv1, shortcut) meet in the
             # conv1 dgrad epilogue (Fn.GradJoin); the shortcut runs after c2
             # so its backward comes first
             j = Fn.GradJoin() if join else None
             o = Fn.conv2d(h, P[name + "c1_w"], None, s, 1, join=j, join_role="final",
-                          out_bf16=True, bn_shift=sh(name + "n1"))
+                          out_bf16=True, bn_out=out_link(name + "n1"),
+                          bn_in=link(h_bn) if h_bn else None)
             o = BN(o, name + "n1", True, twin_only=True)  # only conv c2 reads it
-            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True, bn_shift=sh(name + "n2"))
+            o = Fn.conv2d(o, P[name + "c2_w"], None, 1, 1, out_bf16=True,
+                          bn_out=out_link(name + "n2"), bn_in=link(name + "n1"))
             if down:
                 sc = Fn.conv2d(h, P[name + "ds_w"], None, s, 0, join=j, join_role="stash",
-                               out_bf16=True, bn_shift=sh(name + "nd"))
+                               out_bf16=True, bn_out=out_link(name + "nd"))
                 h = BN(o, name + "n2", True, res=BN(sc, name + "nd", False))
             else:
                 h = BN(o, name + "n2", True, res=h, res_join=j)
+            h_bn = name + "n2"
         h = Fn.global_avgpool(h)
         return Fn.linear(h, P["fc_w"], P["fc_b"])
 

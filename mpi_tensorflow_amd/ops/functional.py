@@ -233,27 +233,32 @@ def _bf16_copy(t: torch.Tensor, s) -> torch.Tensor:
     return tb
 
 
-# BatchNorm statistics written by the producing conv's epilogue (bf16 conv
-# mode): the channel-major partial sums of (y - shift) / (y - shift)^2 with
-# shift = the consuming BatchNorm's running mean, attached to the conv output
-# like the bf16 twins (valid while the tensor is unmodified).
-def _attach_bnstats(t: torch.Tensor, part: torch.Tensor, rows: int, shift: torch.Tensor) -> None:
-    t._mta_bnstats = (part, rows, shift, t._version, t.data_ptr())
+# BatchNorm statistics from the neighbouring convs, wired explicitly by the
+# model (models/generic.py) through one BnLink per BatchNorm and step:
+#   * forward: the conv producing the BatchNorm's input (conv2d(bn_out=L))
+#     writes the channel-major partial sums of its output shifted by
+#     L.shift (the BatchNorm's running mean) in its epilogue -> L.fwd; the
+#     BatchNorm (batchnorm(link=L)) then skips its statistics pass;
+#   * backward: the BatchNorm records what a dgrad needs for its backward
+#     sums (bf16 input x, the bf16 twin of y for the ReLU mask, mean, rstd)
+#     in L.bwd_src; the conv consuming the BatchNorm's output
+#     (conv2d(bn_in=L)) passes it to its dgrad, whose epilogue writes the
+#     sums of Sigma dY' and Sigma dY' x_hat -> L.bwd, and the BatchNorm
+#     backward skips its statistics pass when the dY it receives IS that dX.
+class BnLink:
+    """Statistics hand-offs of one BatchNorm for one forward + backward (see
+    above).  shift: the BatchNorm's running mean (the producer's epilogue
+    shifts its sums by it); the other fields are filled by the ops."""
+
+    __slots__ = ("shift", "fwd", "bwd_src", "bwd")
+
+    def __init__(self, shift: Optional[torch.Tensor] = None):
+        self.shift = shift
+        self.fwd = None      # (partial table, rows): the producer's forward sums
+        self.bwd_src = None  # (x, yb, mean, rstd, relu): set by the BatchNorm forward
+        self.bwd = None      # (partial table, rows, dX): the consumer dgrad's sums
 
 
-def _bnstats(t: torch.Tensor, rmean: torch.Tensor):
-    a = getattr(t, "_mta_bnstats", None)
-    if a is not None and a[2] is rmean and a[3] == t._version and a[4] == t.data_ptr():
-        return a[0], a[1]
-    return None
-
-
-# BatchNorm BACKWARD statistics written by the dgrad that produces the
-# BatchNorm's dY (bf16 conv mode).  The BatchNorm forward marks its output
-# with what that dgrad needs (its bf16 input x, the bf16 twin of its output
-# for the ReLU mask, mean, rstd); the consuming conv's backward passes it to
-# its dgrad, whose epilogue writes the partial table, attached to the dX it
-# returns; the BatchNorm backward then skips its statistics pass.
 # A/B switches of the BatchNorm statistics epilogues (set by tests and labs
 # through the setters below; production runs the defaults)
 _BNB_EPILOGUE = True
@@ -296,23 +301,6 @@ def set_bn_bwd_epilogue(on: bool) -> None:
     _BNB_EPILOGUE = bool(on)
 
 
-def _attach_bnbwd_src(y: torch.Tensor, x: torch.Tensor, yb: Optional[torch.Tensor],
-                      mean: torch.Tensor, rstd: torch.Tensor, relu: bool) -> None:
-    y._mta_bnbwd = (x, yb, mean, rstd, relu)
-
-
-def _attach_bnbwd_stats(dx: torch.Tensor, part: torch.Tensor, rows: int,
-                        mean: torch.Tensor) -> None:
-    dx._mta_bnbwdst = (part, rows, mean, dx._version, dx.data_ptr())
-
-
-def _bnbwd_stats(dy: torch.Tensor, mean: torch.Tensor):
-    a = getattr(dy, "_mta_bnbwdst", None)
-    if a is not None and a[2] is mean and a[3] == dy._version and a[4] == dy.data_ptr():
-        return a[0], a[1]
-    return None
-
-
 def _bf16_out(like: torch.Tensor) -> Optional[torch.Tensor]:
     """A bf16 twin for a BN output when a bf16 conv can consume it."""
     if not _CONV_BF16 or like.shape[-1] % 64 != 0:
@@ -353,7 +341,7 @@ class GradJoin:
 class _ConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, shape, relu, gw, gb, ws, join=None, role=None, wtb=None,
-                wtb_d=None, out_bf16=False, bn_shift=None):
+                wtb_d=None, out_bf16=False, bn_out=None, bn_in=None):
         C = native()
         x = x.contiguous()
         ctx.bf16 = _CONV_BF16
@@ -367,19 +355,20 @@ class _ConvFn(torch.autograd.Function):
         oshape = (shape.N, shape.OH, shape.OW, shape.K)
         y = torch.empty(oshape, dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
         part, rows = None, 0
-        if bn_shift is not None:  # the consuming BatchNorm's statistics
+        if bn_out is not None:  # the consuming BatchNorm's statistics
             # bf16 output: the bf16 family; fp32: the tiled forward (conv2d checks)
             rows = C.ops.conv_fwd_stats_rows(shape, bool(out_bf16))
             part = torch.empty(2 * shape.K * rows, dtype=torch.float32, device=x.device)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), 0 if out_bf16 else ptr(y), relu, ptr(ws), s,
                        ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0, ptr(part), rows,
-                       ptr(bn_shift) if part is not None else 0)
+                       ptr(bn_out.shift) if part is not None else 0)
         if part is not None:
-            _attach_bnstats(y, part, rows, bn_shift)
+            bn_out.fwd = (part, rows)
         ctx.save_for_backward(x, w, y, xb)
-        # x is a BatchNorm's output: the dgrad can write that BatchNorm's
-        # backward statistics (bf16 conv mode, bf16 BatchNorm input)
-        ctx.bnb = getattr(x, "_mta_bnbwd", None) if (ctx.bf16 and _BNB_EPILOGUE) else None
+        # x is a BatchNorm's output (bn_in): the dgrad can write that
+        # BatchNorm's backward statistics (bf16 conv mode, bf16 BatchNorm input)
+        ctx.bnb = bn_in if (ctx.bf16 and _BNB_EPILOGUE and bn_in is not None
+                            and bn_in.bwd_src is not None) else None
         ctx.shape, ctx.relu, ctx.gw, ctx.gb, ctx.ws = shape, relu, gw, gb, ws
         ctx.has_b = b is not None
         ctx.join, ctx.role, ctx.wtb_d = join, role, wtb_d
@@ -403,19 +392,19 @@ class _ConvFn(torch.autograd.Function):
                 add = ctx.join.take() if ctx.role == "final" else None
                 # the BatchNorm statistics need the final dX: not for a stashed
                 # branch, nor a join whose other half is still to be added
-                bnb = ctx.bnb if (ctx.role is None or (ctx.role == "final" and add is not None)) \
+                link = ctx.bnb if (ctx.role is None or (ctx.role == "final" and add is not None)) \
                     else None
                 part, prow = None, 0
-                if bnb is not None:
+                if link is not None:
                     prow = C.ops.conv_bwd_data_stats_rows(sh)
                     if prow > 0:
                         part = torch.empty(2 * sh.C * prow, dtype=torch.float32, device=dx.device)
                 if part is not None:
-                    bx, byb, bmean, brstd, brelu = bnb
+                    bx, byb, bmean, brstd, brelu = link.bwd_src
                     C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
                                         ptr(add), ptr(ctx.wtb_d), ptr(part), prow, ptr(bx),
                                         ptr(byb), ptr(bmean), ptr(brstd), brelu)
-                    _attach_bnbwd_stats(dx, part, prow, bmean)
+                    link.bwd = (part, prow, dx)
                 else:
                     C.ops.conv_bwd_data(sh, 0, ptr(w), ptr(dx), ptr(ctx.ws), s, True, ptr(dyb),
                                         ptr(add), ptr(ctx.wtb_d))
@@ -424,7 +413,7 @@ class _ConvFn(torch.autograd.Function):
                     dx = None
                 elif ctx.role == "final" and add is None:
                     ctx.join.out = dx
-            return dx, None, None, None, None, None, None, None, None, None, None, None, None, None
+            return (dx,) + (None,) * 14
         if ctx.relu:
             dym = torch.empty_like(dy)
             C.ops.relu_bwd(ptr(dy), ptr(y), ptr(dym), dy.numel(), s)
@@ -451,7 +440,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = None
             elif ctx.role == "final" and add is None:
                 ctx.join.out = dx
-        return dx, None, None, None, None, None, None, None, None, None, None, None, None, None
+        return (dx,) + (None,) * 14
 
 
 class _ConvIm2colFn(torch.autograd.Function):
@@ -464,7 +453,7 @@ class _ConvIm2colFn(torch.autograd.Function):
     stem)."""
 
     @staticmethod
-    def forward(ctx, x, w, shape, gw, ws, kp, out_bf16=False, bn_shift=None):
+    def forward(ctx, x, w, shape, gw, ws, kp, out_bf16=False, bn_out=None):
         C = native()
         x = x.contiguous()
         sh = shape
@@ -483,13 +472,13 @@ class _ConvIm2colFn(torch.autograd.Function):
         ctx.implicit = bool(out_bf16)
         if ctx.implicit:
             part, rows = None, 0
-            if bn_shift is not None:  # the consuming BatchNorm's statistics
+            if bn_out is not None:  # the consuming BatchNorm's statistics
                 rows = C.ops.conv_fwd_stem_stats_rows(s1)
                 part = torch.empty(2 * sh.K * rows, dtype=torch.float32, device=x.device)
             C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s, ptr(part), rows,
-                                     ptr(bn_shift) if part is not None else 0)
+                                     ptr(bn_out.shift) if part is not None else 0)
             if part is not None:
-                _attach_bnstats(y, part, rows, bn_shift)
+                bn_out.fwd = (part, rows)
             ctx.save_for_backward(x)
         else:
             col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
@@ -562,16 +551,17 @@ _WS = ConvWorkspace()
 def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: int = 0,
            relu: bool = False, join: Optional[GradJoin] = None,
            join_role: Optional[str] = None, out_bf16: bool = False,
-           bn_shift: Optional[torch.Tensor] = None) -> torch.Tensor:
+           bn_out: Optional[BnLink] = None, bn_in: Optional[BnLink] = None) -> torch.Tensor:
     """x [N,H,W,C] NHWC, w [R,S,C,K] HWIO -> [N,OH,OW,K].  join / join_role
     ("stash" | "final"): fuse the gradient sum at x with another branch (see
     GradJoin).  out_bf16: store the output as bf16 when the bf16 conv family
     runs it (no bias / ReLU epilogue) - for a conv whose only consumer is
-    `batchnorm`, which reads bf16 input.  bn_shift (training): that
-    BatchNorm's running mean - a bf16-output conv (or, in fp32 conv mode, the
-    tiled fp32 forward) then also writes the batch statistics in its epilogue
-    (shifted by it) and the BatchNorm skips its statistics pass.  All GPU
-    only, ignored on the CPU path."""
+    `batchnorm`, which reads bf16 input.  bn_out (training): the BnLink of
+    that BatchNorm - a bf16-output conv (or, in fp32 conv mode, the tiled fp32
+    forward) then also writes the batch statistics in its epilogue (shifted by
+    bn_out.shift) and the BatchNorm skips its statistics pass.  bn_in: the
+    BnLink of the BatchNorm whose output x is - the dgrad then writes that
+    BatchNorm's backward sums.  All GPU only, ignored on the CPU path."""
     N, H, W, Cin = x.shape
     R, S, _, K = w.value.shape
     if x.is_cuda and not _ORACLE:
@@ -583,10 +573,10 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             s1 = C.ops.ConvShape(N, sh.OH, sh.OW, kp, K, 1, 1, 1, 0)
             ws = _WS.get(max(C.ops.conv_ws_floats(s1, False), 4), x.device)
             return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob,
-                                       bn_shift if ob else None)
+                                       bn_out if ob else None)
         ob = ob and C.ops.conv_bf16_ok(sh)
         # fp32 conv mode: the tiled forward writes the statistics instead
-        st32 = bool(bn_shift is not None and not _CONV_BF16 and b is None and not relu and
+        st32 = bool(bn_out is not None and not _CONV_BF16 and b is None and not relu and
                     _BN_FWD_F32 and C.ops.conv_fwd_tiled_ok(sh) and K % 64 == 0 and
                     256 % (K // 4) == 0)
         nws = max(C.ops.conv_ws_floats(sh, b is not None or relu),
@@ -597,7 +587,7 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
             raise ValueError("conv2d: no gradient-join epilogue for this conv shape")
         return _ConvFn.apply(x, w.value, None if b is None else b.value, sh, relu, w.grad_view,
                              None if b is None else b.grad_view, ws, join, join_role, w.wtb,
-                             w.wtb_d, ob, bn_shift if (ob or st32) else None)
+                             w.wtb_d, ob, bn_out if (ob or st32) else None, bn_in)
     y = F.conv2d(x.permute(0, 3, 1, 2), w.value.permute(3, 2, 0, 1),
                  None if b is None else b.value, stride=stride, padding=pad).permute(0, 2, 3, 1)
     return F.relu(y) if relu else y
@@ -650,7 +640,7 @@ def linear(x: torch.Tensor, w: Param, b: Optional[Param], relu: bool = False) ->
 class _BNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, b, res, relu, gg, gb, rmean, rvar, momentum, eps, training,
-                res_join=None, twin_only=False):
+                res_join=None, twin_only=False, link=None):
         C = native()
         x = x.contiguous()
         Cc = x.shape[-1]
@@ -666,8 +656,9 @@ class _BNFn(torch.autograd.Function):
         yf = None if (twin_only and yb is not None) else y
         # batch statistics, running-stat update and the fused apply, on device;
         # the statistics come from the producing conv's epilogue when it wrote them
-        st = _bnstats(x, rmean)
+        st = link.fwd if link is not None else None
         if st is not None:
+            assert link.shift is rmean, "BnLink shift is not this BatchNorm's running mean"
             C.ops.bn_fwd_partials(ptr(st[0]), st[1], ptr(rmean), ptr(x), rows, Cc, ptr(g), ptr(b),
                                   ptr(res), ptr(yf), ptr(mean), ptr(rstd), eps, momentum, relu,
                                   ptr(rmean), ptr(rvar), stream_handle(), ptr(yb), xb16)
@@ -677,8 +668,9 @@ class _BNFn(torch.autograd.Function):
                          stream_handle(), ptr(yb), xb16)
         if yb is not None:
             _attach_bf16(y, yb)
-        if xb16 and (yb is not None or not relu):
-            _attach_bnbwd_src(y, x, yb, mean, rstd, relu)
+        if link is not None and xb16 and (yb is not None or not relu):
+            link.bwd_src = (x, yb, mean, rstd, relu)
+        ctx.link = link
         # the backward's ReLU mask reads the bf16 twin when there is one (same signs)
         ctx.yb16 = yb is not None
         ctx.save_for_backward(x, yb if yb is not None else y, mean, rstd, g)
@@ -705,7 +697,14 @@ class _BNFn(torch.autograd.Function):
         else:
             dx = torch.empty_like(dy)
             dxf, dxb = dx, _bf16_out(dx)
-        st = _bnbwd_stats(dy, mean) if (xb16 and (ctx.yb16 or not ctx.relu)) else None
+        st = None
+        link = ctx.link
+        if link is not None and link.bwd is not None and xb16 and (ctx.yb16 or not ctx.relu):
+            part, prow, dxc = link.bwd
+            # the sums are valid for exactly the dX that dgrad wrote
+            if dxc.data_ptr() == dy.data_ptr() and dxc._version == dy._version:
+                st = (part, prow)
+        ctx.link = None
         if _BN_ROUTE_HOOK is not None:
             _BN_ROUTE_HOOK("epilogue" if st is not None else "pass")
         if st is not None:  # the dgrad producing dy wrote the sums (see above)
@@ -722,23 +721,25 @@ class _BNFn(torch.autograd.Function):
         if dres is not None and ctx.res_join is not None:
             ctx.res_join.stash(dres)
             dres = None
-        return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, dres, None, None, None, None, None, None, None, None, None, None, None
 
 
 def batchnorm(x: torch.Tensor, g: Param, b: Param, rmean: torch.Tensor, rvar: torch.Tensor,
               training: bool, relu: bool = False, residual: Optional[torch.Tensor] = None,
               momentum: float = 0.1, eps: float = 1e-5,
-              res_join: Optional[GradJoin] = None, twin_only: bool = False) -> torch.Tensor:
+              res_join: Optional[GradJoin] = None, twin_only: bool = False,
+              link: Optional[BnLink] = None) -> torch.Tensor:
     """BatchNorm over N,H,W of an NHWC tensor, optional fused residual + ReLU.
     res_join: the residual's gradient is stashed there (GradJoin) instead of
     returned to autograd.  twin_only: the output's only consumer is a bf16
     conv - write just its bf16 twin (bf16 conv mode; the returned fp32 tensor
-    is not written).  Both GPU training only."""
+    is not written).  link: this BatchNorm's BnLink (statistics from / for
+    the neighbouring convs).  All GPU training only."""
     if x.is_cuda and not _ORACLE:
         res = None if residual is None else residual.contiguous()
         if training:
             return _BNFn.apply(x, g.value, b.value, res, relu, g.grad_view, b.grad_view, rmean,
-                               rvar, momentum, eps, True, res_join, twin_only)
+                               rvar, momentum, eps, True, res_join, twin_only, link)
         C = native()
         y = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         Cc = x.shape[-1]

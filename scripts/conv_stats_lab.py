@@ -1,5 +1,5 @@
 """Cost of the BatchNorm-statistics epilogue on the bf16 ResNet-18 convs:
-times conv2d(out_bf16=True) with and without bn_shift, back to back.
+times conv2d(out_bf16=True) with and without a BnLink (epilogue statistics), back to back.
     python scripts/conv_stats_lab.py"""
 import os
 import sys
@@ -29,11 +29,11 @@ def main():
         for shift in (None, rm):
             with torch.no_grad():
                 for _ in range(5):
-                    Fn.conv2d(x, w, None, st, pad, out_bf16=True, bn_shift=shift)
+                    Fn.conv2d(x, w, None, st, pad, out_bf16=True, bn_out=None if shift is None else Fn.BnLink(shift))
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
                 for _ in range(50):
-                    Fn.conv2d(x, w, None, st, pad, out_bf16=True, bn_shift=shift)
+                    Fn.conv2d(x, w, None, st, pad, out_bf16=True, bn_out=None if shift is None else Fn.BnLink(shift))
                 b.record()
                 b.synchronize()
                 res.append(a.elapsed_time(b) * 1000 / 50)

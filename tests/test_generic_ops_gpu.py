@@ -548,7 +548,7 @@ def test_conv_bf16_output_and_bf16_grad(cuda_dev, N, H, Cin, K, R, stride, pad):
 ])
 def test_conv_epilogue_bn_statistics(cuda_dev, N, H, Cin, K, R, stride, pad):
     """A bf16-output conv given the consuming BatchNorm's running mean
-    (bn_shift) writes the batch statistics in its epilogue and the BatchNorm
+    (a BnLink) writes the batch statistics in its epilogue and the BatchNorm
     skips its own statistics pass: the BN output, the running statistics and
     the gradients match the two-pass BatchNorm on the same conv output."""
     g = torch.Generator().manual_seed(17)
@@ -566,10 +566,10 @@ def test_conv_epilogue_bn_statistics(cuda_dev, N, H, Cin, K, R, stride, pad):
             xi = x.clone().requires_grad_(Cin % 4 == 0)
             wp, gp, bp = _param(w), _param(gam), _param(bet)
             rm, rv = rm0.clone(), torch.ones(K, device=cuda_dev)
-            y = Fn.conv2d(xi, wp, None, stride, pad, False, out_bf16=True,
-                          bn_shift=rm if fused else None)
-            assert (Fn._bnstats(y, rm) is not None) == fused
-            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True)
+            lk = Fn.BnLink(rm) if fused else None
+            y = Fn.conv2d(xi, wp, None, stride, pad, False, out_bf16=True, bn_out=lk)
+            assert (lk is not None and lk.fwd is not None) == fused
+            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True, link=lk)
             h.backward(dy)
             out.append((h.detach().clone(), rm.clone(), rv.clone(), wp.grad_view.clone(),
                         gp.grad_view.clone(), bp.grad_view.clone()))
@@ -608,10 +608,11 @@ def test_conv_epilogue_bn_statistics_fp32(cuda_dev, N, H, Cin, K, R, stride, pad
             xi = x.clone().requires_grad_(Cin % 4 == 0)
             wp, gp, bp = _param(w), _param(gam), _param(bet)
             rm, rv = rm0.clone(), torch.ones(K, device=cuda_dev)
-            y = Fn.conv2d(xi, wp, None, stride, pad, False, bn_shift=rm if fused else None)
+            lk = Fn.BnLink(rm) if fused else None
+            y = Fn.conv2d(xi, wp, None, stride, pad, False, bn_out=lk)
             assert y.dtype == torch.float32
-            assert (Fn._bnstats(y, rm) is not None) == fused
-            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True)
+            assert (lk is not None and lk.fwd is not None) == fused
+            h = Fn.batchnorm(y, gp, bp, rm, rv, True, relu=True, link=lk)
             h.backward(dy)
             out.append((h.detach().clone(), rm.clone(), rv.clone(), wp.grad_view.clone(),
                         gp.grad_view.clone(), bp.grad_view.clone()))
@@ -653,8 +654,9 @@ def test_dgrad_epilogue_bn_backward_statistics(cuda_dev, N, H, Cin, K, stride, r
             xi = x.clone().requires_grad_(True)
             gp, bp, wp = _param(gam), _param(bet), _param(w)
             rm, rv = torch.zeros(Cin, device=cuda_dev), torch.ones(Cin, device=cuda_dev)
-            h = Fn.batchnorm(xi, gp, bp, rm, rv, True, relu)
-            y = Fn.conv2d(h, wp, None, stride, 1, False, out_bf16=True)
+            lk = Fn.BnLink()  # no forward hand-off here: the BatchNorm runs its pass
+            h = Fn.batchnorm(xi, gp, bp, rm, rv, True, relu, link=lk)
+            y = Fn.conv2d(h, wp, None, stride, 1, False, out_bf16=True, bn_in=lk)
             y.backward(dy)
             assert routes.count("epilogue") - n0 == (1 if fused else 0)
             out.append((xi.grad.float().clone(), gp.grad_view.clone(), bp.grad_view.clone(),
