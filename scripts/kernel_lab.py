@@ -41,13 +41,24 @@ def main():
         "conv2_fwd_wino": lambda: k.conv2_fwd_wino(ptr(b["a1"]), B, W("conv2_weight"), ptr(b["wino_u"]),
                                                    W("conv2_bias"), ptr(b["a2"]), ptr(b["idx2"]),
                                                    ptr(b["w2t"]), s),
+        "conv12_fwd_wino": lambda: k.conv12_fwd_wino(
+            ptr(e.train_x), ptr(e.step_dev), e.n_local, B, W("conv1_weight"), W("conv1_bias"),
+            ptr(b["a1"]), ptr(b["a1pf"]), ptr(b["idx1"]), W("conv2_weight"), ptr(b["wino_u"]),
+            W("conv2_bias"), ptr(b["a2"]), ptr(b["idx2"]), 0, s, 0, ptr(b["a2ft"])),
         "conv2_bwd_data_wino": lambda: k.conv2_bwd_data_wino(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]),
                                                              B, ptr(b["da1m"]), s),
         "fc1_fwd": lambda: k.fc1_fwd_train(ptr(b["a2"]), W("fc1_weight"), B, ptr(b["fc1_part"]), s),
+        "fc1_fwd_t": lambda: k.fc1_fwd_train_t(ptr(b["a2ft"]), W("fc1_weight"), B, ptr(b["fc1_part"]),
+                                               s),
         "fc_head": lambda: k.fc_head_train(ptr(b["fc1_part"]), W("fc1_bias"), W("fc2_weight"), W("fc2_bias"),
                                            ptr(e.train_y), e.n_local, ptr(e.step_dev), B, 0.5, 1, 0, 0.01, 0.95,
                                            ptr(b["hd"]), ptr(b["dh"]), ptr(b["dlog"]), ptr(b["loss_rows"]),
                                            ptr(e.lr_dev), 0, s),
+        "fc_head[8]": lambda: k.fc_head_train(ptr(b["fc1_part"]), W("fc1_bias"), W("fc2_weight"),
+                                              W("fc2_bias"), ptr(e.train_y), e.n_local, ptr(e.step_dev),
+                                              B, 0.5, 1, 0, 0.01, 0.95, ptr(b["hd"]), ptr(b["dh"]),
+                                              ptr(b["dlog"]), ptr(b["loss_rows"]), ptr(e.lr_dev), 0, s,
+                                              k.fc1_train_t_splits()),
         "fc1_bwd": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]), ptr(b["dlog"]),
                                      W("fc1_weight"), B, G("fc1_weight"), G("fc1_bias"), G("fc2_weight"),
                                      G("fc2_bias"), ptr(b["dy2"]), ptr(b["dy2t"]), s),
