@@ -159,20 +159,28 @@ class GenericEngine:
 
     # ------------------------------------------------------------------ step
     def _step_gpu(self):
-        gscale = self.forward_backward_gpu()
+        if self.wcache is not None and not self._wfresh:
+            self.wcache.refresh()
+            self._wfresh = True
+        gscale = self._forward_backward()
         self.update_gpu(gscale)
 
     def forward_backward_gpu(self) -> float:
         """Batch gather + forward + backward into the flat grad buffer (plus
         the bucketed all-reduce when syncing); returns the gradient scale the
-        update must apply (1/world when the grads hold a cross-rank sum)."""
+        update must apply (1/world when the grads hold a cross-rank sum).
+        Public entry (tests, serial emulations): the caller may have changed
+        the weights, so the conv weight copies are re-derived first."""
+        if self.wcache is not None:
+            self.wcache.refresh()
+            self._wfresh = True
+        return self._forward_backward()
+
+    def _forward_backward(self) -> float:
         C_ = self._C
         Fn.set_conv_bf16(self.bf16)
         s = stream_handle()
         row = int(np.prod(self.xb.shape[1:]))
-        if self.wcache is not None and not self._wfresh:
-            self.wcache.refresh()
-            self._wfresh = True
         # the gather also writes this step's device LR (no separate LR launch)
         C_.ops.gather_batch(ptr(self.train_x), ptr(self.train_y), ptr(self.step_dev), self.n_local,
                             self.B, row, ptr(self.xb), ptr(self.yb), s, self.cfg.base_lr,
