@@ -432,6 +432,9 @@ class NativeMnistEngine(MnistEngineBase):
         steps = 0
         best = None
         self.exe.join(stream_handle())
+        # the candidates' steps take the derived weights (Winograd transforms,
+        # bf16 shadows) as current: derive them from the weights first
+        self.exe.refresh_shadows(stream_handle())
         snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
         for sched, name in self._tune_candidates():
             self._set_schedule(sched)
