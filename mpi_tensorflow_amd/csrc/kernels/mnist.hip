@@ -2414,8 +2414,6 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
     throw std::runtime_error("sgd_step: Winograd filters need both U and Ud");
   if (p.off_w2 % 4 || p.fc_end % 4)
     throw std::runtime_error("sgd_step: misaligned flat segments");
-  if (p.conv && p.part2 == nullptr && p.off_b1 != p.off_w1 + 800)
-    throw std::runtime_error("sgd_step: conv1 weight and bias must be adjacent");
   SgdFinArgs a{};
   if (p.fc_end > 0) {
     FcSgdArgs f{p.w, p.g, p.mom, p.fc_end, p.l2, p.momentum, p.lr, p.fc_rounds};
