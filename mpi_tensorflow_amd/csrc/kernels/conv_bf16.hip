@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void sgd_wcvt_kernel(const SgdWcvtArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const size_t o = (size_t)(c0 + ty + 8 * i) * K + k0 + tx;
-      const float ge = gv[i] * a.gscale + a.l2 * wv[i];
+      const float ge = __builtin_fmaf(a.l2, wv[i], gv[i] * a.gscale);
       const float m = a.momentum * mv[i] + ge;
       const float w = wv[i] - lr * m;
       a.w[base + o] = w;
@@ -248,10 +248,10 @@ __global__ __launch_bounds__(256) void sgd_wcvt_kernel(const SgdWcvtArgs a) {
   const long long stride = nb * 256;
   for (long long i = lo4 + (rb - Rr[2]) * 256 + tid; i < hi4; i += stride) {
     float4 wv = W4[i], gv = G4[i], mv = M4[i];
-    gv.x = gv.x * a.gscale + a.l2 * wv.x;
-    gv.y = gv.y * a.gscale + a.l2 * wv.y;
-    gv.z = gv.z * a.gscale + a.l2 * wv.z;
-    gv.w = gv.w * a.gscale + a.l2 * wv.w;
+    gv.x = __builtin_fmaf(a.l2, wv.x, gv.x * a.gscale);
+    gv.y = __builtin_fmaf(a.l2, wv.y, gv.y * a.gscale);
+    gv.z = __builtin_fmaf(a.l2, wv.z, gv.z * a.gscale);
+    gv.w = __builtin_fmaf(a.l2, wv.w, gv.w * a.gscale);
     mv.x = a.momentum * mv.x + gv.x;
     mv.y = a.momentum * mv.y + gv.y;
     mv.z = a.momentum * mv.z + gv.z;

@@ -2374,8 +2374,8 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
   }
   blk -= nconv2;
   const int lane = tid & 63;
-  // (gscale: the conv bias / conv1 grads go through the sgd4 expression form
-  // g * gs + 0 * w, as in optim::sgd_momentum_flat)
+  // (gscale: the conv bias / conv1 grads go through the sgd4 form
+  // fma(0, w, g * gs), as in optim::sgd_momentum_flat)
   if (blk < 16) {  // conv2 bias: one wave per channel
     const int co = blk * 4 + (tid >> 6);
     float s = 0.f;
@@ -2387,7 +2387,7 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
     }
     if (lane == 0) {
       float* w = a.w + a.off_b2 + co;
-      sgd_elem(w, a.mom + a.off_b2 + co, s * a.gscale + 0.f * *w, lr, a.momentum);
+      sgd_elem(w, a.mom + a.off_b2 + co, __builtin_fmaf(0.f, *w, s * a.gscale), lr, a.momentum);
     }
     return;
   }
@@ -2403,7 +2403,8 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
     for (int b = lane; b < a.nblk1; b += 64) s += a.part1[(size_t)b * 832 + o];
     s = wave_sum(s);
   }
-  if (lane == 0) sgd_elem(a.w + off, a.mom + off, s * a.gscale + 0.f * a.w[off], lr, a.momentum);
+  if (lane == 0)
+    sgd_elem(a.w + off, a.mom + off, __builtin_fmaf(0.f, a.w[off], s * a.gscale), lr, a.momentum);
 }
 
 void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {

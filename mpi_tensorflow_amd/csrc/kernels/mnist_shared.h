@@ -175,10 +175,12 @@ __device__ inline void conv1_filter_unit(int unit, int batch, const C1Filter& c,
 // so every SGD path of the step rounds identically)
 __device__ __forceinline__ void sgd4(float4& wv, float4& mv, float4 gv, float lc, float lr,
                                      float mu, float gs = 1.f) {
-  gv.x = gv.x * gs + lc * wv.x;
-  gv.y = gv.y * gs + lc * wv.y;
-  gv.z = gv.z * gs + lc * wv.z;
-  gv.w = gv.w * gs + lc * wv.w;
+  // explicit fma: the same rounding in every kernel that inlines this (a
+  // free contraction of g * gs + lc * w may fuse either product)
+  gv.x = __builtin_fmaf(lc, wv.x, gv.x * gs);
+  gv.y = __builtin_fmaf(lc, wv.y, gv.y * gs);
+  gv.z = __builtin_fmaf(lc, wv.z, gv.z * gs);
+  gv.w = __builtin_fmaf(lc, wv.w, gv.w * gs);
   mv.x = mu * mv.x + gv.x;
   mv.y = mu * mv.y + gv.y;
   mv.z = mu * mv.z + gv.z;

@@ -23,10 +23,11 @@ __global__ __launch_bounds__(256) void sgd_momentum_flat_kernel(
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     float4 wv = w[i], gv = g[i], mv = mom[i];
     const float lc = i < l2_end4 ? l2 : 0.f;
-    gv.x = gv.x * gscale + lc * wv.x;
-    gv.y = gv.y * gscale + lc * wv.y;
-    gv.z = gv.z * gscale + lc * wv.z;
-    gv.w = gv.w * gscale + lc * wv.w;
+    // explicit fma (mnist_shared.h sgd4 rounds identically)
+    gv.x = __builtin_fmaf(lc, wv.x, gv.x * gscale);
+    gv.y = __builtin_fmaf(lc, wv.y, gv.y * gscale);
+    gv.z = __builtin_fmaf(lc, wv.z, gv.z * gscale);
+    gv.w = __builtin_fmaf(lc, wv.w, gv.w * gscale);
     mv.x = momentum * mv.x + gv.x;
     mv.y = momentum * mv.y + gv.y;
     mv.z = momentum * mv.z + gv.z;

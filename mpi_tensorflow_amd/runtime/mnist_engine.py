@@ -180,10 +180,13 @@ class NativeMnistEngine(MnistEngineBase):
     kind = "native"
 
     def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None,
-                 force_sync: bool = False, fc1_staged: bool = False):
-        """fc1_staged: the fp32 Winograd step's fc1 forward stages its operands
-        through LDS (fc1_fwd_kernel) instead of reading the feature-major a2t
-        copy the conv2 forward writes (fc1_fwd_t_kernel) - kernel labs only."""
+                 force_sync: bool = False, fc1_feature_major: bool = False):
+        """fc1_feature_major (labs): the fp32 Winograd step's conv2 forward
+        also writes a2 feature-major and the fc1 forward reads its operands
+        straight from L2 (fc1_fwd_t_kernel) instead of staging them through
+        LDS.  Equal in isolation (8.0 vs 8.3 us), but 3 us SLOWER in the step
+        (10.0 vs 6.9 us: the 4-byte scattered a2t stores of 256 blocks leave
+        partial lines in every XCD's L2), so off (docs/PERF_NOTES.md)."""
         super().__init__(cfg, train_x, train_y, device, rank, world, comm)
         if force_sync and comm is not None:  # exercise the collective path at world 1
             self.grad_sync = True
@@ -225,7 +228,7 @@ class NativeMnistEngine(MnistEngineBase):
                              wino_ud=torch.empty(36 * 64 * 32, **f32),
                              # the filter gradient's point slabs replace the 25-tap ones
                              part2=torch.empty(k.part2_floats_wino(B), **f32))
-            if not fc1_staged:  # a2 feature-major, the fc1 forward's direct operand
+            if fc1_feature_major:  # a2 feature-major, the fc1 forward's direct operand
                 self.bufs["a2ft"] = torch.empty(M.FC1_IN * B, **f32)
         self.fac = None
         hcomm = comm.native_handle if (self.grad_sync and comm is not None) else None

@@ -22,7 +22,7 @@ def main():
     dev = torch.device("cuda:0")
     x, y = synthetic_rows("train", 0, 4096)
     cfg = C.TrainConfig(batch_size=a.batch, graph=False).validate()
-    e = NativeMnistEngine(cfg, x, y, dev)
+    e = NativeMnistEngine(cfg, x, y, dev, fc1_feature_major=True)  # + the a2ft lab buffer
     e.train(5)
     e.forward_backward_only()
     torch.cuda.synchronize()

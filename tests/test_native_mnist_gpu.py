@@ -303,7 +303,8 @@ def test_fc1_forward_feature_major_matches_staged(cuda_dev, batch):
     assert _rel(ht, ref) < 1e-6 and _rel(hs, ref) < 1e-6
     # the conv2 forward's feature-major copy
     x, y = synthetic_rows("train", 0, 4 * batch)
-    e = NativeMnistEngine(C.TrainConfig(batch_size=batch, graph=False).validate(), x, y, cuda_dev)
+    e = NativeMnistEngine(C.TrainConfig(batch_size=batch, graph=False).validate(), x, y, cuda_dev,
+                          fc1_feature_major=True)
     e.forward_backward_only()
     torch.cuda.synchronize()
     a2n = e.bufs["a2"].view(batch, M.FC1_IN)
