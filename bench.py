@@ -56,7 +56,8 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
-    ap.add_argument("--sync-schedule", default="auto", choices=("auto", "buckets", "sharded", "split", "factors"))
+    ap.add_argument("--sync-schedule", default="auto",
+                    choices=("auto", "buckets", "sharded", "split", "factors", "serial"))
     ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "torch"),
                     help="device communicator (auto: RCCL, or shared memory when ranks share GPUs)")
     ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),

@@ -65,7 +65,7 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
 # "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
 # compute stream over a second communicator
-SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors")
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial")
 # device communicator (world > 1): "auto" = native RCCL when every rank has a
 # GPU of its own, the shared-memory host-staged communicator when ranks share
 # GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",

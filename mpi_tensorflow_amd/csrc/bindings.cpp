@@ -762,6 +762,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_SHARDED_FC") = (int)MnistExecutor::SCHED_SHARDED_FC;
   m.attr("MnistExecutor").attr("SCHED_SPLIT") = (int)MnistExecutor::SCHED_SPLIT;
   m.attr("MnistExecutor").attr("SCHED_FACTORS") = (int)MnistExecutor::SCHED_FACTORS;
+  m.attr("MnistExecutor").attr("SCHED_SERIAL") = (int)MnistExecutor::SCHED_SERIAL;
 
   // ----------------------------------------------------------------- IDX
   // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())

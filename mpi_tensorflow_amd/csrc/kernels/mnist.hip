@@ -1907,26 +1907,41 @@ __global__ __launch_bounds__(256) void conv1_bwd_filter_kernel(int batch, const 
 }
 
 // ------------------------------------------------------------ finalize ----
-// conv2: one thread per dW2 output summing the G image-group slabs; db2 from
-// the 2G centre-tap partials.  conv1: one wave per output (lanes stride over
-// the per-block slabs) + wave reduction.
+// conv2: one thread per dW2 float4 summing the G image-group slabs in group
+// order, 16 slab loads in flight (the sum order of sgd_finalize's
+// conv2_grad4: the world-1 and world > 1 conv gradients agree bit for bit);
+// db2 from the 4G centre-tap partials.  conv1: one wave per output (lanes
+// stride over the per-block slabs) + wave reduction.
 __global__ __launch_bounds__(256) void grad_finalize_kernel(
     const float* __restrict__ part2, const float* __restrict__ part_db2, int ngroups,
     const float* __restrict__ part1, int nblk1, float* __restrict__ g_w2,
     float* __restrict__ g_b2, float* __restrict__ g_w1, float* __restrict__ g_b1) {
-  constexpr int B2 = 51200 / 256;
+  constexpr int B2 = 51200 / 4 / 256;  // 50 blocks of float4
   if ((int)blockIdx.x < B2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    float s = 0.f;
-    {
-      if (ngroups == 16) {
+    const float4* p2 = reinterpret_cast<const float4*>(part2) + i;
+    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 16 <= ngroups; z += 16) {
+      float4 v[16];
 #pragma unroll
-        for (int z = 0; z < 16; ++z) s += part2[(size_t)z * 51200 + i];
-      } else {
-        for (int z = 0; z < ngroups; ++z) s += part2[(size_t)z * 51200 + i];
+      for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        sv.x += v[u].x;
+        sv.y += v[u].y;
+        sv.z += v[u].z;
+        sv.w += v[u].w;
       }
-      g_w2[i] = s;
     }
+    for (; z < ngroups; ++z) {
+      const float4 v = p2[(size_t)z * 12800];
+      sv.x += v.x;
+      sv.y += v.y;
+      sv.z += v.z;
+      sv.w += v.w;
+    }
+    reinterpret_cast<float4*>(g_w2)[i] = sv;
     return;
   }
   if ((int)blockIdx.x < B2 + 16) {  // db2: one wave per channel
@@ -1941,6 +1956,7 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(
   const int lane = threadIdx.x & 63;
   if (o >= 832) return;
   float s = 0.f;
+#pragma unroll 8
   for (int b = lane; b < nblk1; b += 64) s += part1[(size_t)b * 832 + o];
   s = wave_sum(s);
   if (lane == 0) {
@@ -2454,7 +2470,9 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s) {
-  const int b2 = 51200 / 256 + 16;
+  if (reinterpret_cast<uintptr_t>(g_w2) % 16 || reinterpret_cast<uintptr_t>(part2) % 16)
+    throw std::runtime_error("grad_finalize: dW2 / slabs must be 16-byte aligned");
+  const int b2 = 51200 / 4 / 256 + 16;
   const int b1 = cdiv(832, 4);
   grad_finalize_kernel<<<b2 + b1, 256, 0, s>>>(part2, part2 + (size_t)ngroups * 51200, ngroups,
                                                part1, nblk1, g_w2, g_b2, g_w1, g_b1);

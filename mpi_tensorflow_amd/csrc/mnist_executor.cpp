@@ -286,7 +286,7 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
-      sched != SCHED_FACTORS)
+      sched != SCHED_FACTORS && sched != SCHED_SERIAL)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -372,6 +372,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   }
   if (sched_ == SCHED_SHARDED_FC && sharded_ok(comm->size())) {
     train_step_sharded(s, comm, cs);
+    return;
+  }
+  if (sched_ == SCHED_SERIAL) {
+    train_step_serial(s, comm);
     return;
   }
   if (sched_ == SCHED_FACTORS && factors_ok(comm->size())) {
@@ -538,6 +542,27 @@ void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStrea
   mnist::launch_fc1_bwd_weights(a2, dh, hd, dl, n * p.batch, G + p.off_w3, G + p.off_b3,
                                 G + p.off_w4, G + p.off_b4, s);
   HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  if (fused)
+    sgd_step(s, gscale, true, true);
+  else
+    sgd_range(s, 0, p.total, gscale, true);
+}
+
+// Serial schedule: the whole step on ONE queue.  In graph replay every
+// cross-queue event edge costs 5-18 us of idle queue (docs/PERF_NOTES.md)
+// whether or not its event is done; the overlapped schedules pay 3 of them per
+// step.  Here the collective simply runs in stream order after the slab
+// reduction - one all-reduce of the whole 6.65 MB flat gradient (fp32 or the
+// bf16 wire) - followed by the one SGD launch: no fork, no join, no overlap.
+// It wins where the fabric makes the all-reduce shorter than the edges it
+// saves (the startup autotune decides, on the real communicator).
+void MnistExecutor::train_step_serial(hipStream_t s, Collective* comm) {
+  const MnistPtrs& p = p_;
+  const float gscale = 1.0f / (float)comm->size();
+  const bool fused = fused_sgd_ok();
+  wait_fc_params(s);
+  enqueue_fwd_bwd(s, true, nullptr, false, fused);
+  reduce_bucket(comm, 0, p.total, s);
   if (fused)
     sgd_step(s, gscale, true, true);
   else

@@ -102,8 +102,12 @@ class MnistExecutor {
   //                      all-reducing the 6.45 MB FC gradient, then form the
   //                      global FC gradients on every rank (see
   //                      train_step_factors).
+  //   SCHED_SERIAL     - no second queue at all: one all-reduce of the whole
+  //                      flat gradient on the compute stream after the slab
+  //                      reduction, then the SGD (no cross-queue edges, no
+  //                      overlap; see train_step_serial).
   static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
-                       SCHED_FACTORS = 3;
+                       SCHED_FACTORS = 3, SCHED_SERIAL = 4;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
@@ -165,6 +169,7 @@ class MnistExecutor {
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void train_step_factors(hipStream_t s, Collective* comm, hipStream_t cs);
+  void train_step_serial(hipStream_t s, Collective* comm);
   void wait_fc_params(hipStream_t s);
   // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
   void reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs);

@@ -38,7 +38,7 @@ from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
 # sync_schedule="auto": the single-communicator gradient-sync schedules
-# (buckets / sharded / factors (fp32), csrc/mnist_executor.h) are timed on real
+# (buckets / serial / sharded / factors (fp32), csrc/mnist_executor.h) are timed on real
 # training steps and the fastest is kept; all ranks take
 # the decision from the same (max-over-ranks) timings.  The two-communicator
 # "split" schedule (fastest against the comm-emulated 8-rank ring,
@@ -309,9 +309,8 @@ class NativeMnistEngine(MnistEngineBase):
         self._graphs: Dict[tuple, torch.cuda.CUDAGraph] = {}
         self.use_graph = cfg.graph and getattr(self.comm, "kind", "") != "host-staged"
         self.graph_steps = max(1, cfg.graph_steps)
-        self._tuned = not (self.grad_sync and cfg.sync_schedule == "auto" and self.use_graph
-                           and (self.exe.sharded_ok(self._native_comm.size)
-                                or self.exe.factors_ok(self._native_comm.size)))
+        # (auto always has >= 2 candidates: buckets and serial)
+        self._tuned = not (self.grad_sync and cfg.sync_schedule == "auto" and self.use_graph)
         self.tune_log: Dict[str, float] = {}
         self.tune_steps_run = 0
         self._eval_ws = None
@@ -344,6 +343,8 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_SPLIT
         if name == "factors" and self.exe.factors_ok(nranks):
             return E.SCHED_FACTORS
+        if name == "serial":
+            return E.SCHED_SERIAL
         return E.SCHED_BUCKETS  # "auto" until tuned
 
     def _set_schedule(self, sched: int) -> None:
@@ -362,7 +363,8 @@ class NativeMnistEngine(MnistEngineBase):
             return "none"
         E = self._C.MnistExecutor
         return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
-                E.SCHED_FACTORS: "factors"}.get(self.exe.schedule, "buckets")
+                E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial"}.get(self.exe.schedule,
+                                                                           "buckets")
 
     def sync_optimizer_state(self) -> None:
         if self.grad_sync:
@@ -404,7 +406,7 @@ class NativeMnistEngine(MnistEngineBase):
     def _tune_candidates(self):
         E = self._C.MnistExecutor
         n = self._native_comm.size
-        cands = [(E.SCHED_BUCKETS, "buckets")]
+        cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SERIAL, "serial")]
         if self.exe.sharded_ok(n):
             cands.append((E.SCHED_SHARDED_FC, "sharded"))
         # the factor schedule forms the FC gradients in another summation

@@ -75,7 +75,7 @@ def run_fixed(di, sched, dtype, kind, wire="fp32"):
 
 
 def scenario_mnist(di, dtype):
-    scheds = ["buckets", "sharded", "split"] + (["factors"] if dtype == "fp32" else [])
+    scheds = ["buckets", "sharded", "split", "serial"] + (["factors"] if dtype == "fp32" else [])
     eager = {}
     for sched in scheds:
         e, _ = run_fixed(di, sched, dtype, "eager")
@@ -83,7 +83,7 @@ def scenario_mnist(di, dtype):
         same(c, e, f"{sched} captured vs eager")
         eager[sched] = e
         assert len(eng._graphs) == 2, "expected the 3-step and the 1-step graph"
-    for sched in ("sharded", "split"):  # bit-identical schedules
+    for sched in ("sharded", "split", "serial"):  # bit-identical schedules
         same(eager[sched], eager["buckets"], f"{sched} vs buckets")
     # bf16 gradient wire, captured
     for sched in ("buckets", "sharded"):
@@ -103,7 +103,8 @@ def scenario_mnist(di, dtype):
     # captured switching sequence (what a re-tune does mid-run) vs the same
     # sequence eagerly
     E = native().MnistExecutor
-    seq = [E.SCHED_BUCKETS, E.SCHED_SHARDED_FC] + ([E.SCHED_FACTORS] if dtype == "fp32" else [])
+    seq = [E.SCHED_BUCKETS, E.SCHED_SHARDED_FC, E.SCHED_SERIAL] + (
+        [E.SCHED_FACTORS] if dtype == "fp32" else [])
     seq.append(E.SCHED_BUCKETS)
     outs = []
     for kind in ("eager", "shm"):
