@@ -20,6 +20,12 @@ struct FcSgdArgs {
   uint16_t* w1t = nullptr;
   long long w1 = 0;
   float gscale = 1.f;  // world > 1: the grads are the rank sum (1 / ranks)
+  // fp32 single rank, Winograd bwd-data launch: the fc1 weight's gradient is
+  // formed in the SGD itself (dW1 = a2^T dh tiles, no g round trip; fc1
+  // backward then runs without its dW1 role); w1 = the fc1 weight's offset
+  const float* a2 = nullptr;
+  const float* dh = nullptr;
+  int batch = 0;
 };
 // conv1 filter-grad role appended to a conv2 filter-gradient launch (its input
 // dA1m must be final: the conv2 bwd-data launch ran before)
@@ -167,6 +173,10 @@ struct SgdStepArgs {
   uint16_t* w1b = nullptr;
   uint16_t* w1t = nullptr;
   long long off_w1fc = 0;
+  // fused fc1 weight gradient in the FC role (FcSgdArgs::a2; single rank)
+  const float* a2 = nullptr;
+  const float* dh = nullptr;
+  int batch = 0;
   bool conv = true;
   int off_w2 = 0, off_b2 = 0, off_w1 = 0, off_b1 = 0;
   const float* part2 = nullptr;

@@ -464,16 +464,9 @@ __device__ __forceinline__ void fc1_bwd_dx(int L, const float* __restrict__ a2,
   const int lr = lane >> 4, lk = (lane & 15) * 4;
   const float* ap = dh + (size_t)(m0 + lr) * FC1_OUT + wave * 128 + lk;
   const float* bp = w1 + (size_t)(n0 + lr) * FC1_OUT + wave * 128 + lk;
-  float4 a[2][8], b[2][8];
-#pragma unroll
-  for (int rho = 0; rho < 2; ++rho)
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      a[rho][i] = *reinterpret_cast<const float4*>(ap + (size_t)4 * i * FC1_OUT + 64 * rho);
-      b[rho][i] = *reinterpret_cast<const float4*>(bp + (size_t)4 * i * FC1_OUT + 64 * rho);
-    }
   // epilogue operands of this wave's 4 accumulator registers (k = 4 wave + j),
-  // prefetched so their latency hides under the MFMAs
+  // issued first so their latency hides under the MFMAs (the scheduler
+  // otherwise sinks them behind the products)
   const int fi = n0 + r;  // (py, px, co) flat feature index
   float relu_in[4];
   int qsel[4];
@@ -483,6 +476,15 @@ __device__ __forceinline__ void fc1_bwd_dx(int L, const float* __restrict__ a2,
     relu_in[j] = a2[(size_t)n * FC1_IN + fi];
     qsel[j] = idx2[(size_t)n * FC1_IN + fi];
   }
+  float4 a[2][8], b[2][8];
+#pragma unroll
+  for (int rho = 0; rho < 2; ++rho)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[rho][i] = *reinterpret_cast<const float4*>(ap + (size_t)4 * i * FC1_OUT + 64 * rho);
+      b[rho][i] = *reinterpret_cast<const float4*>(bp + (size_t)4 * i * FC1_OUT + 64 * rho);
+    }
+  __builtin_amdgcn_sched_barrier(0);
   f32x16 c0 = zero16(), c1 = zero16();
 #pragma unroll
   for (int rho = 0; rho < 2; ++rho) {
@@ -534,40 +536,91 @@ __device__ __forceinline__ void fc1_bwd_dx(int L, const float* __restrict__ a2,
   }
 }
 
-__device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
-                                           const float* __restrict__ dh, int batch,
-                                           float* __restrict__ g_w3) {
-  const int mt = L >> 1;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int m0 = mt * 32, n0 = (L & 1) * 256 + wave * 64;
+// one wave's 32 x 64 part of dW1 tile L (32 features x 256 hidden; wave w of
+// 4 takes hidden columns 64 w .. 64 w + 63): c0 / c1 = columns n0 .. n0 + 31 /
+// n0 + 32 .. n0 + 63, rows m0 + mfma32_row(k, lane)
+__device__ __forceinline__ void fc1_dw_tile(int L, const float* __restrict__ a2,
+                                            const float* __restrict__ dh, int batch, int wave,
+                                            f32x16& c0, f32x16& c1, int& m0, int& n0) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  m0 = (L >> 1) * 32;
+  n0 = (L & 1) * 256 + wave * 64;
   const float* ap = a2 + m0 + r;
   const float* bp = dh + n0 + r;
-  f32x16 c0 = zero16(), c1 = zero16();
+  c0 = zero16();
+  c1 = zero16();
   for (int k0 = 0; k0 < batch; k0 += 64) {  // 32 MFMA steps (k = k0 + 2t + h)
     float av[32], b0[32], b1[32];
 #pragma unroll
     for (int t = 0; t < 32; ++t) {
-      const int k = k0 + 2 * t + h;
-      const int kc = min(k, batch - 1);
-      const bool ok = k < batch;
-      const float x = ap[(size_t)kc * FC1_IN];
-      const float y0 = bp[kc * FC1_OUT], y1 = bp[kc * FC1_OUT + 32];
-      av[t] = ok ? x : 0.f;
-      b0[t] = y0;
-      b1[t] = y1;
+      const int kc = min(k0 + 2 * t + h, batch - 1);
+      av[t] = ap[(size_t)kc * FC1_IN];
+      b0[t] = bp[kc * FC1_OUT];
+      b1[t] = bp[kc * FC1_OUT + 32];
     }
+    // all 96 loads issued before the first product: left to itself the
+    // scheduler interleaves them with the MFMA chain (one load + wait per
+    // MFMA), exposing the L2-miss latency several times over (12 us alone)
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = 0; t < 32; ++t)
+      if (k0 + 2 * t + h >= batch) av[t] = 0.f;
 #pragma unroll
     for (int t = 0; t < 32; ++t) {
       c0 = mfma32x32x2(av[t], b0[t], c0);
       c1 = mfma32x32x2(av[t], b1[t], c1);
     }
   }
+}
+
+__device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
+                                           const float* __restrict__ dh, int batch,
+                                           float* __restrict__ g_w3, int wave) {
+  f32x16 c0, c1;
+  int m0, n0;
+  fc1_dw_tile(L, a2, dh, batch, wave, c0, c1, m0, n0);
+  const int lane = threadIdx.x & 63, r = lane & 31;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int m = m0 + mfma32_row(k, lane);
     g_w3[(size_t)m * FC1_OUT + n0 + r] = c0[k];
     g_w3[(size_t)m * FC1_OUT + n0 + 32 + r] = c1[k];
   }
+}
+
+// single rank: dW1 tile L formed and applied at once - momentum SGD of those
+// fc1 weights (the sgd4 expression forms, so the parameters match the
+// gradient-buffer path bit for bit).  Runs as the tail of the Winograd
+// bwd-data blocks (256 VGPRs there: the weight / momentum loads follow the
+// products, one accumulator at a time).  tid: index in the 256-thread unit
+__device__ __forceinline__ void fc1_dw_sgd(const FcSgd& a, int L, int tid) {
+  const int lane = tid & 63, r = lane & 31;
+  f32x16 c0, c1;
+  int m0, n0;
+  fc1_dw_tile(L, a.a2, a.dh, a.batch, tid >> 6, c0, c1, m0, n0);
+  float* w = a.w + (size_t)a.w1_off4 * 4;
+  float* mo = a.m + (size_t)a.w1_off4 * 4;
+  const float lr = *a.lr;
+  auto apply = [&](const f32x16 c, int col) {
+    float wv[16], mv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const size_t e = (size_t)(m0 + mfma32_row(k, lane)) * FC1_OUT + col;
+      wv[k] = w[e];
+      mv[k] = mo[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const float g = __builtin_fmaf(a.l2, wv[k], c[k] * a.gs);
+      mv[k] = a.mu * mv[k] + g;
+      wv[k] -= lr * mv[k];
+      const size_t e = (size_t)(m0 + mfma32_row(k, lane)) * FC1_OUT + col;
+      w[e] = wv[k];
+      mo[e] = mv[k];
+    }
+  };
+  apply(c0, n0 + r);
+  apply(c1, n0 + 32 + r);
 }
 
 __global__ __launch_bounds__(256) void fc1_bwd_kernel(
@@ -577,19 +630,19 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     float* __restrict__ g_b4, float* __restrict__ dy2, float* __restrict__ dy2t, int roles) {
   // dy2: NHWC [n][14][14][64]; dy2t: channel-major, zero-bordered
   // [n][64][18][MNIST32_T_LD] (its border is never written)
-  constexpr int S_DX = 4 * FC1DX_WAVE, S_SMALL = 4 * (NCLS + 1) * 64;
+  constexpr int S_DX = 4 * FC1DX_WAVE, S_SMALL = FC1_SMALL_SMEM;
   __shared__ float smem[S_DX > S_SMALL ? S_DX : S_SMALL];
-  const int n_dx = (batch / 32) * (FC1_IN / 32);
+  // the grid holds the blocks of the roles asked for, in the order dX, dW1,
+  // small (launch_fc1_bwd)
+  const int n_dx = (roles & 1) ? (batch / 32) * (FC1_IN / 32) : 0;
+  const int n_dw = (roles & 2) ? FC1BWD_DW_BLOCKS : 0;
   const int L = xcd_remap(blockIdx.x, gridDim.x);
-  const int role = L < n_dx ? 0 : (L < n_dx + FC1BWD_DW_BLOCKS ? 1 : 2);
-  if (!((roles >> role) & 1)) return;
-  if (L < n_dx) {
+  if (L < n_dx)
     fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, dy2t, smem);
-  } else if (L < n_dx + FC1BWD_DW_BLOCKS) {
-    fc1_bwd_dw(L - n_dx, a2, dh, batch, g_w3);
-  } else {
-    fc1_small_grads(L - n_dx - FC1BWD_DW_BLOCKS, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
-  }
+  else if (L < n_dx + n_dw)
+    fc1_bwd_dw(L - n_dx, a2, dh, batch, g_w3, threadIdx.x >> 6);
+  else
+    fc1_small_grads(L - n_dx - n_dw, hd, dh, dlog, batch, g_w4, g_b4, g_b3, smem);
 }
 
 // FC weight gradients from GATHERED factors (SCHED_FACTORS): dW1 = A^T DH,
@@ -602,10 +655,10 @@ __global__ __launch_bounds__(256) void fc1_bwd_weights_kernel(
     const float* __restrict__ a2, const float* __restrict__ dh, const float* __restrict__ hd,
     const float* __restrict__ dlog, int rows, float* __restrict__ g_w3, float* __restrict__ g_b3,
     float* __restrict__ g_w4, float* __restrict__ g_b4) {
-  __shared__ float smem[4 * (NCLS + 1) * 64];
+  __shared__ float smem[FC1_SMALL_SMEM];
   const int L = xcd_remap(blockIdx.x, gridDim.x);
   if (L < FC1BWD_DW_BLOCKS)
-    fc1_bwd_dw(L, a2, dh, rows, g_w3);
+    fc1_bwd_dw(L, a2, dh, rows, g_w3, threadIdx.x >> 6);
   else
     fc1_small_grads(L - FC1BWD_DW_BLOCKS, hd, dh, dlog, rows, g_w4, g_b4, g_b3, smem);
 }
@@ -1220,14 +1273,21 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
 // ------------------------------------ conv2 bwd-data, Winograd F(2x2,5x5) ----
 // dA1 = dY2 (x) rot180(W2) with the channel roles swapped: the forward form
 // on the zero-bordered channel-major dY2 image dy2t [n][64][18][MNIST32_T_LD]
-// (written by fc1 backward) with the filters Ud [36][64][32].  Block = (image,
+// (written by fc1 backward) with the filters Ud [36][64][32].  (Reading the
+// NHWC dy2 instead, lanes along the channels, measured 3.3 us slower in
+// isolation - h0 transform 10.1 vs 6.2 K cycles, h0 products 12.8 vs 6.7 K -
+// more than the 2.7 us the dy2t stores cost fc1 backward.)  Block = (image,
 // pair of 2x2-tile rows) = 14 tiles (M 16), N = 32 input channels of conv2,
 // K = 64 in two halves of 32 (the transformed image V is 72 KB per half).
 // Waves = (ci half, quarter of the 36 points), each point's 8 k-steps per K
 // half folded into the 2x2 outputs at once; the four quarters' partials are
 // summed in order by the epilogue threads.  Half 1's input windows are loaded
 // under half 0's products.  Epilogue: the ReLU1 mask (a1 > 0), NHWC da1m.
-// Optional FC SGD role blocks (single rank) as in conv2_bwd_data_l2_kernel.
+// Optional FC SGD (single rank): every conv block, once its own work is done,
+// updates a 1/(2 x blocks) slice of the FC bucket (two 256-thread units).
+// Appended role blocks instead waited for a free CU behind the conv blocks
+// (one conv block fills a CU: 8 waves at 150 VGPRs), a serial tail of their
+// whole duration (bwd-data 24 us in the step vs 15 alone).
 // c1.part1 != nullptr: each block also computes the conv1 filter-gradient
 // partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
 // values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
@@ -1242,11 +1302,15 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   unsigned long long stamp[7];
   if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
   __shared__ float V[WV_FLOATS];
-  const int nconv = gridDim.x - sgd.nblk / 2;
-  if ((int)blockIdx.x >= nconv) {  // 512-thread blocks: two 256-thread role units
-    fc_sgd_role(sgd, 2 * (blockIdx.x - nconv) + (threadIdx.x >> 8), nullptr, threadIdx.x & 255);
-    return;
-  }
+  // this block's FC SGD slice (sgd.nblk = 2 x blocks units), after its conv work
+  auto fc_sgd_tail = [&]() {
+    if (sgd.n4 == 0) return;
+    const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
+    if (sgd.a2)  // fused fc1 dW1 + SGD tiles, first halves of every block first
+      for (int d = half * gridDim.x + blockIdx.x; d < FC1BWD_DW_BLOCKS; d += 2 * gridDim.x)
+        fc1_dw_sgd(sgd, d, t);
+    fc_sgd_role(sgd, 2 * blockIdx.x + half, nullptr, t);
+  };
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3;
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform in an SGPR: the point index p, its output-transform weights
@@ -1382,51 +1446,46 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
     }
   }
   if constexpr (PROF) stamp[5] = __builtin_amdgcn_s_memtime();
-  if (!do_c1) {
-    if constexpr (PROF) {
-      stamp[6] = stamp[5];
-      if (lane == 0)
-        for (int k = 0; k < 7; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 7 + k] = stamp[k];
-    }
-    return;
-  }
-  // dW1[t][ci] += dA1 * x[argmax pixel + tap] over the thread's 4 positions
-  float acc[26];
+  if (do_c1) {
+    // dW1[t][ci] += dA1 * x[argmax pixel + tap] over the thread's 4 positions
+    float acc[26];
 #pragma unroll
-  for (int k = 0; k < 26; ++k) acc[k] = 0.f;
-  if (own) {
+    for (int k = 0; k < 26; ++k) acc[k] = 0.f;
+    if (own) {
 #pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      if (g1[o] != 0.f) {
-        const int py = 2 * tr + (o >> 1), px = 2 * tc + (o & 1);
-        const int ly = 2 * py + (q1[o] >> 1) - 8 * pg;  // xs1 row of tap kh = 0
-        const int lx = 2 * px + (q1[o] & 1);            // xs1 col of tap kw = 0
+      for (int o = 0; o < 4; ++o) {
+        if (g1[o] != 0.f) {
+          const int py = 2 * tr + (o >> 1), px = 2 * tc + (o & 1);
+          const int ly = 2 * py + (q1[o] >> 1) - 8 * pg;  // xs1 row of tap kh = 0
+          const int lx = 2 * px + (q1[o] & 1);            // xs1 col of tap kw = 0
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
+          for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += g1[o] * xs1[(ly + kh) * 32 + lx + kw];
-        acc[25] += g1[o];
+            for (int kw = 0; kw < 5; ++kw) acc[kh * 5 + kw] += g1[o] * xs1[(ly + kh) * 32 + lx + kw];
+          acc[25] += g1[o];
+        }
       }
     }
-  }
 #pragma unroll
-  for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], 32, 64);  // tiles 2w, 2w + 1
-  if (wave < 7 && (tid & 32) == 0) {
+    for (int k = 0; k < 26; ++k) acc[k] += __shfl_xor(acc[k], 32, 64);  // tiles 2w, 2w + 1
+    if (wave < 7 && (tid & 32) == 0) {
 #pragma unroll
-    for (int k = 0; k < 26; ++k) red1[wave * (26 * 32 + 1) + k * 32 + ci] = acc[k];
-  }
-  __syncthreads();
-  for (int i = tid; i < 26 * 32; i += WNT) {
-    float sv = 0.f;
+      for (int k = 0; k < 26; ++k) red1[wave * (26 * 32 + 1) + k * 32 + ci] = acc[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < 26 * 32; i += WNT) {
+      float sv = 0.f;
 #pragma unroll
-    for (int w = 0; w < 7; ++w) sv += red1[w * (26 * 32 + 1) + i];
-    c1.part1[(size_t)(n * 4 + pg) * 832 + i] = sv;
+      for (int w = 0; w < 7; ++w) sv += red1[w * (26 * 32 + 1) + i];
+      c1.part1[(size_t)(n * 4 + pg) * 832 + i] = sv;
+    }
   }
   if constexpr (PROF) {
-    stamp[6] = __builtin_amdgcn_s_memtime();
+    stamp[6] = do_c1 ? __builtin_amdgcn_s_memtime() : stamp[5];
     if (lane == 0)
       for (int k = 0; k < 7; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 7 + k] = stamp[k];
   }
+  fc_sgd_tail();
 }
 
 // ------------------------------------------ Winograd conv2 bwd-filter ----
@@ -1907,9 +1966,36 @@ __global__ __launch_bounds__(256) void conv1_bwd_filter_kernel(int batch, const 
 }
 
 // ------------------------------------------------------------ finalize ----
+// sum of the conv2 filter-grad slabs at float4 i, in group order z = 0, 1, ...
+// (the one order every path uses, so world 1 and world > 1 agree bit for bit);
+// the loads of up to 32 groups are issued together
+__device__ __forceinline__ float4 slab_sum4(const float4* __restrict__ p2, int ngroups) {
+  float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+  int z = 0;
+  for (; z + 32 <= ngroups; z += 32) {
+    float4 v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = p2[(size_t)(z + u) * 12800];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      sv.x += v[u].x;
+      sv.y += v[u].y;
+      sv.z += v[u].z;
+      sv.w += v[u].w;
+    }
+  }
+  for (; z < ngroups; ++z) {
+    const float4 v = p2[(size_t)z * 12800];
+    sv.x += v.x;
+    sv.y += v.y;
+    sv.z += v.z;
+    sv.w += v.w;
+  }
+  return sv;
+}
+
 // conv2: one thread per dW2 float4 summing the G image-group slabs in group
-// order, 16 slab loads in flight (the sum order of sgd_finalize's
-// conv2_grad4: the world-1 and world > 1 conv gradients agree bit for bit);
+// order (slab_sum4, shared with sgd_finalize);
 // db2 from the 4G centre-tap partials.  conv1: one wave per output (lanes
 // stride over the per-block slabs) + wave reduction.
 __global__ __launch_bounds__(256) void grad_finalize_kernel(
@@ -1919,28 +2005,7 @@ __global__ __launch_bounds__(256) void grad_finalize_kernel(
   constexpr int B2 = 51200 / 4 / 256;  // 50 blocks of float4
   if ((int)blockIdx.x < B2) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const float4* p2 = reinterpret_cast<const float4*>(part2) + i;
-    float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
-    int z = 0;
-    for (; z + 16 <= ngroups; z += 16) {
-      float4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        sv.x += v[u].x;
-        sv.y += v[u].y;
-        sv.z += v[u].z;
-        sv.w += v[u].w;
-      }
-    }
-    for (; z < ngroups; ++z) {
-      const float4 v = p2[(size_t)z * 12800];
-      sv.x += v.x;
-      sv.y += v.y;
-      sv.z += v.z;
-      sv.w += v.w;
-    }
+    const float4 sv = slab_sum4(reinterpret_cast<const float4*>(part2) + i, ngroups);
     reinterpret_cast<float4*>(g_w2)[i] = sv;
     return;
   }
@@ -2113,11 +2178,11 @@ void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const
                     float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,
                     int roles) {
   if (batch <= 0 || batch % 32 != 0) throw std::runtime_error("fc1_bwd: batch % 32 != 0");
-  const int n_dx = (batch / 32) * (FC1_IN / 32);
-  const int grid = roles == 1 ? n_dx : n_dx + FC1BWD_DW_BLOCKS + SMALL_BLOCKS;
-  fc1_bwd_kernel<<<grid, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch,
-                                                            g_w3, g_b3, g_w4, g_b4, dy2, dy2t,
-                                                            roles);
+  if (roles <= 0 || roles > 7) throw std::runtime_error("fc1_bwd: roles must be a mask in 1..7");
+  const int grid = ((roles & 1) ? (batch / 32) * (FC1_IN / 32) : 0) +
+                   ((roles & 2) ? FC1BWD_DW_BLOCKS : 0) + ((roles & 4) ? SMALL_BLOCKS : 0);
+  fc1_bwd_kernel<<<grid, 256, 0, s>>>(a2, idx2, dh, hd, dlog, w1, batch, g_w3, g_b3, g_w4, g_b4,
+                                      dy2, dy2t, roles);
 }
 
 void launch_fc1_bwd_weights(const float* a2, const float* dh, const float* hd, const float* dlog,
@@ -2136,8 +2201,22 @@ FcSgd fc_sgd_args(const FcSgdArgs* a) {
   if (a == nullptr || a->n == 0) return r;
   if (a->n % 4) throw std::runtime_error("fc_sgd: FC bucket not a multiple of 4 floats");
   r = FcSgd{a->w, a->g, a->m, a->n / 4, a->l2, a->momentum, a->lr, 0, nullptr, nullptr, 0,
-            a->gscale};
+            a->gscale, nullptr, nullptr, 0};
   const long long per_blk = 256LL * FC_SGD_UNROLL * a->rounds;
+  if (a->a2) {
+    if (a->w1b || a->dh == nullptr || a->batch <= 0)
+      throw std::runtime_error("fc_sgd: fused dW1 needs a2, dh, batch and no bf16 shadows");
+    if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
+      throw std::runtime_error("fc_sgd: fc1 weight misaligned or outside the FC bucket");
+    r.a2 = a->a2;
+    r.dh = a->dh;
+    r.batch = a->batch;
+    r.w1_off4 = a->w1 / 4;
+    // the streaming units cover the bucket minus the fc1 weight (its tiles are
+    // extra blocks of the launch)
+    r.nblk = (int)((r.n4 - W1_F4 + per_blk - 1) / per_blk);
+    return r;
+  }
   if (a->w1b) {
     if (a->w1 % 4 || a->w1 + (long long)FC1_IN * FC1_OUT > a->n)
       throw std::runtime_error("fc_sgd: fc1 weight misaligned or outside the FC bucket");
@@ -2157,6 +2236,7 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
   if (batch % 8 != 0) throw std::runtime_error("conv2_bwd_data_l2: batch % 8 != 0");
   const int mtiles = batch * 49 / 8;
   const FcSgd sg = fc_sgd_args(fc_sgd);
+  if (sg.a2) throw std::runtime_error("conv2_bwd_data_l2: no fused dW1 SGD (Winograd launch only)");
   conv2_bwd_data_l2_kernel<<<cdiv(mtiles, 2) + sg.nblk, 256, 0, s>>>(dy2t, w2t, a1, batch, da1m,
                                                                      sg);
 }
@@ -2165,15 +2245,15 @@ void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float*
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd,
                                 const C1FilterArgs* c1, unsigned long long* prof) {
   FcSgd sg = fc_sgd_args(fc_sgd);
-  // the SGD role works in 256-thread units: two per 512-thread block
-  const int role_blocks = (sg.nblk + 1) / 2;
-  sg.nblk = 2 * role_blocks;
+  if (sg.w1b) throw std::runtime_error("conv2_bwd_data_wino: the fp32 FC SGD has no shadows");
+  // the FC SGD runs in 256-thread units, two per (conv) block
+  sg.nblk = 2 * batch * 4;
   if (prof)
-    conv2_bwd_data_wino_kernel<true><<<batch * 4 + role_blocks, WNT, 0, s>>>(
-        dy2t, Ud, a1, batch, da1m, sg, c1_args(c1), prof);
+    conv2_bwd_data_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m, sg,
+                                                              c1_args(c1), prof);
   else
-    conv2_bwd_data_wino_kernel<false><<<batch * 4 + role_blocks, WNT, 0, s>>>(
-        dy2t, Ud, a1, batch, da1m, sg, c1_args(c1));
+    conv2_bwd_data_wino_kernel<false><<<batch * 4, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m, sg,
+                                                               c1_args(c1));
 }
 
 void launch_conv2_bwd_filter(const float* a1p, const float* dy2, int batch, float* part2,
@@ -2274,33 +2354,11 @@ __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, 
   *w -= lr * mv;
 }
 
-// dW2 float4 i (HWIO order): slab sum in group order (16 loads in flight), or
+// dW2 float4 i (HWIO order): slab sum in group order (slab_sum4), or
 // the all-reduced flat gradient
 __device__ __forceinline__ float4 conv2_grad4(const SgdFinArgs& a, int i) {
   if (a.flat) return reinterpret_cast<const float4*>(a.g + a.off_w2)[i];
-  const float4* p2 = reinterpret_cast<const float4*>(a.part2) + i;
-  float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
-  int z = 0;
-  for (; z + 16 <= a.ngroups; z += 16) {
-    float4 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v[u] = p2[(size_t)(z + u) * 12800];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      sv.x += v[u].x;
-      sv.y += v[u].y;
-      sv.z += v[u].z;
-      sv.w += v[u].w;
-    }
-  }
-  for (; z < a.ngroups; ++z) {
-    const float4 v = p2[(size_t)z * 12800];
-    sv.x += v.x;
-    sv.y += v.y;
-    sv.z += v.z;
-    sv.w += v.w;
-  }
-  return sv;
+  return slab_sum4(reinterpret_cast<const float4*>(a.part2) + i, a.ngroups);
 }
 
 // conv2 weights of one input channel ci and 16 output channels (block b: ci
@@ -2314,10 +2372,10 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
   if (tid < 100) {
     const int t = tid >> 2, c4 = tid & 3;
     const int i = (t * 32 + ci) * 16 + cq * 4 + c4;  // float4 index in the HWIO block
-    const float4 sv = conv2_grad4(a, i);
     float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
     float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
-    float4 wv = *wp, mv = *mp;
+    float4 wv = *wp, mv = *mp;  // issued ahead of the slab loads
+    const float4 sv = conv2_grad4(a, i);
     sgd4(wv, mv, sv, 0.f, lr, a.momentum, a.gscale);
     *wp = wv;
     *mp = mv;
@@ -2347,10 +2405,10 @@ __device__ void sgd_conv2_wino(const SgdFinArgs& a, int blk, float lr) {
 __device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
   const int tid = threadIdx.x;
   const int i = blk * 256 + tid;
-  const float4 s = conv2_grad4(a, i);
   float4* wp = reinterpret_cast<float4*>(a.w + a.off_w2) + i;
   float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + i;
   float4 wv = *wp, mv = *mp;
+  const float4 s = conv2_grad4(a, i);
   sgd4(wv, mv, s, 0.f, lr, a.momentum, a.gscale);
   *wp = wv;
   *mp = mv;
@@ -2375,6 +2433,12 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
   const int tid = threadIdx.x;
   int blk = blockIdx.x;
   if (a.step && blk == 0 && tid == 0) *a.step += 1;
+  const int ndw = a.fc.a2 ? FC1BWD_DW_BLOCKS : 0;  // fused dW1 + SGD tiles first
+  if (blk < ndw) {
+    fc1_dw_sgd(a.fc, blk, tid);
+    return;
+  }
+  blk -= ndw;
   if (blk < a.fc.nblk) {
     fc_sgd_role(a.fc, blk, tile);
     return;
@@ -2438,6 +2502,9 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
     f.w1t = p.w1t;
     f.w1 = p.off_w1fc;
     f.gscale = p.gscale;
+    f.a2 = p.a2;
+    f.dh = p.dh;
+    f.batch = p.batch;
     a.fc = fc_sgd_args(&f);
   }
   a.w = p.w;
@@ -2463,7 +2530,7 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
   a.w2t = reinterpret_cast<__bf16*>(p.w2tb);
   a.w2b = reinterpret_cast<__bf16*>(p.w2b);
   const int conv_blocks = p.conv ? (p.wino_u ? 128 : 50) + 16 + cdiv(832, 4) : 0;
-  const int grid = a.fc.nblk + conv_blocks;
+  const int grid = (a.fc.a2 ? FC1BWD_DW_BLOCKS : 0) + a.fc.nblk + conv_blocks;
   if (grid == 0) throw std::runtime_error("sgd_step: nothing to update");
   sgd_finalize_kernel<<<grid, 256, 0, s>>>(a);
 }

@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void fc1_bwd_kernel(
     const float* __restrict__ dh, const float* __restrict__ dlog, const bf* __restrict__ w1b,
     int batch, float* __restrict__ g_w3, float* __restrict__ g_b3, float* __restrict__ g_w4,
     float* __restrict__ g_b4, bf* __restrict__ dy2p, bf* __restrict__ dy2t) {
-  __shared__ float smem[4 * (NCLS + 1) * 64];
+  __shared__ float smem[mnist::FC1_SMALL_SMEM];
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
   const int bm = batch / 32;
   const int n_dx = (bm * (FC1_IN / 32) + 3) / 4;

@@ -19,34 +19,44 @@ __device__ __forceinline__ long long batch_offset_dev(const long long* step_ptr,
 }
 
 // fc2 weight / bias and fc1 bias grads (B1, B2): dW4 = hd^T dlog, db4 = sum
-// dlog, db3 = sum dh.  Block blk owns hidden units [64 blk, 64 blk + 64).
-__device__ inline void fc1_small_grads(int blk, const float* hd, const float* dh, const float* dlog,
-                                int batch, float* g_w4, float* g_b4, float* g_b3, float* smem) {
-  // block blk handles hidden units j in [64 blk, 64 blk + 64); 4 row groups
+// dlog, db3 = sum dh.  Block blk owns hidden units [64 blk, 64 blk + 64); its
+// 4 waves take every 4th row.  dlog is staged in LDS 64 rows at a time (one
+// coalesced pass; the rows are then LDS broadcasts): read straight from
+// global memory they were 80 dependent broadcast loads per 8 rows (8.2 us
+// for the role alone).  Row order per thread: rg, rg + 4, rg + 8, ...
+constexpr int FC1_SMALL_SMEM = 64 * NCLS + 4 * (NCLS + 1) * 64;  // floats
+__device__ __forceinline__ void fc1_small_grads(int blk, const float* hd, const float* dh,
+                                                const float* dlog, int batch, float* g_w4,
+                                                float* g_b4, float* g_b3, float* smem) {
   const int tid = threadIdx.x, jl = tid & 63, rg = tid >> 6;
   const int j = blk * 64 + jl;
+  float* dl = smem;              // [64][NCLS]: this chunk's dlog rows
+  float* s = smem + 64 * NCLS;   // [4][NCLS + 1][64]: row-group partials
   float acc[NCLS + 1];
 #pragma unroll
   for (int c = 0; c <= NCLS; ++c) acc[c] = 0.f;
-  for (int n0 = rg; n0 < batch; n0 += 32) {  // 8 rows per round, loads issued together
-    float hv[8], dv[8];
+  for (int r0 = 0; r0 < batch; r0 += 64) {
+    const int rows = min(64, batch - r0);
+    float hv[16], dv[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int n = min(n0 + 4 * u, batch - 1);
-      hv[u] = hd[n * FC1_OUT + j];
-      dv[u] = dh[n * FC1_OUT + j];
+    for (int u = 0; u < 16; ++u) {
+      const int n = min(r0 + rg + 4 * u, batch - 1);
+      hv[u] = hd[(size_t)n * FC1_OUT + j];
+      dv[u] = dh[(size_t)n * FC1_OUT + j];
     }
+    if (r0 > 0) __syncthreads();  // the previous chunk's rows are consumed
+    for (int i = tid; i < rows * NCLS; i += 256) dl[i] = dlog[(size_t)r0 * NCLS + i];
+    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int n = n0 + 4 * u;
-      if (n < batch) {
+    for (int u = 0; u < 16; ++u) {
+      const int r = rg + 4 * u;
+      if (r < rows) {
 #pragma unroll
-        for (int c = 0; c < NCLS; ++c) acc[c] += hv[u] * dlog[n * NCLS + c];
+        for (int c = 0; c < NCLS; ++c) acc[c] += hv[u] * dl[r * NCLS + c];
         acc[NCLS] += dv[u];
       }
     }
   }
-  float* s = smem;  // [4][11][64]
 #pragma unroll
   for (int c = 0; c <= NCLS; ++c) s[(rg * (NCLS + 1) + c) * 64 + jl] = acc[c];
   __syncthreads();
@@ -285,6 +295,11 @@ struct FcSgd {
   __bf16* w1t;
   long long w1_off4;
   float gs;  // gradient scale (1 / ranks: the bucket holds the rank sum)
+  // fused fc1 weight gradient (FcSgdArgs::a2): the fc1 weight's float4s are
+  // skipped by the streaming units and updated by fc1_dw_sgd tiles
+  const float* a2;
+  const float* dh;
+  int batch;
 };
 constexpr int FC_SGD_UNROLL = 4;
 constexpr long long W1_F4 = (long long)FC1_IN * FC1_OUT / 4;
@@ -331,7 +346,7 @@ __device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* ti
 // a.w1b is set (256-thread blocks)
 // tid: the thread's index in its 256-thread unit (a 512-thread block runs two
 // units; the shadow path (a.w1b) needs 256-thread blocks)
-__device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile,
+__device__ __forceinline__ void fc_sgd_role(const FcSgd& a, int blk, float* tile,
                                    int tid = (int)threadIdx.x) {
   float4* W4 = reinterpret_cast<float4*>(a.w);
   float4* M4 = reinterpret_cast<float4*>(a.m);
@@ -348,8 +363,10 @@ __device__ inline void fc_sgd_role(const FcSgd& a, int blk, float* tile,
     nb -= SHADOW_W1_BLOCKS;
     n4 -= W1_F4;  // the rest of the bucket, the fc1 weight's float4s skipped
   }
+  if (a.a2) n4 -= W1_F4;  // the fc1 weight: fc1_dw_sgd tiles
+  const bool skip = a.w1b || a.a2;
   const long long stride = (long long)nb * 256;
-  auto at = [&](long long f) { return (a.w1b && f >= a.w1_off4) ? f + W1_F4 : f; };
+  auto at = [&](long long f) { return (skip && f >= a.w1_off4) ? f + W1_F4 : f; };
   // U float4s per thread per round, every load of a round in flight together
   for (long long i0 = (long long)blk * 256 + tid; i0 < n4; i0 += stride * FC_SGD_UNROLL) {
     float4 wv[FC_SGD_UNROLL], gv[FC_SGD_UNROLL], mv[FC_SGD_UNROLL];

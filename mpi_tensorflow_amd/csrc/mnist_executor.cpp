@@ -42,7 +42,8 @@ MnistExecutor::~MnistExecutor() {
 // launches instead (fc1 backward: dX + dW1 + fc2 grads in one grid).
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
-                                    const mnist::FcSgdArgs* fc_sgd, bool factors, bool fresh) {
+                                    const mnist::FcSgdArgs* fc_sgd, bool factors, bool fresh,
+                                    bool fc1_dw_fused) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
     return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, fresh);
@@ -93,7 +94,8 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
                         P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
-                        P<float>(p.dy2t), s, factors ? 1 : 7);
+                        P<float>(p.dy2t), s,
+                        factors ? 1 : (fc1_dw_fused ? 5 : 7));
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   // conv1 filter grad: Winograd - in the bwd-data blocks' epilogue, from the
   // dA1 values they produce; direct - role blocks of the filter-grad launch
@@ -326,17 +328,26 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
     // the FC bucket's SGD rides in the conv2 bwd-data launch (its grads are final
     // after fc1 backward); the slab sums + conv SGD run in the last launch
     mnist::FcSgdArgs fc{P<float>(p.params), P<const float>(p.grads), P<float>(p.mom),
-                        p.bucket1, p.l2, p.momentum, P<const float>(p.lr), fc_sgd_rounds_};
+                        p.bucket1, p.l2, p.momentum, P<const float>(p.lr),
+                        fc_sgd_rounds_ >= 0 ? fc_sgd_rounds_ : (p.bf16 ? 2 : 0)};
     if (p.bf16) {  // the SGD also writes the fc1 bf16 shadows (see refresh_shadows)
       fc.w1b = P<uint16_t>(p.w1b);
       fc.w1t = P<uint16_t>(p.w1t);
       fc.w1 = p.off_w3;
     }
-    const bool role = fc_sgd_rounds_ > 0;
+    // fp32 Winograd: dW1 is formed inside the FC SGD (fc1 backward skips it)
+    const bool fuse_dw1 = p.wino && !p.bf16;
+    if (fuse_dw1) {
+      fc.a2 = P<const float>(p.a2);
+      fc.dh = P<const float>(p.dh);
+      fc.batch = p.batch;
+      fc.w1 = p.off_w3;
+    }
+    const bool role = fc.rounds > 0;
     // the derived weights (Winograd transforms, bf16 shadows) come from the
     // previous step's SGD (or refresh_shadows() before the first step of a
     // run) and are rewritten by this step's SGD for the next one
-    enqueue_fwd_bwd(s, /*finalize=*/false, role ? &fc : nullptr, false, /*fresh=*/true);
+    enqueue_fwd_bwd(s, /*finalize=*/false, role ? &fc : nullptr, false, /*fresh=*/true, fuse_dw1);
     mnist::SgdStepArgs a;
     a.w = P<float>(p.params);
     a.g = P<const float>(p.grads);
@@ -350,6 +361,9 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
       a.w1b = fc.w1b;
       a.w1t = fc.w1t;
       a.off_w1fc = fc.w1;
+      a.a2 = fc.a2;
+      a.dh = fc.dh;
+      a.batch = fc.batch;
     }
     a.off_w2 = (int)p.off_w2;
     a.off_b2 = (int)p.off_b2;

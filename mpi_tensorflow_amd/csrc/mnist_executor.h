@@ -132,10 +132,13 @@ class MnistExecutor {
                          float keep_prob, uint32_t drop_key, hipStream_t s);
 
   const MnistPtrs& ptrs() const { return p_; }
-  // single-rank step: rounds of FC_SGD_UNROLL float4s per thread of the FC SGD
-  // role appended to the conv2 bwd-data launch (sets its block count); 0 runs
-  // the FC SGD in the final SGD launch instead
-  void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? 0 : r; }
+  // single-rank step: where the FC-bucket SGD runs.  r > 0: in the conv2
+  // bwd-data launch (r rounds of FC_SGD_UNROLL float4s per thread of the
+  // appended role; the Winograd launch spreads it over its own blocks); 0: in
+  // the final SGD launch, beside the latency-bound conv SGD blocks; r < 0: the
+  // measured default per engine - fp32 0 (89.8 vs 94.2 us per step with the
+  // fused dW1 tiles), bf16 2
+  void set_fc_sgd_rounds(int r) { fc_sgd_rounds_ = r < 0 ? -1 : r; }
   // Re-derives every weight copy the step kernels read from the fp32 master
   // weights: the Winograd filter transforms (fp32, wino) and the bf16
   // shadows (bf16 engine).  A single-rank bf16 step writes the fc1 shadows from its SGD and
@@ -155,9 +158,11 @@ class MnistExecutor {
   // fresh: the derived weights (Winograd filter transforms; bf16 shadows) are
   // already current - the previous step's SGD launch wrote them (sgd_step,
   // launch_sgd_step); otherwise the step derives them from the weights first
+  // fc1_dw_fused: the fc1 weight gradient is formed inside this step's SGD
+  // (single rank, fp32 Winograd): fc1 backward skips its dW1 role
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
                        const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
-                       bool fresh = false);
+                       bool fresh = false, bool fc1_dw_fused = false);
   // the fused SGD launch applies (L2 prefix == the FC bucket, as in the
   // reference layout)
   bool fused_sgd_ok() const;
@@ -178,7 +183,7 @@ class MnistExecutor {
   // shadows_fresh: every bf16 weight shadow is current (single-rank step)
   void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,
                             const mnist::FcSgdArgs* fc_sgd = nullptr, bool shadows_fresh = false);
-  int fc_sgd_rounds_ = 2;
+  int fc_sgd_rounds_ = -1;
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;

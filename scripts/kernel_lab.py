@@ -70,14 +70,14 @@ def main():
                                          ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
                                          G("fc1_bias"), G("fc2_weight"), G("fc2_bias"), ptr(b["dy2"]),
                                          ptr(b["dy2t"]), s, 2),
-        "fc1_bwd[none]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
-                                           ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
-                                           G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
-                                           ptr(b["dy2"]), ptr(b["dy2t"]), s, 0),
         "fc1_bwd[small]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
                                             ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
                                             G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
                                             ptr(b["dy2"]), ptr(b["dy2t"]), s, 4),
+        "fc1_bwd[dX,no-t]": lambda: k.fc1_bwd(ptr(b["a2"]), ptr(b["idx2"]), ptr(b["dh"]), ptr(b["hd"]),
+                                              ptr(b["dlog"]), W("fc1_weight"), B, G("fc1_weight"),
+                                              G("fc1_bias"), G("fc2_weight"), G("fc2_bias"),
+                                              ptr(b["dy2"]), 0, s, 1),
         "conv2_bwd_data": lambda: k.conv2_bwd_data_l2(ptr(b["dy2t"]), ptr(b["w2t"]), ptr(b["a1"]), B,
                                                       ptr(b["da1m"]), s),
         "conv2_bwd_filter": lambda: k.conv2_bwd_filter(ptr(b["a1pf"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),

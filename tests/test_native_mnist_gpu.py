@@ -251,6 +251,25 @@ def test_native_rccl_comm_and_graph_capture(cuda_dev, data):
     assert torch.equal(synced.params, plain.params)
 
 
+def test_fc_sgd_placements_bit_identical(cuda_dev, data):
+    """The single-rank FC-bucket SGD - with the fc1 weight gradient formed
+    inside it (fused dW1 tiles, fc1 backward without its dW1 role) - runs in
+    the final SGD launch (fp32 default) or as the tail of the Winograd
+    bwd-data blocks; both update the parameters and momenta bit for bit like
+    the gradient-buffer path (test_native_rccl_comm_and_graph_capture)."""
+    x, y = data
+    runs = []
+    for rounds in (-1, 0, 2):
+        e = NativeMnistEngine(C.TrainConfig(graph=False).validate(), x, y, cuda_dev)
+        e.exe.set_fc_sgd_rounds(rounds)
+        e.train(7)
+        runs.append(e)
+    torch.cuda.synchronize()
+    for e in runs[1:]:
+        assert torch.equal(runs[0].params, e.params)
+        assert torch.equal(runs[0].mom, e.mom)
+
+
 def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     """Startup autotune of the gradient-sync schedule (runtime/mnist_engine.py:
     tune_schedule) against an emulated 8-rank ring (csrc/collective.h EmuComm):

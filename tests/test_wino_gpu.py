@@ -133,10 +133,11 @@ def test_wino_fused_conv12_forward_matches_oracle(cuda_dev, step):
     assert torch.equal(i2[pos], code[pos])
 
 
-@pytest.mark.parametrize("B", [64, 96])
-def test_wino_conv2_bwd_data_matches_oracle(cuda_dev, B):
-    """dA1 = conv2 backward-data of a sparse (pool-scattered) dY2, masked by
-    a1 > 0, vs torch autograd in fp64."""
+@pytest.mark.parametrize("B,dense", [(64, False), (96, False), (64, True)])
+def test_wino_conv2_bwd_data_matches_oracle(cuda_dev, B, dense):
+    """dA1 = conv2 backward-data of a sparse (pool-scattered, as fc1 bwd writes
+    it) or dense dY2, masked by a1 > 0, vs torch autograd in fp64 (the dense
+    case puts nonzeros on every border pixel the zero padding meets)."""
     Cn = native()
     g = torch.Generator().manual_seed(11)
     _, _, w2, _ = _weights(cuda_dev)
@@ -147,6 +148,8 @@ def test_wino_conv2_bwd_data_matches_oracle(cuda_dev, B):
     dy2 = torch.zeros(B, 14, 14, 64)
     for k in range(4):
         dy2[:, k >> 1::2, k & 1::2, :] = torch.where(q == k, dpool, torch.zeros(()))
+    if dense:
+        dy2 = torch.randn(B, 14, 14, 64, generator=g)
     dy2 = dy2.to(cuda_dev)
     dy2t = torch.zeros(B, 64, 18, 20, device=cuda_dev)
     dy2t[:, :, 2:16, 2:16] = dy2.permute(0, 3, 1, 2)
