@@ -590,9 +590,10 @@ __device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
 
 // single rank: dW1 tile L formed and applied at once - momentum SGD of those
 // fc1 weights (the sgd4 expression forms, so the parameters match the
-// gradient-buffer path bit for bit).  Runs as the tail of the Winograd
-// bwd-data blocks (256 VGPRs there: the weight / momentum loads follow the
-// products, one accumulator at a time).  tid: index in the 256-thread unit
+// gradient-buffer path bit for bit).  The weight / momentum loads follow the
+// products, one accumulator at a time: issued ahead of them they took the
+// final SGD launch to 232 VGPRs, halving its occupancy (12.2 -> 15.7 us).
+// tid: index in the 256-thread unit
 __device__ __forceinline__ void fc1_dw_sgd(const FcSgd& a, int L, int tid) {
   const int lane = tid & 63, r = lane & 31;
   f32x16 c0, c1;
@@ -738,9 +739,9 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
     iv[j] = ok ? v : 0.f;
   }
   const int co = lane & 31, kh2 = lane >> 5;
-  float wb[16];
+  float wb[13];
 #pragma unroll
-  for (int st = 0; st < 16; ++st) {
+  for (int st = 0; st < 13; ++st) {
     const int k = 2 * st + kh2;
     const float v = c1.w1[min(k, 24) * 32 + co];
     wb[st] = k < 25 ? v : 0.f;
@@ -795,8 +796,10 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
     const float* ib0 = tile_base(t, v0);
     const float* ib1 = tile_base(two ? t + NW : t, v1);
     f32x16 acc0 = zero16(), acc1 = zero16();
+    // 13 k-steps cover the 25 taps (k 25 is a zero pair); the standalone
+    // kernel's k 26 .. 31 only add exact zeros, so the sums still match it
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
+    for (int st = 0; st < 13; ++st) {
       const int k = 2 * st + kh2, kc = min(k, 24), o = (kc / 5) * C12_IMG_LD + kc % 5;
       const float a0 = ib0[o], a1v = ib1[o];
       acc0 = mfma32x32x2((v0 && k < 25) ? a0 : 0.f, wb[st], acc0);
