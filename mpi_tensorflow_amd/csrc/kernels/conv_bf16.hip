@@ -283,7 +283,7 @@ struct Loader {
   float4 ra[XB ? 1 : AR][2];
   uint4 rab[XB ? AR : 1];
   uint4 rb[BR];
-  static constexpr int EXTRA = 0;  // bf16 elements of extra LDS (StemHaloLoader)
+  static constexpr int EXTRA = 0;  // bf16 elements of loader-owned LDS (none so far)
   __device__ Loader(const ConvShape& s_, const ConvShape&, const XT* x, const __bf16* wt_, int m0,
                     int n0, __bf16*)
       : s(s_), wt(wt_) {
@@ -450,109 +450,6 @@ struct StemLoader {
   }
 };
 
-// The stem's implicit im2col from an LDS halo (replaces StemLoader's per-chunk
-// global gathers).  StemLoader fetches every 8-element k chunk of every A row
-// from L2 as fp32 (M x kp x 4 B = 308 MB of L2 -> CU traffic per ResNet-18
-// step at B = 32: each image pixel is re-read by ~12 output pixels).  Here
-// the block first stages the input rows its BM output pixels read - the
-// stacked NHWC rows (n H + iy) from its first pixel's kh = 0 row to its last
-// pixel's kh = R - 1 row, one contiguous span of the image tensor - once, as
-// bf16, into LDS rows of (pad + W + pad) pixels x C (zero pad columns); the
-// A chunks are then 8 consecutive bf16 of one LDS row: (kh, j0) of output
-// pixel (n, oy, ox) starts at row (n H + oy stride - pad + kh - row0),
-// element ox stride C + j0.  Taps whose image row iy is outside [0, H) (the
-// neighbouring image's rows, or past the edge) and k >= S C of a tap row read
-// zero.  Needs stride * C even (4-byte aligned chunk reads) and a span that
-// fits HALO_ELEMS (stem_halo_ok, host).
-constexpr int HALO_ELEMS = 8192;  // bf16 (16 KB: two 128 x 64 blocks per CU; ResNet stem needs 7,590)
-
-template <int BM, int BN>
-struct StemHaloLoader {
-  static constexpr int AR = BM * BK / 8 / NT;
-  static constexpr int BR = BN * BK / 8 / NT;
-  static constexpr int EXTRA = HALO_ELEMS;
-  ConvShape s, si;
-  const __bf16* wt;
-  const __bf16* halo;
-  int seg, sc, rowld;
-  int hoff[AR], iy0[AR];
-  bool av[AR];
-  const __bf16* bbase[BR];
-  uint4 rab[AR];
-  uint4 rb[BR];
-  __device__ StemHaloLoader(const ConvShape& s_, const ConvShape& si_, const float* x,
-                            const __bf16* wt_, int m0, int n0, __bf16* lds)
-      : s(s_), si(si_), wt(wt_), halo(lds) {
-    const int tid = threadIdx.x, c8 = tid & 7;
-    const int M = s.N * s.OH * s.OW;
-    seg = (si.S * si.C + 7) / 8 * 8;
-    sc = si.S * si.C;
-    const int wc = si.W * si.C, padc = si.pad * si.C;
-    rowld = (wc + 2 * padc + 1) / 2 * 2;
-    // stacked rows of the block: first pixel's kh = 0 row .. last pixel's kh = R-1 row
-    auto srow = [&](int m) {
-      const int t = m / s.OW, oy = t % s.OH, n = t / s.OH;
-      return n * si.H + oy * si.stride - si.pad;
-    };
-    const int row0 = srow(m0), row1 = srow(min(m0 + BM, M) - 1) + si.R - 1;
-    const int nrows = row1 - row0 + 1;  // <= HALO_ELEMS / rowld (host-checked)
-    const long long nimg_rows = (long long)si.N * si.H;
-    for (int e = tid; e < nrows * rowld; e += NT) {
-      const int r = e / rowld, c = e - r * rowld - padc;
-      const long long gr = (long long)row0 + r;
-      const bool ok = c >= 0 && c < wc && gr >= 0 && gr < nimg_rows;
-      const float v = x[ok ? gr * wc + c : 0];
-      lds[e] = (__bf16)(ok ? v : 0.f);
-    }
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int m = m0 + (tid >> 3) + (NT / 8) * i;
-      av[i] = m < M;
-      const int mm = av[i] ? m : m0;
-      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH;
-      iy0[i] = oy * si.stride - si.pad;
-      hoff[i] = (srow(mm) - row0) * rowld + ox * si.stride * si.C;
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) {
-      const int n = min(n0 + (tid >> 3) + (NT / 8) * i, s.K - 1);
-      bbase[i] = wt + (size_t)n * s.C + 8 * c8;
-    }
-    __syncthreads();  // the halo is complete before the first load()
-  }
-  __device__ __forceinline__ void load(int kt) {
-    const int k0 = kt * BK + 8 * (threadIdx.x & 7);
-    const int kh = k0 / seg, j0 = k0 - kh * seg;
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int iy = iy0[i] + kh;
-      const bool ok = av[i] && kh < si.R && iy >= 0 && iy < si.H;
-      const uint32_t* src =
-          reinterpret_cast<const uint32_t*>(halo + (ok ? hoff[i] + kh * rowld + j0 : 0));
-      uint32_t w[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = ok ? src[q] : 0u;
-      // k >= S * C of the tap row (seg padding): zero
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const bool lo = j0 + 2 * q < sc, hi = j0 + 2 * q + 1 < sc;
-        w[q] = (lo ? (w[q] & 0xffffu) : 0u) | (hi ? (w[q] & 0xffff0000u) : 0u);
-      }
-      rab[i] = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-#pragma unroll
-    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const uint4*>(bbase[i] + kt * BK);
-  }
-  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
-    const int tid = threadIdx.x, c8 = tid & 7;
-#pragma unroll
-    for (int i = 0; i < AR; ++i)
-      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rab[i];
-#pragma unroll
-    for (int i = 0; i < BR; ++i)
-      *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[i];
-  }
-};
 
 // BatchNorm statistics in a bf16-output epilogue (ConvStats): lane (r, h) of
 // a wave holds column r of its 32-row tiles; after its own rows are summed
@@ -2395,30 +2292,6 @@ static void stem_check(const ConvShape& s1, const ConvShape& si) {
     throw std::runtime_error("stem conv: inconsistent shapes");
 }
 
-// the halo of every BM-pixel block fits StemHaloLoader's LDS (exact, over
-// the blocks; cached per shape) and its chunk reads are 4-byte aligned
-static bool stem_halo_ok(const ConvShape& s1, const ConvShape& si, int BM) {
-  if ((si.stride * si.C) % 2) return false;
-  static thread_local long long key[8] = {-1};
-  static thread_local bool val = false;
-  const long long k[8] = {si.N, si.H, si.W, si.C, si.R, si.stride, si.pad, BM};
-  bool same = true;
-  for (int i = 0; i < 8; ++i) same = same && key[i] == k[i];
-  if (same) return val;
-  const int M = s1.N * s1.OH * s1.OW;
-  const int rowld = (si.W * si.C + 2 * si.pad * si.C + 1) / 2 * 2;
-  auto srow = [&](int m) {
-    const int t = m / s1.OW, oy = t % s1.OH, n = t / s1.OH;
-    return n * si.H + oy * si.stride - si.pad;
-  };
-  int worst = 0;
-  for (int m0 = 0; m0 < M; m0 += BM)
-    worst = std::max(worst, srow(std::min(m0 + BM, M) - 1) + si.R - srow(m0));
-  val = (long long)worst * rowld <= cbf::HALO_ELEMS;
-  for (int i = 0; i < 8; ++i) key[i] = k[i];
-  return val;
-}
-
 void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x, const void* wtb,
                         void* yb, hipStream_t st, const ConvStats* stats) {
   using namespace cbf;
@@ -2430,17 +2303,14 @@ void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x
       throw std::runtime_error("stem conv: BatchNorm statistics layout mismatch");
     cs = *stats;
   }
-  // 128 x 64 tiles: M = 401 K pixels at B = 32 (3136 blocks), no split; the
-  // A operand from an LDS halo of the block's image rows where it fits
+  // 128 x 64 tiles: M = 401 K pixels at B = 32 (3136 blocks), no split.
+  // (An A operand built from an LDS halo of the block's image rows, staged
+  // once as bf16, measured 105 vs 90 us: the halo's 16 KB of LDS halved the
+  // blocks per CU and the chunk builds cost more than the L2 gathers saved.)
   const dim3 grid(cdiv(M, 128) * (s1.K / 64), 1);
-  if (stem_halo_ok(s1, si, 128))
-    fwd_kernel<128, 64, float, StemHaloLoader<128, 64>><<<grid, NT, 0, st>>>(
-        s1, x, reinterpret_cast<const __bf16*>(wtb), nullptr, nullptr, 0, s1.C / BK, nullptr,
-        reinterpret_cast<__bf16*>(yb), 0, si, cs);
-  else
-    fwd_kernel<128, 64, float, StemLoader<128, 64>><<<grid, NT, 0, st>>>(
-        s1, x, reinterpret_cast<const __bf16*>(wtb), nullptr, nullptr, 0, s1.C / BK, nullptr,
-        reinterpret_cast<__bf16*>(yb), 0, si, cs);
+  fwd_kernel<128, 64, float, StemLoader<128, 64>><<<grid, NT, 0, st>>>(
+      s1, x, reinterpret_cast<const __bf16*>(wtb), nullptr, nullptr, 0, s1.C / BK, nullptr,
+      reinterpret_cast<__bf16*>(yb), 0, si, cs);
 }
 
 void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,

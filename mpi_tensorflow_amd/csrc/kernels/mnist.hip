@@ -593,6 +593,9 @@ __device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
 // gradient-buffer path bit for bit).  The weight / momentum loads follow the
 // products, one accumulator at a time: issued ahead of them they took the
 // final SGD launch to 232 VGPRs, halving its occupancy (12.2 -> 15.7 us).
+// (Half-tile units - one accumulator per wave, buffer-descriptor addressing,
+// 89 VGPRs, 392 blocks - measured 13.2 us: the shorter chains did not pay
+// for the doubled operand traffic and block count.)
 // tid: index in the 256-thread unit
 __device__ __forceinline__ void fc1_dw_sgd(const FcSgd& a, int L, int tid) {
   const int lane = tid & 63, r = lane & 31;
