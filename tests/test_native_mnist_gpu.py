@@ -251,16 +251,19 @@ def test_native_rccl_comm_and_graph_capture(cuda_dev, data):
     assert torch.equal(synced.params, plain.params)
 
 
-def test_fc_sgd_placements_bit_identical(cuda_dev, data):
-    """The single-rank FC-bucket SGD - with the fc1 weight gradient formed
-    inside it (fused dW1 tiles, fc1 backward without its dW1 role) - runs in
-    the final SGD launch (fp32 default) or as the tail of the Winograd
-    bwd-data blocks; both update the parameters and momenta bit for bit like
-    the gradient-buffer path (test_native_rccl_comm_and_graph_capture)."""
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_fc_sgd_placements_bit_identical(cuda_dev, data, dtype):
+    """Where the single-rank FC-bucket SGD runs - fp32: with the fc1 weight
+    gradient formed inside it (fused dW1 tiles; fc1 backward runs without its
+    dW1 role) in the final SGD launch (default) or as the tail of the
+    Winograd bwd-data blocks; bf16: role blocks of the bwd-data launch
+    (default) or the final launch - never changes the parameters or momenta
+    (fp32 against the gradient-buffer path:
+    test_native_rccl_comm_and_graph_capture)."""
     x, y = data
     runs = []
     for rounds in (-1, 0, 2):
-        e = NativeMnistEngine(C.TrainConfig(graph=False).validate(), x, y, cuda_dev)
+        e = NativeMnistEngine(C.TrainConfig(graph=False, dtype=dtype).validate(), x, y, cuda_dev)
         e.exe.set_fc_sgd_rounds(rounds)
         e.train(7)
         runs.append(e)
