@@ -476,6 +476,42 @@ class NativeMnistEngine(MnistEngineBase):
         self.tune_steps_run = steps
         return steps
 
+    def prewarm_train(self, ms: float) -> float:
+        """Untimed, side-effect-free training replays for ~`ms` of wall time
+        (bench.py --prewarm train): the captured G-step graph is replayed
+        with the params, momentum and device step snapshotted first and
+        restored afterwards (as tune_schedule), so training continues
+        exactly where it was.  The replay count is agreed over the ranks
+        (max) before the loop: the graph holds the collectives at N > 1.
+        Returns the wall time spent (ms)."""
+        if ms <= 0 or not self.use_graph:
+            return 0.0
+        import time
+
+        from ..parallel import dist as D
+        if not self._tuned:
+            self.tune_schedule()
+        g = self._graph(self.graph_steps)
+        if g is None:
+            return 0.0
+        t_start = time.perf_counter()
+        self.exe.join(stream_handle())
+        self.exe.refresh_shadows(stream_handle())
+        snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
+        t0 = time.perf_counter()
+        g.replay()
+        torch.cuda.synchronize(self.device)
+        dt = max(time.perf_counter() - t0, 1e-6)
+        reps = int(D.allreduce_max_host(float(max(1, math.ceil(ms / 1000.0 / dt)))))
+        for _ in range(reps - 1):
+            g.replay()
+        self.exe.join(stream_handle())
+        self.params.copy_(snap[0])
+        self.mom.copy_(snap[1])
+        self.step_dev.copy_(snap[2])
+        torch.cuda.synchronize(self.device)
+        return round(1000.0 * (time.perf_counter() - t_start), 1)
+
     def train(self, k: int) -> None:
         if k <= 0:
             return
