@@ -27,7 +27,7 @@
 namespace gops {
 namespace tiled {
 
-constexpr int BK = 32, PAD = 4, NT = 256;
+constexpr int BK = 32, NT = 256;
 
 // Operand precision of the MFMA.  fp32 storage everywhere; BF16 converts the
 // tiles to bf16 as they are staged into LDS and runs v_mfma_f32_32x32x16_bf16
@@ -36,8 +36,18 @@ enum Prec { F32 = 0, BF16 = 1 };
 typedef __bf16 bfx8 __attribute__((ext_vector_type(8)));
 
 // LDS image of one K tile of an operand with ROWS rows (M or N):
-//   F32 : k-major [BK][ROWS + PAD] floats - the 32 lanes of a half-wave read
-//         32 consecutive rows of one k (the fp32 MFMA takes one k per lane)
+//   F32 : k-major [BK][ROWS] floats - the 32 lanes of a half-wave read 32
+//         consecutive rows of one k (the fp32 MFMA takes one k per lane).
+//         Unpadded, rows XOR-swizzled by 32 (k & 1) + 8 ((k >> 2) & 3): the
+//         two half-waves of a fragment read (k, k + 1) land in opposite bank
+//         halves (one pass of the 64-bank array) and a loader store of k = c,
+//         c + 4, ..., c + 28 x 8 rows spreads over 32 banks.  ResNet-18 fp32
+//         step, same box: 6.39 ms vs 6.44 with a pad of 4 floats (fwd 0.44-0.62
+//         vs 1.45-2.2 conflict cycles per LDS instruction, data 1.0 vs 4.0;
+//         profiles/r4_resnet18_fp32_pmc.txt).  A swizzle that also spreads the
+//         stores over all 64 banks (by (k ^ k >> 2) & 1, (k >> 3) & 3) cost
+//         more VALU than it saved (6.65 ms); a pad of 32 made the reads
+//         conflict-free but cost a block per CU (6.92 ms)
 //   BF16: row-major [ROWS][BK + 8] bf16 - each lane reads one 16-byte
 //         fragment (8 consecutive k of its row); the 80-byte row stride makes
 //         the ds_read_b128 lane groups conflict-free
@@ -47,16 +57,21 @@ struct Stage;
 
 template <int ROWS>
 struct Stage<F32, ROWS> {
-  static constexpr int LD = ROWS + PAD;
+  static_assert(ROWS % 64 == 0, "F32 stage rows: multiples of 64 (swizzle within 64-row groups)");
+  static constexpr int LD = ROWS;
   static constexpr int FLOATS = BK * LD;
+  // element (k, row); the swizzle keeps 4-row groups contiguous (put_r4)
+  static __device__ __forceinline__ int at(int k, int row) {
+    return k * LD + (row ^ ((k & 1) << 5) ^ (((k >> 2) & 3) << 3));
+  }
   static __device__ __forceinline__ void put_k4(float* T, int row, int k0, float4 v) {
-    T[(k0 + 0) * LD + row] = v.x;
-    T[(k0 + 1) * LD + row] = v.y;
-    T[(k0 + 2) * LD + row] = v.z;
-    T[(k0 + 3) * LD + row] = v.w;
+    T[at(k0 + 0, row)] = v.x;
+    T[at(k0 + 1, row)] = v.y;
+    T[at(k0 + 2, row)] = v.z;
+    T[at(k0 + 3, row)] = v.w;
   }
   static __device__ __forceinline__ void put_r4(float* T, int row0, int k, float4 v) {
-    *reinterpret_cast<float4*>(T + k * LD + row0) = v;
+    *reinterpret_cast<float4*>(T + at(k, row0)) = v;
   }
 };
 
@@ -93,14 +108,15 @@ __device__ __forceinline__ void mma_tile(const float* As, const float* Bs, int w
   using G = Geo<BM, BN, P>;
   const int r = lane & 31, h = lane >> 5;
   if constexpr (P == F32) {
-    constexpr int LDA = Stage<F32, BM>::LD, LDB = Stage<F32, BN>::LD;
+    using SA = Stage<F32, BM>;
+    using SB = Stage<F32, BN>;
 #pragma unroll
     for (int ks = 0; ks < BK / 2; ++ks) {
       float a[G::TM], b[G::TN];
 #pragma unroll
-      for (int i = 0; i < G::TM; ++i) a[i] = As[(2 * ks + h) * LDA + wm * (BM / 2) + 32 * i + r];
+      for (int i = 0; i < G::TM; ++i) a[i] = As[SA::at(2 * ks + h, wm * (BM / 2) + 32 * i + r)];
 #pragma unroll
-      for (int j = 0; j < G::TN; ++j) b[j] = Bs[(2 * ks + h) * LDB + wn * (BN / 2) + 32 * j + r];
+      for (int j = 0; j < G::TN; ++j) b[j] = Bs[SB::at(2 * ks + h, wn * (BN / 2) + 32 * j + r)];
 #pragma unroll
       for (int i = 0; i < G::TM; ++i)
 #pragma unroll
