@@ -94,6 +94,13 @@ void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float*
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr,
                                 const C1FilterArgs* c1 = nullptr,
                                 unsigned long long* prof = nullptr);
+// Both Winograd conv2 backward products in one launch: bwd-data (as
+// launch_conv2_bwd_data_wino, dy2t / Ud / a1 -> da1m, + the conv1 filter-grad
+// partials c1; no FC SGD) and the filter gradient (as
+// launch_conv2_bwd_filter_wino without its conv1 role: a1p / dy2 -> part2)
+void launch_conv2_bwd_wino(const float* dy2t, const float* Ud, const float* a1, const float* a1p,
+                           const float* dy2, int batch, float* da1m, float* part2,
+                           hipStream_t s, const C1FilterArgs* c1 = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 // fc1 train forward over the feature-major a2t [3136][batch] (batch % 32 ==

@@ -1298,11 +1298,13 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
 // partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
 // values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
 // no second pass over dA1 and no role blocks in the filter-gradient launch.
-template <bool PROF = false>
-__global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
-    const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
-    int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1,
-    unsigned long long* __restrict__ prof = nullptr) {
+// Block body (blk of nblk, threads 0 .. WNT - 1): the standalone kernel below,
+// or the bwd-data role of the merged conv2 backward launch
+template <bool PROF, bool FC = true>
+__device__ __forceinline__ void bwd_data_wino_block(
+    int blk, int nblk, const float* __restrict__ dy2t, const float* __restrict__ Ud,
+    const float* __restrict__ a1, int batch, float* __restrict__ da1m, const FcSgd& sgd,
+    const C1Filter& c1, unsigned long long* __restrict__ prof) {
   // PROF (labs): s_memtime per wave -> prof[block][wave][7]: start, half 0
   // transform / products, half 1 transform / products, dA1 written, end
   unsigned long long stamp[7];
@@ -1310,14 +1312,14 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   __shared__ float V[WV_FLOATS];
   // this block's FC SGD slice (sgd.nblk = 2 x blocks units), after its conv work
   auto fc_sgd_tail = [&]() {
-    if (sgd.n4 == 0) return;
+    if (!FC || sgd.n4 == 0) return;
     const int half = threadIdx.x >> 8, t = threadIdx.x & 255;
     if (sgd.a2)  // fused fc1 dW1 + SGD tiles, first halves of every block first
-      for (int d = half * gridDim.x + blockIdx.x; d < FC1BWD_DW_BLOCKS; d += 2 * gridDim.x)
+      for (int d = half * nblk + blk; d < FC1BWD_DW_BLOCKS; d += 2 * nblk)
         fc1_dw_sgd(sgd, d, t);
-    fc_sgd_role(sgd, 2 * blockIdx.x + half, nullptr, t);
+    fc_sgd_role(sgd, 2 * blk + half, nullptr, t);
   };
-  const int n = blockIdx.x >> 2, pg = blockIdx.x & 3;
+  const int n = blk >> 2, pg = blk & 3;
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform in an SGPR: the point index p, its output-transform weights
   // (scalar loads) and the fragment bases are then scalar
@@ -1489,9 +1491,17 @@ __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
   if constexpr (PROF) {
     stamp[6] = do_c1 ? __builtin_amdgcn_s_memtime() : stamp[5];
     if (lane == 0)
-      for (int k = 0; k < 7; ++k) prof[((size_t)blockIdx.x * WNW + wave) * 7 + k] = stamp[k];
+      for (int k = 0; k < 7; ++k) prof[((size_t)blk * WNW + wave) * 7 + k] = stamp[k];
   }
   fc_sgd_tail();
+}
+
+template <bool PROF = false>
+__global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
+    const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
+    int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1,
+    unsigned long long* __restrict__ prof = nullptr) {
+  bwd_data_wino_block<PROF>(blockIdx.x, gridDim.x, dy2t, Ud, a1, batch, da1m, sgd, c1, prof);
 }
 
 // ------------------------------------------ Winograd conv2 bwd-filter ----
@@ -1587,21 +1597,24 @@ __device__ __forceinline__ void wino_wgrad_row(const float* __restrict__ xs,
 
 // PROF: per-wave s_memtime stamps at the phase boundaries -> prof[block][wave][5]
 // (scripts/wino_lab.py --phases; never used by the executor)
+// Block body (blk): the standalone kernel below, or the filter-gradient role
+// of the merged conv2 backward launch (blk = block index - bwd-data blocks, a
+// multiple of 8: the XCD-aware group mapping is kept)
 template <bool PROF>
-__global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
-    int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
-    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter c1,
+__device__ __forceinline__ void bwd_filter_wino_block(
+    int blk, int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter& c1,
     unsigned long long* __restrict__ prof) {
   unsigned long long stamp[5];
   if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
   constexpr int SM = WF_SMEM > c1f_smem<1, WF_NT / 64>() ? WF_SMEM : c1f_smem<1, WF_NT / 64>();
   __shared__ float smem[SM];
-  if ((int)blockIdx.x >= nwg) {  // conv1 filter-grad role (its dA1 is final)
-    conv1_filter_unit<WF_NT, 1>(blockIdx.x - nwg, batch, c1, smem);
+  if (blk >= nwg) {  // conv1 filter-grad role (its dA1 is final)
+    conv1_filter_unit<WF_NT, 1>(blk - nwg, batch, c1, smem);
     return;
   }
   // XCD-aware: the 8 (ci, co) tiles of an image group share one XCD's L2
-  const int ngroups = nwg / 8, bid = blockIdx.x;
+  const int ngroups = nwg / 8, bid = blk;
   int g, sub;
   if (ngroups % 8 == 0) {
     const int x = bid & 7, idx = bid >> 3;
@@ -1743,7 +1756,38 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
   if constexpr (PROF) {
     stamp[4] = __builtin_amdgcn_s_memtime();
     if (lane == 0)
-      for (int k = 0; k < 5; ++k) prof[((size_t)blockIdx.x * (WF_NT / 64) + wave) * 5 + k] = stamp[k];
+      for (int k = 0; k < 5; ++k) prof[((size_t)blk * (WF_NT / 64) + wave) * 5 + k] = stamp[k];
+  }
+}
+
+template <bool PROF>
+__global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
+    int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter c1,
+    unsigned long long* __restrict__ prof) {
+  bwd_filter_wino_block<PROF>(blockIdx.x, batch, a1p, dy2, part2, part_db2, nwg, c1, prof);
+}
+
+// Both Winograd conv2 backward products in ONE launch (they depend only on
+// fc1 backward): blocks [0, nd) run the bwd-data body on their first WNT
+// threads (the surplus waves end at once - a barrier waits only for the
+// waves still alive), the rest the filter-gradient body.  One block per CU
+// either way (LDS, VGPRs); a CU moves on to its next block as soon as it
+// is done, so there is no launch boundary and no drain between the two.
+// No FC SGD tail here (its registers would spill at 768 threads): with the
+// FC SGD in the bwd-data launch the executor keeps the two launches.
+__global__ __launch_bounds__(WF_NT) void conv2_bwd_wino_kernel(
+    int nd, const float* __restrict__ dy2t, const float* __restrict__ Ud,
+    const float* __restrict__ a1, int batch, float* __restrict__ da1m,
+    const C1Filter c1, const float* __restrict__ a1p, const float* __restrict__ dy2,
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg) {
+  if ((int)blockIdx.x < nd) {
+    if (threadIdx.x >= WNT) return;
+    bwd_data_wino_block<false, false>(blockIdx.x, nd, dy2t, Ud, a1, batch, da1m, FcSgd{}, c1,
+                                      nullptr);
+  } else {
+    bwd_filter_wino_block<false>(blockIdx.x - nd, batch, a1p, dy2, part2, part_db2, nwg, C1Filter{},
+                                 nullptr);
   }
 }
 
@@ -2290,6 +2334,16 @@ void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch,
   const int n1 = c.part1 ? conv1_filter_blocks(batch, 1) : 0;
   conv2_bwd_filter_wino_kernel<false><<<8 * G + n1, WF_NT, 0, s>>>(
       batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, c, nullptr);
+}
+
+void launch_conv2_bwd_wino(const float* dy2t, const float* Ud, const float* a1, const float* a1p,
+                           const float* dy2, int batch, float* da1m, float* part2,
+                           hipStream_t s, const C1FilterArgs* c1) {
+  const int nd = batch * 4;
+  const int G = conv2_wino_filter_groups(batch);
+  conv2_bwd_wino_kernel<<<nd + 8 * G, WF_NT, 0, s>>>(nd, dy2t, Ud, a1, batch, da1m, c1_args(c1),
+                                                     a1p, dy2, part2, part2 + (size_t)G * 51200,
+                                                     8 * G);
 }
 
 void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,

@@ -102,18 +102,22 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
                                P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                P<float>(p.part1)};
-  if (p.wino)
+  if (p.wino && fc_sgd == nullptr) {  // bwd-data (+ conv1 filter grad) and filter grad: one launch
+    mnist::launch_conv2_bwd_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
+                                 P<const float>(p.a1), P<const float>(p.a1pf),
+                                 P<const float>(p.dy2), B, P<float>(p.da1m), P<float>(p.part2), s,
+                                 &c1);
+  } else if (p.wino) {  // the FC SGD rides in the bwd-data launch
     mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
                                       P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd, &c1);
-  else
-    mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
-                                    P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
-  if (p.wino)
     mnist::launch_conv2_bwd_filter_wino(P<const float>(p.a1pf), P<const float>(p.dy2), B,
                                         P<float>(p.part2), s);
-  else
+  } else {
+    mnist::launch_conv2_bwd_data_l2(P<const float>(p.dy2t), P<const float>(p.w2t),
+                                    P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd);
     mnist::launch_conv2_bwd_filter(P<const float>(p.a1pf), P<const float>(p.dy2), B,
                                    P<float>(p.part2), s, &c1);
+  }
   if (finalize)
     mnist::launch_grad_finalize(P<const float>(p.part2), conv2_groups(), P<const float>(p.part1),
                                 conv1_blocks(), G + p.off_w2, G + p.off_b2, G + p.off_w1,
