@@ -21,13 +21,14 @@ def main():
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--step-only", action="store_true",
                     help="only the graph-replayed step per FC SGD placement (any dtype)")
+    ap.add_argument("--rounds", default="0,2", help="FC SGD placements to time (fc_sgd_rounds)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     x, y = synthetic_rows("train", 0, 4096)
     cfg = C.TrainConfig(batch_size=a.batch, graph=False, dtype=a.dtype).validate()
     if a.step_only:
         e = NativeMnistEngine(cfg, x, y, dev)
-        step_placements(e)
+        step_placements(e, [int(r) for r in a.rounds.split(",")])
         return
     e = NativeMnistEngine(cfg, x, y, dev, fc1_feature_major=True)  # + the a2ft lab buffer
     e.train(5)
@@ -142,15 +143,15 @@ def main():
     e1.record()
     e1.synchronize()
     print(f"step (graph replay): {e0.elapsed_time(e1) * 1000.0 / 500:.2f} us")
-    step_placements(e)
+    step_placements(e, [int(r) for r in a.rounds.split(",")])
 
 
-def step_placements(e):
+def step_placements(e, rounds_list=(0, 2)):
     """Graph-replayed step with the single-rank FC momentum SGD in the conv2
     bwd-data launch (rounds > 0) or in the final SGD launch (rounds = 0)."""
     e.cfg.graph = True
     e.use_graph = True
-    for rounds in (0, 2):
+    for rounds in rounds_list:
         e.exe.set_fc_sgd_rounds(rounds)
         e._graphs.clear()
         e.capture(50)
