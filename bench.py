@@ -20,12 +20,12 @@ barrier + device synchronize on both sides; the slowest rank's time is
 used; rank 0 prints one JSON line.  Every timed step is a full training
 step (forward, backward, all-reduce, SGD update); eval is outside the
 timed region.  Before the W warm-up steps, --prewarm-ms (default 1000) of
-untimed replays of the captured training graph bring the GPU out of its
-idle clock state: params, momentum and step are snapshotted first and
-restored afterwards, so the run trains exactly as without it (reported as
-prewarm / prewarm_ms; --prewarm eval runs forward-only test-set passes
-instead: 20 timed steps measured 90.2-93.7 us after it vs 87.3-88.3 after
-the training replays, same box, steady state 85.5).  With N > 1 the
+forward-only test-set passes bring the GPU out of its idle clock state (no
+training state changes; reported as prewarm / prewarm_ms).  --prewarm train
+replays the captured training graph instead, on snapshotted state that is
+restored afterwards: a second of it at full load leaves the clocks lower
+for the short timed window that follows (20 steps: 125-133 us vs 85-92
+after the eval passes on one box, final round-4 build; steady state 84).  With N > 1 the
 sync schedule is autotuned first (real training steps, reported), and
 after the run every rank's weights are checksummed: replicas that differ
 fail the run (replicas_identical in the JSON).
@@ -77,7 +77,7 @@ def parse(argv=None):
                          "training state changes) so a short timed window does not measure "
                          "the GPU clock ramp (1 GPU: 20 replayed steps ran 114.8 -> 109.6 us "
                          "over the first 120 steps, steady state 108.6)")
-    ap.add_argument("--prewarm", default="train", choices=("eval", "train"),
+    ap.add_argument("--prewarm", default="eval", choices=("eval", "train"),
                     help="what the prewarm runs: forward-only test-set passes (eval), or "
                          "training-graph replays on snapshotted state that is restored "
                          "afterwards (train; engines with prewarm_train, else eval)")
