@@ -125,13 +125,14 @@ def test_maxpool(cuda_dev, k, stride, pad, H, C):
 
 
 @pytest.mark.parametrize("C", [16, 64])
-def test_maxpool_bf16_twin(cuda_dev, C):
+@pytest.mark.parametrize("H", [15, 14])  # C = 64: odd -> per-pixel, even -> 2x2-block bwd kernel
+def test_maxpool_bf16_twin(cuda_dev, C, H):
     """bf16 conv mode: the pool reads the input's attached bf16 twin (a
     twin-only BN output, whose fp32 storage is garbage here on purpose),
     records uint8 window taps and gives its output a bf16 twin; values and
     gradients equal torch's pool of the bf16-rounded input."""
     g = torch.Generator().manual_seed(5)
-    x = torch.randn(2, 15, 15, C, generator=g)
+    x = torch.randn(2, H, H, C, generator=g)
     xb = x.to(torch.bfloat16)
     xr = xb.float().clone().requires_grad_(True)
     yr = F.max_pool2d(xr.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
