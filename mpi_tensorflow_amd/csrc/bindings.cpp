@@ -500,6 +500,11 @@ PYBIND11_MODULE(_C, m) {
     check_launch();
   });
   g.def("maxpool_b16_ok", &gops::maxpool_b16_ok);
+  g.def("maxpool_fwd_u8", [](const gops::PoolShape& p, uintptr_t x, uintptr_t y, uintptr_t arg,
+                             uintptr_t st) {
+    gops::maxpool_fwd_u8(p, P<const float>(x), P<float>(y), P<uint8_t>(arg), S(st));
+    check_launch();
+  });
   g.def("maxpool_fwd_b16", [](const gops::PoolShape& p, uintptr_t xb, uintptr_t y, uintptr_t yb,
                               uintptr_t arg, uintptr_t st) {
     gops::maxpool_fwd_b16(p, P<const void>(xb), P<float>(y), P<void>(yb), P<uint8_t>(arg), S(st));

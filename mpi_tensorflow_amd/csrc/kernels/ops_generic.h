@@ -195,6 +195,8 @@ void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx,
 // bf16-twin form: xb = bf16 input, y (fp32) / yb (bf16) outputs each optional,
 // arg = window-relative tap (uint8); C % 4 == 0, k * k < 255
 bool maxpool_b16_ok(const PoolShape& p);
+// fp32 input, uint8 window-relative taps (maxpool_bwd_b8 takes them back)
+void maxpool_fwd_u8(const PoolShape& p, const float* x, float* y, uint8_t* arg, hipStream_t st);
 void maxpool_fwd_b16(const PoolShape& p, const void* xb, float* y, void* yb, uint8_t* arg,
                      hipStream_t st);
 void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, float* dx,

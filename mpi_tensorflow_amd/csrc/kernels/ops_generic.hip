@@ -447,8 +447,12 @@ __device__ __forceinline__ float4 bf4(uint2 u) {
 // KK / SS / PP / CC4: compile-time window, stride, pad and C/4 (the ResNet
 // stem's 3 / 2 / 1 / 16; 0 = read from p): the index math is then multiplies
 // and shifts instead of integer divides
-template <int KK, int SS, int PP, int CC4>
-__global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const uint2* __restrict__ x,
+__device__ __forceinline__ float4 pool_ld4(const uint2* x, int i) { return bf4(x[i]); }
+__device__ __forceinline__ float4 pool_ld4(const float4* x, int i) { return x[i]; }
+
+// XT: uint2 = 4 bf16 (the bf16 twin of the input), float4 = fp32 input
+template <int KK, int SS, int PP, int CC4, class XT = uint2>
+__global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const XT* __restrict__ x,
                                                             float4* __restrict__ y,
                                                             uint2* __restrict__ yb,
                                                             uchar4* __restrict__ arg) {
@@ -473,7 +477,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd4b_kernel(PoolShape p, const u
       for (int kw = 0; kw < p.k; ++kw) {
         const int ix = ox * p.stride - p.pad + kw;
         if (ix < 0 || ix >= p.W) continue;
-        const float4 v = bf4(x[((nn * p.H + iy) * p.W + ix) * C4 + c4]);
+        const float4 v = pool_ld4(x, ((nn * p.H + iy) * p.W + ix) * C4 + c4);
         const unsigned char r = (unsigned char)(kh * p.k + kw);
         if (v.x > b.x) { b.x = v.x; bi.x = r; }
         if (v.y > b.y) { b.y = v.y; bi.y = r; }
@@ -1188,6 +1192,18 @@ void maxpool_fwd_b16(const PoolShape& p, const void* xb, float* y, void* yb, uin
     maxpool_fwd4b_kernel<3, 2, 1, 16><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, YB, A);
   else
     maxpool_fwd4b_kernel<0, 0, 0, 0><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, YB, A);
+}
+
+void maxpool_fwd_u8(const PoolShape& p, const float* x, float* y, uint8_t* arg, hipStream_t st) {
+  if (!maxpool_b16_ok(p)) throw std::runtime_error("maxpool_fwd_u8: unsupported shape");
+  const long long n = (long long)p.N * p.OH * p.OW * p.C;
+  const auto X = reinterpret_cast<const float4*>(x);
+  const auto Y = reinterpret_cast<float4*>(y);
+  const auto A = reinterpret_cast<uchar4*>(arg);
+  if (p.k == 3 && p.stride == 2 && p.pad == 1 && p.C == 64)  // the ResNet stem pool
+    maxpool_fwd4b_kernel<3, 2, 1, 16, float4><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, nullptr, A);
+  else
+    maxpool_fwd4b_kernel<0, 0, 0, 0, float4><<<grid1d(n / 4), 256, 0, st>>>(p, X, Y, nullptr, A);
 }
 
 void maxpool_bwd_b8(const PoolShape& p, const float* dy, const uint8_t* arg, float* dx,

@@ -785,6 +785,12 @@ class _MaxPoolFn(torch.autograd.Function):
             C.ops.maxpool_fwd_b16(sh, ptr(xb), ptr(y), ptr(yb), ptr(arg), s)
             if yb is not None:
                 _attach_bf16(y, yb)
+        elif C.ops.maxpool_b16_ok(sh):
+            # fp32: uint8 window-relative taps too (a quarter of the int32
+            # argmax bytes; the backward's window-shared kernels take them)
+            ctx.b8 = True
+            arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.uint8, device=x.device)
+            C.ops.maxpool_fwd_u8(sh, ptr(x), ptr(y), ptr(arg), s)
         else:
             arg = torch.empty((N, sh.OH, sh.OW, Cc), dtype=torch.int32, device=x.device)
             C.ops.maxpool_fwd(sh, ptr(x), ptr(y), ptr(arg), s)
