@@ -162,20 +162,20 @@ PYBIND11_MODULE(_C, m) {
                                  P<float>(w2t), S(s));
     check_launch();
   });
-  k.def("conv2_bwd_data_wino", [](uintptr_t dy2t, uintptr_t Ud, uintptr_t a1, int batch,
+  k.def("conv2_bwd_data_wino", [](uintptr_t dy2, uintptr_t Ud, uintptr_t a1, int batch,
                                   uintptr_t da1m, uintptr_t s) {
-    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2t), P<const float>(Ud), P<const float>(a1),
+    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2), P<const float>(Ud), P<const float>(a1),
                                       batch, P<float>(da1m), S(s));
     check_launch();
   });
   // labs: with the conv1 filter-gradient epilogue and per-wave phase stamps
-  k.def("conv2_bwd_data_wino_prof", [](uintptr_t dy2t, uintptr_t Ud, uintptr_t a1, int batch,
+  k.def("conv2_bwd_data_wino_prof", [](uintptr_t dy2, uintptr_t Ud, uintptr_t a1, int batch,
                                        uintptr_t da1m, uintptr_t data, uintptr_t step, int n_local,
                                        uintptr_t idx1, uintptr_t part1, uintptr_t prof,
                                        uintptr_t s) {
     const mnist::C1FilterArgs c1{P<const float>(data), P<const long long>(step), n_local,
                                  P<const float>(da1m), P<const uint8_t>(idx1), P<float>(part1)};
-    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2t), P<const float>(Ud), P<const float>(a1),
+    mnist::launch_conv2_bwd_data_wino(P<const float>(dy2), P<const float>(Ud), P<const float>(a1),
                                       batch, P<float>(da1m), S(s), nullptr, &c1,
                                       P<unsigned long long>(prof));
     check_launch();

@@ -87,20 +87,20 @@ void launch_conv12_fwd_wino(const C12In& c1, int batch, const float* w2, const f
                             unsigned long long* prof = nullptr, float* a2t = nullptr);
 void launch_conv2_fwd_wino(const float* a1, int batch, const float* w2, const float* U,
                            const float* b, float* out, uint8_t* argmax, float* w2t, hipStream_t s);
-// Winograd bwd-data: dy2t as for launch_conv2_bwd_data_l2, Ud from
+// Winograd bwd-data: dy2 = NHWC dY2 [B][14][14][64] (launch_fc1_bwd), Ud from
 // launch_conv2_wino_weights; da1m = dA1 masked by a1 > 0
 // prof (labs): per-wave phase stamps [blocks][8 waves][7] (s_memtime)
-void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
+void launch_conv2_bwd_data_wino(const float* dy2, const float* Ud, const float* a1, int batch,
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd = nullptr,
                                 const C1FilterArgs* c1 = nullptr,
                                 unsigned long long* prof = nullptr);
 // Both Winograd conv2 backward products in one launch: bwd-data (as
-// launch_conv2_bwd_data_wino, dy2t / Ud / a1 -> da1m, + the conv1 filter-grad
+// launch_conv2_bwd_data_wino, dy2 / Ud / a1 -> da1m, + the conv1 filter-grad
 // partials c1; no FC SGD) and the filter gradient (as
 // launch_conv2_bwd_filter_wino without its conv1 role: a1p / dy2 -> part2)
-void launch_conv2_bwd_wino(const float* dy2t, const float* Ud, const float* a1, const float* a1p,
-                           const float* dy2, int batch, float* da1m, float* part2,
-                           hipStream_t s, const C1FilterArgs* c1 = nullptr);
+void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, const float* dy2,
+                           int batch, float* da1m, float* part2, hipStream_t s,
+                           const C1FilterArgs* c1 = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 // fc1 train forward over the feature-major a2t [3136][batch] (batch % 32 ==
@@ -118,8 +118,8 @@ void launch_fc_head_train(const float* part, const float* b3, const float* w4, c
                           uint16_t* dht16 = nullptr, int splits = 14);  // slabs in part
 void launch_fc_head_eval(const float* h, const float* w4, const float* b4, const int* labels,
                          int M, float* logits, int* errors, hipStream_t s);
-// dY2 as NHWC dy2 [B][14][14][64] and channel-major zero-bordered dy2t
-// [B][64][18][MNIST32_T_LD]
+// dY2 as NHWC dy2 [B][14][14][64] and (dy2t != nullptr: the direct
+// bwd-data's operand) channel-major zero-bordered dy2t [B][64][18][MNIST32_T_LD]
 void launch_fc1_bwd(const float* a2, const uint8_t* idx2, const float* dh, const float* hd,
                     const float* dlog, const float* w1, int batch, float* g_w3, float* g_b3,
                     float* g_w4, float* g_b4, float* dy2, float* dy2t, hipStream_t s,

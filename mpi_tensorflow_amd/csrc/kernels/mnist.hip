@@ -1278,11 +1278,15 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
 
 // ------------------------------------ conv2 bwd-data, Winograd F(2x2,5x5) ----
 // dA1 = dY2 (x) rot180(W2) with the channel roles swapped: the forward form
-// on the zero-bordered channel-major dY2 image dy2t [n][64][18][MNIST32_T_LD]
-// (written by fc1 backward) with the filters Ud [36][64][32].  (Reading the
-// NHWC dy2 instead, lanes along the channels, measured 3.3 us slower in
-// isolation - h0 transform 10.1 vs 6.2 K cycles, h0 products 12.8 vs 6.7 K -
-// more than the 2.7 us the dy2t stores cost fc1 backward.)  Block = (image,
+// on the NHWC dY2 image dy2 [n][14][14][64] (fc1 backward's coalesced output,
+// the filter gradient's operand) with the filters Ud [36][64][32].  Each
+// half's input band (8 pixel rows x 14 columns x 32 channels) is fetched with
+// coalesced float4 loads - both halves' issued at the start - and staged
+// channel-major with zero borders in LDS (WB_FLOATS), from which the
+// (tile, channel) threads read their 6 x 6 windows.  A channel-major
+// zero-bordered copy written by fc1 backward instead cost its dX role 2.7 us
+// of 8-byte scattered stores; per-thread window loads straight from the NHWC
+// image (36 single floats) were 3.3 us slower than from that copy.  Block = (image,
 // pair of 2x2-tile rows) = 14 tiles (M 16), N = 32 input channels of conv2,
 // K = 64 in two halves of 32 (the transformed image V is 72 KB per half).
 // Waves = (ci half, quarter of the 36 points), each point's 8 k-steps per K
@@ -1298,18 +1302,25 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
 // partial of its band of a1 rows (4 pg .. 4 pg + 3) straight from the dA1
 // values it just produced (part1[n * 4 + pg], the conv1_filter_unit math):
 // no second pass over dA1 and no role blocks in the filter-gradient launch.
-// Block body (blk of nblk, threads 0 .. WNT - 1): the standalone kernel below,
-// or the bwd-data role of the merged conv2 backward launch
+// the staged input band of one K half: [32 ch][8 rows][18 cols] (pixel rows
+// 4 pg - 2 .. 4 pg + 5, columns -2 .. 15; zero outside the image)
+constexpr int WB_ROWS = 8, WB_COLS = 18, WB_FLOATS = 32 * WB_ROWS * WB_COLS;
+constexpr int WD_SMEM = WV_FLOATS + WB_FLOATS;  // bwd-data body LDS (floats)
+
+// Block body (blk of nblk, threads 0 .. WNT - 1, smem: WD_SMEM floats): the
+// standalone kernel below, or the bwd-data role of the merged conv2 backward
+// launch
 template <bool PROF, bool FC = true>
 __device__ __forceinline__ void bwd_data_wino_block(
-    int blk, int nblk, const float* __restrict__ dy2t, const float* __restrict__ Ud,
+    int blk, int nblk, const float* __restrict__ dy2, const float* __restrict__ Ud,
     const float* __restrict__ a1, int batch, float* __restrict__ da1m, const FcSgd& sgd,
-    const C1Filter& c1, unsigned long long* __restrict__ prof) {
+    const C1Filter& c1, unsigned long long* __restrict__ prof, float* smem) {
   // PROF (labs): s_memtime per wave -> prof[block][wave][7]: start, half 0
   // transform / products, half 1 transform / products, dA1 written, end
   unsigned long long stamp[7];
   if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
-  __shared__ float V[WV_FLOATS];
+  float* V = smem;
+  float* SB = smem + WV_FLOATS;  // staged input band (WB_FLOATS)
   // this block's FC SGD slice (sgd.nblk = 2 x blocks units), after its conv work
   auto fc_sgd_tail = [&]() {
     if (!FC || sgd.n4 == 0) return;
@@ -1330,22 +1341,57 @@ __device__ __forceinline__ void bwd_data_wino_block(
   f32x4 y[4];
 #pragma unroll
   for (int o = 0; o < 4; ++o) y[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // input windows of channels 32 half .. 32 half + 31 straight from L2 (one
-  // (tile, channel) item per thread); half 1's loads are issued before half
-  // 0's products so their latency hides under the MFMAs
+  // input bands: 2 x (8 rows x 14 columns x 8 float4) = 2 x 896 float4, both
+  // halves' coalesced loads issued now (rows outside the image read a clamped
+  // row and stage zeros); a (tile, channel) item per thread reads its 6 x 6
+  // window from the staged band
   const int it_t = tid & 15, it_c = tid >> 4;
   const int it_tr = 2 * pg + it_t / 7, it_tc = it_t % 7;
   const bool it_ok = it_t < 14 && it_tr < 7;
-  auto load_in = [&](int half, float (&d)[36]) {
-    const float* src = dy2t + ((size_t)(n * 64 + 32 * half + it_c) * 18 + 2 * (it_ok ? it_tr : 0)) *
-                                  MNIST32_T_LD + 2 * (it_ok ? it_tc : 0);
+  const int y0b = 4 * pg - 2;  // image row of band row 0
+  constexpr int BAND4 = WB_ROWS * 14 * 8, BJ = (BAND4 + WNT - 1) / WNT;  // 896 float4, 2 / thread
+  float4 bq[2][BJ];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const int f = min(tid + WNT * j, BAND4 - 1), c4 = f & 7, pix = f >> 3;
+      const int y = min(max(y0b + pix / 14, 0), 13), x = pix % 14;
+      bq[hh][j] = *reinterpret_cast<const float4*>(dy2 + ((size_t)(n * 14 + y) * 14 + x) * 64 +
+                                                   32 * hh + 4 * c4);
+    }
+  auto stage = [&](int hh) {  // band hh -> SB (zero borders); no barrier
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const int f = tid + WNT * j;
+      if (f < BAND4) {
+        const int c4 = f & 7, pix = f >> 3, r = pix / 14, x = pix % 14;
+        const bool ok = y0b + r >= 0 && y0b + r < 14;
+        float* d = SB + ((4 * c4) * WB_ROWS + r) * WB_COLS + x + 2;
+        d[0] = ok ? bq[hh][j].x : 0.f;
+        d[WB_ROWS * WB_COLS] = ok ? bq[hh][j].y : 0.f;
+        d[2 * WB_ROWS * WB_COLS] = ok ? bq[hh][j].z : 0.f;
+        d[3 * WB_ROWS * WB_COLS] = ok ? bq[hh][j].w : 0.f;
+      }
+    }
+    // the 2 + 2 zero columns of every (channel, row): 32 x 8 x 4 = 1024 cells
+    for (int e = tid; e < 32 * WB_ROWS * 4; e += WNT) {
+      const int col = e & 3, cr = e >> 2;
+      SB[cr * WB_COLS + (col < 2 ? col : WB_COLS - 4 + col)] = 0.f;
+    }
+  };
+  auto load_in = [&](float (&d)[36]) {  // this thread's window from the staged band
+    const float* src = SB + (it_c * WB_ROWS + 2 * (it_ok ? it_tr : 2 * pg) - 4 * pg) * WB_COLS +
+                       2 * (it_ok ? it_tc : 0);
 #pragma unroll
     for (int yy = 0; yy < 6; ++yy)
 #pragma unroll
-      for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[yy * MNIST32_T_LD + xx];
+      for (int xx = 0; xx < 6; ++xx) d[yy * 6 + xx] = src[yy * WB_COLS + xx];
   };
+  stage(0);
+  __syncthreads();
   float din[36];
-  load_in(0, din);
+  load_in(din);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     {  // input transform
@@ -1366,9 +1412,9 @@ __device__ __forceinline__ void bwd_data_wino_block(
     };
     float bA[24], bB[24];
     loadb3(9 * pq, bA);
-    // half 1's inputs, in flight during half 0's products (loads return in
-    // order: issued after the first fragments, the first products do not wait)
-    if (half == 0) load_in(1, din);
+    // half 1's band into the staging buffer (every thread read its half-0
+    // window before the barrier above); read back after the next barrier
+    if (half == 0) stage(1);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {  // three points at a time
       const int p0 = 9 * pq + 3 * i;
@@ -1397,6 +1443,7 @@ __device__ __forceinline__ void bwd_data_wino_block(
     }
     if constexpr (PROF) stamp[2 + 2 * half] = __builtin_amdgcn_s_memtime();
     __syncthreads();  // V is rewritten by the next half / the reduction
+    if (half == 0) load_in(din);
   }
   // every wave's partial outputs -> R [qw][pq][o][reg][lane]; the epilogue
   // threads sum the four point quarters in order
@@ -1498,10 +1545,11 @@ __device__ __forceinline__ void bwd_data_wino_block(
 
 template <bool PROF = false>
 __global__ __launch_bounds__(WNT) void conv2_bwd_data_wino_kernel(
-    const float* __restrict__ dy2t, const float* __restrict__ Ud, const float* __restrict__ a1,
+    const float* __restrict__ dy2, const float* __restrict__ Ud, const float* __restrict__ a1,
     int batch, float* __restrict__ da1m, const FcSgd sgd, const C1Filter c1,
     unsigned long long* __restrict__ prof = nullptr) {
-  bwd_data_wino_block<PROF>(blockIdx.x, gridDim.x, dy2t, Ud, a1, batch, da1m, sgd, c1, prof);
+  __shared__ float smem[WD_SMEM];
+  bwd_data_wino_block<PROF>(blockIdx.x, gridDim.x, dy2, Ud, a1, batch, da1m, sgd, c1, prof, smem);
 }
 
 // ------------------------------------------ Winograd conv2 bwd-filter ----
@@ -1600,15 +1648,14 @@ __device__ __forceinline__ void wino_wgrad_row(const float* __restrict__ xs,
 // Block body (blk): the standalone kernel below, or the filter-gradient role
 // of the merged conv2 backward launch (blk = block index - bwd-data blocks, a
 // multiple of 8: the XCD-aware group mapping is kept)
+constexpr int WF_SMEM_ALL = WF_SMEM > c1f_smem<1, WF_NT / 64>() ? WF_SMEM : c1f_smem<1, WF_NT / 64>();
 template <bool PROF>
 __device__ __forceinline__ void bwd_filter_wino_block(
     int blk, int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
     float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter& c1,
-    unsigned long long* __restrict__ prof) {
+    unsigned long long* __restrict__ prof, float* smem) {
   unsigned long long stamp[5];
   if constexpr (PROF) stamp[0] = __builtin_amdgcn_s_memtime();
-  constexpr int SM = WF_SMEM > c1f_smem<1, WF_NT / 64>() ? WF_SMEM : c1f_smem<1, WF_NT / 64>();
-  __shared__ float smem[SM];
   if (blk >= nwg) {  // conv1 filter-grad role (its dA1 is final)
     conv1_filter_unit<WF_NT, 1>(blk - nwg, batch, c1, smem);
     return;
@@ -1765,7 +1812,8 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
     int batch, const float* __restrict__ a1p, const float* __restrict__ dy2,
     float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const C1Filter c1,
     unsigned long long* __restrict__ prof) {
-  bwd_filter_wino_block<PROF>(blockIdx.x, batch, a1p, dy2, part2, part_db2, nwg, c1, prof);
+  __shared__ float smem[WF_SMEM_ALL];
+  bwd_filter_wino_block<PROF>(blockIdx.x, batch, a1p, dy2, part2, part_db2, nwg, c1, prof, smem);
 }
 
 // Both Winograd conv2 backward products in ONE launch (they depend only on
@@ -1777,17 +1825,19 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
 // No FC SGD tail here (its registers would spill at 768 threads): with the
 // FC SGD in the bwd-data launch the executor keeps the two launches.
 __global__ __launch_bounds__(WF_NT) void conv2_bwd_wino_kernel(
-    int nd, const float* __restrict__ dy2t, const float* __restrict__ Ud,
+    int nd, const float* __restrict__ Ud,
     const float* __restrict__ a1, int batch, float* __restrict__ da1m,
     const C1Filter c1, const float* __restrict__ a1p, const float* __restrict__ dy2,
     float* __restrict__ part2, float* __restrict__ part_db2, int nwg) {
+  // one LDS pool for either role
+  __shared__ float smem[WD_SMEM > WF_SMEM_ALL ? WD_SMEM : WF_SMEM_ALL];
   if ((int)blockIdx.x < nd) {
     if (threadIdx.x >= WNT) return;
-    bwd_data_wino_block<false, false>(blockIdx.x, nd, dy2t, Ud, a1, batch, da1m, FcSgd{}, c1,
-                                      nullptr);
+    bwd_data_wino_block<false, false>(blockIdx.x, nd, dy2, Ud, a1, batch, da1m, FcSgd{}, c1,
+                                      nullptr, smem);
   } else {
     bwd_filter_wino_block<false>(blockIdx.x - nd, batch, a1p, dy2, part2, part_db2, nwg, C1Filter{},
-                                 nullptr);
+                                 nullptr, smem);
   }
 }
 
@@ -2291,7 +2341,7 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
                                                                      sg);
 }
 
-void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float* a1, int batch,
+void launch_conv2_bwd_data_wino(const float* dy2, const float* Ud, const float* a1, int batch,
                                 float* da1m, hipStream_t s, const FcSgdArgs* fc_sgd,
                                 const C1FilterArgs* c1, unsigned long long* prof) {
   FcSgd sg = fc_sgd_args(fc_sgd);
@@ -2299,10 +2349,10 @@ void launch_conv2_bwd_data_wino(const float* dy2t, const float* Ud, const float*
   // the FC SGD runs in 256-thread units, two per (conv) block
   sg.nblk = 2 * batch * 4;
   if (prof)
-    conv2_bwd_data_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m, sg,
+    conv2_bwd_data_wino_kernel<true><<<batch * 4, WNT, 0, s>>>(dy2, Ud, a1, batch, da1m, sg,
                                                               c1_args(c1), prof);
   else
-    conv2_bwd_data_wino_kernel<false><<<batch * 4, WNT, 0, s>>>(dy2t, Ud, a1, batch, da1m, sg,
+    conv2_bwd_data_wino_kernel<false><<<batch * 4, WNT, 0, s>>>(dy2, Ud, a1, batch, da1m, sg,
                                                                c1_args(c1));
 }
 
@@ -2336,14 +2386,13 @@ void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch,
       batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, c, nullptr);
 }
 
-void launch_conv2_bwd_wino(const float* dy2t, const float* Ud, const float* a1, const float* a1p,
-                           const float* dy2, int batch, float* da1m, float* part2,
-                           hipStream_t s, const C1FilterArgs* c1) {
+void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, const float* dy2,
+                           int batch, float* da1m, float* part2, hipStream_t s,
+                           const C1FilterArgs* c1) {
   const int nd = batch * 4;
   const int G = conv2_wino_filter_groups(batch);
-  conv2_bwd_wino_kernel<<<nd + 8 * G, WF_NT, 0, s>>>(nd, dy2t, Ud, a1, batch, da1m, c1_args(c1),
-                                                     a1p, dy2, part2, part2 + (size_t)G * 51200,
-                                                     8 * G);
+  conv2_bwd_wino_kernel<<<nd + 8 * G, WF_NT, 0, s>>>(nd, Ud, a1, batch, da1m, c1_args(c1), a1p,
+                                                     dy2, part2, part2 + (size_t)G * 51200, 8 * G);
 }
 
 void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,

@@ -94,7 +94,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
                         P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
                         G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
-                        P<float>(p.dy2t), s,
+                        p.wino ? nullptr : P<float>(p.dy2t), s,
                         factors ? 1 : (fc1_dw_fused ? 5 : 7));
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   // conv1 filter grad: Winograd - in the bwd-data blocks' epilogue, from the
@@ -103,12 +103,11 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                                P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                P<float>(p.part1)};
   if (p.wino && fc_sgd == nullptr) {  // bwd-data (+ conv1 filter grad) and filter grad: one launch
-    mnist::launch_conv2_bwd_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
-                                 P<const float>(p.a1), P<const float>(p.a1pf),
-                                 P<const float>(p.dy2), B, P<float>(p.da1m), P<float>(p.part2), s,
-                                 &c1);
+    mnist::launch_conv2_bwd_wino(P<const float>(p.wino_ud), P<const float>(p.a1),
+                                 P<const float>(p.a1pf), P<const float>(p.dy2), B,
+                                 P<float>(p.da1m), P<float>(p.part2), s, &c1);
   } else if (p.wino) {  // the FC SGD rides in the bwd-data launch
-    mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2t), P<const float>(p.wino_ud),
+    mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2), P<const float>(p.wino_ud),
                                       P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd, &c1);
     mnist::launch_conv2_bwd_filter_wino(P<const float>(p.a1pf), P<const float>(p.dy2), B,
                                         P<float>(p.part2), s);

@@ -43,7 +43,7 @@ struct MnistPtrs {
   // activations / workspaces
   uintptr_t a1 = 0, idx1 = 0, a2 = 0, idx2 = 0, fc1_part = 0, hd = 0, dh = 0, dlog = 0,
             loss_rows = 0, dy2 = 0, da1m = 0, part2 = 0, part1 = 0, w2t = 0, a1pf = 0;
-  // fp32: dy2t = channel-major zero-bordered dY2 (bwd-data operand); a1pf =
+  // fp32: dy2t = channel-major zero-bordered dY2 (direct bwd-data operand); a1pf =
   // zero-bordered NHWC a1 [B][18][18][32] (filter-grad operand).
   // bf16 engine (bf16 != 0): bf16 activation images and weight shadows
   // (layouts: kernels/mnist_bf16.h); a1 / a2 / dy2 / w2t above are unused

@@ -53,7 +53,7 @@ def main():
             ptr(e.train_x), ptr(e.step_dev), e.n_local, B, W("conv1_weight"), W("conv1_bias"),
             ptr(b["a1"]), ptr(b["a1pf"]), ptr(b["idx1"]), W("conv2_weight"), ptr(b["wino_u"]),
             W("conv2_bias"), ptr(b["a2"]), ptr(b["idx2"]), 0, s, 0, ptr(b["a2ft"])),
-        "conv2_bwd_data_wino": lambda: k.conv2_bwd_data_wino(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]),
+        "conv2_bwd_data_wino": lambda: k.conv2_bwd_data_wino(ptr(b["dy2"]), ptr(b["wino_ud"]), ptr(b["a1"]),
                                                              B, ptr(b["da1m"]), s),
         "fc1_fwd": lambda: k.fc1_fwd_train(ptr(b["a2"]), W("fc1_weight"), B, ptr(b["fc1_part"]), s),
         "fc1_fwd_t": lambda: k.fc1_fwd_train_t(ptr(b["a2ft"]), W("fc1_weight"), B, ptr(b["fc1_part"]),

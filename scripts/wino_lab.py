@@ -46,7 +46,7 @@ def main():
                                                         ptr(b["da1m"]), s),
         "wgrad(direct)": lambda: k.conv2_bwd_filter(ptr(b["a1pf"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
         "wgrad(wino)": lambda: k.conv2_bwd_filter_wino(ptr(b["a1pf"]), ptr(b["dy2"]), B, ptr(b["part2"]), s),
-        "bwd_data(wino)": lambda: k.conv2_bwd_data_wino(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]),
+        "bwd_data(wino)": lambda: k.conv2_bwd_data_wino(ptr(b["dy2"]), ptr(b["wino_ud"]), ptr(b["a1"]),
                                                         B, ptr(b["da1m"]), s),
     }
     if a.phases:
@@ -76,7 +76,7 @@ def main():
                               W_("conv1_bias"), ptr(b["a1"]), ptr(b["a1pf"]), ptr(b["idx1"]),
                               W_("conv2_weight"), ptr(b["wino_u"]), W_("conv2_bias"), ptr(b["a2"]),
                               ptr(b["idx2"]), 0, s, ptr(pf))
-            k.conv2_bwd_data_wino_prof(ptr(b["dy2t"]), ptr(b["wino_ud"]), ptr(b["a1"]), B,
+            k.conv2_bwd_data_wino_prof(ptr(b["dy2"]), ptr(b["wino_ud"]), ptr(b["a1"]), B,
                                        ptr(b["da1m"]), ptr(e.train_x), ptr(e.step_dev), e.n_local,
                                        ptr(b["idx1"]), ptr(part1), ptr(pb), s)
         torch.cuda.synchronize()
