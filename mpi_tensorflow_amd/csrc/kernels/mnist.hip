@@ -813,6 +813,41 @@ __device__ __forceinline__ void conv1_into_halo_t(const C12In& c1, int batch, in
   }
 }
 
+// Winograd forward: the halo tile plus the owned rows' argmax taps in LDS
+// (q1 [4 rows][14][32]); the owned a1 / a1pf / idx1 rows go out at the end of
+// the kernel (halo_flush_owned) as coalesced float4 / u32 stores, so no
+// global store of the conv1 epilogue waits in front of the phase barrier.
+struct HaloF32Tile {
+  float* xs;
+  uint8_t* q1;
+  int y0, yo;  // a1 row of halo row 0, first owned a1 row (4 pg)
+  __device__ __forceinline__ void zero(int tid, int nt) const {
+    for (int i = tid; i < C2_XS; i += nt) xs[i] = 0.f;
+  }
+  __device__ __forceinline__ void put(int y, int x, int co, float o, int qq, bool own) const {
+    xs[((y - y0) * C2_XS_COLS + x + 2) * 33 + co] = o;
+    if (own) q1[((y - yo) * 14 + x) * 32 + co] = (uint8_t)qq;
+  }
+};
+constexpr int C12_Q1_BYTES = 4 * 14 * 32;
+
+// the owned rows 4 pg .. 4 pg + 3 (clipped at 14) from the halo tile: f4 is
+// this thread's float4 index, nt4 the stride (448 float4 per 4 rows)
+__device__ __forceinline__ void halo_flush_owned(const C12In& c1, const float* xs,
+                                                 const uint8_t* q1, int n, int pg, int f4,
+                                                 int nt4) {
+  const int yo = 4 * pg, nf = min(4, 14 - yo) * 14 * 8;
+  for (int e = f4; e < nf; e += nt4) {
+    const int c = 4 * (e & 7), pix = e >> 3, r = pix / 14, x = pix % 14;
+    const float* s = xs + ((r + 2) * C2_XS_COLS + x + 2) * 33 + c;
+    const float4 v = make_float4(s[0], s[1], s[2], s[3]);
+    const size_t pi = ((size_t)(n * 14 + yo + r) * 14 + x) * 32 + c;
+    *reinterpret_cast<float4*>(c1.a1 + pi) = v;
+    *reinterpret_cast<float4*>(c1.a1pf + ((size_t)(n * 18 + yo + r + 2) * 18 + x + 2) * 32 + c) = v;
+    *reinterpret_cast<uint32_t*>(c1.idx1 + pi) = *reinterpret_cast<const uint32_t*>(q1 + pix * 32 + c);
+  }
+}
+
 template <int NT = 256>
 __device__ __forceinline__ void conv1_into_halo(const C12In& c1, int batch, int n, int pg,
                                                 float* __restrict__ xs, float* __restrict__ img) {
@@ -1124,6 +1159,7 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   __shared__ float xs[WX_FLOATS];
   __shared__ float img[FUSED ? C12_IMG_ROWS * C12_IMG_LD : 1];
   __shared__ float V[WV_FLOATS];
+  __shared__ __attribute__((aligned(4))) uint8_t q1[FUSED ? C12_Q1_BYTES : 4];
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3, pr0 = 2 * pg;
   const int tid = threadIdx.x, lane = tid & 63;
   // wave-uniform in an SGPR: the point index p, its output-transform weights
@@ -1137,7 +1173,7 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   }
   for (int i = C2_XS + tid; i < WX_FLOATS; i += WNT) xs[i] = 0.f;
   if constexpr (FUSED) {
-    conv1_into_halo<WNT>(c1, batch, n, pg, xs, img);
+    conv1_into_halo_t<WNT>(c1, batch, n, pg, img, HaloF32Tile{xs, q1, 4 * pg - 2, 4 * pg});
   } else {
     constexpr int NS = C2_XS_ROWS * C2_XS_COLS * 32 / WNT;  // 9
     float sv[NS];
@@ -1268,6 +1304,9 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
         if (out_t) out_t[(size_t)fi * batch + n] = o;
       }
     }
+  } else if constexpr (FUSED) {
+    // the half-1 waves write the owned conv1 rows while half 0 runs the epilogue
+    halo_flush_owned(c1, xs, q1, n, pg, tid - WNT / 2, WNT / 2);
   }
   if constexpr (PROF) {
     stamp[4] = __builtin_amdgcn_s_memtime();
