@@ -61,7 +61,9 @@ def parse(argv=None):
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto",
-                    choices=("auto", "buckets", "sharded", "split", "factors", "serial"))
+                    choices=("auto", "buckets", "sharded", "split", "factors", "serial", "defer"))
+    ap.add_argument("--defer-split", type=float, default=0.5,
+                    help="defer schedule: fraction of the FC bucket reduced under the conv backward")
     ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "torch"),
                     help="device communicator (auto: RCCL, or shared memory when ranks share GPUs)")
     ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),
@@ -214,7 +216,7 @@ def run(a, di, device, wd) -> int:
     cfg = C.TrainConfig(model=a.model, batch_size=a.batch_size, dtype=a.dtype, sync=a.sync,
                         graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend,
                         sync_schedule=a.sync_schedule, comm=a.comm,
-                        grad_comm_dtype=a.grad_comm_dtype,
+                        defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
                         collective_timeout_s=a.collective_timeout_s).validate()
     force = bool((a.force_sync or a.comm_emulate) and N == 1 and device.type == "cuda")
     with wd.guard("start-up (communicator, engine)"):

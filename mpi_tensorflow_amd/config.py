@@ -65,7 +65,7 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
 # "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
 # compute stream over a second communicator
-SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial")
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer")
 # device communicator (world > 1): "auto" = native RCCL when every rank has a
 # GPU of its own, the shared-memory host-staged communicator when ranks share
 # GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",
@@ -88,6 +88,9 @@ class TrainConfig:
     sync: str = "grad"
     sync_every: int = SYNC_EVERY
     sync_schedule: str = "auto"
+    # "defer" schedule: fraction of the FC bucket all-reduced under the conv
+    # backward (the rest overlaps the next step's conv forward)
+    defer_split: float = 0.5
     # dtype of the gradient collectives: fp32 (the reference's MPI Gather of
     # fp32 tensors) or bf16 (half the bytes over xGMI; the sum is rounded to
     # bf16 on the wire, the update stays fp32)
@@ -144,6 +147,8 @@ class TrainConfig:
         if self.sync_schedule not in SYNC_SCHEDULES:
             raise ValueError(f"unknown sync schedule {self.sync_schedule!r}; "
                              f"choose from {SYNC_SCHEDULES}")
+        if not 0.0 < self.defer_split < 1.0:
+            raise ValueError(f"defer_split must be in (0, 1), got {self.defer_split}")
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError(f"unknown grad comm dtype {self.grad_comm_dtype!r}")
         if self.conv_algo not in ("winograd", "direct"):
@@ -198,7 +203,10 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
     p.add_argument("--sync-every", type=int, default=d.sync_every)
     p.add_argument("--sync-schedule", default=d.sync_schedule, choices=SYNC_SCHEDULES,
                    help="native MNIST grad-sync schedule (auto / buckets / sharded FC update / "
-                        "factors: all-gather the FC gradient factors, fp32)")
+                        "factors: all-gather the FC gradient factors, fp32 / defer: FC part B "
+                        "overlaps the next conv forward, fp32)")
+    p.add_argument("--defer-split", type=float, default=d.defer_split,
+                   help="defer schedule: fraction of the FC bucket reduced under the conv backward")
     p.add_argument("--grad-comm-dtype", default=d.grad_comm_dtype, choices=("fp32", "bf16"),
                    help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--comm", default=d.comm, choices=COMMS,

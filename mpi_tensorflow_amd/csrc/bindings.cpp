@@ -738,6 +738,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("schedule", &MnistExecutor::schedule)
       .def("sharded_ok", &MnistExecutor::sharded_ok)
       .def("factors_ok", &MnistExecutor::factors_ok)
+      .def("defer_ok", &MnistExecutor::defer_ok)
+      .def("set_defer_split", &MnistExecutor::set_defer_split)
+      .def_property_readonly("defer_split", &MnistExecutor::defer_split)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
       .def("gather_optimizer_state",
            [](MnistExecutor& e, uintptr_t s, Collective* comm, uintptr_t cs) {
@@ -768,6 +771,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_SPLIT") = (int)MnistExecutor::SCHED_SPLIT;
   m.attr("MnistExecutor").attr("SCHED_FACTORS") = (int)MnistExecutor::SCHED_FACTORS;
   m.attr("MnistExecutor").attr("SCHED_SERIAL") = (int)MnistExecutor::SCHED_SERIAL;
+  m.attr("MnistExecutor").attr("SCHED_DEFER") = (int)MnistExecutor::SCHED_DEFER;
 
   // ----------------------------------------------------------------- IDX
   // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())

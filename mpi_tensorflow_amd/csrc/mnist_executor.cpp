@@ -1,5 +1,6 @@
 #include "mnist_executor.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -230,7 +231,8 @@ void MnistExecutor::sgd_range(hipStream_t s, long long lo, long long hi, float g
 // what it updates - Winograd transforms, bf16 conv2 shadows, with the FC
 // bucket the bf16 fc1 shadows - so the next step's forward takes them as
 // current instead of re-deriving them in a launch of its own.
-void MnistExecutor::sgd_step(hipStream_t s, float gscale, bool fc, bool conv) {
+void MnistExecutor::sgd_step(hipStream_t s, float gscale, bool fc, bool conv,
+                             long long fc_end) {
   const MnistPtrs& p = p_;
   mnist::SgdStepArgs a;
   a.w = P<float>(p.params);
@@ -242,7 +244,7 @@ void MnistExecutor::sgd_step(hipStream_t s, float gscale, bool fc, bool conv) {
   a.lr = P<const float>(p.lr);
   a.step = conv ? P<long long>(p.step) : nullptr;
   if (fc) {
-    a.fc_end = p.bucket1;
+    a.fc_end = fc_end >= 0 ? fc_end : p.bucket1;
     a.fc_rounds = 1;  // a launch of its own: twice the blocks of the in-launch role
     if (p.bf16) {
       a.w1b = P<uint16_t>(p.w1b);
@@ -291,7 +293,7 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
-      sched != SCHED_FACTORS && sched != SCHED_SERIAL)
+      sched != SCHED_FACTORS && sched != SCHED_SERIAL && sched != SCHED_DEFER)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -305,6 +307,13 @@ bool MnistExecutor::sharded_ok(int nranks) const {
 bool MnistExecutor::factors_ok(int nranks) const {
   return nranks > 1 && nranks == p_.fac_ranks && !p_.bf16 && p_.a2_all && p_.dh_all &&
          p_.hd_all && p_.dlog_all;
+}
+
+bool MnistExecutor::defer_ok() const { return !p_.bf16 && fused_sgd_ok(); }
+
+void MnistExecutor::set_defer_split(float f) {
+  if (!(f > 0.f && f < 1.f)) throw std::runtime_error("MnistExecutor: defer split must be in (0, 1)");
+  defer_split_ = f;
 }
 
 void MnistExecutor::wait_fc_params(hipStream_t s) {
@@ -393,6 +402,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   }
   if (sched_ == SCHED_SERIAL) {
     train_step_serial(s, comm);
+    return;
+  }
+  if (sched_ == SCHED_DEFER && defer_ok()) {
+    train_step_defer(s, comm, cs);
     return;
   }
   if (sched_ == SCHED_FACTORS && factors_ok(comm->size())) {
@@ -584,6 +597,37 @@ void MnistExecutor::train_step_serial(hipStream_t s, Collective* comm) {
     sgd_step(s, gscale, true, true);
   else
     sgd_range(s, 0, p.total, gscale, true);
+}
+
+// Deferred-FC schedule (fp32, one communicator).  The FC all-reduce is cut in
+// two parts; the comm stream runs, in order:
+//   FC part A [0, A)          from fc1 backward, under the conv backward
+//   conv bucket               once the slab reduction is done (-> ev_done_)
+//   FC part B [A, bucket1)    + its momentum SGD (-> ev_b1_)
+// The compute stream joins after the conv bucket and runs ONE SGD launch over
+// FC part A and the conv parameters (writing the next step's Winograd
+// filters); the NEXT step's conv forward then runs while part B is still in
+// flight, and only its fc1 forward waits for it (wait_fc_params).  This is
+// the split schedule's overlap without a second communicator: collectives of
+// two RCCL communicators running at once rely on both staying resident.
+// Same sums and SGD forms as buckets (bit-identical).
+void MnistExecutor::train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs) {
+  const MnistPtrs& p = p_;
+  const float gscale = 1.0f / (float)comm->size();
+  const long long A = std::max(4LL, (long long)(defer_split_ * (double)p.bucket1) / 4 * 4);
+  enqueue_fwd_bwd(s, true, nullptr, false, /*fresh=*/true);
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
+  reduce_bucket(comm, 0, A, cs);
+  HIP_CHECK(hipEventRecord(ev_fin_, s));
+  HIP_CHECK(hipStreamWaitEvent(cs, ev_fin_, 0));
+  reduce_bucket(comm, p.bucket1, p.total - p.bucket1, cs);
+  HIP_CHECK(hipEventRecord(ev_done_, cs));
+  reduce_bucket(comm, A, p.bucket1 - A, cs);
+  sgd_range(cs, A, p.bucket1, gscale, false);
+  HIP_CHECK(hipEventRecord(ev_b1_, cs));
+  fc_pending_ = true;
+  HIP_CHECK(hipStreamWaitEvent(s, ev_done_, 0));
+  sgd_step(s, gscale, true, true, A);
 }
 
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {

@@ -106,12 +106,21 @@ class MnistExecutor {
   //                      flat gradient on the compute stream after the slab
   //                      reduction, then the SGD (no cross-queue edges, no
   //                      overlap; see train_step_serial).
+  //   SCHED_DEFER      - (fp32) one communicator: FC part A, conv bucket, FC
+  //                      part B + its SGD in order on the comm stream; the
+  //                      next step's conv forward overlaps part B (see
+  //                      train_step_defer).
   static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
-                       SCHED_FACTORS = 3, SCHED_SERIAL = 4;
+                       SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
   bool factors_ok(int nranks) const;
+  bool defer_ok() const;
+  // SCHED_DEFER: the fraction of the FC bucket in part A (reduced under the
+  // conv backward; the rest overlaps the next step's conv forward)
+  void set_defer_split(float f);
+  float defer_split() const { return defer_split_; }
   // Makes stream s wait for any collective still in flight from the last
   // step (call at the end of every captured / eager run of steps).
   void join(hipStream_t s);
@@ -168,13 +177,16 @@ class MnistExecutor {
   bool fused_sgd_ok() const;
   // world > 1: the fused SGD launch over the all-reduced flat grads (FC
   // bucket and / or conv parameters), writing the next step's derived weights
-  void sgd_step(hipStream_t s, float gscale, bool fc, bool conv);
+  // fc_end >= 0: the FC part is [0, fc_end) instead of the whole bucket
+  void sgd_step(hipStream_t s, float gscale, bool fc, bool conv, long long fc_end = -1);
   int conv1_blocks() const;
   int conv2_groups() const;
   void train_step_sharded(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_split(hipStream_t s, Collective* comm, hipStream_t cs, Collective* comm2);
   void train_step_factors(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_serial(hipStream_t s, Collective* comm);
+  void train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs);
+  float defer_split_ = 0.5f;
   void wait_fc_params(hipStream_t s);
   // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
   void reduce_bucket(Collective* comm, long long lo, long long n, hipStream_t cs);

@@ -38,7 +38,7 @@ from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
 
 # sync_schedule="auto": the single-communicator gradient-sync schedules
-# (buckets / serial / sharded / factors (fp32), csrc/mnist_executor.h) are timed on real
+# (buckets / serial / sharded / factors, defer (fp32), csrc/mnist_executor.h) are timed on real
 # training steps and the fastest is kept; all ranks take
 # the decision from the same (max-over-ranks) timings.  The two-communicator
 # "split" schedule (fastest against the comm-emulated 8-rank ring,
@@ -301,6 +301,7 @@ class NativeMnistEngine(MnistEngineBase):
             self.comm2 = self.comm.duplicate()
         self._native_comm2 = self.comm2.native_handle if self.comm2 is not None else None
         if self.grad_sync:
+            self.exe.set_defer_split(float(cfg.defer_split))
             self.exe.set_schedule(self._pick_schedule(cfg.sync_schedule, self._native_comm.size))
         if getattr(self.comm, "kind", "") == "host-staged":  # test comm: eager only
             self.comm.bases = [self.grads, self.params, self.mom] + (
@@ -345,6 +346,8 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_FACTORS
         if name == "serial":
             return E.SCHED_SERIAL
+        if name == "defer" and self.exe.defer_ok():
+            return E.SCHED_DEFER
         return E.SCHED_BUCKETS  # "auto" until tuned
 
     def _set_schedule(self, sched: int) -> None:
@@ -363,7 +366,8 @@ class NativeMnistEngine(MnistEngineBase):
             return "none"
         E = self._C.MnistExecutor
         return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
-                E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial"}.get(self.exe.schedule,
+                E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial",
+                E.SCHED_DEFER: "defer"}.get(self.exe.schedule,
                                                                            "buckets")
 
     def sync_optimizer_state(self) -> None:
@@ -413,6 +417,8 @@ class NativeMnistEngine(MnistEngineBase):
         # order: under --deterministic auto keeps to the bit-identical ones
         if self.exe.factors_ok(n) and not self.cfg.deterministic:
             cands.append((E.SCHED_FACTORS, "factors"))
+        if self.exe.defer_ok():
+            cands.append((E.SCHED_DEFER, "defer"))
         return cands
 
     def tune_steps(self) -> int:

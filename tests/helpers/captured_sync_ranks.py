@@ -7,7 +7,7 @@ is compared bit for bit with the eager host-staged gloo communicator
 serial emulation of data parallelism on rank 0.
 
 usage: captured_sync_ranks.py SCENARIO [DTYPE]
-  mnist DTYPE   - native MNIST executor: buckets / sharded / split (/ factors,
+  mnist DTYPE   - native MNIST executor: buckets / sharded / split (/ factors, defer,
                   fp32) captured vs eager; bf16 gradient wire; the
                   auto-tune (side-effect free, then the chosen schedule) and
                   a captured switching sequence; replica fingerprints
@@ -75,7 +75,8 @@ def run_fixed(di, sched, dtype, kind, wire="fp32"):
 
 
 def scenario_mnist(di, dtype):
-    scheds = ["buckets", "sharded", "split", "serial"] + (["factors"] if dtype == "fp32" else [])
+    scheds = ["buckets", "sharded", "split", "serial"] + (
+        ["factors", "defer"] if dtype == "fp32" else [])
     eager = {}
     for sched in scheds:
         e, _ = run_fixed(di, sched, dtype, "eager")
@@ -83,8 +84,8 @@ def scenario_mnist(di, dtype):
         same(c, e, f"{sched} captured vs eager")
         eager[sched] = e
         assert len(eng._graphs) == 2, "expected the 3-step and the 1-step graph"
-    for sched in ("sharded", "split", "serial"):  # bit-identical schedules
-        same(eager[sched], eager["buckets"], f"{sched} vs buckets")
+    for sched in ("sharded", "split", "serial") + (("defer",) if dtype == "fp32" else ()):
+        same(eager[sched], eager["buckets"], f"{sched} vs buckets")  # bit-identical schedules
     # bf16 gradient wire, captured
     for sched in ("buckets", "sharded"):
         e, _ = run_fixed(di, sched, dtype, "eager", "bf16")
@@ -104,7 +105,7 @@ def scenario_mnist(di, dtype):
     # sequence eagerly
     E = native().MnistExecutor
     seq = [E.SCHED_BUCKETS, E.SCHED_SHARDED_FC, E.SCHED_SERIAL] + (
-        [E.SCHED_FACTORS] if dtype == "fp32" else [])
+        [E.SCHED_FACTORS, E.SCHED_DEFER] if dtype == "fp32" else [])
     seq.append(E.SCHED_BUCKETS)
     outs = []
     for kind in ("eager", "shm"):
