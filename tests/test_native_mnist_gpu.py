@@ -276,7 +276,7 @@ def test_fc_sgd_placements_bit_identical(cuda_dev, data, dtype):
 def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     """Startup autotune of the gradient-sync schedule (runtime/mnist_engine.py:
     tune_schedule) against an emulated 8-rank ring (csrc/collective.h EmuComm):
-    every single-communicator schedule (buckets, serial, sharded, factors) is
+    every single-communicator schedule (buckets, serial, sharded, factors, defer) is
     captured and timed, the fastest is kept, and the trial steps are
     discarded: params, momentum and the step counter are restored."""
     from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
@@ -288,12 +288,12 @@ def test_sync_schedule_autotune_with_emulated_ring(cuda_dev, data):
     assert eng.sync_schedule == "buckets"  # default until tuned
     assert eng.comm2 is None  # auto never builds the two-communicator schedule
     p0 = eng.params.clone()
-    ncand = len(eng._tune_candidates())  # buckets, serial, sharded, factors
+    ncand = len(eng._tune_candidates())  # buckets, serial, sharded, factors, defer
     n = eng.tune_schedule()
-    assert ncand == 4 and n == ncand * 3 * 5 and eng.step == 0 and int(eng.step_dev.item()) == 0
+    assert ncand == 5 and n == ncand * 3 * 5 and eng.step == 0 and int(eng.step_dev.item()) == 0
     assert torch.equal(eng.params, p0)
     log = eng.tune_log
-    assert set(log) == {"buckets", "serial", "sharded", "factors"}
+    assert set(log) == {"buckets", "serial", "sharded", "factors", "defer"}
     assert eng.sync_schedule == min(log, key=log.get)
     eng.train(7)
     torch.cuda.synchronize()
