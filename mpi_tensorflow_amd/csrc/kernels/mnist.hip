@@ -1193,6 +1193,17 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
       xs[(r * C2_XS_COLS + c) * 33 + ci] = sv[j];
     }
   }
+  // the first point pair's B fragments (U, L2) load under the input transform
+  const int qw = wave & 3, ph = wave >> 2;
+  const float* ub = U + qw * 64 + lane;  // fragment (s, qw) of point p at (32 p + 4 s) * 64
+  auto loadb2 = [&](int p0, float(&b)[16]) {
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) b[pt * 8 + k] = ub[(32 * (p0 + pt) + 4 * k) * 64];
+  };
+  float bA[16], bB[16];
+  loadb2(18 * ph, bA);
   __syncthreads();
   if constexpr (PROF) stamp[1] = __builtin_amdgcn_s_memtime();
   // 2. input transform, one (ci, tile) item per thread.  Tile t = (pooled row
@@ -1224,19 +1235,9 @@ __global__ __launch_bounds__(WNT) void conv2_fwd_wino_kernel(
   // halves' partials meet once (LDS) and the ph = 0 waves finish bias, ReLU,
   // pool and argmax straight from their registers: no (tile, co) re-read of
   // all eight waves' partial outputs.
-  const int qw = wave & 3, ph = wave >> 2;
   f32x4 y[4];  // [output i*2+j] for (tiles, co quarter qw)
 #pragma unroll
   for (int o = 0; o < 4; ++o) y[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const float* ub = U + qw * 64 + lane;  // fragment (s, qw) of point p at (32 p + 4 s) * 64
-  auto loadb2 = [&](int p0, float(&b)[16]) {
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) b[pt * 8 + k] = ub[(32 * (p0 + pt) + 4 * k) * 64];
-  };
-  float bA[16], bB[16];
-  loadb2(18 * ph, bA);
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
     const int p0 = 18 * ph + 2 * i;
