@@ -976,26 +976,56 @@ __global__ __launch_bounds__(256) void conv2_fwd_v3_kernel(
 constexpr int XB_LD = 40;  // bf16 per halo pixel (32 channels + 8: 16-B aligned rows)
 constexpr int XB_ELEMS = C2_XS_ROWS * C2_XS_COLS * XB_LD;
 
-struct HaloB16 {
-  const C12In& c1;
+// bf16 twin of HaloF32Tile: the halo tile plus the owned rows' argmax taps in
+// LDS; halo_b16_flush_owned writes the owned a1p / a1t / idx1 rows at the end
+// of the kernel (16-B a1p segments, 4-B a1t column pairs, u32 idx1 words)
+// instead of 2-byte scattered stores inside the conv1 epilogue
+struct HaloB16Tile {
   __bf16* xb;
-  __bf16* a1p;  // [2][B][18][18][16]
-  __bf16* a1t;  // [B][18][32][MNIST16_T_LD]
-  int n, y0, batch;
+  uint8_t* q1;
+  int y0, yo;
   __device__ __forceinline__ void zero(int tid, int nt) const {
     uint4* z = reinterpret_cast<uint4*>(xb);
     for (int i = tid; i < XB_ELEMS / 8; i += nt) z[i] = make_uint4(0u, 0u, 0u, 0u);
   }
   __device__ __forceinline__ void put(int y, int x, int co, float o, int qq, bool own) const {
-    const __bf16 h = (__bf16)o;
-    xb[((y - y0) * C2_XS_COLS + x + 2) * XB_LD + co] = h;
-    if (own) {
-      c1.idx1[((size_t)(n * 14 + y) * 14 + x) * 32 + co] = (uint8_t)qq;
-      a1p[(((size_t)(co >> 4) * batch + n) * 18 + y + 2) * 18 * 16 + (x + 2) * 16 + (co & 15)] = h;
-      a1t[((size_t)(n * 18 + y + 2) * 32 + co) * MNIST16_T_LD + x + 2] = h;
-    }
+    xb[((y - y0) * C2_XS_COLS + x + 2) * XB_LD + co] = (__bf16)o;
+    if (own) q1[((y - yo) * 14 + x) * 32 + co] = (uint8_t)qq;
   }
 };
+
+__device__ __forceinline__ void halo_b16_flush_owned(const C12In& c1, const __bf16* xb,
+                                                     const uint8_t* q1, __bf16* a1p, __bf16* a1t,
+                                                     int n, int pg, int batch, int tid, int nt) {
+  const int yo = 4 * pg, nr = min(4, 14 - yo);
+  // a1p [2][B][18][18][16]: per (row, plane) 14 pixels x 16 channels contiguous
+  for (int e = tid; e < nr * 56; e += nt) {
+    const int hh = e & 1, x = (e >> 1) % 14, pl = (e / 28) & 1, r = e / 56;
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        xb + ((r + 2) * C2_XS_COLS + x + 2) * XB_LD + pl * 16 + hh * 8);
+    *reinterpret_cast<uint4*>(a1p + (((size_t)pl * batch + n) * 18 + yo + r + 2) * 18 * 16 +
+                              (x + 2) * 16 + hh * 8) = v;
+  }
+  // a1t [B][18][32][MNIST16_T_LD]: per (row, channel) 14 columns at x + 2
+  for (int e = tid; e < nr * 32; e += nt) {
+    const int co = e & 31, r = e >> 5;
+    const __bf16* src = xb + ((r + 2) * C2_XS_COLS + 2) * XB_LD + co;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(
+        a1t + ((size_t)(n * 18 + yo + r + 2) * 32 + co) * MNIST16_T_LD + 2);
+#pragma unroll
+    for (int x = 0; x < 14; x += 2) {
+      const uint32_t lo = __builtin_bit_cast(uint16_t, src[x * XB_LD]);
+      const uint32_t hi = __builtin_bit_cast(uint16_t, src[(x + 1) * XB_LD]);
+      dst[x >> 1] = lo | (hi << 16);
+    }
+  }
+  // idx1 [B][14][14][32] bytes
+  for (int e = tid; e < nr * 14 * 8; e += nt) {
+    const int pix = e >> 3, c = 4 * (e & 7);
+    *reinterpret_cast<uint32_t*>(c1.idx1 + ((size_t)(n * 14 + yo) * 14 + pix) * 32 + c) =
+        *reinterpret_cast<const uint32_t*>(q1 + pix * 32 + c);
+  }
+}
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -1005,11 +1035,11 @@ __global__ __launch_bounds__(256) void conv12_fwd_bf16_kernel(
     __bf16* __restrict__ a2t, uint8_t* __restrict__ idx2) {
   __shared__ __attribute__((aligned(16))) __bf16 xb[XB_ELEMS];
   __shared__ float img[C12_IMG_ROWS * C12_IMG_LD];
+  __shared__ __attribute__((aligned(4))) uint8_t q1[C12_Q1_BYTES];
   const int n = blockIdx.x >> 2, pg = blockIdx.x & 3;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  conv1_into_halo_t<256>(c1, batch, n, pg, img,
-                         HaloB16{c1, xb, a1p, a1t, n, 4 * pg - 2, batch});
+  conv1_into_halo_t<256>(c1, batch, n, pg, img, HaloB16Tile{xb, q1, 4 * pg - 2, 4 * pg});
   // A rows of this wave: pre-pool pixel m = (window, quadrant) of the block's
   // 14 windows (rows 56..63 of the second tile are padding, read pixel 0)
   const int msub = wave & 1, nsub = wave >> 1;
@@ -1069,6 +1099,7 @@ __global__ __launch_bounds__(256) void conv12_fwd_bf16_kernel(
       a2t[((size_t)(n >> 4) * FC1_IN + i) * 16 + (n & 15)] = out;
     }
   }
+  halo_b16_flush_owned(c1, xb, q1, a1p, a1t, n, pg, batch, tid, 256);
 }
 
 // ------------------------------------- conv2 forward, Winograd F(2x2,5x5) ----
