@@ -152,13 +152,20 @@ def _resnet_run(cuda_dev, task, dtype, oracle=False):
     return acc, loss
 
 
+# The oracle's own held-out accuracy after 600 steps moves with the summation
+# order of its MIOpen convolutions (not bit-reproducible from box to box):
+# 88.38, 86.04, 88.67, 89.75 % over four runs of the same code.  The native
+# engines are deterministic, so the pin compares them with the MEAN of those
+# oracle runs instead of one live oracle run (which made the test flaky and
+# cost ~100 s); scripts/resnet_oracle_lab.py re-measures it.  At 1000 / 1500
+# steps the oracle settles (90.72-91.21 / 90.82-91.02 %) and the native engines
+# land within 0.9 (fp32) and 0.5 (bf16) points of it (docs/ACCURACY.md).
+RESNET_ORACLE_RUNS = (88.38, 86.04, 88.67, 89.75)
+
+
 @pytest.fixture(scope="module")
-def resnet_oracle_acc(cuda_dev, resnet_task):
-    acc, loss = _resnet_run(cuda_dev, resnet_task, "fp32", oracle=True)
-    print(f"resnet18 torch oracle (F.conv2d / F.batch_norm autograd, fp32): held-out "
-          f"{acc:.2f}% after {RESNET_ORACLE_STEPS} steps, last loss {loss:.3f}")
-    assert 40.0 < acc < 99.0, "task too easy / too hard to carry information"
-    return acc
+def resnet_oracle_acc():
+    return sum(RESNET_ORACLE_RUNS) / len(RESNET_ORACLE_RUNS)
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
@@ -168,7 +175,8 @@ def test_resnet18_native_matches_torch_oracle_accuracy(cuda_dev, resnet_task, re
     bf16 MFMA convs, fused BatchNorm statistics, hipGraph replay) trained
     RESNET_ORACLE_STEPS steps at B = 32 on the v2 224x224x3 task lands within
     RESNET_ORACLE_TOL points of held-out accuracy of a PyTorch-op oracle of
-    the same model (same init, data and batch order) run on the same GPU."""
+    the same model (same init, data and batch order; the mean of its measured
+    runs, RESNET_ORACLE_RUNS)."""
     acc, loss = _resnet_run(cuda_dev, resnet_task, dtype)
     print(f"resnet18 native {dtype}: held-out {acc:.2f}% (oracle {resnet_oracle_acc:.2f}%), "
           f"last loss {loss:.3f}")
