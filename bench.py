@@ -61,11 +61,19 @@ def parse(argv=None):
     ap.add_argument("--backend", default="auto", choices=("auto", "native", "torch"))
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto",
-                    choices=("auto", "buckets", "sharded", "split", "factors", "serial", "defer"))
+                    choices=("auto", "buckets", "sharded", "split", "factors", "serial", "defer",
+                             "xgmi"))
     ap.add_argument("--defer-split", type=float, default=0.5,
                     help="defer schedule: fraction of the FC bucket reduced under the conv backward")
-    ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "torch"),
-                    help="device communicator (auto: RCCL, or shared memory when ranks share GPUs)")
+    ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "xgmi", "torch"),
+                    help="device communicator (auto: RCCL, or shared memory when ranks share "
+                         "GPUs; on one node the xGMI peer-to-peer schedule is also tuned)")
+    ap.add_argument("--no-xgmi", action="store_true",
+                    help="comm auto: do not set up the xGMI peer-to-peer communicator")
+    ap.add_argument("--xgmi-emulate", default=None, metavar="LAT_US,LINK_GBPS[,N]",
+                    help="1 GPU, MNIST: the xGMI peer-to-peer schedule against N (default 8) "
+                         "virtual ranks whose phases last at least their bytes on one link at "
+                         "LINK_GBPS per direction, plus LAT_US per barrier (timing only)")
     ap.add_argument("--grad-comm-dtype", default="fp32", choices=("fp32", "bf16"),
                     help="wire dtype of the gradient all-reduce (bf16: half the xGMI bytes)")
     ap.add_argument("--comm-emulate", default=None, metavar="LAT_US,BUSBW_GBPS[,N[,BLOCKS]]",
@@ -218,14 +226,25 @@ def run(a, di, device, wd) -> int:
                         sync_schedule=a.sync_schedule, comm=a.comm,
                         defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
                         collective_timeout_s=a.collective_timeout_s).validate()
-    force = bool((a.force_sync or a.comm_emulate) and N == 1 and device.type == "cuda")
+    force = bool((a.force_sync or a.comm_emulate or a.xgmi_emulate) and N == 1
+                 and device.type == "cuda")
     with wd.guard("start-up (communicator, engine)"):
         maybe_fail("before_comm", di.rank)
-        comm = None
+        comm = xcomm = None
         if N > 1 and a.sync == "grad":
             comm = make_comm(di, device, a.comm, shm_capacity=comm_capacity_bytes(cfg),
                              timeout_s=a.collective_timeout_s)
-        if force and a.comm_emulate:
+            # one node, one GPU per rank: the xGMI peer-to-peer schedule is a
+            # tune candidate next to RCCL's (health-checked: timeouts, replicas)
+            if (a.comm == "auto" and not a.no_xgmi and a.model == "mnist_cnn"
+                    and getattr(comm, "kind", "") == "rccl-native"):
+                from mpi_tensorflow_amd.parallel.comm import make_xgmi_comm
+                xcomm = make_xgmi_comm(di, device, min(60.0, a.collective_timeout_s))
+        if force and a.xgmi_emulate:
+            from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+            f = [float(v) for v in a.xgmi_emulate.split(",")]
+            comm = XgmiDeviceComm.emulated(int(f[2]) if len(f) > 2 else 8, f[0], f[1])
+        elif force and a.comm_emulate:
             from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
             f = [float(v) for v in a.comm_emulate.split(",")]
             comm = EmulatedDeviceComm(int(f[2]) if len(f) > 2 else 8, f[0], f[1],
@@ -238,7 +257,7 @@ def run(a, di, device, wd) -> int:
         if a.model == "mnist_cnn":
             shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
             eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
-                              force_sync=force)
+                              force_sync=force, xcomm=xcomm)
             test_x, test_y = shard.test_x, shard.test_y
         else:
             from mpi_tensorflow_amd.models.generic import model_input_shape
@@ -357,6 +376,7 @@ def run(a, di, device, wd) -> int:
                          else "none (1 rank)"),
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
+                "xgmi_comm": getattr(xcomm, "kind", None),
                 "ranks": N,
                 "comm_nranks": comm_nranks,
                 "sync_schedule": getattr(eng, "sync_schedule", "n/a"),

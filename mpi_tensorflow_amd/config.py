@@ -65,12 +65,16 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # FC grads + 1/N-shard SGD + all-gather overlapped with the next forward
 # "split" = FC all-reduce + SGD on the comm stream, conv all-reduce on the
 # compute stream over a second communicator
-SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer")
+# "xgmi" = the peer-to-peer xGMI communicator's fused sync + SGD launch (MNIST,
+# csrc/xgmi_comm.h; one node)
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer", "xgmi")
 # device communicator (world > 1): "auto" = native RCCL when every rank has a
 # GPU of its own, the shared-memory host-staged communicator when ranks share
 # GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",
 # "shm" and "torch" (torch.distributed) force one
-COMMS = ("auto", "rccl", "shm", "torch")
+# "xgmi": collectives as compute-stream kernels reading the peers' memory
+# over the xGMI mesh (IPC-mapped; one node)
+COMMS = ("auto", "rccl", "shm", "xgmi", "torch")
 DTYPES = ("fp32", "bf16")
 
 
@@ -211,7 +215,8 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
                    help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
     p.add_argument("--comm", default=d.comm, choices=COMMS,
                    help="device communicator: RCCL over xGMI (one GPU per rank), shm (host-"
-                        "staged shared memory, ranks may share a GPU) or torch.distributed")
+                        "staged shared memory, ranks may share a GPU), xgmi (peer-to-peer "
+                        "kernels on the compute stream, one node) or torch.distributed")
     p.add_argument("--conv-algo", default=d.conv_algo, choices=("winograd", "direct"),
                    help="fp32 MNIST conv2 algorithm of the native engine")
     p.add_argument("--deterministic", action="store_true",

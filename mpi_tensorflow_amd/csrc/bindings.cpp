@@ -18,6 +18,7 @@
 #include "mnist_executor.h"
 #include "rccl_comm.h"
 #include "shm_comm.h"
+#include "xgmi_comm.h"
 
 namespace py = pybind11;
 
@@ -639,6 +640,38 @@ PYBIND11_MODULE(_C, m) {
   m.attr("ShmComm").attr("BC") = (int)ShmComm::BC;
   m.attr("ShmComm").attr("RD") = (int)ShmComm::RD;
 
+  py::class_<XgmiComm, Collective>(m, "XgmiComm")
+      .def(py::init<int, int, bool, double, double, double>(), py::arg("nranks"), py::arg("rank"),
+           py::arg("emulate") = false, py::arg("lat_us") = 0.0, py::arg("link_gbps") = 0.0,
+           py::arg("timeout_s") = 10.0)
+      .def("flags_handle", [](const XgmiComm& c) { return py::bytes(c.flags_handle()); })
+      .def("open_flags", [](XgmiComm& c, int r, py::bytes h) { c.open_flags(r, std::string(h)); })
+      .def("export_buffer",
+           [](const XgmiComm& c, uintptr_t p, size_t bytes) {
+             auto hb = c.export_buffer(p, bytes);
+             return py::make_tuple(py::bytes(hb.first), hb.second);
+           })
+      .def("open_buffer",
+           [](XgmiComm& c, uintptr_t local, size_t bytes, int r, py::bytes h, size_t off) {
+             c.open_buffer(local, bytes, r, std::string(h), off);
+           })
+      .def("emulate_buffer", &XgmiComm::emulate_buffer)
+      .def("ready", &XgmiComm::ready)
+      .def("registered", [](const XgmiComm& c, uintptr_t p, size_t bytes) {
+        return c.registered(reinterpret_cast<const void*>(p), bytes);
+      })
+      .def("peer_ptr", [](const XgmiComm& c, uintptr_t p, int r) {
+        return reinterpret_cast<uintptr_t>(c.peer_ptr(reinterpret_cast<const void*>(p), r));
+      })
+      .def("error", &XgmiComm::error)
+      .def("clear_error", &XgmiComm::clear_error)
+      .def("gather_segments",
+           [](XgmiComm& c, uintptr_t p, size_t count, uintptr_t s) {
+             c.gather_segments(reinterpret_cast<void*>(p), count, S(s));
+             check_launch();
+           })
+      .def_property_readonly("emulated", &XgmiComm::emulated);
+
   py::class_<RcclComm, Collective>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank) {
              std::string s = uid;
@@ -740,6 +773,8 @@ PYBIND11_MODULE(_C, m) {
       .def("factors_ok", &MnistExecutor::factors_ok)
       .def("defer_ok", &MnistExecutor::defer_ok)
       .def("set_defer_split", &MnistExecutor::set_defer_split)
+      .def("set_xgmi", &MnistExecutor::set_xgmi, py::keep_alive<1, 2>())
+      .def("xgmi_ok", &MnistExecutor::xgmi_ok)
       .def_property_readonly("defer_split", &MnistExecutor::defer_split)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
       .def("gather_optimizer_state",
@@ -772,6 +807,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_FACTORS") = (int)MnistExecutor::SCHED_FACTORS;
   m.attr("MnistExecutor").attr("SCHED_SERIAL") = (int)MnistExecutor::SCHED_SERIAL;
   m.attr("MnistExecutor").attr("SCHED_DEFER") = (int)MnistExecutor::SCHED_DEFER;
+  m.attr("MnistExecutor").attr("SCHED_XGMI") = (int)MnistExecutor::SCHED_XGMI;
 
   // ----------------------------------------------------------------- IDX
   // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())

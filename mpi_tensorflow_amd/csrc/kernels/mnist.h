@@ -4,6 +4,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "xgmi.h"
+
 namespace mnist {
 // world-1 FC-bucket momentum SGD run as extra blocks of a conv2 bwd-data launch
 // (mnist_shared.h fc_sgd_role): flat [0, n) floats, L2 on all of it, device lr
@@ -196,6 +198,44 @@ struct SgdStepArgs {
   uint16_t* w2b = nullptr;
 };
 void launch_sgd_step(const SgdStepArgs& a, hipStream_t s);
+// World > 1 over the xGMI peer-to-peer communicator (MnistExecutor SCHED_XGMI,
+// mnist.hip xgmi_step_kernel): ONE launch on the compute stream does the whole
+// gradient sync and the update.
+//  * FC bucket [0, 4 * fc4): rank r sums float4s of segment r (fc4 / N of
+//    them) over every rank's grads (rank order), applies the momentum SGD to
+//    its own params / momentum there (sharded optimizer state), and after a
+//    barrier copies the other segments' updated params from their owners;
+//  * conv parameters: every rank first writes its own slab sums (the
+//    grad_finalize forms) into its grads, then - after the arrival barrier -
+//    sums every rank's conv grads in rank order and updates the conv
+//    parameters itself (replicated; they are 3 % of the bytes), writing the
+//    next step's Winograd transforms (the bf16 engine re-derives its shadows
+//    in the next step's conv1 launch: fresh = false);
+//  * bumps the device step.
+// g[r] / w[r]: rank r's flat grads / params as mapped here (XgmiComm).
+// Same sums and SGD forms as the buckets schedule over a rank-order
+// all-reduce, so the replicas stay bit-identical.
+struct XgmiStepArgs {
+  xgmi::Sync sync;
+  const float* g[xgmi::kMaxRanks] = {};
+  float* w[xgmi::kMaxRanks] = {};
+  float* mom = nullptr;
+  long long fc4 = 0;  // FC bucket float4s (a multiple of the rank count)
+  float l2 = 0.f, momentum = 0.f, gscale = 1.f;
+  const float* lr = nullptr;
+  long long* step = nullptr;
+  int off_w2 = 0, off_b2 = 0, off_w1 = 0, off_b1 = 0;
+  const float* part2 = nullptr;
+  int ngroups = 0;
+  const float* part1 = nullptr;
+  int nblk1 = 0;
+  float* wino_u = nullptr;
+  float* wino_ud = nullptr;
+  // set by the launcher
+  long long seg4 = 0;
+  int per4 = 0, nfc = 0, ncv = 0;
+};
+void launch_xgmi_step(const XgmiStepArgs& a, hipStream_t s);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

@@ -2715,6 +2715,217 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
   sgd_finalize_kernel<<<grid, 256, 0, s>>>(a);
 }
 
+// ------------------------------------------- xGMI peer-to-peer step sync ----
+// (mnist.h XgmiStepArgs).  Two block roles: [0, nfc) FC segment slices (slice
+// b = float4s [b * per4, (b + 1) * per4) of the segment); [nfc, nfc + ncv)
+// conv blocks, each looping over the "virtual" blocks v = b, b + ncv, ... of
+// sgd_finalize_kernel's conv partition: 128 (Winograd) or 50 (flat) conv2
+// weight blocks, 16 conv2-bias blocks, 208 conv1 blocks.  Few blocks on
+// purpose: a block waiting at a barrier holds its CU slot, and the grid stays
+// small beside whatever else the GPU runs.  Every block takes part in both
+// barriers (arrival; "reduced / done reading"), so a rank leaves the kernel
+// only when every peer has read its grads.
+constexpr int XS_UNROLL = 2;
+constexpr int XS_FC_BLOCKS = 64, XS_CONV_BLOCKS = 32;
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+  return a;
+}
+
+// conv virtual block v: the flat float offset of this thread's output (conv2:
+// a float4 index into the conv2 weight, returned in *i4) or -1
+struct XsConvItem {
+  int kind;  // 0 conv2 weight (float4 i4), 1 scalar (bias / conv1) at off
+  int i4, off;
+};
+
+__device__ __forceinline__ XsConvItem xs_conv_item(const XgmiStepArgs& a, int v, int tid) {
+  const int nconv2 = a.wino_u ? 128 : 50;
+  if (v < nconv2) {
+    int i = -1;
+    if (a.wino_u) {
+      if (tid < 100) i = ((tid >> 2) * 32 + (v >> 2)) * 16 + (v & 3) * 4 + (tid & 3);
+    } else {
+      i = v * 256 + tid;
+    }
+    return XsConvItem{0, i, -1};
+  }
+  v -= nconv2;
+  if (v < 16) return XsConvItem{1, -1, a.off_b2 + v * 4 + (tid >> 6)};
+  const int o = (v - 16) * 4 + (tid >> 6);
+  if (o >= 832) return XsConvItem{1, -1, -1};
+  return XsConvItem{1, -1, o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800)};
+}
+
+__global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
+  __shared__ unsigned ep;
+  __shared__ float wl[25 * 16];
+  const xgmi::Sync& s = a.sync;
+  const int n = s.nranks, me = s.rank, tid = threadIdx.x, lane = tid & 63;
+  float* gl = const_cast<float*>(a.g[me]);
+  const float lr = *a.lr;
+  const unsigned e = xgmi::next_epoch(s, &ep);
+  if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
+    xgmi::barrier(s, 0, e);
+    const long long lo = (long long)blockIdx.x * a.per4;
+    const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
+    long long t0 = xgmi::now_ticks();
+    const long long base = (long long)me * a.seg4;
+    float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+    float4* M4 = reinterpret_cast<float4*>(a.mom);
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
+      float4 v[xgmi::kMaxRanks][XS_UNROLL], wv[XS_UNROLL], mv[XS_UNROLL];
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u) {
+        const bool ok = i0 + 256 * u < hi;
+        const long long i = base + i0 + 256 * u;
+#pragma unroll
+        for (int r = 0; r < xgmi::kMaxRanks; ++r)
+          if (r < n && ok) v[r][u] = reinterpret_cast<const float4*>(a.g[r])[i];
+        if (ok) {
+          wv[u] = W4[i];
+          mv[u] = M4[i];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u) {
+        if (i0 + 256 * u >= hi) continue;
+        float4 sv = v[0][u];
+#pragma unroll
+        for (int r = 1; r < xgmi::kMaxRanks; ++r)
+          if (r < n) sv = add4(sv, v[r][u]);
+        sgd4(wv[u], mv[u], sv, a.l2, lr, a.momentum, a.gscale);
+        const long long i = base + i0 + 256 * u;
+        W4[i] = wv[u];
+        M4[i] = mv[u];
+      }
+    }
+    xgmi::link_floor(s, t0, a.seg4 * 16);
+    xgmi::barrier(s, 1, e);
+    t0 = xgmi::now_ticks();
+    for (int r = 0; r < n; ++r) {
+      if (r == me) continue;
+      const long long rb = (long long)r * a.seg4;
+      const float4* src = reinterpret_cast<const float4*>(a.w[r]);
+      for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
+        float4 v[XS_UNROLL];
+#pragma unroll
+        for (int u = 0; u < XS_UNROLL; ++u)
+          if (i0 + 256 * u < hi) v[u] = src[rb + i0 + 256 * u];
+#pragma unroll
+        for (int u = 0; u < XS_UNROLL; ++u)
+          if (i0 + 256 * u < hi) W4[rb + i0 + 256 * u] = v[u];
+      }
+    }
+    xgmi::link_floor(s, t0, a.seg4 * 16);
+    return;
+  }
+  // ---- conv parameters (replicated update)
+  const int cb = (int)blockIdx.x - a.nfc;
+  const int nvirt = (a.wino_u ? 128 : 50) + 16 + 208;
+  // this rank's slab reductions (grad_finalize_kernel forms) into its grads
+  for (int v = cb; v < nvirt; v += a.ncv) {
+    const XsConvItem it = xs_conv_item(a, v, tid);
+    if (it.kind == 0) {
+      if (it.i4 >= 0)
+        reinterpret_cast<float4*>(gl + a.off_w2)[it.i4] =
+            slab_sum4(reinterpret_cast<const float4*>(a.part2) + it.i4, a.ngroups);
+      continue;
+    }
+    float sl = 0.f;
+    if (it.off >= a.off_b2 && it.off < a.off_b2 + 64) {
+      const int co = it.off - a.off_b2;
+      const float* part_db2 = a.part2 + (size_t)a.ngroups * 51200;
+      for (int z = lane; z < 4 * a.ngroups; z += 64) sl += part_db2[z * 64 + co];
+      sl = wave_sum(sl);
+    } else if (it.off >= 0) {
+      const int o = it.off < a.off_b1 ? it.off - a.off_w1 : 800 + (it.off - a.off_b1);
+#pragma unroll 8
+      for (int b = lane; b < a.nblk1; b += 64) sl += a.part1[(size_t)b * 832 + o];
+      sl = wave_sum(sl);
+    }
+    if (it.off >= 0 && lane == 0) gl[it.off] = sl;
+  }
+  xgmi::barrier(s, 0, e);
+  for (int v = cb; v < nvirt; v += a.ncv) {
+    const XsConvItem it = xs_conv_item(a, v, tid);
+    if (it.kind == 1) {
+      if (it.off >= 0 && lane == 0) {
+        float sv = a.g[0][it.off];
+        for (int r = 1; r < n; ++r) sv += a.g[r][it.off];
+        float* w = a.w[me] + it.off;
+        sgd_elem(w, a.mom + it.off, __builtin_fmaf(0.f, *w, sv * a.gscale), lr, a.momentum);
+      }
+      continue;
+    }
+    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (it.i4 >= 0) {
+      float4* wp = reinterpret_cast<float4*>(a.w[me] + a.off_w2) + it.i4;
+      float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + it.i4;
+      wv = *wp;
+      float4 mv = *mp;
+      float4 sv = reinterpret_cast<const float4*>(a.g[0] + a.off_w2)[it.i4];
+#pragma unroll
+      for (int r = 1; r < xgmi::kMaxRanks; ++r)
+        if (r < n) sv = add4(sv, reinterpret_cast<const float4*>(a.g[r] + a.off_w2)[it.i4]);
+      sgd4(wv, mv, sv, 0.f, lr, a.momentum, a.gscale);
+      *wp = wv;
+      *mp = mv;
+    }
+    if (a.wino_u) {  // the next step's Winograd transforms (sgd_conv2_wino)
+      const int ci = v >> 2, cq = v & 3;
+      __syncthreads();  // wl of the previous virtual block is consumed
+      if (tid < 100) *reinterpret_cast<float4*>(wl + (tid >> 2) * 16 + 4 * (tid & 3)) = wv;
+      __syncthreads();
+      if (tid < 32) {
+        const int cl = tid & 15, co = cq * 16 + cl;
+        float g[25], u[36];
+        if (tid < 16) {
+#pragma unroll
+          for (int t = 0; t < 25; ++t) g[t] = wl[t * 16 + cl];
+          wino::filter_tile(g, u);
+#pragma unroll
+          for (int p = 0; p < 36; ++p) a.wino_u[wino_u_index(p, ci, co)] = u[p];
+        } else {
+#pragma unroll
+          for (int t = 0; t < 25; ++t) g[t] = wl[(24 - t) * 16 + cl];
+          wino::filter_tile(g, u);
+#pragma unroll
+          for (int p = 0; p < 36; ++p) a.wino_ud[wino_ud_index(p, ci, co)] = u[p];
+        }
+      }
+    }
+  }
+  if (a.step && cb == 0 && tid == 0) *a.step += 1;
+  xgmi::barrier(s, 1, e);
+}
+
+void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
+  XgmiStepArgs a = in;
+  const int n = a.sync.nranks;
+  if (n < 1 || n > xgmi::kMaxRanks || !a.sync.flags || !a.sync.epoch || !a.sync.error || !a.lr)
+    throw std::runtime_error("xgmi_step: communicator / lr not set up");
+  for (int r = 0; r < n; ++r)
+    if (!a.g[r] || !a.w[r] || (!a.sync.emulate && !a.sync.peer_flags[r]))
+      throw std::runtime_error("xgmi_step: rank " + std::to_string(r) + " not mapped");
+  if (a.fc4 <= 0 || a.fc4 % n) throw std::runtime_error("xgmi_step: FC bucket not split evenly");
+  if ((a.wino_u == nullptr) != (a.wino_ud == nullptr))
+    throw std::runtime_error("xgmi_step: Winograd transforms need both U and Ud");
+  if (!a.part2 || !a.part1 || a.ngroups <= 0 || a.nblk1 <= 0 || a.off_w2 % 4)
+    throw std::runtime_error("xgmi_step: conv slabs / offsets");
+  a.seg4 = a.fc4 / n;
+  const long long unit = 256 * XS_UNROLL;
+  const long long per = (a.seg4 + XS_FC_BLOCKS - 1) / XS_FC_BLOCKS;
+  a.per4 = (int)((per + unit - 1) / unit * unit);
+  a.nfc = (int)((a.seg4 + a.per4 - 1) / a.per4);
+  a.ncv = XS_CONV_BLOCKS;
+  xgmi_step_kernel<<<a.nfc + a.ncv, 256, 0, s>>>(a);
+}
+
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
                           float* g_w2, float* g_b2, float* g_w1, float* g_b1, hipStream_t s) {
   if (reinterpret_cast<uintptr_t>(g_w2) % 16 || reinterpret_cast<uintptr_t>(part2) % 16)

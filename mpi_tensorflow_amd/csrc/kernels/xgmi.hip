@@ -1,0 +1,77 @@
+// Generic xGMI peer-to-peer kernels (csrc/xgmi_comm.h, kernels/xgmi.h).
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "xgmi.h"
+
+namespace xgmi {
+
+constexpr int kAllReduceUnroll = 2;  // float4s in flight per thread per rank
+
+__global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
+  __shared__ unsigned ep;
+  const Sync& s = a.s;
+  const int n = s.nranks, me = s.rank, tid = threadIdx.x;
+  const unsigned e = next_epoch(s, &ep);
+  barrier(s, 0, e);
+  const long long lo = (long long)blockIdx.x * a.per4;
+  const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
+  long long t0 = now_ticks();
+  if (!a.gather_only) {
+    const long long base = (long long)me * a.seg4;
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * kAllReduceUnroll) {
+      float4 acc[kAllReduceUnroll];
+      float4 v[kMaxRanks][kAllReduceUnroll];
+#pragma unroll
+      for (int r = 0; r < kMaxRanks; ++r)
+#pragma unroll
+        for (int u = 0; u < kAllReduceUnroll; ++u) {
+          const long long i = base + i0 + 256 * u;
+          if (r < n && i0 + 256 * u < hi && i < a.n4)
+            v[r][u] = reinterpret_cast<const float4*>(a.buf[r])[i];
+        }
+#pragma unroll
+      for (int u = 0; u < kAllReduceUnroll; ++u) {
+        acc[u] = v[0][u];
+#pragma unroll
+        for (int r = 1; r < kMaxRanks; ++r)
+          if (r < n) {
+            acc[u].x += v[r][u].x;
+            acc[u].y += v[r][u].y;
+            acc[u].z += v[r][u].z;
+            acc[u].w += v[r][u].w;
+          }
+        const long long i = base + i0 + 256 * u;
+        if (i0 + 256 * u < hi && i < a.n4) reinterpret_cast<float4*>(a.buf[me])[i] = acc[u];
+      }
+    }
+  }
+  if (!a.gather_only) link_floor(s, t0, a.link_bytes);
+  barrier(s, 1, e);
+  t0 = now_ticks();
+  for (int r = 0; r < n; ++r) {
+    if (r == me) continue;
+    const long long base = (long long)r * a.seg4;
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256) {
+      const long long i = base + i0;
+      if (i < a.n4)
+        reinterpret_cast<float4*>(a.buf[me])[i] = reinterpret_cast<const float4*>(a.buf[r])[i];
+    }
+  }
+  link_floor(s, t0, a.link_bytes);
+  barrier(s, 2, e);
+}
+
+void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st) {
+  if (blocks < 1 || blocks > kMaxBlocks)
+    throw std::runtime_error("xgmi all_reduce: grid of " + std::to_string(blocks) + " blocks");
+  if (a.s.nranks < 1 || a.s.nranks > kMaxRanks || !a.s.flags || !a.s.epoch || !a.s.error)
+    throw std::runtime_error("xgmi all_reduce: communicator not set up");
+  for (int r = 0; r < a.s.nranks; ++r)
+    if (!a.buf[r] || (!a.s.emulate && !a.s.peer_flags[r]))
+      throw std::runtime_error("xgmi all_reduce: rank " + std::to_string(r) + " not mapped");
+  allreduce_kernel<<<blocks, 256, 0, st>>>(a);
+}
+
+}  // namespace xgmi

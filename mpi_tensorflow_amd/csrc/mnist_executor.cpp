@@ -281,6 +281,7 @@ void MnistExecutor::reduce_bucket(Collective* comm, long long lo, long long n, h
 }
 
 void MnistExecutor::refresh_shadows(hipStream_t s) {
+  shadows_stale_ = false;
   if (p_.wino) {
     const float* W = P<const float>(p_.params);
     mnist::launch_conv2_wino_weights(W + p_.off_w2, P<float>(p_.wino_u), P<float>(p_.wino_ud), s);
@@ -293,11 +294,22 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
-      sched != SCHED_FACTORS && sched != SCHED_SERIAL && sched != SCHED_DEFER)
+      sched != SCHED_FACTORS && sched != SCHED_SERIAL && sched != SCHED_DEFER &&
+      sched != SCHED_XGMI)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
   sched_ = sched;
+}
+
+// bf16: the sharded schedule's FC shard update leaves the fc1 bf16 shadows
+// (w1b / w1t) one update behind (its next step re-derives them in the conv1
+// launch, fresh = false); a step of any other schedule that would take the
+// shadows as current re-derives them first instead (fresh = false once).
+bool MnistExecutor::take_fresh(bool want) {
+  const bool stale = shadows_stale_;
+  shadows_stale_ = false;
+  return want && !stale;
 }
 
 bool MnistExecutor::sharded_ok(int nranks) const {
@@ -310,6 +322,14 @@ bool MnistExecutor::factors_ok(int nranks) const {
 }
 
 bool MnistExecutor::defer_ok() const { return !p_.bf16 && fused_sgd_ok(); }
+
+bool MnistExecutor::xgmi_ok() const {
+  if (xgmi_ == nullptr || !xgmi_->ready() || !fused_sgd_ok()) return false;
+  const int n = xgmi_->size();
+  const size_t fb = (size_t)p_.total * sizeof(float);
+  return p_.bucket1 % (4LL * n) == 0 && xgmi_->registered(P<const void>(p_.grads), fb) &&
+         xgmi_->registered(P<const void>(p_.params), fb);
+}
 
 void MnistExecutor::set_defer_split(float f) {
   if (!(f > 0.f && f < 1.f)) throw std::runtime_error("MnistExecutor: defer split must be in (0, 1)");
@@ -329,6 +349,10 @@ bool MnistExecutor::fused_sgd_ok() const { return p_.l2_end == p_.bucket1; }
 
 void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                Collective* comm2) {
+  if (sched_ == SCHED_XGMI && xgmi_ok()) {  // the peer-to-peer communicator, no comm stream
+    train_step_xgmi(s);
+    return;
+  }
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
     const MnistPtrs& p = p_;
     wait_fc_params(s);
@@ -359,7 +383,7 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
     // the derived weights (Winograd transforms, bf16 shadows) come from the
     // previous step's SGD (or refresh_shadows() before the first step of a
     // run) and are rewritten by this step's SGD for the next one
-    enqueue_fwd_bwd(s, /*finalize=*/false, role ? &fc : nullptr, false, /*fresh=*/true, fuse_dw1);
+    enqueue_fwd_bwd(s, /*finalize=*/false, role ? &fc : nullptr, false, take_fresh(true), fuse_dw1);
     mnist::SgdStepArgs a;
     a.w = P<float>(p.params);
     a.g = P<const float>(p.grads);
@@ -420,7 +444,7 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
   const bool fused = fused_sgd_ok();
   // fused: this step's single SGD launch writes the next step's derived
   // weights, so the forward reads them as they are (one launch fewer)
-  enqueue_fwd_bwd(s, true, nullptr, false, fused);
+  enqueue_fwd_bwd(s, true, nullptr, false, take_fresh(fused));
   // size-1 comms are allowed (they exercise the capture path on one GPU)
   const float gscale = 1.0f / (float)comm->size();
   // bucket 1 (FC grads, 97 % of the bytes) as soon as fc1 backward is done;
@@ -468,7 +492,8 @@ void MnistExecutor::train_step_sharded(hipStream_t s, Collective* comm, hipStrea
   const float gscale = 1.0f / (float)n;
   const long long chunk = p.bucket1 / n, lo = chunk * comm->rank();
   const bool fused = fused_sgd_ok();
-  enqueue_fwd_bwd(s, true, nullptr, false, fused && !p.bf16);
+  enqueue_fwd_bwd(s, true, nullptr, false, take_fresh(fused && !p.bf16));
+  if (p.bf16) shadows_stale_ = true;  // the FC shard update writes no fc1 shadows
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
   if (p.grad_bf16) {  // bf16 wire: the shard comes back to fp32 before its SGD
     uint16_t* Gb = P<uint16_t>(p.gb16);
@@ -504,7 +529,7 @@ void MnistExecutor::train_step_split(hipStream_t s, Collective* comm, hipStream_
   const MnistPtrs& p = p_;
   const float gscale = 1.0f / (float)comm->size();
   const bool fused = fused_sgd_ok();
-  enqueue_fwd_bwd(s, true, nullptr, false, fused);
+  enqueue_fwd_bwd(s, true, nullptr, false, take_fresh(fused));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
   reduce_bucket(comm, 0, p.bucket1, cs);
   if (fused)
@@ -548,7 +573,7 @@ void MnistExecutor::train_step_factors(hipStream_t s, Collective* comm, hipStrea
   const size_t B = (size_t)p.batch;
   const float gscale = 1.0f / (float)n;
   const bool fused = fused_sgd_ok();
-  enqueue_fwd_bwd(s, /*finalize=*/true, nullptr, /*factors=*/true, fused);
+  enqueue_fwd_bwd(s, /*finalize=*/true, nullptr, /*factors=*/true, take_fresh(fused));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_fac_, 0));
   float* a2 = P<float>(p.a2_all);
   float* dh = P<float>(p.dh_all);
@@ -591,7 +616,7 @@ void MnistExecutor::train_step_serial(hipStream_t s, Collective* comm) {
   const float gscale = 1.0f / (float)comm->size();
   const bool fused = fused_sgd_ok();
   wait_fc_params(s);
-  enqueue_fwd_bwd(s, true, nullptr, false, fused);
+  enqueue_fwd_bwd(s, true, nullptr, false, take_fresh(fused));
   reduce_bucket(comm, 0, p.total, s);
   if (fused)
     sgd_step(s, gscale, true, true);
@@ -615,7 +640,7 @@ void MnistExecutor::train_step_defer(hipStream_t s, Collective* comm, hipStream_
   const MnistPtrs& p = p_;
   const float gscale = 1.0f / (float)comm->size();
   const long long A = std::max(4LL, (long long)(defer_split_ * (double)p.bucket1) / 4 * 4);
-  enqueue_fwd_bwd(s, true, nullptr, false, /*fresh=*/true);
+  enqueue_fwd_bwd(s, true, nullptr, false, take_fresh(true));
   HIP_CHECK(hipStreamWaitEvent(cs, ev_dw_, 0));
   reduce_bucket(comm, 0, A, cs);
   HIP_CHECK(hipEventRecord(ev_fin_, s));
@@ -630,8 +655,53 @@ void MnistExecutor::train_step_defer(hipStream_t s, Collective* comm, hipStream_
   sgd_step(s, gscale, true, true, A);
 }
 
+// xGMI peer-to-peer schedule: forward + backward as at world 1 but with the
+// conv filter grads left as slabs and dW1 formed by fc1 backward, then ONE
+// launch (mnist.h XgmiStepArgs) that syncs and updates everything.  The FC
+// momentum is sharded (each rank keeps its own segment current):
+// gather_optimizer_state() before reading it.  bf16: the FC update writes no
+// fc1 shadows, so the next step re-derives them (fresh = false).
+void MnistExecutor::train_step_xgmi(hipStream_t s) {
+  const MnistPtrs& p = p_;
+  XgmiComm* x = xgmi_;
+  const int n = x->size();
+  wait_fc_params(s);
+  enqueue_fwd_bwd(s, /*finalize=*/false, nullptr, false, take_fresh(!p.bf16));
+  mnist::XgmiStepArgs a;
+  a.sync = x->sync();
+  for (int r = 0; r < n; ++r) {
+    a.g[r] = static_cast<const float*>(x->peer_ptr(P<const void>(p.grads), r));
+    a.w[r] = static_cast<float*>(x->peer_ptr(P<const void>(p.params), r));
+  }
+  a.mom = P<float>(p.mom);
+  a.fc4 = p.bucket1 / 4;
+  a.l2 = p.l2;
+  a.momentum = p.momentum;
+  a.gscale = 1.0f / (float)n;
+  a.lr = P<const float>(p.lr);
+  a.step = P<long long>(p.step);
+  a.off_w2 = (int)p.off_w2;
+  a.off_b2 = (int)p.off_b2;
+  a.off_w1 = (int)p.off_w1;
+  a.off_b1 = (int)p.off_b1;
+  a.part2 = P<const float>(p.part2);
+  a.ngroups = conv2_groups();
+  a.part1 = P<const float>(p.part1);
+  a.nblk1 = conv1_blocks();
+  if (p.wino) {
+    a.wino_u = P<float>(p.wino_u);
+    a.wino_ud = P<float>(p.wino_ud);
+  }
+  mnist::launch_xgmi_step(a, s);
+  if (p.bf16) shadows_stale_ = true;
+}
+
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {
   wait_fc_params(s);
+  if (sched_ == SCHED_XGMI && xgmi_ok()) {  // the FC momentum segments (registered)
+    xgmi_->gather_segments(P<float>(p_.mom), (size_t)p_.bucket1, s);
+    return;
+  }
   if (comm == nullptr || sched_ != SCHED_SHARDED_FC || !sharded_ok(comm->size())) return;
   float* Mo = P<float>(p_.mom);
   const long long chunk = p_.bucket1 / comm->size(), lo = chunk * comm->rank();

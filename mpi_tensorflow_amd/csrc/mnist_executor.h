@@ -28,6 +28,7 @@
 
 #include "collective.h"
 #include "rccl_comm.h"
+#include "xgmi_comm.h"
 
 struct MnistPtrs {
   // dataset (device resident)
@@ -110,8 +111,20 @@ class MnistExecutor {
   //                      part B + its SGD in order on the comm stream; the
   //                      next step's conv forward overlaps part B (see
   //                      train_step_defer).
+  //   SCHED_XGMI       - the xGMI peer-to-peer communicator (set_xgmi): no
+  //                      collective library and no second stream; after the
+  //                      backward ONE launch on the compute stream reduces this
+  //                      rank's 1/N of the FC gradients straight out of every
+  //                      peer's memory, updates those parameters, gathers the
+  //                      other segments back, and updates the (replicated)
+  //                      conv parameters from the summed slab reductions (see
+  //                      train_step_xgmi, mnist.h XgmiStepArgs).
   static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
-                       SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5;
+                       SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5, SCHED_XGMI = 6;
+  // the peer-to-peer communicator of SCHED_XGMI: the flat grads and params must
+  // be registered with it (XgmiComm::open_buffer / emulate_buffer)
+  void set_xgmi(XgmiComm* x) { xgmi_ = x; }
+  bool xgmi_ok() const;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
@@ -186,6 +199,8 @@ class MnistExecutor {
   void train_step_factors(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_serial(hipStream_t s, Collective* comm);
   void train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs);
+  void train_step_xgmi(hipStream_t s);
+  XgmiComm* xgmi_ = nullptr;
   float defer_split_ = 0.5f;
   void wait_fc_params(hipStream_t s);
   // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
@@ -196,6 +211,9 @@ class MnistExecutor {
   void enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize = true,
                             const mnist::FcSgdArgs* fc_sgd = nullptr, bool shadows_fresh = false);
   int fc_sgd_rounds_ = -1;
+  // bf16: the fc1 shadows are one FC update behind (after a sharded step)
+  bool shadows_stale_ = false;
+  bool take_fresh(bool want);
   MnistPtrs p_;
   void sgd_range(hipStream_t s, long long lo, long long hi, float gscale, bool bump_step);
   // ev_dw_: FC grads final (bucket 1 may start); ev_b1_: bucket 1 reduced;

@@ -1,0 +1,99 @@
+// xGMI peer-to-peer communicator: collectives as kernels on the caller's
+// (compute) stream that read the peers' buffers directly over the xGMI mesh.
+//
+// Why (SURVEY.md §5 "Distributed communication backend"): the
+// MNIST step is ~80 us, its 6.65 MB gradient all-reduce is as long as the
+// step on an RCCL ring, and every RCCL overlap schedule pays cross-queue graph
+// edges (~10 us each, scripts/microbench/edge_lab.hip).  On a fully connected
+// 8-GPU node a two-phase direct exchange moves S/N bytes per link per phase on
+// all 7 links at once, and it runs IN the compute stream - so the gradient sum
+// can be fused with the momentum SGD that consumes it (MnistExecutor
+// SCHED_XGMI: one launch reduces this rank's 1/N of the FC gradients from
+// every rank, updates those parameters, and gathers everyone else's updated
+// segments back).
+//
+// Buffers a kernel reads remotely are REGISTERED: each rank exports an IPC
+// handle of the allocation that holds the buffer (+ offset), the handles are
+// exchanged over the gloo bootstrap group (parallel/comm.py XgmiDeviceComm)
+// and opened here.  The flag array lives in uncached device memory
+// (hipDeviceMallocUncached) so remote flag stores are seen by local polls.
+// All ranks must be on ONE node (xGMI); ranks sharing a GPU work too (the IPC
+// mapping is then to the same device - the 2-rank GPU tests use that).
+//
+// Emulation (one GPU): make the communicator with emulate = true; every
+// registered buffer gets N - 1 local stand-ins as the "peers", and the
+// kernels hold each phase for the time its bytes take on one link
+// (link_gbps per direction) plus lat_us per barrier.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "collective.h"
+#include "kernels/xgmi.h"
+
+class XgmiComm : public Collective {
+ public:
+  XgmiComm(int nranks, int rank, bool emulate, double lat_us, double link_gbps, double timeout_s);
+  ~XgmiComm() override;
+  int rank() const override { return rank_; }
+  int size() const override { return nranks_; }
+  bool emulated() const { return emulate_; }
+
+  // --- set-up (collective through the caller's bootstrap group) ---
+  std::string flags_handle() const;               // IPC handle of this rank's flag array
+  void open_flags(int r, const std::string& handle);
+  // IPC handle of the allocation holding [ptr, ptr + bytes) and ptr's offset in it
+  std::pair<std::string, size_t> export_buffer(uintptr_t ptr, size_t bytes) const;
+  // maps rank r's counterpart of the local buffer (handle / offset from its export_buffer)
+  void open_buffer(uintptr_t local, size_t bytes, int r, const std::string& handle, size_t off);
+  // emulation: N - 1 local stand-ins for the local buffer (copies of it)
+  void emulate_buffer(uintptr_t local, size_t bytes);
+  bool ready() const;  // flags of every rank mapped
+
+  // --- device views ---
+  const xgmi::Sync& sync() const { return sync_; }
+  // rank r's counterpart of a local address inside a registered buffer
+  void* peer_ptr(const void* local, int r) const;
+  bool registered(const void* local, size_t bytes) const;
+  // emulated per-phase floor: ticks of the 100 MHz clock per KiB on one link
+  long long link_ticks_per_kb() const { return sync_.link_ticks_per_kb; }
+  unsigned error() const;  // sticky error bits (1: a barrier timed out); synchronizes
+  void clear_error();
+
+  // --- Collective: in-place fp32 sum all-reduce of a registered buffer ---
+  void all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
+                  hipStream_t s) override;
+  void all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                  hipStream_t s) override;
+  // in place, fp32: segment r (ceil(count / N) floats, in float4s) of every
+  // rank's buffer becomes rank r's (the all-reduce's phase 2 alone)
+  void gather_segments(void* buf, size_t count, hipStream_t s);
+  void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                      hipStream_t s) override;
+
+ private:
+  struct Reg {
+    uintptr_t local = 0;
+    size_t bytes = 0;
+    void* peer[xgmi::kMaxRanks] = {};
+  };
+  const Reg* find(const void* p, size_t bytes) const;
+  Reg& reg_for(uintptr_t local, size_t bytes);
+  void* open_handle(int r, const std::string& handle);
+  void launch(void* buf, size_t count, bool gather_only, hipStream_t s);
+
+  int nranks_, rank_;
+  bool emulate_;
+  xgmi::Sync sync_;
+  unsigned* flags_ = nullptr;
+  unsigned* epoch_ = nullptr;
+  unsigned* error_ = nullptr;
+  std::vector<Reg> regs_;
+  std::map<std::pair<int, std::string>, void*> opened_;  // (rank, handle) -> mapped base
+  std::vector<void*> emu_allocs_;
+  std::vector<void*> opened_flags_;
+};

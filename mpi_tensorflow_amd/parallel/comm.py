@@ -17,6 +17,11 @@ Replaces the reference's host-staged, blocking mpi4py collectives
   Each collective is a D2H copy, a host function and an H2D copy on the
   caller's stream, so it too is captured into the step's hipGraph and the
   executors' captured sync schedules run unchanged.
+* `XgmiDeviceComm` - the native `_C.XgmiComm`: collectives as kernels on
+  the COMPUTE stream that read the peers' registered buffers directly over the
+  xGMI mesh (IPC-mapped), two-phase (reduce my 1/N, gather the rest), no
+  collective library and no comm stream.  The MNIST executor's SCHED_XGMI
+  fuses it with the momentum SGD (one launch per step).  One node only.
 * world size 1 -> no communicator at all.
 
 ncclDataType / ncclRedOp enum values follow rccl.h.
@@ -172,6 +177,132 @@ class EmulatedDeviceComm(DeviceComm):
 
     def duplicate(self):
         return EmulatedDeviceComm(*self._args)
+
+
+class XgmiDeviceComm(DeviceComm):
+    """xGMI peer-to-peer communicator (csrc/xgmi_comm.h) of the ranks of one
+    node.  Creation is collective over the gloo group: every rank makes its
+    uncached flag array, the IPC handles are all-gathered and every rank maps
+    every peer's; each step is voted, so a rank that fails makes every rank
+    raise instead of hanging.  Buffers the kernels read remotely must be
+    registered (collective, same order on every rank): `register(t, ...)`.
+
+    `emulated(n, lat_us, link_gbps)`: ONE process stands in for n ranks on one
+    GPU (local stand-in peer buffers; each phase held for the time its bytes
+    take on one link at `link_gbps` per direction, plus `lat_us` per barrier)
+    for timing the schedule before a multi-GPU node is available."""
+
+    kind = "xgmi-p2p"
+
+    def __init__(self, di: Optional[DistInfo], timeout_s: float = 30.0, _emulate=None):
+        C = native()
+        if _emulate is not None:
+            n, lat, bw = _emulate
+            self._c = C.XgmiComm(int(n), 0, True, float(lat), float(bw), float(timeout_s))
+            self.rank, self.size = 0, int(n)
+            self.kind = f"xgmi-emulated(n={n},lat={lat}us,link={bw}GB/s)"
+            self._di = None
+            return
+        n = di.world
+        err, h = None, None
+        self._c = None
+        try:
+            self._c = C.XgmiComm(n, di.rank, False, 0.0, 0.0, float(timeout_s))
+            h = self._c.flags_handle()
+        except Exception as e:  # noqa: BLE001 - reported after the vote
+            err = e
+        if not _all_ranks_ok(err is None, n):
+            raise RuntimeError(f"xGMI communicator unavailable on at least one rank (here: {err!r})")
+        hs = [None] * n
+        if n > 1:
+            dist.all_gather_object(hs, h)
+        else:
+            hs = [h]
+        try:
+            for r, hr in enumerate(hs):
+                self._c.open_flags(r, hr)
+        except Exception as e:  # noqa: BLE001
+            err = e
+        if not _all_ranks_ok(err is None, n):
+            raise RuntimeError(f"xGMI communicator: peer flags not mappable (here: {err!r})")
+        self.rank, self.size = di.rank, n
+        self._di = di
+
+    @classmethod
+    def emulated(cls, nranks: int, lat_us: float = 2.0, link_gbps: float = 64.0,
+                 timeout_s: float = 30.0) -> "XgmiDeviceComm":
+        return cls(None, timeout_s, _emulate=(nranks, lat_us, link_gbps))
+
+    @property
+    def nranks(self) -> int:
+        return self.size
+
+    @property
+    def emulated_comm(self) -> bool:
+        return bool(self._c.emulated)
+
+    def register(self, *tensors: torch.Tensor) -> None:
+        """Maps every rank's counterpart of each tensor (collective: all
+        ranks pass their own tensors of the same roles, sizes and order)."""
+        for t in tensors:
+            if not t.is_cuda or not t.is_contiguous():
+                raise ValueError("xGMI buffers must be contiguous CUDA tensors")
+            nbytes = t.numel() * t.element_size()
+            if self._c.emulated:
+                self._c.emulate_buffer(ptr(t), nbytes)
+                continue
+            err, mine = None, None
+            try:
+                mine = self._c.export_buffer(ptr(t), nbytes)
+            except Exception as e:  # noqa: BLE001
+                err = e
+            if not _all_ranks_ok(err is None, self.size):
+                raise RuntimeError(f"xGMI register: export failed on some rank (here: {err!r})")
+            allh = [None] * self.size
+            dist.all_gather_object(allh, (mine[0], int(mine[1]), nbytes))
+            try:
+                for r, (h, off, nb) in enumerate(allh):
+                    if nb != nbytes:
+                        raise ValueError(f"rank {r} registers {nb} bytes, this rank {nbytes}")
+                    self._c.open_buffer(ptr(t), nbytes, r, h, off)
+            except Exception as e:  # noqa: BLE001
+                err = e
+            if not _all_ranks_ok(err is None, self.size):
+                raise RuntimeError(f"xGMI register: peer buffer not mappable (here: {err!r})")
+
+    def error(self) -> int:
+        """Sticky device error bits (1: a peer barrier timed out); syncs."""
+        return int(self._c.error())
+
+    def all_reduce_(self, t, stream=None):
+        if t.dtype != torch.float32:
+            raise ValueError("xGMI all-reduce: fp32 only")
+        self._c.all_reduce(ptr(t), ptr(t), t.numel(), NCCL_FLOAT32, NCCL_SUM, stream_handle(stream))
+        return t
+
+    @property
+    def native_handle(self):
+        return self._c
+
+    def duplicate(self):
+        raise RuntimeError("the xGMI communicator has no second instance (no comm stream)")
+
+
+def make_xgmi_comm(di: DistInfo, device: torch.device, timeout_s: float = 30.0,
+                   quiet: bool = False) -> Optional["XgmiDeviceComm"]:
+    """The peer-to-peer communicator when every rank is on this node's GPUs,
+    else None (collective: every rank returns the same)."""
+    if di.world <= 1 or device.type != "cuda":
+        return None
+    _, one_host = _auto_vote(di)
+    if not one_host:
+        return None
+    try:
+        return XgmiDeviceComm(di, timeout_s)
+    except RuntimeError as e:
+        if not quiet:
+            print(f"[rank {di.rank}] {e}; no xGMI peer-to-peer schedule", flush=True)
+        return None
 
 
 DEFAULT_SHM_CAPACITY = 64 << 20  # bytes per rank and collective
@@ -435,29 +566,39 @@ def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto",
               shm_capacity: int = DEFAULT_SHM_CAPACITY,
               timeout_s: float = 300.0) -> Optional[DeviceComm]:
     """Communicator for `device`, or None at world size 1.  prefer: auto |
-    rccl (alias native) | shm | torch (TrainConfig.comm).
+    rccl (alias native) | shm | xgmi | torch (TrainConfig.comm).
 
     auto on GPUs: native RCCL when every rank has a GPU of its own; when any
     rank shares its GPU (more local ranks than GPUs: RCCL refuses two ranks
-    on one device) the shared-memory communicator if all ranks are on ONE
-    host (its segment is node-local), else torch.distributed.  The choice is
-    a gloo vote, and a failed shared-memory set-up falls back to
-    torch.distributed on every rank."""
+    on one device) the shared-memory communicator, which needs all ranks on
+    ONE host (its segment is node-local).  Shared GPUs across hosts, or a
+    failed shared-memory set-up, leave no communicator that works (an RCCL /
+    torch `nccl` group rejects two ranks on one device), so every rank
+    raises the same error naming the cause: the decision and the
+    shared-memory constructor are both gloo votes."""
     if di.world <= 1:
         return None
     if prefer == "rccl":
         prefer = "native"
     if device.type == "cuda" and prefer == "shm":
         return ShmDeviceComm(di, shm_capacity, timeout_s)
+    if device.type == "cuda" and prefer == "xgmi":
+        return XgmiDeviceComm(di, min(timeout_s, 60.0))
     if device.type == "cuda" and prefer == "auto":
         share, one_host = _auto_vote(di)
         if share:
-            if one_host:
-                try:  # the constructor votes: every rank raises or none does
-                    return ShmDeviceComm(di, shm_capacity, timeout_s)
-                except RuntimeError as e:
-                    print(f"[rank {di.rank}] {e}; using torch.distributed", flush=True)
-            return TorchDeviceComm(di, device)
+            if not one_host:
+                raise RuntimeError(
+                    "ranks share GPUs across several hosts: RCCL rejects two ranks on one "
+                    "device and the shared-memory communicator is node-local; run one rank "
+                    "per GPU, or all ranks on one host")
+            try:  # the constructor votes: every rank raises or none does
+                return ShmDeviceComm(di, shm_capacity, timeout_s)
+            except RuntimeError as e:
+                raise RuntimeError(
+                    f"ranks share GPUs and the shared-memory communicator could not be set up "
+                    f"({e}); RCCL rejects two ranks on one device, so there is no fallback"
+                ) from e
     if device.type == "cuda" and prefer in ("auto", "native"):
         try:  # every rank takes the same branch: RcclDeviceComm votes first
             return RcclDeviceComm(di)

@@ -32,7 +32,7 @@ import torch
 from .. import config as C
 from ..models import mnist_cnn as M
 from ..ops import native, ptr, stream_handle
-from ..parallel.comm import DeviceComm, all_reduce_grads_
+from ..parallel.comm import DeviceComm, XgmiDeviceComm, all_reduce_grads_
 from ..utils import rng
 from ..utils.data import batch_offset
 from ..utils.schedule import learning_rate
@@ -180,7 +180,8 @@ class NativeMnistEngine(MnistEngineBase):
     kind = "native"
 
     def __init__(self, cfg, train_x, train_y, device, rank=0, world=1, comm=None,
-                 force_sync: bool = False, fc1_feature_major: bool = False):
+                 force_sync: bool = False, fc1_feature_major: bool = False,
+                 xcomm: Optional[XgmiDeviceComm] = None):
         """fc1_feature_major (labs): the fp32 Winograd step's conv2 forward
         also writes a2 feature-major and the fc1 forward reads its operands
         straight from L2 (fc1_fwd_t_kernel) instead of staging them through
@@ -233,7 +234,8 @@ class NativeMnistEngine(MnistEngineBase):
         self.fac = None
         hcomm = comm.native_handle if (self.grad_sync and comm is not None) else None
         nfac = hcomm.size if hcomm is not None else 1
-        if nfac > 1 and not self.bf16:
+        self.comm_is_xgmi = isinstance(comm, XgmiDeviceComm)
+        if nfac > 1 and not self.bf16 and not self.comm_is_xgmi:
             # SCHED_FACTORS: rank-major gathered FC factors; this rank's forward /
             # head kernels write their slot in place (csrc/mnist_executor.cpp
             # train_step_factors).  Sized by the communicator (an emulated
@@ -292,6 +294,14 @@ class NativeMnistEngine(MnistEngineBase):
             p.fac_ranks = nfac
         self.ptrs = p
         self.exe = C_.MnistExecutor(p)
+        # xGMI peer-to-peer schedule: the peers read this rank's grads / params
+        # (and, to gather the sharded FC momentum, its momentum) directly
+        self.xcomm = comm if self.comm_is_xgmi else xcomm
+        if not self.grad_sync:
+            self.xcomm = None
+        if self.xcomm is not None:
+            self.xcomm.register(self.grads, self.params, self.mom)
+            self.exe.set_xgmi(self.xcomm.native_handle)
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
         self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
         if self.grad_sync and self._native_comm is None:
@@ -318,7 +328,7 @@ class NativeMnistEngine(MnistEngineBase):
         if self.grad_sync:  # connection setup of every collective used, outside any capture
             c, g, n, hs = self._native_comm, ptr(self.grads), lay.total, stream_handle()
             c.all_reduce(g, g, n, 7, 0, hs)
-            if self.exe.sharded_ok(c.size):  # grads are zero: RS / AG leave them zero
+            if self.exe.sharded_ok(c.size) and not self.comm_is_xgmi:  # grads are zero: RS / AG leave them zero
                 chunk = self.ptrs.bucket1 // c.size
                 c.reduce_scatter(g, g + 4 * chunk * c.rank, chunk, 7, 0, hs)
                 c.all_gather(g + 4 * chunk * c.rank, g, chunk, 7, hs)
@@ -348,6 +358,10 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_SERIAL
         if name == "defer" and self.exe.defer_ok():
             return E.SCHED_DEFER
+        if (name == "xgmi" or self.comm_is_xgmi) and self.exe.xgmi_ok():
+            return E.SCHED_XGMI
+        if self.comm_is_xgmi:
+            return E.SCHED_SERIAL  # (the xGMI comm's all-reduce)
         return E.SCHED_BUCKETS  # "auto" until tuned
 
     def _set_schedule(self, sched: int) -> None:
@@ -367,7 +381,7 @@ class NativeMnistEngine(MnistEngineBase):
         E = self._C.MnistExecutor
         return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
                 E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial",
-                E.SCHED_DEFER: "defer"}.get(self.exe.schedule,
+                E.SCHED_DEFER: "defer", E.SCHED_XGMI: "xgmi"}.get(self.exe.schedule,
                                                                            "buckets")
 
     def sync_optimizer_state(self) -> None:
@@ -410,7 +424,12 @@ class NativeMnistEngine(MnistEngineBase):
     def _tune_candidates(self):
         E = self._C.MnistExecutor
         n = self._native_comm.size
+        if self.comm_is_xgmi:  # no comm stream: the fused launch or the plain all-reduce
+            return ([(E.SCHED_XGMI, "xgmi")] if self.exe.xgmi_ok() else []) + [
+                (E.SCHED_SERIAL, "serial")]
         cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SERIAL, "serial")]
+        if self.xcomm is not None and self.exe.xgmi_ok():
+            cands.append((E.SCHED_XGMI, "xgmi"))
         if self.exe.sharded_ok(n):
             cands.append((E.SCHED_SHARDED_FC, "sharded"))
         # the factor schedule forms the FC gradients in another summation
@@ -447,9 +466,11 @@ class NativeMnistEngine(MnistEngineBase):
         # bf16 shadows) as current: derive them from the weights first
         self.exe.refresh_shadows(stream_handle())
         snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
-        for sched, name in self._tune_candidates():
+        cands = self._tune_candidates()
+        for sched, name in cands:
             self._set_schedule(sched)
-            g = self._graph(G, sticky=(sched == E.SCHED_BUCKETS))
+            g = self._graph(G, sticky=(sched == cands[-1][0] if self.comm_is_xgmi
+                                       else sched == E.SCHED_BUCKETS))
             # the decision must be collective: a candidate any rank could not
             # capture is dropped on every rank
             ok = D.allreduce_max_host(0.0 if g is not None else 1.0) == 0.0
@@ -460,6 +481,9 @@ class NativeMnistEngine(MnistEngineBase):
                 continue
             g.replay()
             torch.cuda.synchronize(self.device)
+            if sched == E.SCHED_XGMI and not self._xgmi_healthy():
+                self.tune_log[name] = None  # a peer barrier timed out: never pick it
+                continue
             t0 = torch.cuda.Event(enable_timing=True)
             t1 = torch.cuda.Event(enable_timing=True)
             t0.record()
@@ -472,7 +496,8 @@ class NativeMnistEngine(MnistEngineBase):
             self.tune_log[name] = round(us, 2)
             if best is None or us < best[0]:
                 best = (us, sched)
-        self._set_schedule(best[1] if best is not None else E.SCHED_BUCKETS)
+        self._set_schedule(best[1] if best is not None else cands[-1][0] if self.comm_is_xgmi
+                           else E.SCHED_BUCKETS)
         self.exe.join(stream_handle())
         self.params.copy_(snap[0])
         self.mom.copy_(snap[1])
@@ -481,6 +506,22 @@ class NativeMnistEngine(MnistEngineBase):
         self._tuned = True
         self.tune_steps_run = steps
         return steps
+
+    def _xgmi_healthy(self) -> bool:
+        """Collective: no rank's xGMI barrier timed out (the device kernels
+        never hang: a missing peer sets a sticky error bit instead)."""
+        from ..parallel import dist as D
+        from ..parallel.sync import replicas_identical
+        bad = self.xcomm.error() if self.xcomm is not None else 0
+        if D.allreduce_max_host(float(bad)) != 0.0:
+            return False
+        if self.xcomm is None or self.xcomm.emulated_comm:
+            return True
+        # replicas must agree bit for bit after the trial steps (a lost or torn
+        # peer read would show here): gather the sharded momentum and compare
+        self.sync_optimizer_state()
+        torch.cuda.synchronize(self.device)
+        return replicas_identical(self.params) and replicas_identical(self.mom)
 
     def prewarm_train(self, ms: float) -> float:
         """Untimed, side-effect-free training replays for ~`ms` of wall time
@@ -606,12 +647,14 @@ class NativeMnistEngine(MnistEngineBase):
 
 
 def make_engine(cfg: C.TrainConfig, train_x, train_y, device: torch.device, rank=0, world=1,
-                comm=None, backend: Optional[str] = None, force_sync: bool = False):
+                comm=None, backend: Optional[str] = None, force_sync: bool = False,
+                xcomm: Optional[XgmiDeviceComm] = None):
     backend = backend or cfg.backend
     if backend == "auto":
         backend = "native" if device.type == "cuda" else "torch"
     if cfg.dtype != "fp32" and backend != "native":
         raise NotImplementedError(f"dtype {cfg.dtype} needs the native (GPU) MNIST engine")
     if backend == "native":
-        return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)
+        return NativeMnistEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync,
+                                 xcomm=xcomm)
     return TorchMnistEngine(cfg, train_x, train_y, device, rank, world, comm)

@@ -17,6 +17,11 @@ usage: captured_sync_ranks.py SCENARIO [DTYPE]
   generic MODEL - ResNet-18 (B=4, 2-step graphs after the eager warm-up) or
                   the fused LeNet-5 executor with captured bucketed sync vs
                   the serial emulation
+  xgmi DTYPE    - the xGMI peer-to-peer communicator over IPC-mapped buffers
+                  of the two processes (csrc/xgmi_comm.h): its all-reduce and
+                  segment gather vs gloo, and the captured fused sync + SGD
+                  schedule (SCHED_XGMI) and its plain all-reduce schedule vs the
+                  eager buckets schedule, bit for bit
 """
 import os
 import sys
@@ -122,6 +127,51 @@ def scenario_mnist(di, dtype):
     return f"schedules={','.join(scheds)} tuned={picked}"
 
 
+def scenario_xgmi(di, dtype):
+    from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+
+    xc = XgmiDeviceComm(di, timeout_s=20.0)
+    # generic in-place all-reduce of a registered buffer (segments of unequal
+    # length: 100,004 floats over 2 ranks) and the segment gather, vs gloo
+    g = torch.Generator().manual_seed(11 + di.rank)
+    host = torch.randn(100_004, generator=g)
+    t = host.cuda()
+    xc.register(t)
+    want = host.clone()
+    dist.all_reduce(want)
+    for _ in range(3):  # repeated: the per-block epochs advance
+        t.copy_(host.cuda())
+        xc.all_reduce_(t)
+        torch.cuda.synchronize()
+        assert torch.equal(t.cpu(), want), "xgmi all-reduce != gloo sum"
+    t.copy_(host.cuda())
+    xc._c.gather_segments(ptr(t), t.numel(), stream_handle())
+    torch.cuda.synchronize()
+    seg = (t.numel() // 4 + di.world - 1) // di.world * 4
+    parts = [torch.empty_like(host) for _ in range(di.world)]
+    dist.all_gather(parts, host)
+    for r in range(di.world):
+        lo, hi = r * seg, min(t.numel(), (r + 1) * seg)
+        assert torch.equal(t.cpu()[lo:hi], parts[r][lo:hi]), f"gather: segment {r}"
+    assert xc.error() == 0, "an xgmi barrier timed out"
+    # the MNIST schedules over the xgmi communicator vs the eager buckets run
+    ref, _ = run_fixed(di, "buckets", dtype, "eager")
+    picked = []
+    for sched in ("xgmi", "serial", "auto"):
+        cfg = C.TrainConfig(sync_schedule=sched, dtype=dtype, graph=True, graph_steps=G).validate()
+        x, y = NS._shard(di.rank, di.world, cfg.seed)
+        comm = XgmiDeviceComm(di, timeout_s=20.0)
+        eng = NativeMnistEngine(cfg, x, y, torch.device("cuda"), di.rank, di.world, comm)
+        assert eng.use_graph and eng.xcomm is comm
+        if sched != "auto":
+            assert eng.sync_schedule == sched, (eng.sync_schedule, sched)
+        eng.train(STEPS)
+        assert comm.error() == 0, f"{sched}: an xgmi barrier timed out"
+        same(finish(eng), ref, f"xgmi comm, {sched} (captured) vs eager buckets")
+        picked.append(eng.sync_schedule)
+    return f"all_reduce+gather ok; schedules xgmi, serial, auto->{picked[-1]}"
+
+
 def scenario_param_avg(di):
     outs = {}
     for kind in ("shm",):
@@ -224,6 +274,8 @@ def main():
     arg = sys.argv[2] if len(sys.argv) > 2 else ""
     if scen == "mnist":
         msg = scenario_mnist(di, arg or "fp32")
+    elif scen == "xgmi":
+        msg = scenario_xgmi(di, arg or "fp32")
     elif scen == "param_avg":
         msg = scenario_param_avg(di)
     elif scen == "generic":

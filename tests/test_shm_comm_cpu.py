@@ -59,3 +59,29 @@ def test_shm_rejects_bad_layout(tmp_path, bad):
     kw.update(bad)
     with pytest.raises(RuntimeError):
         native().ShmComm(**kw)
+
+
+@pytest.mark.parametrize("case", ["multi_host", "shm_fails"])
+def test_auto_comm_with_shared_gpus_raises_instead_of_rccl_fallback(monkeypatch, case):
+    """comm=auto when ranks share GPUs: with the ranks on several hosts, or
+    when the shared-memory set-up fails, no device communicator can work
+    (RCCL / a torch `nccl` group rejects two ranks on one device), so
+    make_comm raises an error naming the cause instead of returning a
+    torch.distributed communicator that would fail later."""
+    import torch
+    from mpi_tensorflow_amd.parallel import comm as CM
+    from mpi_tensorflow_amd.parallel.dist import DistInfo
+
+    di = DistInfo(rank=0, world=2, local_rank=0, local_world=2, launcher="torchrun")
+    monkeypatch.setattr(CM, "_auto_vote", lambda _di: (True, case != "multi_host"))
+
+    def no_shm(*a, **k):
+        raise RuntimeError("shared-memory communicator unavailable (rank 0: ENOSPC)")
+
+    monkeypatch.setattr(CM, "ShmDeviceComm", no_shm)
+    monkeypatch.setattr(CM, "TorchDeviceComm",
+                        lambda *a, **k: pytest.fail("fell back to torch.distributed"))
+    with pytest.raises(RuntimeError) as ei:
+        CM.make_comm(di, torch.device("cuda"), "auto")
+    msg = str(ei.value)
+    assert ("several hosts" in msg) if case == "multi_host" else ("ENOSPC" in msg and "no fallback" in msg)
