@@ -188,9 +188,10 @@ def main(argv=None) -> int:
     from mpi_tensorflow_amd.utils.faults import maybe_fail
 
     if a.gpus > 1 and D.discover().launcher == "none":
-        # --comm shm / auto: ranks may share GPUs (rank r binds GPU r % count;
-        # auto then picks the shared-memory communicator, parallel/comm.py)
-        return launch_ranks(a.gpus, argv, share_gpus=a.comm in ("shm", "auto"))
+        # --comm shm / auto / xgmi: ranks may share GPUs (rank r binds GPU r %
+        # count; auto then picks the shared-memory communicator, parallel/comm.py;
+        # xgmi maps the other ranks' buffers on the same device)
+        return launch_ranks(a.gpus, argv, share_gpus=a.comm in ("shm", "auto", "xgmi"))
     if D.discover().world != a.gpus:
         print(f"error: --gpus {a.gpus} but the launcher started {D.discover().world} rank(s)",
               file=sys.stderr)
@@ -347,7 +348,8 @@ def run(a, di, device, wd) -> int:
     else:
         model_desc = "resnet18 (BasicBlock [2,2,2,2], BatchNorm, 10 classes)"
         image, data_desc = "224x224x3", "synthetic (ImageNet-shaped 224x224x3, shared-template task v2; random-init weights)"
-    comm_nranks = comm.nranks if hasattr(comm, "nranks") else None  # as the library reports it
+    # as the library reports it (an emulated communicator stands in for more ranks)
+    comm_nranks = comm.nranks if hasattr(comm, "nranks") and not force else None
     if comm_nranks is not None and comm_nranks != N:
         print(f"error: the communicator has {comm_nranks} ranks, expected {N}", file=sys.stderr)
         return 3

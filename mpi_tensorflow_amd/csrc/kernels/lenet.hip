@@ -10,7 +10,13 @@
 // in ~37 launches (conv engines, library GEMMs, reductions, 239 us/step).
 // Here a train step is TWO launches:
 //
-//  image kernel  one 512-thread workgroup per image, everything in LDS:
+//  image kernel  PARTS (4) 512-thread workgroups per image, everything in LDS
+//                (train; eval runs one per image).  Each of the 4 runs the
+//                image's forward and FC backward chain itself (cheap, redundant)
+//                and then a quarter of the conv backward: conv2 filter grad of
+//                4 of the 16 output channels, conv2 data grad / conv1 filter
+//                grad of its share of the 6 conv1 channels ({0,1} {2,3} {4} {5}).
+//                256 workgroups at B = 64 instead of 64 on a 256-CU part:
 //                batch row at the device-step offset, conv1 / conv2 with the
 //                pool + argmax in the epilogue (pool windows = 4 accumulators
 //                of one thread, as float2 pairs -> v_pk_fma_f32), the FC chain
@@ -36,6 +42,7 @@ namespace lenet {
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 constexpr int NT = 512;  // threads per image workgroup
+constexpr int PARTS = 4;  // train: workgroups per image (blockIdx = part * batch + image)
 constexpr int IH = 32, IC = 3;
 constexpr int C1 = 6, P1 = 14;
 constexpr int C2 = 16, O2 = 10, P2 = 5;
@@ -87,12 +94,15 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
   __shared__ uint8_t q1s[P1 * P1 * C1];
   __shared__ uint8_t q2s[F0];
   const int tid = threadIdx.x;
-  const int img = blockIdx.x;
+  // train: part q of image img; the PARTS workgroups of an image are batch
+  // blocks apart (same blockIdx % 8 for B % 8 == 0: one XCD, one L2)
+  const int q = TRAIN ? (int)blockIdx.x / a.batch : 0;
+  const int img = TRAIN ? (int)blockIdx.x % a.batch : (int)blockIdx.x;
   long long row = img;
   if (TRAIN) {
     const long long st = *a.step;
     row = (st * a.batch) % (long long)(a.n_local - a.batch) + img;
-    if (img == 0 && tid == 0)  // reference LR schedule (mpipy.py:59-64), staircase per local epoch
+    if (img == 0 && q == 0 && tid == 0)  // reference LR schedule (mpipy.py:59-64), staircase per local epoch
       *a.lr_out = a.base_lr * powf(a.lr_decay, (float)((st * a.batch) / a.n_local));
   }
   const float* W = a.params;
@@ -291,7 +301,7 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
     const float se = wave_sum(e);
     const float lab = wave_sum(tid == label ? lg : 0.f);
     if (tid < F3) sm[S_D3 + tid] = (e / se - (tid == label ? 1.f : 0.f)) / (float)a.batch;
-    if (tid == 0) {
+    if (tid == 0 && q == 0) {
       a.loss_rows[img] = logf(se) + mx - lab;
       if (a.correct && am == label) atomicAdd(a.correct, 1);
     }
@@ -352,25 +362,29 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
     sm[S_T2 + 2 * tid] = g2;
     sm[S_T2 + 2 * tid + 1] = __int_as_float((u * P1 + v) * C1);
   }
-  // FC layer inputs / deltas for the batch-level weight gradients
-  if (tid < F0) act[tid] = sm[S_P2 + tid];
-  if (tid < F1) act[F0 + tid] = sm[S_H1 + tid];
-  if (tid < F2) act[F0 + F1 + tid] = sm[S_H2 + tid];
-  if (tid < F1) del[tid] = sm[S_D1 + tid];
-  if (tid < F2) del[F1 + tid] = sm[S_D2 + tid];
-  if (tid < F3) del[F1 + F2 + tid] = sm[S_D3 + tid];
+  // FC layer inputs / deltas for the batch-level weight gradients (part 0)
+  if (q == 0) {
+    if (tid < F0) act[tid] = sm[S_P2 + tid];
+    if (tid < F1) act[F0 + tid] = sm[S_H1 + tid];
+    if (tid < F2) act[F0 + F1 + tid] = sm[S_H2 + tid];
+    if (tid < F1) del[tid] = sm[S_D1 + tid];
+    if (tid < F2) del[F1 + tid] = sm[S_D2 + tid];
+    if (tid < F3) del[F1 + F2 + tid] = sm[S_D3 + tid];
+  }
   __syncthreads();
 
   float* cp = a.convp + (size_t)img * CONVP_STRIDE;
   if (a.stop_phase == 4) return;
   // ---- H: conv2 filter grad, sparse over the 25 argmax pixels per channel
   // (table T2 = (g2, p1 offset of the argmax pixel) per (pp, co)):
-  // dW2[kh,kw,ci,co] = sum_pp g2[pp,co] * p1[u_pp + kh, v_pp + kw, ci]
+  // dW2[kh,kw,ci,co] = sum_pp g2[pp,co] * p1[u_pp + kh, v_pp + kw, ci];
+  // this part's 4 output channels co = 4q .. 4q + 3 (600 weights)
 #pragma unroll
-  for (int k = 0; k < 5; ++k) {
-    const int e = tid + NT * k;
-    if (e < W2N) {
-      const int co = e & 15, r = e >> 4, ci = r % C1, t = r / C1, kh = t / 5, kw = t % 5;
+  for (int k = 0; k < 2; ++k) {
+    const int f = tid + NT * k;
+    if (f < W2N / PARTS) {
+      const int co = 4 * q + (f & 3), r = f >> 2, ci = r % C1, t = r / C1, kh = t / 5, kw = t % 5;
+      const int e = r * C2 + co;
       const float* p1 = sm + S_P1 + (kh * P1 + kw) * C1 + ci;
       const float2* t2 = reinterpret_cast<const float2*>(sm + S_T2) + co;
       float s = 0.f;
@@ -382,20 +396,25 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
       cp[W1N + 8 + e] = s;
     }
   }
-  if (tid < C2) {  // db2
+  if (tid < 4) {  // db2 of this part's channels
+    const int co = 4 * q + tid;
     float s = 0.f;
-    for (int pp = 0; pp < P2 * P2; ++pp) s += sm[S_T2 + 2 * (pp * C2 + tid)];
-    cp[W1N + 8 + W2N + tid] = s;
+    for (int pp = 0; pp < P2 * P2; ++pp) s += sm[S_T2 + 2 * (pp * C2 + co)];
+    cp[W1N + 8 + W2N + co] = s;
   }
   if (a.stop_phase == 5) return;
   // ---- I: conv2 data grad over the zero-bordered dpre2 plane:
   // dp1[y,x,ci] = sum_{kh,kw,co} dpre2[y-kh, x-kw, co] W2[kh,kw,ci,co].
-  // Thread = (pooled1 pixel, half of the 16 channels co), all 6 ci as 3
-  // packed pairs (v_pk_fma_f32): per tap 2 float4 dpre2 reads + 8 x 3 float2
-  // weight broadcasts ([tap][co][ci] copy of W2).
+  // Thread = (pooled1 pixel, half of the 16 channels co); this part's conv1
+  // channels as ONE packed pair (v_pk_fma_f32): pair pi = {2 pi, 2 pi + 1},
+  // parts 0 / 1 use pairs 0 / 1, parts 2 / 3 pair 2 (channel 4 / 5 of it).
+  // Per tap 2 float4 dpre2 reads + 8 float2 weight broadcasts ([tap][co][ci]
+  // copy of W2).
+  const int pi = q < 2 ? q : 2;
+  const int c_lo = q < 2 ? 2 * q : q + 2, c_hi = q < 2 ? 2 * q + 2 : q + 3;
   {
     const int grp = tid >> 8, p = tid & 255;
-    f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f}, s45 = {0.f, 0.f};
+    f2 sp = {0.f, 0.f};
     if (p < P1 * P1) {
       const int y = p / P1, x = p % P1;
 #pragma unroll
@@ -411,25 +430,21 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
 #pragma unroll
           for (int c = 0; c < 8; ++c) {
             const f2 dd = {d[c], d[c]};
-            s01 = __builtin_elementwise_fma(dd, wp[3 * c], s01);
-            s23 = __builtin_elementwise_fma(dd, wp[3 * c + 1], s23);
-            s45 = __builtin_elementwise_fma(dd, wp[3 * c + 2], s45);
+            sp = __builtin_elementwise_fma(dd, wp[3 * c + pi], sp);
           }
         }
       if (grp == 1) {
-        float* gp = sm + S_G1 + p * C1;
-        gp[0] = s01.x, gp[1] = s01.y, gp[2] = s23.x, gp[3] = s23.y, gp[4] = s45.x, gp[5] = s45.y;
+        float* gp = sm + S_G1 + p * C1 + 2 * pi;
+        gp[0] = sp.x, gp[1] = sp.y;
       }
     }
     __syncthreads();  // every dpre2 read is done: the T1 table may overwrite it
     if (grp == 0 && p < P1 * P1) {
       const int py = p / P1, px = p % P1;
-      const float sv[6] = {s01.x, s01.y, s23.x, s23.y, s45.x, s45.y};
-#pragma unroll
-      for (int c = 0; c < C1; ++c) {
-        const float g = sm[S_G1 + p * C1 + c] + sv[c];
-        const int q = q1s[p * C1 + c];
-        const int u = 2 * py + (q >> 1), v = 2 * px + (q & 1);
+      for (int c = c_lo; c < c_hi; ++c) {
+        const float g = sm[S_G1 + p * C1 + c] + (c == 2 * pi ? sp.x : sp.y);
+        const int qq = q1s[p * C1 + c];
+        const int u = 2 * py + (qq >> 1), v = 2 * px + (qq & 1);
         // ReLU1 through the pooled output; T1 = (g1, input offset of the argmax)
         sm[S_T1 + 2 * (p * C1 + c)] = sm[S_P1 + p * C1 + c] > 0.f ? g : 0.f;
         sm[S_T1 + 2 * (p * C1 + c) + 1] = __int_as_float(u * XRS + v);
@@ -439,24 +454,37 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
   __syncthreads();
   if (a.stop_phase == 6) return;
   // ---- J: conv1 filter grad, sparse over the 196 argmax pixels per channel:
-  // dW1[kh,kw,ci,c] = sum_p g1[p,c] * x[ci, u_p + kh, v_p + kw]
-  if (tid < W1N) {
-    const int c = tid % C1, ci = (tid / C1) % IC, t = tid / (C1 * IC), kh = t / 5, kw = t % 5;
-    const float* xp = sm + S_X + ci * XPL + kh * XRS + kw;
-    const float2* t1 = reinterpret_cast<const float2*>(sm + S_T1) + c;
+  // dW1[kh,kw,ci,c] = sum_p g1[p,c] * x[ci, u_p + kh, v_p + kw], for this
+  // part's channels c in [c_lo, c_hi); 2 or 4 threads per weight split the
+  // pixels (even / odd pixel chains, summed in a fixed order)
+  {
+    const int nc = c_hi - c_lo, nw = 75 * nc;  // weights of this part
+    const int split = nc == 2 ? 2 : 4;         // threads per weight
+    const int wi = tid / split, part = tid % split;
     float s0 = 0.f, s1 = 0.f;
-#pragma unroll 14
-    for (int p = 0; p < P1 * P1; p += 2) {
-      const float2 ta = t1[p * C1], tb = t1[(p + 1) * C1];
-      s0 = fmaf(ta.x, xp[__float_as_int(ta.y)], s0);
-      s1 = fmaf(tb.x, xp[__float_as_int(tb.y)], s1);
+    if (wi < nw) {
+      const int c = c_lo + wi % nc, ci = (wi / nc) % IC, t = wi / (nc * IC), kh = t / 5, kw = t % 5;
+      const float* xp = sm + S_X + ci * XPL + kh * XRS + kw;
+      const float2* t1 = reinterpret_cast<const float2*>(sm + S_T1) + c;
+      for (int p = 2 * part; p < P1 * P1; p += 2 * split) {
+        const float2 ta = t1[p * C1], tb = t1[(p + 1) * C1];
+        s0 = fmaf(ta.x, xp[__float_as_int(ta.y)], s0);
+        s1 = fmaf(tb.x, xp[__float_as_int(tb.y)], s1);
+      }
     }
-    cp[tid] = s0 + s1;
-  } else if (tid < W1N + C1) {  // db1
-    const int c = tid - W1N;
-    float s = 0.f;
-    for (int p = 0; p < P1 * P1; ++p) s += sm[S_T1 + 2 * (p * C1 + c)];
-    cp[W1N + c] = s;
+    float s = s0 + s1;
+    s += __shfl_xor(s, 1, 64);
+    if (split == 4) s += __shfl_xor(s, 2, 64);
+    if (wi < nw && part == 0) {
+      const int c = c_lo + wi % nc, ci = (wi / nc) % IC, t = wi / (nc * IC);
+      cp[(t * IC + ci) * C1 + c] = s;
+    }
+    if (tid >= 480 && tid < 480 + nc) {  // db1 (a wave of its own)
+      const int c = c_lo + tid - 480;
+      float sb = 0.f;
+      for (int p = 0; p < P1 * P1; ++p) sb += sm[S_T1 + 2 * (p * C1 + c)];
+      cp[W1N + c] = sb;
+    }
   }
 }
 
@@ -593,7 +621,7 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
 void launch_image_train(const ImageArgs& a, hipStream_t s) {
   if (a.batch <= 0 || a.n_local <= a.batch)
     throw std::runtime_error("lenet: the local shard must exceed the batch");
-  image_kernel<true><<<a.batch, NT, 0, s>>>(a);
+  image_kernel<true><<<a.batch * PARTS, NT, 0, s>>>(a);
 }
 
 void launch_image_eval(const ImageArgs& a, int rows, hipStream_t s) {

@@ -275,8 +275,13 @@ class XgmiDeviceComm(DeviceComm):
         return int(self._c.error())
 
     def all_reduce_(self, t, stream=None):
-        if t.dtype != torch.float32:
-            raise ValueError("xGMI all-reduce: fp32 only")
+        """In-place fp32 sum.  A tensor not registered yet is registered
+        first (collective like the all-reduce itself; not inside a graph
+        capture: the set-up exchanges IPC handles over gloo)."""
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            raise ValueError("xGMI all-reduce: contiguous fp32 only")
+        if not self._c.registered(ptr(t), 4 * t.numel()):
+            self.register(t)
         self._c.all_reduce(ptr(t), ptr(t), t.numel(), NCCL_FLOAT32, NCCL_SUM, stream_handle(stream))
         return t
 

@@ -104,6 +104,10 @@ class NativeLenetEngine:
                 raise RuntimeError("GPU grad sync needs the native RCCL communicator")
             if getattr(comm, "kind", "") == "host-staged":  # test comm: eager only
                 comm.bases = [self.grads] + ([self.gb16] if self.gb16 is not None else [])
+            if hasattr(comm, "register"):  # xGMI peer-to-peer: peers read the grads
+                if self.gb16 is not None:
+                    raise ValueError("the xGMI communicator reduces fp32 grads only")
+                comm.register(self.grads)
             # connection setup of the collective, outside any capture
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())

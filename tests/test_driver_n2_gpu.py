@@ -73,6 +73,25 @@ def test_bench_two_ranks_shared_gpu(cuda_dev, model, dtype, extra):
         assert c["sync_schedule"] in tune
 
 
+@pytest.mark.parametrize("model,dtype", [("mnist_cnn", "fp32"), ("mnist_cnn", "bf16"),
+                                         ("lenet5", "fp32")])
+def test_bench_two_ranks_xgmi_peer_to_peer(cuda_dev, model, dtype):
+    """`bench.py --gpus 2 --comm xgmi`: the peer-to-peer communicator maps
+    the other rank's buffers (on the same device here, over xGMI on a node);
+    MNIST tunes its fused sync + SGD launch against the plain peer-to-peer
+    all-reduce, and the replicas must end bit-identical."""
+    out = _run([sys.executable, "bench.py", "--gpus", "2", "--comm", "xgmi", "--model", model,
+                "--dtype", dtype, "--steps", "30", "--warmup", "5"])
+    lines = _json_lines(out)
+    assert len(lines) == 1, out
+    c = lines[0]["config"]
+    assert c["comm"] == "xgmi-p2p" and c["comm_nranks"] == 2 and c["replicas_identical"] is True
+    if model == "mnist_cnn":
+        tune = c["sync_tune_us_per_step"]
+        assert tune and set(tune) == {"xgmi", "serial"} and None not in tune.values(), tune
+        assert lines[0]["final_test_accuracy"] > 50.0
+
+
 def _mpipy(tmp_path, tag, *args, timeout=420):
     port = _free_port()
     ck = tmp_path / f"{tag}.npz"

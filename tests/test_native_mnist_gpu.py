@@ -161,27 +161,37 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties, 
 
 
 def test_training_trajectory_matches_oracle(cuda_dev, data):
-    nat, ref = _engines(cuda_dev, data)
-    p0 = ref.params.clone()
-    losses_n, losses_r = [], []
-    for _ in range(6):
-        nat.train(5)
-        ref.train(5)
-        torch.cuda.synchronize()
-        losses_n.append(nat.loss_value())
-        losses_r.append(ref.loss_value())
+    """30 native steps vs the fp32 PyTorch oracle run on the CPU: the CPU
+    oracle is deterministic (fixed thread count), so the bound measures the
+    native engine's own drift (the GPU oracle's MIOpen convolutions moved the
+    same native run by 3.6e-2 .. 5.24e-2 from box to box; VERDICT r4 #7)."""
+    x, y = data
+    cfg = C.TrainConfig(graph=False).validate()
+    nat = NativeMnistEngine(cfg, x, y, cuda_dev)
+    nthreads = torch.get_num_threads()
+    torch.set_num_threads(4)
+    try:
+        ref = TorchMnistEngine(cfg, x, y, torch.device("cpu"))
+        p0 = ref.params.clone()
+        losses_n, losses_r = [], []
+        for _ in range(6):
+            nat.train(5)
+            ref.train(5)
+            torch.cuda.synchronize()
+            losses_n.append(nat.loss_value())
+            losses_r.append(ref.loss_value())
+    finally:
+        torch.set_num_threads(nthreads)
     assert nat.step == ref.step == 30
     assert int(nat.step_dev.item()) == 30
     assert abs(nat.device_lr() - ref.lr(29)) < 1e-9
     # fp32 summation-order differences can flip a ReLU / max-pool tie and route
     # one element's gradient differently; over 30 steps that drift compounds,
-    # so the trajectory is compared loosely (the strict check is per step).
-    # The oracle's own MIOpen convolutions are not bit-reproducible from box to
-    # box: the same native build measured 3.6e-2 .. 5.24e-2 here, hence 8e-2.
-    d = nat.params - ref.params
+    # so the trajectory is compared loosely (the strict check is per step)
+    d = nat.params.cpu() - ref.params
     rel_upd = (d.norm() / (ref.params - p0).norm()).item()
     print(f"trajectory: rel_update_err={rel_upd:.3e} losses native={losses_n} ref={losses_r}")
-    assert rel_upd < 8e-2, rel_upd
+    assert rel_upd < 5e-2, rel_upd
     for a, b in zip(losses_n, losses_r):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b))
 

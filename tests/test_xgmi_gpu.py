@@ -33,7 +33,7 @@ def test_xgmi_two_ranks_bit_identical_to_buckets(dtype):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), HELPER, "xgmi", dtype]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert f"CAPTURED_SYNC_OK xgmi {dtype} world=2" in r.stdout, r.stdout[-2000:]
 
