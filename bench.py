@@ -91,6 +91,9 @@ def parse(argv=None):
                     help="what the prewarm runs: forward-only test-set passes (eval), or "
                          "training-graph replays on snapshotted state that is restored "
                          "afterwards (train; engines with prewarm_train, else eval)")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="lenet5 / resnet18: target gradient bytes per all-reduce bucket (MiB; "
+                         "default models/generic.py BUCKET_BYTES)")
     ap.add_argument("--collective-timeout-s", type=float, default=300.0,
                     help="watchdog deadline per device-waiting region (N > 1): a hung or "
                          "failed collective aborts the communicators and exits non-zero")
@@ -244,13 +247,17 @@ def run(a, di, device, wd) -> int:
         if force and a.xgmi_emulate:
             from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
             f = [float(v) for v in a.xgmi_emulate.split(",")]
-            comm = XgmiDeviceComm.emulated(int(f[2]) if len(f) > 2 else 8, f[0], f[1])
-        elif force and a.comm_emulate:
+            xe = XgmiDeviceComm.emulated(int(f[2]) if len(f) > 2 else 8, f[0], f[1])
+            if a.comm_emulate:  # both: the xGMI schedule is a candidate next to the RCCL ones
+                xcomm = xe
+            else:
+                comm = xe
+        if force and a.comm_emulate:
             from mpi_tensorflow_amd.parallel.comm import EmulatedDeviceComm
             f = [float(v) for v in a.comm_emulate.split(",")]
             comm = EmulatedDeviceComm(int(f[2]) if len(f) > 2 else 8, f[0], f[1],
                                       int(f[3]) if len(f) > 3 else 32)
-        elif force:
+        elif force and not a.xgmi_emulate:
             from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
             comm = RcclDeviceComm(di)
         wd.add(comm)
@@ -261,7 +268,11 @@ def run(a, di, device, wd) -> int:
                               force_sync=force, xcomm=xcomm)
             test_x, test_y = shard.test_x, shard.test_y
         else:
+            from mpi_tensorflow_amd.models import generic as GM
             from mpi_tensorflow_amd.models.generic import model_input_shape
+            if a.bucket_mb:
+                GM.BUCKET_BYTES = int(a.bucket_mb * (1 << 20))
+                GM.MAX_BUCKETS = 64
             from mpi_tensorflow_amd.runtime.generic_engine import make_image_engine
             from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 

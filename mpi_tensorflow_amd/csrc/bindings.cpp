@@ -775,6 +775,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_defer_split", &MnistExecutor::set_defer_split)
       .def("set_xgmi", &MnistExecutor::set_xgmi, py::keep_alive<1, 2>())
       .def("xgmi_ok", &MnistExecutor::xgmi_ok)
+      .def("set_xgmi_fc_in_bwd", &MnistExecutor::set_xgmi_fc_in_bwd)
       .def_property_readonly("defer_split", &MnistExecutor::defer_split)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
       .def("gather_optimizer_state",

@@ -100,9 +100,13 @@ void launch_conv2_bwd_data_wino(const float* dy2, const float* Ud, const float* 
 // launch_conv2_bwd_data_wino, dy2 / Ud / a1 -> da1m, + the conv1 filter-grad
 // partials c1; no FC SGD) and the filter gradient (as
 // launch_conv2_bwd_filter_wino without its conv1 role: a1p / dy2 -> part2)
+// xfc (optional, world > 1 over xGMI): the FC bucket's exchange + SGD as the
+// first blocks of this launch (mnist.h XgmiStepArgs; then launch_xgmi_step
+// with fc_in_bwd for the conv parameters)
+struct XgmiStepArgs;
 void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, const float* dy2,
                            int batch, float* da1m, float* part2, hipStream_t s,
-                           const C1FilterArgs* c1 = nullptr);
+                           const C1FilterArgs* c1 = nullptr, const XgmiStepArgs* xfc = nullptr);
 int fc1_train_splits();
 void launch_fc1_fwd_train(const float* a2, const float* w, int batch, float* part, hipStream_t s);
 // fc1 train forward over the feature-major a2t [3136][batch] (batch % 32 ==
@@ -231,11 +235,16 @@ struct XgmiStepArgs {
   int nblk1 = 0;
   float* wino_u = nullptr;
   float* wino_ud = nullptr;
-  // set by the launcher
+  // the FC bucket already went through the conv2 backward launch's role
+  // blocks (launch_conv2_bwd_wino with these args): the step does the conv part
+  int fc_in_bwd = 0;
+  // set by the launchers (xgmi_fc_plan)
   long long seg4 = 0;
   int per4 = 0, nfc = 0, ncv = 0;
 };
 void launch_xgmi_step(const XgmiStepArgs& a, hipStream_t s);
+// FC role geometry for `threads`-thread blocks (<= 64 blocks)
+void xgmi_fc_plan(XgmiStepArgs& a, int threads);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

@@ -1895,19 +1895,100 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
 // is done, so there is no launch boundary and no drain between the two.
 // No FC SGD tail here (its registers would spill at 768 threads): with the
 // FC SGD in the bwd-data launch the executor keeps the two launches.
+// ---- xGMI FC role (mnist.h XgmiStepArgs): slice blk = blockIdx.x of this
+// rank's FC segment - sum every rank's grads (rank order), momentum SGD on
+// this rank's params / momentum, barrier, then copy the same slice of every
+// other segment from its owner.  Run by xgmi_step_kernel, or as the first
+// blocks of the merged conv2 backward launch (conv2_bwd_wino_kernel: the FC
+// exchange overlaps the conv backward on the other CUs).
+constexpr int XS_UNROLL = 2;
+
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+  return a;
+}
+
+__device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
+  const xgmi::Sync& s = a.sync;
+  const int n = s.nranks, me = s.rank, tid = threadIdx.x, nt = blockDim.x;
+  const float lr = *a.lr;
+  const unsigned e = xgmi::next_epoch(s, ep);
+  xgmi::barrier(s, 0, e);
+  const long long lo = (long long)blockIdx.x * a.per4;
+  const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
+  long long t0 = xgmi::now_ticks();
+  const long long base = (long long)me * a.seg4;
+  float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+  float4* M4 = reinterpret_cast<float4*>(a.mom);
+  for (long long i0 = lo + tid; i0 < hi; i0 += (long long)nt * XS_UNROLL) {
+    float4 v[xgmi::kMaxRanks][XS_UNROLL], wv[XS_UNROLL], mv[XS_UNROLL];
+#pragma unroll
+    for (int u = 0; u < XS_UNROLL; ++u) {
+      const bool ok = i0 + nt * u < hi;
+      const long long i = base + i0 + nt * u;
+#pragma unroll
+      for (int r = 0; r < xgmi::kMaxRanks; ++r)
+        if (r < n && ok) v[r][u] = reinterpret_cast<const float4*>(a.g[r])[i];
+      if (ok) {
+        wv[u] = W4[i];
+        mv[u] = M4[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < XS_UNROLL; ++u) {
+      if (i0 + nt * u >= hi) continue;
+      float4 sv = v[0][u];
+#pragma unroll
+      for (int r = 1; r < xgmi::kMaxRanks; ++r)
+        if (r < n) sv = add4(sv, v[r][u]);
+      sgd4(wv[u], mv[u], sv, a.l2, lr, a.momentum, a.gscale);
+      const long long i = base + i0 + nt * u;
+      W4[i] = wv[u];
+      M4[i] = mv[u];
+    }
+  }
+  xgmi::link_floor(s, t0, a.seg4 * 16);
+  xgmi::barrier(s, 1, e);
+  t0 = xgmi::now_ticks();
+  for (int r = 0; r < n; ++r) {
+    if (r == me) continue;
+    const long long rb = (long long)r * a.seg4;
+    const float4* src = reinterpret_cast<const float4*>(a.w[r]);
+    for (long long i0 = lo + tid; i0 < hi; i0 += (long long)nt * XS_UNROLL) {
+      float4 v[XS_UNROLL];
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u)
+        if (i0 + nt * u < hi) v[u] = src[rb + i0 + nt * u];
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u)
+        if (i0 + nt * u < hi) W4[rb + i0 + nt * u] = v[u];
+    }
+  }
+  xgmi::link_floor(s, t0, a.seg4 * 16);
+}
+
 __global__ __launch_bounds__(WF_NT) void conv2_bwd_wino_kernel(
     int nd, const float* __restrict__ Ud,
     const float* __restrict__ a1, int batch, float* __restrict__ da1m,
     const C1Filter c1, const float* __restrict__ a1p, const float* __restrict__ dy2,
-    float* __restrict__ part2, float* __restrict__ part_db2, int nwg) {
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const XgmiStepArgs xfc) {
   // one LDS pool for either role
   __shared__ float smem[WD_SMEM > WF_SMEM_ALL ? WD_SMEM : WF_SMEM_ALL];
-  if ((int)blockIdx.x < nd) {
+  // world > 1 over xGMI: the first xfc.nfc blocks exchange + update the FC
+  // bucket (its grads are final after fc1 backward) while the conv blocks run
+  if ((int)blockIdx.x < xfc.nfc) {
+    xgmi_fc_role(xfc, reinterpret_cast<unsigned*>(smem));
+    return;
+  }
+  const int b = (int)blockIdx.x - xfc.nfc;
+  if (b < nd) {
     if (threadIdx.x >= WNT) return;
-    bwd_data_wino_block<false, false>(blockIdx.x, nd, dy2, Ud, a1, batch, da1m, FcSgd{}, c1,
-                                      nullptr, smem);
+    bwd_data_wino_block<false, false>(b, nd, dy2, Ud, a1, batch, da1m, FcSgd{}, c1, nullptr, smem);
   } else {
-    bwd_filter_wino_block<false>(blockIdx.x - nd, batch, a1p, dy2, part2, part_db2, nwg, C1Filter{},
+    bwd_filter_wino_block<false>(b - nd, batch, a1p, dy2, part2, part_db2, nwg, C1Filter{},
                                  nullptr, smem);
   }
 }
@@ -2459,11 +2540,16 @@ void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch,
 
 void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, const float* dy2,
                            int batch, float* da1m, float* part2, hipStream_t s,
-                           const C1FilterArgs* c1) {
+                           const C1FilterArgs* c1, const XgmiStepArgs* xfc) {
   const int nd = batch * 4;
   const int G = conv2_wino_filter_groups(batch);
-  conv2_bwd_wino_kernel<<<nd + 8 * G, WF_NT, 0, s>>>(nd, Ud, a1, batch, da1m, c1_args(c1), a1p,
-                                                     dy2, part2, part2 + (size_t)G * 51200, 8 * G);
+  XgmiStepArgs xa{};
+  if (xfc) {
+    xa = *xfc;
+    xgmi_fc_plan(xa, WF_NT);
+  }
+  conv2_bwd_wino_kernel<<<xa.nfc + nd + 8 * G, WF_NT, 0, s>>>(
+      nd, Ud, a1, batch, da1m, c1_args(c1), a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, xa);
 }
 
 void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,
@@ -2725,16 +2811,7 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
 // small beside whatever else the GPU runs.  Every block takes part in both
 // barriers (arrival; "reduced / done reading"), so a rank leaves the kernel
 // only when every peer has read its grads.
-constexpr int XS_UNROLL = 2;
 constexpr int XS_FC_BLOCKS = 64, XS_CONV_BLOCKS = 32;
-
-__device__ __forceinline__ float4 add4(float4 a, float4 b) {
-  a.x += b.x;
-  a.y += b.y;
-  a.z += b.z;
-  a.w += b.w;
-  return a;
-}
 
 // conv virtual block v: the flat float offset of this thread's output (conv2:
 // a float4 index into the conv2 weight, returned in *i4) or -1
@@ -2768,63 +2845,12 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, lane = tid & 63;
   float* gl = const_cast<float*>(a.g[me]);
   const float lr = *a.lr;
-  const unsigned e = xgmi::next_epoch(s, &ep);
   if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
-    xgmi::barrier(s, 0, e);
-    const long long lo = (long long)blockIdx.x * a.per4;
-    const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
-    long long t0 = xgmi::now_ticks();
-    const long long base = (long long)me * a.seg4;
-    float4* W4 = reinterpret_cast<float4*>(a.w[me]);
-    float4* M4 = reinterpret_cast<float4*>(a.mom);
-    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
-      float4 v[xgmi::kMaxRanks][XS_UNROLL], wv[XS_UNROLL], mv[XS_UNROLL];
-#pragma unroll
-      for (int u = 0; u < XS_UNROLL; ++u) {
-        const bool ok = i0 + 256 * u < hi;
-        const long long i = base + i0 + 256 * u;
-#pragma unroll
-        for (int r = 0; r < xgmi::kMaxRanks; ++r)
-          if (r < n && ok) v[r][u] = reinterpret_cast<const float4*>(a.g[r])[i];
-        if (ok) {
-          wv[u] = W4[i];
-          mv[u] = M4[i];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < XS_UNROLL; ++u) {
-        if (i0 + 256 * u >= hi) continue;
-        float4 sv = v[0][u];
-#pragma unroll
-        for (int r = 1; r < xgmi::kMaxRanks; ++r)
-          if (r < n) sv = add4(sv, v[r][u]);
-        sgd4(wv[u], mv[u], sv, a.l2, lr, a.momentum, a.gscale);
-        const long long i = base + i0 + 256 * u;
-        W4[i] = wv[u];
-        M4[i] = mv[u];
-      }
-    }
-    xgmi::link_floor(s, t0, a.seg4 * 16);
-    xgmi::barrier(s, 1, e);
-    t0 = xgmi::now_ticks();
-    for (int r = 0; r < n; ++r) {
-      if (r == me) continue;
-      const long long rb = (long long)r * a.seg4;
-      const float4* src = reinterpret_cast<const float4*>(a.w[r]);
-      for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
-        float4 v[XS_UNROLL];
-#pragma unroll
-        for (int u = 0; u < XS_UNROLL; ++u)
-          if (i0 + 256 * u < hi) v[u] = src[rb + i0 + 256 * u];
-#pragma unroll
-        for (int u = 0; u < XS_UNROLL; ++u)
-          if (i0 + 256 * u < hi) W4[rb + i0 + 256 * u] = v[u];
-      }
-    }
-    xgmi::link_floor(s, t0, a.seg4 * 16);
+    xgmi_fc_role(a, &ep);
     return;
   }
   // ---- conv parameters (replicated update)
+  const unsigned e = xgmi::next_epoch(s, &ep);
   const int cb = (int)blockIdx.x - a.nfc;
   const int nvirt = (a.wino_u ? 128 : 50) + 16 + 208;
   // this rank's slab reductions (grad_finalize_kernel forms) into its grads
@@ -2904,6 +2930,17 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   xgmi::barrier(s, 1, e);
 }
 
+void xgmi_fc_plan(XgmiStepArgs& a, int threads) {
+  const int n = a.sync.nranks;
+  if (n < 1 || a.fc4 <= 0 || a.fc4 % n) throw std::runtime_error("xgmi: FC bucket not split evenly");
+  a.seg4 = a.fc4 / n;
+  const long long unit = (long long)threads * XS_UNROLL;
+  const long long per = (a.seg4 + XS_FC_BLOCKS - 1) / XS_FC_BLOCKS;
+  a.per4 = (int)((per + unit - 1) / unit * unit);
+  // a multiple of 8: blocks after the role keep blockIdx % 8 (their XCD mapping)
+  a.nfc = (int)((a.seg4 + a.per4 - 1) / a.per4 + 7) / 8 * 8;
+}
+
 void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
   XgmiStepArgs a = in;
   const int n = a.sync.nranks;
@@ -2917,11 +2954,11 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
     throw std::runtime_error("xgmi_step: Winograd transforms need both U and Ud");
   if (!a.part2 || !a.part1 || a.ngroups <= 0 || a.nblk1 <= 0 || a.off_w2 % 4)
     throw std::runtime_error("xgmi_step: conv slabs / offsets");
-  a.seg4 = a.fc4 / n;
-  const long long unit = 256 * XS_UNROLL;
-  const long long per = (a.seg4 + XS_FC_BLOCKS - 1) / XS_FC_BLOCKS;
-  a.per4 = (int)((per + unit - 1) / unit * unit);
-  a.nfc = (int)((a.seg4 + a.per4 - 1) / a.per4);
+  if (a.fc_in_bwd) {
+    a.nfc = 0;  // the FC bucket was done by the conv2 backward launch's role blocks
+  } else {
+    xgmi_fc_plan(a, 256);
+  }
   a.ncv = XS_CONV_BLOCKS;
   xgmi_step_kernel<<<a.nfc + a.ncv, 256, 0, s>>>(a);
 }

@@ -44,7 +44,7 @@ MnistExecutor::~MnistExecutor() {
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                                     const mnist::FcSgdArgs* fc_sgd, bool factors, bool fresh,
-                                    bool fc1_dw_fused) {
+                                    bool fc1_dw_fused, const mnist::XgmiStepArgs* xfc) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
     return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, fresh);
@@ -106,7 +106,7 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
   if (p.wino && fc_sgd == nullptr) {  // bwd-data (+ conv1 filter grad) and filter grad: one launch
     mnist::launch_conv2_bwd_wino(P<const float>(p.wino_ud), P<const float>(p.a1),
                                  P<const float>(p.a1pf), P<const float>(p.dy2), B,
-                                 P<float>(p.da1m), P<float>(p.part2), s, &c1);
+                                 P<float>(p.da1m), P<float>(p.part2), s, &c1, xfc);
   } else if (p.wino) {  // the FC SGD rides in the bwd-data launch
     mnist::launch_conv2_bwd_data_wino(P<const float>(p.dy2), P<const float>(p.wino_ud),
                                       P<const float>(p.a1), B, P<float>(p.da1m), s, fc_sgd, &c1);
@@ -666,7 +666,6 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
   XgmiComm* x = xgmi_;
   const int n = x->size();
   wait_fc_params(s);
-  enqueue_fwd_bwd(s, /*finalize=*/false, nullptr, false, take_fresh(!p.bf16));
   mnist::XgmiStepArgs a;
   a.sync = x->sync();
   for (int r = 0; r < n; ++r) {
@@ -692,6 +691,14 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
     a.wino_u = P<float>(p.wino_u);
     a.wino_ud = P<float>(p.wino_ud);
   }
+  // fp32 Winograd: the FC exchange + SGD ride as the first blocks of the
+  // merged conv2 backward launch (its grads are final after fc1 backward), so
+  // the link time overlaps the conv backward; the step launch then syncs the
+  // conv parameters only
+  const bool fc_in_bwd = p.wino && !p.bf16 && xgmi_fc_in_bwd_;
+  a.fc_in_bwd = fc_in_bwd ? 1 : 0;
+  enqueue_fwd_bwd(s, /*finalize=*/false, nullptr, false, take_fresh(!p.bf16), false,
+                  fc_in_bwd ? &a : nullptr);
   mnist::launch_xgmi_step(a, s);
   if (p.bf16) shadows_stale_ = true;
 }

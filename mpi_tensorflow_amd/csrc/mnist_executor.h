@@ -76,6 +76,7 @@ struct MnistPtrs {
 
 namespace mnist {
 struct FcSgdArgs;
+struct XgmiStepArgs;
 }
 
 class MnistExecutor {
@@ -124,6 +125,9 @@ class MnistExecutor {
   // the peer-to-peer communicator of SCHED_XGMI: the flat grads and params must
   // be registered with it (XgmiComm::open_buffer / emulate_buffer)
   void set_xgmi(XgmiComm* x) { xgmi_ = x; }
+  // fp32: the FC exchange inside the conv2 backward launch (default) or in the
+  // step launch (labs)
+  void set_xgmi_fc_in_bwd(bool on) { xgmi_fc_in_bwd_ = on; }
   bool xgmi_ok() const;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
@@ -182,9 +186,12 @@ class MnistExecutor {
   // launch_sgd_step); otherwise the step derives them from the weights first
   // fc1_dw_fused: the fc1 weight gradient is formed inside this step's SGD
   // (single rank, fp32 Winograd): fc1 backward skips its dW1 role
+  // xfc (fp32 Winograd, SCHED_XGMI): the FC bucket's peer-to-peer exchange +
+  // SGD as role blocks of the merged conv2 backward launch
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
                        const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
-                       bool fresh = false, bool fc1_dw_fused = false);
+                       bool fresh = false, bool fc1_dw_fused = false,
+                       const mnist::XgmiStepArgs* xfc = nullptr);
   // the fused SGD launch applies (L2 prefix == the FC bucket, as in the
   // reference layout)
   bool fused_sgd_ok() const;
@@ -201,6 +208,7 @@ class MnistExecutor {
   void train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_xgmi(hipStream_t s);
   XgmiComm* xgmi_ = nullptr;
+  bool xgmi_fc_in_bwd_ = true;
   float defer_split_ = 0.5f;
   void wait_fc_params(hipStream_t s);
   // all-reduce (sum) of grads [lo, lo + n) on cs, over the bf16 wire if set
