@@ -134,6 +134,15 @@ struct AllReduceArgs {
   int per4 = 0;                // float4s per block per segment
   long long link_bytes = 0;    // one phase's bytes on one link (emulation floor)
   int gather_only = 0;         // skip phase 1: every rank's segment is already final
+  // momentum SGD fused into phase 1 (all_reduce_sgd): buf = the grads; the
+  // reduced segment updates w[rank] / mom there (optim::sgd_momentum_flat's
+  // forms; L2 on float4s < l2_end4), and phase 2 gathers w instead of buf
+  float* w[kMaxRanks] = {};
+  float* mom = nullptr;
+  const float* lr = nullptr;
+  float momentum = 0.f, gscale = 1.f, l2 = 0.f;
+  long long l2_end4 = 0;
+  long long* step = nullptr;  // bumped once (optional)
 };
 void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st);
 

@@ -15,6 +15,8 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
   const int n = s.nranks, me = s.rank, tid = threadIdx.x;
   const unsigned e = next_epoch(s, &ep);
   barrier(s, 0, e);
+  const bool sgd = a.mom != nullptr;
+  const float lr = sgd ? *a.lr : 0.f;
   const long long lo = (long long)blockIdx.x * a.per4;
   const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
   long long t0 = now_ticks();
@@ -43,22 +45,46 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
             acc[u].w += v[r][u].w;
           }
         const long long i = base + i0 + 256 * u;
-        if (i0 + 256 * u < hi && i < a.n4) reinterpret_cast<float4*>(a.buf[me])[i] = acc[u];
+        if (!(i0 + 256 * u < hi && i < a.n4)) continue;
+        if (sgd) {  // optim::sgd_momentum_flat_kernel's expression forms
+          float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+          float4* M4 = reinterpret_cast<float4*>(a.mom);
+          float4 wv = W4[i], gv = acc[u], mv = M4[i];
+          const float lc = i < a.l2_end4 ? a.l2 : 0.f;
+          gv.x = __builtin_fmaf(lc, wv.x, gv.x * a.gscale);
+          gv.y = __builtin_fmaf(lc, wv.y, gv.y * a.gscale);
+          gv.z = __builtin_fmaf(lc, wv.z, gv.z * a.gscale);
+          gv.w = __builtin_fmaf(lc, wv.w, gv.w * a.gscale);
+          mv.x = a.momentum * mv.x + gv.x;
+          mv.y = a.momentum * mv.y + gv.y;
+          mv.z = a.momentum * mv.z + gv.z;
+          mv.w = a.momentum * mv.w + gv.w;
+          wv.x -= lr * mv.x;
+          wv.y -= lr * mv.y;
+          wv.z -= lr * mv.z;
+          wv.w -= lr * mv.w;
+          W4[i] = wv;
+          M4[i] = mv;
+        } else {
+          reinterpret_cast<float4*>(a.buf[me])[i] = acc[u];
+        }
       }
     }
   }
   if (!a.gather_only) link_floor(s, t0, a.link_bytes);
   barrier(s, 1, e);
   t0 = now_ticks();
+  float* const* out = sgd ? a.w : a.buf;  // phase 2 gathers the updated params
   for (int r = 0; r < n; ++r) {
     if (r == me) continue;
     const long long base = (long long)r * a.seg4;
     for (long long i0 = lo + tid; i0 < hi; i0 += 256) {
       const long long i = base + i0;
       if (i < a.n4)
-        reinterpret_cast<float4*>(a.buf[me])[i] = reinterpret_cast<const float4*>(a.buf[r])[i];
+        reinterpret_cast<float4*>(out[me])[i] = reinterpret_cast<const float4*>(out[r])[i];
     }
   }
+  if (a.step && blockIdx.x == 0 && tid == 0) *a.step += 1;
   link_floor(s, t0, a.link_bytes);
   barrier(s, 2, e);
 }

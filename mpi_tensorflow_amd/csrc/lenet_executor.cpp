@@ -3,6 +3,7 @@
 #include <stdexcept>
 
 #include "kernels/mnist.h"  // optim::launch_sgd_momentum
+#include "xgmi_comm.h"
 
 template <class T>
 static inline T* P(uintptr_t v) {
@@ -50,6 +51,14 @@ void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
                        p_.momentum, P<const float>(p_.lr), P<long long>(p_.step), apply, s);
   if (apply) return;
   float* G = P<float>(p_.grads);
+  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && !p_.grad_bf16) {
+    // xGMI peer to peer: the sum of this rank's segment and its SGD in one
+    // launch on this stream, then the updated segments gathered (sharded momentum)
+    x->all_reduce_sgd(G, P<float>(p_.params), P<float>(p_.mom), (size_t)p_.total, 0, 0.f,
+                      p_.momentum, 1.0f / (float)comm->size(), P<const float>(p_.lr),
+                      P<long long>(p_.step), s);
+    return;
+  }
   if (p_.grad_bf16) {
     uint16_t* B = P<uint16_t>(p_.gb16);
     optim::launch_to_bf16(G, B, p_.total, s);

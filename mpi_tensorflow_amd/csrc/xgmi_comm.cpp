@@ -184,13 +184,33 @@ void XgmiComm::gather_segments(void* buf, size_t count, hipStream_t s) {
   launch(buf, count, true, s);
 }
 
-void XgmiComm::launch(void* recv, size_t count, bool gather_only, hipStream_t s) {
+void XgmiComm::all_reduce_sgd(float* grads, float* params, float* mom, size_t count,
+                              long long l2_end, float l2, float momentum, float gscale,
+                              const float* lr, long long* step, hipStream_t s) {
+  if (!mom || !lr || l2_end % 4) throw std::runtime_error("XgmiComm::all_reduce_sgd: arguments");
+  if (!registered(params, count * sizeof(float)))
+    throw std::runtime_error("XgmiComm::all_reduce_sgd: params not registered");
+  xgmi::AllReduceArgs a;
+  for (int r = 0; r < nranks_; ++r) a.w[r] = static_cast<float*>(peer_ptr(params, r));
+  a.mom = mom;
+  a.lr = lr;
+  a.momentum = momentum;
+  a.gscale = gscale;
+  a.l2 = l2;
+  a.l2_end4 = l2_end / 4;
+  a.step = step;
+  launch(grads, count, false, s, &a);
+}
+
+void XgmiComm::launch(void* recv, size_t count, bool gather_only, hipStream_t s,
+                      const xgmi::AllReduceArgs* sgd) {
   if (count == 0) return;
   if (count % 4) throw std::runtime_error("XgmiComm::all_reduce: count must be a multiple of 4");
   if (!ready()) throw std::runtime_error("XgmiComm: flags of some rank not mapped");
   const size_t bytes = count * sizeof(float);
   if (!registered(recv, bytes)) throw std::runtime_error("XgmiComm::all_reduce: unregistered buffer");
   xgmi::AllReduceArgs a;
+  if (sgd) a = *sgd;
   a.s = sync_;
   for (int r = 0; r < nranks_; ++r) a.buf[r] = static_cast<float*>(peer_ptr(recv, r));
   a.n4 = (long long)(count / 4);

@@ -72,6 +72,14 @@ class XgmiComm : public Collective {
   // in place, fp32: segment r (ceil(count / N) floats, in float4s) of every
   // rank's buffer becomes rank r's (the all-reduce's phase 2 alone)
   void gather_segments(void* buf, size_t count, hipStream_t s);
+  // in-place fp32 sum of the registered grads fused with the momentum SGD of
+  // the registered params: each rank updates its own segment (the momentum is
+  // sharded: gather_segments(mom) makes it whole) and gathers the others'
+  // (optim::launch_sgd_momentum's arguments; bit-identical to all_reduce +
+  // that SGD with a rank-order sum)
+  void all_reduce_sgd(float* grads, float* params, float* mom, size_t count, long long l2_end,
+                      float l2, float momentum, float gscale, const float* lr, long long* step,
+                      hipStream_t s);
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                       hipStream_t s) override;
 
@@ -84,7 +92,8 @@ class XgmiComm : public Collective {
   const Reg* find(const void* p, size_t bytes) const;
   Reg& reg_for(uintptr_t local, size_t bytes);
   void* open_handle(int r, const std::string& handle);
-  void launch(void* buf, size_t count, bool gather_only, hipStream_t s);
+  void launch(void* buf, size_t count, bool gather_only, hipStream_t s,
+              const xgmi::AllReduceArgs* sgd = nullptr);
 
   int nranks_, rank_;
   bool emulate_;

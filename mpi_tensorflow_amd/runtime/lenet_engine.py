@@ -104,10 +104,12 @@ class NativeLenetEngine:
                 raise RuntimeError("GPU grad sync needs the native RCCL communicator")
             if getattr(comm, "kind", "") == "host-staged":  # test comm: eager only
                 comm.bases = [self.grads] + ([self.gb16] if self.gb16 is not None else [])
-            if hasattr(comm, "register"):  # xGMI peer-to-peer: peers read the grads
+            self._xgmi = hasattr(comm, "register")
+            if self._xgmi:  # xGMI peer to peer: peers read the grads and params,
+                # and (to make it whole) the sharded momentum
                 if self.gb16 is not None:
                     raise ValueError("the xGMI communicator reduces fp32 grads only")
-                comm.register(self.grads)
+                comm.register(self.grads, self.params, self.mom)
             # connection setup of the collective, outside any capture
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())
@@ -122,7 +124,12 @@ class NativeLenetEngine:
         return learning_rate(s, self.n_local, self.B, self.cfg.base_lr, self.cfg.lr_decay)
 
     def sync_optimizer_state(self) -> None:
-        """Replicated optimizer state: nothing to gather."""
+        """Replicated optimizer state: nothing to gather, except over the xGMI
+        communicator, whose fused all-reduce + SGD keeps each rank's momentum
+        segment only (csrc/xgmi_comm.h all_reduce_sgd)."""
+        if self.grad_sync and getattr(self, "_xgmi", False):
+            self._native_comm.gather_segments(ptr(self.mom), self.layout.total, stream_handle())
+            torch.cuda.synchronize(self.device)
 
     def extra_state(self):
         return {}

@@ -218,6 +218,8 @@ def scenario_generic(di, model):
     from mpi_tensorflow_amd.runtime.lenet_engine import NativeLenetEngine
     from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
+    xg = model.endswith("-xgmi")  # the xGMI peer-to-peer communicator instead of shm
+    model = model[:-5] if xg else model
     fused = model == "lenet5-native"
     name = "lenet5" if fused else model
     Eng = NativeLenetEngine if fused else GenericEngine
@@ -231,14 +233,22 @@ def scenario_generic(di, model):
         return x.numpy(), y.numpy()
 
     dev = torch.device("cuda")
-    comm = ShmDeviceComm(di, comm_capacity_bytes(cfg), timeout_s=60.0)
+    if xg:
+        from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+        comm = XgmiDeviceComm(di, timeout_s=20.0)
+    else:
+        comm = ShmDeviceComm(di, comm_capacity_bytes(cfg), timeout_s=60.0)
     eng = Eng(cfg, *shard(di.rank), dev, di.rank, di.world, comm)
     assert eng.grad_sync and eng.use_graph
     eng.train(steps)
     torch.cuda.synchronize()
     assert eng.use_graph and len(eng._graphs) >= 1, "the step was not captured"
+    eng.sync_optimizer_state()
     p = eng.params.detach().cpu()
     assert replicas_identical(eng.params.detach()), "replicas diverged"
+    if xg:
+        assert comm.error() == 0, "an xgmi barrier timed out"
+        assert replicas_identical(eng.mom.detach()), "momentum replicas diverged"
     if di.rank == 0:
         ecfg = C.TrainConfig(model=name, batch_size=B, graph=False).validate()
         engs = [Eng(ecfg, *shard(r), dev, r, di.world, None) for r in range(di.world)]
@@ -264,8 +274,11 @@ def scenario_generic(di, model):
         torch.cuda.synchronize()
         q = lead.params.detach().cpu()
         assert torch.equal(p, q), f"captured {model} vs serial emulation: {(p - q).abs().max().item()}"
+        if xg:
+            mq = lead.mom.detach().cpu()
+            assert torch.equal(eng.mom.detach().cpu(), mq), "xgmi momentum vs serial emulation"
         assert np.isfinite(p.numpy()).all()
-    return f"model={model} steps={steps}"
+    return f"model={model}{'-xgmi' if xg else ''} steps={steps}"
 
 
 def main():
