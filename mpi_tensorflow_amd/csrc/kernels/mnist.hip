@@ -2959,7 +2959,9 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
   } else {
     xgmi_fc_plan(a, 256);
   }
-  a.ncv = XS_CONV_BLOCKS;
+  // one block per conv unit (latency-bound slab sums: they want the whole
+  // chip), or XS_CONV_BLOCKS looping over them when the ranks share a GPU
+  a.ncv = a.sync.lean ? XS_CONV_BLOCKS : (a.wino_u ? 128 : 50) + 16 + 208;
   xgmi_step_kernel<<<a.nfc + a.ncv, 256, 0, s>>>(a);
 }
 

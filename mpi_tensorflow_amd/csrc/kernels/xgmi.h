@@ -58,6 +58,9 @@ struct Sync {
   long long lat_ticks = 0;                    // emulated hop latency (100 MHz ticks)
   long long link_ticks_per_kb = 0;            // emulated link time per KiB per link
   long long timeout_ticks = 1000000000;       // 10 s
+  // the ranks share ONE GPU (tests): launch few spinning blocks, so a rank
+  // waiting at a barrier leaves CUs for the other ranks' kernels on the device
+  int lean = 0;
 };
 
 __device__ __forceinline__ long long now_ticks() {

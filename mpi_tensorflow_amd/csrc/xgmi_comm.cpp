@@ -215,9 +215,10 @@ void XgmiComm::launch(void* recv, size_t count, bool gather_only, hipStream_t s,
   for (int r = 0; r < nranks_; ++r) a.buf[r] = static_cast<float*>(peer_ptr(recv, r));
   a.n4 = (long long)(count / 4);
   a.seg4 = (a.n4 + nranks_ - 1) / nranks_;
-  // <= 64 blocks: a block waiting at a barrier holds its CU slot, and each
-  // block keeps 8 x 2 float4 loads per lane in flight - enough for the links
-  const long long per = (a.seg4 + 63) / 64;
+  // <= 256 blocks (64 when the ranks share a GPU: a block waiting at a
+  // barrier holds its CU slot); each keeps 8 x 2 float4 loads per lane in flight
+  const long long nb = sync_.lean ? 64 : 256;
+  const long long per = (a.seg4 + nb - 1) / nb;
   const long long per4 = std::max<long long>(512, (per + 511) / 512 * 512);
   a.per4 = (int)per4;
   a.link_bytes = a.seg4 * 16;

@@ -53,6 +53,9 @@ class XgmiComm : public Collective {
   // emulation: N - 1 local stand-ins for the local buffer (copies of it)
   void emulate_buffer(uintptr_t local, size_t bytes);
   bool ready() const;  // flags of every rank mapped
+  // the ranks share one GPU: the kernels keep their grids small (Sync::lean)
+  void set_lean(bool on) { sync_.lean = on ? 1 : 0; }
+  bool lean() const { return sync_.lean != 0; }
 
   // --- device views ---
   const xgmi::Sync& sync() const { return sync_; }

@@ -225,6 +225,10 @@ class XgmiDeviceComm(DeviceComm):
             err = e
         if not _all_ranks_ok(err is None, n):
             raise RuntimeError(f"xGMI communicator: peer flags not mappable (here: {err!r})")
+        # ranks sharing a GPU (the 2-rank tests): small grids, so a rank
+        # spinning at a barrier leaves CUs for the other ranks' kernels
+        share, _ = _auto_vote(di)
+        self._c.set_lean(bool(share))
         self.rank, self.size = di.rank, n
         self._di = di
 
