@@ -479,11 +479,14 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
       const int c = c_lo + wi % nc, ci = (wi / nc) % IC, t = wi / (nc * IC);
       cp[(t * IC + ci) * C1 + c] = s;
     }
-    if (tid >= 480 && tid < 480 + nc) {  // db1 (a wave of its own)
-      const int c = c_lo + tid - 480;
-      float sb = 0.f;
-      for (int p = 0; p < P1 * P1; ++p) sb += sm[S_T1 + 2 * (p * C1 + c)];
-      cp[W1N + c] = sb;
+    if (tid >= 448) {  // db1: wave 7 (idle above), lanes over the pixels + a wave sum
+      const int lane = tid - 448;
+      for (int c = c_lo; c < c_hi; ++c) {
+        float sb = 0.f;
+        for (int p = lane; p < P1 * P1; p += 64) sb += sm[S_T1 + 2 * (p * C1 + c)];
+        sb = wave_sum(sb);
+        if (lane == 0) cp[W1N + c] = sb;
+      }
     }
   }
 }

@@ -1915,8 +1915,17 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
   const xgmi::Sync& s = a.sync;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, nt = blockDim.x;
   const float lr = *a.lr;
+  // peer-visible bytes go through system-scope loads / stores (kernels/xgmi.h)
+  const long long fcb = a.fc4 * 16;
+  xgmi::Rsrc gr[xgmi::kMaxRanks], wr[xgmi::kMaxRanks];
+#pragma unroll
+  for (int r = 0; r < xgmi::kMaxRanks; ++r)
+    if (r < n) {
+      gr[r] = xgmi::rsrc(a.g[r], fcb);
+      wr[r] = xgmi::rsrc(a.w[r], fcb);
+    }
   const unsigned e = xgmi::next_epoch(s, ep);
-  xgmi::barrier(s, 0, e);
+  xgmi::barrier(s, 0, e, /*release=*/true);  // the grads come from fc1 backward
   const long long lo = (long long)blockIdx.x * a.per4;
   const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
   long long t0 = xgmi::now_ticks();
@@ -1928,13 +1937,13 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
 #pragma unroll
     for (int u = 0; u < XS_UNROLL; ++u) {
       const bool ok = i0 + nt * u < hi;
-      const long long i = base + i0 + nt * u;
+      const unsigned off = (unsigned)((base + i0 + nt * u) * 16);
 #pragma unroll
       for (int r = 0; r < xgmi::kMaxRanks; ++r)
-        if (r < n && ok) v[r][u] = reinterpret_cast<const float4*>(a.g[r])[i];
+        if (r < n && ok) v[r][u] = xgmi::ld4_sys(gr[r], off);
       if (ok) {
-        wv[u] = W4[i];
-        mv[u] = M4[i];
+        wv[u] = W4[base + i0 + nt * u];
+        mv[u] = M4[base + i0 + nt * u];
       }
     }
 #pragma unroll
@@ -1946,22 +1955,22 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
         if (r < n) sv = add4(sv, v[r][u]);
       sgd4(wv[u], mv[u], sv, a.l2, lr, a.momentum, a.gscale);
       const long long i = base + i0 + nt * u;
-      W4[i] = wv[u];
+      xgmi::st4_sys(wr[me], (unsigned)(i * 16), wv[u]);  // the peers gather it
       M4[i] = mv[u];
     }
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
-  xgmi::barrier(s, 1, e);
+  xgmi::barrier(s, 1, e, false);
   t0 = xgmi::now_ticks();
-  for (int r = 0; r < n; ++r) {
-    if (r == me) continue;
+#pragma unroll
+  for (int r = 0; r < xgmi::kMaxRanks; ++r) {
+    if (r >= n || r == me) continue;
     const long long rb = (long long)r * a.seg4;
-    const float4* src = reinterpret_cast<const float4*>(a.w[r]);
     for (long long i0 = lo + tid; i0 < hi; i0 += (long long)nt * XS_UNROLL) {
       float4 v[XS_UNROLL];
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
-        if (i0 + nt * u < hi) v[u] = src[rb + i0 + nt * u];
+        if (i0 + nt * u < hi) v[u] = xgmi::ld4_sys(wr[r], (unsigned)((rb + i0 + nt * u) * 16));
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
         if (i0 + nt * u < hi) W4[rb + i0 + nt * u] = v[u];
@@ -2843,7 +2852,6 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   __shared__ float wl[25 * 16];
   const xgmi::Sync& s = a.sync;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, lane = tid & 63;
-  float* gl = const_cast<float*>(a.g[me]);
   const float lr = *a.lr;
   if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
     xgmi_fc_role(a, &ep);
@@ -2853,13 +2861,21 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   const unsigned e = xgmi::next_epoch(s, &ep);
   const int cb = (int)blockIdx.x - a.nfc;
   const int nvirt = (a.wino_u ? 128 : 50) + 16 + 208;
-  // this rank's slab reductions (grad_finalize_kernel forms) into its grads
+  // every rank's conv grads, system-scope (kernels/xgmi.h): conv2 weight
+  // float4s from off_w2, scalars (conv2 bias, conv1) from the buffer start
+  const long long cbytes = 4LL * (a.off_b1 + 32);
+  xgmi::Rsrc gr[xgmi::kMaxRanks];
+#pragma unroll
+  for (int r = 0; r < xgmi::kMaxRanks; ++r)
+    if (r < n) gr[r] = xgmi::rsrc(a.g[r], cbytes);
+  // this rank's slab reductions (grad_finalize_kernel forms) into its grads,
+  // written through for the peers
   for (int v = cb; v < nvirt; v += a.ncv) {
     const XsConvItem it = xs_conv_item(a, v, tid);
     if (it.kind == 0) {
       if (it.i4 >= 0)
-        reinterpret_cast<float4*>(gl + a.off_w2)[it.i4] =
-            slab_sum4(reinterpret_cast<const float4*>(a.part2) + it.i4, a.ngroups);
+        xgmi::st4_sys(gr[me], (unsigned)(4 * a.off_w2 + 16 * it.i4),
+                      slab_sum4(reinterpret_cast<const float4*>(a.part2) + it.i4, a.ngroups));
       continue;
     }
     float sl = 0.f;
@@ -2874,15 +2890,17 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
       for (int b = lane; b < a.nblk1; b += 64) sl += a.part1[(size_t)b * 832 + o];
       sl = wave_sum(sl);
     }
-    if (it.off >= 0 && lane == 0) gl[it.off] = sl;
+    if (it.off >= 0 && lane == 0) xgmi::st_sys(gr[me], (unsigned)(4 * it.off), sl);
   }
-  xgmi::barrier(s, 0, e);
+  xgmi::barrier(s, 0, e, false);
   for (int v = cb; v < nvirt; v += a.ncv) {
     const XsConvItem it = xs_conv_item(a, v, tid);
     if (it.kind == 1) {
       if (it.off >= 0 && lane == 0) {
-        float sv = a.g[0][it.off];
-        for (int r = 1; r < n; ++r) sv += a.g[r][it.off];
+        float sv = xgmi::ld_sys(gr[0], (unsigned)(4 * it.off));
+#pragma unroll
+        for (int r = 1; r < xgmi::kMaxRanks; ++r)
+          if (r < n) sv += xgmi::ld_sys(gr[r], (unsigned)(4 * it.off));
         float* w = a.w[me] + it.off;
         sgd_elem(w, a.mom + it.off, __builtin_fmaf(0.f, *w, sv * a.gscale), lr, a.momentum);
       }
@@ -2894,10 +2912,11 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
       float4* mp = reinterpret_cast<float4*>(a.mom + a.off_w2) + it.i4;
       wv = *wp;
       float4 mv = *mp;
-      float4 sv = reinterpret_cast<const float4*>(a.g[0] + a.off_w2)[it.i4];
+      const unsigned off = (unsigned)(4 * a.off_w2 + 16 * it.i4);
+      float4 sv = xgmi::ld4_sys(gr[0], off);
 #pragma unroll
       for (int r = 1; r < xgmi::kMaxRanks; ++r)
-        if (r < n) sv = add4(sv, reinterpret_cast<const float4*>(a.g[r] + a.off_w2)[it.i4]);
+        if (r < n) sv = add4(sv, xgmi::ld4_sys(gr[r], off));
       sgd4(wv, mv, sv, 0.f, lr, a.momentum, a.gscale);
       *wp = wv;
       *mp = mv;
@@ -2927,7 +2946,7 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
     }
   }
   if (a.step && cb == 0 && tid == 0) *a.step += 1;
-  xgmi::barrier(s, 1, e);
+  xgmi::barrier(s, 1, e, false);
 }
 
 void xgmi_fc_plan(XgmiStepArgs& a, int threads) {

@@ -15,14 +15,20 @@
 // id order on every GPU, so the lowest waiting block always has its peers
 // resident (no deadlock for any grid size).
 //
-// Memory model (scoped, HIP / LLVM AMDGPU):
+// Memory model (scoped, HIP / LLVM AMDGPU).  Every byte a peer reads goes
+// through system-scope ("sc0 sc1") 16-byte buffer loads, and every byte a
+// kernel publishes to its peers goes through system-scope stores
+// (write-through): the same cache treatment the LLVM memory model gives
+// system-scope atomics, so no L2-wide fence is needed on either side (an
+// acquire fence would invalidate the whole XCD's L2 under the conv blocks that
+// share it; measured: the conv2 backward launch 31 -> 45 us with them):
 //   publish: every storing wave `s_waitcnt vmcnt(0)` -> workgroup barrier ->
-//            lane 0 SYSTEM-scope release fence (writes back this XCD's L2) ->
-//            `s_waitcnt vmcnt(0)` (MI355X_MICROARCH.md: the compiler may drop
-//            the wait after the write-back) -> relaxed system-scope flag stores
-//   consume: relaxed system-scope flag polls (bounded) -> SYSTEM-scope
-//            acquire fence -> `s_waitcnt vmcnt(0)` -> workgroup barrier ->
-//            plain loads of peer memory
+//            relaxed system-scope flag stores (data from EARLIER kernels: a
+//            system-scope release fence first, `release`);
+//            `s_waitcnt vmcnt(0)` after the fence (MI355X_MICROARCH.md: the
+//            compiler may drop the wait after the write-back)
+//   consume: relaxed system-scope flag polls (bounded) -> workgroup barrier
+//            -> system-scope loads of the peer bytes
 // Every spin is bounded: a peer that never arrives sets the error word
 // (XgmiComm::error()) and the kernel runs to its end instead of hanging.
 //
@@ -79,15 +85,20 @@ __device__ __forceinline__ unsigned next_epoch(const Sync& s, unsigned* lds) {
 }
 
 // Publishes this block's arrival at (stage, e) to every rank and waits for
-// every rank's block blockIdx.x to arrive too.  All threads of the block call it.
-__device__ __forceinline__ void barrier(const Sync& s, int stage, unsigned e) {
+// every rank's block blockIdx.x to arrive too.  All threads of the block call
+// it.  release: this block's arrival also publishes plain stores of EARLIER
+// kernels (a system-scope release fence; the kernels' own peer-visible stores
+// are system-scope stores and need none).
+__device__ __forceinline__ void barrier(const Sync& s, int stage, unsigned e, bool release) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int t = threadIdx.x;
   const int b = blockIdx.x;
   if (t < 64) {
-    if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (release) {
+      if (t == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (t < s.nranks) {
       unsigned* dst = s.emulate ? s.flags + flag_slot(stage, t, b)
                                 : s.peer_flags[t] + flag_slot(stage, s.rank, b);
@@ -106,10 +117,32 @@ __device__ __forceinline__ void barrier(const Sync& s, int stage, unsigned e) {
         while (now_ticks() - t1 < s.lat_ticks) __builtin_amdgcn_s_sleep(1);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+}
+
+// ---- system-scope ("sc0 sc1") 16 / 4-byte accesses of peer-visible memory.
+// Buffer descriptors over [base, base + bytes) (< 4 GiB), offsets in bytes.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr int kSysCpol = 1 | 16;  // sc0 | sc1: system scope
+
+__device__ __forceinline__ Rsrc rsrc(const void* base, long long bytes) {
+  const long long lim = 0xffffffffLL;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                           (int)(bytes < lim ? bytes : lim), 0x00020000);
+}
+__device__ __forceinline__ float4 ld4_sys(Rsrc r, unsigned off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kSysCpol));
+}
+__device__ __forceinline__ void st4_sys(Rsrc r, unsigned off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b128(r, 0, 0, 0)), v),
+                                         r, (int)off, 0, kSysCpol);
+}
+__device__ __forceinline__ float ld_sys(Rsrc r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, kSysCpol));
+}
+__device__ __forceinline__ void st_sys(Rsrc r, unsigned off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, kSysCpol);
 }
 
 // emulation: hold the block until `bytes` (a whole phase's bytes on ONE

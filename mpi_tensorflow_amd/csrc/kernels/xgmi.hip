@@ -13,9 +13,17 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
   __shared__ unsigned ep;
   const Sync& s = a.s;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x;
-  const unsigned e = next_epoch(s, &ep);
-  barrier(s, 0, e);
   const bool sgd = a.mom != nullptr;
+  // every peer-visible byte through system-scope loads / stores (xgmi.h)
+  Rsrc br[kMaxRanks], wr[kMaxRanks];
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r)
+    if (r < n) {
+      br[r] = rsrc(a.buf[r], a.n4 * 16);
+      if (sgd) wr[r] = rsrc(a.w[r], a.n4 * 16);
+    }
+  const unsigned e = next_epoch(s, &ep);
+  barrier(s, 0, e, /*release=*/true);  // the buffer comes from earlier kernels
   const float lr = sgd ? *a.lr : 0.f;
   const long long lo = (long long)blockIdx.x * a.per4;
   const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
@@ -30,8 +38,7 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
 #pragma unroll
         for (int u = 0; u < kAllReduceUnroll; ++u) {
           const long long i = base + i0 + 256 * u;
-          if (r < n && i0 + 256 * u < hi && i < a.n4)
-            v[r][u] = reinterpret_cast<const float4*>(a.buf[r])[i];
+          if (r < n && i0 + 256 * u < hi && i < a.n4) v[r][u] = ld4_sys(br[r], (unsigned)(i * 16));
         }
 #pragma unroll
       for (int u = 0; u < kAllReduceUnroll; ++u) {
@@ -47,9 +54,8 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
         const long long i = base + i0 + 256 * u;
         if (!(i0 + 256 * u < hi && i < a.n4)) continue;
         if (sgd) {  // optim::sgd_momentum_flat_kernel's expression forms
-          float4* W4 = reinterpret_cast<float4*>(a.w[me]);
           float4* M4 = reinterpret_cast<float4*>(a.mom);
-          float4 wv = W4[i], gv = acc[u], mv = M4[i];
+          float4 wv = reinterpret_cast<const float4*>(a.w[me])[i], gv = acc[u], mv = M4[i];
           const float lc = i < a.l2_end4 ? a.l2 : 0.f;
           gv.x = __builtin_fmaf(lc, wv.x, gv.x * a.gscale);
           gv.y = __builtin_fmaf(lc, wv.y, gv.y * a.gscale);
@@ -63,30 +69,31 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
           wv.y -= lr * mv.y;
           wv.z -= lr * mv.z;
           wv.w -= lr * mv.w;
-          W4[i] = wv;
+          st4_sys(wr[me], (unsigned)(i * 16), wv);
           M4[i] = mv;
         } else {
-          reinterpret_cast<float4*>(a.buf[me])[i] = acc[u];
+          st4_sys(br[me], (unsigned)(i * 16), acc[u]);
         }
       }
     }
   }
   if (!a.gather_only) link_floor(s, t0, a.link_bytes);
-  barrier(s, 1, e);
+  barrier(s, 1, e, false);
   t0 = now_ticks();
   float* const* out = sgd ? a.w : a.buf;  // phase 2 gathers the updated params
-  for (int r = 0; r < n; ++r) {
-    if (r == me) continue;
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r) {
+    if (r >= n || r == me) continue;
+    const Rsrc src = sgd ? wr[r] : br[r];
     const long long base = (long long)r * a.seg4;
     for (long long i0 = lo + tid; i0 < hi; i0 += 256) {
       const long long i = base + i0;
-      if (i < a.n4)
-        reinterpret_cast<float4*>(out[me])[i] = reinterpret_cast<const float4*>(out[r])[i];
+      if (i < a.n4) reinterpret_cast<float4*>(out[me])[i] = ld4_sys(src, (unsigned)(i * 16));
     }
   }
   if (a.step && blockIdx.x == 0 && tid == 0) *a.step += 1;
   link_floor(s, t0, a.link_bytes);
-  barrier(s, 2, e);
+  barrier(s, 2, e, false);
 }
 
 void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st) {

@@ -44,9 +44,11 @@ class GenericModel:
         total = sum(4 * s.numel for s in flat_order)
         nb = max(1, min(MAX_BUCKETS, -(-total // BUCKET_BYTES)))
         sized, acc = [], 0
+        ids: Dict[int, int] = {}  # dense bucket ids (a tensor larger than a bucket skips ids)
         for s in flat_order:
             b = min(nb - 1, (acc * nb) // total)
             acc += 4 * s.numel
+            b = ids.setdefault(b, len(ids))
             sized.append(ParamSpec(s.name, s.tf_name, s.shape, s.init, s.l2, bucket=b))
         self.layout = FlatLayout.build(sized)
         self.bn_channels: Dict[str, int] = self._bn()
