@@ -1902,6 +1902,10 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_filter_wino_kernel(
 // blocks of the merged conv2 backward launch (conv2_bwd_wino_kernel: the FC
 // exchange overlaps the conv backward on the other CUs).
 constexpr int XS_UNROLL = 2;
+// as role blocks of the conv2 backward launch: few, so they hand their CUs
+// back within the launch's first round of conv blocks (512 blocks = 2 exact
+// rounds on 256 CUs; every CU held longer costs a third round)
+constexpr int XS_FC_ROLE_BLOCKS = 16;
 
 __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   a.x += b.x;
@@ -1961,6 +1965,7 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
   xgmi::barrier(s, 1, e, false);
+  if (a.fc_in_bwd) return;  // the step launch gathers (xgmi_fc_gather)
   t0 = xgmi::now_ticks();
 #pragma unroll
   for (int r = 0; r < xgmi::kMaxRanks; ++r) {
@@ -1974,6 +1979,37 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
         if (i0 + nt * u < hi) W4[rb + i0 + nt * u] = v[u];
+    }
+  }
+  xgmi::link_floor(s, t0, a.seg4 * 16);
+}
+
+// The gather half on its own (fc_in_bwd: the conv2 backward launch's role
+// blocks did the exchange + SGD and passed their closing barrier, so every
+// peer's segment is final): block gb of ng copies slice gb of every other
+// rank's segment.  No barrier: a peer rewrites its segment only after the next
+// step's arrival barrier, which this rank reaches after this launch.
+__device__ void xgmi_fc_gather(const XgmiStepArgs& a, int gb, int ng) {
+  const xgmi::Sync& s = a.sync;
+  const int n = s.nranks, me = s.rank, tid = threadIdx.x;
+  const long long fcb = a.fc4 * 16;
+  const long long per = ((a.seg4 + ng - 1) / ng + 255) / 256 * 256;
+  const long long lo = (long long)gb * per, hi = lo + per < a.seg4 ? lo + per : a.seg4;
+  const long long t0 = xgmi::now_ticks();
+  float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+#pragma unroll
+  for (int r = 0; r < xgmi::kMaxRanks; ++r) {
+    if (r >= n || r == me) continue;
+    const xgmi::Rsrc wr = xgmi::rsrc(a.w[r], fcb);
+    const long long rb = (long long)r * a.seg4;
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
+      float4 v[XS_UNROLL];
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u)
+        if (i0 + 256 * u < hi) v[u] = xgmi::ld4_sys(wr, (unsigned)((rb + i0 + 256 * u) * 16));
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u)
+        if (i0 + 256 * u < hi) W4[rb + i0 + 256 * u] = v[u];
     }
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
@@ -2555,7 +2591,7 @@ void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, c
   XgmiStepArgs xa{};
   if (xfc) {
     xa = *xfc;
-    xgmi_fc_plan(xa, WF_NT);
+    xgmi_fc_plan(xa, WF_NT, XS_FC_ROLE_BLOCKS);
   }
   conv2_bwd_wino_kernel<<<xa.nfc + nd + 8 * G, WF_NT, 0, s>>>(
       nd, Ud, a1, batch, da1m, c1_args(c1), a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, xa);
@@ -2853,13 +2889,17 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   const xgmi::Sync& s = a.sync;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, lane = tid & 63;
   const float lr = *a.lr;
+  if (a.fc_in_bwd && (int)blockIdx.x < a.ngather) {  // ---- the FC gather
+    xgmi_fc_gather(a, blockIdx.x, a.ngather);
+    return;
+  }
   if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
     xgmi_fc_role(a, &ep);
     return;
   }
   // ---- conv parameters (replicated update)
   const unsigned e = xgmi::next_epoch(s, &ep);
-  const int cb = (int)blockIdx.x - a.nfc;
+  const int cb = (int)blockIdx.x - (a.fc_in_bwd ? a.ngather : a.nfc);
   const int nvirt = (a.wino_u ? 128 : 50) + 16 + 208;
   // every rank's conv grads, system-scope (kernels/xgmi.h): conv2 weight
   // float4s from off_w2, scalars (conv2 bias, conv1) from the buffer start
@@ -2949,12 +2989,12 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   xgmi::barrier(s, 1, e, false);
 }
 
-void xgmi_fc_plan(XgmiStepArgs& a, int threads) {
+void xgmi_fc_plan(XgmiStepArgs& a, int threads, int max_blocks) {
   const int n = a.sync.nranks;
   if (n < 1 || a.fc4 <= 0 || a.fc4 % n) throw std::runtime_error("xgmi: FC bucket not split evenly");
   a.seg4 = a.fc4 / n;
   const long long unit = (long long)threads * XS_UNROLL;
-  const long long per = (a.seg4 + XS_FC_BLOCKS - 1) / XS_FC_BLOCKS;
+  const long long per = (a.seg4 + max_blocks - 1) / max_blocks;
   a.per4 = (int)((per + unit - 1) / unit * unit);
   // a multiple of 8: blocks after the role keep blockIdx % 8 (their XCD mapping)
   a.nfc = (int)((a.seg4 + a.per4 - 1) / a.per4 + 7) / 8 * 8;
@@ -2974,14 +3014,19 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
   if (!a.part2 || !a.part1 || a.ngroups <= 0 || a.nblk1 <= 0 || a.off_w2 % 4)
     throw std::runtime_error("xgmi_step: conv slabs / offsets");
   if (a.fc_in_bwd) {
-    a.nfc = 0;  // the FC bucket was done by the conv2 backward launch's role blocks
+    // the exchange + SGD ran in the conv2 backward launch; this one gathers
+    a.fc4 = in.fc4;
+    a.seg4 = a.fc4 / n;
+    a.nfc = 0;
+    a.ngather = a.sync.lean ? 16 : 64;
   } else {
-    xgmi_fc_plan(a, 256);
+    xgmi_fc_plan(a, 256, XS_FC_BLOCKS);
+    a.ngather = 0;
   }
   // one block per conv unit (latency-bound slab sums: they want the whole
   // chip), or XS_CONV_BLOCKS looping over them when the ranks share a GPU
   a.ncv = a.sync.lean ? XS_CONV_BLOCKS : (a.wino_u ? 128 : 50) + 16 + 208;
-  xgmi_step_kernel<<<a.nfc + a.ncv, 256, 0, s>>>(a);
+  xgmi_step_kernel<<<a.nfc + a.ngather + a.ncv, 256, 0, s>>>(a);
 }
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
