@@ -243,7 +243,7 @@ def run(a, di, device, wd) -> int:
             if (a.comm == "auto" and not a.no_xgmi and a.model == "mnist_cnn"
                     and getattr(comm, "kind", "") == "rccl-native"):
                 from mpi_tensorflow_amd.parallel.comm import make_xgmi_comm
-                xcomm = make_xgmi_comm(di, device, min(60.0, a.collective_timeout_s))
+                xcomm = make_xgmi_comm(di, device, min(20.0, a.collective_timeout_s))
         if force and a.xgmi_emulate:
             from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
             f = [float(v) for v in a.xgmi_emulate.split(",")]

@@ -668,6 +668,7 @@ PYBIND11_MODULE(_C, m) {
       .def("emulate_buffer", &XgmiComm::emulate_buffer)
       .def("ready", &XgmiComm::ready)
       .def("set_lean", &XgmiComm::set_lean)
+      .def("emulate_dead_rank", &XgmiComm::emulate_dead_rank)
       .def_property_readonly("lean", &XgmiComm::lean)
       .def("registered", [](const XgmiComm& c, uintptr_t p, size_t bytes) {
         return c.registered(reinterpret_cast<const void*>(p), bytes);

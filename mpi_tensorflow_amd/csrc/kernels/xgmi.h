@@ -67,6 +67,9 @@ struct Sync {
   // the ranks share ONE GPU (tests): launch few spinning blocks, so a rank
   // waiting at a barrier leaves CUs for the other ranks' kernels on the device
   int lean = 0;
+  // emulation, failure injection: this virtual rank never arrives (its flag
+  // slots stay unwritten), so every barrier times out (-1: none)
+  int dead_rank = -1;
 };
 
 __device__ __forceinline__ long long now_ticks() {
@@ -102,10 +105,15 @@ __device__ __forceinline__ void barrier(const Sync& s, int stage, unsigned e, bo
     if (t < s.nranks) {
       unsigned* dst = s.emulate ? s.flags + flag_slot(stage, t, b)
                                 : s.peer_flags[t] + flag_slot(stage, s.rank, b);
-      __hip_atomic_store(dst, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (!(s.emulate && t == s.dead_rank))
+        __hip_atomic_store(dst, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const unsigned* src = s.flags + flag_slot(stage, t, b);
       const long long t0 = now_ticks();
-      while ((int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      // fail fast: once any barrier of this communicator timed out, later ones
+      // do not wait again (the caller sees the sticky error and drops the path)
+      const bool failed = __hip_atomic_load(s.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+      while (!failed &&
+             (int)(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
         if (now_ticks() - t0 > s.timeout_ticks) {
           __hip_atomic_fetch_or(s.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;

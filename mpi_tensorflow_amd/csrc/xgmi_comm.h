@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <map>
+#include <stdexcept>
 #include <string>
 #include <utility>
 #include <vector>
@@ -55,6 +56,11 @@ class XgmiComm : public Collective {
   bool ready() const;  // flags of every rank mapped
   // the ranks share one GPU: the kernels keep their grids small (Sync::lean)
   void set_lean(bool on) { sync_.lean = on ? 1 : 0; }
+  // emulation, failure injection: virtual rank r never arrives at a barrier
+  void emulate_dead_rank(int r) {
+    if (!emulate_) throw std::runtime_error("XgmiComm: dead-rank injection needs emulation");
+    sync_.dead_rank = r;
+  }
   bool lean() const { return sync_.lean != 0; }
 
   // --- device views ---

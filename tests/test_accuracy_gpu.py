@@ -7,6 +7,8 @@ shows up as an accuracy gap.  All three runs share the data, the init and the
 dropout stream; they differ only in rounding, so the tolerance covers the
 trajectory drift that rounding alone causes (docs/ACCURACY.md)."""
 
+import os
+
 import pytest
 import torch
 
@@ -120,10 +122,11 @@ def test_resnet18_bf16_tracks_fp32_loss_curve(cuda_dev):
 
 
 # ------------------------------------------- ResNet-18 vs a PyTorch oracle
-RESNET_ORACLE_STEPS = 600
+RESNET_ORACLE_STEPS = 1500
 RESNET_ORACLE_ROWS, RESNET_ORACLE_TEST = 4096, 1024
-# held-out accuracy gap to the oracle, points
-RESNET_ORACLE_TOL = {"fp32": 1.5, "bf16": 2.5}
+# held-out accuracy gap to the oracle, points (at 1,500 steps,
+# where the oracle itself has settled)
+RESNET_ORACLE_TOL = {"fp32": 1.0, "bf16": 1.5}
 
 
 @pytest.fixture(scope="module")
@@ -152,15 +155,17 @@ def _resnet_run(cuda_dev, task, dtype, oracle=False):
     return acc, loss
 
 
-# The oracle's own held-out accuracy after 600 steps moves with the summation
-# order of its MIOpen convolutions (not bit-reproducible from box to box):
-# 88.38, 86.04, 88.67, 89.75 % over four runs of the same code.  The native
-# engines are deterministic, so the pin compares them with the MEAN of those
-# oracle runs instead of one live oracle run (which made the test flaky and
-# cost ~100 s); scripts/resnet_oracle_lab.py re-measures it.  At 1000 / 1500
-# steps the oracle settles (90.72-91.21 / 90.82-91.02 %) and the native engines
-# land within 0.9 (fp32) and 0.5 (bf16) points of it (docs/ACCURACY.md).
-RESNET_ORACLE_RUNS = (88.38, 86.04, 88.67, 89.75)
+# The oracle's (GenericEngine(oracle=True): F.conv2d / F.batch_norm autograd in
+# fp32) held-out accuracy moves with the summation order of its MIOpen
+# convolutions, which is not reproducible even between two runs on one box;
+# the native engines are deterministic.  The pin therefore compares them with
+# the MEAN of recorded oracle runs at RESNET_ORACLE_STEPS (same task, init,
+# batch order; scripts/resnet_oracle_lab.py --steps 1000,1500):
+#   round 4 (closing build, one box):        91.02, 90.82 %
+#   round 5 (scripts/sessions/r5_s5.steps, one box):  90.43, 90.33 %
+# spread 0.69 points, mean 90.65 %.  MTA_LIVE_ORACLE=1 also runs the oracle
+# live (test_resnet18_live_oracle_within_recorded_spread, ~1 min).
+RESNET_ORACLE_RUNS = (91.02, 90.82, 90.43, 90.33)
 
 
 @pytest.fixture(scope="module")
@@ -181,3 +186,15 @@ def test_resnet18_native_matches_torch_oracle_accuracy(cuda_dev, resnet_task, re
     print(f"resnet18 native {dtype}: held-out {acc:.2f}% (oracle {resnet_oracle_acc:.2f}%), "
           f"last loss {loss:.3f}")
     assert abs(acc - resnet_oracle_acc) <= RESNET_ORACLE_TOL[dtype]
+
+
+@pytest.mark.skipif(os.environ.get("MTA_LIVE_ORACLE") != "1",
+                    reason="opt-in (MTA_LIVE_ORACLE=1): a live ResNet-18 oracle run")
+def test_resnet18_live_oracle_within_recorded_spread(cuda_dev, resnet_task, resnet_oracle_acc):
+    """A live run of the PyTorch-op oracle lands within 0.5 points of the
+    recorded runs' range (its data, init and batch-order plumbing - shared
+    with the native engines - still produce the recorded task)."""
+    acc, _ = _resnet_run(cuda_dev, resnet_task, "fp32", oracle=True)
+    lo, hi = min(RESNET_ORACLE_RUNS), max(RESNET_ORACLE_RUNS)
+    print(f"resnet18 oracle live: {acc:.2f}% (recorded {lo:.2f}-{hi:.2f}%)")
+    assert lo - 0.5 <= acc <= hi + 0.5

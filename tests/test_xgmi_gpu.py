@@ -71,3 +71,31 @@ def test_xgmi_emulated_eight_ranks_trains(cuda_dev):
     assert comm.error() == 0
     assert int(eng.step_dev.item()) == 10
     assert torch.isfinite(eng.params).all() and not torch.equal(eng.params, p0)
+
+
+@pytest.mark.gpu
+def test_xgmi_missing_peer_times_out_and_fails_fast(cuda_dev):
+    """Failure detection: a peer that never arrives makes the barrier time out
+    (bounded spin), the kernel completes and sets the sticky error bit, and
+    every later collective of that communicator skips the wait (fail fast)
+    instead of waiting the timeout again - no GPU hang."""
+    import time
+
+    from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+
+    comm = XgmiDeviceComm.emulated(4, lat_us=0.0, link_gbps=0.0, timeout_s=0.3)
+    comm.native_handle.emulate_dead_rank(2)
+    t = torch.ones(1 << 16, device=cuda_dev)
+    comm.register(t)
+    t0 = time.perf_counter()
+    comm.all_reduce_(t)
+    torch.cuda.synchronize()
+    first = time.perf_counter() - t0
+    assert comm.error() == 1
+    t0 = time.perf_counter()
+    for _ in range(5):
+        comm.all_reduce_(t)
+    torch.cuda.synchronize()
+    later = time.perf_counter() - t0
+    print(f"xgmi dead peer: first collective {first * 1e3:.0f} ms, next five {later * 1e3:.1f} ms")
+    assert first >= 0.25 and later < 0.25
