@@ -547,8 +547,24 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
     const int woff = layer == 0 ? o.f1w : (layer == 1 ? o.f2w : o.f3w);
     const int boff = layer == 0 ? o.f1b : (layer == 1 ? o.f2b : o.f3b);
     const int i0 = tile * UT;
-    // thread -> (row i0 + r, columns j = c, c + 32, c + 64, c + 96) ; r < 16 (tid >> 5... )
-    const int r = tid >> 4, c0 = tid & 15;  // 16 rows x 16 column lanes, 8 columns each
+    // thread -> (row i0 + r, columns j = c0 + 16 u); 16 rows x 16 column lanes, 8 columns each
+    const int r = tid >> 4, c0 = tid & 15;
+    // the SGD operands of this thread's weights are independent of the
+    // gradient: issued first, they arrive under the staging and the products
+    float wv[8], mv[8], bw[8], bm[8];
+    if (APPLY) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = c0 + 16 * u;
+        const bool ok = i0 + r < nin && j < nout;
+        const int wi = woff + (i0 + r) * nout + j;
+        wv[u] = ok ? w[wi] : 0.f;
+        mv[u] = ok ? m[wi] : 0.f;
+        const bool bok = tile == 0 && r == 0 && j < nout;
+        bw[u] = bok ? w[boff + j] : 0.f;
+        bm[u] = bok ? m[boff + j] : 0.f;
+      }
+    }
     float acc[8], bacc[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc[u] = bacc[u] = 0.f;
@@ -587,14 +603,29 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int j = c0 + 16 * u;
-        if (j < nout) apply_one<APPLY>(w, g, m, woff + (i0 + r) * nout + j, acc[u], mu, lr);
+        if (j >= nout) continue;
+        const int wi = woff + (i0 + r) * nout + j;
+        if (APPLY) {
+          const float mn = mu * mv[u] + acc[u];
+          m[wi] = mn;
+          w[wi] = wv[u] - lr * mn;
+        } else {
+          g[wi] = acc[u];
+        }
       }
     }
     if (tile == 0 && r == 0) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int j = c0 + 16 * u;
-        if (j < nout) apply_one<APPLY>(w, g, m, boff + j, bacc[u], mu, lr);
+        if (j >= nout) continue;
+        if (APPLY) {
+          const float mn = mu * bm[u] + bacc[u];
+          m[boff + j] = mn;
+          w[boff + j] = bw[u] - lr * mn;
+        } else {
+          g[boff + j] = bacc[u];
+        }
       }
     }
     return;
@@ -608,14 +639,25 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
   else if (e < W1N + 8) return;
   else if (e < W1N + 8 + W2N) dst = o.c2w + (e - W1N - 8);
   else dst = o.c2b + (e - W1N - 8 - W2N);
+  float wd = 0.f, md = 0.f;
+  if (APPLY) {  // SGD operands first (independent of the gradient)
+    wd = w[dst];
+    md = m[dst];
+  }
   float s = 0.f;
-  for (int n0 = 0; n0 < batch; n0 += 32) {  // 32 image partials in flight, summed in order
-    float v[32];
+  for (int n0 = 0; n0 < batch; n0 += 64) {  // 64 image partials in flight, summed in order
+    float v[64];
 #pragma unroll
-    for (int u = 0; u < 32; ++u)
+    for (int u = 0; u < 64; ++u)
       v[u] = n0 + u < batch ? convp[(size_t)(n0 + u) * CONVP_STRIDE + e] : 0.f;
 #pragma unroll
-    for (int u = 0; u < 32; ++u) s += v[u];
+    for (int u = 0; u < 64; ++u) s += v[u];
+  }
+  if (APPLY) {
+    const float mn = mu * md + s;
+    m[dst] = mn;
+    w[dst] = wd - lr * mn;
+    return;
   }
   apply_one<APPLY>(w, g, m, dst, s, mu, lr);
 }
