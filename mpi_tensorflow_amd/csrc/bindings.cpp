@@ -292,16 +292,6 @@ PYBIND11_MODULE(_C, m) {
                                P<long long>(step_ptr), S(s));
     check_launch();
   });
-  o.def("flag_signal", [](uintptr_t word, uintptr_t s) {
-    optim::launch_flag_signal(P<unsigned>(word), S(s));
-    check_launch();
-  });
-  o.def("flag_wait", [](uintptr_t word, uintptr_t expect, uintptr_t error, double timeout_s,
-                        uintptr_t s) {
-    optim::launch_flag_wait(P<const unsigned>(word), P<unsigned>(expect), P<unsigned>(error),
-                            timeout_s, S(s));
-    check_launch();
-  });
   o.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t s) {
     optim::launch_to_bf16(P<const float>(x), P<uint16_t>(y), n, S(s));
     check_launch();

@@ -264,10 +264,4 @@ void launch_to_bf16(const float* x, uint16_t* y, long long n, hipStream_t s);
 void launch_from_bf16(const uint16_t* x, float* y, long long n, hipStream_t s);
 // *out = replica fingerprint of n raw 32-bit words (sgd.hip hash_words_kernel)
 void launch_hash_words(const uint32_t* x, long long n, unsigned long long* out, hipStream_t s);
-// stream hand-off through a device counter (streamflag.hip): signal adds 1;
-// wait bumps *expect and polls until *word reaches it (bounded: timeout_s,
-// then *error |= 1 and the stream goes on)
-void launch_flag_signal(unsigned* word, hipStream_t s);
-void launch_flag_wait(const unsigned* word, unsigned* expect, unsigned* error, double timeout_s,
-                      hipStream_t s);
 }  // namespace optim

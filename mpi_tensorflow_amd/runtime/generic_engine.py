@@ -174,10 +174,7 @@ class GenericEngine:
         if self.wcache is not None:
             self.wcache.refresh()
             self._wfresh = True
-        gscale = self._forward_backward()
-        if self.bucketer is not None:
-            self.bucketer.join()
-        return gscale
+        return self._forward_backward()
 
     def _forward_backward(self) -> float:
         C_ = self._C
@@ -256,8 +253,6 @@ class GenericEngine:
                 with torch.cuda.graph(g):
                     for _ in range(n):
                         self._step_gpu()
-                    if self.bucketer is not None:  # the comm stream rejoins inside the capture
-                        self.bucketer.join()
             except RuntimeError as e:  # keep training eagerly rather than fail the run
                 print(f"[rank {self.rank}] hipGraph capture failed ({e}); using eager launches",
                       flush=True)
@@ -282,8 +277,6 @@ class GenericEngine:
         with torch.cuda.stream(s):
             for _ in range(n):
                 self._step_gpu()
-            if self.bucketer is not None:
-                self.bucketer.join()
         torch.cuda.current_stream().wait_stream(s)
         self._warm = True
         self.step += n
@@ -321,8 +314,6 @@ class GenericEngine:
         if not self.use_graph:
             for _ in range(left):
                 self._step_gpu()
-            if self.bucketer is not None:
-                self.bucketer.join()
         else:
             G = self.graph_steps
             full, rem = divmod(left, G)
@@ -340,8 +331,6 @@ class GenericEngine:
             else:
                 for _ in range(rem):  # remainder eagerly (avoids capturing odd sizes)
                     self._step_gpu()
-                if self.bucketer is not None:
-                    self.bucketer.join()
         self.step += left
 
     # ------------------------------------------------------------------ eval
