@@ -91,6 +91,9 @@ def parse(argv=None):
                     help="what the prewarm runs: forward-only test-set passes (eval), or "
                          "training-graph replays on snapshotted state that is restored "
                          "afterwards (train; engines with prewarm_train, else eval)")
+    ap.add_argument("--xgmi-fc-in-step", action="store_true",
+                    help="lab: the xGMI FC exchange in the step launch instead of role blocks of "
+                         "the conv2 backward launch")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="lenet5 / resnet18: target gradient bytes per all-reduce bucket (MiB; "
                          "default models/generic.py BUCKET_BYTES)")
@@ -266,6 +269,8 @@ def run(a, di, device, wd) -> int:
             shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
             eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
                               force_sync=force, xcomm=xcomm)
+            if a.xgmi_fc_in_step and hasattr(eng, "exe"):
+                eng.exe.set_xgmi_fc_in_bwd(False)
             test_x, test_y = shard.test_x, shard.test_y
         else:
             from mpi_tensorflow_amd.models import generic as GM
