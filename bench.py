@@ -62,7 +62,7 @@ def parse(argv=None):
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto",
                     choices=("auto", "buckets", "sharded", "split", "factors", "serial", "defer",
-                             "xgmi"))
+                             "xgmi", "xgmi-step"))
     ap.add_argument("--defer-split", type=float, default=0.5,
                     help="defer schedule: fraction of the FC bucket reduced under the conv backward")
     ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "xgmi", "torch"),
@@ -91,9 +91,6 @@ def parse(argv=None):
                     help="what the prewarm runs: forward-only test-set passes (eval), or "
                          "training-graph replays on snapshotted state that is restored "
                          "afterwards (train; engines with prewarm_train, else eval)")
-    ap.add_argument("--xgmi-fc-in-step", action="store_true",
-                    help="lab: the xGMI FC exchange in the step launch instead of role blocks of "
-                         "the conv2 backward launch")
     ap.add_argument("--bucket-mb", type=float, default=None,
                     help="lenet5 / resnet18: target gradient bytes per all-reduce bucket (MiB; "
                          "default models/generic.py BUCKET_BYTES)")
@@ -269,8 +266,6 @@ def run(a, di, device, wd) -> int:
             shard = load_mnist_shard(di.rank, N, synthetic=True, seed=cfg.seed)
             eng = make_engine(cfg, shard.train_x, shard.train_y, device, di.rank, N, comm,
                               force_sync=force, xcomm=xcomm)
-            if a.xgmi_fc_in_step and hasattr(eng, "exe"):
-                eng.exe.set_xgmi_fc_in_bwd(False)
             test_x, test_y = shard.test_x, shard.test_y
         else:
             from mpi_tensorflow_amd.models import generic as GM

@@ -67,7 +67,8 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # compute stream over a second communicator
 # "xgmi" = the peer-to-peer xGMI communicator's fused sync + SGD launch (MNIST,
 # csrc/xgmi_comm.h; one node)
-SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer", "xgmi")
+SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer", "xgmi",
+                  "xgmi-step")
 # device communicator (world > 1): "auto" = native RCCL when every rank has a
 # GPU of its own, the shared-memory host-staged communicator when ranks share
 # GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",

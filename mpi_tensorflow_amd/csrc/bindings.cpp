@@ -812,6 +812,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_SERIAL") = (int)MnistExecutor::SCHED_SERIAL;
   m.attr("MnistExecutor").attr("SCHED_DEFER") = (int)MnistExecutor::SCHED_DEFER;
   m.attr("MnistExecutor").attr("SCHED_XGMI") = (int)MnistExecutor::SCHED_XGMI;
+  m.attr("MnistExecutor").attr("SCHED_XGMI_STEP") = (int)MnistExecutor::SCHED_XGMI_STEP;
 
   // ----------------------------------------------------------------- IDX
   // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())

@@ -3018,9 +3018,11 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
     a.fc4 = in.fc4;
     a.seg4 = a.fc4 / n;
     a.nfc = 0;
-    a.ngather = a.sync.lean ? 16 : 64;
+    a.ngather = a.sync.lean ? 16 : 256;
   } else {
-    xgmi_fc_plan(a, 256, XS_FC_BLOCKS);
+    // latency-bound loads when the links are fast: many blocks (few when the
+    // ranks share a GPU)
+    xgmi_fc_plan(a, 256, a.sync.lean ? XS_FC_BLOCKS : 4 * XS_FC_BLOCKS);
     a.ngather = 0;
   }
   // one block per conv unit (latency-bound slab sums: they want the whole

@@ -295,7 +295,7 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
       sched != SCHED_FACTORS && sched != SCHED_SERIAL && sched != SCHED_DEFER &&
-      sched != SCHED_XGMI)
+      sched != SCHED_XGMI && sched != SCHED_XGMI_STEP)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -349,7 +349,7 @@ bool MnistExecutor::fused_sgd_ok() const { return p_.l2_end == p_.bucket1; }
 
 void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                Collective* comm2) {
-  if (sched_ == SCHED_XGMI && xgmi_ok()) {  // the peer-to-peer communicator, no comm stream
+  if ((sched_ == SCHED_XGMI || sched_ == SCHED_XGMI_STEP) && xgmi_ok()) {  // no comm stream
     train_step_xgmi(s);
     return;
   }
@@ -695,7 +695,7 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
   // merged conv2 backward launch (its grads are final after fc1 backward), so
   // the link time overlaps the conv backward; the step launch then syncs the
   // conv parameters only
-  const bool fc_in_bwd = p.wino && !p.bf16 && xgmi_fc_in_bwd_;
+  const bool fc_in_bwd = p.wino && !p.bf16 && xgmi_fc_in_bwd_ && sched_ == SCHED_XGMI;
   a.fc_in_bwd = fc_in_bwd ? 1 : 0;
   enqueue_fwd_bwd(s, /*finalize=*/false, nullptr, false, take_fresh(!p.bf16), false,
                   fc_in_bwd ? &a : nullptr);
@@ -705,7 +705,7 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
 
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {
   wait_fc_params(s);
-  if (sched_ == SCHED_XGMI && xgmi_ok()) {  // the FC momentum segments (registered)
+  if ((sched_ == SCHED_XGMI || sched_ == SCHED_XGMI_STEP) && xgmi_ok()) {  // FC momentum segments
     xgmi_->gather_segments(P<float>(p_.mom), (size_t)p_.bucket1, s);
     return;
   }

@@ -119,14 +119,22 @@ class MnistExecutor {
   //                      peer's memory, updates those parameters, gathers the
   //                      other segments back, and updates the (replicated)
   //                      conv parameters from the summed slab reductions (see
-  //                      train_step_xgmi, mnist.h XgmiStepArgs).
+  //                      train_step_xgmi, mnist.h XgmiStepArgs).  fp32: the
+  //                      FC exchange + SGD ride as role blocks of the conv2
+  //                      backward launch (overlapping its link time with the
+  //                      conv backward);
+  //   SCHED_XGMI_STEP  - the same with the whole FC exchange in the step
+  //                      launch (no CUs taken from the conv backward: its 512
+  //                      blocks are 2 exact rounds on 256 CUs, role blocks add a
+  //                      third; the auto-tune picks by the real link speed).
   static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
-                       SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5, SCHED_XGMI = 6;
+                       SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5, SCHED_XGMI = 6,
+                       SCHED_XGMI_STEP = 7;
   // the peer-to-peer communicator of SCHED_XGMI: the flat grads and params must
   // be registered with it (XgmiComm::open_buffer / emulate_buffer)
   void set_xgmi(XgmiComm* x) { xgmi_ = x; }
-  // fp32: the FC exchange inside the conv2 backward launch (default) or in the
-  // step launch (labs)
+  // fp32 SCHED_XGMI: the FC exchange inside the conv2 backward launch
+  // (default) or in the step launch (= SCHED_XGMI_STEP; labs)
   void set_xgmi_fc_in_bwd(bool on) { xgmi_fc_in_bwd_ = on; }
   bool xgmi_ok() const;
   void set_schedule(int sched);

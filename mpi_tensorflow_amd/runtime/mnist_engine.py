@@ -358,6 +358,8 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_SERIAL
         if name == "defer" and self.exe.defer_ok():
             return E.SCHED_DEFER
+        if name == "xgmi-step" and self.exe.xgmi_ok():
+            return E.SCHED_XGMI_STEP
         if (name == "xgmi" or self.comm_is_xgmi) and self.exe.xgmi_ok():
             return E.SCHED_XGMI
         if self.comm_is_xgmi:
@@ -381,7 +383,8 @@ class NativeMnistEngine(MnistEngineBase):
         E = self._C.MnistExecutor
         return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
                 E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial",
-                E.SCHED_DEFER: "defer", E.SCHED_XGMI: "xgmi"}.get(self.exe.schedule,
+                E.SCHED_DEFER: "defer", E.SCHED_XGMI: "xgmi",
+                E.SCHED_XGMI_STEP: "xgmi-step"}.get(self.exe.schedule,
                                                                            "buckets")
 
     def sync_optimizer_state(self) -> None:
@@ -424,12 +427,13 @@ class NativeMnistEngine(MnistEngineBase):
     def _tune_candidates(self):
         E = self._C.MnistExecutor
         n = self._native_comm.size
-        if self.comm_is_xgmi:  # no comm stream: the fused launch or the plain all-reduce
-            return ([(E.SCHED_XGMI, "xgmi")] if self.exe.xgmi_ok() else []) + [
-                (E.SCHED_SERIAL, "serial")]
+        xg = []
+        if self.exe.xgmi_ok():  # fp32: the FC exchange in the conv2 backward, or in the step launch
+            xg = [(E.SCHED_XGMI, "xgmi")] + ([] if self.bf16 else [(E.SCHED_XGMI_STEP, "xgmi-step")])
+        if self.comm_is_xgmi:  # no comm stream: the fused launches or the plain all-reduce
+            return xg + [(E.SCHED_SERIAL, "serial")]
         cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SERIAL, "serial")]
-        if self.xcomm is not None and self.exe.xgmi_ok():
-            cands.append((E.SCHED_XGMI, "xgmi"))
+        cands += xg
         if self.exe.sharded_ok(n):
             cands.append((E.SCHED_SHARDED_FC, "sharded"))
         # the factor schedule forms the FC gradients in another summation
@@ -481,7 +485,7 @@ class NativeMnistEngine(MnistEngineBase):
                 continue
             g.replay()
             torch.cuda.synchronize(self.device)
-            if sched == E.SCHED_XGMI and not self._xgmi_healthy():
+            if sched in (E.SCHED_XGMI, E.SCHED_XGMI_STEP) and not self._xgmi_healthy():
                 self.tune_log[name] = None  # a peer barrier timed out: never pick it
                 continue
             t0 = torch.cuda.Event(enable_timing=True)

@@ -88,7 +88,9 @@ def test_bench_two_ranks_xgmi_peer_to_peer(cuda_dev, model, dtype):
     assert c["comm"] == "xgmi-p2p" and c["comm_nranks"] == 2 and c["replicas_identical"] is True
     if model == "mnist_cnn":
         tune = c["sync_tune_us_per_step"]
-        assert tune and set(tune) == {"xgmi", "serial"} and None not in tune.values(), tune
+        # fp32 tunes the FC exchange placement too (conv2 backward / step launch)
+        want = {"xgmi", "serial"} | ({"xgmi-step"} if dtype == "fp32" else set())
+        assert tune and set(tune) == want and None not in tune.values(), tune
         assert lines[0]["final_test_accuracy"] > 50.0
 
 
@@ -146,3 +148,17 @@ def test_mpipy_torchrun_reference_quirks_root_only(cuda_dev, tmp_path):
                        "--sync-every", "50")
     assert s["world"] == 2 and s["steps"] == 151
     assert "0  process at  100 with test error:" in out
+
+
+@pytest.mark.parametrize("sync", ["grad", "param_avg"])
+def test_mpipy_torchrun_xgmi_comm(cuda_dev, tmp_path, sync):
+    """`mpipy.py --comm xgmi` through torchrun: the reference's script API on
+    the peer-to-peer communicator - per-step gradient sync (the fused xGMI
+    schedule, tuned against its plain all-reduce) or the reference's periodic
+    weight averaging (mpipy.py:87-91) over the xGMI all-reduce; replicas
+    checked at every eval event and at the end."""
+    extra = ["--sync", sync] + (["--sync-every", "50"] if sync == "param_avg" else [])
+    out, s, _ = _mpipy(tmp_path, f"xgmi-{sync}", "--comm", "xgmi", "--eval-every", "50", *extra)
+    assert s["world"] == 2 and s["steps"] == 151 and s["comm"] == "xgmi-p2p"
+    if sync == "grad":
+        assert s["sync_schedule"] in ("xgmi", "serial"), s
