@@ -193,6 +193,10 @@ PYBIND11_MODULE(_C, m) {
   k.def("fc1_part_floats", &mnist::fc1_part_floats);
   k.def("part2_floats_bf16", &mnist16::part2_floats);
   k.def("conv2_filter_groups_bf16", &mnist16::conv2_filter_groups);
+  k.def("conv2_bwd_conv1_rows_bf16", &mnist16::conv2_bwd_conv1_rows);
+  k.def("set_conv2_bwd_prof_bf16", [](uintptr_t p) {
+    mnist16::set_conv2_bwd_prof(reinterpret_cast<unsigned long long*>(p));
+  });
   k.def("fc1_fwd_train", [](uintptr_t a2, uintptr_t w, int batch, uintptr_t part, uintptr_t s) {
     mnist::launch_fc1_fwd_train(P<const float>(a2), P<const float>(w), batch, P<float>(part), S(s));
     check_launch();

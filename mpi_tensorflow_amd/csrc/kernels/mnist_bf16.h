@@ -60,4 +60,16 @@ void launch_conv2_bwd_filter(const uint16_t* a1t, const uint16_t* dy2t, int batc
                              hipStream_t s,
                              const mnist::C1FilterArgs* c1 = nullptr);
 size_t part2_floats(int batch);
+// the whole conv2 backward in one launch: filter-grad slabs (as above), da1m
+// (as launch_conv2_bwd_data), the conv1 filter-grad partials of c1 (one part1
+// row per 128 pooled pixels: conv2_bwd_conv1_rows) and the optional
+// single-rank FC SGD
+int conv2_bwd_conv1_rows(int batch);
+// labs: per-block [start, end] 100 MHz clock stamps of launch_conv2_bwd into p
+// (2 x blocks u64; null turns them off)
+void set_conv2_bwd_prof(unsigned long long* p);
+void launch_conv2_bwd(const uint16_t* dy2p, const uint16_t* w2b, const uint16_t* a1p,
+                      const uint16_t* a1t, const uint16_t* dy2t, int batch, float* da1m,
+                      float* part2, hipStream_t s, const mnist::FcSgdArgs* fc_sgd,
+                      const mnist::C1FilterArgs* c1);
 }  // namespace mnist16

@@ -13,6 +13,8 @@
 // checks or a transpose - only the split-K reductions touch LDS.  The filter
 // grad reads its shifted operand at 2-byte alignment, which runs at full
 // speed on gfx950 (scripts/microbench/unaligned_b128.hip).
+#include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 
 #include "common.h"
@@ -324,20 +326,13 @@ __global__ __launch_bounds__(256) void conv2_bwd_data_kernel(const bf* __restric
 // (which visits every pixel once) also sums dY2 per channel (db2).
 constexpr int C2F_IMG = 8;
 
-__global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(const bf* __restrict__ a1t,
-                                                               const bf* __restrict__ dy2t,
-                                                               int batch, float* __restrict__ part2,
-                                                               float* __restrict__ part_db2,
-                                                               int nc2, const mnist::C1Filter c1f) {
-  constexpr int SM = 3 * 2 * 16 * 64 > mnist::C1F_SMEM ? 3 * 2 * 16 * 64 : mnist::C1F_SMEM;
-  __shared__ float smem[SM];
-  if ((int)blockIdx.x >= nc2) {  // conv1 filter-grad role (mnist_shared.h)
-    mnist::conv1_filter_unit<512>(blockIdx.x - nc2, batch, c1f, smem);
-    return;
-  }
+// filter-grad block bid (< 25 x groups) of 512 threads; smem >= 3 x 2 x 16 x 64
+__device__ __forceinline__ void conv2_bwd_filter_body(int bid, const bf* __restrict__ a1t,
+                                                      const bf* __restrict__ dy2t, int batch,
+                                                      float* __restrict__ part2,
+                                                      float* __restrict__ part_db2, float* smem) {
   auto red = reinterpret_cast<float(*)[2][16][64]>(smem);
   const int ngroups = (batch + C2F_IMG - 1) / C2F_IMG;
-  const int bid = blockIdx.x;
   int t, g;
   if (ngroups % 8 == 0) {  // all taps of an image group on one XCD (shared L2)
     const int xx = bid & 7, idx = bid >> 3;
@@ -392,6 +387,275 @@ __global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(const bf* __restr
   }
 }
 
+__global__ __launch_bounds__(512) void conv2_bwd_filter_kernel(const bf* __restrict__ a1t,
+                                                               const bf* __restrict__ dy2t,
+                                                               int batch, float* __restrict__ part2,
+                                                               float* __restrict__ part_db2,
+                                                               int nc2, const mnist::C1Filter c1f) {
+  constexpr int SM = 3 * 2 * 16 * 64 > mnist::C1F_SMEM ? 3 * 2 * 16 * 64 : mnist::C1F_SMEM;
+  __shared__ float smem[SM];
+  if ((int)blockIdx.x >= nc2) {  // conv1 filter-grad role (mnist_shared.h)
+    mnist::conv1_filter_unit<512>(blockIdx.x - nc2, batch, c1f, smem);
+    return;
+  }
+  conv2_bwd_filter_body(blockIdx.x, a1t, dy2t, batch, part2, part_db2, smem);
+}
+
+// ------------------------------------------------ conv2 backward, merged ----
+// The whole conv2 backward in ONE launch of 512-thread blocks (the fp32 set's
+// merged Winograd launch is the model).  Standalone, bwd-data (196 blocks) and
+// bwd-filter (200) each left CUs idle with their operand latency exposed: the
+// two launches ran 25.3 us, this one ~17 (step 64.8 -> 57.2 us).  Roles:
+//   [0, nd)             bwd-data: 64 pooled pixels (2 M tiles) a block, 8 waves
+//                       = 2 tiles x 4 K quarters (one 16-channel dY2 chunk
+//                       each, 25 taps), summed in LDS; then the conv1
+//                       filter-grad partial of those pixels from the masked dA1
+//                       they just produced, kept in LDS (one part1 row per
+//                       block: no second pass over da1m and no role that has to
+//                       wait for it);
+//   [nd, nd + nc2)      filter grad: the conv2_bwd_filter_kernel body;
+//   [nd + nc2, ...)     the single-rank FC SGD (two fc_sgd_role units a round).
+// Every global operand of the data role is requested up front (all its blocks
+// load at the launch start, where a round trip costs several us - per-phase
+// stamps, scripts/c2b_stamps.py): the dY2 rows of its pixels (staged into LDS,
+// no per-K-step L2 latency), a1 for the ReLU1 mask, the input images and pool1
+// argmax bytes for conv1, all coalesced.
+// The conv1 filter grad of a block is one fp32-MFMA GEMM: dW1[tap][co] = sum
+// over k = (pixel, pool1 quadrant q) of X[tap][k] S[k][co], X = the input
+// window of the pixel at quadrant q (row 25: 1, the bias), S = the masked dA1
+// where the channel's argmax IS q, else 0: K = 64 x 4, 16 products of
+// v_mfma_f32_32x32x2f32 a wave.  (Per-thread FMA loops over the 25 taps, the
+// conv1_filter_unit form, cost ~2x: 2-way conflicted LDS reads.)  The images
+// sit in LDS with a 37-float row pitch: one window's 25 taps, 25 banks.
+constexpr int C2B_PIX = 64;                  // pooled pixels per data block
+constexpr int C2B_RED = 2 * 3 * 16 * 64;     // K quarters 1..3 of the 2 tiles
+constexpr int C2B_DA = C2B_PIX * 32;         // masked dA1 of the block's pixels
+constexpr int C2B_XLD = 37, C2B_XIMG = 32 * C2B_XLD;
+constexpr int C2B_XS = 2 * C2B_XIMG;         // <= 2 input images, zero-padded by 2
+constexpr int C2B_QS = C2B_PIX * 32 / 4;     // pool1 argmax bytes
+constexpr int C2B_CRED = 8 * 832;            // per-wave conv1 partials
+constexpr int C2B_A1S = C2B_PIX * 32 / 2;    // a1 (the ReLU1 mask source), bf16
+constexpr int C2B_DATA_SM = C2B_RED + C2B_DA + C2B_XS + C2B_QS + C2B_CRED + C2B_A1S;
+// the staged dY2 rows alias dA .. cred (used only after the K loop)
+constexpr int C2B_ROWS = 16;
+static_assert(4 * 2 * C2B_ROWS * 18 * 4 <= C2B_DA + C2B_XS + C2B_QS + C2B_CRED, "dY2 stage");
+constexpr int C2B_FILT_SM = 3 * 2 * 16 * 64;
+constexpr int C2B_SM = C2B_DATA_SM > C2B_FILT_SM ? C2B_DATA_SM : C2B_FILT_SM;
+static_assert(C2B_SM >= 2 * 64 * 65, "FC SGD tiles of two units");
+
+__device__ __forceinline__ void c2b_data_block(int db, const bf* __restrict__ dy2p,
+                                               const bf* __restrict__ w2b,
+                                               const bf* __restrict__ a1p, int batch,
+                                               float* __restrict__ da1m,
+                                               const mnist::C1Filter& c1, float* smem,
+                                               unsigned long long* __restrict__ stamps) {
+  // stamps (labs): wave 0's clock after each phase -> stamps[0..4]
+  auto stamp = [&](int i) {
+    if (stamps && threadIdx.x == 0) stamps[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  auto red = reinterpret_cast<float(*)[3][16][64]>(smem);  // [tile][K quarter - 1][k][lane]
+  float* dA = smem + C2B_RED;
+  float* xs = dA + C2B_DA;
+  uint8_t* qs = reinterpret_cast<uint8_t*>(xs + C2B_XS);
+  float* cred = xs + C2B_XS + C2B_QS;
+  uint16_t* a1s = reinterpret_cast<uint16_t*>(cred + C2B_CRED);  // own region
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, h = lane >> 5, wave = tid >> 6;
+  const int tl = wave & 1, kq = wave >> 1;
+  const int M = batch * 196, mtiles = M / 32, pbase = db * C2B_PIX;
+  const int mt_raw = db * 2 + tl;
+  const int mt = min(mt_raw, mtiles - 1);
+  const bool conv1 = c1.part1 != nullptr;
+  const int n_first = pbase / 196;
+  // dY2 rows: image n0's padded rows ya0 .. ya1 + 4, then (pixels past that
+  // image) image n0 + 1's rows 0 .. yb1 + 4, all 18 columns, as [chunk 4]
+  // [half 2][row][18][8 bf16] - a 16-lane group of a fragment read covers 256
+  // contiguous bytes
+  const size_t cplane = (size_t)batch * IMG;
+  const int pend = min(pbase + C2B_PIX, M), pa_end = min(pend, (n_first + 1) * 196);
+  const int ya0 = (pbase - n_first * 196) / 14, ya1 = (pa_end - 1 - n_first * 196) / 14;
+  const int Ra = ya1 - ya0 + 5;
+  const int Rb = pend > pa_end ? (pend - 1 - (n_first + 1) * 196) / 14 + 5 : 0;
+  const int R = Ra + Rb;  // <= C2B_ROWS
+  uint4* stg = reinterpret_cast<uint4*>(dA);
+  constexpr int SJ = (4 * C2B_ROWS * 18 * 2 + 511) / 512;
+  uint4 sv[SJ];
+  const int npc = 4 * R * 18 * 2;
+#pragma unroll
+  for (int j = 0; j < SJ; ++j) {
+    const int i = min(tid + 512 * j, npc - 1);
+    const int hh = i & 1, col = (i >> 1) % 18, rw = (i >> 1) / 18, row = rw % R, c = rw / R;
+    const int nn = row < Ra ? n_first : n_first + 1, Y = row < Ra ? ya0 + row : row - Ra;
+    sv[j] = *reinterpret_cast<const uint4*>(dy2p + c * cplane + (size_t)nn * IMG +
+                                            (Y * 18 + col) * 16 + 8 * hh);
+  }
+  // a1 of the block's pixels x 32 channels, a 16-byte piece a thread (< 256)
+  uint4 a1v = make_uint4(0u, 0u, 0u, 0u);
+  {
+    const int pl = tid >> 2, pg = pbase + pl, pc = (tid >> 1) & 1, hh = tid & 1;
+    if (pl < C2B_PIX && pg < M) {
+      const int nn = pg / 196, pp = pg % 196, yy = pp / 14, xx = pp % 14;
+      a1v = *reinterpret_cast<const uint4*>(a1p + pc * cplane + (size_t)nn * IMG +
+                                            ((yy + 2) * 18 + xx + 2) * 16 + 8 * hh);
+    }
+  }
+  // conv1 operands: the input images (the block's pixels span <= 2) and the
+  // pool1 argmax bytes (contiguous: 8 a thread, < 256)
+  constexpr int XJ = (C2B_XS + 511) / 512;
+  float xv[XJ];
+  uint2 qv = make_uint2(0u, 0u);
+  if (conv1) {
+    if (tid < C2B_PIX * 4 && pbase + (tid >> 2) < M)
+      qv = *reinterpret_cast<const uint2*>(c1.idx1 + (size_t)pbase * 32 + 8 * tid);
+    const long long off = mnist::batch_offset_dev(c1.step, c1.n_local, batch);
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int i = tid + 512 * j;
+      const int im = i / C2B_XIMG, rc = i - im * C2B_XIMG, row = rc / C2B_XLD;
+      const int nn = n_first + im, yy = row - 2, xx = rc - row * C2B_XLD - 2;
+      const bool ok = i < C2B_XS && nn < batch && yy >= 0 && yy < 28 && xx >= 0 && xx < 28;
+      xv[j] = c1.data[ok ? (off + nn) * 784 + yy * 28 + xx : off * 784];
+      if (!ok) xv[j] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < SJ; ++j) {
+    const int i = tid + 512 * j;
+    if (i < npc) {
+      const int hh = i & 1, col = (i >> 1) % 18, rw = (i >> 1) / 18, row = rw % R, c = rw / R;
+      stg[((c * 2 + hh) * R + row) * 18 + col] = sv[j];
+    }
+  }
+  if (tid < C2B_PIX * 4) reinterpret_cast<uint4*>(a1s)[tid] = a1v;  // a1s[pixel][channel]
+  __syncthreads();
+  stamp(0);
+  // this lane's pixel (a dead tile - M % 32 == 0 - takes the block's first)
+  const int m = mt_raw < mtiles ? mt_raw * 32 + r : pbase, n = m / 196, p = m % 196,
+            y = p / 14, x = p % 14;
+  const int row0 = (n == n_first ? y - ya0 : Ra + y) + 4;  // LDS row of tap kh = 0
+  const uint4* sa = stg + ((kq * 2 + h) * R + row0) * 18 + x + 4;
+  const bf* bp = w2b + (kq * 32 + r) * 16 + 8 * h;
+  f32x16 c0 = zero16(), c1a = zero16();
+  kloop<5>(
+      25,
+      [&](int t, bfx8& a, bfx8& b) {
+        const int kh = t / 5, kw = t % 5;
+        a = __builtin_bit_cast(bfx8, sa[-kh * 18 - kw]);
+        b = ld8(bp + t * 4 * 512);
+      },
+      c0, c1a);
+  stamp(1);
+  if (kq > 0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) red[tl][kq - 1][k][lane] = c0[k] + c1a[k];
+  }
+  __syncthreads();
+  if (kq == 0) {
+    const bool live = mt_raw < mtiles;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int mm = mt * 32 + mfma32_row(k, lane);
+      const float g = ((c0[k] + c1a[k]) + red[tl][0][k][lane]) + (red[tl][1][k][lane] +
+                                                                  red[tl][2][k][lane]);
+      const float a = __uint_as_float(
+          (uint32_t)a1s[(tl * 32 + mfma32_row(k, lane)) * 32 + r] << 16);
+      const float v = a > 0.f ? g : 0.f;
+      if (live) da1m[(size_t)mm * 32 + r] = v;
+      dA[(tl * 32 + mfma32_row(k, lane)) * 32 + r] = live ? v : 0.f;
+    }
+  }
+  stamp(2);
+  if (!conv1) return;  // block-uniform
+#pragma unroll
+  for (int j = 0; j < XJ; ++j)
+    if (tid + 512 * j < C2B_XS) xs[tid + 512 * j] = xv[j];
+  if (tid < C2B_PIX * 4) reinterpret_cast<uint2*>(qs)[tid] = qv;
+  __syncthreads();
+  stamp(3);
+  // wave w: pixels 8 w .. 8 w + 7; K-step pair (2 j, 2 j + 1) of pixel j
+  // covers its quadrants q = h (row pair 0) and q = 2 + h (row pair 1).  Four
+  // pixels' operands are read before their 8 products.
+  const int ti = r, kh = ti / 5, kw = ti - 5 * kh;  // A row = tap (25: bias, 26..31: 0)
+  const float a_fix = ti == 25 ? 1.f : 0.f;
+  f32x16 cw = zero16();
+#pragma unroll
+  for (int jb = 0; jb < 8; jb += 4) {
+    float ae[4], ao[4], bv[4];
+    int qb[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int pl = 8 * wave + jb + u, pg = pbase + pl;
+      const int nn = pg / 196, pp = pg - 196 * nn, py = pp / 14, px = pp - 14 * py;
+      const float* xr = xs + (nn - n_first) * C2B_XIMG + (2 * py + kh) * C2B_XLD + 2 * px + h + kw;
+      ae[u] = ti < 25 ? xr[0] : a_fix;
+      ao[u] = ti < 25 ? xr[C2B_XLD] : a_fix;
+      bv[u] = dA[pl * 32 + r];
+      qb[u] = qs[pl * 32 + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      cw = mfma32x32x2(ae[u], qb[u] == h ? bv[u] : 0.f, cw);
+      cw = mfma32x32x2(ao[u], qb[u] == 2 + h ? bv[u] : 0.f, cw);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int t = mfma32_row(k, lane);
+    if (t < 26) cred[wave * 832 + t * 32 + r] = cw[k];
+  }
+  __syncthreads();
+  stamp(4);
+  for (int i = tid; i < 832; i += 512) {
+    float sum = 0.f;
+#pragma unroll
+    for (int wv = 0; wv < 8; ++wv) sum += cred[wv * 832 + i];
+    c1.part1[(size_t)db * 832 + i] = sum;
+  }
+}
+
+// Blocks [0, nd) data, [nd, nd + nc2) filter grad, then the FC SGD: the data
+// role is the longest (its operands' round trips at the launch start), so its
+// loads go first (data first: 57.2 vs 59.2 us a step, scripts/sessions/r5_s25.steps)
+__global__ __launch_bounds__(512) void conv2_bwd_kernel(
+    const bf* __restrict__ dy2p, const bf* __restrict__ w2b, const bf* __restrict__ a1p,
+    const bf* __restrict__ a1t, const bf* __restrict__ dy2t, int batch, float* __restrict__ da1m,
+    float* __restrict__ part2, float* __restrict__ part_db2, int nc2, int nd,
+    const mnist::C1Filter c1, const mnist::FcSgd sgd, unsigned long long* __restrict__ prof) {
+  __shared__ float smem[C2B_SM];
+  const int b = blockIdx.x;
+  // prof (labs): per block [start, end] of the constant 100 MHz clock, then 8
+  // phase stamps per data block
+  unsigned long long t0 = 0;
+  if (prof) t0 = __builtin_amdgcn_s_memrealtime();
+  if (b < nd) {
+    c2b_data_block(b, dy2p, w2b, a1p, batch, da1m, c1, smem,
+                   prof ? prof + 2 * gridDim.x + 8 * b : nullptr);
+  } else if (b < nd + nc2) {
+    // (the filter role keeps its XCD grouping: blocks b and b' share an XCD
+    // iff (b - nd) & 7 == (b' - nd) & 7)
+    conv2_bwd_filter_body(b - nd, a1t, dy2t, batch, part2, part_db2, smem);
+  } else {
+    // FC SGD: two units a round (unit pairs take the same path - SHADOW_W1_BLOCKS
+    // is even - so the tile path's barrier is met by both halves)
+    const int half = threadIdx.x >> 8, nsg = gridDim.x - nc2 - nd;
+    for (int u0 = 2 * (b - nc2 - nd); u0 < sgd.nblk; u0 += 2 * nsg) {
+      const int u = u0 + half;
+      if (u < sgd.nblk) mnist::fc_sgd_role(sgd, u, smem + half * 64 * 65, threadIdx.x & 255);
+    }
+  }
+  if (prof) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      prof[2 * b] = t0;
+      prof[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
+}
+
+// lab: the FC SGD units as a launch of their own
+__global__ __launch_bounds__(256) void fc_sgd_kernel(const mnist::FcSgd sgd) {
+  __shared__ float tile[64 * 65];
+  mnist::fc_sgd_role(sgd, blockIdx.x, tile);
+}
 }  // namespace mnist16
 
 // ======================================================================
@@ -466,5 +730,35 @@ void launch_conv2_bwd_filter(const uint16_t* a1t, const uint16_t* dy2t, int batc
 }
 
 size_t part2_floats(int batch) { return (size_t)conv2_filter_groups(batch) * (51200 + 256); }
+
+int conv2_bwd_conv1_rows(int batch) { return cdiv(batch * 196, C2B_PIX); }
+
+// labs: per-block clock stamps of the merged conv2 backward (null: off)
+static unsigned long long* g_c2b_prof = nullptr;
+void set_conv2_bwd_prof(unsigned long long* p) { g_c2b_prof = p; }
+
+void launch_conv2_bwd(const uint16_t* dy2p, const uint16_t* w2b, const uint16_t* a1p,
+                      const uint16_t* a1t, const uint16_t* dy2t, int batch, float* da1m,
+                      float* part2, hipStream_t s, const mnist::FcSgdArgs* fc_sgd,
+                      const mnist::C1FilterArgs* c1) {
+  if (batch % 8 != 0) throw std::runtime_error("mnist16 conv2_bwd: batch % 8 != 0");
+  const int G = conv2_filter_groups(batch);
+  const int nc2 = 25 * G, nd = conv2_bwd_conv1_rows(batch);
+  const mnist::FcSgd sg = mnist::fc_sgd_args(fc_sgd);
+  mnist::C1Filter c = mnist::c1_args(c1);
+  // lab switch (MTA_C2B_LAB): 1 = the FC SGD as a launch of its own after this
+  // one, 2 = no conv1 filter-grad epilogue (timing only: conv1 grads unset)
+  static const int lab = [] {
+    const char* e = getenv("MTA_C2B_LAB");
+    return e ? atoi(e) : 0;
+  }();
+  mnist::FcSgd sg_in = sg;
+  if (lab == 1) sg_in.nblk = 0;
+  if (lab == 2) c.part1 = nullptr;
+  conv2_bwd_kernel<<<nd + nc2 + cdiv(sg_in.nblk, 2), 512, 0, s>>>(
+      C16(dy2p), C16(w2b), C16(a1p), C16(a1t), C16(dy2t), batch, da1m, part2,
+      part2 + (size_t)G * 51200, nc2, nd, c, sg_in, g_c2b_prof);
+  if (lab == 1 && sg.nblk > 0) fc_sgd_kernel<<<sg.nblk, 256, 0, s>>>(sg);
+}
 
 }  // namespace mnist16

@@ -217,6 +217,7 @@ struct ShadowPtrs {
   __bf16* w2b;
 };
 constexpr int SHADOW_W1_BLOCKS = (FC1_IN / 64) * (FC1_OUT / 64), SHADOW_W2_BLOCKS = 51200 / 1024;
+static_assert(SHADOW_W1_BLOCKS % 2 == 0, "fc_sgd_role: unit pairs of a 512-thread block");
 constexpr int SHADOW_BLOCKS = SHADOW_W1_BLOCKS + SHADOW_W2_BLOCKS;
 constexpr int SHADOW_SMEM_FLOATS = 64 * 65;
 
@@ -305,9 +306,9 @@ constexpr int FC_SGD_UNROLL = 4;
 constexpr long long W1_F4 = (long long)FC1_IN * FC1_OUT / 4;
 FcSgd fc_sgd_args(const FcSgdArgs* a);  // host: role off when a == nullptr (mnist.hip)
 
-// one 64 x 64 tile of the fc1 weight: momentum SGD + both bf16 shadows
-__device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* tile) {
-  const int tid = threadIdx.x;
+// one 64 x 64 tile of the fc1 weight: momentum SGD + both bf16 shadows (tid:
+// the thread's index in its 256-thread unit; every unit of a block runs one)
+__device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* tile, int tid) {
   const int i0 = (L % (FC1_IN / 64)) * 64, j0 = (L / (FC1_IN / 64)) * 64;
   const int row = tid >> 2, ck = tid & 3;
   const size_t e0 = (size_t)a.w1_off4 * 4 + (size_t)(i0 + row) * FC1_OUT + j0 + 16 * ck;
@@ -342,10 +343,11 @@ __device__ inline void fc_sgd_w1_tile(const FcSgd& a, int L, float lr, float* ti
   shadow_store16(a.w1t + ((size_t)((i0 >> 4) + ck) * FC1_OUT + j0 + col) * 16, v);
 }
 
-// blk: index among the role's blocks; tile: >= 64 x 65 floats of LDS when
-// a.w1b is set (256-thread blocks)
+// blk: index among the role's blocks; tile: >= 64 x 65 floats of LDS (the
+// unit's own) when a.w1b is set
 // tid: the thread's index in its 256-thread unit (a 512-thread block runs two
-// units; the shadow path (a.w1b) needs 256-thread blocks)
+// units; with a.w1b the two take the same path - SHADOW_W1_BLOCKS is even - so
+// the tile path's barrier is met by both)
 __device__ __forceinline__ void fc_sgd_role(const FcSgd& a, int blk, float* tile,
                                    int tid = (int)threadIdx.x) {
   float4* W4 = reinterpret_cast<float4*>(a.w);
@@ -356,7 +358,7 @@ __device__ __forceinline__ void fc_sgd_role(const FcSgd& a, int blk, float* tile
   int nb = a.nblk;
   if (a.w1b) {
     if (blk < SHADOW_W1_BLOCKS) {
-      fc_sgd_w1_tile(a, blk, lr, tile);
+      fc_sgd_w1_tile(a, blk, lr, tile, tid);
       return;
     }
     blk -= SHADOW_W1_BLOCKS;

@@ -1,6 +1,7 @@
 #include "mnist_executor.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -178,16 +179,27 @@ void MnistExecutor::enqueue_fwd_bwd_bf16(hipStream_t s, bool finalize,
                           G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<U16>(p.dy2p),
                           P<U16>(p.dy2t), s);
   HIP_CHECK(hipEventRecord(ev_dw_, s));
-  mnist16::launch_conv2_bwd_data(P<const U16>(p.dy2p), P<const U16>(p.w2b), P<const U16>(p.a1p), B,
-                                 P<float>(p.da1m), s, fc_sgd);
+  // conv2 bwd-data (+ conv1 filter grad) | conv2 filter grad | FC SGD: one launch
   const mnist::C1FilterArgs c1{P<const float>(p.train_x), step, p.n_local,
                                P<const float>(p.da1m), P<const uint8_t>(p.idx1),
                                P<float>(p.part1)};
-  mnist16::launch_conv2_bwd_filter(P<const U16>(p.a1t), P<const U16>(p.dy2t), B,
-                                   P<float>(p.part2), s, &c1);
+  static const bool lab_split = [] {  // lab (MTA_C2B_LAB=3): the two-launch form
+    const char* e = getenv("MTA_C2B_LAB");
+    return e && atoi(e) == 3;
+  }();
+  if (lab_split) {
+    mnist16::launch_conv2_bwd_data(P<const U16>(p.dy2p), P<const U16>(p.w2b), P<const U16>(p.a1p),
+                                   B, P<float>(p.da1m), s, fc_sgd);
+    mnist16::launch_conv2_bwd_filter(P<const U16>(p.a1t), P<const U16>(p.dy2t), B,
+                                     P<float>(p.part2), s, &c1);
+  } else {
+    mnist16::launch_conv2_bwd(P<const U16>(p.dy2p), P<const U16>(p.w2b), P<const U16>(p.a1p),
+                              P<const U16>(p.a1t), P<const U16>(p.dy2t), B, P<float>(p.da1m),
+                              P<float>(p.part2), s, fc_sgd, &c1);
+  }
   if (finalize)
     mnist::launch_grad_finalize(P<const float>(p.part2), mnist16::conv2_filter_groups(B),
-                                P<const float>(p.part1), mnist::conv1_filter_blocks(B),
+                                P<const float>(p.part1), conv1_blocks(),
                                 G + p.off_w2, G + p.off_b2, G + p.off_w1, G + p.off_b1, s);
 }
 
@@ -197,9 +209,15 @@ int MnistExecutor::conv2_groups() const {
                  : mnist::conv2_filter_splits(p_.batch);
 }
 
-// the Winograd bwd-data blocks produce one conv1 partial per band of 4 a1 rows
+// the Winograd bwd-data blocks produce one conv1 partial per band of 4 a1 rows,
+// the bf16 merged conv2 backward one per 128 pooled pixels
 int MnistExecutor::conv1_blocks() const {
-  return mnist::conv1_filter_blocks(p_.batch, (p_.wino && !p_.bf16) ? 4 : 7);
+  if (p_.bf16) {
+    const char* e = getenv("MTA_C2B_LAB");
+    if (e && atoi(e) == 3) return mnist::conv1_filter_blocks(p_.batch, 7);
+    return mnist16::conv2_bwd_conv1_rows(p_.batch);
+  }
+  return mnist::conv1_filter_blocks(p_.batch, p_.wino ? 4 : 7);
 }
 
 void MnistExecutor::forward_backward(hipStream_t s) {

@@ -95,21 +95,32 @@ def test_fused_conv12_forward_matches_oracle(cuda_dev, data, step):
                         ptr(i1), ptr(w2), ptr(b2), ptr(a2), ptr(i2), ptr(w2t), stream_handle())
     torch.cuda.synchronize()
     off = (step * B) % (n_local - B)
-    xn = xd[off:off + B].permute(0, 3, 1, 2)
-    z1 = F.conv2d(xn, w1.permute(3, 2, 0, 1), b1, padding=2)
-    r1, ri1 = F.max_pool2d(F.relu(z1), 2, 2, return_indices=True)
-    z2 = F.conv2d(r1, w2.permute(3, 2, 0, 1), b2, padding=2)
-    r2, ri2 = F.max_pool2d(F.relu(z2), 2, 2, return_indices=True)
+    # deterministic oracle: float64 on the CPU (a GPU oracle's convolutions
+    # round differently from box to box and flip near-tied pooling argmaxes)
+    c64 = lambda t: t.detach().cpu().double()  # noqa: E731
+    xn = c64(xd[off:off + B]).permute(0, 3, 1, 2)
+    z1 = F.relu(F.conv2d(xn, c64(w1).permute(3, 2, 0, 1), c64(b1), padding=2))
+    r1 = F.max_pool2d(z1, 2, 2)
+    z2 = F.relu(F.conv2d(r1, c64(w2).permute(3, 2, 0, 1), c64(b2), padding=2))
+    r2 = F.max_pool2d(z2, 2, 2)
     r1h = r1.permute(0, 2, 3, 1)
-    assert _rel(a1, r1h) < 1e-5
+    assert _rel(c64(a1), r1h) < 1e-5
     assert torch.equal(a1pf[:, 2:16, 2:16], a1)
     assert float(a1pf[:, :2].abs().sum() + a1pf[:, 16:].abs().sum()) == 0.0  # border untouched
-    assert _rel(a2, r2.permute(0, 2, 3, 1)) < 1e-5
+    assert _rel(c64(a2), r2.permute(0, 2, 3, 1)) < 1e-5
     assert torch.equal(w2t.view(25, 64, 32), w2.view(25, 32, 64).transpose(1, 2))
-    for idx, ri, r, w in ((i1, ri1, r1h, 28), (i2, ri2, r2.permute(0, 2, 3, 1), 14)):
-        code = (((ri // w) % 2) * 2 + (ri % w) % 2).permute(0, 2, 3, 1).to(torch.uint8)
-        pos = r > 0
-        assert torch.equal(idx[pos], code[pos])
+    for idx, z in ((i1, z1), (i2, z2)):
+        # the 2x2 windows, quadrant code 2 dy + dx; compare where the maximum is
+        # positive and clear of the runner-up (an fp32 tie may go either way)
+        Bn, Cc, H, W = z.shape
+        win = z.view(Bn, Cc, H // 2, 2, W // 2, 2).permute(0, 2, 4, 1, 3, 5).reshape(
+            Bn, H // 2, W // 2, Cc, 4)
+        top = win.topk(2, dim=-1)
+        code = top.indices[..., 0].to(torch.uint8)
+        gap = top.values[..., 0] - top.values[..., 1]
+        pos = (top.values[..., 0] > 0) & (gap > 1e-4 * top.values[..., 0].clamp(min=1.0))
+        assert float(pos.float().mean()) > 0.3
+        assert torch.equal(idx.cpu()[pos], code[pos])
 
 
 @pytest.mark.parametrize("batch", [64, 96, 128])
