@@ -186,7 +186,7 @@ PYBIND11_MODULE(_C, m) {
   k.def("conv1_filter_blocks", [](int batch, int split) {
     return mnist::conv1_filter_blocks(batch, split);
   }, py::arg("batch"), py::arg("split") = 7);
-  k.def("conv2_wino_filter_groups", &mnist::conv2_wino_filter_groups);
+
   k.def("part2_floats", &mnist::part2_floats);
   k.def("part2_floats_wino", &mnist::part2_floats_wino);
   k.def("part1_floats", &mnist::part1_floats);
@@ -194,6 +194,14 @@ PYBIND11_MODULE(_C, m) {
   k.def("part2_floats_bf16", &mnist16::part2_floats);
   k.def("conv2_filter_groups_bf16", &mnist16::conv2_filter_groups);
   k.def("conv2_bwd_conv1_rows_bf16", &mnist16::conv2_bwd_conv1_rows);
+  k.def("xgmi_conv_floats", &mnist::xgmi_conv_floats);
+  k.def("set_xgmi_step_prof", [](uintptr_t p) {
+    mnist::set_xgmi_step_prof(reinterpret_cast<unsigned long long*>(p));
+  });
+  k.def("set_conv2_bwd_wino_prof", [](uintptr_t p) {
+    mnist::set_conv2_bwd_wino_prof(reinterpret_cast<unsigned long long*>(p));
+  });
+  k.def("conv2_wino_filter_groups", &mnist::conv2_wino_filter_groups);
   k.def("set_conv2_bwd_prof_bf16", [](uintptr_t p) {
     mnist16::set_conv2_bwd_prof(reinterpret_cast<unsigned long long*>(p));
   });
@@ -783,6 +791,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_xgmi", &MnistExecutor::set_xgmi, py::keep_alive<1, 2>())
       .def("xgmi_ok", &MnistExecutor::xgmi_ok)
       .def("set_xgmi_fc_in_bwd", &MnistExecutor::set_xgmi_fc_in_bwd)
+      .def("set_xgmi_xconv", &MnistExecutor::set_xgmi_xconv)
       .def_property_readonly("defer_split", &MnistExecutor::defer_split)
       .def("join", [](MnistExecutor& e, uintptr_t s) { e.join(S(s)); })
       .def("gather_optimizer_state",

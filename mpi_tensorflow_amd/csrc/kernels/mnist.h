@@ -161,6 +161,11 @@ void launch_conv2_bwd_data_l2(const float* dy2t, const float* w2t, const float* 
 // default; 4: the Winograd bwd-data blocks' bands of 4 a1 rows; 1: whole
 // images)
 int conv1_filter_blocks(int batch, int split = 7);
+// labs: 6 clock stamps per block of launch_xgmi_step into p (null: off)
+void set_xgmi_step_prof(unsigned long long* p);
+// labs: per-block [start, end] 100 MHz clock stamps of launch_conv2_bwd_wino into
+// p (2 x blocks u64; null turns them off)
+void set_conv2_bwd_wino_prof(unsigned long long* p);
 void launch_conv1_bwd_filter(const float* data, const long long* step, int n_local, int batch,
                              const float* da1m, const uint8_t* idx1, float* part1, hipStream_t s);
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,
@@ -241,10 +246,20 @@ struct XgmiStepArgs {
   // set by the launchers (xgmi_fc_plan)
   long long seg4 = 0;
   int per4 = 0, nfc = 0, ncv = 0, ngather = 0;
+  // every rank's conv-grad exchange buffer (2 x cstride floats, by epoch
+  // parity; xgmi_conv_floats), or null: the conv grads go through the grads
+  // buffer and the conv blocks keep the closing "done reading" barrier
+  float* xc[xgmi::kMaxRanks] = {};
+  long long cstride = 0;
+  // labs: per block 6 clock stamps (100 MHz) of xgmi_step_kernel, or null
+  unsigned long long* prof = nullptr;
 };
 void launch_xgmi_step(const XgmiStepArgs& a, hipStream_t s);
 // FC role geometry for `threads`-thread blocks (<= max_blocks, rounded up to 8)
 void xgmi_fc_plan(XgmiStepArgs& a, int threads, int max_blocks);
+// floats of one parity half of the conv-grad exchange buffer (off_b1: the
+// conv1 bias offset, the conv params being the flat buffer's prefix)
+long long xgmi_conv_floats(long long off_b1);
 size_t part2_floats(int batch);
 size_t part1_floats(int batch);
 size_t fc1_part_floats(int batch);

@@ -1915,6 +1915,11 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return a;
 }
 
+// labs (XgmiStepArgs::prof): stamp i of this block
+__device__ __forceinline__ void xs_stamp(const XgmiStepArgs& a, int i) {
+  if (a.prof && threadIdx.x == 0) a.prof[6 * blockIdx.x + i] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
   const xgmi::Sync& s = a.sync;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, nt = blockDim.x;
@@ -1929,7 +1934,9 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
       wr[r] = xgmi::rsrc(a.w[r], fcb);
     }
   const unsigned e = xgmi::next_epoch(s, ep);
+  xs_stamp(a, 1);
   xgmi::barrier(s, 0, e, /*release=*/true);  // the grads come from fc1 backward
+  xs_stamp(a, 2);
   const long long lo = (long long)blockIdx.x * a.per4;
   const long long hi = lo + a.per4 < a.seg4 ? lo + a.per4 : a.seg4;
   long long t0 = xgmi::now_ticks();
@@ -1964,22 +1971,26 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
     }
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
+  xs_stamp(a, 3);
   xgmi::barrier(s, 1, e, false);
+  xs_stamp(a, 4);
   if (a.fc_in_bwd) return;  // the step launch gathers (xgmi_fc_gather)
   t0 = xgmi::now_ticks();
+  // every other rank's slice at once (one round trip per XS_UNROLL float4s,
+  // not one per rank)
+  for (long long i0 = lo + tid; i0 < hi; i0 += (long long)nt * XS_UNROLL) {
+    float4 v[xgmi::kMaxRanks][XS_UNROLL];
 #pragma unroll
-  for (int r = 0; r < xgmi::kMaxRanks; ++r) {
-    if (r >= n || r == me) continue;
-    const long long rb = (long long)r * a.seg4;
-    for (long long i0 = lo + tid; i0 < hi; i0 += (long long)nt * XS_UNROLL) {
-      float4 v[XS_UNROLL];
-#pragma unroll
-      for (int u = 0; u < XS_UNROLL; ++u)
-        if (i0 + nt * u < hi) v[u] = xgmi::ld4_sys(wr[r], (unsigned)((rb + i0 + nt * u) * 16));
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
-        if (i0 + nt * u < hi) W4[rb + i0 + nt * u] = v[u];
-    }
+        if (r < n && r != me && i0 + nt * u < hi)
+          v[r][u] = xgmi::ld4_sys(wr[r], (unsigned)(((long long)r * a.seg4 + i0 + nt * u) * 16));
+#pragma unroll
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u)
+        if (r < n && r != me && i0 + nt * u < hi) W4[(long long)r * a.seg4 + i0 + nt * u] = v[r][u];
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
 }
@@ -1997,20 +2008,25 @@ __device__ void xgmi_fc_gather(const XgmiStepArgs& a, int gb, int ng) {
   const long long lo = (long long)gb * per, hi = lo + per < a.seg4 ? lo + per : a.seg4;
   const long long t0 = xgmi::now_ticks();
   float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+  xgmi::Rsrc wr[xgmi::kMaxRanks];
 #pragma unroll
-  for (int r = 0; r < xgmi::kMaxRanks; ++r) {
-    if (r >= n || r == me) continue;
-    const xgmi::Rsrc wr = xgmi::rsrc(a.w[r], fcb);
-    const long long rb = (long long)r * a.seg4;
-    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
-      float4 v[XS_UNROLL];
+  for (int r = 0; r < xgmi::kMaxRanks; ++r)
+    if (r < n) wr[r] = xgmi::rsrc(a.w[r], fcb);
+  // every other rank's slice at once (one round trip, not one per rank)
+  for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
+    float4 v[xgmi::kMaxRanks][XS_UNROLL];
+#pragma unroll
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
-        if (i0 + 256 * u < hi) v[u] = xgmi::ld4_sys(wr, (unsigned)((rb + i0 + 256 * u) * 16));
+        if (r < n && r != me && i0 + 256 * u < hi)
+          v[r][u] = xgmi::ld4_sys(wr[r], (unsigned)(((long long)r * a.seg4 + i0 + 256 * u) * 16));
+#pragma unroll
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
 #pragma unroll
       for (int u = 0; u < XS_UNROLL; ++u)
-        if (i0 + 256 * u < hi) W4[rb + i0 + 256 * u] = v[u];
-    }
+        if (r < n && r != me && i0 + 256 * u < hi)
+          W4[(long long)r * a.seg4 + i0 + 256 * u] = v[r][u];
   }
   xgmi::link_floor(s, t0, a.seg4 * 16);
 }
@@ -2019,9 +2035,22 @@ __global__ __launch_bounds__(WF_NT) void conv2_bwd_wino_kernel(
     int nd, const float* __restrict__ Ud,
     const float* __restrict__ a1, int batch, float* __restrict__ da1m,
     const C1Filter c1, const float* __restrict__ a1p, const float* __restrict__ dy2,
-    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const XgmiStepArgs xfc) {
+    float* __restrict__ part2, float* __restrict__ part_db2, int nwg, const XgmiStepArgs xfc,
+    unsigned long long* __restrict__ prof) {
   // one LDS pool for either role
   __shared__ float smem[WD_SMEM > WF_SMEM_ALL ? WD_SMEM : WF_SMEM_ALL];
+  // prof (labs): per block [start, end] of the constant 100 MHz clock
+  const unsigned long long t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  struct Stamp {
+    unsigned long long* p;
+    unsigned long long t0;
+    __device__ ~Stamp() {
+      if (p && threadIdx.x == 0) {
+        p[2 * blockIdx.x] = t0;
+        p[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+  } stamp{prof, t0};
   // world > 1 over xGMI: the first xfc.nfc blocks exchange + update the FC
   // bucket (its grads are final after fc1 backward) while the conv blocks run
   if ((int)blockIdx.x < xfc.nfc) {
@@ -2583,6 +2612,9 @@ void launch_conv2_bwd_filter_wino(const float* a1p, const float* dy2, int batch,
       batch, a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, c, nullptr);
 }
 
+// labs: per-block clock stamps of the merged conv2 backward (null: off)
+static unsigned long long* g_c2bw_prof = nullptr;
+
 void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, const float* dy2,
                            int batch, float* da1m, float* part2, hipStream_t s,
                            const C1FilterArgs* c1, const XgmiStepArgs* xfc) {
@@ -2594,8 +2626,11 @@ void launch_conv2_bwd_wino(const float* Ud, const float* a1, const float* a1p, c
     xgmi_fc_plan(xa, WF_NT, XS_FC_ROLE_BLOCKS);
   }
   conv2_bwd_wino_kernel<<<xa.nfc + nd + 8 * G, WF_NT, 0, s>>>(
-      nd, Ud, a1, batch, da1m, c1_args(c1), a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, xa);
+      nd, Ud, a1, batch, da1m, c1_args(c1), a1p, dy2, part2, part2 + (size_t)G * 51200, 8 * G, xa,
+      g_c2bw_prof);
 }
+
+void set_conv2_bwd_wino_prof(unsigned long long* p) { g_c2bw_prof = p; }
 
 void launch_conv2_bwd_filter_wino_prof(const float* a1p, const float* dy2, int batch,
                                        float* part2, unsigned long long* prof, hipStream_t s) {
@@ -2886,15 +2921,22 @@ __device__ __forceinline__ XsConvItem xs_conv_item(const XgmiStepArgs& a, int v,
 __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   __shared__ unsigned ep;
   __shared__ float wl[25 * 16];
+  xs_stamp(a, 0);
+  struct End {
+    const XgmiStepArgs& a;
+    __device__ ~End() { xs_stamp(a, 5); }
+  } end{a};
   const xgmi::Sync& s = a.sync;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x, lane = tid & 63;
   const float lr = *a.lr;
   if (a.fc_in_bwd && (int)blockIdx.x < a.ngather) {  // ---- the FC gather
+    xs_stamp(a, 1);  // (labs: the role in slot 1's gap; gather blocks stamp 1 at once)
     xgmi_fc_gather(a, blockIdx.x, a.ngather);
     return;
   }
   if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
     xgmi_fc_role(a, &ep);
+    if (a.prof && threadIdx.x == 0) a.prof[6 * blockIdx.x] |= 1ull << 60;  // role tag: FC
     return;
   }
   // ---- conv parameters (replicated update)
@@ -2902,12 +2944,17 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
   const int cb = (int)blockIdx.x - (a.fc_in_bwd ? a.ngather : a.nfc);
   const int nvirt = (a.wino_u ? 128 : 50) + 16 + 208;
   // every rank's conv grads, system-scope (kernels/xgmi.h): conv2 weight
-  // float4s from off_w2, scalars (conv2 bias, conv1) from the buffer start
+  // float4s from off_w2, scalars (conv2 bias, conv1) from the buffer start.
+  // With the exchange buffer the half of this launch's epoch parity: a block
+  // slot writes that half again two launches on, after the next launch's
+  // arrival barrier, which no peer's block passes before it has read this one
+  // - so no closing barrier
+  const bool dbuf = a.xc[0] != nullptr;
   const long long cbytes = 4LL * (a.off_b1 + 32);
   xgmi::Rsrc gr[xgmi::kMaxRanks];
 #pragma unroll
   for (int r = 0; r < xgmi::kMaxRanks; ++r)
-    if (r < n) gr[r] = xgmi::rsrc(a.g[r], cbytes);
+    if (r < n) gr[r] = xgmi::rsrc(dbuf ? a.xc[r] + (e & 1) * a.cstride : a.g[r], cbytes);
   // this rank's slab reductions (grad_finalize_kernel forms) into its grads,
   // written through for the peers
   for (int v = cb; v < nvirt; v += a.ncv) {
@@ -2932,7 +2979,9 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
     }
     if (it.off >= 0 && lane == 0) xgmi::st_sys(gr[me], (unsigned)(4 * it.off), sl);
   }
+  xs_stamp(a, 1);
   xgmi::barrier(s, 0, e, false);
+  xs_stamp(a, 2);
   for (int v = cb; v < nvirt; v += a.ncv) {
     const XsConvItem it = xs_conv_item(a, v, tid);
     if (it.kind == 1) {
@@ -2986,7 +3035,9 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
     }
   }
   if (a.step && cb == 0 && tid == 0) *a.step += 1;
-  xgmi::barrier(s, 1, e, false);
+  xs_stamp(a, 3);
+  if (!dbuf) xgmi::barrier(s, 1, e, false);
+  xs_stamp(a, 4);
 }
 
 void xgmi_fc_plan(XgmiStepArgs& a, int threads, int max_blocks) {
@@ -3000,8 +3051,14 @@ void xgmi_fc_plan(XgmiStepArgs& a, int threads, int max_blocks) {
   a.nfc = (int)((a.seg4 + a.per4 - 1) / a.per4 + 7) / 8 * 8;
 }
 
+static unsigned long long* g_xs_prof = nullptr;
+void set_xgmi_step_prof(unsigned long long* p) { g_xs_prof = p; }
+
+long long xgmi_conv_floats(long long off_b1) { return (off_b1 + 32 + 63) / 64 * 64; }
+
 void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
   XgmiStepArgs a = in;
+  a.prof = g_xs_prof;
   const int n = a.sync.nranks;
   if (n < 1 || n > xgmi::kMaxRanks || !a.sync.flags || !a.sync.epoch || !a.sync.error || !a.lr)
     throw std::runtime_error("xgmi_step: communicator / lr not set up");
@@ -3009,6 +3066,12 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
     if (!a.g[r] || !a.w[r] || (!a.sync.emulate && !a.sync.peer_flags[r]))
       throw std::runtime_error("xgmi_step: rank " + std::to_string(r) + " not mapped");
   if (a.fc4 <= 0 || a.fc4 % n) throw std::runtime_error("xgmi_step: FC bucket not split evenly");
+  if (a.xc[0] != nullptr) {
+    for (int r = 0; r < n; ++r)
+      if (!a.xc[r]) throw std::runtime_error("xgmi_step: conv exchange buffer of a rank not mapped");
+    if (a.cstride < xgmi_conv_floats(a.off_b1))
+      throw std::runtime_error("xgmi_step: conv exchange buffer too small");
+  }
   if ((a.wino_u == nullptr) != (a.wino_ud == nullptr))
     throw std::runtime_error("xgmi_step: Winograd transforms need both U and Ud");
   if (!a.part2 || !a.part1 || a.ngroups <= 0 || a.nblk1 <= 0 || a.off_w2 % 4)

@@ -690,6 +690,12 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
     a.g[r] = static_cast<const float*>(x->peer_ptr(P<const void>(p.grads), r));
     a.w[r] = static_cast<float*>(x->peer_ptr(P<const void>(p.params), r));
   }
+  const long long cf = mnist::xgmi_conv_floats(p.off_b1);
+  if (xconv_ && x->registered(reinterpret_cast<const void*>(xconv_), 2 * cf * sizeof(float))) {
+    for (int r = 0; r < n; ++r)
+      a.xc[r] = static_cast<float*>(x->peer_ptr(reinterpret_cast<const void*>(xconv_), r));
+    a.cstride = cf;
+  }
   a.mom = P<float>(p.mom);
   a.fc4 = p.bucket1 / 4;
   a.l2 = p.l2;

@@ -133,6 +133,10 @@ class MnistExecutor {
   // the peer-to-peer communicator of SCHED_XGMI: the flat grads and params must
   // be registered with it (XgmiComm::open_buffer / emulate_buffer)
   void set_xgmi(XgmiComm* x) { xgmi_ = x; }
+  // the conv-grad exchange buffer of the step launch (2 x
+  // mnist::xgmi_conv_floats(off_b1) floats, registered with the communicator;
+  // 0: the conv grads go through the grads buffer)
+  void set_xgmi_xconv(uintptr_t p) { xconv_ = p; }
   // fp32 SCHED_XGMI: the FC exchange inside the conv2 backward launch
   // (default) or in the step launch (= SCHED_XGMI_STEP; labs)
   void set_xgmi_fc_in_bwd(bool on) { xgmi_fc_in_bwd_ = on; }
@@ -216,6 +220,7 @@ class MnistExecutor {
   void train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_xgmi(hipStream_t s);
   XgmiComm* xgmi_ = nullptr;
+  uintptr_t xconv_ = 0;
   bool xgmi_fc_in_bwd_ = true;
   float defer_split_ = 0.5f;
   void wait_fc_params(hipStream_t s);

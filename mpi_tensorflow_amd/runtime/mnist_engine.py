@@ -300,8 +300,13 @@ class NativeMnistEngine(MnistEngineBase):
         if not self.grad_sync:
             self.xcomm = None
         if self.xcomm is not None:
-            self.xcomm.register(self.grads, self.params, self.mom)
+            # + the conv-grad exchange buffer of the step launch (two halves
+            # by barrier epoch parity: no closing barrier for the conv blocks)
+            cf = C_.mnist.xgmi_conv_floats(self.layout.offsets["conv1_bias"])
+            self.xconv = torch.zeros(2 * cf, device=dev)
+            self.xcomm.register(self.grads, self.params, self.mom, self.xconv)
             self.exe.set_xgmi(self.xcomm.native_handle)
+            self.exe.set_xgmi_xconv(ptr(self.xconv))
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
         self._native_comm = self.comm.native_handle if (self.grad_sync and self.comm) else None
         if self.grad_sync and self._native_comm is None:
