@@ -88,8 +88,19 @@ __device__ __forceinline__ void pool4(f2 a01, f2 a23, float& v, int& q) {
   if (a23.y > v) { v = a23.y; q = 3; }
 }
 
+// Phase barrier for LDS hand-offs only: __syncthreads() also waits for every
+// outstanding global load (s_waitcnt vmcnt(0)), which would drain the FC weight
+// prefetches below at the first barrier they cross
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// one workgroup per CU (LDS): 2 waves a SIMD, up to 256 VGPRs a lane - the room
+// the FC weight prefetches live in
 template <bool TRAIN>
-__global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
+__global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   __shared__ float sm[S_TOTAL];
   __shared__ uint8_t q1s[P1 * P1 * C1];
   __shared__ uint8_t q2s[F0];
@@ -156,9 +167,8 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
       }
   }
   const int label = a.y[row];
-  __syncthreads();
+  lds_barrier();
   if (a.stop_phase == 0) return;
-
   // ---- B: conv1 + bias + ReLU + pool: thread = (pooled pixel, 3 channels);
   // the channel triple is wave-uniform (weights are LDS broadcasts)
   {
@@ -195,8 +205,17 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (a.stop_phase == 1) return;
+  // the FC1 weights of phase D, requested now: their round trip hides under
+  // conv2 (issued in D it was one exposed round trip per FC layer)
+  const int fj = tid & 127, fg = tid >> 7;
+  float wv1[100];
+  if (fj < F1) {
+    const float* wp = W + o.f1w + (fg * 100) * F1 + fj;
+#pragma unroll
+    for (int i = 0; i < 100; ++i) wv1[i] = wp[i * F1];
+  }
 
   // ---- C: conv2 + bias + ReLU + pool: thread = (pooled pixel, channel)
   if (tid < F0) {
@@ -221,54 +240,78 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
     sm[S_P2 + tid] = relu(v + sm[S_B2 + co]);  // (h, w, c) flatten = FC1 input order
     q2s[tid] = (uint8_t)q;
   }
-  __syncthreads();
+  lds_barrier();
   if (a.stop_phase == 2) return;
 
-  // ---- D: FC1 400 -> 120 + ReLU: 4-way split K, coalesced weight columns,
-  // all 100 loads of a thread in flight
+  // FC2 / FC3 weights of phases E, F
+  float wv2[30], wv3[3];
+  if (fj < F2) {
+    const float* wp = W + o.f2w + (fg * 30) * F2 + fj;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) wv2[i] = wp[i * F2];
+  }
   {
-    const int j = tid & 127, g = tid >> 7;
+    const int j3 = tid & 15, g3 = tid >> 4;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int i = g3 + 32 * u;
+      wv3[u] = (j3 < F3 && i < F2) ? W[o.f3w + i * F3 + j3] : 0.f;
+    }
+  }
+  // ---- D: FC1 400 -> 120 + ReLU: 4-way split K, coalesced weight columns
+  // (prefetched after phase A)
+  {
     float acc = 0.f;
-    if (j < F1) {
-      const float* wp = W + o.f1w + (g * 100) * F1 + j;
-      const float* xp = sm + S_P2 + g * 100;
-      float wv[100];
+    if (fj < F1) {
+      const float* xp = sm + S_P2 + fg * 100;
 #pragma unroll
-      for (int i = 0; i < 100; ++i) wv[i] = wp[i * F1];
-#pragma unroll
-      for (int i = 0; i < 100; ++i) acc = fmaf(xp[i], wv[i], acc);
+      for (int i = 0; i < 100; ++i) acc = fmaf(xp[i], wv1[i], acc);
     }
     sm[S_RED + tid] = acc;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < F1) {
     const float z = W[o.f1b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
                     sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
     sm[S_H1 + tid] = relu(z);
   }
-  __syncthreads();
+  lds_barrier();
+  // the FC backward (dX chain) weights of phase G, requested now (train)
+  float g3w[F3], g2w[21];
+  float4 g1w[F1 / 4];
+  if (TRAIN) {
+    if (tid < F2) {
+#pragma unroll
+      for (int j = 0; j < F3; ++j) g3w[j] = W[o.f3w + tid * F3 + j];
+    }
+    if ((tid >> 2) < F1) {
+      const float* wp = W + o.f2w + (tid >> 2) * F2 + (tid & 3) * 21;
+#pragma unroll
+      for (int j = 0; j < 21; ++j) g2w[j] = wp[j];
+    }
+    if (tid < F0) {
+      const float4* wp = reinterpret_cast<const float4*>(W + o.f1w + tid * F1);
+#pragma unroll
+      for (int j4 = 0; j4 < F1 / 4; ++j4) g1w[j4] = wp[j4];
+    }
+  }
   // ---- E: FC2 120 -> 84 + ReLU
   {
-    const int j = tid & 127, g = tid >> 7;
     float acc = 0.f;
-    if (j < F2) {
-      const float* wp = W + o.f2w + (g * 30) * F2 + j;
-      const float* xp = sm + S_H1 + g * 30;
-      float wv[30];
+    if (fj < F2) {
+      const float* xp = sm + S_H1 + fg * 30;
 #pragma unroll
-      for (int i = 0; i < 30; ++i) wv[i] = wp[i * F2];
-#pragma unroll
-      for (int i = 0; i < 30; ++i) acc = fmaf(xp[i], wv[i], acc);
+      for (int i = 0; i < 30; ++i) acc = fmaf(xp[i], wv2[i], acc);
     }
     sm[S_RED + tid] = acc;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < F2) {
     const float z = W[o.f2b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
                     sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
     sm[S_H2 + tid] = relu(z);
   }
-  __syncthreads();
+  lds_barrier();
   // ---- F: FC3 84 -> 10: 32 K groups of <= 3
   {
     const int j = tid & 15, g = tid >> 4;
@@ -277,11 +320,11 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
 #pragma unroll
       for (int u = 0; u < 3; ++u) {
         const int i = g + 32 * u;
-        if (i < F2) acc = fmaf(sm[S_H2 + i], W[o.f3w + i * F3 + j], acc);
+        if (i < F2) acc = fmaf(sm[S_H2 + i], wv3[u], acc);
       }
     sm[S_RED + tid] = acc;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < 64) {  // one wave: logits, softmax xent, argmax
     float lg = -INFINITY;
     if (tid < F3) {
@@ -307,44 +350,33 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
     }
   }
   if (!TRAIN) return;
-  __syncthreads();
+  lds_barrier();
   if (a.stop_phase == 3) return;
 
   // ---- G: FC backward (dX chain), ReLU masks from the stored activations
   float* act = a.acts + (size_t)img * ACT_STRIDE;
   float* del = a.deltas + (size_t)img * DELTA_STRIDE;
   if (tid < F2) {  // dz2 = relu'(h2) * W3 dz3
-    const float* wp = W + o.f3w + tid * F3;
-    float wv[F3];
-#pragma unroll
-    for (int j = 0; j < F3; ++j) wv[j] = wp[j];
     float s = 0.f;
 #pragma unroll
-    for (int j = 0; j < F3; ++j) s = fmaf(wv[j], sm[S_D3 + j], s);
+    for (int j = 0; j < F3; ++j) s = fmaf(g3w[j], sm[S_D3 + j], s);
     sm[S_D2 + tid] = sm[S_H2 + tid] > 0.f ? s : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
   {  // dz1 = relu'(h1) * W2f dz2: 4 lanes per row, 21 columns each
     const int i = tid >> 2, part = tid & 3;
     float s = 0.f;
     if (i < F1) {
-      const float* wp = W + o.f2w + i * F2 + part * 21;
-      float wv[21];
 #pragma unroll
-      for (int j = 0; j < 21; ++j) wv[j] = wp[j];
-#pragma unroll
-      for (int j = 0; j < 21; ++j) s = fmaf(wv[j], sm[S_D2 + part * 21 + j], s);
+      for (int j = 0; j < 21; ++j) s = fmaf(g2w[j], sm[S_D2 + part * 21 + j], s);
     }
     s += __shfl_xor(s, 1, 64);
     s += __shfl_xor(s, 2, 64);
     if (i < F1 && part == 0) sm[S_D1 + i] = sm[S_H1 + i] > 0.f ? s : 0.f;
   }
-  __syncthreads();
+  lds_barrier();
   if (tid < F0) {  // da2 = W1f dz1, through ReLU2 (pooled > 0) -> g2
-    const float4* wp = reinterpret_cast<const float4*>(W + o.f1w + tid * F1);
-    float4 wv[F1 / 4];
-#pragma unroll
-    for (int j4 = 0; j4 < F1 / 4; ++j4) wv[j4] = wp[j4];
+    const float4* wv = g1w;
     float s = 0.f;
 #pragma unroll
     for (int j4 = 0; j4 < F1 / 4; ++j4) {
@@ -371,7 +403,7 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
     if (tid < F2) del[F1 + tid] = sm[S_D2 + tid];
     if (tid < F3) del[F1 + F2 + tid] = sm[S_D3 + tid];
   }
-  __syncthreads();
+  lds_barrier();
 
   float* cp = a.convp + (size_t)img * CONVP_STRIDE;
   if (a.stop_phase == 4) return;
@@ -438,7 +470,7 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
         gp[0] = sp.x, gp[1] = sp.y;
       }
     }
-    __syncthreads();  // every dpre2 read is done: the T1 table may overwrite it
+    lds_barrier();  // every dpre2 read is done: the T1 table may overwrite it
     if (grp == 0 && p < P1 * P1) {
       const int py = p / P1, px = p % P1;
       for (int c = c_lo; c < c_hi; ++c) {
@@ -451,7 +483,7 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   if (a.stop_phase == 6) return;
   // ---- J: conv1 filter grad, sparse over the 196 argmax pixels per channel:
   // dW1[kh,kw,ci,c] = sum_p g1[p,c] * x[ci, u_p + kh, v_p + kw], for this
@@ -492,13 +524,18 @@ __global__ __launch_bounds__(NT) void image_kernel(const ImageArgs a) {
 }
 
 // ------------------------------------------------------------- update ----
-// Blocks: FC weight tiles of 16 input rows x all outputs (f1: 25, f2: 8,
-// f3: 6; tile 0 of each layer also reduces the bias), then 12 blocks of 256
-// conv parameters.  FC grads: g[i][j] = sum_n act[n][i] delta[n][j], act and
-// delta staged through LDS in chunks of 64 images.
-constexpr int UT = 16;
-constexpr int UB_F1 = F0 / UT, UB_F2 = (F1 + UT - 1) / UT, UB_F3 = (F2 + UT - 1) / UT;
-constexpr int UB_FC = UB_F1 + UB_F2 + UB_F3;
+// Blocks: FC weight gradients as fp32-MFMA tiles, g[i][j] = sum_n act[n][i]
+// delta[n][j] (M = inputs i, N = outputs j, K = the batch): one 32 x 32 tile a
+// wave, four a block (f1: 13 x 4, f2: 4 x 3, f3: 3 x 1 tiles; the row-0 tiles
+// also sum the bias), operands straight from L2 with every load of a 64-image
+// chunk in flight; then 12 blocks of 256 conv parameters.  (The round-4
+// VALU form - 16-row tiles on 39 blocks, LDS-staged deltas - was ~2/3 of the
+// 10.5 us update launch.)
+constexpr int FT_F1 = ((F0 + 31) / 32) * ((F1 + 31) / 32);  // 52
+constexpr int FT_F2 = ((F1 + 31) / 32) * ((F2 + 31) / 32);  // 12
+constexpr int FT_F3 = ((F2 + 31) / 32) * ((F3 + 31) / 32);  // 3
+constexpr int FT_ALL = FT_F1 + FT_F2 + FT_F3;
+constexpr int UB_FC = (FT_ALL + 3) / 4;
 constexpr int CONV_N = W1N + 8 + W2N + C2;  // 2874 slots (2872 used)
 constexpr int UB_CONV = (CONV_N + 255) / 256;
 
@@ -522,23 +559,23 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
                                                      float* __restrict__ g, float* __restrict__ m,
                                                      float mu, const float* lr_ptr,
                                                      long long* step) {
-  __shared__ float sa[64 * UT];
-  __shared__ float sd[64 * 128];
   const int tid = threadIdx.x;
   const float lr = APPLY ? *lr_ptr : 0.f;
   int blk = blockIdx.x;
   if (APPLY && blk == 0 && tid == 0) *step += 1;
   if (blk < UB_FC) {
-    int layer, tile;
-    if (blk < UB_F1) {
+    const int lane = tid & 63, ft = blk * 4 + (tid >> 6);
+    if (ft >= FT_ALL) return;
+    int layer, t;
+    if (ft < FT_F1) {
       layer = 0;
-      tile = blk;
-    } else if (blk < UB_F1 + UB_F2) {
+      t = ft;
+    } else if (ft < FT_F1 + FT_F2) {
       layer = 1;
-      tile = blk - UB_F1;
+      t = ft - FT_F1;
     } else {
       layer = 2;
-      tile = blk - UB_F1 - UB_F2;
+      t = ft - FT_F1 - FT_F2;
     }
     const int nin = layer == 0 ? F0 : (layer == 1 ? F1 : F2);
     const int nout = layer == 0 ? F1 : (layer == 1 ? F2 : F3);
@@ -546,85 +583,68 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
     const int doff = layer == 0 ? 0 : (layer == 1 ? F1 : F1 + F2);
     const int woff = layer == 0 ? o.f1w : (layer == 1 ? o.f2w : o.f3w);
     const int boff = layer == 0 ? o.f1b : (layer == 1 ? o.f2b : o.f3b);
-    const int i0 = tile * UT;
-    // thread -> (row i0 + r, columns j = c0 + 16 u); 16 rows x 16 column lanes, 8 columns each
-    const int r = tid >> 4, c0 = tid & 15;
-    // the SGD operands of this thread's weights are independent of the
-    // gradient: issued first, they arrive under the staging and the products
-    float wv[8], mv[8], bw[8], bm[8];
+    const int ntj = (nout + 31) / 32;
+    const int i0 = (t / ntj) * 32, j0 = (t % ntj) * 32;
+    const int l31 = lane & 31, kh = lane >> 5;
+    const int ia = min(i0 + l31, nin - 1), jb = min(j0 + l31, nout - 1);
+    const bool bias_tile = i0 == 0;
+    // the SGD operands of this lane's 16 weights (+ its bias) first: they are
+    // independent of the gradient and arrive under the products
+    float wv[16], mv[16], bwv = 0.f, bmv = 0.f;
     if (APPLY) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = c0 + 16 * u;
-        const bool ok = i0 + r < nin && j < nout;
-        const int wi = woff + (i0 + r) * nout + j;
-        wv[u] = ok ? w[wi] : 0.f;
-        mv[u] = ok ? m[wi] : 0.f;
-        const bool bok = tile == 0 && r == 0 && j < nout;
-        bw[u] = bok ? w[boff + j] : 0.f;
-        bm[u] = bok ? m[boff + j] : 0.f;
+      for (int q = 0; q < 16; ++q) {
+        const int wi = woff + min(i0 + mfma32_row(q, lane), nin - 1) * nout + jb;
+        wv[q] = w[wi];
+        mv[q] = m[wi];
+      }
+      if (bias_tile) {
+        bwv = w[boff + jb];
+        bmv = m[boff + jb];
       }
     }
-    float acc[8], bacc[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = bacc[u] = 0.f;
+    f32x16 acc = zero16();
+    float bs = 0.f;
     for (int n0 = 0; n0 < batch; n0 += 64) {
-      const int nn = min(64, batch - n0);
-      __syncthreads();
-      // all staging loads in flight before the LDS stores (one round trip)
-      float va[4], vd[32];
+      float av[32], dv[32];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int e = tid + 256 * k, n = e / UT, i = e % UT;
-        va[k] = (n < nn && i0 + i < nin) ? acts[(size_t)(n0 + n) * ACT_STRIDE + aoff + i0 + i]
-                                        : 0.f;
+      for (int st = 0; st < 32; ++st) {
+        const int n = min(n0 + 2 * st + kh, batch - 1);
+        av[st] = acts[(size_t)n * ACT_STRIDE + aoff + ia];
+        dv[st] = deltas[(size_t)n * DELTA_STRIDE + doff + jb];
       }
+      // every load of the chunk issued before the first product
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int k = 0; k < 32; ++k) {
-        const int e = tid + 256 * k, n = e >> 7, j = e & 127;
-        vd[k] = (n < nn && j < nout) ? deltas[(size_t)(n0 + n) * DELTA_STRIDE + doff + j] : 0.f;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sa[tid + 256 * k] = va[k];
-#pragma unroll
-      for (int k = 0; k < 32; ++k) sd[tid + 256 * k] = vd[k];
-      __syncthreads();
-      for (int n = 0; n < nn; ++n) {
-        const float av = sa[n * UT + r];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const float dv = sd[n * 128 + c0 + 16 * u];
-          acc[u] = fmaf(av, dv, acc[u]);
-          if (tile == 0) bacc[u] += dv;  // block-uniform: the bias row
-        }
+      for (int st = 0; st < 32; ++st) {
+        const bool ok = n0 + 2 * st + kh < batch;
+        const float d = ok ? dv[st] : 0.f;
+        acc = mfma32x32x2(av[st], d, acc);
+        bs += d;
       }
     }
-    if (i0 + r < nin) {
+    bs += __shfl_xor(bs, 32, 64);
+    if (j0 + l31 < nout) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = c0 + 16 * u;
-        if (j >= nout) continue;
-        const int wi = woff + (i0 + r) * nout + j;
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + mfma32_row(q, lane);
+        if (i >= nin) continue;
+        const int wi = woff + i * nout + j0 + l31;
         if (APPLY) {
-          const float mn = mu * mv[u] + acc[u];
+          const float mn = mu * mv[q] + acc[q];
           m[wi] = mn;
-          w[wi] = wv[u] - lr * mn;
+          w[wi] = wv[q] - lr * mn;
         } else {
-          g[wi] = acc[u];
+          g[wi] = acc[q];
         }
       }
-    }
-    if (tile == 0 && r == 0) {
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int j = c0 + 16 * u;
-        if (j >= nout) continue;
+      if (bias_tile && kh == 0) {
         if (APPLY) {
-          const float mn = mu * bm[u] + bacc[u];
-          m[boff + j] = mn;
-          w[boff + j] = bw[u] - lr * mn;
+          const float mn = mu * bmv + bs;
+          m[boff + j0 + l31] = mn;
+          w[boff + j0 + l31] = bwv - lr * mn;
         } else {
-          g[boff + j] = bacc[u];
+          g[boff + j0 + l31] = bs;
         }
       }
     }
