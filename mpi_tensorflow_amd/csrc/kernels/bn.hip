@@ -257,6 +257,49 @@ __global__ __launch_bounds__(256) void finalize_kernel(const float* __restrict__
                 (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]), rows);
 }
 
+// Pass 2 for the conv-epilogue layout with few partial rows (P <= 128: the
+// deep layers): one block per 64-channel group, lane = channel, so every load
+// is a coalesced 256-byte row, and wave w sums rows w, w + 4, ... (all of a
+// lane's <= 32 loads in flight at once); the 4 wave sums are added in order.
+// (finalize_kernel's block per channel reads each row 64 times over, strided,
+// and launches C blocks for a few dozen partials: ~5.5 us a call.)
+constexpr int FIN64_MAXP = 128;
+__global__ __launch_bounds__(256) void finalize64_kernel(const float* __restrict__ part, int nb,
+                                                         int C, long long rows, Fin fin) {
+  __shared__ float red[2][4][64];
+  const int grp = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t base = (size_t)grp * nb * 64 + lane, half = (size_t)C * nb;
+  constexpr int PER = FIN64_MAXP / 4;
+  float va[PER], vb[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const int r = wave + 4 * k;
+    va[k] = r < nb ? part[base + (size_t)r * 64] : 0.f;
+    vb[k] = r < nb ? part[half + base + (size_t)r * 64] : 0.f;
+  }
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    a += va[k];
+    b += vb[k];
+  }
+  red[0][wave][lane] = a;
+  red[1][wave][lane] = b;
+  __syncthreads();
+  if (tid < 64)
+    fin_channel(fin, grp * 64 + tid, (red[0][0][tid] + red[0][1][tid]) + (red[0][2][tid] + red[0][3][tid]),
+                (red[1][0][tid] + red[1][1][tid]) + (red[1][2][tid] + red[1][3][tid]), rows);
+}
+
+// the conv-epilogue layout [2][C / 64][P][64] -> fin
+static void finalize_grp64(const float* part, int P, int C, long long rows, const Fin& fin,
+                           hipStream_t st) {
+  if (P <= FIN64_MAXP)
+    finalize64_kernel<<<C / 64, 256, 0, st>>>(part, P, C, rows, fin);
+  else
+    finalize_kernel<<<C, 256, 0, st>>>(part, P, C, rows, fin, 1);
+}
+
 // y = (x - mean) rstd g + b (+ res) (relu); eval: mean / var from running stats
 template <bool XB>
 __global__ __launch_bounds__(256) void apply_kernel(const void* __restrict__ x,
@@ -447,7 +490,7 @@ void bn_fwd_partials(const float* part, int P, const float* shift, const void* x
   uint2* ybv = reinterpret_cast<uint2*>(yb);
   // fp32 shift (the running mean, read by fin_channel before its update)
   const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, shift, 0};
-  bn::finalize_kernel<<<C, 256, 0, st>>>(part, P, C, rows, fin, 1);
+  bn::finalize_grp64(part, P, C, rows, fin, st);
   if (xb16)
     bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
                                                                relu ? 1 : 0, 0, eps, ybv);
@@ -490,7 +533,7 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
   if (C % 64 != 0 || C > 1024 || P < 1 || !part || (!dx && !dxb) || (relu && !y))
     throw std::runtime_error("bn_bwd_partials: needs C % 64 == 0, C <= 1024, a dx output");
   // the dgrad epilogue's rows [2][C / 64][P][64] -> db, dg
-  bn::finalize_kernel<<<C, 256, 0, st>>>(part, P, C, rows, sums(db, dg), 1);
+  bn::finalize_grp64(part, P, C, rows, sums(db, dg), st);
   const long long n4 = rows * C / 4;
   bn::bwd_apply_kernel<true, true><<<bn::grid_elems(n4), 256, 0, st>>>(
       x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0,
