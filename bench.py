@@ -62,7 +62,7 @@ def parse(argv=None):
     ap.add_argument("--no-eval", action="store_true")
     ap.add_argument("--sync-schedule", default="auto",
                     choices=("auto", "buckets", "sharded", "split", "factors", "serial", "defer",
-                             "xgmi", "xgmi-step"))
+                             "xgmi", "xgmi-step", "xgmi-fac"))
     ap.add_argument("--defer-split", type=float, default=0.5,
                     help="defer schedule: fraction of the FC bucket reduced under the conv backward")
     ap.add_argument("--comm", default="auto", choices=("auto", "rccl", "shm", "xgmi", "torch"),

@@ -68,7 +68,7 @@ SYNC_MODES = ("grad", "param_avg", "none")
 # "xgmi" = the peer-to-peer xGMI communicator's fused sync + SGD launch (MNIST,
 # csrc/xgmi_comm.h; one node)
 SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "defer", "xgmi",
-                  "xgmi-step")
+                  "xgmi-step", "xgmi-fac")
 # device communicator (world > 1): "auto" = native RCCL when every rank has a
 # GPU of its own, the shared-memory host-staged communicator when ranks share
 # GPUs (the reference's layout: every rank on /GPU:0, quirk Q13); "rccl",

@@ -790,6 +790,7 @@ PYBIND11_MODULE(_C, m) {
       .def("set_defer_split", &MnistExecutor::set_defer_split)
       .def("set_xgmi", &MnistExecutor::set_xgmi, py::keep_alive<1, 2>())
       .def("xgmi_ok", &MnistExecutor::xgmi_ok)
+      .def("xgmi_fac_ok", &MnistExecutor::xgmi_fac_ok)
       .def("set_xgmi_fc_in_bwd", &MnistExecutor::set_xgmi_fc_in_bwd)
       .def("set_xgmi_xconv", &MnistExecutor::set_xgmi_xconv)
       .def_property_readonly("defer_split", &MnistExecutor::defer_split)
@@ -826,6 +827,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("MnistExecutor").attr("SCHED_DEFER") = (int)MnistExecutor::SCHED_DEFER;
   m.attr("MnistExecutor").attr("SCHED_XGMI") = (int)MnistExecutor::SCHED_XGMI;
   m.attr("MnistExecutor").attr("SCHED_XGMI_STEP") = (int)MnistExecutor::SCHED_XGMI_STEP;
+  m.attr("MnistExecutor").attr("SCHED_XGMI_FAC") = (int)MnistExecutor::SCHED_XGMI_FAC;
 
   // ----------------------------------------------------------------- IDX
   // pre-uploads an instantiated graph (torch CUDAGraph.raw_cuda_graph_exec())

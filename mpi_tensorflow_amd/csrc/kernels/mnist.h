@@ -251,10 +251,41 @@ struct XgmiStepArgs {
   // buffer and the conv blocks keep the closing "done reading" barrier
   float* xc[xgmi::kMaxRanks] = {};
   long long cstride = 0;
+  // SCHED_XGMI_FAC: the FC grads are already the global sums (formed from the
+  // gathered factors, launch_xgmi_fac_gather + launch_fc1_bwd_weights): the FC
+  // blocks apply the momentum SGD to the whole bucket locally - no FC exchange,
+  // no FC barrier, replicated FC momentum
+  int fc_local = 0;
+  // fc_local: the FC factors of every rank (rank-major, frows = N x B rows):
+  // the fc1 weight's gradient tiles are formed and applied in the step launch
+  // (fc1_dw_sgd, K = frows); the small FC grads come from launch_fc1_small_grads
+  const float* fa2 = nullptr;
+  const float* fdh = nullptr;
+  int frows = 0, off_w3 = 0;
   // labs: per block 6 clock stamps (100 MHz) of xgmi_step_kernel, or null
   unsigned long long* prof = nullptr;
 };
 void launch_xgmi_step(const XgmiStepArgs& a, hipStream_t s);
+// SCHED_XGMI_FAC factor gather: nbuf rank-major gathered buffers (slot r =
+// rank r's rows, slot4[k] float4s a slot); every rank copies each peer's own
+// slot out of that peer's buffer (buf[k][r]: rank r's buffer k) over its link,
+// after an arrival barrier (the peers' forward / head kernels wrote them)
+struct XgmiFacArgs {
+  xgmi::Sync sync;
+  static constexpr int kBufs = 4;
+  float* buf[kBufs][xgmi::kMaxRanks] = {};
+  long long slot4[kBufs] = {};
+};
+void launch_xgmi_fac_gather(const XgmiFacArgs& a, hipStream_t s);
+// fc1 backward dX (roles == 1 grid of launch_fc1_bwd) with the SCHED_XGMI_FAC
+// factor gather as extra role blocks (the factors are final after the head)
+void launch_fc1_bwd_dx_fac_gather(const float* a2, const uint8_t* idx2, const float* dh,
+                                  const float* w1, int batch, float* dy2, float* dy2t,
+                                  const XgmiFacArgs& f, hipStream_t s);
+// fc2 / bias grads (dW2, db2, db1) over `rows` gathered rows (the small role of
+// launch_fc1_bwd_weights alone)
+void launch_fc1_small_grads(const float* dh, const float* hd, const float* dlog, int rows,
+                            float* g_b3, float* g_w4, float* g_b4, hipStream_t s);
 // FC role geometry for `threads`-thread blocks (<= max_blocks, rounded up to 8)
 void xgmi_fc_plan(XgmiStepArgs& a, int threads, int max_blocks);
 // floats of one parity half of the conv-grad exchange buffer (off_b1: the

@@ -2934,6 +2934,55 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
     xgmi_fc_gather(a, blockIdx.x, a.ngather);
     return;
   }
+  if (a.fc_local && a.fa2 && (int)blockIdx.x < a.nfc) {
+    // ---- FC bucket from the gathered factors: the fc1 weight tiles (dW1 over
+    // every rank's rows + SGD, fc1_dw_sgd), then the rest of the bucket
+    // streamed (its grads from launch_fc1_small_grads)
+    FcSgd f{};
+    f.w = a.w[me];
+    f.g = a.g[me];
+    f.m = a.mom;
+    f.n4 = a.fc4;
+    f.l2 = a.l2;
+    f.mu = a.momentum;
+    f.lr = a.lr;
+    f.nblk = a.nfc - FC1BWD_DW_BLOCKS;
+    f.w1_off4 = a.off_w3 / 4;
+    f.gs = a.gscale;
+    f.a2 = a.fa2;
+    f.dh = a.fdh;
+    f.batch = a.frows;
+    if ((int)blockIdx.x < FC1BWD_DW_BLOCKS)
+      fc1_dw_sgd(f, blockIdx.x, tid);
+    else
+      fc_sgd_role(f, blockIdx.x - FC1BWD_DW_BLOCKS, nullptr, tid);
+    return;
+  }
+  if (a.fc_local && (int)blockIdx.x < a.nfc) {  // ---- FC bucket, grads already global sums
+    float4* W4 = reinterpret_cast<float4*>(a.w[me]);
+    float4* M4 = reinterpret_cast<float4*>(a.mom);
+    const float4* G4 = reinterpret_cast<const float4*>(a.g[me]);
+    const long long stride = (long long)a.nfc * 256;
+    for (long long i0 = (long long)blockIdx.x * 256 + tid; i0 < a.fc4; i0 += stride * XS_UNROLL) {
+      float4 wv[XS_UNROLL], mv[XS_UNROLL], gv[XS_UNROLL];
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u) {
+        const long long i = min(i0 + stride * u, a.fc4 - 1);
+        wv[u] = W4[i];
+        mv[u] = M4[i];
+        gv[u] = G4[i];
+      }
+#pragma unroll
+      for (int u = 0; u < XS_UNROLL; ++u) {
+        const long long i = i0 + stride * u;
+        if (i >= a.fc4) continue;
+        sgd4(wv[u], mv[u], gv[u], a.l2, lr, a.momentum, a.gscale);
+        W4[i] = wv[u];
+        M4[i] = mv[u];
+      }
+    }
+    return;
+  }
   if ((int)blockIdx.x < a.nfc) {  // ---- FC bucket: this rank's segment, then the gather
     xgmi_fc_role(a, &ep);
     if (a.prof && threadIdx.x == 0) a.prof[6 * blockIdx.x] |= 1ull << 60;  // role tag: FC
@@ -3076,7 +3125,19 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
     throw std::runtime_error("xgmi_step: Winograd transforms need both U and Ud");
   if (!a.part2 || !a.part1 || a.ngroups <= 0 || a.nblk1 <= 0 || a.off_w2 % 4)
     throw std::runtime_error("xgmi_step: conv slabs / offsets");
-  if (a.fc_in_bwd) {
+  if (a.fc_local && a.fa2) {
+    // fc1 weight tiles + the rest of the bucket in streaming units
+    if (!a.fdh || a.frows <= 0 || a.off_w3 % 4 || a.off_w3 / 4 + W1_F4 > a.fc4)
+      throw std::runtime_error("xgmi_step: FC factors / fc1 weight offset");
+    a.fc_in_bwd = 0;
+    a.nfc = FC1BWD_DW_BLOCKS + (int)((a.fc4 - W1_F4 + 256 * FC_SGD_UNROLL - 1) / (256 * FC_SGD_UNROLL));
+    a.ngather = 0;
+  } else if (a.fc_local) {
+    // the FC grads are global sums: a local streaming SGD of the whole bucket
+    a.fc_in_bwd = 0;
+    a.nfc = a.sync.lean ? 32 : 256;
+    a.ngather = 0;
+  } else if (a.fc_in_bwd) {
     // the exchange + SGD ran in the conv2 backward launch; this one gathers
     a.fc4 = in.fc4;
     a.seg4 = a.fc4 / n;
@@ -3092,6 +3153,115 @@ void launch_xgmi_step(const XgmiStepArgs& in, hipStream_t s) {
   // chip), or XS_CONV_BLOCKS looping over them when the ranks share a GPU
   a.ncv = a.sync.lean ? XS_CONV_BLOCKS : (a.wino_u ? 128 : 50) + 16 + 208;
   xgmi_step_kernel<<<a.nfc + a.ngather + a.ncv, 256, 0, s>>>(a);
+}
+
+// SCHED_XGMI_FAC: every peer's factor rows over its link (see XgmiFacArgs).
+// Block b copies slice b of every (buffer, peer) slot, all of a thread's loads
+// in flight together.  No closing barrier: a peer rewrites its slot only in its
+// next step's forward, after its step launch's conv barrier, which waits for
+// this rank's step launch - queued behind this copy.
+__device__ void xgmi_fac_gather_block(const XgmiFacArgs& a, int gb, int ngb, unsigned* ep) {
+  const xgmi::Sync& s = a.sync;
+  const int n = s.nranks, me = s.rank, tid = threadIdx.x;
+  const unsigned e = xgmi::next_epoch(s, ep);
+  xgmi::barrier(s, 0, e, /*release=*/true);  // the rows come from the forward / head kernels
+  const long long t0 = xgmi::now_ticks();
+  long long bytes = 0;
+#pragma unroll
+  for (int k = 0; k < XgmiFacArgs::kBufs; ++k) {
+    const long long n4 = a.slot4[k];
+    bytes += n4 * 16;
+    if (n4 == 0) continue;
+    const long long per = ((n4 + ngb - 1) / ngb + 255) / 256 * 256;
+    const long long lo = (long long)gb * per, hi = min(lo + per, n4);
+    float4* mine = reinterpret_cast<float4*>(a.buf[k][me]);
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * XS_UNROLL) {
+      float4 v[xgmi::kMaxRanks][XS_UNROLL];
+#pragma unroll
+      for (int r = 0; r < xgmi::kMaxRanks; ++r)
+#pragma unroll
+        for (int u = 0; u < XS_UNROLL; ++u)
+          if (r < n && r != me && i0 + 256 * u < hi) {
+            const xgmi::Rsrc rs = xgmi::rsrc(a.buf[k][r], (unsigned long long)n * n4 * 16);
+            v[r][u] = xgmi::ld4_sys(rs, (unsigned)(((long long)r * n4 + i0 + 256 * u) * 16));
+          }
+#pragma unroll
+      for (int r = 0; r < xgmi::kMaxRanks; ++r)
+#pragma unroll
+        for (int u = 0; u < XS_UNROLL; ++u)
+          if (r < n && r != me && i0 + 256 * u < hi) mine[(long long)r * n4 + i0 + 256 * u] = v[r][u];
+    }
+  }
+  xgmi::link_floor(s, t0, bytes);
+}
+
+__global__ __launch_bounds__(256) void xgmi_fac_gather_kernel(const XgmiFacArgs a) {
+  __shared__ unsigned ep;
+  xgmi_fac_gather_block(a, blockIdx.x, gridDim.x, &ep);
+}
+
+// fc1 dX blocks | factor gather blocks (the gather's barrier slots are its
+// own block indices 0 .. ngb - 1: the flag protocol is per block index)
+__global__ __launch_bounds__(256) void fc1_bwd_dx_fac_kernel(
+    const float* __restrict__ a2, const uint8_t* __restrict__ idx2, const float* __restrict__ dh,
+    const float* __restrict__ w1, int batch, float* __restrict__ dy2, float* __restrict__ dy2t,
+    int ngb, const XgmiFacArgs f) {
+  __shared__ float smem[4 * FC1DX_WAVE];
+  if ((int)blockIdx.x < ngb) {
+    xgmi_fac_gather_block(f, blockIdx.x, ngb, reinterpret_cast<unsigned*>(smem));
+    return;
+  }
+  const int nb = (int)gridDim.x - ngb;
+  const int L = xcd_remap((int)blockIdx.x - ngb, nb);
+  fc1_bwd_dx(L, a2, idx2, dh, w1, batch, dy2, dy2t, smem);
+}
+
+static void check_fac(const XgmiFacArgs& a) {
+  const int n = a.sync.nranks;
+  if (n < 1 || n > xgmi::kMaxRanks || !a.sync.flags || !a.sync.epoch || !a.sync.error)
+    throw std::runtime_error("xgmi_fac_gather: communicator not set up");
+  for (int k = 0; k < XgmiFacArgs::kBufs; ++k)
+    for (int r = 0; r < n; ++r)
+      if (a.slot4[k] > 0 && !a.buf[k][r])
+        throw std::runtime_error("xgmi_fac_gather: a rank's factor buffer is not mapped");
+}
+
+void launch_fc1_bwd_dx_fac_gather(const float* a2, const uint8_t* idx2, const float* dh,
+                                  const float* w1, int batch, float* dy2, float* dy2t,
+                                  const XgmiFacArgs& f, hipStream_t s) {
+  if (batch <= 0 || batch % 32 != 0) throw std::runtime_error("fc1_bwd: batch % 32 != 0");
+  check_fac(f);
+  // 196 dX blocks at B = 64 + 56 gather blocks: one round on 256 CUs
+  const int ndx = (batch / 32) * (FC1_IN / 32);
+  const int ngb = f.sync.lean ? 16 : std::max(16, std::min(128, 256 - ndx));
+  fc1_bwd_dx_fac_kernel<<<ngb + ndx, 256, 0, s>>>(a2, idx2, dh, w1, batch, dy2, dy2t, ngb, f);
+}
+
+__global__ __launch_bounds__(256) void fc1_small_grads_kernel(const float* __restrict__ dh,
+                                                              const float* __restrict__ hd,
+                                                              const float* __restrict__ dlog,
+                                                              int rows, float* __restrict__ g_b3,
+                                                              float* __restrict__ g_w4,
+                                                              float* __restrict__ g_b4) {
+  __shared__ float smem[FC1_SMALL_SMEM];
+  fc1_small_grads(blockIdx.x, hd, dh, dlog, rows, g_w4, g_b4, g_b3, smem);
+}
+
+void launch_fc1_small_grads(const float* dh, const float* hd, const float* dlog, int rows,
+                            float* g_b3, float* g_w4, float* g_b4, hipStream_t s) {
+  if (rows <= 0 || rows % 32 != 0) throw std::runtime_error("fc1_small_grads: rows % 32 != 0");
+  fc1_small_grads_kernel<<<SMALL_BLOCKS, 256, 0, s>>>(dh, hd, dlog, rows, g_b3, g_w4, g_b4);
+}
+
+void launch_xgmi_fac_gather(const XgmiFacArgs& a, hipStream_t s) {
+  const int n = a.sync.nranks;
+  if (n < 1 || n > xgmi::kMaxRanks || !a.sync.flags || !a.sync.epoch || !a.sync.error)
+    throw std::runtime_error("xgmi_fac_gather: communicator not set up");
+  for (int k = 0; k < XgmiFacArgs::kBufs; ++k)
+    for (int r = 0; r < n; ++r)
+      if (a.slot4[k] > 0 && !a.buf[k][r])
+        throw std::runtime_error("xgmi_fac_gather: a rank's factor buffer is not mapped");
+  xgmi_fac_gather_kernel<<<a.sync.lean ? 16 : 128, 256, 0, s>>>(a);
 }
 
 void launch_grad_finalize(const float* part2, int ngroups, const float* part1, int nblk1,

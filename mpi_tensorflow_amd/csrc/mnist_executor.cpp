@@ -45,7 +45,8 @@ MnistExecutor::~MnistExecutor() {
 // ev_dw_ is recorded when the FC bucket (bucket 1) of the grads is final.
 void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                                     const mnist::FcSgdArgs* fc_sgd, bool factors, bool fresh,
-                                    bool fc1_dw_fused, const mnist::XgmiStepArgs* xfc) {
+                                    bool fc1_dw_fused, const mnist::XgmiStepArgs* xfc,
+                                    const mnist::XgmiFacArgs* xfac) {
   if (p_.bf16) {
     if (factors) throw std::runtime_error("MnistExecutor: SCHED_FACTORS is fp32 only");
     return enqueue_fwd_bwd_bf16(s, finalize, fc_sgd, fresh);
@@ -91,13 +92,19 @@ void MnistExecutor::enqueue_fwd_bwd(hipStream_t s, bool finalize,
                               P<float>(p.dh), P<float>(p.dlog), P<float>(p.loss_rows),
                               P<float>(p.lr), P<int>(p.correct), s, nullptr, nullptr,
                               fc1_t ? mnist::fc1_train_t_splits() : mnist::fc1_train_splits());
-  if (factors) HIP_CHECK(hipEventRecord(ev_fac_, s));
+  if (factors && sched_ == SCHED_FACTORS) HIP_CHECK(hipEventRecord(ev_fac_, s));
   // backward: fc1 dX (+pool2/ReLU2 scatter) | dW1 | fc2 grads, one launch
-  mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
-                        P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
-                        G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4, P<float>(p.dy2),
-                        p.wino ? nullptr : P<float>(p.dy2t), s,
-                        factors ? 1 : (fc1_dw_fused ? 5 : 7));
+  // (SCHED_XGMI_FAC: dX | the peers' factor rows over the links)
+  if (xfac)
+    mnist::launch_fc1_bwd_dx_fac_gather(P<const float>(p.a2), P<const uint8_t>(p.idx2),
+                                        P<const float>(p.dh), W + p.off_w3, B, P<float>(p.dy2),
+                                        p.wino ? nullptr : P<float>(p.dy2t), *xfac, s);
+  else
+    mnist::launch_fc1_bwd(P<const float>(p.a2), P<const uint8_t>(p.idx2), P<const float>(p.dh),
+                          P<const float>(p.hd), P<const float>(p.dlog), W + p.off_w3, B,
+                          G + p.off_w3, G + p.off_b3, G + p.off_w4, G + p.off_b4,
+                          P<float>(p.dy2), p.wino ? nullptr : P<float>(p.dy2t), s,
+                          factors ? 1 : (fc1_dw_fused ? 5 : 7));
   HIP_CHECK(hipEventRecord(ev_dw_, s));
   // conv1 filter grad: Winograd - in the bwd-data blocks' epilogue, from the
   // dA1 values they produce; direct - role blocks of the filter-grad launch
@@ -313,7 +320,7 @@ void MnistExecutor::refresh_shadows(hipStream_t s) {
 void MnistExecutor::set_schedule(int sched) {
   if (sched != SCHED_BUCKETS && sched != SCHED_SHARDED_FC && sched != SCHED_SPLIT &&
       sched != SCHED_FACTORS && sched != SCHED_SERIAL && sched != SCHED_DEFER &&
-      sched != SCHED_XGMI && sched != SCHED_XGMI_STEP)
+      sched != SCHED_XGMI && sched != SCHED_XGMI_STEP && sched != SCHED_XGMI_FAC)
     throw std::runtime_error("MnistExecutor: unknown sync schedule");
   if (fc_pending_)
     throw std::runtime_error("MnistExecutor: join() the stream before changing the schedule");
@@ -349,6 +356,20 @@ bool MnistExecutor::xgmi_ok() const {
          xgmi_->registered(P<const void>(p_.params), fb);
 }
 
+// the factor schedule over xGMI: fp32 Winograd, the rank-major factor
+// buffers sized for this communicator and mapped on every rank
+bool MnistExecutor::xgmi_fac_ok() const {
+  if (!xgmi_ok() || p_.bf16 || !p_.wino) return false;
+  const int n = xgmi_->size();
+  if (n < 2 || n != p_.fac_ranks || !p_.a2_all || !p_.dh_all || !p_.hd_all || !p_.dlog_all)
+    return false;
+  const size_t B = (size_t)p_.batch;
+  return xgmi_->registered(P<const void>(p_.a2_all), n * B * kFc1In * sizeof(float)) &&
+         xgmi_->registered(P<const void>(p_.dh_all), n * B * kFc1Out * sizeof(float)) &&
+         xgmi_->registered(P<const void>(p_.hd_all), n * B * kFc1Out * sizeof(float)) &&
+         xgmi_->registered(P<const void>(p_.dlog_all), n * B * kNcls * sizeof(float));
+}
+
 void MnistExecutor::set_defer_split(float f) {
   if (!(f > 0.f && f < 1.f)) throw std::runtime_error("MnistExecutor: defer split must be in (0, 1)");
   defer_split_ = f;
@@ -369,6 +390,10 @@ void MnistExecutor::train_step(hipStream_t s, Collective* comm, hipStream_t cs,
                                Collective* comm2) {
   if ((sched_ == SCHED_XGMI || sched_ == SCHED_XGMI_STEP) && xgmi_ok()) {  // no comm stream
     train_step_xgmi(s);
+    return;
+  }
+  if (sched_ == SCHED_XGMI_FAC && xgmi_fac_ok()) {
+    train_step_xgmi_fac(s);
     return;
   }
   if (comm == nullptr) {  // single rank (or caller-driven parameter averaging)
@@ -679,11 +704,10 @@ void MnistExecutor::train_step_defer(hipStream_t s, Collective* comm, hipStream_
 // momentum is sharded (each rank keeps its own segment current):
 // gather_optimizer_state() before reading it.  bf16: the FC update writes no
 // fc1 shadows, so the next step re-derives them (fresh = false).
-void MnistExecutor::train_step_xgmi(hipStream_t s) {
+mnist::XgmiStepArgs MnistExecutor::xgmi_step_args() const {
   const MnistPtrs& p = p_;
   XgmiComm* x = xgmi_;
   const int n = x->size();
-  wait_fc_params(s);
   mnist::XgmiStepArgs a;
   a.sync = x->sync();
   for (int r = 0; r < n; ++r) {
@@ -715,6 +739,13 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
     a.wino_u = P<float>(p.wino_u);
     a.wino_ud = P<float>(p.wino_ud);
   }
+  return a;
+}
+
+void MnistExecutor::train_step_xgmi(hipStream_t s) {
+  const MnistPtrs& p = p_;
+  wait_fc_params(s);
+  mnist::XgmiStepArgs a = xgmi_step_args();
   // fp32 Winograd: the FC exchange + SGD ride as the first blocks of the
   // merged conv2 backward launch (its grads are final after fc1 backward), so
   // the link time overlaps the conv backward; the step launch then syncs the
@@ -727,8 +758,48 @@ void MnistExecutor::train_step_xgmi(hipStream_t s) {
   if (p.bf16) shadows_stale_ = true;
 }
 
+// SCHED_XGMI_FAC: forward (the factor rows land in this rank's slots of the
+// rank-major buffers) | fc1 dX only | conv2 backward; the peers' factor rows
+// over the links; the FC gradients over all N x B rows (the exact global
+// sums, formed in one fixed order on every rank); the step launch: local FC
+// SGD + the conv sync.  No FC exchange, no FC momentum shard.
+void MnistExecutor::train_step_xgmi_fac(hipStream_t s) {
+  const MnistPtrs& p = p_;
+  XgmiComm* x = xgmi_;
+  const int n = x->size();
+  wait_fc_params(s);
+  mnist::XgmiFacArgs f;
+  f.sync = x->sync();
+  const size_t B = (size_t)p.batch;
+  const uintptr_t bufs[4] = {p.a2_all, p.dh_all, p.hd_all, p.dlog_all};
+  const size_t rows[4] = {B * kFc1In, B * kFc1Out, B * kFc1Out, B * kNcls};
+  for (int k = 0; k < 4; ++k) {
+    if (rows[k] % 4) throw std::runtime_error("xgmi_fac: factor slot not a multiple of 4 floats");
+    f.slot4[k] = (long long)(rows[k] / 4);
+    for (int r = 0; r < n; ++r)
+      f.buf[k][r] = static_cast<float*>(x->peer_ptr(reinterpret_cast<const void*>(bufs[k]), r));
+  }
+  // forward; fc1 dX | the factor gather; conv2 backward
+  enqueue_fwd_bwd(s, /*finalize=*/false, nullptr, /*factors=*/true, take_fresh(true), false,
+                  nullptr, &f);
+  // the fc2 / bias grads over every rank's rows; the fc1 weight's are formed
+  // and applied by the step launch's FC tiles
+  float* G = P<float>(p.grads);
+  mnist::launch_fc1_small_grads(P<const float>(p.dh_all), P<const float>(p.hd_all),
+                                P<const float>(p.dlog_all), n * p.batch, G + p.off_b3,
+                                G + p.off_w4, G + p.off_b4, s);
+  mnist::XgmiStepArgs a = xgmi_step_args();
+  a.fc_local = 1;
+  a.fa2 = P<const float>(p.a2_all);
+  a.fdh = P<const float>(p.dh_all);
+  a.frows = n * p.batch;
+  a.off_w3 = (int)p.off_w3;
+  mnist::launch_xgmi_step(a, s);
+}
+
 void MnistExecutor::gather_optimizer_state(hipStream_t s, Collective* comm, hipStream_t cs) {
   wait_fc_params(s);
+  if (sched_ == SCHED_XGMI_FAC) return;  // every FC / conv momentum is replicated
   if ((sched_ == SCHED_XGMI || sched_ == SCHED_XGMI_STEP) && xgmi_ok()) {  // FC momentum segments
     xgmi_->gather_segments(P<float>(p_.mom), (size_t)p_.bucket1, s);
     return;

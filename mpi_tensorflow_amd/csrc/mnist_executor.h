@@ -77,6 +77,7 @@ struct MnistPtrs {
 namespace mnist {
 struct FcSgdArgs;
 struct XgmiStepArgs;
+struct XgmiFacArgs;
 }
 
 class MnistExecutor {
@@ -123,13 +124,20 @@ class MnistExecutor {
   //                      FC exchange + SGD ride as role blocks of the conv2
   //                      backward launch (overlapping its link time with the
   //                      conv backward);
+  //   SCHED_XGMI_FAC   - fp32: the FC factors (a2, dh, hd, dlog: 1.07 MB a
+  //                      rank at B = 64, against a 6.4 MB FC gradient) copied
+  //                      from every peer over its link (train_step_xgmi_fac),
+  //                      the FC gradients formed from them with K = N x B
+  //                      (the global sums, the same on every rank) and applied
+  //                      locally; the conv sync as SCHED_XGMI_STEP.  Few
+  //                      ranks: one link per peer carries 1/6 of the bytes.
   //   SCHED_XGMI_STEP  - the same with the whole FC exchange in the step
   //                      launch (no CUs taken from the conv backward: its 512
   //                      blocks are 2 exact rounds on 256 CUs, role blocks add a
   //                      third; the auto-tune picks by the real link speed).
   static constexpr int SCHED_BUCKETS = 0, SCHED_SHARDED_FC = 1, SCHED_SPLIT = 2,
                        SCHED_FACTORS = 3, SCHED_SERIAL = 4, SCHED_DEFER = 5, SCHED_XGMI = 6,
-                       SCHED_XGMI_STEP = 7;
+                       SCHED_XGMI_STEP = 7, SCHED_XGMI_FAC = 8;
   // the peer-to-peer communicator of SCHED_XGMI: the flat grads and params must
   // be registered with it (XgmiComm::open_buffer / emulate_buffer)
   void set_xgmi(XgmiComm* x) { xgmi_ = x; }
@@ -141,6 +149,7 @@ class MnistExecutor {
   // (default) or in the step launch (= SCHED_XGMI_STEP; labs)
   void set_xgmi_fc_in_bwd(bool on) { xgmi_fc_in_bwd_ = on; }
   bool xgmi_ok() const;
+  bool xgmi_fac_ok() const;
   void set_schedule(int sched);
   int schedule() const { return sched_; }
   bool sharded_ok(int nranks) const;
@@ -203,7 +212,8 @@ class MnistExecutor {
   void enqueue_fwd_bwd(hipStream_t s, bool finalize = true,
                        const mnist::FcSgdArgs* fc_sgd = nullptr, bool factors = false,
                        bool fresh = false, bool fc1_dw_fused = false,
-                       const mnist::XgmiStepArgs* xfc = nullptr);
+                       const mnist::XgmiStepArgs* xfc = nullptr,
+                       const mnist::XgmiFacArgs* xfac = nullptr);
   // the fused SGD launch applies (L2 prefix == the FC bucket, as in the
   // reference layout)
   bool fused_sgd_ok() const;
@@ -219,6 +229,8 @@ class MnistExecutor {
   void train_step_serial(hipStream_t s, Collective* comm);
   void train_step_defer(hipStream_t s, Collective* comm, hipStream_t cs);
   void train_step_xgmi(hipStream_t s);
+  void train_step_xgmi_fac(hipStream_t s);
+  mnist::XgmiStepArgs xgmi_step_args() const;
   XgmiComm* xgmi_ = nullptr;
   uintptr_t xconv_ = 0;
   bool xgmi_fc_in_bwd_ = true;

@@ -235,10 +235,10 @@ class NativeMnistEngine(MnistEngineBase):
         hcomm = comm.native_handle if (self.grad_sync and comm is not None) else None
         nfac = hcomm.size if hcomm is not None else 1
         self.comm_is_xgmi = isinstance(comm, XgmiDeviceComm)
-        if nfac > 1 and not self.bf16 and not self.comm_is_xgmi:
-            # SCHED_FACTORS: rank-major gathered FC factors; this rank's forward /
-            # head kernels write their slot in place (csrc/mnist_executor.cpp
-            # train_step_factors).  Sized by the communicator (an emulated
+        if nfac > 1 and not self.bf16:
+            # SCHED_FACTORS / SCHED_XGMI_FAC: rank-major gathered FC factors;
+            # this rank's forward / head kernels write their slot in place
+            # (csrc/mnist_executor.cpp train_step_factors, train_step_xgmi_fac).  Sized by the communicator (an emulated
             # N-rank comm on one GPU gets N slots, rank 0's filled).
             crank = hcomm.rank
             self.fac = dict(a2=torch.zeros(nfac * B * M.FC1_IN, **f32),
@@ -304,7 +304,10 @@ class NativeMnistEngine(MnistEngineBase):
             # by barrier epoch parity: no closing barrier for the conv blocks)
             cf = C_.mnist.xgmi_conv_floats(self.layout.offsets["conv1_bias"])
             self.xconv = torch.zeros(2 * cf, device=dev)
-            self.xcomm.register(self.grads, self.params, self.mom, self.xconv)
+            facs = list(self.fac.values()) if self.fac is not None else []
+            if facs and self.xcomm.size != nfac:
+                facs = []  # sized for another communicator: no xgmi-fac
+            self.xcomm.register(self.grads, self.params, self.mom, self.xconv, *facs)
             self.exe.set_xgmi(self.xcomm.native_handle)
             self.exe.set_xgmi_xconv(ptr(self.xconv))
         self.comm_stream = torch.cuda.Stream(device=dev) if self.grad_sync else None
@@ -337,7 +340,7 @@ class NativeMnistEngine(MnistEngineBase):
                 chunk = self.ptrs.bucket1 // c.size
                 c.reduce_scatter(g, g + 4 * chunk * c.rank, chunk, 7, 0, hs)
                 c.all_gather(g + 4 * chunk * c.rank, g, chunk, 7, hs)
-            if self.exe.factors_ok(c.size):  # factor all-gathers, in place
+            if self.exe.factors_ok(c.size) and not self.comm_is_xgmi:  # factor all-gathers, in place
                 for t in self.fac.values():
                     k = t.numel() // c.size
                     c.all_gather(ptr(t) + 4 * k * c.rank, ptr(t), k, 7, hs)
@@ -357,7 +360,7 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_SHARDED_FC
         if name == "split" and self._native_comm2 is not None:
             return E.SCHED_SPLIT
-        if name == "factors" and self.exe.factors_ok(nranks):
+        if name == "factors" and self.exe.factors_ok(nranks) and not self.comm_is_xgmi:
             return E.SCHED_FACTORS
         if name == "serial":
             return E.SCHED_SERIAL
@@ -365,6 +368,8 @@ class NativeMnistEngine(MnistEngineBase):
             return E.SCHED_DEFER
         if name == "xgmi-step" and self.exe.xgmi_ok():
             return E.SCHED_XGMI_STEP
+        if name == "xgmi-fac" and self.exe.xgmi_fac_ok():
+            return E.SCHED_XGMI_FAC
         if (name == "xgmi" or self.comm_is_xgmi) and self.exe.xgmi_ok():
             return E.SCHED_XGMI
         if self.comm_is_xgmi:
@@ -389,7 +394,8 @@ class NativeMnistEngine(MnistEngineBase):
         return {E.SCHED_SHARDED_FC: "sharded", E.SCHED_SPLIT: "split",
                 E.SCHED_FACTORS: "factors", E.SCHED_SERIAL: "serial",
                 E.SCHED_DEFER: "defer", E.SCHED_XGMI: "xgmi",
-                E.SCHED_XGMI_STEP: "xgmi-step"}.get(self.exe.schedule,
+                E.SCHED_XGMI_STEP: "xgmi-step", E.SCHED_XGMI_FAC: "xgmi-fac"}.get(
+                    self.exe.schedule,
                                                                            "buckets")
 
     def sync_optimizer_state(self) -> None:
@@ -435,6 +441,10 @@ class NativeMnistEngine(MnistEngineBase):
         xg = []
         if self.exe.xgmi_ok():  # fp32: the FC exchange in the conv2 backward, or in the step launch
             xg = [(E.SCHED_XGMI, "xgmi")] + ([] if self.bf16 else [(E.SCHED_XGMI_STEP, "xgmi-step")])
+        # the FC gradients from the gathered factors (another summation order:
+        # under --deterministic auto keeps to the bit-identical schedules)
+        if self.exe.xgmi_fac_ok() and not self.cfg.deterministic:
+            xg.append((E.SCHED_XGMI_FAC, "xgmi-fac"))
         if self.comm_is_xgmi:  # no comm stream: the fused launches or the plain all-reduce
             return xg + [(E.SCHED_SERIAL, "serial")]
         cands = [(E.SCHED_BUCKETS, "buckets"), (E.SCHED_SERIAL, "serial")]
@@ -490,7 +500,8 @@ class NativeMnistEngine(MnistEngineBase):
                 continue
             g.replay()
             torch.cuda.synchronize(self.device)
-            if sched in (E.SCHED_XGMI, E.SCHED_XGMI_STEP) and not self._xgmi_healthy():
+            if (sched in (E.SCHED_XGMI, E.SCHED_XGMI_STEP, E.SCHED_XGMI_FAC)
+                    and not self._xgmi_healthy()):
                 self.tune_log[name] = None  # a peer barrier timed out: never pick it
                 continue
             t0 = torch.cuda.Event(enable_timing=True)

@@ -155,9 +155,16 @@ def scenario_xgmi(di, dtype):
         assert torch.equal(t.cpu()[lo:hi], parts[r][lo:hi]), f"gather: segment {r}"
     assert xc.error() == 0, "an xgmi barrier timed out"
     # the MNIST schedules over the xgmi communicator vs the eager buckets run
+    # (xgmi-fac, fp32: vs the eager factor schedule - the same FC gradients
+    # from the same gathered rows, another summation order than buckets)
     ref, _ = run_fixed(di, "buckets", dtype, "eager")
+    refs = {"buckets": ref}
+    scheds = ["xgmi", "serial"]
+    if dtype == "fp32":
+        refs["factors"], _ = run_fixed(di, "factors", dtype, "eager")
+        scheds += ["xgmi-step", "xgmi-fac"]
     picked = []
-    for sched in ("xgmi", "serial", "auto"):
+    for sched in scheds + ["auto"]:
         cfg = C.TrainConfig(sync_schedule=sched, dtype=dtype, graph=True, graph_steps=G).validate()
         x, y = NS._shard(di.rank, di.world, cfg.seed)
         comm = XgmiDeviceComm(di, timeout_s=20.0)
@@ -167,9 +174,12 @@ def scenario_xgmi(di, dtype):
             assert eng.sync_schedule == sched, (eng.sync_schedule, sched)
         eng.train(STEPS)
         assert comm.error() == 0, f"{sched}: an xgmi barrier timed out"
-        same(finish(eng), ref, f"xgmi comm, {sched} (captured) vs eager buckets")
-        picked.append(eng.sync_schedule)
-    return f"all_reduce+gather ok; schedules xgmi, serial, auto->{picked[-1]}"
+        got = eng.sync_schedule
+        want = refs["factors"] if got == "xgmi-fac" else ref
+        same(finish(eng), want, f"xgmi comm, {got} (captured) vs eager "
+             + ("factors" if got == "xgmi-fac" else "buckets"))
+        picked.append(got)
+    return f"all_reduce+gather ok; schedules {','.join(scheds)}, auto->{picked[-1]}"
 
 
 def scenario_param_avg(di):

@@ -88,8 +88,9 @@ def test_bench_two_ranks_xgmi_peer_to_peer(cuda_dev, model, dtype):
     assert c["comm"] == "xgmi-p2p" and c["comm_nranks"] == 2 and c["replicas_identical"] is True
     if model == "mnist_cnn":
         tune = c["sync_tune_us_per_step"]
-        # fp32 tunes the FC exchange placement too (conv2 backward / step launch)
-        want = {"xgmi", "serial"} | ({"xgmi-step"} if dtype == "fp32" else set())
+        # fp32 tunes the FC exchange placement too (conv2 backward / step
+        # launch) and the factor gather
+        want = {"xgmi", "serial"} | ({"xgmi-step", "xgmi-fac"} if dtype == "fp32" else set())
         assert tune and set(tune) == want and None not in tune.values(), tune
         assert lines[0]["final_test_accuracy"] > 50.0
 
