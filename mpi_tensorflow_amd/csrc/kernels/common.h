@@ -38,6 +38,17 @@ __device__ __forceinline__ int mfma32_row(int r, int lane) {
   return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() also waits for
+// every outstanding global load (s_waitcnt vmcnt(0)): a prefetch issued before
+// it (the next phase's operands) would be drained there instead of landing
+// under the phase in between.  Global data exchanged between the waves of a
+// block needs __syncthreads().
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }

@@ -88,15 +88,8 @@ __device__ __forceinline__ void pool4(f2 a01, f2 a23, float& v, int& q) {
   if (a23.y > v) { v = a23.y; q = 3; }
 }
 
-// Phase barrier for LDS hand-offs only: __syncthreads() also waits for every
-// outstanding global load (s_waitcnt vmcnt(0)), which would drain the FC weight
-// prefetches below at the first barrier they cross
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
+// (phase barriers: lds_barrier, common.h - the FC weight prefetches below stay
+// in flight across them)
 // one workgroup per CU (LDS): 2 waves a SIMD, up to 256 VGPRs a lane - the room
 // the FC weight prefetches live in
 template <bool TRAIN>
