@@ -91,9 +91,11 @@ def parse(argv=None):
                     help="what the prewarm runs: forward-only test-set passes (eval), or "
                          "training-graph replays on snapshotted state that is restored "
                          "afterwards (train; engines with prewarm_train, else eval)")
+    ap.add_argument("--bucket-plan", default="auto",
+                    help="resnet18: gradient all-reduce buckets (auto: timed at start-up over "
+                         "parallel/overlap.py BUCKET_PLANS / layout / one / bytes:MiB / geo:RATIO)")
     ap.add_argument("--bucket-mb", type=float, default=None,
-                    help="lenet5 / resnet18: target gradient bytes per all-reduce bucket (MiB; "
-                         "default models/generic.py BUCKET_BYTES)")
+                    help="resnet18: shorthand for --bucket-plan bytes:MiB")
     ap.add_argument("--collective-timeout-s", type=float, default=300.0,
                     help="watchdog deadline per device-waiting region (N > 1): a hung or "
                          "failed collective aborts the communicators and exits non-zero")
@@ -229,6 +231,7 @@ def run(a, di, device, wd) -> int:
                         graph=not a.no_graph, graph_steps=a.graph_steps, backend=a.backend,
                         sync_schedule=a.sync_schedule, comm=a.comm,
                         defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
+                        bucket_plan=f"bytes:{a.bucket_mb:g}" if a.bucket_mb else a.bucket_plan,
                         collective_timeout_s=a.collective_timeout_s).validate()
     force = bool((a.force_sync or a.comm_emulate or a.xgmi_emulate) and N == 1
                  and device.type == "cuda")
@@ -268,11 +271,7 @@ def run(a, di, device, wd) -> int:
                               force_sync=force, xcomm=xcomm)
             test_x, test_y = shard.test_x, shard.test_y
         else:
-            from mpi_tensorflow_amd.models import generic as GM
             from mpi_tensorflow_amd.models.generic import model_input_shape
-            if a.bucket_mb:
-                GM.BUCKET_BYTES = int(a.bucket_mb * (1 << 20))
-                GM.MAX_BUCKETS = 64
             from mpi_tensorflow_amd.runtime.generic_engine import make_image_engine
             from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 

@@ -100,6 +100,10 @@ class TrainConfig:
     # fp32 tensors) or bf16 (half the bytes over xGMI; the sum is rounded to
     # bf16 on the wire, the update stays fp32)
     grad_comm_dtype: str = "fp32"
+    # generic models (ResNet-18): how the flat gradients are cut into
+    # all-reduce buckets (parallel/overlap.py plan_layout); "auto" times the
+    # BUCKET_PLANS candidates on the real communicator at startup
+    bucket_plan: str = "auto"
     comm: str = "auto"
     # fp32 MNIST conv2 algorithm on the native engine: "winograd" (F(2x2,5x5),
     # kernels/wino.h; 2.8x fewer MFMAs, fp32 arithmetic throughout, ~1e-6
@@ -156,6 +160,9 @@ class TrainConfig:
             raise ValueError(f"defer_split must be in (0, 1), got {self.defer_split}")
         if self.grad_comm_dtype not in ("fp32", "bf16"):
             raise ValueError(f"unknown grad comm dtype {self.grad_comm_dtype!r}")
+        if self.bucket_plan != "auto":
+            from .parallel.overlap import check_plan
+            check_plan(self.bucket_plan)
         if self.conv_algo not in ("winograd", "direct"):
             raise ValueError(f"unknown conv algo {self.conv_algo!r}")
         if self.comm not in COMMS:
@@ -214,6 +221,9 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
                    help="defer schedule: fraction of the FC bucket reduced under the conv backward")
     p.add_argument("--grad-comm-dtype", default=d.grad_comm_dtype, choices=("fp32", "bf16"),
                    help="wire dtype of the gradient all-reduce (bf16 halves the xGMI bytes)")
+    p.add_argument("--bucket-plan", default=d.bucket_plan,
+                   help="generic models: gradient all-reduce buckets (auto / layout / one / "
+                        "bytes:MiB / geo:RATIO)")
     p.add_argument("--comm", default=d.comm, choices=COMMS,
                    help="device communicator: RCCL over xGMI (one GPU per rank), shm (host-"
                         "staged shared memory, ranks may share a GPU), xgmi (peer-to-peer "

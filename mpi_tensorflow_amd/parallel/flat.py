@@ -103,6 +103,11 @@ class FlatLayout:
             raise ValueError("buckets do not cover the flat buffer")
         return out  # type: ignore[return-value]
 
+    def with_buckets(self, ids: Sequence[int]) -> "FlatLayout":
+        """The same segments with new bucket ids (one per spec, flat order)."""
+        specs = [dataclasses.replace(s, bucket=int(b)) for s, b in zip(self.specs, ids, strict=True)]
+        return FlatLayout(specs, dict(self.offsets), self.total)
+
     def l2_range(self) -> Tuple[int, int]:
         """[0, end) of the L2-regularised prefix (specs with l2=True must
         come first in flat order)."""

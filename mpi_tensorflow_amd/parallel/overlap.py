@@ -33,12 +33,73 @@ from typing import Dict, List, Optional
 import torch
 
 from .comm import DeviceComm, all_reduce_grads_
-from .flat import FlatLayout
+from .flat import FlatLayout, _round_up
+
+GEO_MIN_BYTES = 1 << 20  # geometric plans: no bucket cut below this many bytes
+# the startup auto-tune's candidates (GenericEngine.tune_schedule); plans that
+# cut a model's buckets identically are timed once
+BUCKET_PLANS = ("layout", "one", "bytes:16", "geo:4", "geo:8")
+
+
+def check_plan(plan: str) -> None:
+    kind, _, arg = plan.partition(":")
+    ok = (plan in ("layout", "one") or
+          (kind in ("bytes", "geo") and arg.replace(".", "", 1).isdigit()
+           and float(arg) > (1.0 if kind == "geo" else 0.0)))
+    if not ok:
+        raise ValueError(f"unknown bucket plan {plan!r} (auto / layout / one / bytes:MiB / "
+                         "geo:RATIO>1)")
+
+
+def plan_layout(layout: FlatLayout, plan: str) -> FlatLayout:
+    """`layout` with its all-reduce buckets re-cut at parameter boundaries:
+
+    * ``layout``  - the model's own buckets (models/generic.py BUCKET_BYTES);
+    * ``one``     - a single bucket, reduced on the compute stream after backward;
+    * ``bytes:M`` - buckets of ~M MiB each;
+    * ``geo:R``   - geometric buckets from the front of the flat (backward)
+      order, each 1/R of the one before: a CNN's deep stages hold most of the
+      parameters and finish their backward first, so the first bucket is big
+      and reduces under the rest of the backward, and the bucket left for the
+      end of backward is small (ResNet-18, R=4: 33.6 / 8.4 / 2.7 MB = layer4 /
+      layer3 / the rest).
+
+    The flat order is unchanged; only the bucket ids move."""
+    sizes = [4 * _round_up(s.numel) for s in layout.specs]
+    total = sum(sizes)
+    if plan == "layout":
+        return layout
+    if plan == "one":
+        return layout.with_buckets([0] * len(sizes))
+    kind, _, arg = plan.partition(":")
+    if kind == "bytes":
+        target = max(1, int(float(arg) * (1 << 20)))
+        nb = max(1, -(-total // target))
+        cuts = [total * (k + 1) / nb for k in range(nb - 1)]
+    elif kind == "geo":
+        r = float(arg)
+        if r <= 1.0:
+            raise ValueError(f"geometric bucket ratio must be > 1: {plan!r}")
+        cuts, rest = [], float(total)
+        while rest / r >= GEO_MIN_BYTES:  # the next cut leaves rest/r behind it
+            rest /= r
+            cuts.append(total - rest)
+    else:
+        raise ValueError(f"unknown bucket plan {plan!r}")
+    ids, acc, b = [], 0, 0
+    for sz in sizes:
+        while b < len(cuts) and acc >= cuts[b]:
+            b += 1
+        ids.append(b)
+        acc += sz
+    dense = {v: i for i, v in enumerate(sorted(set(ids)))}  # (a big tensor skips ids)
+    return layout.with_buckets([dense[v] for v in ids])
 
 
 class BucketedAllReduce:
     def __init__(self, layout: FlatLayout, grads: torch.Tensor, comm: DeviceComm,
-                 device: torch.device, wire: str = "fp32"):
+                 device: torch.device, wire: str = "fp32",
+                 stream: Optional[torch.cuda.Stream] = None):
         self.comm = comm
         self.grads = grads
         self.wire = wire  # gradient wire dtype (TrainConfig.grad_comm_dtype)
@@ -54,7 +115,7 @@ class BucketedAllReduce:
         for s in layout.specs:
             self.bucket_of[views[s.name].data_ptr()] = s.bucket
             self.size[s.bucket] += 1
-        self.stream = torch.cuda.Stream(device=device)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=device)
         self.events = [torch.cuda.Event() for _ in ranges]
         self.count = [0] * len(ranges)
         self.launched = [False] * len(ranges)

@@ -39,7 +39,7 @@ from ..models.generic import make_model
 from ..ops import functional as Fn
 from ..ops import native, ptr, stream_handle
 from ..parallel.comm import DeviceComm, all_reduce_grads_
-from ..parallel.overlap import BucketedAllReduce
+from ..parallel.overlap import BUCKET_PLANS, BucketedAllReduce, plan_layout
 from ..utils.data import batch_offset
 from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
@@ -51,6 +51,9 @@ class _null:
 
     def __exit__(self, *exc):
         return False
+
+
+TUNE_REPLAYS = 2  # timed graph replays per bucket-plan candidate (after one untimed)
 
 
 class GenericEngine:
@@ -104,13 +107,17 @@ class GenericEngine:
         self.loss_buf = torch.zeros(()).to(device)
         self._eval_x = DeviceArrayCache()
         self.bucketer = None
+        self.bucket_plan = None
+        self._tuned = cfg.bucket_plan != "auto"
+        self.tune_log = {}
+        self.tune_steps_run = 0
         if self.on_gpu:
             self._C = native()
             if self.grad_sync:
                 if comm.native_handle is None:
                     raise RuntimeError("GPU grad sync needs the native RCCL communicator")
-                self.bucketer = BucketedAllReduce(self.layout, self.grads, comm, device,
-                                                  wire=cfg.grad_comm_dtype)
+                self.bucket_plan = "layout" if cfg.bucket_plan == "auto" else cfg.bucket_plan
+                self.bucketer = self._make_bucketer(self.bucket_plan)
                 comm.all_reduce_(self.grads)  # connection setup outside any capture
                 torch.cuda.synchronize(device)
             h, w, c = train_x.shape[1:]
@@ -129,6 +136,91 @@ class GenericEngine:
             self._wfresh = False  # the copies match the fp32 weights
 
     # ------------------------------------------------------------------ util
+    @property
+    def sync_schedule(self) -> str:
+        return f"buckets({self.bucket_plan})" if self.bucketer is not None else "n/a"
+
+    def _make_bucketer(self, plan: str) -> BucketedAllReduce:
+        # every plan runs on the same comm stream (a new stream could land on
+        # another hardware queue and time differently for that alone)
+        stream = self.bucketer.stream if self.bucketer is not None else None
+        return BucketedAllReduce(plan_layout(self.layout, plan), self.grads, self.comm,
+                                 self.device, wire=self.cfg.grad_comm_dtype, stream=stream)
+
+    def _set_bucket_plan(self, plan: str) -> None:
+        """Switches the all-reduce bucketing; the captured graphs (which hold
+        the old buckets' events and collectives) are dropped."""
+        if plan == self.bucket_plan:
+            return
+        torch.cuda.synchronize(self.device)
+        self.bucketer = self._make_bucketer(plan)
+        self.bucket_plan = plan
+        self._graphs.clear()
+        self._graph_loss.clear()
+
+    def tune_schedule(self) -> int:
+        """cfg.bucket_plan == "auto" with a bucketed all-reduce: times
+        TUNE_REPLAYS graph replays of every overlap/BUCKET_PLANS candidate
+        (after one untimed replay each) on the real communicator and keeps the
+        fastest - how much of the gradient all-reduce hides under backward
+        depends on the link speed, the rank count and what a live second
+        stream costs the graph, so the bucket count is measured, not fixed
+        (PERF_NOTES "ResNet-18 all-reduce buckets").  Collective over the
+        ranks: every rank times the same candidates in the same order and
+        decides from the max-over-ranks times.  Side-effect free: params,
+        momentum, BatchNorm running statistics and the step are restored, so
+        the trial steps do not count.  Returns the number of trial steps."""
+        if self._tuned or self.bucketer is None or not self.use_graph:
+            self._tuned = True
+            return 0
+        from ..parallel import dist as D
+        G = self.graph_steps
+        host_step = self.step
+        snap = (self.params.detach().clone(), self.mom.clone(), self.step_dev.clone(),
+                {k: (rm.clone(), rv.clone()) for k, (rm, rv) in self.bn.items()})
+        self._warmup(3)  # the capture precondition; its steps are undone below too
+        seen, best, steps = {}, None, 0
+        for plan in BUCKET_PLANS:
+            key = tuple(plan_layout(self.layout, plan).buckets())
+            if key in seen:  # same cut as an earlier candidate
+                self.tune_log[plan] = self.tune_log[seen[key]]
+                continue
+            seen[key] = plan
+            self._set_bucket_plan(plan)
+            g = self._graph(G)
+            if D.allreduce_max_host(0.0 if g is not None else 1.0) != 0.0:
+                self.use_graph = False  # some rank could not capture: every rank runs eagerly
+                best = None
+                break
+            g.replay()
+            t0 = torch.cuda.Event(enable_timing=True)
+            t1 = torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(TUNE_REPLAYS):
+                g.replay()
+            t1.record()
+            torch.cuda.synchronize(self.device)
+            steps += (1 + TUNE_REPLAYS) * G
+            us = D.allreduce_max_host(1000.0 * t0.elapsed_time(t1) / (TUNE_REPLAYS * G))
+            self.tune_log[plan] = round(us, 1)
+            if best is None or us < best[0]:
+                best = (us, plan)
+        self._set_bucket_plan(best[1] if best is not None else "layout")
+        self.params.data.copy_(snap[0])
+        self.mom.copy_(snap[1])
+        self.step_dev.copy_(snap[2])
+        for k, (rm, rv) in snap[3].items():
+            self.bn[k][0].copy_(rm)
+            self.bn[k][1].copy_(rv)
+        if self.wcache is not None:  # the bf16 weight copies follow the restored weights
+            self.wcache.refresh()
+            self._wfresh = True
+        torch.cuda.synchronize(self.device)
+        self.step = host_step
+        self._tuned = True
+        self.tune_steps_run = steps
+        return steps
+
     def lr(self, step: Optional[int] = None) -> float:
         s = self.step if step is None else step
         return learning_rate(s, self.n_local, self.B, self.cfg.base_lr, self.cfg.lr_decay)

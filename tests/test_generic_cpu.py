@@ -25,6 +25,33 @@ def test_param_counts():
     assert rn.layout.specs[0].name == "fc_b" or rn.layout.specs[0].name == "fc_w"
 
 
+def test_bucket_plans():
+    """parallel/overlap.py plan_layout: every plan tiles the flat buffer with
+    contiguous buckets at parameter boundaries in backward order; geo:4 puts
+    ResNet-18's layer4 (+ head), layer3 and the rest in three buckets."""
+    from mpi_tensorflow_amd.parallel.overlap import BUCKET_PLANS, check_plan, plan_layout
+
+    L = ResNet18().layout
+    for plan in BUCKET_PLANS + ("bytes:8", "geo:2"):
+        check_plan(plan)
+        pl = plan_layout(L, plan)
+        b = pl.buckets()  # raises unless contiguous and covering
+        ids = [s.bucket for s in pl.specs]
+        assert ids == sorted(ids) and set(ids) == set(range(len(b)))
+        assert [s.name for s in pl.specs] == [s.name for s in L.specs]
+    assert plan_layout(L, "layout").buckets() == L.buckets()
+    assert len(plan_layout(L, "one").buckets()) == 1
+    geo = plan_layout(L, "geo:4")
+    first = {s.name.split("_")[0] for s in geo.specs if s.bucket == 0}
+    assert [round(4 * (hi - lo) / 1e6, 1) for lo, hi in geo.buckets()] == [33.6, 8.4, 2.7]
+    assert all(n.startswith(("fc", "l4")) for n in first), first
+    for bad in ("geo:1", "bytes:0", "two", "geo:x"):
+        with pytest.raises(ValueError):
+            check_plan(bad)
+    with pytest.raises(ValueError):
+        C.TrainConfig(bucket_plan="geo:1").validate()
+
+
 def _nchw_lenet(flat_views, x):
     v = flat_views
     h = F.conv2d(x.permute(0, 3, 1, 2), v["c1_w"].permute(3, 2, 0, 1), v["c1_b"]).relu()

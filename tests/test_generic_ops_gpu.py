@@ -2,6 +2,7 @@
 vs plain PyTorch fp32, and of whole LeNet-5 / ResNet-18 training steps vs the
 CPU oracle path."""
 
+import dataclasses
 
 import numpy as np
 import pytest
@@ -242,6 +243,42 @@ def test_generic_bucketed_allreduce_overlap(cuda_dev):
     nb = len(synced.layout.buckets())
     assert nb == 6 and synced.bucketer.order == list(range(nb))  # backward completion order
     assert torch.equal(synced.params.detach(), plain.params.detach())
+
+
+def test_generic_bucket_plan_autotune(cuda_dev):
+    """bucket_plan="auto": the start-up tune times every distinct plan of
+    parallel/overlap.py BUCKET_PLANS as captured graph replays on the native
+    RCCL communicator, keeps one, and leaves no trace - the params, momentum,
+    BatchNorm running statistics and step afterwards are those of before, so
+    the tuned engine's training equals an untuned, unsynchronised run."""
+    from mpi_tensorflow_amd.parallel.comm import RcclDeviceComm
+    from mpi_tensorflow_amd.parallel.dist import DistInfo
+    from mpi_tensorflow_amd.parallel.overlap import BUCKET_PLANS
+    from mpi_tensorflow_amd.runtime.generic_engine import GenericEngine
+    from mpi_tensorflow_amd.utils.data import synthetic_rows
+
+    comm = RcclDeviceComm(DistInfo())
+    x, y = synthetic_rows("train", 0, 64, shape=(32, 32, 3))
+    cfg = C.TrainConfig(model="resnet18", dtype="bf16", batch_size=8, graph=True,
+                        graph_steps=2).validate()
+    tuned = GenericEngine(cfg, x, y, cuda_dev, comm=comm, force_sync=True)
+    plain = GenericEngine(dataclasses.replace(cfg, graph=False), x, y, cuda_dev)
+    before = tuned.params.detach().clone()
+    steps = tuned.tune_schedule()
+    torch.cuda.synchronize()
+    assert steps > 0 and tuned.step == 0
+    assert set(tuned.tune_log) == set(BUCKET_PLANS)
+    assert all(v is not None and v > 0 for v in tuned.tune_log.values()), tuned.tune_log
+    assert tuned.bucket_plan in BUCKET_PLANS
+    assert min(tuned.tune_log.values()) == tuned.tune_log[tuned.bucket_plan]
+    assert torch.equal(tuned.params.detach(), before)
+    assert tuned.tune_schedule() == 0  # once
+    tuned.train(7)
+    plain.train(7)
+    torch.cuda.synchronize()
+    assert torch.equal(tuned.params.detach(), plain.params.detach())
+    for k, (rm, rv) in plain.bn.items():
+        assert torch.equal(tuned.bn[k][0], rm) and torch.equal(tuned.bn[k][1], rv)
 
 
 @pytest.mark.parametrize("N,H,W,Cin,K,R,stride,pad", [
