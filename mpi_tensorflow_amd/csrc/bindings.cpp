@@ -28,6 +28,10 @@ static inline T* P(uintptr_t v) {
 }
 static inline hipStream_t S(uintptr_t v) { return reinterpret_cast<hipStream_t>(v); }
 
+static void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
 static void check_launch() {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
@@ -835,6 +839,41 @@ PYBIND11_MODULE(_C, m) {
   m.def("graph_upload", [](uintptr_t exec, uintptr_t s) {
     const hipError_t e = hipGraphUpload(reinterpret_cast<hipGraphExec_t>(exec), S(s));
     if (e != hipSuccess) throw std::runtime_error(std::string("hipGraphUpload: ") + hipGetErrorString(e));
+  });
+  // stream-ordering events between two streams of this device: no timing and a
+  // device-scope release (a default event's system-scope fence writes back and
+  // invalidates the caches under the work that follows it)
+  m.def("event_create", []() -> uintptr_t {
+    hipEvent_t e = nullptr;
+    hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice),
+           "hipEventCreateWithFlags");
+    return reinterpret_cast<uintptr_t>(e);
+  });
+  m.def("event_destroy", [](uintptr_t e) {
+    hip_ok(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)), "hipEventDestroy");
+  });
+  m.def("event_record", [](uintptr_t e, uintptr_t s) {
+    hip_ok(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(s)), "hipEventRecord");
+  });
+  m.def("stream_wait_event", [](uintptr_t s, uintptr_t e) {
+    hip_ok(hipStreamWaitEvent(S(s), reinterpret_cast<hipEvent_t>(e), 0), "hipStreamWaitEvent");
+  });
+  // nodes captured so far on a capturing stream (-1: not capturing); the
+  // segmented step capture (runtime/generic_engine.py) never ends an empty segment
+  m.def("capture_node_count", [](uintptr_t s) -> long long {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    hipError_t e = hipStreamGetCaptureInfo_v2(S(s), &st, &id, &g, &deps, &nd);
+    if (e != hipSuccess)
+      throw std::runtime_error(std::string("hipStreamGetCaptureInfo_v2: ") + hipGetErrorString(e));
+    if (st != hipStreamCaptureStatusActive || g == nullptr) return -1;
+    size_t n = 0;
+    e = hipGraphGetNodes(g, nullptr, &n);
+    if (e != hipSuccess) throw std::runtime_error(std::string("hipGraphGetNodes: ") + hipGetErrorString(e));
+    return (long long)n;
   });
   m.def("idx_header", [](const std::string& path) {
     IdxHeader h = idx_header(path);

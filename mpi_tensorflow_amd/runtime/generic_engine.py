@@ -39,7 +39,7 @@ from ..models.generic import make_model
 from ..ops import functional as Fn
 from ..ops import native, ptr, stream_handle
 from ..parallel.comm import DeviceComm, all_reduce_grads_
-from ..parallel.overlap import BUCKET_PLANS, BucketedAllReduce, plan_layout
+from ..parallel.overlap import BUCKET_PLANS, BucketedAllReduce, SegmentedStep, plan_layout
 from ..utils.data import batch_offset
 from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
@@ -337,7 +337,53 @@ class GenericEngine:
             self.mom.mul_(self.cfg.momentum).add_(self.grads)
             self.params.sub_(self.lr() * self.mom)
 
+    def _segmented(self) -> bool:
+        return self.bucketer is not None and len(self.bucketer.slices) > 1
+
+    def _seg_graph(self, n: int):
+        """n steps as linear compute segments + per-bucket collective graphs
+        (parallel/overlap.py SegmentedStep): one step's optimizer and the
+        next step's forward share a segment, so a step pays one graph
+        boundary per overlapped bucket and nothing between steps."""
+        g = self._graphs.get(n)
+        if g is not None:
+            return g
+        torch.cuda.synchronize(self.device)
+        cap = torch.cuda.Stream(device=self.device)
+        cap.wait_stream(torch.cuda.current_stream())
+        seg = SegmentedStep(self.bucketer.stream, torch.cuda.graph_pool_handle(),
+                            lambda st: self._C.capture_node_count(stream_handle(st)))
+        self.bucketer.segment = seg
+        err = None
+        with torch.cuda.stream(cap):
+            try:
+                seg.begin()
+                for _ in range(n):
+                    self._step_gpu()
+                seg.end()
+            except RuntimeError as e:
+                err = e
+                if seg.cur is not None:  # leave no capture open on the stream
+                    try:
+                        seg.cur.capture_end()
+                    except RuntimeError:
+                        pass
+            finally:
+                self.bucketer.segment = None
+        if err is not None:  # keep training eagerly rather than fail the run
+            print(f"[rank {self.rank}] segmented hipGraph capture failed ({err}); using "
+                  "eager launches", flush=True)
+            self.use_graph = False
+            torch.cuda.synchronize(self.device)
+            return None
+        torch.cuda.current_stream().wait_stream(cap)
+        self._graphs[n] = seg
+        self._graph_loss[n] = self._loss_t
+        return seg
+
     def _graph(self, n: int):
+        if self._segmented():
+            return self._seg_graph(n)
         g = self._graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
