@@ -72,8 +72,11 @@ constexpr int S_DPRE2 = S_T2 + 2 * F0;        // dpre2 [18][18][DPS], zero borde
 constexpr int S_T1 = S_DPRE2;                 // (g1, x offset of the argmax) per (p, c): after I
 constexpr int S_G1 = S_DPRE2 + DP * DP * DPS; // data-grad partial of the 2nd channel group
 constexpr int S_RED = S_G1 + P1 * P1 * C1;    // split-K partials
-constexpr int S_TOTAL = S_RED + NT;
+constexpr int S_FB = S_RED + NT;              // FC biases [120 | 84 | 10] (loaded in A)
+constexpr int S_C2P = S_FB + F1 + F2 + F3 + 2;  // conv2 partials [ci][pp][4][co] (phase C)
+constexpr int S_TOTAL = S_C2P + C1 * P2 * P2 * 4 * C2;
 static_assert(S_TOTAL * 4 <= 160 * 1024, "image kernel LDS budget");
+static_assert(S_W2 % 4 == 0 && S_C2P % 4 == 0, "float4 LDS regions");
 static_assert(2 * P1 * P1 * C1 <= DP * DP * DPS, "T1 must fit in the dpre2 region");
 
 __device__ __forceinline__ float relu(float v) { return v > 0.f ? v : 0.f; }
@@ -123,6 +126,10 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     const float w1v = tid < W1N ? W[o.c1w + tid] : 0.f;
     const float b1v = tid < C1 ? W[o.c1b + tid] : 0.f;
     const float b2v = tid < C2 ? W[o.c2b + tid] : 0.f;
+    // the FC biases (read after a phase barrier, each was an exposed round trip)
+    const float fbv = tid < F1 ? W[o.f1b + tid]
+                      : tid < F1 + F2 ? W[o.f2b + tid - F1]
+                      : tid < F1 + F2 + F3 ? W[o.f3b + tid - F1 - F2] : 0.f;
     float w2v[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -143,6 +150,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     if (tid < W1N) sm[S_W1 + tid] = w1v;
     if (tid < C1) sm[S_B1 + tid] = b1v;
     if (tid < C2) sm[S_B2 + tid] = b2v;
+    if (tid < F1 + F2 + F3) sm[S_FB + tid] = fbv;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int e = tid + NT * k;
@@ -210,26 +218,63 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     for (int i = 0; i < 100; ++i) wv1[i] = wp[i * F1];
   }
 
-  // ---- C: conv2 + bias + ReLU + pool: thread = (pooled pixel, channel)
-  if (tid < F0) {
-    const int co = tid & 15, pp = tid >> 4, py = pp / P2, px = pp % P2;
-    f2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+  // ---- C: conv2 + bias + ReLU + pool, register-blocked: thread = (input
+  // channel ci, output-channel octet cg, pooled pixel pp) holds the 6 x 6 input
+  // patch of its pool window in registers and forms 8 channels x 4 window
+  // positions from each pair of float4 weight reads - a quarter of the LDS
+  // bytes of one thread per (pp, co), which made this phase LDS-bound.  The 6
+  // per-channel partials are then summed in ci order by (pp, co) threads.
+  if (tid < C1 * 2 * P2 * P2) {
+    const int ci = tid / 50, r = tid % 50, cg = r / 25, pp = r % 25, py = pp / P2, px = pp % P2;
+    float xq[6][6];
+    const float* xb = sm + S_P1 + (2 * py * P1 + 2 * px) * C1 + ci;
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) xq[i][j] = xb[(i * P1 + j) * C1];
+    f2 acc[4][4];  // [window position (dy, dx)][output-channel pair]
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[u][c] = f2{0.f, 0.f};
 #pragma unroll
     for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw)
+      for (int kw = 0; kw < 5; ++kw) {
+        const float4* wp =
+            reinterpret_cast<const float4*>(sm + S_W2 + ((kh * 5 + kw) * C1 + ci) * C2 + 8 * cg);
+        const float4 wa = wp[0], wb = wp[1];
+        const f2 w[4] = {{wa.x, wa.y}, {wa.z, wa.w}, {wb.x, wb.y}, {wb.z, wb.w}};
 #pragma unroll
-        for (int ci = 0; ci < C1; ++ci) {
-          const float* xp = sm + S_P1 + ((2 * py + kh) * P1 + 2 * px + kw) * C1 + ci;
-          const f2 x01 = {xp[0], xp[C1]}, x23 = {xp[P1 * C1], xp[P1 * C1 + C1]};
-          const float wv = sm[S_W2 + ((kh * 5 + kw) * C1 + ci) * C2 + co];
-          const f2 w = {wv, wv};
-          s01 = __builtin_elementwise_fma(x01, w, s01);
-          s23 = __builtin_elementwise_fma(x23, w, s23);
+        for (int u = 0; u < 4; ++u) {
+          const float xv = xq[kh + (u >> 1)][kw + (u & 1)];
+          const f2 xx = {xv, xv};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[u][c] = __builtin_elementwise_fma(xx, w[c], acc[u][c]);
         }
+      }
+    // partials [ci][pp][position][co]
+    float4* pp4 = reinterpret_cast<float4*>(sm + S_C2P + ((ci * 25 + pp) * 4) * C2 + 8 * cg);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      pp4[u * 4] = make_float4(acc[u][0].x, acc[u][0].y, acc[u][1].x, acc[u][1].y);
+      pp4[u * 4 + 1] = make_float4(acc[u][2].x, acc[u][2].y, acc[u][3].x, acc[u][3].y);
+    }
+  }
+  lds_barrier();
+  if (tid < F0) {
+    const int co = tid & 15, pp = tid >> 4;
+    float v4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float s = 0.f;
+#pragma unroll
+      for (int ci = 0; ci < C1; ++ci) s += sm[S_C2P + ((ci * 25 + pp) * 4 + u) * C2 + co];
+      v4[u] = s;
+    }
     float v;
     int q;
-    pool4(s01, s23, v, q);
+    pool4(f2{v4[0], v4[1]}, f2{v4[2], v4[3]}, v, q);
     sm[S_P2 + tid] = relu(v + sm[S_B2 + co]);  // (h, w, c) flatten = FC1 input order
     q2s[tid] = (uint8_t)q;
   }
@@ -264,7 +309,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   }
   lds_barrier();
   if (tid < F1) {
-    const float z = W[o.f1b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
+    const float z = sm[S_FB + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
                     sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
     sm[S_H1 + tid] = relu(z);
   }
@@ -300,7 +345,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   }
   lds_barrier();
   if (tid < F2) {
-    const float z = W[o.f2b + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
+    const float z = sm[S_FB + F1 + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
                     sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
     sm[S_H2 + tid] = relu(z);
   }
@@ -321,7 +366,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   if (tid < 64) {  // one wave: logits, softmax xent, argmax
     float lg = -INFINITY;
     if (tid < F3) {
-      float z = W[o.f3b + tid];
+      float z = sm[S_FB + F1 + F2 + tid];
       for (int g = 0; g < 32; ++g) z += sm[S_RED + g * 16 + tid];
       lg = z;
     }
