@@ -1479,6 +1479,44 @@ __global__ __launch_bounds__(256) void slab_fold4_kernel(float4* __restrict__ pa
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Deep, narrow slab stacks in ONE pass (the fold + sum pair of launches
+// before): G lanes per output float4 (lanes i * G .. i * G + G - 1 of a
+// block), lane g summing slabs g, g + G, g + 2G, ... in order with 4 loads in
+// flight, then a fixed xor tree over the G lanes - the same association on
+// every run.  Plain fp32 outputs only (no statistics / addend / bf16 copy).
+template <int G>
+__global__ __launch_bounds__(256) void slab_sumg4_kernel(const float4* __restrict__ part, int nz,
+                                                         long long n4, float4* __restrict__ out) {
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long i = t / G;
+  const int g = (int)(t % G);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i < n4) {
+    int z = g;
+    for (; z + 3 * G < nz; z += 4 * G) {
+      const float4 v0 = part[(long long)z * n4 + i], v1 = part[(long long)(z + G) * n4 + i];
+      const float4 v2 = part[(long long)(z + 2 * G) * n4 + i];
+      const float4 v3 = part[(long long)(z + 3 * G) * n4 + i];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      a.x += v1.x; a.y += v1.y; a.z += v1.z; a.w += v1.w;
+      a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+      a.x += v3.x; a.y += v3.y; a.z += v3.z; a.w += v3.w;
+    }
+    for (; z < nz; z += G) {
+      const float4 v = part[(long long)z * n4 + i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) {
+    a.x += __shfl_xor(a.x, m, 64);
+    a.y += __shfl_xor(a.y, m, 64);
+    a.z += __shfl_xor(a.z, m, 64);
+    a.w += __shfl_xor(a.w, m, 64);
+  }
+  if (g == 0 && i < n4) out[i] = a;
+}
+
 // Deterministic sum of nz slabs of n4 float4s into out (fixed association
 // order for a given nz).
 // outb: bf16 output instead of out
@@ -1492,6 +1530,16 @@ static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStrea
                         const ConvStats* stats = nullptr, int C = 0,
                         const BnBwdStats* bstats = nullptr) {
   const long long b = slab_blocks(n4);
+  if (b < 128 && nz >= 32 && !addend && !outb && !(stats && stats->part) &&
+      !(bstats && bstats->part)) {
+    if (nz >= 128)
+      slab_sumg4_kernel<16><<<cdiv(n4 * 16, 256), 256, 0, st>>>(
+          reinterpret_cast<const float4*>(slabs), nz, n4, reinterpret_cast<float4*>(out));
+    else
+      slab_sumg4_kernel<8><<<cdiv(n4 * 8, 256), 256, 0, st>>>(
+          reinterpret_cast<const float4*>(slabs), nz, n4, reinterpret_cast<float4*>(out));
+    return;
+  }
   int G = 1;
   if (b < 128 && nz >= 32) {
     G = 8;

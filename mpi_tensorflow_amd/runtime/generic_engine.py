@@ -28,6 +28,7 @@ On CPU the same model runs through the PyTorch oracle ops.
 from __future__ import annotations
 
 import dataclasses
+import gc
 
 from typing import Optional
 
@@ -157,6 +158,7 @@ class GenericEngine:
         self.bucket_plan = plan
         self._graphs.clear()
         self._graph_loss.clear()
+        gc.collect()  # the dropped graphs go now, never inside a later capture
 
     def tune_schedule(self) -> int:
         """cfg.bucket_plan == "auto" with a bucketed all-reduce: times
@@ -348,6 +350,10 @@ class GenericEngine:
         g = self._graphs.get(n)
         if g is not None:
             return g
+        # (as torch.cuda.graph does: collect before capturing - a graph or an
+        # event freed by a collection inside the capture aborts the process -
+        # and keep the collector off until the capture has ended)
+        gc.collect()
         torch.cuda.synchronize(self.device)
         cap = torch.cuda.Stream(device=self.device)
         cap.wait_stream(torch.cuda.current_stream())
@@ -355,6 +361,8 @@ class GenericEngine:
                             lambda st: self._C.capture_node_count(stream_handle(st)))
         self.bucketer.segment = seg
         err = None
+        gc_was_on = gc.isenabled()
+        gc.disable()
         with torch.cuda.stream(cap):
             try:
                 seg.begin()
@@ -370,6 +378,8 @@ class GenericEngine:
                         pass
             finally:
                 self.bucketer.segment = None
+                if gc_was_on:
+                    gc.enable()
         if err is not None:  # keep training eagerly rather than fail the run
             print(f"[rank {self.rank}] segmented hipGraph capture failed ({err}); using "
                   "eager launches", flush=True)
