@@ -70,8 +70,8 @@ constexpr int S_D1 = S_D2 + 88;               // dz1
 constexpr int S_T2 = S_D1 + 128;              // (g2, p1 offset of the argmax) per (pp, co)
 constexpr int S_DPRE2 = S_T2 + 2 * F0;        // dpre2 [18][18][DPS], zero border
 constexpr int S_T1 = S_DPRE2;                 // (g1, x offset of the argmax) per (p, c): after I
-constexpr int S_G1 = S_DPRE2 + DP * DP * DPS; // data-grad partial of the 2nd channel group
-constexpr int S_RED = S_G1 + P1 * P1 * C1;    // split-K partials
+constexpr int S_G1 = S_DPRE2 + DP * DP * DPS; // data-grad partials of co quarters 1..3
+constexpr int S_RED = S_G1 + 3 * P1 * P1 * C1; // split-K partials
 constexpr int S_FB = S_RED + NT;              // FC biases [120 | 84 | 10] (loaded in A)
 constexpr int S_C2P = S_FB + F1 + F2 + F3 + 2;  // conv2 partials [ci][pp][4][co] (phase C)
 constexpr int S_TOTAL = S_C2P + C1 * P2 * P2 * 4 * C2;
@@ -475,49 +475,64 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   if (a.stop_phase == 5) return;
   // ---- I: conv2 data grad over the zero-bordered dpre2 plane:
   // dp1[y,x,ci] = sum_{kh,kw,co} dpre2[y-kh, x-kw, co] W2[kh,kw,ci,co].
-  // Thread = (pooled1 pixel, half of the 16 channels co); this part's conv1
-  // channels as ONE packed pair (v_pk_fma_f32): pair pi = {2 pi, 2 pi + 1},
-  // parts 0 / 1 use pairs 0 / 1, parts 2 / 3 pair 2 (channel 4 / 5 of it).
-  // Per tap 2 float4 dpre2 reads + 8 float2 weight broadcasts ([tap][co][ci]
-  // copy of W2).
+  // This part's conv1 channels as ONE packed pair (v_pk_fma_f32): pair pi =
+  // {2 pi, 2 pi + 1}, parts 0 / 1 use pairs 0 / 1, parts 2 / 3 pair 2 (channel
+  // 4 / 5 of it); the weights from the [tap][co][ci] copy of W2.
   const int pi = q < 2 ? q : 2;
   const int c_lo = q < 2 ? 2 * q : q + 2, c_hi = q < 2 ? 2 * q + 2 : q + 3;
+  // Register-blocked: thread = (output-channel quarter grp, pair of adjacent
+  // pooled1 pixels) - the two pixels' 5 x 5 dpre2 windows share 4 of their
+  // 5 columns (6 float4 reads a kernel row for both) and every weight read
+  // serves both pixels.  The quarters' partials are summed in grp order.
   {
-    const int grp = tid >> 8, p = tid & 255;
-    f2 sp = {0.f, 0.f};
-    if (p < P1 * P1) {
-      const int y = p / P1, x = p % P1;
+    const int grp = tid >> 7, pr = tid & 127;
+    const bool act = pr < P1 * P1 / 2;
+    const int y = pr / (P1 / 2), x = 2 * (pr % (P1 / 2));
+    f2 s0 = {0.f, 0.f}, s1 = {0.f, 0.f};  // pixels (y, x), (y, x + 1)
+    if (act) {
 #pragma unroll
-      for (int kh = 0; kh < 5; ++kh)
+      for (int kh = 0; kh < 5; ++kh) {
+        const float4* rp =
+            reinterpret_cast<const float4*>(sm + S_DPRE2 + ((y - kh + 4) * DP + x) * DPS + 4 * grp);
+        float4 dr[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) dr[k] = rp[k * (DPS / 4)];
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const float4* dp = reinterpret_cast<const float4*>(
-              sm + S_DPRE2 + ((y - kh + 4) * DP + x - kw + 4) * DPS + 8 * grp);
-          const float4 da = dp[0], db = dp[1];
-          const float d[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
           const f2* wp =
-              reinterpret_cast<const f2*>(sm + S_W2T + ((kh * 5 + kw) * C2 + 8 * grp) * C1);
+              reinterpret_cast<const f2*>(sm + S_W2T + ((kh * 5 + kw) * C2 + 4 * grp) * C1);
+          const float4 da = dr[4 - kw], db = dr[5 - kw];
+          const float av[4] = {da.x, da.y, da.z, da.w}, bv[4] = {db.x, db.y, db.z, db.w};
 #pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const f2 dd = {d[c], d[c]};
-            sp = __builtin_elementwise_fma(dd, wp[3 * c + pi], sp);
+          for (int c = 0; c < 4; ++c) {
+            const f2 w = wp[3 * c + pi];
+            s0 = __builtin_elementwise_fma(f2{av[c], av[c]}, w, s0);
+            s1 = __builtin_elementwise_fma(f2{bv[c], bv[c]}, w, s1);
           }
         }
-      if (grp == 1) {
-        float* gp = sm + S_G1 + p * C1 + 2 * pi;
-        gp[0] = sp.x, gp[1] = sp.y;
+      }
+      if (grp > 0) {
+        float* gp = sm + S_G1 + (grp - 1) * (P1 * P1 * C1) + (y * P1 + x) * C1 + 2 * pi;
+        gp[0] = s0.x, gp[1] = s0.y;
+        gp[C1] = s1.x, gp[C1 + 1] = s1.y;
       }
     }
     lds_barrier();  // every dpre2 read is done: the T1 table may overwrite it
-    if (grp == 0 && p < P1 * P1) {
-      const int py = p / P1, px = p % P1;
-      for (int c = c_lo; c < c_hi; ++c) {
-        const float g = sm[S_G1 + p * C1 + c] + (c == 2 * pi ? sp.x : sp.y);
-        const int qq = q1s[p * C1 + c];
-        const int u = 2 * py + (qq >> 1), v = 2 * px + (qq & 1);
-        // ReLU1 through the pooled output; T1 = (g1, input offset of the argmax)
-        sm[S_T1 + 2 * (p * C1 + c)] = sm[S_P1 + p * C1 + c] > 0.f ? g : 0.f;
-        sm[S_T1 + 2 * (p * C1 + c) + 1] = __int_as_float(u * XRS + v);
+    if (grp == 0 && act) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int px = x + h, p = y * P1 + px;
+        const f2 sp = h ? s1 : s0;
+        for (int c = c_lo; c < c_hi; ++c) {
+          float g = c == 2 * pi ? sp.x : sp.y;
+#pragma unroll
+          for (int k = 0; k < 3; ++k) g += sm[S_G1 + k * (P1 * P1 * C1) + p * C1 + c];
+          const int qq = q1s[p * C1 + c];
+          const int u = 2 * y + (qq >> 1), v = 2 * px + (qq & 1);
+          // ReLU1 through the pooled output; T1 = (g1, input offset of the argmax)
+          sm[S_T1 + 2 * (p * C1 + c)] = sm[S_P1 + p * C1 + c] > 0.f ? g : 0.f;
+          sm[S_T1 + 2 * (p * C1 + c) + 1] = __int_as_float(u * XRS + v);
+        }
       }
     }
   }
