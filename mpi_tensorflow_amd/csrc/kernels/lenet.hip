@@ -540,29 +540,37 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   if (a.stop_phase == 6) return;
   // ---- J: conv1 filter grad, sparse over the 196 argmax pixels per channel:
   // dW1[kh,kw,ci,c] = sum_p g1[p,c] * x[ci, u_p + kh, v_p + kw], for this
-  // part's channels c in [c_lo, c_hi); 2 or 4 threads per weight split the
-  // pixels (even / odd pixel chains, summed in a fixed order)
+  // part's channels c in [c_lo, c_hi).  Register-blocked over kw: a thread
+  // forms the 5 weights of one (c, ci, kh) row from one T1 read per pixel;
+  // S threads of a row split the pixels (p = part, part + S, ...), summed by a
+  // fixed xor tree.  240 threads: waves 0-3 (db1 below runs in wave 7).
   {
-    const int nc = c_hi - c_lo, nw = 75 * nc;  // weights of this part
-    const int split = nc == 2 ? 2 : 4;         // threads per weight
-    const int wi = tid / split, part = tid % split;
-    float s0 = 0.f, s1 = 0.f;
-    if (wi < nw) {
-      const int c = c_lo + wi % nc, ci = (wi / nc) % IC, t = wi / (nc * IC), kh = t / 5, kw = t % 5;
-      const float* xp = sm + S_X + ci * XPL + kh * XRS + kw;
+    const int nc = c_hi - c_lo;              // 2 (parts 0, 1) or 1 (parts 2, 3)
+    const int lgS = nc == 2 ? 3 : 4, S = 1 << lgS;
+    const int row = tid >> lgS, part = tid & (S - 1);
+    const bool act = row < 15 * nc;          // (c, ci, kh) rows of this part
+    float acc[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    const int c = c_lo + row % nc, ci = (row / nc) % IC, kh = row / (nc * IC);
+    if (act) {
+      const float* xp = sm + S_X + ci * XPL + kh * XRS;
       const float2* t1 = reinterpret_cast<const float2*>(sm + S_T1) + c;
-      for (int p = 2 * part; p < P1 * P1; p += 2 * split) {
-        const float2 ta = t1[p * C1], tb = t1[(p + 1) * C1];
-        s0 = fmaf(ta.x, xp[__float_as_int(ta.y)], s0);
-        s1 = fmaf(tb.x, xp[__float_as_int(tb.y)], s1);
+#pragma unroll 4
+      for (int p = part; p < P1 * P1; p += S) {
+        const float2 tv = t1[p * C1];
+        const float* xr = xp + __float_as_int(tv.y);
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) acc[kw] = fmaf(tv.x, xr[kw], acc[kw]);
       }
     }
-    float s = s0 + s1;
-    s += __shfl_xor(s, 1, 64);
-    if (split == 4) s += __shfl_xor(s, 2, 64);
-    if (wi < nw && part == 0) {
-      const int c = c_lo + wi % nc, ci = (wi / nc) % IC, t = wi / (nc * IC);
-      cp[(t * IC + ci) * C1 + c] = s;
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1)
+        if (m < S) acc[kw] += __shfl_xor(acc[kw], m, 64);
+    }
+    if (act && part == 0) {
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) cp[((kh * 5 + kw) * IC + ci) * C1 + c] = acc[kw];
     }
     if (tid >= 448) {  // db1: wave 7 (idle above), lanes over the pixels + a wave sum
       const int lane = tid - 448;
