@@ -208,14 +208,26 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   }
   lds_barrier();
   if (a.stop_phase == 1) return;
-  // the FC1 weights of phase D, requested now: their round trip hides under
-  // conv2 (issued in D it was one exposed round trip per FC layer)
+  // the FC1 weights, requested now (their round trip hides under conv2) and
+  // kept in registers for BOTH FC1 passes: thread t < 480 holds the 10 x 10
+  // block (rows 10 rb .., columns 10 cb ..) of W1 [400][120] - forward
+  // (phase D) and backward (da2 in phase G) each sum in-thread over one block
+  // axis and across threads over the other, through LDS.  (With a column per
+  // thread, the backward had to read W1 again by rows: a 49 MB burst over all
+  // workgroups at once, ~3 us.)
   const int fj = tid & 127, fg = tid >> 7;
-  float wv1[100];
-  if (fj < F1) {
-    const float* wp = W + o.f1w + (fg * 100) * F1 + fj;
+  const int rb = min(tid, 479) / 12, cb = min(tid, 479) % 12, i0 = 10 * rb, j0 = 10 * cb;
+  float w1b[10][10];
+  {
+    const float2* wp = reinterpret_cast<const float2*>(W + o.f1w + i0 * F1 + j0);
 #pragma unroll
-    for (int i = 0; i < 100; ++i) wv1[i] = wp[i * F1];
+    for (int r = 0; r < 10; ++r)
+#pragma unroll
+      for (int c = 0; c < 5; ++c) {
+        const float2 v = wp[(r * F1) / 2 + c];
+        w1b[r][2 * c] = v.x;
+        w1b[r][2 * c + 1] = v.y;
+      }
   }
 
   // ---- C: conv2 + bias + ReLU + pool, register-blocked: thread = (input
@@ -296,27 +308,32 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
       wv3[u] = (j3 < F3 && i < F2) ? W[o.f3w + i * F3 + j3] : 0.f;
     }
   }
-  // ---- D: FC1 400 -> 120 + ReLU: 4-way split K, coalesced weight columns
-  // (prefetched after phase A)
-  {
-    float acc = 0.f;
-    if (fj < F1) {
-      const float* xp = sm + S_P2 + fg * 100;
+  // ---- D: FC1 400 -> 120 + ReLU from the register blocks: partials
+  // [rb][j] in the (free) conv2 partial region, then 40 row blocks summed in
+  // order per output
+  if (tid < 480) {
+    float xv[10];
 #pragma unroll
-      for (int i = 0; i < 100; ++i) acc = fmaf(xp[i], wv1[i], acc);
+    for (int r = 0; r < 10; ++r) xv[r] = sm[S_P2 + i0 + r];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) {
+      float acc = 0.f;
+#pragma unroll
+      for (int r = 0; r < 10; ++r) acc = fmaf(xv[r], w1b[r][c], acc);
+      sm[S_C2P + rb * F1 + j0 + c] = acc;
     }
-    sm[S_RED + tid] = acc;
   }
   lds_barrier();
   if (tid < F1) {
-    const float z = sm[S_FB + tid] + sm[S_RED + tid] + sm[S_RED + 128 + tid] +
-                    sm[S_RED + 256 + tid] + sm[S_RED + 384 + tid];
+    float z = sm[S_FB + tid];
+#pragma unroll 8
+    for (int r = 0; r < 40; ++r) z += sm[S_C2P + r * F1 + tid];
     sm[S_H1 + tid] = relu(z);
   }
   lds_barrier();
+  if (a.stop_phase == 10) return;  // (labs: lenet_phases.py sub-phase stops)
   // the FC backward (dX chain) weights of phase G, requested now (train)
   float g3w[F3], g2w[21];
-  float4 g1w[F1 / 4];
   if (TRAIN) {
     if (tid < F2) {
 #pragma unroll
@@ -326,11 +343,6 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
       const float* wp = W + o.f2w + (tid >> 2) * F2 + (tid & 3) * 21;
 #pragma unroll
       for (int j = 0; j < 21; ++j) g2w[j] = wp[j];
-    }
-    if (tid < F0) {
-      const float4* wp = reinterpret_cast<const float4*>(W + o.f1w + tid * F1);
-#pragma unroll
-      for (int j4 = 0; j4 < F1 / 4; ++j4) g1w[j4] = wp[j4];
     }
   }
   // ---- E: FC2 120 -> 84 + ReLU
@@ -350,6 +362,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     sm[S_H2 + tid] = relu(z);
   }
   lds_barrier();
+  if (a.stop_phase == 11) return;
   // ---- F: FC3 84 -> 10: 32 K groups of <= 3
   {
     const int j = tid & 15, g = tid >> 4;
@@ -363,6 +376,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     sm[S_RED + tid] = acc;
   }
   lds_barrier();
+  if (a.stop_phase == 12) return;
   if (tid < 64) {  // one wave: logits, softmax xent, argmax
     float lg = -INFINITY;
     if (tid < F3) {
@@ -413,17 +427,25 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     if (i < F1 && part == 0) sm[S_D1 + i] = sm[S_H1 + i] > 0.f ? s : 0.f;
   }
   lds_barrier();
-  if (tid < F0) {  // da2 = W1f dz1, through ReLU2 (pooled > 0) -> g2
-    const float4* wv = g1w;
+  // da2 = W1f dz1 from the register blocks: partials [cb][i], then 12 column
+  // blocks summed in order per input, through ReLU2 (pooled > 0) -> g2
+  if (tid < 480) {
+    float dv[10];
+#pragma unroll
+    for (int c = 0; c < 10; ++c) dv[c] = sm[S_D1 + j0 + c];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 10; ++c) acc = fmaf(w1b[r][c], dv[c], acc);
+      sm[S_C2P + cb * F0 + i0 + r] = acc;
+    }
+  }
+  lds_barrier();
+  if (tid < F0) {
     float s = 0.f;
 #pragma unroll
-    for (int j4 = 0; j4 < F1 / 4; ++j4) {
-      const float* d = sm + S_D1 + 4 * j4;
-      s = fmaf(wv[j4].x, d[0], s);
-      s = fmaf(wv[j4].y, d[1], s);
-      s = fmaf(wv[j4].z, d[2], s);
-      s = fmaf(wv[j4].w, d[3], s);
-    }
+    for (int c = 0; c < 12; ++c) s += sm[S_C2P + c * F0 + tid];
     const float g2 = sm[S_P2 + tid] > 0.f ? s : 0.f;
     // pool2 backward: the gradient lands on the argmax pixel of the window
     const int co = tid & 15, pp = tid >> 4, py = pp / P2, px = pp % P2, q = q2s[tid];

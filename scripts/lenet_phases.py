@@ -17,7 +17,7 @@ e = NativeLenetEngine(C.TrainConfig(model="lenet5", batch_size=B).validate(), x,
 e.train(5)
 Cn = native()
 prev = 0.0
-for stop in (0, 1, 2, 3, 4, 5, 6, 99):
+for stop in (0, 1, 2, 10, 11, 12, 3, 4, 5, 6, 99):  # 10-12: D / E / F inside 3
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         for _ in range(50):
