@@ -1530,14 +1530,17 @@ static void slab_reduce(float* slabs, int nz, long long n4, float* out, hipStrea
                         const ConvStats* stats = nullptr, int C = 0,
                         const BnBwdStats* bstats = nullptr) {
   const long long b = slab_blocks(n4);
-  if (b < 128 && nz >= 32 && !addend && !outb && !(stats && stats->part) &&
-      !(bstats && bstats->part)) {
+  if (nz >= 16 && !addend && !outb && !(stats && stats->part) && !(bstats && bstats->part)) {
+    // plain sums of 16+ slabs: G lanes per output keep more loads in flight
+    // than one thread walking every slab
+    const float4* P4 = reinterpret_cast<const float4*>(slabs);
+    float4* O4 = reinterpret_cast<float4*>(out);
     if (nz >= 128)
-      slab_sumg4_kernel<16><<<cdiv(n4 * 16, 256), 256, 0, st>>>(
-          reinterpret_cast<const float4*>(slabs), nz, n4, reinterpret_cast<float4*>(out));
+      slab_sumg4_kernel<16><<<cdiv(n4 * 16, 256), 256, 0, st>>>(P4, nz, n4, O4);
+    else if (nz >= 32)
+      slab_sumg4_kernel<8><<<cdiv(n4 * 8, 256), 256, 0, st>>>(P4, nz, n4, O4);
     else
-      slab_sumg4_kernel<8><<<cdiv(n4 * 8, 256), 256, 0, st>>>(
-          reinterpret_cast<const float4*>(slabs), nz, n4, reinterpret_cast<float4*>(out));
+      slab_sumg4_kernel<4><<<cdiv(n4 * 4, 256), 256, 0, st>>>(P4, nz, n4, O4);
     return;
   }
   int G = 1;
