@@ -2818,19 +2818,40 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
     return;
   }
   blk -= 16;
-  const int o = blk * 4 + (tid >> 6);
-  if (o >= 832) return;
-  const int off = o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800);
-  float s = 0.f;
+  // conv1 weights + bias: 4 consecutive parameters a wave (16 a block, so the
+  // launch fits one round of 2 blocks per CU), their partial rows as one
+  // float4 per row; each parameter's sum runs in the same order as one wave
+  // per parameter did
+  const int o0 = (blk * 4 + (tid >> 6)) * 4;
+  if (o0 >= 832) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
   if (a.flat) {
-    s = a.g[off];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = o0 + k;
+      s[k] = a.g[o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800)];
+    }
   } else {
 #pragma unroll 8
-    for (int b = lane; b < a.nblk1; b += 64) s += a.part1[(size_t)b * 832 + o];
-    s = wave_sum(s);
+    for (int b = lane; b < a.nblk1; b += 64) {
+      const float4 v = *reinterpret_cast<const float4*>(a.part1 + (size_t)b * 832 + o0);
+      s[0] += v.x;
+      s[1] += v.y;
+      s[2] += v.z;
+      s[3] += v.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) s[k] = wave_sum(s[k]);
   }
-  if (lane == 0)
-    sgd_elem(a.w + off, a.mom + off, __builtin_fmaf(0.f, a.w[off], s * a.gscale), lr, a.momentum);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = o0 + k;
+      const int off = o < 800 ? a.off_w1 + o : a.off_b1 + (o - 800);
+      sgd_elem(a.w + off, a.mom + off, __builtin_fmaf(0.f, a.w[off], s[k] * a.gscale), lr,
+               a.momentum);
+    }
+  }
 }
 
 void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
@@ -2875,7 +2896,7 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
   a.Ud = p.wino_ud;
   a.w2t = reinterpret_cast<__bf16*>(p.w2tb);
   a.w2b = reinterpret_cast<__bf16*>(p.w2b);
-  const int conv_blocks = p.conv ? (p.wino_u ? 128 : 50) + 16 + cdiv(832, 4) : 0;
+  const int conv_blocks = p.conv ? (p.wino_u ? 128 : 50) + 16 + cdiv(832, 16) : 0;
   const int grid = (a.fc.a2 ? FC1BWD_DW_BLOCKS : 0) + a.fc.nblk + conv_blocks;
   if (grid == 0) throw std::runtime_error("sgd_step: nothing to update");
   sgd_finalize_kernel<<<grid, 256, 0, s>>>(a);
