@@ -93,7 +93,12 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
   }
   if (a.step && blockIdx.x == 0 && tid == 0) *a.step += 1;
   link_floor(s, t0, a.link_bytes);
-  barrier(s, 2, e, false);
+  // closing "done reading" barrier: a plain all-reduce's peers rewrite the
+  // buffers this gather reads (their next grads) right after the kernel.  The
+  // fused SGD's gather reads the peers' PARAMS, which a peer rewrites only in
+  // its next call's phase 1 - after that call's arrival barrier, which this
+  // rank reaches only once this kernel (gather included) is done: no barrier
+  if (!sgd) barrier(s, 2, e, false);
 }
 
 void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st) {
