@@ -209,24 +209,26 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   lds_barrier();
   if (a.stop_phase == 1) return;
   // the FC1 weights, requested now (their round trip hides under conv2) and
-  // kept in registers for BOTH FC1 passes: thread t < 480 holds the 10 x 10
-  // block (rows 10 rb .., columns 10 cb ..) of W1 [400][120] - forward
+  // kept in registers for BOTH FC1 passes: thread t < 500 holds the 8 x 12
+  // block (rows 8 rb .., columns 12 cb ..) of W1 [400][120] - forward
   // (phase D) and backward (da2 in phase G) each sum in-thread over one block
   // axis and across threads over the other, through LDS.  (With a column per
   // thread, the backward had to read W1 again by rows: a 49 MB burst over all
   // workgroups at once, ~3 us.)
   const int fj = tid & 127, fg = tid >> 7;
-  const int rb = min(tid, 479) / 12, cb = min(tid, 479) % 12, i0 = 10 * rb, j0 = 10 * cb;
-  float w1b[10][10];
+  const int rb = min(tid, 499) / 10, cb = min(tid, 499) % 10, i0 = 8 * rb, j0 = 12 * cb;
+  float w1b[8][12];
   {
-    const float2* wp = reinterpret_cast<const float2*>(W + o.f1w + i0 * F1 + j0);
+    const float4* wp = reinterpret_cast<const float4*>(W + o.f1w + i0 * F1 + j0);
 #pragma unroll
-    for (int r = 0; r < 10; ++r)
+    for (int r = 0; r < 8; ++r)
 #pragma unroll
-      for (int c = 0; c < 5; ++c) {
-        const float2 v = wp[(r * F1) / 2 + c];
-        w1b[r][2 * c] = v.x;
-        w1b[r][2 * c + 1] = v.y;
+      for (int c = 0; c < 3; ++c) {
+        const float4 v = wp[(r * F1) / 4 + c];
+        w1b[r][4 * c] = v.x;
+        w1b[r][4 * c + 1] = v.y;
+        w1b[r][4 * c + 2] = v.z;
+        w1b[r][4 * c + 3] = v.w;
       }
   }
 
@@ -309,25 +311,25 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     }
   }
   // ---- D: FC1 400 -> 120 + ReLU from the register blocks: partials
-  // [rb][j] in the (free) conv2 partial region, then 40 row blocks summed in
+  // [rb][j] in the (free) conv2 partial region, then 50 row blocks summed in
   // order per output
-  if (tid < 480) {
-    float xv[10];
+  if (tid < 500) {
+    float xv[8];
 #pragma unroll
-    for (int r = 0; r < 10; ++r) xv[r] = sm[S_P2 + i0 + r];
+    for (int r = 0; r < 8; ++r) xv[r] = sm[S_P2 + i0 + r];
 #pragma unroll
-    for (int c = 0; c < 10; ++c) {
+    for (int c = 0; c < 12; ++c) {
       float acc = 0.f;
 #pragma unroll
-      for (int r = 0; r < 10; ++r) acc = fmaf(xv[r], w1b[r][c], acc);
+      for (int r = 0; r < 8; ++r) acc = fmaf(xv[r], w1b[r][c], acc);
       sm[S_C2P + rb * F1 + j0 + c] = acc;
     }
   }
   lds_barrier();
   if (tid < F1) {
     float z = sm[S_FB + tid];
-#pragma unroll 8
-    for (int r = 0; r < 40; ++r) z += sm[S_C2P + r * F1 + tid];
+#pragma unroll 10
+    for (int r = 0; r < 50; ++r) z += sm[S_C2P + r * F1 + tid];
     sm[S_H1 + tid] = relu(z);
   }
   lds_barrier();
@@ -427,17 +429,17 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
     if (i < F1 && part == 0) sm[S_D1 + i] = sm[S_H1 + i] > 0.f ? s : 0.f;
   }
   lds_barrier();
-  // da2 = W1f dz1 from the register blocks: partials [cb][i], then 12 column
+  // da2 = W1f dz1 from the register blocks: partials [cb][i], then 10 column
   // blocks summed in order per input, through ReLU2 (pooled > 0) -> g2
-  if (tid < 480) {
-    float dv[10];
+  if (tid < 500) {
+    float dv[12];
 #pragma unroll
-    for (int c = 0; c < 10; ++c) dv[c] = sm[S_D1 + j0 + c];
+    for (int c = 0; c < 12; ++c) dv[c] = sm[S_D1 + j0 + c];
 #pragma unroll
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < 8; ++r) {
       float acc = 0.f;
 #pragma unroll
-      for (int c = 0; c < 10; ++c) acc = fmaf(w1b[r][c], dv[c], acc);
+      for (int c = 0; c < 12; ++c) acc = fmaf(w1b[r][c], dv[c], acc);
       sm[S_C2P + cb * F0 + i0 + r] = acc;
     }
   }
@@ -445,7 +447,7 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   if (tid < F0) {
     float s = 0.f;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) s += sm[S_C2P + c * F0 + tid];
+    for (int c = 0; c < 10; ++c) s += sm[S_C2P + c * F0 + tid];
     const float g2 = sm[S_P2 + tid] > 0.f ? s : 0.f;
     // pool2 backward: the gradient lands on the argmax pixel of the window
     const int co = tid & 15, pp = tid >> 4, py = pp / P2, px = pp % P2, q = q2s[tid];
