@@ -170,40 +170,36 @@ __global__ __launch_bounds__(NT, 1) void image_kernel(const ImageArgs a) {
   const int label = a.y[row];
   lds_barrier();
   if (a.stop_phase == 0) return;
-  // ---- B: conv1 + bias + ReLU + pool: thread = (pooled pixel, 3 channels);
-  // the channel triple is wave-uniform (weights are LDS broadcasts)
-  {
-    const int cg = tid >> 8, p = tid & 255;
-    if (p < P1 * P1) {
-      const int py = p / P1, px = p % P1;
-      f2 s01[3], s23[3];
+  // ---- B: conv1 + bias + ReLU + pool: thread = pooled pixel, all 6 channels
+  // (each input read feeds 6 channels; the weights are LDS broadcasts)
+  if (tid < P1 * P1) {
+    const int p = tid, py = p / P1, px = p % P1;
+    f2 s01[C1], s23[C1];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) s01[c] = s23[c] = f2{0.f, 0.f};
+    for (int c = 0; c < C1; ++c) s01[c] = s23[c] = f2{0.f, 0.f};
 #pragma unroll
-      for (int ci = 0; ci < IC; ++ci)
+    for (int ci = 0; ci < IC; ++ci)
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
+      for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-          for (int kw = 0; kw < 5; ++kw) {
-            const float* xp = sm + S_X + ci * XPL + (2 * py + kh) * XRS + 2 * px + kw;
-            const f2 x01 = {xp[0], xp[1]}, x23 = {xp[XRS], xp[XRS + 1]};
-            const float* wp = sm + S_W1 + ((kh * 5 + kw) * IC + ci) * C1 + 3 * cg;
+        for (int kw = 0; kw < 5; ++kw) {
+          const float* xp = sm + S_X + ci * XPL + (2 * py + kh) * XRS + 2 * px + kw;
+          const f2 x01 = {xp[0], xp[1]}, x23 = {xp[XRS], xp[XRS + 1]};
+          const float* wp = sm + S_W1 + ((kh * 5 + kw) * IC + ci) * C1;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              const f2 w = {wp[c], wp[c]};
-              s01[c] = __builtin_elementwise_fma(x01, w, s01[c]);
-              s23[c] = __builtin_elementwise_fma(x23, w, s23[c]);
-            }
+          for (int c = 0; c < C1; ++c) {
+            const f2 w = {wp[c], wp[c]};
+            s01[c] = __builtin_elementwise_fma(x01, w, s01[c]);
+            s23[c] = __builtin_elementwise_fma(x23, w, s23[c]);
           }
+        }
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float v;
-        int q;
-        pool4(s01[c], s23[c], v, q);
-        const int co = 3 * cg + c;
-        sm[S_P1 + p * C1 + co] = relu(v + sm[S_B1 + co]);
-        q1s[p * C1 + co] = (uint8_t)q;
-      }
+    for (int c = 0; c < C1; ++c) {
+      float v;
+      int q;
+      pool4(s01[c], s23[c], v, q);
+      sm[S_P1 + p * C1 + c] = relu(v + sm[S_B1 + c]);
+      q1s[p * C1 + c] = (uint8_t)q;
     }
   }
   lds_barrier();
