@@ -70,6 +70,9 @@ def parse(argv=None):
                          "GPUs; on one node the xGMI peer-to-peer schedule is also tuned)")
     ap.add_argument("--no-xgmi", action="store_true",
                     help="comm auto: do not set up the xGMI peer-to-peer communicator")
+    ap.add_argument("--xgmi-inject-skip-peer", type=int, default=-1, metavar="R",
+                    help="failure injection (tests): the xGMI phase-1 reductions leave out rank "
+                         "R; the exactness gate must then reject the xGMI communicator")
     ap.add_argument("--xgmi-emulate", default=None, metavar="LAT_US,LINK_GBPS[,N]",
                     help="1 GPU, MNIST: the xGMI peer-to-peer schedule against N (default 8) "
                          "virtual ranks whose phases last at least their bytes on one link at "
@@ -217,10 +220,9 @@ def main(argv=None) -> int:
 def run(a, di, device, wd) -> int:
     from mpi_tensorflow_amd import config as C
     from mpi_tensorflow_amd.parallel import dist as D
-    from mpi_tensorflow_amd.parallel.comm import make_comm
+    from mpi_tensorflow_amd.parallel.setup import check_health, setup_comms
     from mpi_tensorflow_amd.parallel.watchdog import run_in_chunks
     from mpi_tensorflow_amd.runtime.mnist_engine import make_engine
-    from mpi_tensorflow_amd.runtime.trainer import comm_capacity_bytes
     from mpi_tensorflow_amd.utils.data import load_mnist_shard
     from mpi_tensorflow_amd.utils.faults import maybe_fail
 
@@ -232,25 +234,32 @@ def run(a, di, device, wd) -> int:
                         sync_schedule=a.sync_schedule, comm=a.comm,
                         defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
                         bucket_plan=f"bytes:{a.bucket_mb:g}" if a.bucket_mb else a.bucket_plan,
-                        collective_timeout_s=a.collective_timeout_s).validate()
+                        collective_timeout_s=a.collective_timeout_s,
+                        no_xgmi=a.no_xgmi).validate()
     force = bool((a.force_sync or a.comm_emulate or a.xgmi_emulate) and N == 1
                  and device.type == "cuda")
     with wd.guard("start-up (communicator, engine)"):
         maybe_fail("before_comm", di.rank)
-        comm = xcomm = None
-        if N > 1 and a.sync == "grad":
-            comm = make_comm(di, device, a.comm, shm_capacity=comm_capacity_bytes(cfg),
-                             timeout_s=a.collective_timeout_s)
-            # one node, one GPU per rank: the xGMI peer-to-peer schedule is a
-            # tune candidate next to RCCL's (health-checked: timeouts, replicas)
-            if (a.comm == "auto" and not a.no_xgmi and a.model == "mnist_cnn"
-                    and getattr(comm, "kind", "") == "rccl-native"):
-                from mpi_tensorflow_amd.parallel.comm import make_xgmi_comm
-                xcomm = make_xgmi_comm(di, device, min(20.0, a.collective_timeout_s))
+        # the same set-up as the mpipy.py Trainer (parallel/setup.py): the device
+        # comm and, on one node, the exactness-gated xGMI candidate
+        if a.xgmi_inject_skip_peer >= 0:
+            import mpi_tensorflow_amd.parallel.comm as CM
+            CM.INJECT_SKIP_PEER = a.xgmi_inject_skip_peer
+        comms = setup_comms(di, device, cfg, no_xgmi=a.no_xgmi,
+                            xgmi_timeout_s=min(20.0, a.collective_timeout_s))
+        comm, xcomm = comms.comm, comms.xcomm
         if force and a.xgmi_emulate:
-            from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+            from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm, xgmi_exactness_check
             f = [float(v) for v in a.xgmi_emulate.split(",")]
             xe = XgmiDeviceComm.emulated(int(f[2]) if len(f) > 2 else 8, f[0], f[1])
+            if a.xgmi_inject_skip_peer >= 0:
+                xe.inject_skip_peer(a.xgmi_inject_skip_peer)
+            why = xgmi_exactness_check(xe)
+            comms.xgmi_status = "passed" if why is None else f"dropped: exactness check failed ({why})"
+            if why is not None:
+                print(f"error: the emulated xGMI communicator failed its exactness check ({why})",
+                      file=sys.stderr)
+                return 5
             if a.comm_emulate:  # both: the xGMI schedule is a candidate next to the RCCL ones
                 xcomm = xe
             else:
@@ -322,6 +331,8 @@ def run(a, di, device, wd) -> int:
         t1 = time.perf_counter()
     D.barrier()
     dt = D.allreduce_max_host(t1 - t0)
+    if N > 1:  # every rank stops when any rank's xGMI barrier timed out
+        check_health("timed steps", comm, eng)
     err = float("nan")
     if not a.no_eval:
         # accuracy of the reference's full run: MNIST trains `epochs` local
@@ -389,6 +400,7 @@ def run(a, di, device, wd) -> int:
                 "engine": eng.kind,
                 "comm": getattr(comm, "kind", "none"),
                 "xgmi_comm": getattr(xcomm, "kind", None),
+                "xgmi_gate": comms.xgmi_status,
                 "ranks": N,
                 "comm_nranks": comm_nranks,
                 "sync_schedule": getattr(eng, "sync_schedule", "n/a"),
@@ -399,6 +411,10 @@ def run(a, di, device, wd) -> int:
                 "prewarm_ms": prewarm_ms,
                 "prewarm": prewarm_mode,
                 "replicas_identical": replicas,
+                # generic engines' segmented step: nodes of each overlapped
+                # bucket's collective graph (N > 1: every one moves bytes)
+                "collective_graph_nodes": (eng.collective_graph_nodes()
+                                           if hasattr(eng, "collective_graph_nodes") else None),
             },
             "final_test_accuracy": None if err != err else round(100.0 - err, 3),
             "test_eval_after_steps": int(eng.step),

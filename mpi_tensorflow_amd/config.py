@@ -105,6 +105,9 @@ class TrainConfig:
     # BUCKET_PLANS candidates on the real communicator at startup
     bucket_plan: str = "auto"
     comm: str = "auto"
+    # comm auto, one node: do not set up the xGMI peer-to-peer communicator as
+    # an extra sync-schedule candidate (parallel/setup.py setup_comms)
+    no_xgmi: bool = False
     # fp32 MNIST conv2 algorithm on the native engine: "winograd" (F(2x2,5x5),
     # kernels/wino.h; 2.8x fewer MFMAs, fp32 arithmetic throughout, ~1e-6
     # relative error) or "direct" (25-tap implicit GEMM)
@@ -228,6 +231,9 @@ def build_arg_parser(prog: str = "mpipy.py") -> argparse.ArgumentParser:
                    help="device communicator: RCCL over xGMI (one GPU per rank), shm (host-"
                         "staged shared memory, ranks may share a GPU), xgmi (peer-to-peer "
                         "kernels on the compute stream, one node) or torch.distributed")
+    p.add_argument("--no-xgmi", action="store_true",
+                   help="comm auto: do not set up the xGMI peer-to-peer communicator "
+                        "(otherwise gated by an exactness check, then tuned next to RCCL)")
     p.add_argument("--conv-algo", default=d.conv_algo, choices=("winograd", "direct"),
                    help="fp32 MNIST conv2 algorithm of the native engine")
     p.add_argument("--deterministic", action="store_true",

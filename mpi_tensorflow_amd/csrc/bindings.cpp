@@ -675,6 +675,10 @@ PYBIND11_MODULE(_C, m) {
       .def("ready", &XgmiComm::ready)
       .def("set_lean", &XgmiComm::set_lean)
       .def("emulate_dead_rank", &XgmiComm::emulate_dead_rank)
+      .def("inject_skip_peer", &XgmiComm::inject_skip_peer)
+      .def_property_readonly("skip_peer", &XgmiComm::skip_peer)
+      .def_property_readonly("link_ticks_per_mib", &XgmiComm::link_ticks_per_mib)
+      .def("emulate_fill_peer", &XgmiComm::emulate_fill_peer)
       .def_property_readonly("lean", &XgmiComm::lean)
       .def("registered", [](const XgmiComm& c, uintptr_t p, size_t bytes) {
         return c.registered(reinterpret_cast<const void*>(p), bytes);

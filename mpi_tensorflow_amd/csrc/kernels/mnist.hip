@@ -1951,7 +1951,7 @@ __device__ void xgmi_fc_role(const XgmiStepArgs& a, unsigned* ep) {
       const unsigned off = (unsigned)((base + i0 + nt * u) * 16);
 #pragma unroll
       for (int r = 0; r < xgmi::kMaxRanks; ++r)
-        if (r < n && ok) v[r][u] = xgmi::ld4_sys(gr[r], off);
+        if (r < n && ok) v[r][u] = xgmi::ld4_peer(s, r, gr[r], off);
       if (ok) {
         wv[u] = W4[base + i0 + nt * u];
         mv[u] = M4[base + i0 + nt * u];
@@ -3056,10 +3056,10 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
     const XsConvItem it = xs_conv_item(a, v, tid);
     if (it.kind == 1) {
       if (it.off >= 0 && lane == 0) {
-        float sv = xgmi::ld_sys(gr[0], (unsigned)(4 * it.off));
+        float sv = xgmi::ld_peer(s, 0, gr[0], (unsigned)(4 * it.off));
 #pragma unroll
         for (int r = 1; r < xgmi::kMaxRanks; ++r)
-          if (r < n) sv += xgmi::ld_sys(gr[r], (unsigned)(4 * it.off));
+          if (r < n) sv += xgmi::ld_peer(s, r, gr[r], (unsigned)(4 * it.off));
         float* w = a.w[me] + it.off;
         sgd_elem(w, a.mom + it.off, __builtin_fmaf(0.f, *w, sv * a.gscale), lr, a.momentum);
       }
@@ -3072,10 +3072,10 @@ __global__ __launch_bounds__(256) void xgmi_step_kernel(const XgmiStepArgs a) {
       wv = *wp;
       float4 mv = *mp;
       const unsigned off = (unsigned)(4 * a.off_w2 + 16 * it.i4);
-      float4 sv = xgmi::ld4_sys(gr[0], off);
+      float4 sv = xgmi::ld4_peer(s, 0, gr[0], off);
 #pragma unroll
       for (int r = 1; r < xgmi::kMaxRanks; ++r)
-        if (r < n) sv = add4(sv, xgmi::ld4_sys(gr[r], off));
+        if (r < n) sv = add4(sv, xgmi::ld4_peer(s, r, gr[r], off));
       sgd4(wv, mv, sv, 0.f, lr, a.momentum, a.gscale);
       *wp = wv;
       *mp = mv;

@@ -35,7 +35,7 @@
 // Emulation (one GPU, `emulate`): the N - 1 peers are local stand-in buffers,
 // a block's flag stores go to its own array for every source slot, and each
 // phase lasts at least the time its bytes take on one xGMI link
-// (`link_ticks_per_kb`), plus `lat_ticks` per barrier, so schedules can be
+// (`link_ticks_per_mib`), plus `lat_ticks` per barrier, so schedules can be
 // timed before a multi-GPU node is available.  Numerics of an emulated run
 // are NOT those of N ranks.
 #pragma once
@@ -62,7 +62,9 @@ struct Sync {
   unsigned* error = nullptr;                  // bit 0: a barrier timed out
   int emulate = 0;
   long long lat_ticks = 0;                    // emulated hop latency (100 MHz ticks)
-  long long link_ticks_per_kb = 0;            // emulated link time per KiB per link
+  // emulated link time per MiB per link, in 100 MHz ticks (a MiB keeps the
+  // rounding below 0.1 % at any xGMI rate: 150 GB/s = 699 ticks)
+  long long link_ticks_per_mib = 0;
   long long timeout_ticks = 1000000000;       // 10 s
   // the ranks share ONE GPU (tests): launch few spinning blocks, so a rank
   // waiting at a barrier leaves CUs for the other ranks' kernels on the device
@@ -70,7 +72,18 @@ struct Sync {
   // emulation, failure injection: this virtual rank never arrives (its flag
   // slots stay unwritten), so every barrier times out (-1: none)
   int dead_rank = -1;
+  // failure injection (tests, any communicator): the reductions leave out rank
+  // skip_peer's contribution (-1: none), on every rank that has it set - rank
+  // skip_peer itself included, as if its gradients never arrived anywhere.
+  // Every rank then ends with the same wrong sums - identical replicas - which
+  // only an exactness check can see (parallel/comm.py xgmi_exactness_check)
+  int skip_peer = -1;
 };
+
+// rank r's contribution enters a reduction on this rank
+__device__ __forceinline__ bool contributes(const Sync& s, int r) {
+  return r < s.nranks && r != s.skip_peer;
+}
 
 __device__ __forceinline__ long long now_ticks() {
   return (long long)__builtin_amdgcn_s_memrealtime();  // 100 MHz, shader-clock independent
@@ -153,12 +166,20 @@ __device__ __forceinline__ void st_sys(Rsrc r, unsigned off, float v) {
   __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, kSysCpol);
 }
 
+// a phase-1 operand: rank r's value, or 0 when the skip-peer fault leaves it out
+__device__ __forceinline__ float4 ld4_peer(const Sync& s, int r, Rsrc rs, unsigned off) {
+  return contributes(s, r) ? ld4_sys(rs, off) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float ld_peer(const Sync& s, int r, Rsrc rs, unsigned off) {
+  return contributes(s, r) ? ld_sys(rs, off) : 0.f;
+}
+
 // emulation: hold the block until `bytes` (a whole phase's bytes on ONE
 // link: every block of the phase shares the links) would have crossed an xGMI
 // link since t0 (no-op on real peers)
 __device__ __forceinline__ void link_floor(const Sync& s, long long t0, long long bytes) {
-  if (!s.emulate || s.link_ticks_per_kb <= 0) return;
-  const long long until = t0 + (bytes * s.link_ticks_per_kb) / 1024;
+  if (!s.emulate || s.link_ticks_per_mib <= 0) return;
+  const long long until = t0 + (bytes * s.link_ticks_per_mib) / (1LL << 20);
   if (threadIdx.x == 0)
     while (now_ticks() < until) __builtin_amdgcn_s_sleep(2);
   __syncthreads();
@@ -178,6 +199,9 @@ struct AllReduceArgs {
   int per4 = 0;                // float4s per block per segment
   long long link_bytes = 0;    // one phase's bytes on one link (emulation floor)
   int gather_only = 0;         // skip phase 1: every rank's segment is already final
+  // reduce-scatter: phase 1 only, the reduced segment of this rank goes to
+  // `out` (local, seg4 float4s) instead of back into buf (no phase 2)
+  float* out = nullptr;
   // momentum SGD fused into phase 1 (all_reduce_sgd): buf = the grads; the
   // reduced segment updates w[rank] / mom there (optim::sgd_momentum_flat's
   // forms; L2 on float4s < l2_end4), and phase 2 gathers w instead of buf
@@ -188,6 +212,8 @@ struct AllReduceArgs {
   long long l2_end4 = 0;
   long long* step = nullptr;  // bumped once (optional)
 };
-void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st);
+// nt: threads per block (64 for small buffers: more blocks, each with one
+// float4 a thread in flight per rank; 256 otherwise)
+void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st);
 
 }  // namespace xgmi

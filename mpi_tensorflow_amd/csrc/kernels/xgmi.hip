@@ -9,11 +9,13 @@ namespace xgmi {
 
 constexpr int kAllReduceUnroll = 2;  // float4s in flight per thread per rank
 
-__global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void allreduce_kernel(const AllReduceArgs a) {
   __shared__ unsigned ep;
   const Sync& s = a.s;
   const int n = s.nranks, me = s.rank, tid = threadIdx.x;
   const bool sgd = a.mom != nullptr;
+  const bool reduce_only = a.out != nullptr;
   // every peer-visible byte through system-scope loads / stores (xgmi.h)
   Rsrc br[kMaxRanks], wr[kMaxRanks];
 #pragma unroll
@@ -30,19 +32,22 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
   long long t0 = now_ticks();
   if (!a.gather_only) {
     const long long base = (long long)me * a.seg4;
-    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * kAllReduceUnroll) {
+    for (long long i0 = lo + tid; i0 < hi; i0 += NT * kAllReduceUnroll) {
       float4 acc[kAllReduceUnroll];
       float4 v[kMaxRanks][kAllReduceUnroll];
+      // every rank's loads in flight at once (one round trip per unroll)
 #pragma unroll
       for (int r = 0; r < kMaxRanks; ++r)
 #pragma unroll
         for (int u = 0; u < kAllReduceUnroll; ++u) {
-          const long long i = base + i0 + 256 * u;
-          if (r < n && i0 + 256 * u < hi && i < a.n4) v[r][u] = ld4_sys(br[r], (unsigned)(i * 16));
+          const long long i = base + i0 + NT * u;
+          v[r][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (contributes(s, r) && i0 + NT * u < hi && i < a.n4)
+            v[r][u] = ld4_sys(br[r], (unsigned)(i * 16));
         }
 #pragma unroll
       for (int u = 0; u < kAllReduceUnroll; ++u) {
-        acc[u] = v[0][u];
+        acc[u] = v[0][u];  // rank order 0..N-1, as a host reduction in rank order
 #pragma unroll
         for (int r = 1; r < kMaxRanks; ++r)
           if (r < n) {
@@ -51,8 +56,8 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
             acc[u].z += v[r][u].z;
             acc[u].w += v[r][u].w;
           }
-        const long long i = base + i0 + 256 * u;
-        if (!(i0 + 256 * u < hi && i < a.n4)) continue;
+        const long long i = base + i0 + NT * u;
+        if (!(i0 + NT * u < hi && i < a.n4)) continue;
         if (sgd) {  // optim::sgd_momentum_flat_kernel's expression forms
           float4* M4 = reinterpret_cast<float4*>(a.mom);
           float4 wv = reinterpret_cast<const float4*>(a.w[me])[i], gv = acc[u], mv = M4[i];
@@ -71,25 +76,42 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
           wv.w -= lr * mv.w;
           st4_sys(wr[me], (unsigned)(i * 16), wv);
           M4[i] = mv;
+        } else if (reduce_only) {
+          reinterpret_cast<float4*>(a.out)[i - base] = acc[u];  // local: no peer reads it
         } else {
           st4_sys(br[me], (unsigned)(i * 16), acc[u]);
         }
       }
     }
+    link_floor(s, t0, a.link_bytes);
   }
-  if (!a.gather_only) link_floor(s, t0, a.link_bytes);
-  barrier(s, 1, e, false);
+  // reduce-scatter: this barrier is the "done reading" one (the peers may
+  // rewrite their send buffers after the kernel); gather-only: every segment
+  // was final at the arrival barrier, no second one
+  if (!a.gather_only) barrier(s, 1, e, false);
+  if (reduce_only) return;
   t0 = now_ticks();
   float* const* out = sgd ? a.w : a.buf;  // phase 2 gathers the updated params
+  float4* O4 = reinterpret_cast<float4*>(out[me]);
+  // every other rank's slice with all loads in flight before the stores (one
+  // round trip per unroll, not one per rank)
+  for (long long i0 = lo + tid; i0 < hi; i0 += NT * kAllReduceUnroll) {
+    float4 v[kMaxRanks][kAllReduceUnroll];
 #pragma unroll
-  for (int r = 0; r < kMaxRanks; ++r) {
-    if (r >= n || r == me) continue;
-    const Rsrc src = sgd ? wr[r] : br[r];
-    const long long base = (long long)r * a.seg4;
-    for (long long i0 = lo + tid; i0 < hi; i0 += 256) {
-      const long long i = base + i0;
-      if (i < a.n4) reinterpret_cast<float4*>(out[me])[i] = ld4_sys(src, (unsigned)(i * 16));
-    }
+    for (int r = 0; r < kMaxRanks; ++r)
+#pragma unroll
+      for (int u = 0; u < kAllReduceUnroll; ++u) {
+        const long long i = (long long)r * a.seg4 + i0 + NT * u;
+        if (r < n && r != me && i0 + NT * u < hi && i < a.n4)
+          v[r][u] = ld4_sys(sgd ? wr[r] : br[r], (unsigned)(i * 16));
+      }
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+#pragma unroll
+      for (int u = 0; u < kAllReduceUnroll; ++u) {
+        const long long i = (long long)r * a.seg4 + i0 + NT * u;
+        if (r < n && r != me && i0 + NT * u < hi && i < a.n4) O4[i] = v[r][u];
+      }
   }
   if (a.step && blockIdx.x == 0 && tid == 0) *a.step += 1;
   link_floor(s, t0, a.link_bytes);
@@ -101,7 +123,7 @@ __global__ __launch_bounds__(256) void allreduce_kernel(const AllReduceArgs a) {
   if (!sgd) barrier(s, 2, e, false);
 }
 
-void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st) {
+void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st) {
   if (blocks < 1 || blocks > kMaxBlocks)
     throw std::runtime_error("xgmi all_reduce: grid of " + std::to_string(blocks) + " blocks");
   if (a.s.nranks < 1 || a.s.nranks > kMaxRanks || !a.s.flags || !a.s.epoch || !a.s.error)
@@ -109,7 +131,14 @@ void launch_allreduce(const AllReduceArgs& a, int blocks, hipStream_t st) {
   for (int r = 0; r < a.s.nranks; ++r)
     if (!a.buf[r] || (!a.s.emulate && !a.s.peer_flags[r]))
       throw std::runtime_error("xgmi all_reduce: rank " + std::to_string(r) + " not mapped");
-  allreduce_kernel<<<blocks, 256, 0, st>>>(a);
+  if ((long long)blocks * a.per4 < a.seg4 || a.per4 % nt)
+    throw std::runtime_error("xgmi all_reduce: grid does not cover the segment");
+  if (nt == 64)
+    allreduce_kernel<64><<<blocks, 64, 0, st>>>(a);
+  else if (nt == 256)
+    allreduce_kernel<256><<<blocks, 256, 0, st>>>(a);
+  else
+    throw std::runtime_error("xgmi all_reduce: 64 or 256 threads a block");
 }
 
 }  // namespace xgmi

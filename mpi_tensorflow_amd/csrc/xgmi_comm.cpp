@@ -46,8 +46,9 @@ XgmiComm::XgmiComm(int nranks, int rank, bool emulate, double lat_us, double lin
   sync_.timeout_ticks = (long long)(timeout_s * 1e8);
   if (emulate) {
     sync_.lat_ticks = (long long)(lat_us * 100.0);
-    // 1 KiB at link_gbps GB/s, in 100 MHz ticks
-    sync_.link_ticks_per_kb = link_gbps > 0 ? (long long)(1024.0 / (link_gbps * 1e9) * 1e8 + 0.5) : 0;
+    // 1 MiB at link_gbps GB/s, in 100 MHz ticks
+    sync_.link_ticks_per_mib =
+        link_gbps > 0 ? (long long)(1048576.0 / (link_gbps * 1e9) * 1e8 + 0.5) : 0;
     for (int r = 0; r < nranks; ++r) sync_.peer_flags[r] = flags_;
   }
 }
@@ -202,8 +203,16 @@ void XgmiComm::all_reduce_sgd(float* grads, float* params, float* mom, size_t co
   launch(grads, count, false, s, &a);
 }
 
+void XgmiComm::emulate_fill_peer(uintptr_t local, int r, uintptr_t src, size_t bytes) {
+  if (!emulate_) throw std::runtime_error("XgmiComm: emulate_fill_peer on a real communicator");
+  const Reg* g = find(reinterpret_cast<const void*>(local), bytes);
+  if (!g || r < 0 || r >= nranks_) throw std::runtime_error("XgmiComm: emulate_fill_peer target");
+  HIP_CHECK(hipMemcpy(peer_ptr(reinterpret_cast<const void*>(local), r),
+                      reinterpret_cast<const void*>(src), bytes, hipMemcpyDeviceToDevice));
+}
+
 void XgmiComm::launch(void* recv, size_t count, bool gather_only, hipStream_t s,
-                      const xgmi::AllReduceArgs* sgd) {
+                      const xgmi::AllReduceArgs* sgd, float* out) {
   if (count == 0) return;
   if (count % 4) throw std::runtime_error("XgmiComm::all_reduce: count must be a multiple of 4");
   if (!ready()) throw std::runtime_error("XgmiComm: flags of some rank not mapped");
@@ -215,22 +224,42 @@ void XgmiComm::launch(void* recv, size_t count, bool gather_only, hipStream_t s,
   for (int r = 0; r < nranks_; ++r) a.buf[r] = static_cast<float*>(peer_ptr(recv, r));
   a.n4 = (long long)(count / 4);
   a.seg4 = (a.n4 + nranks_ - 1) / nranks_;
-  // <= 256 blocks (64 when the ranks share a GPU: a block waiting at a
-  // barrier holds its CU slot); each keeps 8 x 2 float4 loads per lane in flight
+  a.out = out;
+  // Grid: <= 256 blocks (64 when the ranks share a GPU: a block waiting at a
+  // barrier holds its CU slot).  Segments under 256 float4s a block at that
+  // grid (LeNet-5's 62 K floats: 1,938 float4s a segment at N = 8) take
+  // 64-thread blocks of >= 64 float4s, so the grid stays wide instead of
+  // collapsing to a few 256-thread blocks that walk the segment serially; a
+  // thread keeps kAllReduceUnroll float4s of every rank in flight.
   const long long nb = sync_.lean ? 64 : 256;
   const long long per = (a.seg4 + nb - 1) / nb;
-  const long long per4 = std::max<long long>(512, (per + 511) / 512 * 512);
+  const int nt = per >= 512 ? 256 : 64;
+  const long long gran = nt * 2LL;  // one unrolled pass of the block
+  const long long per4 = std::max<long long>(nt, (per + gran - 1) / gran * gran);
   a.per4 = (int)per4;
   a.link_bytes = a.seg4 * 16;
   a.gather_only = gather_only ? 1 : 0;
   const int blocks = (int)std::max<long long>(1, (a.seg4 + per4 - 1) / per4);
-  xgmi::launch_allreduce(a, blocks, s);
+  xgmi::launch_allreduce(a, blocks, nt, s);
 }
 
-void XgmiComm::all_gather(const void*, void*, size_t, int, hipStream_t) {
-  throw std::runtime_error("XgmiComm: all_gather is not implemented (use SCHED_XGMI / all_reduce)");
+void XgmiComm::all_gather(const void* send, void* recv, size_t send_count, int dtype,
+                          hipStream_t s) {
+  if (dtype != ncclFloat32 || send_count % 4)
+    throw std::runtime_error("XgmiComm::all_gather: fp32, a multiple of 4 floats a rank");
+  float* mine = static_cast<float*>(recv) + (size_t)rank_ * send_count;
+  if (send != mine)  // the peers read this rank's slot of ITS recv buffer
+    HIP_CHECK(hipMemcpyAsync(mine, send, send_count * sizeof(float), hipMemcpyDeviceToDevice, s));
+  launch(recv, send_count * nranks_, true, s);
 }
 
-void XgmiComm::reduce_scatter(const void*, void*, size_t, int, int, hipStream_t) {
-  throw std::runtime_error("XgmiComm: reduce_scatter is not implemented (use SCHED_XGMI / all_reduce)");
+void XgmiComm::reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
+                              hipStream_t s) {
+  if (dtype != ncclFloat32 || op != ncclSum || recv_count % 4)
+    throw std::runtime_error("XgmiComm::reduce_scatter: fp32 sum, a multiple of 4 floats a rank");
+  // the send buffer is what the peers read (registered).  The reduced
+  // segment is a plain local store into recv: in place (recv = this rank's
+  // slot of send) is safe, since the peers read only the OTHER slots of it
+  launch(const_cast<void*>(send), recv_count * nranks_, false, s, nullptr,
+         static_cast<float*>(recv));
 }

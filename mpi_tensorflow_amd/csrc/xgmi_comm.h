@@ -68,14 +68,26 @@ class XgmiComm : public Collective {
   // rank r's counterpart of a local address inside a registered buffer
   void* peer_ptr(const void* local, int r) const;
   bool registered(const void* local, size_t bytes) const;
-  // emulated per-phase floor: ticks of the 100 MHz clock per KiB on one link
-  long long link_ticks_per_kb() const { return sync_.link_ticks_per_kb; }
+  // emulated per-phase floor: ticks of the 100 MHz clock per MiB on one link
+  long long link_ticks_per_mib() const { return sync_.link_ticks_per_mib; }
+  // failure injection (tests): phase-1 reductions leave out rank r (-1: off)
+  void inject_skip_peer(int r) {
+    if (r >= nranks_) throw std::runtime_error("XgmiComm: skip-peer rank out of range");
+    sync_.skip_peer = r < 0 ? -1 : r;
+  }
+  int skip_peer() const { return sync_.skip_peer; }
+  // emulation: writes `bytes` at src (device) into virtual rank r's stand-in of
+  // the registered local buffer (the exactness check gives every virtual rank
+  // its own contribution)
+  void emulate_fill_peer(uintptr_t local, int r, uintptr_t src, size_t bytes);
   unsigned error() const;  // sticky error bits (1: a barrier timed out); synchronizes
   void clear_error();
 
   // --- Collective: in-place fp32 sum all-reduce of a registered buffer ---
   void all_reduce(const void* send, void* recv, size_t count, int dtype, int op,
                   hipStream_t s) override;
+  // recv (send_count x N floats) registered; send is copied into this rank's
+  // slot first unless it is that slot
   void all_gather(const void* send, void* recv, size_t send_count, int dtype,
                   hipStream_t s) override;
   // in place, fp32: segment r (ceil(count / N) floats, in float4s) of every
@@ -89,6 +101,8 @@ class XgmiComm : public Collective {
   void all_reduce_sgd(float* grads, float* params, float* mom, size_t count, long long l2_end,
                       float l2, float momentum, float gscale, const float* lr, long long* step,
                       hipStream_t s);
+  // send (recv_count x N floats) registered and left unchanged unless recv is
+  // this rank's slot of it (in place: the reduced segment lands there)
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,
                       hipStream_t s) override;
 
@@ -102,7 +116,7 @@ class XgmiComm : public Collective {
   Reg& reg_for(uintptr_t local, size_t bytes);
   void* open_handle(int r, const std::string& handle);
   void launch(void* buf, size_t count, bool gather_only, hipStream_t s,
-              const xgmi::AllReduceArgs* sgd = nullptr);
+              const xgmi::AllReduceArgs* sgd = nullptr, float* out = nullptr);
 
   int nranks_, rank_;
   bool emulate_;

@@ -179,6 +179,11 @@ class EmulatedDeviceComm(DeviceComm):
         return EmulatedDeviceComm(*self._args)
 
 
+# failure injection (tests, bench.py --xgmi-inject-skip-peer): every xGMI
+# communicator created from here on leaves rank R out of its phase-1 sums
+INJECT_SKIP_PEER = int(os.environ.get("MTA_XGMI_INJECT_SKIP_PEER", "-1"))
+
+
 class XgmiDeviceComm(DeviceComm):
     """xGMI peer-to-peer communicator (csrc/xgmi_comm.h) of the ranks of one
     node.  Creation is collective over the gloo group: every rank makes its
@@ -202,6 +207,8 @@ class XgmiDeviceComm(DeviceComm):
             self.rank, self.size = 0, int(n)
             self.kind = f"xgmi-emulated(n={n},lat={lat}us,link={bw}GB/s)"
             self._di = None
+            self._check_bufs = {}
+            self.gate = "unchecked"
             return
         n = di.world
         err, h = None, None
@@ -231,6 +238,10 @@ class XgmiDeviceComm(DeviceComm):
         self._c.set_lean(bool(share))
         self.rank, self.size = di.rank, n
         self._di = di
+        self._check_bufs = {}
+        self.gate = "unchecked"
+        if 0 <= INJECT_SKIP_PEER < n:
+            self.inject_skip_peer(INJECT_SKIP_PEER)
 
     @classmethod
     def emulated(cls, nranks: int, lat_us: float = 2.0, link_gbps: float = 64.0,
@@ -278,6 +289,12 @@ class XgmiDeviceComm(DeviceComm):
         """Sticky device error bits (1: a peer barrier timed out); syncs."""
         return int(self._c.error())
 
+    def inject_skip_peer(self, r: int) -> None:
+        """Failure injection (tests): phase-1 reductions leave out rank r's
+        contribution (-1: off), on this rank.  Injected on every rank it gives
+        identical replicas with wrong sums (xgmi_exactness_check's target)."""
+        self._c.inject_skip_peer(int(r))
+
     def all_reduce_(self, t, stream=None):
         """In-place fp32 sum.  A tensor not registered yet is registered
         first (collective like the all-reduce itself; not inside a graph
@@ -297,21 +314,171 @@ class XgmiDeviceComm(DeviceComm):
         raise RuntimeError("the xGMI communicator has no second instance (no comm stream)")
 
 
+# exactness check of the xGMI collectives (xgmi_exactness_check): flat sizes
+# of the LeNet-5 class (62 K floats: 64-thread blocks) and of the MNIST /
+# ResNet class (2 M floats: 256-thread blocks, every block of the grid)
+XGMI_CHECK_COUNTS = (61_440, 1 << 21)
+
+
+def exact_pattern(rank: int, salt: int, count: int) -> torch.Tensor:
+    """Rank r's contribution to the exactness check: integers in [-125, 125]
+    stored as fp32, so any sum of <= 8 of them is exact in ANY order.  Two
+    ranks differ at every element ((r - r') * 17 is never 0 mod 251 for
+    |r - r'| <= 7), so a rank left out of a sum changes ~250 of 251 elements."""
+    i = torch.arange(count, dtype=torch.int64)
+    return (((i * 31 + rank * 17 + salt * 7) % 251) - 125).to(torch.float32)
+
+
+def exact_sum(n: int, salt: int, count: int) -> torch.Tensor:
+    tot = torch.zeros(count, dtype=torch.int64)
+    for r in range(n):
+        tot += exact_pattern(r, salt, count).to(torch.int64)
+    return tot.to(torch.float32)
+
+
+def xgmi_exactness_check(xc: "XgmiDeviceComm", ref: Optional[DeviceComm] = None,
+                         counts=XGMI_CHECK_COUNTS, rounds: int = 2) -> Optional[str]:
+    """Gate of the xGMI peer-to-peer collectives (collective over the ranks;
+    None = passed on EVERY rank, else the reason this rank saw, or that some
+    other rank failed).
+
+    Why: each rank reduces its own segment out of its peers' memory and every
+    rank then gathers that result (kernels/xgmi.hip), so a stale or torn peer
+    read in phase 1 corrupts the owner's segment IDENTICALLY on every rank -
+    replicas stay bit-identical while the sums are wrong, and a replica
+    checksum cannot see it.  Here every rank contributes rank-dependent small
+    integers stored as fp32, whose sum is exact in any order, so the
+    all-reduce, reduce-scatter and all-gather results must equal the exact
+    host sums bit for bit, over `rounds` rounds of fresh data (a read of the
+    previous round's bytes fails), at every buffer size class of
+    XGMI_CHECK_COUNTS.  `ref` (the RCCL / shared-memory communicator the ranks
+    also hold) must produce the same bits on the same data.  Emulated
+    communicators (one GPU) give each virtual rank its own contribution in its
+    stand-in buffer.  The reference's sync is a Gather to root + mean
+    (/root/reference/mpipy.py:121-137): exact up to the mean's rounding."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, me = xc.size, xc.rank
+    emu = xc.emulated_comm
+    world = 1 if emu else n
+    reason = None
+    bufs = xc._check_bufs
+    try:
+        for count in counts:
+            if count not in bufs:  # registered once, kept for the communicator's life
+                bufs[count] = (torch.zeros(count, device=dev), torch.zeros(count, device=dev))
+                xc.register(*bufs[count])
+            buf, gbuf = bufs[count]
+            rc = count // (4 * n) * 4  # reduce-scatter / all-gather floats a rank
+            for k in range(rounds):
+                salt = 2 * k + (count & 1)
+                buf.copy_(exact_pattern(me, salt, count))
+                if emu:
+                    for r in range(1, n):
+                        src = exact_pattern(r, salt, count).to(dev)
+                        xc._c.emulate_fill_peer(ptr(buf), r, ptr(src), 4 * count)
+                torch.cuda.synchronize(dev)
+                want = exact_sum(n, salt, count)
+                if emu:  # the stand-ins run no phase 1: segment r (> 0) is gathered as is
+                    seg = 4 * ((count // 4 + n - 1) // n)
+                    for r in range(1, n):
+                        want[r * seg:(r + 1) * seg] = exact_pattern(r, salt, count)[r * seg:(r + 1) * seg]
+                xc.all_reduce_(buf)
+                got = buf.cpu()
+                if not torch.equal(got, want):
+                    bad = int((got != want).sum())
+                    reason = (f"all_reduce of {count} floats (round {k}): {bad} elements differ "
+                              f"from the exact integer sum")
+                    break
+                if ref is not None and not isinstance(ref, XgmiDeviceComm):
+                    t = exact_pattern(me, salt, count).to(dev)
+                    ref.all_reduce_(t)
+                    torch.cuda.synchronize(dev)
+                    if not torch.equal(t.cpu(), got):
+                        reason = (f"all_reduce of {count} floats (round {k}): the {ref.kind} "
+                                  f"communicator's sum and the xGMI sum differ")
+                        break
+                # reduce-scatter (out of place: the send buffer stays as it is)
+                buf.copy_(exact_pattern(me, salt + 1, count))
+                if emu:
+                    for r in range(1, n):
+                        src = exact_pattern(r, salt + 1, count).to(dev)
+                        xc._c.emulate_fill_peer(ptr(buf), r, ptr(src), 4 * count)
+                out = torch.full((rc,), float("nan"), device=dev)
+                torch.cuda.synchronize(dev)
+                xc._c.reduce_scatter(ptr(buf), ptr(out), rc, NCCL_FLOAT32, NCCL_SUM, stream_handle())
+                want = exact_sum(n, salt + 1, count)[me * rc:(me + 1) * rc]
+                if not torch.equal(out.cpu(), want):
+                    reason = f"reduce_scatter of {rc} floats a rank (round {k}) is not exact"
+                    break
+                if not torch.equal(buf.cpu(), exact_pattern(me, salt + 1, count)):
+                    reason = f"reduce_scatter of {rc} floats a rank changed its send buffer"
+                    break
+                # all-gather: slot r of every rank's gbuf = rank r's rows
+                gbuf.fill_(float("nan"))
+                if emu:
+                    for r in range(1, n):
+                        src = torch.full((count,), float("nan"))
+                        src[r * rc:(r + 1) * rc] = exact_pattern(r, salt, rc)
+                        src = src.to(dev)
+                        xc._c.emulate_fill_peer(ptr(gbuf), r, ptr(src), 4 * count)
+                send = exact_pattern(me, salt, rc).to(dev)
+                torch.cuda.synchronize(dev)
+                xc._c.all_gather(ptr(send), ptr(gbuf), rc, NCCL_FLOAT32, stream_handle())
+                got = gbuf.cpu()[:n * rc]
+                want = torch.cat([exact_pattern(r, salt, rc) for r in range(n)])
+                if not torch.equal(got, want):
+                    reason = f"all_gather of {rc} floats a rank (round {k}) is not exact"
+                    break
+            if reason is not None:
+                break
+        torch.cuda.synchronize(dev)
+    except Exception as e:  # noqa: BLE001 - reported after the vote
+        reason = f"{type(e).__name__}: {e}"
+    try:
+        if xc.error():
+            reason = reason or "a peer barrier timed out"
+    except Exception as e:  # noqa: BLE001
+        reason = reason or f"{type(e).__name__}: {e}"
+    if not _all_ranks_ok(reason is None, world):
+        return reason or "the exactness check failed on another rank"
+    return None
+
+
 def make_xgmi_comm(di: DistInfo, device: torch.device, timeout_s: float = 30.0,
-                   quiet: bool = False) -> Optional["XgmiDeviceComm"]:
-    """The peer-to-peer communicator when every rank is on this node's GPUs,
-    else None (collective: every rank returns the same)."""
+                   quiet: bool = False, ref: Optional[DeviceComm] = None
+                   ) -> Optional["XgmiDeviceComm"]:
+    """The peer-to-peer communicator when every rank is on this node's GPUs
+    AND it passed the exactness check against `ref` (xgmi_exactness_check),
+    else None (collective: every rank returns the same; the reason is logged
+    and kept in `last_xgmi_status`)."""
+    global last_xgmi_status
+    last_xgmi_status = "n/a"
     if di.world <= 1 or device.type != "cuda":
         return None
     _, one_host = _auto_vote(di)
     if not one_host:
+        last_xgmi_status = "not set up: ranks on several hosts"
         return None
     try:
-        return XgmiDeviceComm(di, timeout_s)
+        xc = XgmiDeviceComm(di, timeout_s)
     except RuntimeError as e:
+        last_xgmi_status = f"not set up: {e}"
         if not quiet:
             print(f"[rank {di.rank}] {e}; no xGMI peer-to-peer schedule", flush=True)
         return None
+    why = xgmi_exactness_check(xc, ref)
+    if why is not None:
+        last_xgmi_status = f"dropped: exactness check failed ({why})"
+        if not quiet:
+            print(f"[rank {di.rank}] xGMI exactness check failed ({why}); "
+                  f"no xGMI peer-to-peer schedule", flush=True)
+        return None
+    last_xgmi_status = "passed"
+    xc.gate = "passed"
+    return xc
+
+
+last_xgmi_status = "n/a"  # what the last make_xgmi_comm decided (bench / trainer report it)
 
 
 DEFAULT_SHM_CAPACITY = 64 << 20  # bytes per rank and collective
@@ -592,7 +759,12 @@ def make_comm(di: DistInfo, device: torch.device, prefer: str = "auto",
     if device.type == "cuda" and prefer == "shm":
         return ShmDeviceComm(di, shm_capacity, timeout_s)
     if device.type == "cuda" and prefer == "xgmi":
-        return XgmiDeviceComm(di, min(timeout_s, 60.0))
+        xc = XgmiDeviceComm(di, min(timeout_s, 60.0))
+        why = xgmi_exactness_check(xc)  # collective: every rank raises or none does
+        if why is not None:
+            raise RuntimeError(f"xGMI communicator failed its exactness check ({why})")
+        xc.gate = "passed"
+        return xc
     if device.type == "cuda" and prefer == "auto":
         share, one_host = _auto_vote(di)
         if share:

@@ -191,8 +191,9 @@ class SegmentedStep:
         with torch.cuda.stream(self.comm_stream):
             g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
             collective()
+            nodes = self.node_count(self.comm_stream)  # what this bucket's graph moves
             g.capture_end()
-        self.items.append(("m", g, DevEvent()))
+        self.items.append(("m", g, DevEvent(), nodes))
         if closed:
             self._open()
 
@@ -205,6 +206,12 @@ class SegmentedStep:
         with warnings.catch_warnings():  # an empty last segment is ended and dropped
             warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
             self._close(force=True)
+
+    def collective_nodes(self) -> List[int]:
+        """Nodes captured in each overlapped bucket's collective graph, in
+        order (0 would be a collective that captured nothing: at world 1 the
+        communicator returns at once; at N > 1 every one must move bytes)."""
+        return [it[3] for it in self.items if it[0] == "m"]
 
     def replay(self) -> None:
         cs = torch.cuda.current_stream()

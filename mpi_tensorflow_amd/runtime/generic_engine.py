@@ -357,6 +357,7 @@ class GenericEngine:
         torch.cuda.synchronize(self.device)
         cap = torch.cuda.Stream(device=self.device)
         cap.wait_stream(torch.cuda.current_stream())
+        host = self._host_state()
         seg = SegmentedStep(self.bucketer.stream, torch.cuda.graph_pool_handle(),
                             lambda st: self._C.capture_node_count(stream_handle(st)))
         self.bucketer.segment = seg
@@ -380,13 +381,9 @@ class GenericEngine:
                 self.bucketer.segment = None
                 if gc_was_on:
                     gc.enable()
-        if err is not None:  # keep training eagerly rather than fail the run
-            print(f"[rank {self.rank}] segmented hipGraph capture failed ({err}); using "
-                  "eager launches", flush=True)
-            self.use_graph = False
-            torch.cuda.synchronize(self.device)
-            return None
         torch.cuda.current_stream().wait_stream(cap)
+        if not self._capture_voted(err, host, "segmented hipGraph capture"):
+            return None
         self._graphs[n] = seg
         self._graph_loss[n] = self._loss_t
         return seg
@@ -397,21 +394,50 @@ class GenericEngine:
         g = self._graphs.get(n)
         if g is None:
             g = torch.cuda.CUDAGraph()
+            host = self._host_state()
+            err = None
             try:
                 with torch.cuda.graph(g):
                     for _ in range(n):
                         self._step_gpu()
-            except RuntimeError as e:  # keep training eagerly rather than fail the run
-                print(f"[rank {self.rank}] hipGraph capture failed ({e}); using eager launches",
-                      flush=True)
-                self.use_graph = False
-                torch.cuda.synchronize(self.device)
+            except RuntimeError as e:
+                err = e
+            if not self._capture_voted(err, host, "hipGraph capture"):
                 return None
             self._graphs[n] = g
             # the loss tensor of the LAST step in this graph: its storage
             # belongs to the graph and is rewritten by every replay
             self._graph_loss[n] = self._loss_t
         return g
+
+    def collective_graph_nodes(self):
+        """Per overlapped (non-final) bucket of the longest captured segmented
+        graph: the nodes its collective graph captured (None without one)."""
+        segs = [v for k, v in sorted(self._graphs.items()) if isinstance(v, SegmentedStep)]
+        return segs[-1].collective_nodes() if segs else None
+
+    def _host_state(self):
+        """Host-side state a captured step changes (the bucketer resets its own
+        per-step state in begin()): restored when a capture is abandoned."""
+        return (getattr(self, "_loss_t", None), self._wfresh, getattr(self, "_lr_fresh", False))
+
+    def _capture_voted(self, err, host, what: str) -> bool:
+        """Collective: a capture is kept only if it succeeded on EVERY rank
+        (a rank training eagerly next to captured peers would issue its
+        collectives on another schedule); otherwise every rank restores the
+        host state the aborted capture changed and trains eagerly."""
+        ok = err is None
+        if self.world > 1 and self.comm is not None:
+            from ..parallel import dist as D
+            ok = D.allreduce_max_host(0.0 if ok else 1.0) == 0.0
+        if ok:
+            return True
+        why = err if err is not None else "it failed on another rank"
+        print(f"[rank {self.rank}] {what} failed ({why}); using eager launches", flush=True)
+        self._loss_t, self._wfresh, self._lr_fresh = host
+        self.use_graph = False
+        torch.cuda.synchronize(self.device)
+        return False
 
     def _warmup(self, k: int) -> int:
         """Eager warm-up on a side stream before the first capture (torch's

@@ -46,6 +46,8 @@ from ..utils.schedule import learning_rate
 # streams at once; it is opt-in (--sync-schedule split) and never picked by
 # auto until it has run on a real multi-GPU node.
 TUNE_REPLAYS = 2
+# _xgmi_step_matches: max |update(xGMI) - update(serial)| / max |update(serial)|
+XGMI_STEP_RTOL = 1e-4
 
 
 class MnistEngineBase:
@@ -331,6 +333,8 @@ class NativeMnistEngine(MnistEngineBase):
         # (auto always has >= 2 candidates: buckets and serial)
         self._tuned = not (self.grad_sync and cfg.sync_schedule == "auto" and self.use_graph)
         self.tune_log: Dict[str, float] = {}
+        self.tune_reject: Dict[str, str] = {}  # candidate -> why it was dropped
+        self.xgmi_step_check: Dict[str, float] = {}  # xGMI schedule -> measured update rel. diff
         self.tune_steps_run = 0
         self._eval_ws = None
         if self.grad_sync:  # connection setup of every collective used, outside any capture
@@ -486,7 +490,15 @@ class NativeMnistEngine(MnistEngineBase):
         self.exe.refresh_shadows(stream_handle())
         snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
         cands = self._tune_candidates()
+        xgmi_scheds = (E.SCHED_XGMI, E.SCHED_XGMI_STEP, E.SCHED_XGMI_FAC)
+        xgmi_dead = False
         for sched, name in cands:
+            uses_xgmi = sched in xgmi_scheds or self.comm_is_xgmi
+            if uses_xgmi and xgmi_dead:
+                # a timed-out barrier leaves the communicator's sticky error set and
+                # its later barriers no longer wait: nothing over it may run again
+                self.tune_log[name] = None
+                continue
             self._set_schedule(sched)
             g = self._graph(G, sticky=(sched == cands[-1][0] if self.comm_is_xgmi
                                        else sched == E.SCHED_BUCKETS))
@@ -500,10 +512,23 @@ class NativeMnistEngine(MnistEngineBase):
                 continue
             g.replay()
             torch.cuda.synchronize(self.device)
-            if (sched in (E.SCHED_XGMI, E.SCHED_XGMI_STEP, E.SCHED_XGMI_FAC)
-                    and not self._xgmi_healthy()):
-                self.tune_log[name] = None  # a peer barrier timed out: never pick it
-                continue
+            if uses_xgmi:
+                why = self._xgmi_healthy()
+                if why is None and sched in xgmi_scheds:
+                    why = self._xgmi_step_matches(sched, snap)
+                if why is not None:
+                    self.tune_log[name] = None  # never pick it
+                    self.tune_reject[name] = why
+                    if self.rank == 0:
+                        print(f"[rank 0] sync schedule {name} rejected: {why}", flush=True)
+                    if "timed out" in why:
+                        xgmi_dead = True
+                        if self.comm_is_xgmi:
+                            raise RuntimeError(f"xGMI communicator failed during the sync-schedule "
+                                               f"autotune ({why}); there is no other communicator")
+                        # RCCL trains on; the dead xGMI comm leaves the health votes
+                        self.xcomm = None
+                    continue
             t0 = torch.cuda.Event(enable_timing=True)
             t1 = torch.cuda.Event(enable_timing=True)
             t0.record()
@@ -516,8 +541,10 @@ class NativeMnistEngine(MnistEngineBase):
             self.tune_log[name] = round(us, 2)
             if best is None or us < best[0]:
                 best = (us, sched)
-        self._set_schedule(best[1] if best is not None else cands[-1][0] if self.comm_is_xgmi
-                           else E.SCHED_BUCKETS)
+        if best is None and self.comm_is_xgmi:
+            raise RuntimeError("no sync schedule over the xGMI communicator passed its checks: "
+                               + "; ".join(f"{k}: {v}" for k, v in self.tune_reject.items()))
+        self._set_schedule(best[1] if best is not None else E.SCHED_BUCKETS)
         self.exe.join(stream_handle())
         self.params.copy_(snap[0])
         self.mom.copy_(snap[1])
@@ -527,21 +554,68 @@ class NativeMnistEngine(MnistEngineBase):
         self.tune_steps_run = steps
         return steps
 
-    def _xgmi_healthy(self) -> bool:
-        """Collective: no rank's xGMI barrier timed out (the device kernels
-        never hang: a missing peer sets a sticky error bit instead)."""
+    def _xgmi_healthy(self) -> Optional[str]:
+        """Collective: None when no rank's xGMI barrier timed out (the device
+        kernels never hang: a missing peer sets a sticky error bit instead)
+        and the replicas agree bit for bit after the trial steps, else why."""
         from ..parallel import dist as D
         from ..parallel.sync import replicas_identical
         bad = self.xcomm.error() if self.xcomm is not None else 0
         if D.allreduce_max_host(float(bad)) != 0.0:
-            return False
+            return "a peer barrier timed out"
         if self.xcomm is None or self.xcomm.emulated_comm:
-            return True
+            return None
         # replicas must agree bit for bit after the trial steps (a lost or torn
         # peer read would show here): gather the sharded momentum and compare
         self.sync_optimizer_state()
         torch.cuda.synchronize(self.device)
-        return replicas_identical(self.params) and replicas_identical(self.mom)
+        if not (replicas_identical(self.params) and replicas_identical(self.mom)):
+            return "the replicas differ after the trial steps"
+        return None
+
+    def _xgmi_step_matches(self, sched: int, snap) -> Optional[str]:
+        """Collective: one eager step of the xGMI schedule `sched` against one
+        eager step of the serial schedule over the other communicator (RCCL;
+        the xGMI comm's exactness-checked all-reduce when it is the only one),
+        both from the state `snap`.  Identical replicas cannot reveal a
+        wrong-but-consistent reduction (every rank gathers the same wrong
+        segments), this can: the two parameter updates must agree to
+        XGMI_STEP_RTOL of the largest update (rank-order vs RCCL summation is
+        ~1e-7; a rank left out of the sum is ~1/N).  None = match, else why.
+        The state is restored to `snap` afterwards.  Emulated communicators
+        are not compared (their numerics are not those of N ranks)."""
+        from ..parallel import dist as D
+        if self.xcomm is None or self.xcomm.emulated_comm:
+            return None
+        E = self._C.MnistExecutor
+        s = stream_handle()
+        outs = []
+        for sc in (sched, E.SCHED_SERIAL):
+            self._set_schedule(sc)
+            self.params.copy_(snap[0])
+            self.mom.copy_(snap[1])
+            self.step_dev.copy_(snap[2])
+            self.exe.refresh_shadows(s)
+            self._launch_one()
+            self.exe.join(s)
+            torch.cuda.synchronize(self.device)
+            outs.append(self.params.clone())
+        self._set_schedule(sched)
+        self.params.copy_(snap[0])
+        self.mom.copy_(snap[1])
+        self.step_dev.copy_(snap[2])
+        self.exe.refresh_shadows(s)
+        torch.cuda.synchronize(self.device)
+        dx, ds = outs[0] - snap[0], outs[1] - snap[0]
+        ref = float(ds.abs().max())
+        err = float((dx - ds).abs().max())
+        bad = not (err <= XGMI_STEP_RTOL * ref) or not math.isfinite(err)
+        worst = D.allreduce_max_host(err / max(ref, 1e-30))
+        if D.allreduce_max_host(1.0 if bad else 0.0) != 0.0:
+            return (f"one trial step differs from the serial schedule's by {worst:.2e} of the "
+                    f"largest update (bound {XGMI_STEP_RTOL:g})")
+        self.xgmi_step_check[self.sync_schedule] = worst
+        return None
 
     def prewarm_train(self, ms: float) -> float:
         """Untimed, side-effect-free training replays for ~`ms` of wall time

@@ -28,7 +28,7 @@ import torch
 
 from .. import config as C
 from ..parallel import dist as D
-from ..parallel.comm import make_comm
+from ..parallel.setup import check_health, comm_capacity_bytes, setup_comms  # noqa: F401
 from ..parallel.watchdog import make_watchdog, run_in_chunks
 from ..parallel.sync import average_params, average_params_root_only, replicas_identical
 from ..utils import checkpoint as ckpt_mod
@@ -39,25 +39,6 @@ from ..ops import functional as Fn
 from ..utils.data import batch_offset
 from ..utils.faults import maybe_fail
 from ..utils.profiling import SegmentTimer
-
-
-def comm_capacity_bytes(cfg: C.TrainConfig) -> int:
-    """Largest per-rank contribution of one collective of this model's step,
-    rounded up to 1 MiB: the capacity a shared-memory communicator needs.
-    That is the whole flat fp32 gradient / parameter buffer, or for the MNIST
-    factor schedule (csrc/mnist_executor.cpp train_step_factors) one rank's
-    FC-factor slice a2 / dh / hd / dlog, B x (3136 + 2 x 512 + 10) floats,
-    when that is larger (B > ~400)."""
-    if cfg.model == "mnist_cnn":
-        from ..models import mnist_cnn as M
-
-        total = M.layout().total
-        total = max(total, cfg.batch_size * (M.FC1_IN + 2 * M.FC1_OUT + 10))
-    else:
-        from ..models.generic import make_model
-
-        total = make_model(cfg.model).layout.total
-    return ((4 * total + (1 << 20) - 1) >> 20) << 20
 
 
 @dataclasses.dataclass
@@ -80,6 +61,7 @@ class RunSummary:
     comm: str
     synthetic: bool
     sync_schedule: str = "n/a"
+    xgmi_gate: str = "n/a"
 
     def as_dict(self) -> Dict:
         return dataclasses.asdict(self)
@@ -100,11 +82,10 @@ class Trainer:
         with self.watchdog.guard("start-up (data, communicator, engine)"):
             self._prepare_data()
             maybe_fail("before_comm", self.rank)
-            self.comm = None
-            if self.world > 1:
-                self.comm = make_comm(self.di, self.device, cfg.comm,
-                                      shm_capacity=comm_capacity_bytes(cfg),
-                                      timeout_s=cfg.collective_timeout_s)
+            # the same communicator set-up as bench.py (parallel/setup.py): the
+            # device comm, plus on one node the exactness-gated xGMI candidate
+            self.comms = setup_comms(self.di, self.device, cfg, no_xgmi=cfg.no_xgmi)
+            self.comm = self.comms.comm
             self.watchdog.add(self.comm)
             maybe_fail("after_comm", self.rank)
             self.engine = self._make_engine()
@@ -154,7 +135,7 @@ class Trainer:
             from .mnist_engine import make_engine
 
             return make_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
-                               self.comm)
+                               self.comm, xcomm=self.comms.xcomm)
         from .generic_engine import make_image_engine
 
         return make_image_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
@@ -233,6 +214,7 @@ class Trainer:
             with self.watchdog.guard("sync-schedule autotune"):
                 eng.tune_schedule()
                 self._sync()
+        self._health("after the sync-schedule autotune")
         maybe_fail("before_train", self.rank)
         steps = self.total_steps()
         s = eng.step
@@ -258,6 +240,7 @@ class Trainer:
             last = s - 1
             if not self._event(last):
                 continue
+            self._health(f"step {last}")
             ev = cfg.effective_eval_every()
             if ev and last % ev == 0:
                 t1 = time.perf_counter()
@@ -285,6 +268,7 @@ class Trainer:
                     self.check_replicas(last, averaged=True)
             if cfg.ckpt and cfg.ckpt_every and last % cfg.ckpt_every == 0:
                 self.save_checkpoint(cfg.ckpt)
+        self._health(f"end of training (step {s - 1})")
         if cfg.check_replicas:
             self.check_replicas(s - 1)
         t1 = time.perf_counter()
@@ -304,14 +288,22 @@ class Trainer:
             final_loss=eng.loss_value(), final_lr=eng.lr(max(0, s - 1)),
             device_step_ms=timer.step_ms(), engine=eng.kind,
             comm=getattr(self.comm, "kind", "none"), synthetic=self.shard.synthetic,
-            sync_schedule=self.sync_schedule())
+            sync_schedule=self.sync_schedule(), xgmi_gate=self.comms.xgmi_status)
         self.metrics.write(final=True, **summary.as_dict())
         if cfg.ckpt:
             self.save_checkpoint(cfg.ckpt)
         self.metrics.close()
         return summary
 
+    def _health(self, where: str) -> None:
+        """Every rank stops when any rank's xGMI barrier timed out (the later
+        barriers of that communicator stop waiting: training on would read the
+        peers' buffers unsynchronised); a vote, so all ranks raise together."""
+        if self.world > 1:
+            check_health(where, self.comm, self.engine)
+
     def save_checkpoint(self, path: str) -> None:
+        self._health("before a checkpoint")
         self.engine.sync_optimizer_state()  # sharded FC momentum -> whole buffer
         if self.rank == 0:
             ckpt_mod.save(path, self.engine.layout, self.engine.params, self.engine.mom,

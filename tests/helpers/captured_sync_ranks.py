@@ -182,6 +182,55 @@ def scenario_xgmi(di, dtype):
     return f"all_reduce+gather ok; schedules {','.join(scheds)}, auto->{picked[-1]}"
 
 
+def scenario_xgmi_gate(di):
+    """VERDICT r5 #1: the exactness gate and the trial-step compare."""
+    from mpi_tensorflow_amd.parallel.comm import (XgmiDeviceComm, exact_pattern, exact_sum,
+                                                  xgmi_exactness_check)
+
+    cfg = C.TrainConfig(graph=True, graph_steps=G).validate()
+    shm = ShmDeviceComm(di, comm_capacity_bytes(cfg), timeout_s=60.0)
+    good = XgmiDeviceComm(di, timeout_s=20.0)
+    assert xgmi_exactness_check(good, shm) is None, "a healthy communicator failed the gate"
+    # the fault on both ranks: identical on both ranks, and wrong
+    bad = XgmiDeviceComm(di, timeout_s=20.0)
+    bad.inject_skip_peer(1)
+    t = exact_pattern(di.rank, 9, 1 << 20).cuda()
+    bad.register(t)
+    bad.all_reduce_(t)
+    torch.cuda.synchronize()
+    assert replicas_identical(t), "the skip-peer fault should leave the replicas identical"
+    assert not torch.equal(t.cpu(), exact_sum(di.world, 9, 1 << 20)), "the fault did not bite"
+    why = xgmi_exactness_check(bad, shm)
+    assert why is not None and "exact integer sum" in why, why
+    assert bad.error() == 0
+    # the MNIST auto-tune: xGMI candidates next to the shm schedules
+    picks = {}
+    for fault in (False, True):
+        x, y = NS._shard(di.rank, di.world, cfg.seed)
+        xc = XgmiDeviceComm(di, timeout_s=20.0)
+        assert xgmi_exactness_check(xc, shm) is None
+        comm = ShmDeviceComm(di, comm_capacity_bytes(cfg), timeout_s=60.0)
+        eng = NativeMnistEngine(cfg, x, y, torch.device("cuda"), di.rank, di.world, comm, xcomm=xc)
+        if fault:
+            xc.inject_skip_peer(1)
+        p0 = eng.params.clone()
+        eng.tune_schedule()
+        assert torch.equal(eng.params, p0), "tune changed the state"
+        xg = [k for k in eng.tune_log if k.startswith("xgmi")]
+        assert xg, eng.tune_log
+        if fault:
+            assert all(eng.tune_log[k] is None for k in xg), eng.tune_log
+            assert all("trial step differs" in eng.tune_reject[k] for k in xg), eng.tune_reject
+            assert not eng.sync_schedule.startswith("xgmi")
+        else:
+            assert all(eng.tune_log[k] is not None for k in xg), (eng.tune_log, eng.tune_reject)
+            assert eng.xgmi_step_check and max(eng.xgmi_step_check.values()) < 1e-4
+        picks[fault] = eng.sync_schedule
+        eng.train(STEPS)
+        finish(eng)
+    return f"gate ok; picks {picks}"
+
+
 def scenario_param_avg(di):
     outs = {}
     for kind in ("shm",):
@@ -299,6 +348,8 @@ def main():
         msg = scenario_mnist(di, arg or "fp32")
     elif scen == "xgmi":
         msg = scenario_xgmi(di, arg or "fp32")
+    elif scen == "xgmi_gate":
+        msg = scenario_xgmi_gate(di)
     elif scen == "param_avg":
         msg = scenario_param_avg(di)
     elif scen == "generic":

@@ -75,6 +75,10 @@ def test_bench_two_ranks_shared_gpu(cuda_dev, model, dtype, extra):
         tune = c["sync_tune_us_per_step"]
         assert tune and None not in tune.values() and len(set(tune.values())) >= 2, tune
         assert c["sync_schedule"].startswith("buckets(") and c["sync_schedule"][8:-1] in tune
+        # every overlapped (non-final) bucket's collective graph moved bytes
+        nodes = c["collective_graph_nodes"]
+        if c["sync_schedule"] != "buckets(one)":
+            assert nodes and all(k > 0 for k in nodes), nodes
 
 
 @pytest.mark.parametrize("model,dtype", [("mnist_cnn", "fp32"), ("mnist_cnn", "bf16"),

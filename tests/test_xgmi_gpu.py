@@ -99,3 +99,61 @@ def test_xgmi_missing_peer_times_out_and_fails_fast(cuda_dev):
     later = time.perf_counter() - t0
     print(f"xgmi dead peer: first collective {first * 1e3:.0f} ms, next five {later * 1e3:.1f} ms")
     assert first >= 0.25 and later < 0.25
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_xgmi_exactness_gate_emulated_rejects_a_skipped_peer(cuda_dev, n):
+    """The gate (parallel/comm.py xgmi_exactness_check): integer data whose
+    sum is exact in any order; the all-reduce, reduce-scatter and all-gather
+    (64- and 256-thread grids) must match the exact sums bit for bit.  With
+    the skip-peer fault (phase-1 sums leave one rank out, which on real ranks
+    gives identical replicas with wrong sums) the gate must reject."""
+    from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm, xgmi_exactness_check
+
+    good = XgmiDeviceComm.emulated(n, lat_us=0.0, link_gbps=0.0)
+    assert xgmi_exactness_check(good) is None
+    bad = XgmiDeviceComm.emulated(n, lat_us=0.0, link_gbps=0.0)
+    bad.inject_skip_peer(n - 1)
+    why = xgmi_exactness_check(bad)
+    assert why is not None and "exact integer sum" in why, why
+    assert good.error() == 0 and bad.error() == 0  # wrong sums, no timeout
+
+
+@pytest.mark.gpu
+def test_xgmi_emulated_link_rate_is_not_rounded_away(cuda_dev):
+    """the emulated link floor at 150 GB/s was rounded to whole
+    ticks a KiB (~102 GB/s); a MiB keeps the rate within 0.1 %."""
+    from mpi_tensorflow_amd.parallel.comm import XgmiDeviceComm
+
+    for gbps in (64.0, 150.0, 400.0):
+        c = XgmiDeviceComm.emulated(8, 1.0, gbps)
+        t = c.native_handle.link_ticks_per_mib
+        assert abs((1 << 20) / (t / 1e8) / 1e9 - gbps) / gbps < 2e-3, (gbps, t)
+
+
+@pytest.mark.gpu
+def test_bench_emulated_xgmi_with_skipped_peer_fails_the_gate(cuda_dev):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--xgmi-emulate", "0,0,8",
+                        "--xgmi-inject-skip-peer", "5", "--steps", "2", "--warmup", "1",
+                        "--no-eval", "--prewarm-ms", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 5, r.stdout[-2000:] + r.stderr[-3000:]
+    assert "exactness check" in r.stderr
+
+
+@pytest.mark.gpu
+def test_xgmi_two_ranks_gate_catches_identical_but_wrong_sums():
+    """2 ranks over IPC: the skip-peer fault on both ranks gives bit-identical
+    results on the two ranks that are NOT the sum - what a replica checksum
+    cannot see.  The exactness gate rejects it, the MNIST auto-tune's trial
+    step compare (one xGMI step vs one serial step over the shared-memory
+    communicator) rejects every xGMI schedule of a faulty communicator that
+    passed the gate before the fault, and accepts them without the fault."""
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), HELPER, "xgmi_gate"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert "CAPTURED_SYNC_OK xgmi_gate" in r.stdout, r.stdout[-2000:]
