@@ -736,7 +736,8 @@ PYBIND11_MODULE(_C, m) {
 #define RWL(f) .def_readwrite(#f, &LenetPtrs::f)
           RWL(train_x) RWL(train_y) RWL(n_local) RWL(batch) RWL(params) RWL(grads) RWL(mom)
               RWL(total) RWL(off) RWL(step) RWL(lr) RWL(correct) RWL(acts) RWL(deltas) RWL(convp)
-                  RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum) RWL(grad_bf16) RWL(gb16);
+                  RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum) RWL(grad_bf16) RWL(gb16)
+                  RWL(xrecv);
 #undef RWL
   m.def("lenet_buffer_floats", [](int batch) {
     return py::make_tuple(lenet::acts_floats(batch), lenet::deltas_floats(batch),

@@ -632,6 +632,94 @@ __device__ __forceinline__ void apply_one(float* w, float* g, float* m, int i, f
   }
 }
 
+// FC tile ft (0 .. FT_ALL - 1) of the update launch: geometry and the lane's
+// weight / bias indices
+struct FcTile {
+  int nin, nout, aoff, doff, woff, boff, i0, j0, ia, jb;
+  bool bias_tile;
+};
+__device__ __forceinline__ FcTile fc_tile(int ft, const Offsets& o, int lane) {
+  int layer, t;
+  if (ft < FT_F1) {
+    layer = 0;
+    t = ft;
+  } else if (ft < FT_F1 + FT_F2) {
+    layer = 1;
+    t = ft - FT_F1;
+  } else {
+    layer = 2;
+    t = ft - FT_F1 - FT_F2;
+  }
+  FcTile f;
+  f.nin = layer == 0 ? F0 : (layer == 1 ? F1 : F2);
+  f.nout = layer == 0 ? F1 : (layer == 1 ? F2 : F3);
+  f.aoff = layer == 0 ? 0 : (layer == 1 ? F0 : F0 + F1);
+  f.doff = layer == 0 ? 0 : (layer == 1 ? F1 : F1 + F2);
+  f.woff = layer == 0 ? o.f1w : (layer == 1 ? o.f2w : o.f3w);
+  f.boff = layer == 0 ? o.f1b : (layer == 1 ? o.f2b : o.f3b);
+  const int ntj = (f.nout + 31) / 32;
+  f.i0 = (t / ntj) * 32;
+  f.j0 = (t % ntj) * 32;
+  f.ia = min(f.i0 + (lane & 31), f.nin - 1);
+  f.jb = min(f.j0 + (lane & 31), f.nout - 1);
+  f.bias_tile = f.i0 == 0;
+  return f;
+}
+
+// g[i][j] = sum_n act[n][i] delta[n][j] of the tile (acc) and, on the row-0
+// tiles, the bias column sum (bs, both lane halves)
+__device__ __forceinline__ void fc_tile_product(const float* __restrict__ acts,
+                                                const float* __restrict__ deltas, int batch,
+                                                const FcTile& f, int lane, f32x16& acc, float& bs) {
+  const int kh = lane >> 5;
+  acc = zero16();
+  bs = 0.f;
+  for (int n0 = 0; n0 < batch; n0 += 64) {
+    float av[32], dv[32];
+#pragma unroll
+    for (int st = 0; st < 32; ++st) {
+      const int n = min(n0 + 2 * st + kh, batch - 1);
+      av[st] = acts[(size_t)n * ACT_STRIDE + f.aoff + f.ia];
+      dv[st] = deltas[(size_t)n * DELTA_STRIDE + f.doff + f.jb];
+    }
+    // every load of the chunk issued before the first product
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int st = 0; st < 32; ++st) {
+      const bool ok = n0 + 2 * st + kh < batch;
+      const float d = ok ? dv[st] : 0.f;
+      acc = mfma32x32x2(av[st], d, acc);
+      bs += d;
+    }
+  }
+  bs += __shfl_xor(bs, 32, 64);
+}
+
+// conv slot e (0 .. CONV_N - 1) -> flat parameter index, or -1 (padding)
+__device__ __forceinline__ int conv_dst(int e, const Offsets& o) {
+  if (e >= CONV_N) return -1;
+  if (e < W1N) return o.c1w + e;
+  if (e < W1N + C1) return o.c1b + (e - W1N);
+  if (e < W1N + 8) return -1;
+  if (e < W1N + 8 + W2N) return o.c2w + (e - W1N - 8);
+  return o.c2b + (e - W1N - 8 - W2N);
+}
+
+// the sum of the per-image partials of conv slot e, in image order
+__device__ __forceinline__ float conv_partial_sum(const float* __restrict__ convp, int batch,
+                                                  int e) {
+  float s = 0.f;
+  for (int n0 = 0; n0 < batch; n0 += 64) {  // 64 image partials in flight, summed in order
+    float v[64];
+#pragma unroll
+    for (int u = 0; u < 64; ++u)
+      v[u] = n0 + u < batch ? convp[(size_t)(n0 + u) * CONVP_STRIDE + e] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 64; ++u) s += v[u];
+  }
+  return s;
+}
+
 template <bool APPLY>
 __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ acts,
                                                      const float* __restrict__ deltas,
@@ -647,70 +735,32 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
   if (blk < UB_FC) {
     const int lane = tid & 63, ft = blk * 4 + (tid >> 6);
     if (ft >= FT_ALL) return;
-    int layer, t;
-    if (ft < FT_F1) {
-      layer = 0;
-      t = ft;
-    } else if (ft < FT_F1 + FT_F2) {
-      layer = 1;
-      t = ft - FT_F1;
-    } else {
-      layer = 2;
-      t = ft - FT_F1 - FT_F2;
-    }
-    const int nin = layer == 0 ? F0 : (layer == 1 ? F1 : F2);
-    const int nout = layer == 0 ? F1 : (layer == 1 ? F2 : F3);
-    const int aoff = layer == 0 ? 0 : (layer == 1 ? F0 : F0 + F1);
-    const int doff = layer == 0 ? 0 : (layer == 1 ? F1 : F1 + F2);
-    const int woff = layer == 0 ? o.f1w : (layer == 1 ? o.f2w : o.f3w);
-    const int boff = layer == 0 ? o.f1b : (layer == 1 ? o.f2b : o.f3b);
-    const int ntj = (nout + 31) / 32;
-    const int i0 = (t / ntj) * 32, j0 = (t % ntj) * 32;
+    const FcTile f = fc_tile(ft, o, lane);
     const int l31 = lane & 31, kh = lane >> 5;
-    const int ia = min(i0 + l31, nin - 1), jb = min(j0 + l31, nout - 1);
-    const bool bias_tile = i0 == 0;
     // the SGD operands of this lane's 16 weights (+ its bias) first: they are
     // independent of the gradient and arrive under the products
     float wv[16], mv[16], bwv = 0.f, bmv = 0.f;
     if (APPLY) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int wi = woff + min(i0 + mfma32_row(q, lane), nin - 1) * nout + jb;
+        const int wi = f.woff + min(f.i0 + mfma32_row(q, lane), f.nin - 1) * f.nout + f.jb;
         wv[q] = w[wi];
         mv[q] = m[wi];
       }
-      if (bias_tile) {
-        bwv = w[boff + jb];
-        bmv = m[boff + jb];
+      if (f.bias_tile) {
+        bwv = w[f.boff + f.jb];
+        bmv = m[f.boff + f.jb];
       }
     }
-    f32x16 acc = zero16();
-    float bs = 0.f;
-    for (int n0 = 0; n0 < batch; n0 += 64) {
-      float av[32], dv[32];
-#pragma unroll
-      for (int st = 0; st < 32; ++st) {
-        const int n = min(n0 + 2 * st + kh, batch - 1);
-        av[st] = acts[(size_t)n * ACT_STRIDE + aoff + ia];
-        dv[st] = deltas[(size_t)n * DELTA_STRIDE + doff + jb];
-      }
-      // every load of the chunk issued before the first product
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int st = 0; st < 32; ++st) {
-        const bool ok = n0 + 2 * st + kh < batch;
-        const float d = ok ? dv[st] : 0.f;
-        acc = mfma32x32x2(av[st], d, acc);
-        bs += d;
-      }
-    }
-    bs += __shfl_xor(bs, 32, 64);
-    if (j0 + l31 < nout) {
+    f32x16 acc;
+    float bs;
+    fc_tile_product(acts, deltas, batch, f, lane, acc, bs);
+    if (f.j0 + l31 < f.nout) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const int i = i0 + mfma32_row(q, lane);
-        if (i >= nin) continue;
-        const int wi = woff + i * nout + j0 + l31;
+        const int i = f.i0 + mfma32_row(q, lane);
+        if (i >= f.nin) continue;
+        const int wi = f.woff + i * f.nout + f.j0 + l31;
         if (APPLY) {
           const float mn = mu * mv[q] + acc[q];
           m[wi] = mn;
@@ -719,13 +769,13 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
           g[wi] = acc[q];
         }
       }
-      if (bias_tile && kh == 0) {
+      if (f.bias_tile && kh == 0) {
         if (APPLY) {
           const float mn = mu * bmv + bs;
-          m[boff + j0 + l31] = mn;
-          w[boff + j0 + l31] = bwv - lr * mn;
+          m[f.boff + f.j0 + l31] = mn;
+          w[f.boff + f.j0 + l31] = bwv - lr * mn;
         } else {
-          g[boff + j0 + l31] = bs;
+          g[f.boff + f.j0 + l31] = bs;
         }
       }
     }
@@ -733,27 +783,14 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
   }
   // conv parameters: sum of the per-image partials, in image order
   const int e = (blk - UB_FC) * 256 + tid;
-  if (e >= CONV_N) return;
-  int dst;
-  if (e < W1N) dst = o.c1w + e;
-  else if (e < W1N + C1) dst = o.c1b + (e - W1N);
-  else if (e < W1N + 8) return;
-  else if (e < W1N + 8 + W2N) dst = o.c2w + (e - W1N - 8);
-  else dst = o.c2b + (e - W1N - 8 - W2N);
+  const int dst = conv_dst(e, o);
+  if (dst < 0) return;
   float wd = 0.f, md = 0.f;
   if (APPLY) {  // SGD operands first (independent of the gradient)
     wd = w[dst];
     md = m[dst];
   }
-  float s = 0.f;
-  for (int n0 = 0; n0 < batch; n0 += 64) {  // 64 image partials in flight, summed in order
-    float v[64];
-#pragma unroll
-    for (int u = 0; u < 64; ++u)
-      v[u] = n0 + u < batch ? convp[(size_t)(n0 + u) * CONVP_STRIDE + e] : 0.f;
-#pragma unroll
-    for (int u = 0; u < 64; ++u) s += v[u];
-  }
+  const float s = conv_partial_sum(convp, batch, e);
   if (APPLY) {
     const float mn = mu * md + s;
     m[dst] = mn;
@@ -761,6 +798,98 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
     return;
   }
   apply_one<APPLY>(w, g, m, dst, s, mu, lr);
+}
+
+// The update launch with the xGMI push sync (PushArgs, lenet.h).  Same blocks
+// and gradient forms as update_kernel; no thread leaves before the barrier
+// (every block takes part in it).  A lane's values: FC - its 16 weights of
+// the tile (+ the bias on the row-0 tiles, lanes 0-31); conv - one slot.
+constexpr int PUSH_VALS = 17;
+__global__ __launch_bounds__(256) void update_push_kernel(
+    const float* __restrict__ acts, const float* __restrict__ deltas,
+    const float* __restrict__ convp, int batch, const Offsets o, float* __restrict__ w,
+    float* __restrict__ m, float mu, const float* lr_ptr, long long* step, const PushArgs pa) {
+  __shared__ unsigned ep;
+  const xgmi::Sync& S = pa.sync;
+  const int n = S.nranks, me = S.rank, tid = threadIdx.x, lane = tid & 63;
+  const int blk = blockIdx.x;
+  if (blk == 0 && tid == 0) *step += 1;
+  float gv[PUSH_VALS];
+  int wi[PUSH_VALS];  // flat index of value v, or -1
+#pragma unroll
+  for (int v = 0; v < PUSH_VALS; ++v) {
+    gv[v] = 0.f;
+    wi[v] = -1;
+  }
+  if (blk < UB_FC) {
+    const int ft = blk * 4 + (tid >> 6);
+    if (ft < FT_ALL) {
+      const FcTile f = fc_tile(ft, o, lane);
+      f32x16 acc;
+      float bs;
+      fc_tile_product(acts, deltas, batch, f, lane, acc, bs);
+      if (f.j0 + (lane & 31) < f.nout) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int i = f.i0 + mfma32_row(q, lane);
+          gv[q] = acc[q];
+          wi[q] = i < f.nin ? f.woff + i * f.nout + f.j0 + (lane & 31) : -1;
+        }
+        if (f.bias_tile && lane < 32) {
+          gv[16] = bs;
+          wi[16] = f.boff + f.j0 + lane;
+        }
+      }
+    }
+  } else {
+    const int e = (blk - UB_FC) * 256 + tid;
+    const int dst = conv_dst(e, o);
+    if (dst >= 0) {
+      gv[0] = conv_partial_sum(convp, batch, e);
+      wi[0] = dst;
+    }
+  }
+  // push: slot [parity][me] of every peer's receive buffer
+  const long long slot_bytes = pa.total * 4;
+  const long long rbytes = 2 * (long long)n * slot_bytes;
+  const unsigned e = xgmi::next_epoch(S, &ep);
+  const int par = (int)(e & 1u);
+  const long long t0 = xgmi::now_ticks();
+#pragma unroll
+  for (int r = 0; r < xgmi::kMaxRanks; ++r) {
+    if (r >= n || r == me) continue;
+    const xgmi::Rsrc rs = xgmi::rsrc(pa.recv[r], rbytes);
+    const unsigned base = (unsigned)(((long long)par * n + me) * slot_bytes);
+#pragma unroll
+    for (int v = 0; v < PUSH_VALS; ++v)
+      if (wi[v] >= 0) xgmi::st_sys(rs, base + 4u * (unsigned)wi[v], gv[v]);
+  }
+  xgmi::link_floor(S, t0, slot_bytes);
+  xgmi::barrier(S, 0, e, /*release=*/false);  // the pushed values are system-scope stores
+  // every rank's values in flight, then summed in rank order and applied
+  const xgmi::Rsrc mine = xgmi::rsrc(pa.recv[me], rbytes);
+  const float lr = *lr_ptr;
+#pragma unroll
+  for (int v = 0; v < PUSH_VALS; ++v) {
+    if (wi[v] < 0) continue;
+    float x[xgmi::kMaxRanks];
+#pragma unroll
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
+      if (r < n)
+        x[r] = !xgmi::contributes(S, r) ? 0.f
+               : r == me ? gv[v]
+                         : xgmi::ld_sys(mine, (unsigned)(((long long)par * n + r) * slot_bytes +
+                                                         4LL * wi[v]));
+    float sum = x[0];
+#pragma unroll
+    for (int r = 1; r < xgmi::kMaxRanks; ++r)
+      if (r < n) sum += x[r];
+    // optim::sgd_momentum_flat_kernel's expression forms (l2 = 0)
+    const float g = __builtin_fmaf(0.f, w[wi[v]], sum * pa.gscale);
+    const float mn = mu * m[wi[v]] + g;
+    m[wi[v]] = mn;
+    w[wi[v]] -= lr * mn;
+  }
 }
 
 // ------------------------------------------------------------- launchers ----
@@ -785,6 +914,19 @@ void launch_update(const float* acts, const float* deltas, const float* convp, i
   else
     update_kernel<false><<<blocks, 256, 0, s>>>(acts, deltas, convp, batch, off, params, grads,
                                                 mom, momentum, lr, step);
+}
+
+void launch_update_push(const float* acts, const float* deltas, const float* convp, int batch,
+                        const Offsets& off, float* params, float* mom, float momentum,
+                        const float* lr, long long* step, const PushArgs& pa, hipStream_t s) {
+  const int n = pa.sync.nranks;
+  if (n < 1 || n > xgmi::kMaxRanks || !pa.sync.flags || !pa.sync.epoch || !pa.sync.error ||
+      pa.total <= 0 || 2LL * n * pa.total * 4 >= (1LL << 32))
+    throw std::runtime_error("lenet push sync: communicator / receive buffer not set up");
+  for (int r = 0; r < n; ++r)
+    if (!pa.recv[r]) throw std::runtime_error("lenet push sync: receive buffer of a rank unmapped");
+  update_push_kernel<<<UB_FC + UB_CONV, 256, 0, s>>>(acts, deltas, convp, batch, off, params, mom,
+                                                     momentum, lr, step, pa);
 }
 
 size_t acts_floats(int batch) { return (size_t)batch * ACT_STRIDE; }

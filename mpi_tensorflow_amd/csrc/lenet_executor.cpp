@@ -45,6 +45,19 @@ void LenetExecutor::forward_backward(hipStream_t s) {
 
 void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
   lenet::launch_image_train(image_args(), s);
+  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && p_.xrecv != 0) {
+    lenet::PushArgs pa;
+    pa.sync = x->sync();
+    for (int r = 0; r < x->size(); ++r)
+      pa.recv[r] = static_cast<float*>(x->peer_ptr(reinterpret_cast<const void*>(p_.xrecv), r));
+    pa.total = p_.total;
+    pa.gscale = 1.0f / (float)x->size();
+    lenet::launch_update_push(P<const float>(p_.acts), P<const float>(p_.deltas),
+                              P<const float>(p_.convp), p_.batch, p_.off, P<float>(p_.params),
+                              P<float>(p_.mom), p_.momentum, P<const float>(p_.lr),
+                              P<long long>(p_.step), pa, s);
+    return;
+  }
   const bool apply = comm == nullptr;
   lenet::launch_update(P<const float>(p_.acts), P<const float>(p_.deltas), P<const float>(p_.convp),
                        p_.batch, p_.off, P<float>(p_.params), P<float>(p_.grads), P<float>(p_.mom),

@@ -5,6 +5,8 @@
 // and no host-side step state (batch offset and LR come from the device step
 // counter), so the Python engine captures G steps into one hipGraph.
 //   world 1:  image kernel -> update kernel (grads + momentum SGD)   2 launches
+//   world N, xGMI communicator with a receive buffer: image kernel -> update
+//             kernel with the push sync fused (lenet.h PushArgs)   2 launches
 //   world N:  image kernel -> update kernel (grads into the flat buffer)
 //             -> in-place all-reduce of the whole 250 KB flat gradient on
 //             the compute stream (one latency-bound bucket: a cross-stream
@@ -30,6 +32,9 @@ struct LenetPtrs {
   // elements) of the grads
   int grad_bf16 = 0;
   uintptr_t gb16 = 0;
+  // xGMI push sync (lenet.h PushArgs): the registered receive buffer
+  // [2][N][total] floats; 0 = the two-phase all_reduce_sgd instead
+  uintptr_t xrecv = 0;
 };
 
 class LenetExecutor {

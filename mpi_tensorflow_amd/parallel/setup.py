@@ -9,13 +9,14 @@ Gather-to-root weight averaging (`:121-137`).  Here a run gets:
 * `comm`  - the device communicator of parallel/comm.py `make_comm` (RCCL over
   xGMI, the shared-memory one when ranks share GPUs, gloo on the CPU), for
   world > 1 whenever the ranks sync at all;
-* `xcomm` - on one node with one GPU per rank, for the MNIST CNN with
-  `--comm auto`: the xGMI peer-to-peer communicator as an extra sync-schedule
+* `xcomm` - on one node with one GPU per rank, for the MNIST CNN and LeNet-5
+  with `--comm auto`: the xGMI peer-to-peer communicator as an extra sync
   candidate - only after it passed the exactness check
   (`comm.xgmi_exactness_check`: integer data, bitwise equal to the exact sum
   and to `comm`'s sum).  The engine's auto-tune then also compares one trial
-  step of each xGMI schedule with the serial schedule over `comm`
-  (runtime/mnist_engine.py `_xgmi_step_matches`).
+  step of each xGMI schedule with a step synced over `comm`
+  (runtime/mnist_engine.py `_xgmi_step_matches`, runtime/lenet_engine.py
+  `tune_schedule`).
 
 `health_vote` is the run-time half: the xGMI kernels never hang (a missing
 peer sets a sticky error bit and the later barriers stop waiting), so every
@@ -61,12 +62,12 @@ def wants_comm(cfg: C.TrainConfig, world: int) -> bool:
 
 
 def wants_xgmi_candidate(cfg: C.TrainConfig, comm_kind: str, no_xgmi: bool = False) -> bool:
-    """The xGMI peer-to-peer schedules are tuned next to RCCL's for the MNIST
-    CNN when the user left the communicator to `auto`, RCCL is what auto chose
-    (one GPU per rank; ranks sharing GPUs use the host shared-memory path) and
-    the ranks sync gradients every step.  Pure: both entry points decide with
-    it (tests/test_spec.py pins that)."""
-    return (cfg.comm == "auto" and not no_xgmi and cfg.model == "mnist_cnn"
+    """The xGMI peer-to-peer syncs are tuned next to RCCL's for the MNIST CNN
+    and LeNet-5 (the fused executors) when the user left the communicator to
+    `auto`, RCCL is what auto chose (one GPU per rank; ranks sharing GPUs use
+    the host shared-memory path) and the ranks sync gradients every step.
+    Pure: both entry points decide with it (tests/test_comm_setup_cpu.py)."""
+    return (cfg.comm == "auto" and not no_xgmi and cfg.model in ("mnist_cnn", "lenet5")
             and cfg.sync == "grad" and comm_kind == "rccl-native")
 
 

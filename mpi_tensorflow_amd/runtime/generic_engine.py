@@ -549,7 +549,8 @@ class GenericEngine:
 
 def make_image_engine(cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
                       device: torch.device, rank: int = 0, world: int = 1,
-                      comm: Optional[DeviceComm] = None, force_sync: bool = False):
+                      comm: Optional[DeviceComm] = None, force_sync: bool = False,
+                      xcomm=None):
     """Engine for the extra image models: LeNet-5 on a GPU runs the fused
     two-launch executor (runtime/lenet_engine.py); everything else (ResNet-18,
     the CPU oracle) runs the op-by-op engine.  LeNet-5 has no bf16 variant:
@@ -565,5 +566,6 @@ def make_image_engine(cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarr
                 print("[lenet5] --dtype bf16: LeNet-5's layers are VALU-bound at any operand "
                       "type; running the fp32 fused executor", flush=True)
             cfg = dataclasses.replace(cfg, dtype="fp32")
-        return NativeLenetEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)
+        return NativeLenetEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync,
+                                 xcomm=xcomm)
     return GenericEngine(cfg, train_x, train_y, device, rank, world, comm, force_sync)

@@ -22,7 +22,7 @@ import torch
 from .. import config as C
 from ..models.generic import make_model
 from ..ops import native, ptr, stream_handle
-from ..parallel.comm import DeviceComm
+from ..parallel.comm import DeviceComm, XgmiDeviceComm
 from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
 
@@ -35,7 +35,11 @@ class NativeLenetEngine:
 
     def __init__(self, cfg: C.TrainConfig, train_x: np.ndarray, train_y: np.ndarray,
                  device: torch.device, rank: int = 0, world: int = 1,
-                 comm: Optional[DeviceComm] = None, force_sync: bool = False):
+                 comm: Optional[DeviceComm] = None, force_sync: bool = False,
+                 xcomm: Optional[XgmiDeviceComm] = None):
+        """xcomm: an exactness-gated xGMI communicator (parallel/setup.py) next
+        to an RCCL `comm`: tune_schedule() times both syncs and keeps the
+        faster (the xGMI one only after one trial step matched RCCL's)."""
         if device.type != "cuda":
             raise RuntimeError("NativeLenetEngine needs a GPU")
         if cfg.model != "lenet5":
@@ -95,25 +99,45 @@ class NativeLenetEngine:
                 raise RuntimeError("bf16 gradient wire needs a flat buffer of 4k floats")
             self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)
             p.grad_bf16, p.gb16 = 1, ptr(self.gb16)
-        self.ptrs = p
-        self.exe = C_.LenetExecutor(p)
         self._native_comm = None
+        self.xgmi_push = False
+        self.xcomm = None
+        self._sync = None  # the communicator the step syncs over (native handle)
         if self.grad_sync:
             self._native_comm = comm.native_handle
             if self._native_comm is None:
                 raise RuntimeError("GPU grad sync needs the native RCCL communicator")
             if getattr(comm, "kind", "") == "host-staged":  # test comm: eager only
                 comm.bases = [self.grads] + ([self.gb16] if self.gb16 is not None else [])
-            self._xgmi = hasattr(comm, "register")
-            if self._xgmi:  # xGMI peer to peer: peers read the grads and params,
-                # and (to make it whole) the sharded momentum
+            self.xcomm = comm if isinstance(comm, XgmiDeviceComm) else xcomm
+            if self.xcomm is not None:  # xGMI peer to peer: peers read the grads and
+                # params, and (to make it whole) the sharded momentum
                 if self.gb16 is not None:
                     raise ValueError("the xGMI communicator reduces fp32 grads only")
-                comm.register(self.grads, self.params, self.mom)
-            # connection setup of the collective, outside any capture
+                self.xcomm.register(self.grads, self.params, self.mom)
+                if cfg.xgmi_push:
+                    # push sync fused into the update launch (lenet.h PushArgs):
+                    # receive slots [2 parities][N ranks][total], replicated momentum
+                    self.xrecv = torch.zeros(2 * self.xcomm.size * self.layout.total, device=dev)
+                    self.xcomm.register(self.xrecv)
+                    p.xrecv = ptr(self.xrecv)
+                    self.xgmi_push = True
+            self._sync = self._native_comm
+            # connection setup of the collective, outside any capture (the
+            # executor copies the pointer struct: made after xrecv is set)
+            self.ptrs = p
+            self.exe = C_.LenetExecutor(p)
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())
             torch.cuda.synchronize(dev)
+        if not self.grad_sync:
+            self.ptrs = p
+            self.exe = C_.LenetExecutor(p)
+        self.tune_log: Dict[str, Optional[float]] = {}
+        self.tune_reject: Dict[str, str] = {}
+        self.xgmi_step_check: Dict[str, float] = {}
+        self._tuned = not (self.grad_sync and xcomm is not None and self.xcomm is xcomm
+                           and cfg.graph and cfg.sync_schedule == "auto")
         self.use_graph = cfg.graph and getattr(comm, "kind", "") != "host-staged"
         self.graph_steps = max(1, cfg.graph_steps)
         self._graphs: Dict[int, torch.cuda.CUDAGraph] = {}
@@ -125,11 +149,23 @@ class NativeLenetEngine:
 
     def sync_optimizer_state(self) -> None:
         """Replicated optimizer state: nothing to gather, except over the xGMI
-        communicator, whose fused all-reduce + SGD keeps each rank's momentum
-        segment only (csrc/xgmi_comm.h all_reduce_sgd)."""
-        if self.grad_sync and getattr(self, "_xgmi", False):
-            self._native_comm.gather_segments(ptr(self.mom), self.layout.total, stream_handle())
+        communicator's two-phase sync, whose fused all-reduce + SGD keeps each
+        rank's momentum segment only (csrc/xgmi_comm.h all_reduce_sgd); the
+        push sync (default) keeps the momentum replicated."""
+        if self._syncs_over_xgmi() and not self.xgmi_push:
+            self._sync.gather_segments(ptr(self.mom), self.layout.total, stream_handle())
             torch.cuda.synchronize(self.device)
+
+    def _syncs_over_xgmi(self) -> bool:
+        return self.xcomm is not None and self._sync is self.xcomm.native_handle
+
+    @property
+    def sync_schedule(self) -> str:
+        if not self.grad_sync:
+            return "none"
+        if self._syncs_over_xgmi():
+            return "xgmi-push" if self.xgmi_push else "xgmi"
+        return "all-reduce"
 
     def extra_state(self):
         return {}
@@ -146,10 +182,17 @@ class NativeLenetEngine:
 
     # ------------------------------------------------------------------ step
     def _launch_one(self) -> None:
-        self.exe.train_step(stream_handle(), self._native_comm)
+        self.exe.train_step(stream_handle(), self._sync)
+
+    def _set_sync(self, c) -> None:
+        if c is self._sync:
+            return
+        self.sync_optimizer_state()  # (two-phase xGMI: the sharded momentum made whole)
+        self._sync = c
 
     def _graph(self, n: int):
-        g = self._graphs.get(n)
+        key = (id(self._sync), n)
+        g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
             try:
@@ -162,8 +205,97 @@ class NativeLenetEngine:
                 self.use_graph = False
                 torch.cuda.synchronize(self.device)
                 return None
-            self._graphs[n] = g
+            self._graphs[key] = g
         return g
+
+    def tune_schedule(self) -> int:
+        """With an xGMI candidate next to RCCL (setup_comms): times TUNE
+        replays of each sync's captured G-step graph and keeps the faster.
+        The xGMI sync must first pass the health vote (no barrier timed out,
+        identical replicas) and one trial step equal to RCCL's within
+        XGMI_STEP_RTOL of the update (identical replicas cannot show a
+        wrong-but-consistent sum).  Side-effect free (params, momentum and the
+        device step are restored); collective (max-over-ranks times, voted
+        checks).  Returns the trial steps run."""
+        if self._tuned:
+            return 0
+        from ..parallel import dist as D
+        from ..parallel.sync import replicas_identical
+        from .mnist_engine import TUNE_REPLAYS, XGMI_STEP_RTOL
+        G = self.graph_steps
+        snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
+        name_x = "xgmi-push" if self.xgmi_push else "xgmi"
+        cands = [("all-reduce", self._native_comm), (name_x, self.xcomm.native_handle)]
+        best, steps = None, 0
+
+        def restore():
+            self.params.copy_(snap[0])
+            self.mom.copy_(snap[1])
+            self.step_dev.copy_(snap[2])
+            torch.cuda.synchronize(self.device)
+
+        for name, c in cands:
+            self._set_sync(c)
+            restore()
+            g = self._graph(G)
+            if D.allreduce_max_host(0.0 if g is not None else 1.0) != 0.0:
+                self.tune_log[name] = None
+                continue
+            g.replay()
+            torch.cuda.synchronize(self.device)
+            steps += G
+            if c is not self._native_comm:
+                why = None
+                if D.allreduce_max_host(float(self.xcomm.error())) != 0.0:
+                    why = "a peer barrier timed out"
+                else:
+                    self.sync_optimizer_state()
+                    if not (replicas_identical(self.params) and replicas_identical(self.mom)):
+                        why = "the replicas differ after the trial steps"
+                if why is None and not self.xcomm.emulated_comm:  # one eager step each
+                    outs = []
+                    for cc in (c, self._native_comm):
+                        self._set_sync(cc)
+                        restore()
+                        self._launch_one()
+                        torch.cuda.synchronize(self.device)
+                        outs.append(self.params.clone())
+                    self._set_sync(c)
+                    dx, ds = outs[0] - snap[0], outs[1] - snap[0]
+                    ref = float(ds.abs().max())
+                    err = float((dx - ds).abs().max())
+                    worst = D.allreduce_max_host(err / max(ref, 1e-30))
+                    bad = not (err <= XGMI_STEP_RTOL * ref)
+                    if D.allreduce_max_host(1.0 if bad else 0.0) != 0.0:
+                        why = (f"one trial step differs from the all-reduce's by {worst:.2e} of "
+                               f"the largest update (bound {XGMI_STEP_RTOL:g})")
+                    else:
+                        self.xgmi_step_check[name] = worst
+                if why is not None:
+                    self.tune_log[name] = None
+                    self.tune_reject[name] = why
+                    if self.rank == 0:
+                        print(f"[rank 0] sync {name} rejected: {why}", flush=True)
+                    if "timed out" in why:
+                        self.xcomm = None  # never used again (its barriers stop waiting)
+                    continue
+                restore()
+            t0 = torch.cuda.Event(enable_timing=True)
+            t1 = torch.cuda.Event(enable_timing=True)
+            t0.record()
+            for _ in range(TUNE_REPLAYS):
+                g.replay()
+            t1.record()
+            torch.cuda.synchronize(self.device)
+            steps += TUNE_REPLAYS * G
+            us = D.allreduce_max_host(1000.0 * t0.elapsed_time(t1) / (TUNE_REPLAYS * G))
+            self.tune_log[name] = round(us, 2)
+            if best is None or us < best[0]:
+                best = (us, c)
+        self._set_sync(best[1] if best is not None else self._native_comm)
+        restore()
+        self._tuned = True
+        return steps
 
     def capture(self, k: int) -> None:
         if self.use_graph and k > 0:
@@ -176,6 +308,8 @@ class NativeLenetEngine:
     def train(self, k: int) -> None:
         if k <= 0:
             return
+        if not self._tuned:  # side-effect free: restores the state it trained
+            self.tune_schedule()
         done = 0
         if self.use_graph:
             G = self.graph_steps

@@ -139,7 +139,7 @@ class Trainer:
         from .generic_engine import make_image_engine
 
         return make_image_engine(cfg, sh.train_x, sh.train_y, self.device, self.rank, self.world,
-                                 self.comm)
+                                 self.comm, xcomm=self.comms.xcomm)
 
     # ------------------------------------------------------------------- run
     def total_steps(self) -> int:

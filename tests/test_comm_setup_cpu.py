@@ -19,7 +19,8 @@ def test_xgmi_candidate_rule():
     assert not SU.wants_xgmi_candidate(base, "rccl-native", no_xgmi=True)
     assert not SU.wants_xgmi_candidate(base, "host-shm")  # ranks share GPUs
     assert not SU.wants_xgmi_candidate(base, "torch-gloo")
-    for kw in (dict(comm="rccl"), dict(model="lenet5"), dict(sync="param_avg"), dict(no_xgmi=True)):
+    assert SU.wants_xgmi_candidate(C.TrainConfig(model="lenet5").validate(), "rccl-native")
+    for kw in (dict(comm="rccl"), dict(model="resnet18"), dict(sync="param_avg"), dict(no_xgmi=True)):
         cfg = C.TrainConfig(**kw).validate()
         assert not SU.wants_xgmi_candidate(cfg, "rccl-native", no_xgmi=cfg.no_xgmi), kw
     assert SU.wants_comm(base, 2) and not SU.wants_comm(base, 1)

@@ -39,18 +39,21 @@ def test_xgmi_two_ranks_bit_identical_to_buckets(dtype):
 
 
 @pytest.mark.gpu
-def test_xgmi_lenet5_two_ranks_fused_allreduce_sgd_matches_serial():
-    """The fused LeNet-5 executor over the xGMI communicator: one launch
-    sums this rank's segment of the grads and applies the momentum SGD there
-    (sharded momentum), then gathers the other segments - bit-identical to the
-    serial emulation of data parallelism (rank-order sum + flat SGD)."""
+@pytest.mark.parametrize("mode", ["xgmi", "xgmi2p"])
+def test_xgmi_lenet5_two_ranks_fused_sync_matches_serial(mode):
+    """The fused LeNet-5 executor over the xGMI communicator, bit-identical to
+    the serial emulation of data parallelism (rank-order sum + flat SGD):
+    xgmi - the push sync in the update launch (every block pushes its
+    gradient values into the peers' receive slots, one barrier, rank-order
+    sum, replicated SGD); xgmi2p - the two-phase launch (this rank's segment
+    summed and updated, sharded momentum, then the other segments gathered)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), HELPER, "generic",
-           "lenet5-native-xgmi"]
+           f"lenet5-native-{mode}"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
-    assert "CAPTURED_SYNC_OK generic lenet5-native-xgmi world=2" in r.stdout, r.stdout[-2000:]
+    assert f"CAPTURED_SYNC_OK generic lenet5-native-{mode} world=2" in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.gpu
