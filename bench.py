@@ -70,9 +70,9 @@ def parse(argv=None):
                          "GPUs; on one node the xGMI peer-to-peer schedule is also tuned)")
     ap.add_argument("--no-xgmi", action="store_true",
                     help="comm auto: do not set up the xGMI peer-to-peer communicator")
-    ap.add_argument("--xgmi-two-phase", action="store_true",
-                    help="lenet5 over xGMI: the two-phase all-reduce + SGD launch instead of "
-                         "the push sync fused into the update launch")
+    ap.add_argument("--xgmi-push", action="store_true",
+                    help="lenet5 over xGMI: the push sync fused into the update launch instead "
+                         "of the two-phase all-reduce + SGD launch (comm auto tunes both)")
     ap.add_argument("--xgmi-inject-skip-peer", type=int, default=-1, metavar="R",
                     help="failure injection (tests): the xGMI phase-1 reductions leave out rank "
                          "R; the exactness gate must then reject the xGMI communicator")
@@ -238,7 +238,7 @@ def run(a, di, device, wd) -> int:
                         defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
                         bucket_plan=f"bytes:{a.bucket_mb:g}" if a.bucket_mb else a.bucket_plan,
                         collective_timeout_s=a.collective_timeout_s,
-                        no_xgmi=a.no_xgmi, xgmi_push=not a.xgmi_two_phase).validate()
+                        no_xgmi=a.no_xgmi, xgmi_push=a.xgmi_push).validate()
     force = bool((a.force_sync or a.comm_emulate or a.xgmi_emulate) and N == 1
                  and device.type == "cuda")
     with wd.guard("start-up (communicator, engine)"):

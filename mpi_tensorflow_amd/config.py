@@ -108,10 +108,11 @@ class TrainConfig:
     # comm auto, one node: do not set up the xGMI peer-to-peer communicator as
     # an extra sync-schedule candidate (parallel/setup.py setup_comms)
     no_xgmi: bool = False
-    # LeNet-5 over the xGMI communicator: the push sync fused into the update
-    # launch (one barrier, replicated momentum) instead of the two-phase
-    # all-reduce + SGD launch (kernels/lenet.h PushArgs)
-    xgmi_push: bool = True
+    # LeNet-5 over the xGMI communicator (--comm xgmi): the push sync fused
+    # into the update launch (one barrier, replicated momentum, kernels/lenet.h
+    # PushArgs) instead of the two-phase all-reduce + SGD launch; with --comm
+    # auto both are tuned next to RCCL
+    xgmi_push: bool = False
     # fp32 MNIST conv2 algorithm on the native engine: "winograd" (F(2x2,5x5),
     # kernels/wino.h; 2.8x fewer MFMAs, fp32 arithmetic throughout, ~1e-6
     # relative error) or "direct" (25-tap implicit GEMM)

@@ -389,6 +389,36 @@ PYBIND11_MODULE(_C, m) {
                                           P<float>(ws), P<float>(dw), S(st));
           check_launch();
         });
+  g.def("conv_fwd_s2d_stem_bf16", [](const gops::ConvShape& si, uintptr_t xs, uintptr_t wt8,
+                                     uintptr_t yb, uintptr_t st, uintptr_t stats_part,
+                                     int stats_rows, uintptr_t stats_shift) {
+    const gops::ConvStats cs{P<float>(stats_part), stats_rows, P<const float>(stats_shift)};
+    gops::conv_fwd_s2d_stem_bf16(si, P<const void>(xs), P<const void>(wt8), P<void>(yb), S(st),
+                                 &cs);
+    check_launch();
+  }, py::arg("si"), py::arg("xs"), py::arg("wt8"), py::arg("yb"), py::arg("st"),
+     py::arg("stats_part") = 0, py::arg("stats_rows") = 0, py::arg("stats_shift") = 0);
+  g.def("conv_bwd_filter_s2d_stem_bf16",
+        [](const gops::ConvShape& si, uintptr_t xs, uintptr_t dyb, uintptr_t ws, uintptr_t dw8,
+           uintptr_t st) {
+          gops::conv_bwd_filter_s2d_stem_bf16(si, P<const void>(xs), P<const void>(dyb),
+                                              P<float>(ws), P<float>(dw8), S(st));
+          check_launch();
+        });
+  g.def("s2d_stem_ws_floats", &gops::s2d_stem_ws_floats);
+  g.def("s2d_stem_input", [](uintptr_t x, int N, int H, int W, int OH, int OW, uintptr_t xs,
+                             uintptr_t st) {
+    gops::s2d_stem_input(P<const float>(x), N, H, W, OH, OW, P<void>(xs), S(st));
+    check_launch();
+  });
+  g.def("s2d_stem_weight", [](uintptr_t w, int K, uintptr_t wt8, uintptr_t st) {
+    gops::s2d_stem_weight(P<const float>(w), K, P<void>(wt8), S(st));
+    check_launch();
+  });
+  g.def("s2d_stem_wgrad", [](uintptr_t dw8, int K, uintptr_t gw, uintptr_t st) {
+    gops::s2d_stem_wgrad(P<const float>(dw8), K, P<float>(gw), S(st));
+    check_launch();
+  });
   g.def("to_bf16", [](uintptr_t x, uintptr_t y, long long n, uintptr_t st) {
     gops::to_bf16(P<const float>(x), P<void>(y), n, S(st));
     check_launch();
@@ -763,6 +793,8 @@ PYBIND11_MODULE(_C, m) {
   });
   py::class_<LenetExecutor>(m, "LenetExecutor")
       .def(py::init<const LenetPtrs&>())
+      .def("set_xgmi_push", &LenetExecutor::set_xgmi_push)
+      .def_property_readonly("xgmi_push", &LenetExecutor::xgmi_push)
       .def("train_step",
            [](LenetExecutor& e, uintptr_t s, Collective* comm) {
              e.train_step(S(s), comm);

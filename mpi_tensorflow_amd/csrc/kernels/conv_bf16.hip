@@ -450,6 +450,65 @@ struct StemLoader {
   }
 };
 
+// Space-to-depth stem (conv_fwd_s2d_stem_bf16): the 7x7 / stride-2 / pad-3
+// conv over 3 channels, re-cast as a 4x4 / stride-1 conv over the bf16
+// space-to-depth image xs [N][OH + 3][OW + 3][16] (s2d_stem_input: pixel
+// (Y, X) holds the 2x2 input block at rows 2 (Y - 2) + p, columns
+// 2 (X - 2) + q as channels (p * 2 + q) * 3 + ci, 4 zero channels, zero
+// outside the image), with the 8x8-extended filter (tap (a, b) <- kernel
+// (2a + p - 1, 2b + q - 1), zero off the 7x7).  GEMM K = 16 taps x 16
+// channels: K tile kt = tap row a, a thread's 8 consecutive k = half of tap
+// (a, c8 / 2)'s channels = ONE aligned 16-byte load, always inside the padded
+// image - no masks, no fp32 gather, no conversion (the StemLoader's implicit
+// im2col did 2 unaligned fp32 float4 loads + masks + a pack per 8 k).
+template <int BM, int BN>
+struct S2dLoader {
+  static constexpr int AR = BM * BK / 8 / NT;
+  static constexpr int BR = BN * BK / 8 / NT;
+  static constexpr int EXTRA = 0;
+  const __bf16* abase[AR];
+  bool av[AR];
+  const __bf16* bbase[BR];
+  uint4 ra[AR];
+  uint4 rb[BR];
+  int ws16;  // one s2d image row, in bf16 (16 channels a pixel)
+  __device__ S2dLoader(const ConvShape& s, const ConvShape& si, const __bf16* x,
+                       const __bf16* wt, int m0, int n0, __bf16*) {
+    const int tid = threadIdx.x, c8 = tid & 7;
+    const int M = s.N * s.OH * s.OW;
+    ws16 = si.W * 16;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + (NT / 8) * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+      abase[i] = x + (((size_t)n * si.H + oy) * si.W + ox + (c8 >> 1)) * 16 + 8 * (c8 & 1);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = min(n0 + (tid >> 3) + (NT / 8) * i, s.K - 1);
+      bbase[i] = wt + (size_t)n * s.C + 8 * c8;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      ra[i] = av[i] ? *reinterpret_cast<const uint4*>(abase[i] + (size_t)kt * ws16)
+                    : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int i = 0; i < BR; ++i) rb[i] = *reinterpret_cast<const uint4*>(bbase[i] + kt * BK);
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x, c8 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[i];
+  }
+};
 
 // BatchNorm statistics in a bf16-output epilogue (ConvStats): lane (r, h) of
 // a wave holds column r of its 32-row tiles; after its own rows are summed
@@ -2386,6 +2445,71 @@ void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const f
     STEM_WG(64, 64);
 #undef STEM_WG
   if (p.z > 1) slab_reduce(ws, p.z, (long long)s1.C * s1.K / 4, dw, st);
+}
+
+// ---- space-to-depth stem (S2dLoader) -----------------------------------
+// si: the 4x4 stride-1 conv over the s2d image (N, OH + 3, OW + 3, 16 -> K);
+// s1 its 1x1 GEMM view (N, OH, OW, 256 -> K)
+static ConvShape s2d_gemm_shape(const ConvShape& si) {
+  ConvShape s1{};
+  s1.N = si.N;
+  s1.H = s1.OH = si.OH;
+  s1.W = s1.OW = si.OW;
+  s1.C = 256;
+  s1.K = si.K;
+  s1.R = s1.S = s1.stride = 1;
+  s1.pad = 0;
+  return s1;
+}
+static void s2d_check(const ConvShape& si) {
+  if (si.C != 16 || si.R != 4 || si.S != 4 || si.stride != 1 || si.pad != 0 || si.K % 64 ||
+      si.OH != si.H - 3 || si.OW != si.W - 3 || (long long)si.N * si.H * si.W * 16 >= (1LL << 31))
+    throw std::runtime_error("s2d stem conv: inconsistent shapes");
+}
+
+void conv_fwd_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* wt8, void* yb,
+                            hipStream_t st, const ConvStats* stats) {
+  using namespace cbf;
+  s2d_check(si);
+  const ConvShape s1 = s2d_gemm_shape(si);
+  ConvStats cs;
+  if (stats && stats->part) {
+    if (stats->P != conv_fwd_stem_stats_rows(s1))
+      throw std::runtime_error("s2d stem conv: BatchNorm statistics layout mismatch");
+    cs = *stats;
+  }
+  const long long M = (long long)s1.N * s1.OH * s1.OW;
+  const dim3 grid(cdiv(M, 128) * (s1.K / 64), 1);
+  fwd_kernel<128, 64, __bf16, S2dLoader<128, 64>><<<grid, NT, 0, st>>>(
+      s1, reinterpret_cast<const __bf16*>(xs), reinterpret_cast<const __bf16*>(wt8), nullptr,
+      nullptr, 0, s1.C / BK, nullptr, reinterpret_cast<__bf16*>(yb), 0, si, cs);
+}
+
+// the 4x4 conv's filter gradient over the s2d image: the generic bf16 wgrad
+// (rows m = tap * 16 + channel; a channel quad never straddles taps), split-K
+// slabs summed into dw8 [256][K]
+void conv_bwd_filter_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* dyb,
+                                   float* ws, float* dw8, hipStream_t st) {
+  using namespace cbf;
+  s2d_check(si);
+  const WgPlan p = wg_plan(si);
+  if (p.z > 1 && !ws) throw std::runtime_error("s2d stem wgrad: split-K needs a workspace");
+  float* out = p.z > 1 ? ws : dw8;
+  const int blocks = cdiv(256, p.bm) * (si.K / p.bn) * p.z;
+  const __bf16* xh = reinterpret_cast<const __bf16*>(xs);
+  const __bf16* dh = reinterpret_cast<const __bf16*>(dyb);
+  if (p.bn == 128)
+    wgrad_kernel<64, 128, true><<<blocks, NT, 0, st>>>(si, xh, dh, out, p.kchunk, si);
+  else
+    wgrad_kernel<64, 64, true><<<blocks, NT, 0, st>>>(si, xh, dh, out, p.kchunk, si);
+  if (p.z > 1) slab_reduce(ws, p.z, 256LL * si.K / 4, dw8, st);
+}
+
+size_t s2d_stem_ws_floats(const ConvShape& si) {
+  using namespace cbf;
+  s2d_check(si);
+  const WgPlan p = wg_plan(si);
+  return p.z > 1 ? (size_t)p.z * 256 * si.K : 0;
 }
 
 }  // namespace gops

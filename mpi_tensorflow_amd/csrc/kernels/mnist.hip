@@ -597,13 +597,17 @@ __device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
 // 89 VGPRs, 392 blocks - measured 13.2 us: the shorter chains did not pay
 // for the doubled operand traffic and block count.)
 // tid: index in the 256-thread unit
+// (Negative, round 6: the weights / momentum of the tile requested into LDS
+// with global_load_lds before the products - no VGPRs - so the SGD would not
+// wait for two HBM / MALL round trips after the MFMAs: the launch went 11.5
+// -> 13.4 us, r6_s1.)
 __device__ __forceinline__ void fc1_dw_sgd(const FcSgd& a, int L, int tid) {
-  const int lane = tid & 63, r = lane & 31;
-  f32x16 c0, c1;
-  int m0, n0;
-  fc1_dw_tile(L, a.a2, a.dh, a.batch, tid >> 6, c0, c1, m0, n0);
+  const int lane = tid & 63, r = lane & 31, wave = tid >> 6;
   float* w = a.w + (size_t)a.w1_off4 * 4;
   float* mo = a.m + (size_t)a.w1_off4 * 4;
+  f32x16 c0, c1;
+  int m0, n0;
+  fc1_dw_tile(L, a.a2, a.dh, a.batch, wave, c0, c1, m0, n0);
   const float lr = *a.lr;
   auto apply = [&](const f32x16 c, int col) {
     float wv[16], mv[16];

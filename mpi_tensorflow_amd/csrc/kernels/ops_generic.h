@@ -83,6 +83,23 @@ void conv_fwd_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x
                         void* yb, hipStream_t st, const ConvStats* stats = nullptr);
 void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const float* x,
                                const void* dyb, float* ws, float* dw, hipStream_t st);
+// The ResNet stem (7x7 / stride 2 / pad 3 over 3 channels) by space-to-depth:
+// a 4x4 / stride-1 conv over the bf16 s2d image xs [N][OH + 3][OW + 3][16]
+// (s2d_stem_input) with the 8x8-extended filter wt8 [K][256] (s2d_stem_weight);
+// si = ConvShape(N, OH + 3, OW + 3, 16, K, 4, 4, 1, 0).  Forward: bf16 output
+// yb (+ BatchNorm statistics, conv_fwd_stem_stats_rows of the GEMM view);
+// filter gradient: dw8 [256][K] fp32 (s2d_stem_wgrad maps it back to HWIO),
+// ws of s2d_stem_ws_floats(si) floats.
+void conv_fwd_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* wt8, void* yb,
+                            hipStream_t st, const ConvStats* stats);
+void conv_bwd_filter_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* dyb,
+                                   float* ws, float* dw8, hipStream_t st);
+size_t s2d_stem_ws_floats(const ConvShape& si);
+// x fp32 NHWC [N][H][W][3] -> xs; w HWIO fp32 [7][7][3][K] -> wt8; dw8 -> gw HWIO
+void s2d_stem_input(const float* x, int N, int H, int W, int OH, int OW, void* xs,
+                    hipStream_t st);
+void s2d_stem_weight(const float* w, int K, void* wt8, hipStream_t st);
+void s2d_stem_wgrad(const float* dw8, int K, float* gw, hipStream_t st);
 void conv_fwd_bf16(const ConvShape& s, const float* x, const float* w, const float* bias, float* y,
                    bool relu, float* ws, hipStream_t st, const void* xb = nullptr,
                    const void* wtb = nullptr, void* yb = nullptr,

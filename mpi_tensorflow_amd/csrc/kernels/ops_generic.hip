@@ -1296,6 +1296,81 @@ void stem_wgrad(const float* gpad, int R, int sc, int seg, int K, float* gw, hip
   stem_wgrad_kernel<<<grid1d((long long)R * sc * K), 256, 0, st>>>(gpad, R, sc, seg, K, gw);
 }
 
+// Space-to-depth stem (conv_bf16.hip conv_fwd_s2d_stem_bf16): one thread per
+// s2d pixel (n, Y, X) of [N][OH + 3][OW + 3]: channels (p * 2 + q) * 3 + ci
+// = x[n][2 (Y - 2) + p][2 (X - 2) + q][ci] (zero outside the image), 4 zero
+// channels; two 16-byte stores.
+__global__ __launch_bounds__(256) void s2d_stem_input_kernel(const float* __restrict__ x, int N,
+                                                             int H, int W, int Hs, int Ws,
+                                                             uint4* __restrict__ xs) {
+  const long long n_pix = (long long)N * Hs * Ws;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n_pix;
+       i += (long long)gridDim.x * 256) {
+    const int X = (int)(i % Ws);
+    const long long t = i / Ws;
+    const int Y = (int)(t % Hs), n = (int)(t / Hs);
+    __bf16 v[16];
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const int iy = 2 * (Y - 2) + p;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ix = 2 * (X - 2) + q;
+        const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const float* src = x + (((size_t)n * H + (ok ? iy : 0)) * W + (ok ? ix : 0)) * 3;
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) v[(p * 2 + q) * 3 + ci] = (__bf16)(ok ? src[ci] : 0.f);
+      }
+    }
+#pragma unroll
+    for (int c = 12; c < 16; ++c) v[c] = (__bf16)0.f;
+    const uint4* pv = reinterpret_cast<const uint4*>(v);
+    xs[2 * i] = pv[0];
+    xs[2 * i + 1] = pv[1];
+  }
+}
+
+// wt8 [co][k], k = (a * 4 + b) * 16 + (p * 2 + q) * 3 + ci  <-  w[2a + p - 1][2b + q - 1][ci][co]
+// (zero off the 7x7 kernel and on the 4 padding channels)
+__global__ __launch_bounds__(256) void s2d_stem_weight_kernel(const float* __restrict__ w, int K,
+                                                              __bf16* __restrict__ wt8) {
+  const int n = K * 256;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int co = i >> 8, k = i & 255, tap = k >> 4, ch = k & 15;
+    const int a = tap >> 2, b = tap & 3, pq = ch / 3, ci = ch - 3 * pq;
+    const int ky = 2 * a + (pq >> 1) - 1, kx = 2 * b + (pq & 1) - 1;
+    const bool ok = ch < 12 && ky >= 0 && ky < 7 && kx >= 0 && kx < 7;
+    wt8[i] = (__bf16)(ok ? w[((size_t)(ky * 7 + kx) * 3 + ci) * K + co] : 0.f);
+  }
+}
+
+// gw HWIO [7][7][3][K]  <-  dw8 [k][K] at the k of each real (ky, kx, ci)
+__global__ __launch_bounds__(256) void s2d_stem_wgrad_kernel(const float* __restrict__ dw8, int K,
+                                                             float* __restrict__ gw) {
+  const int n = 147 * K;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const int co = i % K, t = i / K, ci = t % 3, kk = t / 3, ky = kk / 7, kx = kk % 7;
+    const int a = (ky + 1) >> 1, p = (ky + 1) & 1, b = (kx + 1) >> 1, q = (kx + 1) & 1;
+    gw[i] = dw8[(size_t)((a * 4 + b) * 16 + (p * 2 + q) * 3 + ci) * K + co];
+  }
+}
+
+void s2d_stem_input(const float* x, int N, int H, int W, int OH, int OW, void* xs,
+                    hipStream_t st) {
+  const long long n = (long long)N * (OH + 3) * (OW + 3);
+  s2d_stem_input_kernel<<<grid1d(n), 256, 0, st>>>(x, N, H, W, OH + 3, OW + 3,
+                                                   reinterpret_cast<uint4*>(xs));
+}
+
+void s2d_stem_weight(const float* w, int K, void* wt8, hipStream_t st) {
+  s2d_stem_weight_kernel<<<grid1d((long long)K * 256), 256, 0, st>>>(w, K,
+                                                                    reinterpret_cast<__bf16*>(wt8));
+}
+
+void s2d_stem_wgrad(const float* dw8, int K, float* gw, hipStream_t st) {
+  s2d_stem_wgrad_kernel<<<grid1d(147LL * K), 256, 0, st>>>(dw8, K, gw);
+}
+
 // Row softmax (the reference's train_prediction / eval_prediction heads,
 // /root/reference/mpipy.py:67-68): one wave per row, max-subtracted.
 __global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ x,

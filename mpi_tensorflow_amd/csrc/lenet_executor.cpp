@@ -10,7 +10,7 @@ static inline T* P(uintptr_t v) {
   return reinterpret_cast<T*>(v);
 }
 
-LenetExecutor::LenetExecutor(const LenetPtrs& p) : p_(p) {
+LenetExecutor::LenetExecutor(const LenetPtrs& p) : p_(p), push_(p.xrecv != 0) {
   if (p_.batch <= 0 || p_.n_local <= p_.batch)
     throw std::runtime_error("LenetExecutor: the local shard must exceed the batch");
   if (p_.total % 4 != 0) throw std::runtime_error("LenetExecutor: flat buffer not float4-sized");
@@ -45,7 +45,7 @@ void LenetExecutor::forward_backward(hipStream_t s) {
 
 void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
   lenet::launch_image_train(image_args(), s);
-  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && p_.xrecv != 0) {
+  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && push_) {
     lenet::PushArgs pa;
     pa.sync = x->sync();
     for (int r = 0; r < x->size(); ++r)

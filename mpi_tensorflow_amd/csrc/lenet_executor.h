@@ -41,6 +41,10 @@ class LenetExecutor {
  public:
   explicit LenetExecutor(const LenetPtrs& p);
   void train_step(hipStream_t s, Collective* comm);
+  // over an XgmiComm with a receive buffer (xrecv): the push sync fused into
+  // the update launch (on), or the two-phase all_reduce_sgd launch (off)
+  void set_xgmi_push(bool on) { push_ = on && p_.xrecv != 0; }
+  bool xgmi_push() const { return push_; }
   // forward + backward with the weight grads in the flat grad buffer (no
   // sync, no SGD, no step bump): numerics tests
   void forward_backward(hipStream_t s);
@@ -51,4 +55,5 @@ class LenetExecutor {
  private:
   lenet::ImageArgs image_args() const;
   LenetPtrs p_;
+  bool push_ = false;
 };

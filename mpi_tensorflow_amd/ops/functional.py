@@ -462,7 +462,8 @@ class _ConvIm2colFn(torch.autograd.Function):
         # weights in the im2col's k order (tap row kh at kh * seg, (kw, ci)
         # inside), written straight as the 1x1 conv's bf16 [K][kp] layout
         wtb = torch.empty(sh.K * kp, dtype=torch.bfloat16, device=x.device)
-        C.ops.stem_weight_bf16(ptr(w), sh.R, sc, seg, kp, sh.K, ptr(wtb), s)
+        if not out_bf16:
+            C.ops.stem_weight_bf16(ptr(w), sh.R, sc, seg, kp, sh.K, ptr(wtb), s)
         s1 = C.ops.ConvShape(sh.N, sh.OH, sh.OW, kp, sh.K, 1, 1, 1, 0)
         y = torch.empty((sh.N, sh.OH, sh.OW, sh.K),
                         dtype=torch.bfloat16 if out_bf16 else x.dtype, device=x.device)
@@ -470,16 +471,32 @@ class _ConvIm2colFn(torch.autograd.Function):
         # from the image (conv_bf16.hip StemLoader / StemWgLoader); else the
         # column matrix is materialised
         ctx.implicit = bool(out_bf16)
+        ctx.s2d = None
         if ctx.implicit:
             part, rows = None, 0
             if bn_out is not None:  # the consuming BatchNorm's statistics
                 rows = C.ops.conv_fwd_stem_stats_rows(s1)
                 part = torch.empty(2 * sh.K * rows, dtype=torch.float32, device=x.device)
-            C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s, ptr(part), rows,
-                                     ptr(bn_out.shift) if part is not None else 0)
+            shift = ptr(bn_out.shift) if part is not None else 0
+            if _s2d_stem_ok(sh):
+                # space-to-depth: the bf16 s2d image (saved for the filter
+                # gradient) and the 8x8-extended filter, then the 4x4 conv
+                si = _s2d_shape(sh)
+                xs = torch.empty(sh.N * si.H * si.W * 16, dtype=torch.bfloat16, device=x.device)
+                C.ops.s2d_stem_input(ptr(x), sh.N, sh.H, sh.W, sh.OH, sh.OW, ptr(xs), s)
+                wt8 = torch.empty(sh.K * 256, dtype=torch.bfloat16, device=x.device)
+                C.ops.s2d_stem_weight(ptr(w), sh.K, ptr(wt8), s)
+                C.ops.conv_fwd_s2d_stem_bf16(si, ptr(xs), ptr(wt8), ptr(y), s, ptr(part), rows,
+                                             shift)
+                ctx.s2d = si
+                ctx.save_for_backward(xs)
+            else:
+                C.ops.stem_weight_bf16(ptr(w), sh.R, sc, seg, kp, sh.K, ptr(wtb), s)
+                C.ops.conv_fwd_stem_bf16(s1, sh, ptr(x), ptr(wtb), ptr(y), s, ptr(part), rows,
+                                         shift)
+                ctx.save_for_backward(x)
             if part is not None:
                 bn_out.fwd = (part, rows)
-            ctx.save_for_backward(x)
         else:
             col = torch.empty((sh.N, sh.OH, sh.OW, kp), dtype=torch.bfloat16, device=x.device)
             C.ops.im2col_bf16(sh, ptr(x), kp, ptr(col), s)
@@ -496,6 +513,13 @@ class _ConvIm2colFn(torch.autograd.Function):
         s = stream_handle()
         dy = dy.contiguous()
         dyb = _bf16_copy(dy, s)
+        if ctx.s2d is not None:  # the 4x4 conv's filter gradient over the s2d image
+            dw8 = torch.empty((256, s1.K), device=dy.device, dtype=torch.float32)
+            C.ops.conv_bwd_filter_s2d_stem_bf16(ctx.s2d, ptr(src), ptr(dyb), ptr(ctx.ws), ptr(dw8),
+                                                s)
+            C.ops.s2d_stem_wgrad(ptr(dw8), s1.K, ptr(ctx.gw), s)
+            _grad_done(ctx.gw)
+            return None, None, None, None, None, None, None, None
         gpad = torch.empty((s1.C, s1.K), device=dy.device, dtype=torch.float32)
         if ctx.implicit:
             C.ops.conv_bwd_filter_stem_bf16(s1, ctx.si, ptr(src), ptr(dyb), ptr(ctx.ws), ptr(gpad),
@@ -517,6 +541,18 @@ def _im2col_kp(sh, x: torch.Tensor, has_bias: bool, relu: bool) -> int:
     if rseg < 64 or sh.K % 64 != 0:
         return 0
     return (rseg + 63) // 64 * 64
+
+
+def _s2d_stem_ok(sh) -> bool:
+    """The ResNet stem (7x7, stride 2, pad 3, 3 channels, K % 64 == 0) runs
+    by space-to-depth (conv_bf16.hip conv_fwd_s2d_stem_bf16): a 4x4 stride-1
+    conv over a bf16 image of 2x2 input blocks x 3 channels (+ 4 zero)."""
+    return (sh.R == 7 and sh.S == 7 and sh.stride == 2 and sh.pad == 3 and sh.C == 3
+            and sh.K % 64 == 0)
+
+
+def _s2d_shape(sh):
+    return native().ops.ConvShape(sh.N, sh.OH + 3, sh.OW + 3, 16, sh.K, 4, 4, 1, 0)
 
 
 def _im2col_seg(sh) -> int:
@@ -571,7 +607,10 @@ def conv2d(x: torch.Tensor, w: Param, b: Optional[Param], stride: int = 1, pad: 
         ob = bool(out_bf16 and _CONV_BF16 and b is None and not relu)
         if kp:
             s1 = C.ops.ConvShape(N, sh.OH, sh.OW, kp, K, 1, 1, 1, 0)
-            ws = _WS.get(max(C.ops.conv_ws_floats(s1, False), 4), x.device)
+            nws = C.ops.conv_ws_floats(s1, False)
+            if ob and _s2d_stem_ok(sh):
+                nws = max(nws, C.ops.s2d_stem_ws_floats(_s2d_shape(sh)))
+            ws = _WS.get(max(nws, 4), x.device)
             return _ConvIm2colFn.apply(x, w.value, sh, w.grad_view, ws, kp, ob,
                                        bn_out if ob else None)
         ob = ob and C.ops.conv_bf16_ok(sh)

@@ -100,7 +100,6 @@ class NativeLenetEngine:
             self.gb16 = torch.zeros(self.layout.total, dtype=torch.bfloat16, device=dev)
             p.grad_bf16, p.gb16 = 1, ptr(self.gb16)
         self._native_comm = None
-        self.xgmi_push = False
         self.xcomm = None
         self._sync = None  # the communicator the step syncs over (native handle)
         if self.grad_sync:
@@ -115,18 +114,18 @@ class NativeLenetEngine:
                 if self.gb16 is not None:
                     raise ValueError("the xGMI communicator reduces fp32 grads only")
                 self.xcomm.register(self.grads, self.params, self.mom)
-                if cfg.xgmi_push:
-                    # push sync fused into the update launch (lenet.h PushArgs):
-                    # receive slots [2 parities][N ranks][total], replicated momentum
-                    self.xrecv = torch.zeros(2 * self.xcomm.size * self.layout.total, device=dev)
-                    self.xcomm.register(self.xrecv)
-                    p.xrecv = ptr(self.xrecv)
-                    self.xgmi_push = True
+                # receive slots [2 parities][N ranks][total] of the push sync
+                # fused into the update launch (lenet.h PushArgs, replicated
+                # momentum); the two-phase launch is the other xGMI form
+                self.xrecv = torch.zeros(2 * self.xcomm.size * self.layout.total, device=dev)
+                self.xcomm.register(self.xrecv)
+                p.xrecv = ptr(self.xrecv)
             self._sync = self._native_comm
             # connection setup of the collective, outside any capture (the
             # executor copies the pointer struct: made after xrecv is set)
             self.ptrs = p
             self.exe = C_.LenetExecutor(p)
+            self.exe.set_xgmi_push(bool(cfg.xgmi_push))
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())
             torch.cuda.synchronize(dev)
@@ -160,6 +159,10 @@ class NativeLenetEngine:
         return self.xcomm is not None and self._sync is self.xcomm.native_handle
 
     @property
+    def xgmi_push(self) -> bool:
+        return bool(getattr(self, "exe", None) is not None and self.exe.xgmi_push)
+
+    @property
     def sync_schedule(self) -> str:
         if not self.grad_sync:
             return "none"
@@ -184,14 +187,16 @@ class NativeLenetEngine:
     def _launch_one(self) -> None:
         self.exe.train_step(stream_handle(), self._sync)
 
-    def _set_sync(self, c) -> None:
-        if c is self._sync:
+    def _set_sync(self, c, push: Optional[bool] = None) -> None:
+        push = self.xgmi_push if push is None else push
+        if c is self._sync and push == self.xgmi_push:
             return
         self.sync_optimizer_state()  # (two-phase xGMI: the sharded momentum made whole)
         self._sync = c
+        self.exe.set_xgmi_push(push)
 
     def _graph(self, n: int):
-        key = (id(self._sync), n)
+        key = (id(self._sync), self.xgmi_push, n)
         g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
@@ -224,8 +229,9 @@ class NativeLenetEngine:
         from .mnist_engine import TUNE_REPLAYS, XGMI_STEP_RTOL
         G = self.graph_steps
         snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
-        name_x = "xgmi-push" if self.xgmi_push else "xgmi"
-        cands = [("all-reduce", self._native_comm), (name_x, self.xcomm.native_handle)]
+        xh = self.xcomm.native_handle
+        cands = [("all-reduce", self._native_comm, False), ("xgmi", xh, False),
+                 ("xgmi-push", xh, True)]
         best, steps = None, 0
 
         def restore():
@@ -234,8 +240,11 @@ class NativeLenetEngine:
             self.step_dev.copy_(snap[2])
             torch.cuda.synchronize(self.device)
 
-        for name, c in cands:
-            self._set_sync(c)
+        for name, c, push in cands:
+            if c is not self._native_comm and self.xcomm is None:
+                self.tune_log[name] = None  # (the xGMI communicator timed out before)
+                continue
+            self._set_sync(c, push)
             restore()
             g = self._graph(G)
             if D.allreduce_max_host(0.0 if g is not None else 1.0) != 0.0:
@@ -254,13 +263,13 @@ class NativeLenetEngine:
                         why = "the replicas differ after the trial steps"
                 if why is None and not self.xcomm.emulated_comm:  # one eager step each
                     outs = []
-                    for cc in (c, self._native_comm):
-                        self._set_sync(cc)
+                    for cc, pp in ((c, push), (self._native_comm, False)):
+                        self._set_sync(cc, pp)
                         restore()
                         self._launch_one()
                         torch.cuda.synchronize(self.device)
                         outs.append(self.params.clone())
-                    self._set_sync(c)
+                    self._set_sync(c, push)
                     dx, ds = outs[0] - snap[0], outs[1] - snap[0]
                     ref = float(ds.abs().max())
                     err = float((dx - ds).abs().max())
@@ -291,8 +300,10 @@ class NativeLenetEngine:
             us = D.allreduce_max_host(1000.0 * t0.elapsed_time(t1) / (TUNE_REPLAYS * G))
             self.tune_log[name] = round(us, 2)
             if best is None or us < best[0]:
-                best = (us, c)
-        self._set_sync(best[1] if best is not None else self._native_comm)
+                best = (us, c, push)
+        if best is None:
+            best = (0.0, self._native_comm, False)
+        self._set_sync(best[1], best[2])
         restore()
         self._tuned = True
         return steps

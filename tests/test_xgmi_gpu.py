@@ -39,14 +39,14 @@ def test_xgmi_two_ranks_bit_identical_to_buckets(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["xgmi", "xgmi2p"])
+@pytest.mark.parametrize("mode", ["xgmi", "xgmipush"])
 def test_xgmi_lenet5_two_ranks_fused_sync_matches_serial(mode):
     """The fused LeNet-5 executor over the xGMI communicator, bit-identical to
     the serial emulation of data parallelism (rank-order sum + flat SGD):
-    xgmi - the push sync in the update launch (every block pushes its
-    gradient values into the peers' receive slots, one barrier, rank-order
-    sum, replicated SGD); xgmi2p - the two-phase launch (this rank's segment
-    summed and updated, sharded momentum, then the other segments gathered)."""
+    xgmi - the two-phase launch (this rank's segment summed and updated,
+    sharded momentum, then the other segments gathered); xgmipush - the push
+    sync in the update launch (every block pushes its gradient values into the
+    peers' receive slots, one barrier, rank-order sum, replicated SGD)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), HELPER, "generic",
