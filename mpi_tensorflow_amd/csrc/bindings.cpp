@@ -494,6 +494,8 @@ PYBIND11_MODULE(_C, m) {
                   P<float>(ws), S(st));
     check_launch();
   });
+  g.def("bn_set_fused", &gops::bn_set_fused);
+  g.def("bn_fused_error", &gops::bn_fused_error);
   g.def("bn_fwd_partials", [](uintptr_t part, int nrows, uintptr_t shift, uintptr_t x, long long rows,
                               int C, uintptr_t gm, uintptr_t bt, uintptr_t res, uintptr_t y,
                               uintptr_t mean, uintptr_t rstd, float eps, float momentum, bool relu,

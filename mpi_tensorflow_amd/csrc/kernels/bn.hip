@@ -25,10 +25,12 @@
 // output (y forward, dx backward), which the next conv reads as its bf16
 // operand (forward input / dY of the filter and data gradients) instead of
 // a separate to_bf16 pass over the fp32 tensor.
+#include <algorithm>
 #include <stdexcept>
 
 #include "common.h"
 #include "ops_generic.h"
+#include "xgmi.h"  // system-scope buffer loads / stores (fused finalize hand-off)
 
 namespace gops {
 namespace bn {
@@ -373,6 +375,170 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
   }
 }
 
+// ---- finalize fused into the apply launch (bn_fwd_partials /
+// bn_bwd_partials): phase A - block b reduces the partial rows of channels
+// b, b + G, ... (finalize_kernel's order) and publishes the statistics with
+// system-scope stores; a grid-wide barrier; phase B - every block stages the
+// C channels' statistics in LDS (system-scope loads: another XCD's L2 may hold
+// the writer's line) and runs the apply loop.  One launch and one dispatch
+// instead of two per BatchNorm and direction (ResNet-18: 40 finalize launches
+// a step).  The grid is capped at FUSED_BLOCKS_PER_CU blocks a CU, well under
+// what the CUs hold next to a concurrent collective, so every block is
+// resident before any waits; the spin is bounded (a timeout sets *err).
+constexpr int FUSED_BLOCKS_PER_CU = 2;
+
+struct GridBar {
+  unsigned* cnt;  // arrivals of the current barrier (reset by the last one)
+  unsigned* gen;  // barrier generation
+  unsigned* err;  // sticky: a spin timed out
+};
+
+__device__ __forceinline__ void grid_barrier(const GridBar& b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's published stores landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned g = __hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned t = __hip_atomic_fetch_add(b.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(b.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(b.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const long long t0 = xgmi::now_ticks();
+      while (__hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        if (xgmi::now_ticks() - t0 > 200000000LL) {  // 2 s
+          __hip_atomic_fetch_or(b.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// phase A: channels blockIdx.x, + gridDim.x, ... of the conv-epilogue table
+// [2][C / 64][P][64]; stat 0 / 1 of channel c published at pub0 / pub1
+// (system scope): mean / rstd (forward) or the sums db / dg (backward)
+__device__ __forceinline__ void fused_finalize(const float* __restrict__ part, int P, int C,
+                                               long long rows, const Fin& fin, float* pub0,
+                                               float* pub1) {
+  __shared__ float red[2][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const size_t half = (size_t)C * P;
+  const xgmi::Rsrc r0 = xgmi::rsrc(pub0, 4LL * C), r1 = xgmi::rsrc(pub1, 4LL * C);
+  for (int c = blockIdx.x; c < C; c += gridDim.x) {
+    const float* pa = part + (size_t)(c >> 6) * P * 64 + (c & 63);
+    const float* pb = pa + half;
+    float a = 0.f, b = 0.f;
+#pragma unroll 4
+    for (int k = tid; k < P; k += 256) {
+      a += pa[(size_t)k * 64];
+      b += pb[(size_t)k * 64];
+    }
+    a = wave_sum(a);
+    b = wave_sum(b);
+    if (lane == 0) {
+      red[0][wave] = a;
+      red[1][wave] = b;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const float sa = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+      const float sb = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+      fin_channel(fin, c, sa, sb, rows);
+      xgmi::st_sys(r0, 4u * c, fin.bn_fwd ? fin.mean[c] : sa);
+      xgmi::st_sys(r1, 4u * c, fin.bn_fwd ? fin.rstd[c] : sb);
+    }
+    __syncthreads();
+  }
+}
+
+// phase B's statistics: C floats of each of the n arrays into LDS
+__device__ __forceinline__ void stage_stats(float* lds, const float* const* src, int n, int C) {
+  for (int j = 0; j < n; ++j) {
+    const xgmi::Rsrc r = xgmi::rsrc(src[j], 4LL * C);
+    for (int c = threadIdx.x; c < C; c += blockDim.x) lds[j * C + c] = xgmi::ld_sys(r, 4u * c);
+  }
+  __syncthreads();
+}
+
+constexpr int FUSED_MAXC = 1024;
+
+template <bool XB>
+__global__ __launch_bounds__(256) void finalize_apply_kernel(
+    const float* __restrict__ part, int P, long long rows, Fin fin, GridBar bar,
+    const void* __restrict__ x, const float* __restrict__ g, const float* __restrict__ bb,
+    const float* __restrict__ res, float* __restrict__ y, long long n4, int C, int relu,
+    uint2* __restrict__ yb) {
+  __shared__ float st[2 * FUSED_MAXC];
+  fused_finalize(part, P, C, rows, fin, fin.mean, fin.rstd);
+  grid_barrier(bar);
+  const float* srcs[2] = {fin.mean, fin.rstd};
+  stage_stats(st, srcs, 2, C);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int cq = C >> 2;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int c = (int)(i % cq) * 4;
+    const float4 v = ldx<XB>(x, 4 * i);
+    const float4 m = *reinterpret_cast<const float4*>(st + c);
+    const float4 r = *reinterpret_cast<const float4*>(st + C + c);
+    const float4 gg = ld4(g + c), b4 = ld4(bb + c);
+    float4 o;  // apply_kernel's expression forms
+    o.x = (v.x - m.x) * r.x * gg.x + b4.x;
+    o.y = (v.y - m.y) * r.y * gg.y + b4.y;
+    o.z = (v.z - m.z) * r.z * gg.z + b4.z;
+    o.w = (v.w - m.w) * r.w * gg.w + b4.w;
+    if (res) {
+      const float4 q = ld4(res + 4 * i);
+      o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+    }
+    if (relu) {
+      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+    }
+    if (y) *reinterpret_cast<float4*>(y + 4 * i) = o;
+    if (yb) yb[i] = pack4(o);
+  }
+}
+
+// backward: phase A forms db = sum dy', dg = sum dy' xhat (fin.s1 / fin.s2)
+__global__ __launch_bounds__(256) void finalize_bwd_apply_kernel(
+    const float* __restrict__ part, int P, Fin fin, GridBar bar, const void* __restrict__ x,
+    const float* __restrict__ dy, const void* __restrict__ y, const float* __restrict__ mean,
+    const float* __restrict__ rstd, const float* __restrict__ g, float* __restrict__ dx,
+    float* __restrict__ dres, long long n4, int C, long long rows, int relu,
+    uint2* __restrict__ dxb) {
+  __shared__ float st[2 * FUSED_MAXC];
+  fused_finalize(part, P, C, rows, fin, fin.s1, fin.s2);
+  grid_barrier(bar);
+  const float* srcs[2] = {fin.s1, fin.s2};
+  stage_stats(st, srcs, 2, C);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const int cq = C >> 2;
+  const float inv = 1.f / (float)rows;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int c = (int)(i % cq) * 4;
+    float4 d = ld4(dy + 4 * i);
+    if (relu) {
+      const float4 yy = ldx<true>(y, 4 * i);
+      d.x = yy.x > 0.f ? d.x : 0.f;
+      d.y = yy.y > 0.f ? d.y : 0.f;
+      d.z = yy.z > 0.f ? d.z : 0.f;
+      d.w = yy.w > 0.f ? d.w : 0.f;
+    }
+    if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
+    const float4 v = ldx<true>(x, 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
+    const float4 a = *reinterpret_cast<const float4*>(st + c);
+    const float4 b = *reinterpret_cast<const float4*>(st + C + c);
+    float4 o;  // bwd_apply_kernel's expression forms
+    o.x = gg.x * r.x * (d.x - a.x * inv - (v.x - m.x) * r.x * b.x * inv);
+    o.y = gg.y * r.y * (d.y - a.y * inv - (v.y - m.y) * r.y * b.y * inv);
+    o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
+    o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
+    if (dx) *reinterpret_cast<float4*>(dx + 4 * i) = o;
+    if (dxb) dxb[i] = pack4(o);
+  }
+}
+
 static inline int grid_elems(long long n) {
   long long b = (n + 255) / 256;
   return (int)(b > 8192 ? 8192 : (b < 1 ? 1 : b));
@@ -480,6 +646,36 @@ void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b
   }
 }
 
+// the fused launches' barrier state and grid cap (one device per process)
+static bn::GridBar g_bar{nullptr, nullptr, nullptr};
+static int g_fused_cap = 0;
+static bool g_fused_on = true;
+
+static bool fused_ready() {
+  if (!g_fused_on) return false;
+  if (!g_bar.cnt) {
+    unsigned* p = nullptr;
+    HIP_CHECK(hipMalloc(&p, 64 * sizeof(unsigned)));
+    HIP_CHECK(hipMemset(p, 0, 64 * sizeof(unsigned)));
+    HIP_CHECK(hipDeviceSynchronize());
+    g_bar = {p, p + 16, p + 32};  // separate 64-byte lines
+    int dev = 0, cus = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    g_fused_cap = cus * bn::FUSED_BLOCKS_PER_CU;
+  }
+  return g_fused_cap > 0;
+}
+
+void bn_set_fused(bool on) { g_fused_on = on; }
+unsigned bn_fused_error() {
+  if (!g_bar.err) return 0;
+  unsigned v = 0;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(&v, g_bar.err, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
+}
+
 void bn_fwd_partials(const float* part, int P, const float* shift, const void* x, long long rows,
                      int C, const float* g, const float* b, const float* res, float* y, float* mean,
                      float* rstd, float eps, float momentum, bool relu, float* rmean, float* rvar,
@@ -490,6 +686,16 @@ void bn_fwd_partials(const float* part, int P, const float* shift, const void* x
   uint2* ybv = reinterpret_cast<uint2*>(yb);
   // fp32 shift (the running mean, read by fin_channel before its update)
   const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, shift, 0};
+  if (fused_ready()) {  // finalize + apply in one launch
+    const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
+    if (xb16)
+      bn::finalize_apply_kernel<true><<<grid, 256, 0, st>>>(part, P, rows, fin, g_bar, x, g, b, res,
+                                                            y, n4, C, relu ? 1 : 0, ybv);
+    else
+      bn::finalize_apply_kernel<false><<<grid, 256, 0, st>>>(part, P, rows, fin, g_bar, x, g, b,
+                                                             res, y, n4, C, relu ? 1 : 0, ybv);
+    return;
+  }
   bn::finalize_grp64(part, P, C, rows, fin, st);
   if (xb16)
     bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
@@ -533,8 +739,15 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
   if (C % 64 != 0 || C > 1024 || P < 1 || !part || (!dx && !dxb) || (relu && !y))
     throw std::runtime_error("bn_bwd_partials: needs C % 64 == 0, C <= 1024, a dx output");
   // the dgrad epilogue's rows [2][C / 64][P][64] -> db, dg
-  bn::finalize_grp64(part, P, C, rows, sums(db, dg), st);
   const long long n4 = rows * C / 4;
+  if (fused_ready() && db && dg) {  // finalize + apply in one launch
+    const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
+    bn::finalize_bwd_apply_kernel<<<grid, 256, 0, st>>>(part, P, sums(db, dg), g_bar, x, dy, y,
+                                                        mean, rstd, g, dx, dres, n4, C, rows,
+                                                        relu ? 1 : 0, reinterpret_cast<uint2*>(dxb));
+    return;
+  }
+  bn::finalize_grp64(part, P, C, rows, sums(db, dg), st);
   bn::bwd_apply_kernel<true, true><<<bn::grid_elems(n4), 256, 0, st>>>(
       x, dy, y, mean, rstd, g, db, dg, dx, dres, n4, C, rows, relu ? 1 : 0,
       reinterpret_cast<uint2*>(dxb));

@@ -866,29 +866,41 @@ __global__ __launch_bounds__(256) void update_push_kernel(
   }
   xgmi::link_floor(S, t0, slot_bytes);
   xgmi::barrier(S, 0, e, /*release=*/false);  // the pushed values are system-scope stores
-  // every rank's values in flight, then summed in rank order and applied
+  // every rank's values of every slot in flight at once (one round trip: the
+  // SGD stores of a slot would otherwise keep the next slot's loads behind
+  // them), then summed in rank order and applied
   const xgmi::Rsrc mine = xgmi::rsrc(pa.recv[me], rbytes);
   const float lr = *lr_ptr;
+  float x[PUSH_VALS][xgmi::kMaxRanks];
+#pragma unroll
+  for (int v = 0; v < PUSH_VALS; ++v)
+#pragma unroll
+    for (int r = 0; r < xgmi::kMaxRanks; ++r)
+      if (r < n && wi[v] >= 0)
+        x[v][r] = !xgmi::contributes(S, r) ? 0.f
+                  : r == me ? gv[v]
+                            : xgmi::ld_sys(mine, (unsigned)(((long long)par * n + r) * slot_bytes +
+                                                            4LL * wi[v]));
+  float wv[PUSH_VALS], mv[PUSH_VALS];
+#pragma unroll
+  for (int v = 0; v < PUSH_VALS; ++v)
+    if (wi[v] >= 0) {
+      wv[v] = w[wi[v]];
+      mv[v] = m[wi[v]];
+    }
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int v = 0; v < PUSH_VALS; ++v) {
     if (wi[v] < 0) continue;
-    float x[xgmi::kMaxRanks];
-#pragma unroll
-    for (int r = 0; r < xgmi::kMaxRanks; ++r)
-      if (r < n)
-        x[r] = !xgmi::contributes(S, r) ? 0.f
-               : r == me ? gv[v]
-                         : xgmi::ld_sys(mine, (unsigned)(((long long)par * n + r) * slot_bytes +
-                                                         4LL * wi[v]));
-    float sum = x[0];
+    float sum = x[v][0];
 #pragma unroll
     for (int r = 1; r < xgmi::kMaxRanks; ++r)
-      if (r < n) sum += x[r];
+      if (r < n) sum += x[v][r];
     // optim::sgd_momentum_flat_kernel's expression forms (l2 = 0)
-    const float g = __builtin_fmaf(0.f, w[wi[v]], sum * pa.gscale);
-    const float mn = mu * m[wi[v]] + g;
+    const float g = __builtin_fmaf(0.f, wv[v], sum * pa.gscale);
+    const float mn = mu * mv[v] + g;
     m[wi[v]] = mn;
-    w[wi[v]] -= lr * mn;
+    w[wi[v]] = wv[v] - lr * mn;
   }
 }
 

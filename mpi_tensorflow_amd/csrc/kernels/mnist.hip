@@ -601,6 +601,8 @@ __device__ __forceinline__ void fc1_bwd_dw(int L, const float* __restrict__ a2,
 // with global_load_lds before the products - no VGPRs - so the SGD would not
 // wait for two HBM / MALL round trips after the MFMAs: the launch went 11.5
 // -> 13.4 us, r6_s1.)
+// (Also negative: the first accumulator's weights / momentum requested before
+// the products took the launch to 240 VGPRs, one wave a SIMD.)
 __device__ __forceinline__ void fc1_dw_sgd(const FcSgd& a, int L, int tid) {
   const int lane = tid & 63, r = lane & 31, wave = tid >> 6;
   float* w = a.w + (size_t)a.w1_off4 * 4;

@@ -207,6 +207,11 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
                      const float* mean, const float* rstd, const float* g, long long rows, int C,
                      bool relu, float* dg, float* db, float* dx, float* dres, hipStream_t st,
                      void* dxb);
+// bn_fwd_partials / bn_bwd_partials run the finalize inside the apply launch
+// (one launch, grid-wide barrier) unless turned off (A/B, tests); the sticky
+// error word is non-zero if a barrier spin ever timed out
+void bn_set_fused(bool on);
+unsigned bn_fused_error();
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 // bf16-twin form: xb = bf16 input, y (fp32) / yb (bf16) outputs each optional,

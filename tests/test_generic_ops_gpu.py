@@ -909,3 +909,53 @@ def test_sgd_writes_conv_weight_copies(cuda_dev, dtype):
     assert torch.equal(mom, m_ref), "momentum differs from the flat SGD"
     assert torch.equal(wc.buf, buf_ref), "weight copies differ from wcvt_batch"
     assert wc.sgd_njobs > 0 and wc.nranges > 0
+
+
+@pytest.mark.parametrize("N,H,C", [(4, 14, 64), (2, 28, 128), (8, 56, 64)])
+def test_bn_finalize_fused_into_apply(cuda_dev, N, H, C):
+    """The BatchNorm finalize (the partial-row reduction of the conv epilogue's
+    statistics -> mean / rstd, or the backward sums) runs inside the apply
+    launch behind a grid-wide barrier (bn.hip finalize_apply_kernel /
+    finalize_bwd_apply_kernel): one launch per BatchNorm and direction instead
+    of two.  Against the two-launch form on a conv -> BN(+ReLU) -> conv chain
+    (forward statistics from the first conv's epilogue, backward sums from the
+    second conv's dgrad epilogue): outputs, running statistics and every
+    gradient agree (the same sums; only the few-row reduction order of the
+    two-launch finalize64 differs), and no barrier spin timed out."""
+    from mpi_tensorflow_amd.ops import native
+
+    g = torch.Generator().manual_seed(23)
+    x = (torch.randn(N, H, H, C, generator=g)).to(torch.bfloat16).to(cuda_dev)
+    w1 = (torch.randn(3, 3, C, C, generator=g) * 0.05).to(cuda_dev)
+    w2 = (torch.randn(3, 3, C, C, generator=g) * 0.05).to(cuda_dev)
+    gam = (torch.rand(C, generator=g) + 0.5).to(cuda_dev)
+    bet = torch.randn(C, generator=g).to(cuda_dev)
+    rm0 = (torch.randn(C, generator=g) * 0.3).to(cuda_dev)
+    dy = torch.randn(N, H, H, C, generator=g).to(torch.bfloat16).to(cuda_dev)
+    ops = native().ops
+    out = []
+    Fn.set_conv_bf16(True)
+    try:
+        for fused in (False, True):
+            ops.bn_set_fused(fused)
+            routes = []
+            Fn.set_bn_route_hook(routes.append)
+            p1, p2, gp, bp = _param(w1), _param(w2), _param(gam), _param(bet)
+            rm, rv = rm0.clone(), torch.ones(C, device=cuda_dev)
+            lk = Fn.BnLink(rm)
+            y1 = Fn.conv2d(x, p1, None, 1, 1, False, out_bf16=True, bn_out=lk)
+            assert lk.fwd is not None
+            h = Fn.batchnorm(y1, gp, bp, rm, rv, True, relu=True, link=lk, twin_only=True)
+            y2 = Fn.conv2d(h, p2, None, 1, 1, False, out_bf16=True, bn_in=lk)
+            y2.backward(dy)
+            torch.cuda.synchronize()
+            assert routes == ["epilogue"], routes
+            out.append((y2.detach().float().clone(), rm.clone(), rv.clone(), p1.grad_view.clone(),
+                        p2.grad_view.clone(), gp.grad_view.clone(), bp.grad_view.clone()))
+    finally:
+        ops.bn_set_fused(True)
+        Fn.set_bn_route_hook(None)
+        Fn.set_conv_bf16(False)
+    assert ops.bn_fused_error() == 0
+    for a, b in zip(out[0], out[1]):
+        assert _rel(b, a) < 1e-4, (_rel(b, a))
