@@ -416,24 +416,25 @@ __device__ __forceinline__ void grid_barrier(const GridBar& b) {
   __syncthreads();
 }
 
-// phase A: channels blockIdx.x, + gridDim.x, ... of the conv-epilogue table
-// [2][C / 64][P][64]; stat 0 / 1 of channel c published at pub0 / pub1
+// phase A: channels blockIdx.x, + gridDim.x, ... of the partial table - the
+// conv-epilogue layout [2][C / 64][P][64] (grp64), or partial_kernel's
+// channel-major [2][C][P]; stat 0 / 1 of channel c published at pub0 / pub1
 // (system scope): mean / rstd (forward) or the sums db / dg (backward)
 __device__ __forceinline__ void fused_finalize(const float* __restrict__ part, int P, int C,
                                                long long rows, const Fin& fin, float* pub0,
-                                               float* pub1) {
+                                               float* pub1, int grp64) {
   __shared__ float red[2][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const size_t half = (size_t)C * P;
+  const size_t half = (size_t)C * P, step = grp64 ? 64 : 1;
   const xgmi::Rsrc r0 = xgmi::rsrc(pub0, 4LL * C), r1 = xgmi::rsrc(pub1, 4LL * C);
   for (int c = blockIdx.x; c < C; c += gridDim.x) {
-    const float* pa = part + (size_t)(c >> 6) * P * 64 + (c & 63);
+    const float* pa = part + (grp64 ? (size_t)(c >> 6) * P * 64 + (c & 63) : (size_t)c * P);
     const float* pb = pa + half;
     float a = 0.f, b = 0.f;
 #pragma unroll 4
     for (int k = tid; k < P; k += 256) {
-      a += pa[(size_t)k * 64];
-      b += pb[(size_t)k * 64];
+      a += pa[(size_t)k * step];
+      b += pb[(size_t)k * step];
     }
     a = wave_sum(a);
     b = wave_sum(b);
@@ -466,12 +467,12 @@ constexpr int FUSED_MAXC = 1024;
 
 template <bool XB>
 __global__ __launch_bounds__(256) void finalize_apply_kernel(
-    const float* __restrict__ part, int P, long long rows, Fin fin, GridBar bar,
+    const float* __restrict__ part, int P, int grp64, long long rows, Fin fin, GridBar bar,
     const void* __restrict__ x, const float* __restrict__ g, const float* __restrict__ bb,
     const float* __restrict__ res, float* __restrict__ y, long long n4, int C, int relu,
     uint2* __restrict__ yb) {
   __shared__ float st[2 * FUSED_MAXC];
-  fused_finalize(part, P, C, rows, fin, fin.mean, fin.rstd);
+  fused_finalize(part, P, C, rows, fin, fin.mean, fin.rstd, grp64);
   grid_barrier(bar);
   const float* srcs[2] = {fin.mean, fin.rstd};
   stage_stats(st, srcs, 2, C);
@@ -501,14 +502,15 @@ __global__ __launch_bounds__(256) void finalize_apply_kernel(
 }
 
 // backward: phase A forms db = sum dy', dg = sum dy' xhat (fin.s1 / fin.s2)
+template <bool XB, bool YB>
 __global__ __launch_bounds__(256) void finalize_bwd_apply_kernel(
-    const float* __restrict__ part, int P, Fin fin, GridBar bar, const void* __restrict__ x,
-    const float* __restrict__ dy, const void* __restrict__ y, const float* __restrict__ mean,
-    const float* __restrict__ rstd, const float* __restrict__ g, float* __restrict__ dx,
-    float* __restrict__ dres, long long n4, int C, long long rows, int relu,
-    uint2* __restrict__ dxb) {
+    const float* __restrict__ part, int P, int grp64, Fin fin, GridBar bar,
+    const void* __restrict__ x, const float* __restrict__ dy, const void* __restrict__ y,
+    const float* __restrict__ mean, const float* __restrict__ rstd, const float* __restrict__ g,
+    float* __restrict__ dx, float* __restrict__ dres, long long n4, int C, long long rows,
+    int relu, uint2* __restrict__ dxb) {
   __shared__ float st[2 * FUSED_MAXC];
-  fused_finalize(part, P, C, rows, fin, fin.s1, fin.s2);
+  fused_finalize(part, P, C, rows, fin, fin.s1, fin.s2, grp64);
   grid_barrier(bar);
   const float* srcs[2] = {fin.s1, fin.s2};
   stage_stats(st, srcs, 2, C);
@@ -519,14 +521,14 @@ __global__ __launch_bounds__(256) void finalize_bwd_apply_kernel(
     const int c = (int)(i % cq) * 4;
     float4 d = ld4(dy + 4 * i);
     if (relu) {
-      const float4 yy = ldx<true>(y, 4 * i);
+      const float4 yy = ldx<YB>(y, 4 * i);
       d.x = yy.x > 0.f ? d.x : 0.f;
       d.y = yy.y > 0.f ? d.y : 0.f;
       d.z = yy.z > 0.f ? d.z : 0.f;
       d.w = yy.w > 0.f ? d.w : 0.f;
     }
     if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
-    const float4 v = ldx<true>(x, 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
+    const float4 v = ldx<XB>(x, 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
     const float4 a = *reinterpret_cast<const float4*>(st + c);
     const float4 b = *reinterpret_cast<const float4*>(st + C + c);
     float4 o;  // bwd_apply_kernel's expression forms
@@ -571,7 +573,7 @@ long long chan_reduce_ws_floats(long long rows, int C) {
 template <bool XB, bool YB>
 static void run_partials_t(int mode, const void* a, const float* b, const void* y,
                            const void* mean, const float* rstd, int relu, long long rows, int C,
-                           float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
+                           float* ws, int nb, const bn::Fin& fin, hipStream_t st, bool finalize) {
   const int rpb = (int)((rows + nb - 1) / nb);
   switch (mode) {
     case bn::SUM_SQ:
@@ -583,20 +585,22 @@ static void run_partials_t(int mode, const void* a, const float* b, const void* 
     default:
       bn::partial_kernel<bn::BN_BWD, XB, YB><<<nb, bn::PT, 0, st>>>(a, b, y, mean, rstd, relu, rows, C, rpb, ws);
   }
-  bn::finalize_kernel<<<C, 256, 0, st>>>(ws, nb, C, rows, fin, 0);
+  if (finalize) bn::finalize_kernel<<<C, 256, 0, st>>>(ws, nb, C, rows, fin, 0);
 }
 
+// finalize = false: only the partial rows (the caller's fused launch finalizes)
 static void run_partials(int mode, const void* a, bool ab16, const float* b, const void* y,
                          bool yb16, const void* mean, const float* rstd, int relu, long long rows,
-                         int C, float* ws, int nb, const bn::Fin& fin, hipStream_t st) {
+                         int C, float* ws, int nb, const bn::Fin& fin, hipStream_t st,
+                         bool finalize = true) {
   if (ab16 && yb16)
-    run_partials_t<true, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+    run_partials_t<true, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st, finalize);
   else if (ab16)
-    run_partials_t<true, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+    run_partials_t<true, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st, finalize);
   else if (yb16)
-    run_partials_t<false, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+    run_partials_t<false, true>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st, finalize);
   else
-    run_partials_t<false, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st);
+    run_partials_t<false, false>(mode, a, b, y, mean, rstd, relu, rows, C, ws, nb, fin, st, finalize);
 }
 
 static bn::Fin sums(float* s1, float* s2) {
@@ -614,35 +618,6 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
     const int rpb = (int)((rows + nb - 1) / nb);
     bn::partial1_kernel<<<nb, 256, 0, st>>>(a, b, mode, rows, C, rpb, ws);
     bn::finalize_kernel<<<C, 256, 0, st>>>(ws, nb, C, rows, sums(s1, s2), 0);
-  }
-}
-
-void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
-            const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
-            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
-            void* yb, bool xb16) {
-  if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_fwd: needs C % 4 == 0, C <= 1024");
-  const long long n4 = rows * C / 4;
-  uint2* ybv = reinterpret_cast<uint2*>(yb);
-  if (training) {
-    const int nb = bn::nblocks(rows, C);
-    // shift K = row 0 of x (passed as the partials' `mean`)
-    const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x, xb16 ? 1 : 0};
-    run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, false, x, nullptr, 0, rows, C, ws, nb, fin,
-                 st);
-    if (xb16)
-      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
-                                                                 relu ? 1 : 0, 0, eps, ybv);
-    else
-      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4,
-                                                                  C, relu ? 1 : 0, 0, eps, ybv);
-  } else {
-    if (xb16)
-      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
-                                                                 C, relu ? 1 : 0, 1, eps, ybv);
-    else
-      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
-                                                                  C, relu ? 1 : 0, 1, eps, ybv);
   }
 }
 
@@ -676,6 +651,47 @@ unsigned bn_fused_error() {
   return v;
 }
 
+void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
+            const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
+            float momentum, bool relu, bool training, float* rmean, float* rvar, hipStream_t st,
+            void* yb, bool xb16) {
+  if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_fwd: needs C % 4 == 0, C <= 1024");
+  const long long n4 = rows * C / 4;
+  uint2* ybv = reinterpret_cast<uint2*>(yb);
+  if (training) {
+    const int nb = bn::nblocks(rows, C);
+    // shift K = row 0 of x (passed as the partials' `mean`)
+    const bn::Fin fin{nullptr, nullptr, 1, eps, momentum, mean, rstd, rmean, rvar, x, xb16 ? 1 : 0};
+    if (fused_ready()) {  // statistics pass, then finalize + apply in one launch
+      run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, false, x, nullptr, 0, rows, C, ws, nb,
+                   fin, st, /*finalize=*/false);
+      const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
+      if (xb16)
+        bn::finalize_apply_kernel<true><<<grid, 256, 0, st>>>(ws, nb, 0, rows, fin, g_bar, x, g, b,
+                                                              res, y, n4, C, relu ? 1 : 0, ybv);
+      else
+        bn::finalize_apply_kernel<false><<<grid, 256, 0, st>>>(ws, nb, 0, rows, fin, g_bar, x, g, b,
+                                                               res, y, n4, C, relu ? 1 : 0, ybv);
+      return;
+    }
+    run_partials(bn::SUM_SQ, x, xb16, nullptr, nullptr, false, x, nullptr, 0, rows, C, ws, nb, fin,
+                 st);
+    if (xb16)
+      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4, C,
+                                                                 relu ? 1 : 0, 0, eps, ybv);
+    else
+      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, mean, rstd, g, b, res, y, n4,
+                                                                  C, relu ? 1 : 0, 0, eps, ybv);
+  } else {
+    if (xb16)
+      bn::apply_kernel<true><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
+                                                                 C, relu ? 1 : 0, 1, eps, ybv);
+    else
+      bn::apply_kernel<false><<<bn::grid_elems(n4), 256, 0, st>>>(x, rmean, rvar, g, b, res, y, n4,
+                                                                  C, relu ? 1 : 0, 1, eps, ybv);
+  }
+}
+
 void bn_fwd_partials(const float* part, int P, const float* shift, const void* x, long long rows,
                      int C, const float* g, const float* b, const float* res, float* y, float* mean,
                      float* rstd, float eps, float momentum, bool relu, float* rmean, float* rvar,
@@ -689,10 +705,10 @@ void bn_fwd_partials(const float* part, int P, const float* shift, const void* x
   if (fused_ready()) {  // finalize + apply in one launch
     const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
     if (xb16)
-      bn::finalize_apply_kernel<true><<<grid, 256, 0, st>>>(part, P, rows, fin, g_bar, x, g, b, res,
-                                                            y, n4, C, relu ? 1 : 0, ybv);
+      bn::finalize_apply_kernel<true><<<grid, 256, 0, st>>>(part, P, 1, rows, fin, g_bar, x, g, b,
+                                                            res, y, n4, C, relu ? 1 : 0, ybv);
     else
-      bn::finalize_apply_kernel<false><<<grid, 256, 0, st>>>(part, P, rows, fin, g_bar, x, g, b,
+      bn::finalize_apply_kernel<false><<<grid, 256, 0, st>>>(part, P, 1, rows, fin, g_bar, x, g, b,
                                                              res, y, n4, C, relu ? 1 : 0, ybv);
     return;
   }
@@ -711,12 +727,30 @@ void bn_bwd(const void* x, const float* dy, const void* y, const float* mean, co
   if (C % 4 != 0 || C > 1024) throw std::runtime_error("bn_bwd: needs C % 4 == 0, C <= 1024");
   if (!dx && !dxb) throw std::runtime_error("bn_bwd: no dx output");
   const int nb = bn::nblocks(rows, C);
-  // db = sum dy', dg = sum dy' xhat
-  run_partials(bn::BN_BWD, x, xb16, dy, y, yb16, mean, rstd, relu ? 1 : 0, rows, C, ws, nb,
-               sums(db, dg), st);
   const long long n4 = rows * C / 4;
   uint2* dxbv = reinterpret_cast<uint2*>(dxb);
   const int rl = relu ? 1 : 0;
+  // db = sum dy', dg = sum dy' xhat
+  const bool fused = fused_ready() && db && dg;
+  run_partials(bn::BN_BWD, x, xb16, dy, y, yb16, mean, rstd, relu ? 1 : 0, rows, C, ws, nb,
+               sums(db, dg), st, /*finalize=*/!fused);
+  if (fused) {  // finalize + apply in one launch
+    const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
+#define FBWD(XB_, YB_)                                                                          \
+  bn::finalize_bwd_apply_kernel<XB_, YB_><<<grid, 256, 0, st>>>(ws, nb, 0, sums(db, dg), g_bar, x, \
+                                                                dy, y, mean, rstd, g, dx, dres, n4, \
+                                                                C, rows, rl, dxbv)
+    if (xb16 && yb16)
+      FBWD(true, true);
+    else if (xb16)
+      FBWD(true, false);
+    else if (yb16)
+      FBWD(false, true);
+    else
+      FBWD(false, false);
+#undef FBWD
+    return;
+  }
   const int gr = bn::grid_elems(n4);
 #define BWD_APPLY(XB_, YB_)                                                               \
   bn::bwd_apply_kernel<XB_, YB_><<<gr, 256, 0, st>>>(x, dy, y, mean, rstd, g, db, dg, dx, dres, \
@@ -742,9 +776,9 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
   const long long n4 = rows * C / 4;
   if (fused_ready() && db && dg) {  // finalize + apply in one launch
     const int grid = std::min(bn::grid_elems(n4), g_fused_cap);
-    bn::finalize_bwd_apply_kernel<<<grid, 256, 0, st>>>(part, P, sums(db, dg), g_bar, x, dy, y,
-                                                        mean, rstd, g, dx, dres, n4, C, rows,
-                                                        relu ? 1 : 0, reinterpret_cast<uint2*>(dxb));
+    bn::finalize_bwd_apply_kernel<true, true><<<grid, 256, 0, st>>>(
+        part, P, 1, sums(db, dg), g_bar, x, dy, y, mean, rstd, g, dx, dres, n4, C, rows,
+        relu ? 1 : 0, reinterpret_cast<uint2*>(dxb));
     return;
   }
   bn::finalize_grp64(part, P, C, rows, sums(db, dg), st);
