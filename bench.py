@@ -70,6 +70,11 @@ def parse(argv=None):
                          "GPUs; on one node the xGMI peer-to-peer schedule is also tuned)")
     ap.add_argument("--no-xgmi", action="store_true",
                     help="comm auto: do not set up the xGMI peer-to-peer communicator")
+    ap.add_argument("--bn-fused", choices=("on", "off"), default=None,
+                    help="BatchNorm finalize fused into the apply launch (grid barrier) or "
+                         "the separate finalize launch (A/B; default: the library's)")
+    ap.add_argument("--bn-fused-bpc", type=int, default=None,
+                    help="fused BatchNorm grid: blocks a CU (1..8)")
     ap.add_argument("--xgmi-push", action="store_true",
                     help="lenet5 over xGMI: the push sync fused into the update launch instead "
                          "of the two-phase all-reduce + SGD launch (comm auto tunes both)")
@@ -210,6 +215,12 @@ def main(argv=None) -> int:
     device = D.resolve_device("auto")
     di = D.init(str(device))
     N = di.world
+    if device.type == "cuda" and (a.bn_fused is not None or a.bn_fused_bpc is not None):
+        from mpi_tensorflow_amd.ops import native as _native
+        if a.bn_fused is not None:
+            _native().ops.bn_set_fused(a.bn_fused == "on")
+        if a.bn_fused_bpc is not None:
+            _native().ops.bn_set_fused_blocks_per_cu(a.bn_fused_bpc)
     maybe_fail("after_init", di.rank)
     # the watchdog exists before the communicator: start-up collectives
     # (communicator init, the engines' connection setup) are guarded too

@@ -206,6 +206,9 @@ PYBIND11_MODULE(_C, m) {
     mnist::set_conv2_bwd_wino_prof(reinterpret_cast<unsigned long long*>(p));
   });
   k.def("conv2_wino_filter_groups", &mnist::conv2_wino_filter_groups);
+  k.def("set_sgd_prof", [](uintptr_t p) {
+    mnist::set_sgd_prof(reinterpret_cast<unsigned long long*>(p));
+  });
   k.def("set_conv2_bwd_prof_bf16", [](uintptr_t p) {
     mnist16::set_conv2_bwd_prof(reinterpret_cast<unsigned long long*>(p));
   });
@@ -496,6 +499,9 @@ PYBIND11_MODULE(_C, m) {
   });
   g.def("bn_set_fused", &gops::bn_set_fused);
   g.def("bn_fused_error", &gops::bn_fused_error);
+  g.def("bn_set_fused_blocks_per_cu", &gops::bn_set_fused_blocks_per_cu);
+  g.def("gsync_barrier_us", &gops::gsync_barrier_us);
+  g.def("bn_fused_grid_cap", &gops::bn_fused_grid_cap);
   g.def("bn_fwd_partials", [](uintptr_t part, int nrows, uintptr_t shift, uintptr_t x, long long rows,
                               int C, uintptr_t gm, uintptr_t bt, uintptr_t res, uintptr_t y,
                               uintptr_t mean, uintptr_t rstd, float eps, float momentum, bool relu,

@@ -30,7 +30,7 @@
 
 #include "common.h"
 #include "ops_generic.h"
-#include "xgmi.h"  // system-scope buffer loads / stores (fused finalize hand-off)
+#include "grid_sync.h"  // grid barrier + system-scope hand-off (fused finalize)
 
 namespace gops {
 namespace bn {
@@ -385,36 +385,11 @@ __global__ __launch_bounds__(256) void bwd_apply_kernel(
 // a step).  The grid is capped at FUSED_BLOCKS_PER_CU blocks a CU, well under
 // what the CUs hold next to a concurrent collective, so every block is
 // resident before any waits; the spin is bounded (a timeout sets *err).
-constexpr int FUSED_BLOCKS_PER_CU = 2;
+constexpr int FUSED_BLOCKS_PER_CU = 2;  // default; bn_set_fused_blocks_per_cu
+constexpr int FU = 4;
 
-struct GridBar {
-  unsigned* cnt;  // arrivals of the current barrier (reset by the last one)
-  unsigned* gen;  // barrier generation
-  unsigned* err;  // sticky: a spin timed out
-};
-
-__device__ __forceinline__ void grid_barrier(const GridBar& b) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's published stores landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned g = __hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned t = __hip_atomic_fetch_add(b.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == gridDim.x - 1) {
-      __hip_atomic_store(b.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(b.gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      const long long t0 = xgmi::now_ticks();
-      while (__hip_atomic_load(b.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-        if (xgmi::now_ticks() - t0 > 200000000LL) {  // 2 s
-          __hip_atomic_fetch_or(b.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-  }
-  __syncthreads();
-}
+using gsync::GridBar;
+using gsync::grid_barrier;
 
 // phase A: channels blockIdx.x, + gridDim.x, ... of the partial table - the
 // conv-epilogue layout [2][C / 64][P][64] (grp64), or partial_kernel's
@@ -478,26 +453,42 @@ __global__ __launch_bounds__(256) void finalize_apply_kernel(
   stage_stats(st, srcs, 2, C);
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int cq = C >> 2;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int c = (int)(i % cq) * 4;
-    const float4 v = ldx<XB>(x, 4 * i);
-    const float4 m = *reinterpret_cast<const float4*>(st + c);
-    const float4 r = *reinterpret_cast<const float4*>(st + C + c);
-    const float4 gg = ld4(g + c), b4 = ld4(bb + c);
-    float4 o;  // apply_kernel's expression forms
-    o.x = (v.x - m.x) * r.x * gg.x + b4.x;
-    o.y = (v.y - m.y) * r.y * gg.y + b4.y;
-    o.z = (v.z - m.z) * r.z * gg.z + b4.z;
-    o.w = (v.w - m.w) * r.w * gg.w + b4.w;
-    if (res) {
-      const float4 q = ld4(res + 4 * i);
-      o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+  // FU elements a thread in flight: the grid is a few blocks a CU, so each
+  // thread's loads are batched ahead of its math (one load at a time left
+  // HBM latency exposed: 28.5 us against apply_kernel's 7.6)
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4;
+       i0 += FU * stride) {
+    float4 v[FU], q[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i < n4) {
+        v[u] = ldx<XB>(x, 4 * i);
+        if (res) q[u] = ld4(res + 4 * i);
+      }
     }
-    if (relu) {
-      o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n4) break;
+      const int c = (int)(i % cq) * 4;
+      const float4 m = *reinterpret_cast<const float4*>(st + c);
+      const float4 r = *reinterpret_cast<const float4*>(st + C + c);
+      const float4 gg = ld4(g + c), b4 = ld4(bb + c);
+      float4 o;  // apply_kernel's expression forms
+      o.x = (v[u].x - m.x) * r.x * gg.x + b4.x;
+      o.y = (v[u].y - m.y) * r.y * gg.y + b4.y;
+      o.z = (v[u].z - m.z) * r.z * gg.z + b4.z;
+      o.w = (v[u].w - m.w) * r.w * gg.w + b4.w;
+      if (res) {
+        o.x += q[u].x; o.y += q[u].y; o.z += q[u].z; o.w += q[u].w;
+      }
+      if (relu) {
+        o.x = fmaxf(o.x, 0.f); o.y = fmaxf(o.y, 0.f); o.z = fmaxf(o.z, 0.f); o.w = fmaxf(o.w, 0.f);
+      }
+      if (y) *reinterpret_cast<float4*>(y + 4 * i) = o;
+      if (yb) yb[i] = pack4(o);
     }
-    if (y) *reinterpret_cast<float4*>(y + 4 * i) = o;
-    if (yb) yb[i] = pack4(o);
   }
 }
 
@@ -517,28 +508,48 @@ __global__ __launch_bounds__(256) void finalize_bwd_apply_kernel(
   const long long stride = (long long)gridDim.x * blockDim.x;
   const int cq = C >> 2;
   const float inv = 1.f / (float)rows;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int c = (int)(i % cq) * 4;
-    float4 d = ld4(dy + 4 * i);
-    if (relu) {
-      const float4 yy = ldx<YB>(y, 4 * i);
-      d.x = yy.x > 0.f ? d.x : 0.f;
-      d.y = yy.y > 0.f ? d.y : 0.f;
-      d.z = yy.z > 0.f ? d.z : 0.f;
-      d.w = yy.w > 0.f ? d.w : 0.f;
+  for (long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4;
+       i0 += FU * stride) {  // FU elements in flight (finalize_apply_kernel)
+    float4 dd[FU], yv[FU], xv[FU];
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i < n4) {
+        dd[u] = ld4(dy + 4 * i);
+        if (relu) yv[u] = ldx<YB>(y, 4 * i);
+        xv[u] = ldx<XB>(x, 4 * i);
+      }
     }
-    if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
-    const float4 v = ldx<XB>(x, 4 * i), m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
-    const float4 a = *reinterpret_cast<const float4*>(st + c);
-    const float4 b = *reinterpret_cast<const float4*>(st + C + c);
-    float4 o;  // bwd_apply_kernel's expression forms
-    o.x = gg.x * r.x * (d.x - a.x * inv - (v.x - m.x) * r.x * b.x * inv);
-    o.y = gg.y * r.y * (d.y - a.y * inv - (v.y - m.y) * r.y * b.y * inv);
-    o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
-    o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
-    if (dx) *reinterpret_cast<float4*>(dx + 4 * i) = o;
-    if (dxb) dxb[i] = pack4(o);
+#pragma unroll
+    for (int u = 0; u < FU; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= n4) break;
+      const int c = (int)(i % cq) * 4;
+      float4 d = dd[u];
+      if (relu) {
+        d.x = yv[u].x > 0.f ? d.x : 0.f;
+        d.y = yv[u].y > 0.f ? d.y : 0.f;
+        d.z = yv[u].z > 0.f ? d.z : 0.f;
+        d.w = yv[u].w > 0.f ? d.w : 0.f;
+      }
+      if (dres) *reinterpret_cast<float4*>(dres + 4 * i) = d;
+      const float4 v = xv[u], m = ld4(mean + c), r = ld4(rstd + c), gg = ld4(g + c);
+      const float4 a = *reinterpret_cast<const float4*>(st + c);
+      const float4 b = *reinterpret_cast<const float4*>(st + C + c);
+      float4 o;  // bwd_apply_kernel's expression forms
+      o.x = gg.x * r.x * (d.x - a.x * inv - (v.x - m.x) * r.x * b.x * inv);
+      o.y = gg.y * r.y * (d.y - a.y * inv - (v.y - m.y) * r.y * b.y * inv);
+      o.z = gg.z * r.z * (d.z - a.z * inv - (v.z - m.z) * r.z * b.z * inv);
+      o.w = gg.w * r.w * (d.w - a.w * inv - (v.w - m.w) * r.w * b.w * inv);
+      if (dx) *reinterpret_cast<float4*>(dx + 4 * i) = o;
+      if (dxb) dxb[i] = pack4(o);
+    }
   }
+}
+
+// a grid of back-to-back barriers (gsync_barrier_us: the cost of one)
+__global__ __launch_bounds__(256) void barrier_lab_kernel(GridBar bar, int iters) {
+  for (int k = 0; k < iters; ++k) grid_barrier(bar);
 }
 
 static inline int grid_elems(long long n) {
@@ -624,32 +635,66 @@ void chan_reduce(const float* a, const float* b, long long rows, int C, float* s
 // the fused launches' barrier state and grid cap (one device per process)
 static bn::GridBar g_bar{nullptr, nullptr, nullptr};
 static int g_fused_cap = 0;
-static bool g_fused_on = true;
+static bool g_fused_on = false;  // opt-in: PERF_NOTES round 6
+
+static int g_bpc = bn::FUSED_BLOCKS_PER_CU;
+
+// blocks a CU holds of every fused kernel (VGPRs: the backward ones hold 3)
+static int fused_occupancy() {
+  int lo = 8;
+  auto occ = [&](const void* f) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, f, 256, 0) != hipSuccess) n = 0;
+    lo = std::min(lo, n);
+  };
+  occ(reinterpret_cast<const void*>(&bn::finalize_apply_kernel<true>));
+  occ(reinterpret_cast<const void*>(&bn::finalize_apply_kernel<false>));
+  occ(reinterpret_cast<const void*>(&bn::finalize_bwd_apply_kernel<true, true>));
+  occ(reinterpret_cast<const void*>(&bn::finalize_bwd_apply_kernel<true, false>));
+  occ(reinterpret_cast<const void*>(&bn::finalize_bwd_apply_kernel<false, true>));
+  occ(reinterpret_cast<const void*>(&bn::finalize_bwd_apply_kernel<false, false>));
+  return lo;
+}
 
 static bool fused_ready() {
   if (!g_fused_on) return false;
   if (!g_bar.cnt) {
-    unsigned* p = nullptr;
-    HIP_CHECK(hipMalloc(&p, 64 * sizeof(unsigned)));
-    HIP_CHECK(hipMemset(p, 0, 64 * sizeof(unsigned)));
-    HIP_CHECK(hipDeviceSynchronize());
-    g_bar = {p, p + 16, p + 32};  // separate 64-byte lines
-    int dev = 0, cus = 0;
-    HIP_CHECK(hipGetDevice(&dev));
-    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    g_fused_cap = cus * bn::FUSED_BLOCKS_PER_CU;
+    g_bar = gsync::tu_bar();
+    g_fused_cap = gsync::cu_count() * std::min(g_bpc, fused_occupancy());
   }
   return g_fused_cap > 0;
 }
 
 void bn_set_fused(bool on) { g_fused_on = on; }
-unsigned bn_fused_error() {
-  if (!g_bar.err) return 0;
-  unsigned v = 0;
-  HIP_CHECK(hipDeviceSynchronize());
-  HIP_CHECK(hipMemcpy(&v, g_bar.err, sizeof(v), hipMemcpyDeviceToHost));
-  return v;
+void bn_set_fused_blocks_per_cu(int bpc) {
+  if (bpc < 1 || bpc > 8) throw std::runtime_error("bn_set_fused_blocks_per_cu: 1..8");
+  g_bpc = bpc;
+  g_fused_cap = g_bar.cnt ? gsync::cu_count() * std::min(g_bpc, fused_occupancy()) : 0;
 }
+int bn_fused_grid_cap() { fused_ready(); return g_fused_cap; }
+
+float gsync_barrier_us(int blocks, int iters) {
+  int occ = 0;
+  HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &occ, reinterpret_cast<const void*>(&bn::barrier_lab_kernel), 256, 0));
+  if (blocks < 1 || blocks > gsync::cu_count() * occ || iters < 1)
+    throw std::runtime_error("gsync_barrier_us: 1 <= blocks <= resident capacity");
+  const bn::GridBar bar = gsync::tu_bar();
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  bn::barrier_lab_kernel<<<blocks, 256>>>(bar, 1);  // warm
+  HIP_CHECK(hipEventRecord(e0, nullptr));
+  bn::barrier_lab_kernel<<<blocks, 256>>>(bar, iters);
+  HIP_CHECK(hipEventRecord(e1, nullptr));
+  HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  return 1000.f * ms / (float)iters;
+}
+unsigned bn_fused_error() { return g_bar.cnt ? gsync::bar_error(g_bar) : 0u; }
 
 void bn_fwd(const void* x, long long rows, int C, const float* g, const float* b,
             const float* res, float* y, float* mean, float* rstd, float* ws, float eps,
@@ -788,3 +833,18 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
 }
 
 }  // namespace gops
+
+namespace gsync {
+int cu_count() {
+  int dev = 0, cus = 0;
+  HIP_CHECK(hipGetDevice(&dev));
+  HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  return cus;
+}
+unsigned bar_error(const GridBar& b) {
+  unsigned v = 0;
+  HIP_CHECK(hipDeviceSynchronize());
+  HIP_CHECK(hipMemcpy(&v, b.err, sizeof(v), hipMemcpyDeviceToHost));
+  return v;
+}
+}  // namespace gsync

@@ -207,6 +207,8 @@ struct SgdStepArgs {
   uint16_t* w2b = nullptr;
 };
 void launch_sgd_step(const SgdStepArgs& a, hipStream_t s);
+// lab: per-block [start, end] clock pairs of later SGD launches (nullptr: off)
+void set_sgd_prof(unsigned long long* p);
 // World > 1 over the xGMI peer-to-peer communicator (MnistExecutor SCHED_XGMI,
 // mnist.hip xgmi_step_kernel): ONE launch on the compute stream does the whole
 // gradient sync and the update.

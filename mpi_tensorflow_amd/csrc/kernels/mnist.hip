@@ -2698,6 +2698,7 @@ struct SgdFinArgs {
   // (mnist_bf16.h layouts) for the NEXT step's fused forward and bwd-data
   __bf16* w2t;
   __bf16* w2b;
+  unsigned long long* prof;  // lab: per-block start / end clock (set_sgd_prof)
 };
 
 __device__ __forceinline__ void sgd_elem(float* w, float* m, float g, float lr, float mu) {
@@ -2779,8 +2780,24 @@ __device__ void sgd_conv2_flat(const SgdFinArgs& a, int blk, float lr) {
   }
 }
 
+__device__ __forceinline__ void sgd_finalize_body(const SgdFinArgs& a, float* tile);
+
 __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
   __shared__ float tile[SHADOW_SMEM_FLOATS];  // fc1 shadow tiles (bf16, world > 1)
+  if (!a.prof) {
+    sgd_finalize_body(a, tile);
+    return;
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  sgd_finalize_body(a, tile);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    a.prof[2 * blockIdx.x] = t0;
+    a.prof[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+__device__ __forceinline__ void sgd_finalize_body(const SgdFinArgs& a, float* tile) {
   const float lr = *a.lr;
   const int tid = threadIdx.x;
   int blk = blockIdx.x;
@@ -2860,6 +2877,8 @@ __global__ __launch_bounds__(256) void sgd_finalize_kernel(const SgdFinArgs a) {
   }
 }
 
+static unsigned long long* g_sgd_prof = nullptr;
+
 void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
   const SgdStepArgs& p = s_;
   if ((p.w2tb == nullptr) != (p.w2b == nullptr) || (p.w2tb && p.wino_u))
@@ -2905,8 +2924,11 @@ void launch_sgd_step(const SgdStepArgs& s_, hipStream_t s) {
   const int conv_blocks = p.conv ? (p.wino_u ? 128 : 50) + 16 + cdiv(832, 16) : 0;
   const int grid = (a.fc.a2 ? FC1BWD_DW_BLOCKS : 0) + a.fc.nblk + conv_blocks;
   if (grid == 0) throw std::runtime_error("sgd_step: nothing to update");
+  a.prof = g_sgd_prof;
   sgd_finalize_kernel<<<grid, 256, 0, s>>>(a);
 }
+
+void set_sgd_prof(unsigned long long* p) { g_sgd_prof = p; }
 
 // ------------------------------------------- xGMI peer-to-peer step sync ----
 // (mnist.h XgmiStepArgs).  Two block roles: [0, nfc) FC segment slices (slice

@@ -212,6 +212,10 @@ void bn_bwd_partials(const float* part, int P, const void* x, const float* dy, c
 // error word is non-zero if a barrier spin ever timed out
 void bn_set_fused(bool on);
 unsigned bn_fused_error();
+void bn_set_fused_blocks_per_cu(int bpc);
+int bn_fused_grid_cap();  // blocks of a fused launch (0: fused off)
+// microseconds per grid-wide barrier (grid_sync.h) of `blocks` 256-thread blocks
+float gsync_barrier_us(int blocks, int iters);
 void maxpool_fwd(const PoolShape& p, const float* x, float* y, int* arg, hipStream_t st);
 void maxpool_bwd(const PoolShape& p, const float* dy, const int* arg, float* dx, hipStream_t st);
 // bf16-twin form: xb = bf16 input, y (fp32) / yb (bf16) outputs each optional,

@@ -188,9 +188,13 @@ class XgmiDeviceComm(DeviceComm):
     """xGMI peer-to-peer communicator (csrc/xgmi_comm.h) of the ranks of one
     node.  Creation is collective over the gloo group: every rank makes its
     uncached flag array, the IPC handles are all-gathered and every rank maps
-    every peer's; each step is voted, so a rank that fails makes every rank
-    raise instead of hanging.  Buffers the kernels read remotely must be
-    registered (collective, same order on every rank): `register(t, ...)`.
+    every peer's; each set-up step is voted, so a rank that fails makes every
+    rank raise instead of hanging.  At run time the kernels never hang (a
+    missing peer sets the sticky error word, `error()`); the entry points vote
+    on it at their sync points (parallel/setup.py check_health) and stop on
+    every rank.  Buffers the kernels read remotely must be registered
+    (collective, same order on every rank): `register(t, ...)`.  Before any
+    schedule may use it, `xgmi_exactness_check` gates it on exact sums.
 
     `emulated(n, lat_us, link_gbps)`: ONE process stands in for n ranks on one
     GPU (local stand-in peer buffers; each phase held for the time its bytes

@@ -936,8 +936,9 @@ def test_bn_finalize_fused_into_apply(cuda_dev, N, H, C):
     out = []
     Fn.set_conv_bf16(True)
     try:
-        for fused in (False, True):
+        for fused, bpc in ((False, 2), (True, 2), (True, 8)):
             ops.bn_set_fused(fused)
+            ops.bn_set_fused_blocks_per_cu(bpc)
             routes = []
             Fn.set_bn_route_hook(routes.append)
             p1, p2, gp, bp = _param(w1), _param(w2), _param(gam), _param(bet)
@@ -953,9 +954,28 @@ def test_bn_finalize_fused_into_apply(cuda_dev, N, H, C):
             out.append((y2.detach().float().clone(), rm.clone(), rv.clone(), p1.grad_view.clone(),
                         p2.grad_view.clone(), gp.grad_view.clone(), bp.grad_view.clone()))
     finally:
-        ops.bn_set_fused(True)
+        ops.bn_set_fused(False)
+        ops.bn_set_fused_blocks_per_cu(2)
         Fn.set_bn_route_hook(None)
         Fn.set_conv_bf16(False)
     assert ops.bn_fused_error() == 0
+    for a, b in zip(out[1], out[2]):  # the grid cap changes nothing but the launch
+        assert torch.equal(a, b)
     for a, b in zip(out[0], out[1]):
         assert _rel(b, a) < 1e-4, (_rel(b, a))
+
+
+@pytest.mark.gpu
+def test_grid_barrier_cost(cuda_dev):
+    """grid_sync.h's barrier at 224 blocks (the MNIST FC chain experiment's
+    grid) and at 1-3 blocks a CU (the fused BatchNorm's): completes without a
+    spin timeout; the cost per barrier is printed (PERF_NOTES round 6)."""
+    from mpi_tensorflow_amd.ops import native
+
+    ops = native().ops
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for blocks in (224, cus, 2 * cus, 3 * cus):
+        us = ops.gsync_barrier_us(blocks, 200)
+        print(f"grid barrier: {blocks} blocks {us:.2f} us")
+        assert 0 < us < 1000
+    assert ops.bn_fused_error() == 0
