@@ -199,6 +199,12 @@ PYBIND11_MODULE(_C, m) {
   k.def("conv2_filter_groups_bf16", &mnist16::conv2_filter_groups);
   k.def("conv2_bwd_conv1_rows_bf16", &mnist16::conv2_bwd_conv1_rows);
   k.def("xgmi_conv_floats", &mnist::xgmi_conv_floats);
+  k.def("xgmi_dispatch_probe", [](uintptr_t ctr, uintptr_t out, int blocks, long long spin,
+                                   uintptr_t s) {
+    xgmi::launch_dispatch_probe(reinterpret_cast<unsigned*>(ctr),
+                                reinterpret_cast<unsigned long long*>(out), blocks, spin, S(s));
+    check_launch();
+  });
   k.def("set_xgmi_step_prof", [](uintptr_t p) {
     mnist::set_xgmi_step_prof(reinterpret_cast<unsigned long long*>(p));
   });

@@ -11,9 +11,15 @@
 // into slot [stage][me][b] of every rank's flag array (uncached device memory,
 // written by remote stores) and waits until slots [stage][r][b] of its own
 // array hold that epoch for every r.  All ranks launch the same grids in the
-// same order, so per-block epochs agree; blocks are dispatched in increasing
-// id order on every GPU, so the lowest waiting block always has its peers
-// resident (no deadlock for any grid size).
+// same order, so per-block epochs agree.  Each XCD starts its blocks in
+// increasing id order (block b goes to XCD (b + o) mod 8, o where the
+// dispatcher's round robin stood after the previous launch - it differs
+// between ranks), so the lowest unfinished block id is resident on every rank:
+// all lower ids have finished everywhere, so nothing is ahead of it in its
+// XCD's queue on any rank.  It passes its barriers and finishes, and by
+// induction so does every block: no deadlock for any grid size.
+// tests/test_xgmi_gpu.py checks that dispatch order on the box
+// (dispatch_probe_kernel).
 //
 // Memory model (scoped, HIP / LLVM AMDGPU).  Every byte a peer reads goes
 // through system-scope ("sc0 sc1") 16-byte buffer loads, and every byte a
@@ -215,5 +221,8 @@ struct AllReduceArgs {
 // nt: threads per block (64 for small buffers: more blocks, each with one
 // float4 a thread in flight per rank; 256 otherwise)
 void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st);
+// test: per-block XCD and per-XCD start ticket (the dispatch-order assumption)
+void launch_dispatch_probe(unsigned* ctr, unsigned long long* out, int blocks,
+                           long long spin_ticks, hipStream_t st);
 
 }  // namespace xgmi

@@ -141,4 +141,34 @@ void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st
     throw std::runtime_error("xgmi all_reduce: 64 or 256 threads a block");
 }
 
+// The dispatch order the barrier argument above relies on (xgmi.h): block b
+// goes to XCD b mod 8, and each XCD starts its blocks in increasing id order.
+// Each block's first thread records its XCD (hardware register XCC_ID), a
+// ticket from its XCD's counter and its start clock, then holds its CU for
+// spin_ticks, so a grid several times the resident capacity exercises the
+// dispatcher's queue.  out[3 b] = XCD, out[3 b + 1] = ticket, out[3 b + 2] =
+// start (100 MHz); ctr: >= 16 x 16 zeroed words.
+__global__ __launch_bounds__(64) void dispatch_probe_kernel(unsigned* ctr,
+                                                            unsigned long long* out,
+                                                            long long spin_ticks) {
+  if (threadIdx.x != 0) return;
+  const long long t0 = now_ticks();
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  x &= 0xfu;
+  const unsigned t =
+      __hip_atomic_fetch_add(ctr + 16 * x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  out[3 * blockIdx.x] = x;
+  out[3 * blockIdx.x + 1] = t;
+  out[3 * blockIdx.x + 2] = (unsigned long long)t0;
+  while (now_ticks() - t0 < spin_ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+void launch_dispatch_probe(unsigned* ctr, unsigned long long* out, int blocks,
+                           long long spin_ticks, hipStream_t st) {
+  if (blocks < 1 || blocks > (1 << 20) || spin_ticks < 0 || spin_ticks > 100000)
+    throw std::runtime_error("xgmi dispatch probe: 1..2^20 blocks, spin <= 1 ms");
+  dispatch_probe_kernel<<<blocks, 64, 0, st>>>(ctr, out, spin_ticks);
+}
+
 }  // namespace xgmi

@@ -160,3 +160,45 @@ def test_xgmi_two_ranks_gate_catches_identical_but_wrong_sums():
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert "CAPTURED_SYNC_OK xgmi_gate" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_block_dispatch_order_per_xcd(cuda_dev):
+    """The no-deadlock argument of the xGMI per-block barriers (kernels/xgmi.h)
+    rests on the dispatcher: no block starts before the lower-id blocks of its
+    XCD.  Measured here: block b runs on XCD (b + o) mod 8, o = where the
+    dispatcher's round robin stood after the previous launch (first run on the
+    box: block 0 on XCD 5), so XCD-aware tilings group ids by b mod 8 and the
+    barrier argument uses per-XCD order only.  A grid of 4x the resident
+    capacity (64-thread blocks holding their CU 20 us each) records every
+    block's XCD and start clock (xgmi.hip dispatch_probe_kernel)."""
+    import numpy as np
+
+    from mpi_tensorflow_amd.ops import native, stream_handle
+
+    cus = torch.cuda.get_device_properties(cuda_dev).multi_processor_count
+    blocks = cus * 32 * 4
+    ctr = torch.zeros(256, dtype=torch.int32, device=cuda_dev)
+    out = torch.zeros(3 * blocks, dtype=torch.int64, device=cuda_dev)
+    native().mnist.xgmi_dispatch_probe(ctr.data_ptr(), out.data_ptr(), blocks, 2000,
+                                       stream_handle())
+    torch.cuda.synchronize()
+    o = out.cpu().numpy().reshape(blocks, 3)
+    xcc, start = o[:, 0], o[:, 2]
+    ids = np.arange(blocks)
+    nx = len(np.unique(xcc))
+    print(f"dispatch probe: {blocks} blocks over {nx} XCDs")
+    if nx == 8:
+        o = int(xcc[0])
+        print(f"dispatch probe: block 0 on XCD {o}")
+        assert np.array_equal(xcc, (ids + o) % 8), "blocks are not assigned to XCDs round-robin"
+    worst = 0
+    for x in np.unique(xcc):
+        s = start[xcc == x]  # in id order
+        # the latest start among lower ids, against each block's own start
+        late = np.maximum.accumulate(s)[:-1] - s[1:]
+        worst = max(worst, int(late.max(initial=0)))
+    # 2 us of slack for blocks dispatched together on different shader engines
+    # (one spin is 20 us: a block dispatched out of order would start >= 20 us
+    # before a lower id)
+    assert worst <= 200, f"a block started {worst / 100:.1f} us before a lower-id block of its XCD"
