@@ -75,9 +75,11 @@ def parse(argv=None):
                          "the separate finalize launch (A/B; default: the library's)")
     ap.add_argument("--bn-fused-bpc", type=int, default=None,
                     help="fused BatchNorm grid: blocks a CU (1..8)")
-    ap.add_argument("--xgmi-push", action="store_true",
-                    help="lenet5 over xGMI: the push sync fused into the update launch instead "
-                         "of the two-phase all-reduce + SGD launch (comm auto tunes both)")
+    ap.add_argument("--xgmi-mode", default="pull", choices=("two-phase", "push", "pull"),
+                    help="lenet5 over xGMI: the two-phase all-reduce + SGD launch, the push sync "
+                         "fused into the update launch, or the one-barrier pull of every rank's "
+                         "double-buffered gradient (comm auto tunes all three)")
+    ap.add_argument("--xgmi-push", action="store_true", help="= --xgmi-mode push")
     ap.add_argument("--xgmi-inject-skip-peer", type=int, default=-1, metavar="R",
                     help="failure injection (tests): the xGMI phase-1 reductions leave out rank "
                          "R; the exactness gate must then reject the xGMI communicator")
@@ -249,7 +251,8 @@ def run(a, di, device, wd) -> int:
                         defer_split=a.defer_split, grad_comm_dtype=a.grad_comm_dtype,
                         bucket_plan=f"bytes:{a.bucket_mb:g}" if a.bucket_mb else a.bucket_plan,
                         collective_timeout_s=a.collective_timeout_s,
-                        no_xgmi=a.no_xgmi, xgmi_push=a.xgmi_push).validate()
+                        no_xgmi=a.no_xgmi,
+                        xgmi_mode="push" if a.xgmi_push else a.xgmi_mode).validate()
     force = bool((a.force_sync or a.comm_emulate or a.xgmi_emulate) and N == 1
                  and device.type == "cuda")
     with wd.guard("start-up (communicator, engine)"):

@@ -76,6 +76,8 @@ SYNC_SCHEDULES = ("auto", "buckets", "sharded", "split", "factors", "serial", "d
 # "xgmi": collectives as compute-stream kernels reading the peers' memory
 # over the xGMI mesh (IPC-mapped; one node)
 COMMS = ("auto", "rccl", "shm", "xgmi", "torch")
+# LeNet-5's sync over the xGMI communicator (TrainConfig.xgmi_mode)
+XGMI_MODES = ("two-phase", "push", "pull")
 DTYPES = ("fp32", "bf16")
 
 
@@ -108,11 +110,15 @@ class TrainConfig:
     # comm auto, one node: do not set up the xGMI peer-to-peer communicator as
     # an extra sync-schedule candidate (parallel/setup.py setup_comms)
     no_xgmi: bool = False
-    # LeNet-5 over the xGMI communicator (--comm xgmi): the push sync fused
-    # into the update launch (one barrier, replicated momentum, kernels/lenet.h
-    # PushArgs) instead of the two-phase all-reduce + SGD launch; with --comm
-    # auto both are tuned next to RCCL
-    xgmi_push: bool = False
+    # LeNet-5 over the xGMI communicator (--comm xgmi): "two-phase" (this
+    # rank's segment summed + SGD, then the others gathered; sharded momentum),
+    # "push" (the gradient pushed into the peers' receive slots from the update
+    # launch, one barrier, kernels/lenet.h PushArgs) or "pull" (double-buffered
+    # gradient slots, one launch reads every rank's whole gradient, one
+    # barrier, replicated SGD; kernels/xgmi.h OneShotArgs); with --comm auto
+    # all three are tuned next to RCCL.  Default pull: emulated 8 ranks at
+    # 1 us / 150 GB/s 34.97 us a step against 42.31 two-phase, 44.1 push
+    xgmi_mode: str = "pull"
     # fp32 MNIST conv2 algorithm on the native engine: "winograd" (F(2x2,5x5),
     # kernels/wino.h; 2.8x fewer MFMAs, fp32 arithmetic throughout, ~1e-6
     # relative error) or "direct" (25-tap implicit GEMM)
@@ -161,6 +167,8 @@ class TrainConfig:
             raise ValueError(f"unknown model {self.model!r}; choose from {MODELS}")
         if self.sync not in SYNC_MODES:
             raise ValueError(f"unknown sync {self.sync!r}; choose from {SYNC_MODES}")
+        if self.xgmi_mode not in XGMI_MODES:
+            raise ValueError(f"unknown xgmi mode {self.xgmi_mode!r}; choose from {XGMI_MODES}")
         if self.sync_schedule not in SYNC_SCHEDULES:
             raise ValueError(f"unknown sync schedule {self.sync_schedule!r}; "
                              f"choose from {SYNC_SCHEDULES}")

@@ -398,6 +398,7 @@ PYBIND11_MODULE(_C, m) {
                                           P<float>(ws), P<float>(dw), S(st));
           check_launch();
         });
+  g.def("s2d_stem_set_preload", &gops::s2d_stem_set_preload);
   g.def("conv_fwd_s2d_stem_bf16", [](const gops::ConvShape& si, uintptr_t xs, uintptr_t wt8,
                                      uintptr_t yb, uintptr_t st, uintptr_t stats_part,
                                      int stats_rows, uintptr_t stats_shift) {
@@ -781,7 +782,7 @@ PYBIND11_MODULE(_C, m) {
           RWL(train_x) RWL(train_y) RWL(n_local) RWL(batch) RWL(params) RWL(grads) RWL(mom)
               RWL(total) RWL(off) RWL(step) RWL(lr) RWL(correct) RWL(acts) RWL(deltas) RWL(convp)
                   RWL(loss_rows) RWL(base_lr) RWL(lr_decay) RWL(momentum) RWL(grad_bf16) RWL(gb16)
-                  RWL(xrecv);
+                  RWL(xrecv) RWL(xgrads2) RWL(xdone);
 #undef RWL
   m.def("lenet_buffer_floats", [](int batch) {
     return py::make_tuple(lenet::acts_floats(batch), lenet::deltas_floats(batch),
@@ -807,8 +808,8 @@ PYBIND11_MODULE(_C, m) {
   });
   py::class_<LenetExecutor>(m, "LenetExecutor")
       .def(py::init<const LenetPtrs&>())
-      .def("set_xgmi_push", &LenetExecutor::set_xgmi_push)
-      .def_property_readonly("xgmi_push", &LenetExecutor::xgmi_push)
+      .def("set_xgmi_mode", &LenetExecutor::set_xgmi_mode)
+      .def_property_readonly("xgmi_mode", &LenetExecutor::xgmi_mode)
       .def("train_step",
            [](LenetExecutor& e, uintptr_t s, Collective* comm) {
              e.train_step(S(s), comm);

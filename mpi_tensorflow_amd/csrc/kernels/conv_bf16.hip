@@ -510,6 +510,86 @@ struct S2dLoader {
   }
 };
 
+// The same operands with every K tile requested at once: the stem GEMM has
+// only 4 K tiles (K = 256) a block, so fwd_kernel's one-tile-ahead pipeline
+// waited on 4 dependent load round trips per block at 2 blocks a CU.  Here the
+// first load() issues all 4 tiles' A / B loads (64 + 32 VGPRs) and store()
+// writes the tile the last load() named (a uniform switch: no dynamic register
+// indexing).
+template <int BM, int BN>
+struct S2dLoaderPre {
+  static constexpr int AR = BM * BK / 8 / NT;
+  static constexpr int BR = BN * BK / 8 / NT;
+  static constexpr int NKT = 4;  // tap rows = K tiles
+  static constexpr int EXTRA = 0;
+  const __bf16* abase[AR];
+  bool av[AR];
+  const __bf16* bbase[BR];
+  uint4 ra[NKT][AR];
+  uint4 rb[NKT][BR];
+  int ws16, cur = 0;
+  __device__ S2dLoaderPre(const ConvShape& s, const ConvShape& si, const __bf16* x,
+                          const __bf16* wt, int m0, int n0, __bf16*) {
+    const int tid = threadIdx.x, c8 = tid & 7;
+    const int M = s.N * s.OH * s.OW;
+    ws16 = si.W * 16;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int m = m0 + (tid >> 3) + (NT / 8) * i;
+      av[i] = m < M;
+      const int mm = av[i] ? m : 0;
+      const int ox = mm % s.OW, t = mm / s.OW, oy = t % s.OH, n = t / s.OH;
+      abase[i] = x + (((size_t)n * si.H + oy) * si.W + ox + (c8 >> 1)) * 16 + 8 * (c8 & 1);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int n = min(n0 + (tid >> 3) + (NT / 8) * i, s.K - 1);
+      bbase[i] = wt + (size_t)n * s.C + 8 * c8;
+    }
+  }
+  __device__ __forceinline__ void load(int kt) {
+    cur = kt;
+    if (kt != 0) return;
+#pragma unroll
+    for (int k = 0; k < NKT; ++k) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i)
+        ra[k][i] = av[i] ? *reinterpret_cast<const uint4*>(abase[i] + (size_t)k * ws16)
+                         : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int i = 0; i < BR; ++i) rb[k][i] = *reinterpret_cast<const uint4*>(bbase[i] + k * BK);
+    }
+  }
+  template <int K>
+  __device__ __forceinline__ void store_k(__bf16* As, __bf16* Bs) const {
+    const int tid = threadIdx.x, c8 = tid & 7;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      *reinterpret_cast<uint4*>(As + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = ra[K][i];
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      *reinterpret_cast<uint4*>(Bs + ((tid >> 3) + (NT / 8) * i) * LDK + 8 * c8) = rb[K][i];
+  }
+  __device__ __forceinline__ void store(__bf16* As, __bf16* Bs) const {
+    switch (cur) {
+      case 0: store_k<0>(As, Bs); break;
+      case 1: store_k<1>(As, Bs); break;
+      case 2: store_k<2>(As, Bs); break;
+      default: store_k<3>(As, Bs); break;
+    }
+  }
+};
+
+// K tiles a loader holds at once (fwd_kernel unrolls its loop for them), 0: streamed
+template <class LD>
+struct FixedNk {
+  static constexpr int v = 0;
+};
+template <int BM, int BN>
+struct FixedNk<S2dLoaderPre<BM, BN>> {
+  static constexpr int v = S2dLoaderPre<BM, BN>::NKT;
+};
+
 // BatchNorm statistics in a bf16-output epilogue (ConvStats): lane (r, h) of
 // a wave holds column r of its 32-row tiles; after its own rows are summed
 // the two half-waves combine, and lanes h == 0 write the wave's partial row
@@ -584,7 +664,42 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = zero16();
-  if (nk > 0) {
+  auto mma = [&](const __bf16* A, const __bf16* B) {
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bfx8 a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        a[i] = *reinterpret_cast<const bfx8*>(A + (wm * (BM / 2) + 32 * i + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        b[j] = *reinterpret_cast<const bfx8*>(B + (wn * (BN / 2) + 32 * j + r) * LDK + 16 * ks + 8 * h);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  if constexpr (FixedNk<LD>::v > 0) {
+    // a loader holding all K tiles in registers: the loop unrolled, so its
+    // per-tile stores index the tiles with constants (no scratch)
+    constexpr int NK = FixedNk<LD>::v;
+    ld.load(0);
+    ld.store(smem, smem + BM * LDK);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < NK; ++kt) {
+      const __bf16* A = smem + (kt & 1) * STAGE;
+      mma(A, A + BM * LDK);
+      if (kt + 1 < NK) {
+        __bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
+        ld.cur = kt + 1;
+        ld.store(nxt, nxt + BM * LDK);
+      }
+      __syncthreads();
+    }
+  } else if (nk > 0) {
     ld.load(kb);
     ld.store(smem, smem + BM * LDK);
     __syncthreads();
@@ -594,21 +709,7 @@ __global__ __launch_bounds__(NT) void fwd_kernel(ConvShape s, const XT* __restri
       __bf16* nxt = smem + ((kt + 1) & 1) * STAGE;
       const bool more = kt + 1 < nk;
       if (more) ld.load(kb + kt + 1);
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        bfx8 a[TM], b[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          a[i] = *reinterpret_cast<const bfx8*>(A + (wm * (BM / 2) + 32 * i + r) * LDK + 16 * ks + 8 * h);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          b[j] = *reinterpret_cast<const bfx8*>(B + (wn * (BN / 2) + 32 * j + r) * LDK + 16 * ks + 8 * h);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
+      mma(A, B);
       if (more) ld.store(nxt, nxt + BM * LDK);
       __syncthreads();
     }
@@ -2467,6 +2568,8 @@ static void s2d_check(const ConvShape& si) {
     throw std::runtime_error("s2d stem conv: inconsistent shapes");
 }
 
+static bool g_s2d_preload = true;  // A/B: S2dLoaderPre (all K tiles at once) vs S2dLoader
+
 void conv_fwd_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* wt8, void* yb,
                             hipStream_t st, const ConvStats* stats) {
   using namespace cbf;
@@ -2480,10 +2583,17 @@ void conv_fwd_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* wt8
   }
   const long long M = (long long)s1.N * s1.OH * s1.OW;
   const dim3 grid(cdiv(M, 128) * (s1.K / 64), 1);
-  fwd_kernel<128, 64, __bf16, S2dLoader<128, 64>><<<grid, NT, 0, st>>>(
-      s1, reinterpret_cast<const __bf16*>(xs), reinterpret_cast<const __bf16*>(wt8), nullptr,
-      nullptr, 0, s1.C / BK, nullptr, reinterpret_cast<__bf16*>(yb), 0, si, cs);
+  if (s1.C / BK != S2dLoaderPre<128, 64>::NKT) throw std::runtime_error("s2d stem conv: K tiles");
+  if (g_s2d_preload)
+    fwd_kernel<128, 64, __bf16, S2dLoaderPre<128, 64>><<<grid, NT, 0, st>>>(
+        s1, reinterpret_cast<const __bf16*>(xs), reinterpret_cast<const __bf16*>(wt8), nullptr,
+        nullptr, 0, s1.C / BK, nullptr, reinterpret_cast<__bf16*>(yb), 0, si, cs);
+  else
+    fwd_kernel<128, 64, __bf16, S2dLoader<128, 64>><<<grid, NT, 0, st>>>(
+        s1, reinterpret_cast<const __bf16*>(xs), reinterpret_cast<const __bf16*>(wt8), nullptr,
+        nullptr, 0, s1.C / BK, nullptr, reinterpret_cast<__bf16*>(yb), 0, si, cs);
 }
+void s2d_stem_set_preload(bool on) { g_s2d_preload = on; }
 
 // the 4x4 conv's filter gradient over the s2d image: the generic bf16 wgrad
 // (rows m = tap * 16 + channel; a channel quad never straddles taps), split-K

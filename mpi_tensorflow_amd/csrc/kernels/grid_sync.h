@@ -66,7 +66,7 @@ __device__ __forceinline__ void grid_barrier(const GridBar& b) {
 // is needed - the first launch may come while a stream is being captured.
 static __device__ unsigned gsync_state_[48];
 
-inline GridBar tu_bar() {
+static inline GridBar tu_bar() {  // internal linkage: one per TU, as gsync_state_
   static GridBar b{nullptr, nullptr, nullptr};
   if (!b.cnt) {
     void* p = nullptr;

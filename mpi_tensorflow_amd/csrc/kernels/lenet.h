@@ -53,7 +53,9 @@ void launch_image_eval(const ImageArgs& a, int rows, hipStream_t s);
 // follows, then the flat SGD kernel)
 void launch_update(const float* acts, const float* deltas, const float* convp, int batch,
                    const Offsets& off, float* params, float* grads, float* mom, float momentum,
-                   const float* lr, long long* step, bool apply, hipStream_t s);
+                   const float* lr, long long* step, bool apply, hipStream_t s, long long dbuf = 0);
+// dbuf > 0 (apply = false): the grads go to slot (*step) & 1 of a double-
+// buffered [2][dbuf] buffer at `grads` (the xGMI one-shot sync reads it)
 
 // xGMI "push" sync fused into the update launch (LenetExecutor with an
 // XgmiComm and a registered receive buffer): every block pushes its freshly

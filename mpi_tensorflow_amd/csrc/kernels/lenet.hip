@@ -727,9 +727,10 @@ __global__ __launch_bounds__(256) void update_kernel(const float* __restrict__ a
                                                      const Offsets o, float* __restrict__ w,
                                                      float* __restrict__ g, float* __restrict__ m,
                                                      float mu, const float* lr_ptr,
-                                                     long long* step) {
+                                                     long long* step, long long dbuf) {
   const int tid = threadIdx.x;
   const float lr = APPLY ? *lr_ptr : 0.f;
+  if (!APPLY && dbuf > 0) g += ((*step) & 1) * dbuf;  // the one-shot sync's slot
   int blk = blockIdx.x;
   if (APPLY && blk == 0 && tid == 0) *step += 1;
   if (blk < UB_FC) {
@@ -918,14 +919,15 @@ void launch_image_eval(const ImageArgs& a, int rows, hipStream_t s) {
 
 void launch_update(const float* acts, const float* deltas, const float* convp, int batch,
                    const Offsets& off, float* params, float* grads, float* mom, float momentum,
-                   const float* lr, long long* step, bool apply, hipStream_t s) {
+                   const float* lr, long long* step, bool apply, hipStream_t s, long long dbuf) {
   const int blocks = UB_FC + UB_CONV;
+  if (dbuf && (apply || !step)) throw std::runtime_error("lenet update: dbuf needs grads + step");
   if (apply)
     update_kernel<true><<<blocks, 256, 0, s>>>(acts, deltas, convp, batch, off, params, grads, mom,
-                                               momentum, lr, step);
+                                               momentum, lr, step, 0);
   else
     update_kernel<false><<<blocks, 256, 0, s>>>(acts, deltas, convp, batch, off, params, grads,
-                                                mom, momentum, lr, step);
+                                                mom, momentum, lr, step, dbuf);
 }
 
 void launch_update_push(const float* acts, const float* deltas, const float* convp, int batch,

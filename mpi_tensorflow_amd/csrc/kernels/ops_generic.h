@@ -92,6 +92,9 @@ void conv_bwd_filter_stem_bf16(const ConvShape& s1, const ConvShape& si, const f
 // ws of s2d_stem_ws_floats(si) floats.
 void conv_fwd_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* wt8, void* yb,
                             hipStream_t st, const ConvStats* stats);
+// A/B: the s2d stem forward with every K tile requested at once (default) or
+// one tile ahead (fwd_kernel's generic pipeline)
+void s2d_stem_set_preload(bool on);
 void conv_bwd_filter_s2d_stem_bf16(const ConvShape& si, const void* xs, const void* dyb,
                                    float* ws, float* dw8, hipStream_t st);
 size_t s2d_stem_ws_floats(const ConvShape& si);

@@ -221,6 +221,31 @@ struct AllReduceArgs {
 // nt: threads per block (64 for small buffers: more blocks, each with one
 // float4 a thread in flight per rank; 256 otherwise)
 void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st);
+// One-shot all-reduce + momentum SGD for small buffers (LeNet-5's 62 K
+// parameters: the two-phase launch's two barriers and two dependent memory
+// phases cost ~13 us for 248 KB).  Every rank's gradient lives in slot
+// (*step) & 1 of a double-buffered registered buffer g2 [2][n4 float4s]
+// (the update launch writes it there); after ONE arrival barrier each block
+// loads its float4s of every rank's slot (all in flight), sums them in rank
+// order and applies the replicated SGD (optim::sgd_momentum_flat's forms) to
+// its params / momentum.  Each link carries the whole buffer once (vs 2 x
+// 1/N of it), which is nothing at this size.  No closing barrier: a peer
+// rewrites slot p two steps later, after the next launch's arrival barrier,
+// which this rank's blocks reach only once this launch has completed.  The
+// step is bumped by the last block to finish (a completion ticket on `done`),
+// after every block has read it for the parity.
+struct OneShotArgs {
+  Sync s;
+  const float* g[kMaxRanks] = {};  // every rank's g2, mapped here ([rank] local)
+  float* w = nullptr;              // this rank's params / momentum
+  float* mom = nullptr;
+  long long n4 = 0;                // float4s of ONE slot
+  const float* lr = nullptr;
+  float momentum = 0.f, gscale = 1.f;
+  long long* step = nullptr;       // read for the slot parity, bumped once
+  unsigned* done = nullptr;        // zeroed completion counter (reset by the last block)
+};
+void launch_oneshot_sgd(const OneShotArgs& a, hipStream_t st);
 // test: per-block XCD and per-XCD start ticket (the dispatch-order assumption)
 void launch_dispatch_probe(unsigned* ctr, unsigned long long* out, int blocks,
                            long long spin_ticks, hipStream_t st);

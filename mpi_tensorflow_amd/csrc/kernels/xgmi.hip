@@ -141,6 +141,80 @@ void launch_allreduce(const AllReduceArgs& a, int blocks, int nt, hipStream_t st
     throw std::runtime_error("xgmi all_reduce: 64 or 256 threads a block");
 }
 
+// (xgmi.h OneShotArgs) one float4 of every rank a thread, 256 threads a block
+__global__ __launch_bounds__(256) void oneshot_sgd_kernel(const OneShotArgs a) {
+  __shared__ unsigned ep;
+  const Sync& s = a.s;
+  const int n = s.nranks, tid = threadIdx.x;
+  const long long st = *a.step;  // every block reads it before its completion ticket
+  const unsigned slot = (unsigned)((st & 1) * a.n4 * 16);
+  Rsrc gr[kMaxRanks];
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r)
+    if (r < n) gr[r] = rsrc(a.g[r], 2 * a.n4 * 16);
+  const unsigned e = next_epoch(s, &ep);
+  barrier(s, 0, e, /*release=*/true);  // the grads come from the update launch
+  const long long t0 = now_ticks();
+  const long long i = (long long)blockIdx.x * 256 + tid;
+  if (i < a.n4) {
+    float4 v[kMaxRanks];
+#pragma unroll
+    for (int r = 0; r < kMaxRanks; ++r)
+      v[r] = r < n ? ld4_peer(s, r, gr[r], slot + (unsigned)(i * 16)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4* W4 = reinterpret_cast<float4*>(a.w);
+    float4* M4 = reinterpret_cast<float4*>(a.mom);
+    float4 wv = W4[i], mv = M4[i];
+    const float lr = *a.lr;
+    float4 gv = v[0];  // rank order 0..N-1
+#pragma unroll
+    for (int r = 1; r < kMaxRanks; ++r)
+      if (r < n) {
+        gv.x += v[r].x;
+        gv.y += v[r].y;
+        gv.z += v[r].z;
+        gv.w += v[r].w;
+      }
+    // optim::sgd_momentum_flat_kernel's expression forms (l2 = 0)
+    gv.x = __builtin_fmaf(0.f, wv.x, gv.x * a.gscale);
+    gv.y = __builtin_fmaf(0.f, wv.y, gv.y * a.gscale);
+    gv.z = __builtin_fmaf(0.f, wv.z, gv.z * a.gscale);
+    gv.w = __builtin_fmaf(0.f, wv.w, gv.w * a.gscale);
+    mv.x = a.momentum * mv.x + gv.x;
+    mv.y = a.momentum * mv.y + gv.y;
+    mv.z = a.momentum * mv.z + gv.z;
+    mv.w = a.momentum * mv.w + gv.w;
+    wv.x -= lr * mv.x;
+    wv.y -= lr * mv.y;
+    wv.z -= lr * mv.z;
+    wv.w -= lr * mv.w;
+    W4[i] = wv;
+    M4[i] = mv;
+  }
+  link_floor(s, t0, a.n4 * 16);
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned t =
+        __hip_atomic_fetch_add(a.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(a.done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *a.step = st + 1;
+    }
+  }
+}
+
+void launch_oneshot_sgd(const OneShotArgs& a, hipStream_t st) {
+  if (a.s.nranks < 1 || a.s.nranks > kMaxRanks || !a.s.flags || !a.s.epoch || !a.s.error)
+    throw std::runtime_error("xgmi one-shot sgd: communicator not set up");
+  for (int r = 0; r < a.s.nranks; ++r)
+    if (!a.g[r] || (!a.s.emulate && !a.s.peer_flags[r]))
+      throw std::runtime_error("xgmi one-shot sgd: rank " + std::to_string(r) + " not mapped");
+  if (!a.w || !a.mom || !a.lr || !a.step || !a.done || a.n4 <= 0 || 2 * a.n4 * 16 >= (1LL << 32))
+    throw std::runtime_error("xgmi one-shot sgd: arguments");
+  const long long blocks = (a.n4 + 255) / 256;
+  if (blocks > kMaxBlocks) throw std::runtime_error("xgmi one-shot sgd: buffer too large");
+  oneshot_sgd_kernel<<<(int)blocks, 256, 0, st>>>(a);
+}
+
 // The dispatch order the barrier argument above relies on (xgmi.h): block b
 // goes to XCD b mod 8, and each XCD starts its blocks in increasing id order.
 // Each block's first thread records its XCD (hardware register XCC_ID), a

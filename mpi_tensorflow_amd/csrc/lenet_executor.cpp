@@ -10,10 +10,18 @@ static inline T* P(uintptr_t v) {
   return reinterpret_cast<T*>(v);
 }
 
-LenetExecutor::LenetExecutor(const LenetPtrs& p) : p_(p), push_(p.xrecv != 0) {
+LenetExecutor::LenetExecutor(const LenetPtrs& p) : p_(p) {
   if (p_.batch <= 0 || p_.n_local <= p_.batch)
     throw std::runtime_error("LenetExecutor: the local shard must exceed the batch");
   if (p_.total % 4 != 0) throw std::runtime_error("LenetExecutor: flat buffer not float4-sized");
+}
+
+void LenetExecutor::set_xgmi_mode(int m) {
+  if (m == XGMI_PUSH && !p_.xrecv) throw std::runtime_error("LenetExecutor: push needs xrecv");
+  if (m == XGMI_PULL && (!p_.xgrads2 || !p_.xdone))
+    throw std::runtime_error("LenetExecutor: pull needs xgrads2 and xdone");
+  if (m < XGMI_TWO_PHASE || m > XGMI_PULL) throw std::runtime_error("LenetExecutor: xgmi mode");
+  mode_ = m;
 }
 
 lenet::ImageArgs LenetExecutor::image_args() const {
@@ -45,7 +53,18 @@ void LenetExecutor::forward_backward(hipStream_t s) {
 
 void LenetExecutor::train_step(hipStream_t s, Collective* comm) {
   lenet::launch_image_train(image_args(), s);
-  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && push_) {
+  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && mode_ == XGMI_PULL) {
+    float* G2 = P<float>(p_.xgrads2);
+    lenet::launch_update(P<const float>(p_.acts), P<const float>(p_.deltas),
+                         P<const float>(p_.convp), p_.batch, p_.off, P<float>(p_.params), G2,
+                         P<float>(p_.mom), p_.momentum, P<const float>(p_.lr),
+                         P<long long>(p_.step), false, s, p_.total);
+    x->all_reduce_sgd_oneshot(G2, P<float>(p_.params), P<float>(p_.mom), (size_t)p_.total,
+                              p_.momentum, 1.0f / (float)x->size(), P<const float>(p_.lr),
+                              P<long long>(p_.step), P<unsigned>(p_.xdone), s);
+    return;
+  }
+  if (auto* x = dynamic_cast<XgmiComm*>(comm); x != nullptr && mode_ == XGMI_PUSH) {
     lenet::PushArgs pa;
     pa.sync = x->sync();
     for (int r = 0; r < x->size(); ++r)

@@ -5,8 +5,13 @@
 // and no host-side step state (batch offset and LR come from the device step
 // counter), so the Python engine captures G steps into one hipGraph.
 //   world 1:  image kernel -> update kernel (grads + momentum SGD)   2 launches
-//   world N, xGMI communicator with a receive buffer: image kernel -> update
-//             kernel with the push sync fused (lenet.h PushArgs)   2 launches
+//   world N, xGMI communicator, mode push: image kernel -> update kernel
+//             with the push sync fused (lenet.h PushArgs)           2 launches
+//   world N, xGMI communicator, mode pull: image kernel -> update kernel
+//             (grads into slot step & 1 of xgrads2) -> one-shot sum of every
+//             rank's slot + replicated SGD (xgmi.h OneShotArgs)     3 launches
+//   world N, xGMI communicator, mode two-phase: image -> update (grads) ->
+//             all_reduce_sgd (segment sum + SGD, gather)           3 launches
 //   world N:  image kernel -> update kernel (grads into the flat buffer)
 //             -> in-place all-reduce of the whole 250 KB flat gradient on
 //             the compute stream (one latency-bound bucket: a cross-stream
@@ -35,16 +40,20 @@ struct LenetPtrs {
   // xGMI push sync (lenet.h PushArgs): the registered receive buffer
   // [2][N][total] floats; 0 = the two-phase all_reduce_sgd instead
   uintptr_t xrecv = 0;
+  // xGMI one-shot (pull) sync: the registered double-buffered gradient
+  // [2][total] floats and a zeroed device word (the launch's completion count)
+  uintptr_t xgrads2 = 0, xdone = 0;
 };
 
 class LenetExecutor {
  public:
   explicit LenetExecutor(const LenetPtrs& p);
   void train_step(hipStream_t s, Collective* comm);
-  // over an XgmiComm with a receive buffer (xrecv): the push sync fused into
-  // the update launch (on), or the two-phase all_reduce_sgd launch (off)
-  void set_xgmi_push(bool on) { push_ = on && p_.xrecv != 0; }
-  bool xgmi_push() const { return push_; }
+  // the sync over an XgmiComm: XGMI_TWO_PHASE (all_reduce_sgd), XGMI_PUSH
+  // (needs xrecv) or XGMI_PULL (needs xgrads2 + xdone)
+  enum { XGMI_TWO_PHASE = 0, XGMI_PUSH = 1, XGMI_PULL = 2 };
+  void set_xgmi_mode(int m);
+  int xgmi_mode() const { return mode_; }
   // forward + backward with the weight grads in the flat grad buffer (no
   // sync, no SGD, no step bump): numerics tests
   void forward_backward(hipStream_t s);
@@ -55,5 +64,5 @@ class LenetExecutor {
  private:
   lenet::ImageArgs image_args() const;
   LenetPtrs p_;
-  bool push_ = false;
+  int mode_ = XGMI_TWO_PHASE;
 };

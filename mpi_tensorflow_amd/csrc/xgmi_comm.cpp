@@ -203,6 +203,27 @@ void XgmiComm::all_reduce_sgd(float* grads, float* params, float* mom, size_t co
   launch(grads, count, false, s, &a);
 }
 
+void XgmiComm::all_reduce_sgd_oneshot(const float* grads2, float* params, float* mom,
+                                      size_t count, float momentum, float gscale, const float* lr,
+                                      long long* step, unsigned* done, hipStream_t s) {
+  if (count == 0 || count % 4) throw std::runtime_error("XgmiComm::all_reduce_sgd_oneshot: count");
+  if (!ready()) throw std::runtime_error("XgmiComm: flags of some rank not mapped");
+  if (!registered(grads2, 2 * count * sizeof(float)))
+    throw std::runtime_error("XgmiComm::all_reduce_sgd_oneshot: grads2 [2][count] not registered");
+  xgmi::OneShotArgs a;
+  a.s = sync_;
+  for (int r = 0; r < nranks_; ++r) a.g[r] = static_cast<const float*>(peer_ptr(grads2, r));
+  a.w = params;
+  a.mom = mom;
+  a.n4 = (long long)(count / 4);
+  a.lr = lr;
+  a.momentum = momentum;
+  a.gscale = gscale;
+  a.step = step;
+  a.done = done;
+  xgmi::launch_oneshot_sgd(a, s);
+}
+
 void XgmiComm::emulate_fill_peer(uintptr_t local, int r, uintptr_t src, size_t bytes) {
   if (!emulate_) throw std::runtime_error("XgmiComm: emulate_fill_peer on a real communicator");
   const Reg* g = find(reinterpret_cast<const void*>(local), bytes);

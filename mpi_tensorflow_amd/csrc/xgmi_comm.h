@@ -101,6 +101,14 @@ class XgmiComm : public Collective {
   void all_reduce_sgd(float* grads, float* params, float* mom, size_t count, long long l2_end,
                       float l2, float momentum, float gscale, const float* lr, long long* step,
                       hipStream_t s);
+  // small buffers: the one-shot form (kernels/xgmi.h OneShotArgs) - grads2 is
+  // the registered double-buffered gradient [2][count] whose slot (*step & 1)
+  // the caller wrote this step; one barrier, every rank's slot summed in rank
+  // order, the replicated SGD (bit-identical to all_reduce + that SGD with a
+  // rank-order sum); *step bumped; done: a zeroed device counter
+  void all_reduce_sgd_oneshot(const float* grads2, float* params, float* mom, size_t count,
+                              float momentum, float gscale, const float* lr, long long* step,
+                              unsigned* done, hipStream_t s);
   // send (recv_count x N floats) registered and left unchanged unless recv is
   // this rank's slot of it (in place: the reduced segment lands there)
   void reduce_scatter(const void* send, void* recv, size_t recv_count, int dtype, int op,

@@ -26,6 +26,10 @@ from ..parallel.comm import DeviceComm, XgmiDeviceComm
 from ..utils.devcache import DeviceArrayCache
 from ..utils.schedule import learning_rate
 
+# the executor's xGMI sync modes (csrc/lenet_executor.h XGMI_*)
+XGMI_MODES = C.XGMI_MODES
+XGMI_MODE_IDS = {m: i for i, m in enumerate(XGMI_MODES)}
+
 _OFFSETS = (("c1w", "c1_w"), ("c1b", "c1_b"), ("c2w", "c2_w"), ("c2b", "c2_b"), ("f1w", "f1_w"),
             ("f1b", "f1_b"), ("f2w", "f2_w"), ("f2b", "f2_b"), ("f3w", "f3_w"), ("f3b", "f3_b"))
 
@@ -120,12 +124,19 @@ class NativeLenetEngine:
                 self.xrecv = torch.zeros(2 * self.xcomm.size * self.layout.total, device=dev)
                 self.xcomm.register(self.xrecv)
                 p.xrecv = ptr(self.xrecv)
+                # the one-shot (pull) sync: double-buffered gradient slots
+                # [2][total] read by every peer, and its completion counter
+                self.xgrads2 = torch.zeros(2 * self.layout.total, device=dev)
+                self.xcomm.register(self.xgrads2)
+                self.xdone = torch.zeros(16, dtype=torch.int32, device=dev)
+                p.xgrads2, p.xdone = ptr(self.xgrads2), ptr(self.xdone)
             self._sync = self._native_comm
             # connection setup of the collective, outside any capture (the
             # executor copies the pointer struct: made after xrecv is set)
             self.ptrs = p
             self.exe = C_.LenetExecutor(p)
-            self.exe.set_xgmi_push(bool(cfg.xgmi_push))
+            if self.xcomm is not None:
+                self.exe.set_xgmi_mode(XGMI_MODE_IDS[cfg.xgmi_mode])
             self._native_comm.all_reduce(ptr(self.grads), ptr(self.grads), self.layout.total, 7, 0,
                                          stream_handle())
             torch.cuda.synchronize(dev)
@@ -150,8 +161,8 @@ class NativeLenetEngine:
         """Replicated optimizer state: nothing to gather, except over the xGMI
         communicator's two-phase sync, whose fused all-reduce + SGD keeps each
         rank's momentum segment only (csrc/xgmi_comm.h all_reduce_sgd); the
-        push sync (default) keeps the momentum replicated."""
-        if self._syncs_over_xgmi() and not self.xgmi_push:
+        push and pull syncs keep the momentum replicated."""
+        if self._syncs_over_xgmi() and self.xgmi_mode == "two-phase":
             self._sync.gather_segments(ptr(self.mom), self.layout.total, stream_handle())
             torch.cuda.synchronize(self.device)
 
@@ -159,15 +170,17 @@ class NativeLenetEngine:
         return self.xcomm is not None and self._sync is self.xcomm.native_handle
 
     @property
-    def xgmi_push(self) -> bool:
-        return bool(getattr(self, "exe", None) is not None and self.exe.xgmi_push)
+    def xgmi_mode(self) -> str:
+        """The sync over the xGMI communicator: two-phase | push | pull."""
+        m = self.exe.xgmi_mode if getattr(self, "exe", None) is not None else 0
+        return XGMI_MODES[m]
 
     @property
     def sync_schedule(self) -> str:
         if not self.grad_sync:
             return "none"
         if self._syncs_over_xgmi():
-            return "xgmi-push" if self.xgmi_push else "xgmi"
+            return {"two-phase": "xgmi", "push": "xgmi-push", "pull": "xgmi-pull"}[self.xgmi_mode]
         return "all-reduce"
 
     def extra_state(self):
@@ -187,16 +200,16 @@ class NativeLenetEngine:
     def _launch_one(self) -> None:
         self.exe.train_step(stream_handle(), self._sync)
 
-    def _set_sync(self, c, push: Optional[bool] = None) -> None:
-        push = self.xgmi_push if push is None else push
-        if c is self._sync and push == self.xgmi_push:
+    def _set_sync(self, c, mode: Optional[str] = None) -> None:
+        mode = self.xgmi_mode if mode is None else mode
+        if c is self._sync and mode == self.xgmi_mode:
             return
         self.sync_optimizer_state()  # (two-phase xGMI: the sharded momentum made whole)
         self._sync = c
-        self.exe.set_xgmi_push(push)
+        self.exe.set_xgmi_mode(XGMI_MODE_IDS[mode])
 
     def _graph(self, n: int):
-        key = (id(self._sync), self.xgmi_push, n)
+        key = (id(self._sync), self.xgmi_mode, n)
         g = self._graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
@@ -230,8 +243,8 @@ class NativeLenetEngine:
         G = self.graph_steps
         snap = (self.params.clone(), self.mom.clone(), self.step_dev.clone())
         xh = self.xcomm.native_handle
-        cands = [("all-reduce", self._native_comm, False), ("xgmi", xh, False),
-                 ("xgmi-push", xh, True)]
+        cands = [("all-reduce", self._native_comm, "two-phase"), ("xgmi", xh, "two-phase"),
+                 ("xgmi-push", xh, "push"), ("xgmi-pull", xh, "pull")]
         best, steps = None, 0
 
         def restore():
@@ -240,11 +253,11 @@ class NativeLenetEngine:
             self.step_dev.copy_(snap[2])
             torch.cuda.synchronize(self.device)
 
-        for name, c, push in cands:
+        for name, c, mode in cands:
             if c is not self._native_comm and self.xcomm is None:
                 self.tune_log[name] = None  # (the xGMI communicator timed out before)
                 continue
-            self._set_sync(c, push)
+            self._set_sync(c, mode)
             restore()
             g = self._graph(G)
             if D.allreduce_max_host(0.0 if g is not None else 1.0) != 0.0:
@@ -263,13 +276,13 @@ class NativeLenetEngine:
                         why = "the replicas differ after the trial steps"
                 if why is None and not self.xcomm.emulated_comm:  # one eager step each
                     outs = []
-                    for cc, pp in ((c, push), (self._native_comm, False)):
+                    for cc, pp in ((c, mode), (self._native_comm, "two-phase")):
                         self._set_sync(cc, pp)
                         restore()
                         self._launch_one()
                         torch.cuda.synchronize(self.device)
                         outs.append(self.params.clone())
-                    self._set_sync(c, push)
+                    self._set_sync(c, mode)
                     dx, ds = outs[0] - snap[0], outs[1] - snap[0]
                     ref = float(ds.abs().max())
                     err = float((dx - ds).abs().max())
@@ -300,9 +313,9 @@ class NativeLenetEngine:
             us = D.allreduce_max_host(1000.0 * t0.elapsed_time(t1) / (TUNE_REPLAYS * G))
             self.tune_log[name] = round(us, 2)
             if best is None or us < best[0]:
-                best = (us, c, push)
+                best = (us, c, mode)
         if best is None:
-            best = (0.0, self._native_comm, False)
+            best = (0.0, self._native_comm, "two-phase")
         self._set_sync(best[1], best[2])
         restore()
         self._tuned = True

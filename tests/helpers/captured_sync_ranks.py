@@ -277,8 +277,12 @@ def scenario_generic(di, model):
     from mpi_tensorflow_amd.runtime.lenet_engine import NativeLenetEngine
     from mpi_tensorflow_amd.utils.data import synthetic_images_torch
 
-    push = model.endswith("-xgmipush")  # LeNet-5: the push sync in the update launch
-    model = model[:-4] if push else model
+    # LeNet-5 over xGMI: -xgmipush = the push sync in the update launch,
+    # -xgmipull = the one-shot pull of every rank's double-buffered gradient
+    xmode = "two-phase"
+    for m in ("push", "pull"):
+        if model.endswith("-xgmi" + m):
+            xmode, model = m, model[:-4]
     xg = model.endswith("-xgmi")  # the xGMI peer-to-peer communicator instead of shm
     model = model[:-5] if xg else model
     fused = model == "lenet5-native"
@@ -288,7 +292,7 @@ def scenario_generic(di, model):
     steps = 7 if fused else 5  # resnet: 3 eager warm-up steps + one 2-step graph
     rows = 4 * B
     cfg = C.TrainConfig(model=name, batch_size=B, graph=True, graph_steps=2,
-                        xgmi_push=push).validate()
+                        xgmi_mode=xmode).validate()
 
     def shard(r):
         x, y = synthetic_images_torch(rows, model_input_shape(name), seed=cfg.seed, start=r * rows)
@@ -341,8 +345,8 @@ def scenario_generic(di, model):
             assert torch.equal(eng.mom.detach().cpu(), mq), "xgmi momentum vs serial emulation"
         assert np.isfinite(p.numpy()).all()
     if fused and xg:
-        assert eng.xgmi_push == push
-    return f"model={model}{'-xgmi' if xg else ''}{'push' if push else ''} steps={steps}"
+        assert eng.xgmi_mode == xmode
+    return f"model={model}{'-xgmi' if xg else ''} mode={xmode} steps={steps}"
 
 
 def main():

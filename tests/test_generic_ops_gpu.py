@@ -394,6 +394,44 @@ def test_stem_conv_bf16_im2col_route(cuda_dev, R, st, pad, K, kp, hw, out_bf16):
         assert torch.equal(grads[0], grads[1])
 
 
+@pytest.mark.parametrize("hw", [(224, 224), (37, 41)])
+def test_s2d_stem_preload_bit_identical(cuda_dev, hw):
+    """The s2d stem forward with every K tile requested at once
+    (S2dLoaderPre, default) stores the same tiles in the same LDS stages as
+    the one-tile-ahead loader: outputs and BatchNorm partial rows bit for bit."""
+    from mpi_tensorflow_amd.ops import native, ptr, stream_handle
+
+    ops = native().ops
+    g = torch.Generator().manual_seed(3)
+    N, K = 4, 64
+    x = torch.randn(N, hw[0], hw[1], 3, generator=g).to(cuda_dev)
+    w = (torch.randn(7, 7, 3, K, generator=g) * 0.1).to(cuda_dev)
+    sh = ops.ConvShape(N, hw[0], hw[1], 3, K, 7, 7, 2, 3)
+    si = Fn._s2d_shape(sh)
+    s = stream_handle()
+    xs = torch.empty(N * si.H * si.W * 16, dtype=torch.bfloat16, device=cuda_dev)
+    ops.s2d_stem_input(ptr(x), N, sh.H, sh.W, sh.OH, sh.OW, ptr(xs), s)
+    wt8 = torch.empty(K * 256, dtype=torch.bfloat16, device=cuda_dev)
+    ops.s2d_stem_weight(ptr(w), K, ptr(wt8), s)
+    s1 = ops.ConvShape(N, sh.OH, sh.OW, 256, K, 1, 1, 1, 0)
+    rows = ops.conv_fwd_stem_stats_rows(s1)
+    shift = (torch.randn(K, generator=g) * 0.1).to(cuda_dev)
+    outs = []
+    try:
+        for pre in (False, True):
+            ops.s2d_stem_set_preload(pre)
+            y = torch.empty(N, sh.OH, sh.OW, K, dtype=torch.bfloat16, device=cuda_dev)
+            part = torch.empty(2 * K * rows, device=cuda_dev)
+            ops.conv_fwd_s2d_stem_bf16(si, ptr(xs), ptr(wt8), ptr(y), s, ptr(part), rows,
+                                       ptr(shift))
+            torch.cuda.synchronize()
+            outs.append((y, part))
+    finally:
+        ops.s2d_stem_set_preload(True)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+
+
 def test_bn_bf16_twin_feeds_conv(cuda_dev):
     """bf16 mode: BatchNorm writes a bf16 twin of y (forward) and dx
     (backward); the consuming conv reads it instead of converting.  The result

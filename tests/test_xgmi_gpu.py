@@ -39,14 +39,17 @@ def test_xgmi_two_ranks_bit_identical_to_buckets(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["xgmi", "xgmipush"])
+@pytest.mark.parametrize("mode", ["xgmi", "xgmipush", "xgmipull"])
 def test_xgmi_lenet5_two_ranks_fused_sync_matches_serial(mode):
     """The fused LeNet-5 executor over the xGMI communicator, bit-identical to
     the serial emulation of data parallelism (rank-order sum + flat SGD):
     xgmi - the two-phase launch (this rank's segment summed and updated,
     sharded momentum, then the other segments gathered); xgmipush - the push
     sync in the update launch (every block pushes its gradient values into the
-    peers' receive slots, one barrier, rank-order sum, replicated SGD)."""
+    peers' receive slots, one barrier, rank-order sum, replicated SGD);
+    xgmipull - the one-shot launch (every rank's double-buffered gradient slot
+    read after one barrier, rank-order sum, replicated SGD, graph-captured
+    steps alternating the slots)."""
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), HELPER, "generic",
@@ -202,3 +205,23 @@ def test_block_dispatch_order_per_xcd(cuda_dev):
     # (one spin is 20 us: a block dispatched out of order would start >= 20 us
     # before a lower id)
     assert worst <= 200, f"a block started {worst / 100:.1f} us before a lower-id block of its XCD"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["two-phase", "push", "pull"])
+def test_bench_lenet5_emulated_xgmi_modes(cuda_dev, mode):
+    """bench.py on 8 emulated xGMI ranks, LeNet-5, each sync mode: one JSON
+    line naming the mode, the gate passed, no barrier timed out."""
+    import json
+
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--model", "lenet5",
+                        "--xgmi-emulate", "1,150,8", "--xgmi-mode", mode, "--steps", "50",
+                        "--warmup", "10", "--no-eval", "--prewarm-ms", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=ROOT))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    name = {"two-phase": "xgmi", "push": "xgmi-push", "pull": "xgmi-pull"}[mode]
+    assert out["config"]["sync_schedule"] == name, out["config"]
+    assert out["config"]["xgmi_gate"] == "passed"
+    print(f"lenet5 emulated 8 ranks {mode}: {1000 * out['ms_per_step']:.2f} us/step")
