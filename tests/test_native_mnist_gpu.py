@@ -171,15 +171,19 @@ def test_per_step_grads_along_native_trajectory(cuda_dev, data, algo, max_ties, 
     assert ties <= max_ties, ties
 
 
-def test_training_trajectory_matches_oracle(cuda_dev, data):
+@pytest.mark.parametrize("algo,bound", [("winograd", 7.5e-2), ("direct", 7.5e-2)])
+def test_training_trajectory_matches_oracle(cuda_dev, data, algo, bound):
     """30 native steps vs the fp32 PyTorch oracle run on the CPU.  Both are
     deterministic (the oracle at a fixed thread count), so the drift is one
-    reproducible number - 6.69e-2 on the round-5 build (the GPU oracle's
-    MIOpen convolutions moved it 3.6e-2 .. 5.24e-2 from box to box in round
-    4) - and the bound sits just above it: a native numerics change moves it.
-    The strict per-step check is test_per_step_grads_along_native_trajectory."""
+    reproducible number per conv2 algorithm: Winograd (the default) 6.69e-2,
+    the direct 25-tap kernels 6.57e-2 (round 6; the GPU oracle's MIOpen
+    convolutions moved it 3.6e-2 .. 5.24e-2 from box to box in round 4).  The
+    two agree, so the drift is the max-pool / ReLU tie flips of fp32
+    summation order compounding over the steps, not the Winograd arithmetic;
+    the bound sits just above both: a native numerics change moves it.  The
+    strict per-step check is test_per_step_grads_along_native_trajectory."""
     x, y = data
-    cfg = C.TrainConfig(graph=False).validate()
+    cfg = C.TrainConfig(graph=False, conv_algo=algo).validate()
     nat = NativeMnistEngine(cfg, x, y, cuda_dev)
     nthreads = torch.get_num_threads()
     torch.set_num_threads(4)
@@ -203,8 +207,9 @@ def test_training_trajectory_matches_oracle(cuda_dev, data):
     # so the trajectory is compared loosely (the strict check is per step)
     d = nat.params.cpu() - ref.params
     rel_upd = (d.norm() / (ref.params - p0).norm()).item()
-    print(f"trajectory: rel_update_err={rel_upd:.3e} losses native={losses_n} ref={losses_r}")
-    assert rel_upd < 7.5e-2, rel_upd
+    print(f"trajectory ({algo}): rel_update_err={rel_upd:.3e} losses native={losses_n} "
+          f"ref={losses_r}")
+    assert rel_upd < bound, rel_upd
     for a, b in zip(losses_n, losses_r):
         assert abs(a - b) < 2e-2 * max(1.0, abs(b))
 
