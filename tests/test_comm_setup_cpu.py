@@ -83,3 +83,19 @@ def test_exactness_pattern_sums_are_exact_and_ranks_differ(n):
     # rounds use fresh data: a read of the previous round's bytes fails
     assert float((CM.exact_pattern(0, 3, count) != CM.exact_pattern(0, 5, count)).double().mean()) > 0.99
     assert np.all(np.diff([CM.exact_pattern(r, 0, 8)[0].item() for r in range(n)]) != 0)
+
+
+def test_lenet_xgmi_mode_config_and_bench_flags():
+    """LeNet-5's xGMI sync mode: validated by TrainConfig (default pull), and
+    bench.py's --xgmi-mode / --xgmi-push map onto it."""
+    assert C.TrainConfig().validate().xgmi_mode == "pull"
+    for m in C.XGMI_MODES:
+        assert C.TrainConfig(xgmi_mode=m).validate().xgmi_mode == m
+    with pytest.raises(ValueError):
+        C.TrainConfig(xgmi_mode="ring").validate()
+    assert bench.parse([]).xgmi_mode == "pull"
+    assert bench.parse(["--xgmi-mode", "two-phase"]).xgmi_mode == "two-phase"
+    a = bench.parse(["--xgmi-push"])
+    assert a.xgmi_push and ("push" if a.xgmi_push else a.xgmi_mode) == "push"
+    a = bench.parse(["--bn-fused", "on", "--bn-fused-bpc", "3"])
+    assert a.bn_fused == "on" and a.bn_fused_bpc == 3
