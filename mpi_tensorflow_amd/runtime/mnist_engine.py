@@ -437,6 +437,9 @@ class NativeMnistEngine(MnistEngineBase):
                 self.use_graph = self.use_graph and not sticky
                 torch.cuda.synchronize(self.device)
                 return None
+            # the executable goes to the device now, not inside its first
+            # (possibly timed) launch
+            self._C.graph_upload(g.raw_cuda_graph_exec(), stream_handle())
             self._graphs[key] = g
         return g
 
