@@ -371,7 +371,9 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("gcap", &gops::TiledPlan::gcap)
       .def_readwrite("vcap", &gops::TiledPlan::vcap)
       .def_readwrite("dgrad_fwd", &gops::TiledPlan::dgrad_fwd)
-      .def_readwrite("wg64", &gops::TiledPlan::wg64);
+      .def_readwrite("wg64", &gops::TiledPlan::wg64)
+      .def_readwrite("halo_f32", &gops::TiledPlan::halo_f32);
+  g.def("conv3f_ok", &gops::conv3f_ok);
   g.def("get_tiled_plan", []() { return gops::tiled_plan(); });
   g.def("set_tiled_plan", [](const gops::TiledPlan& p) { gops::tiled_plan() = p; });
   g.def("im2col_bf16", [](const gops::ConvShape& s, uintptr_t x, int kp, uintptr_t col,

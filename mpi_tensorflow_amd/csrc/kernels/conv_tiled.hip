@@ -870,6 +870,203 @@ __global__ __launch_bounds__(256) void slab_sum4_stats_kernel(const float4* __re
   }
 }
 
+// ------------------------------------ fp32 3x3 stride-1 halo conv ----
+// The fp32 port of conv_bf16.hip's conv3_kernel (forward and stride-1 dgrad
+// of ResNet-18's 3x3 layers).  The tiled fwd_kernel above re-stages the A
+// tile through L2 for each of the 9 taps, one K tile in flight: on the
+// 56x56x64 layer at B = 32 it ran 100 us, 47 % of the fp32 MFMA rate.  Here a
+// block owns BM consecutive output pixels x BN output channels and, per
+// 32-channel chunk (128-byte LDS rows, the bf16 kernel's geometry):
+//   * stages the activation halo once (the stacked image rows from one above
+//     the tile to one below) with global_load_lds_dwordx4;
+//   * reads each tap's A fragments out of it at per-lane shifted rows
+//     (padding taps read an all-zero row);
+//   * streams the 9 taps' weight tiles [BN out][32 in] through an RB-deep LDS
+//     ring, RB - 1 in flight.
+// 16-byte chunks are XOR-swizzled by ((row >> 1) & 7) through the DMA source
+// address, so a ds_read_b128 lane group reads 16 rows conflict-free.  MFMA
+// v_mfma_f32_32x32x2f32: lane (r, h) of a fragment read takes chunk 2c + h
+// (channels 8c + 4h .. + 3) and element e feeds MFMA e, so MFMA e of group c
+// reduces the channel pair {8c + e, 8c + 4 + e} on both operands.
+// Weights: wt[tap'][out][in] (in contiguous) read at tap' = 8 - t: the
+// forward passes the stride-1 dgrad copy (wflip_kernel / the SGD's kind-1
+// job: W[8 - t] transposed), the dgrad the original HWIO weights (W[8 - t]
+// with in = the conv's K is already [out = C][in = K]).
+// LDS (HCAP + 1) x 128 B + RB x BN x 128 B = 76 KiB at BN = 64, RB = 4: two
+// blocks a CU.  Split-K over channel chunks (blockIdx.y, slabs) for small M.
+namespace h3f {
+constexpr int ROWB = 128;  // bytes per LDS row: 32 fp32 channels
+constexpr int CH = 32;     // channels per chunk
+constexpr int HCAP = 344;  // halo pixel rows (multiple of 8); row HCAP is all zeros
+__device__ uint4 g_zero[4];  // never written: the DMA source of rows outside the tensor
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void glds(const void* src, char* dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+}
+inline int halo_rows(const ConvShape& s, int bm) { return ((bm + s.W - 2) / s.W + 3) * s.W; }
+}  // namespace h3f
+
+template <int BM, int BN, int RB>
+__global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __restrict__ x,
+                                                    const float* __restrict__ wt,
+                                                    float* __restrict__ y, int cps,
+                                                    const float* __restrict__ addend) {
+  using h3f::ROWB;
+  using h3f::HCAP;
+  using h3f::CH;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int GB = BN / 32;  // weight DMA instructions per wave per tap
+  constexpr int HB = (HCAP + 1) * ROWB;
+  constexpr int BSZ = BN * ROWB;
+  static_assert(RB >= 3 && RB <= 4, "ring depth");
+  __shared__ __attribute__((aligned(1024))) char smem[HB + RB * BSZ];
+  const int M = s.N * s.H * s.W;
+  const int W = s.W, H = s.H;
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;
+  const int nch = s.C / CH;
+  const int cc0 = blockIdx.y * cps, cc1 = min(nch, cc0 + cps);
+  const int g_first = m0 / W, g_last = (min(m0 + BM, M) - 1) / W;
+  const long long hbase = (long long)(g_first - 1) * W;  // global pixel of halo row 0
+  const int npix = (g_last - g_first + 3) * W;
+  const int nins = (npix + 7) >> 3;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5, lr = lane >> 3;
+  if (tid < 8) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  int gl[TM], oxs[TM], oys[TM];
+  bool mv[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / 2) + 32 * i + r;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : m0;
+    const int g = mm / W;
+    oxs[i] = mm - g * W;
+    oys[i] = g % H;
+    gl[i] = g - g_first + 1;
+  }
+  const float* bsrc[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = wave * (BN / 4) + 8 * j + lr;
+    bsrc[j] = wt + (size_t)(n0 + row) * s.C + 4 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  auto issue_b = [&](int tap, int cc, int slot) {
+    const size_t o = (size_t)(8 - tap) * s.K * s.C + (size_t)cc * CH;
+    char* dst = smem + HB + slot * BSZ + wave * (BN / 4) * ROWB;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) h3f::glds(bsrc[j] + o, dst + 8 * j * ROWB);
+  };
+  auto issue_halo = [&](int cc) {
+    for (int ins = wave; ins < nins; ins += 4) {
+      const int p = 8 * ins + lr;
+      const long long gp = hbase + p;
+      const bool ok = p < npix && gp >= 0 && gp < M;
+      const void* src = ok ? (const void*)(x + gp * s.C + (size_t)cc * CH +
+                                           4 * ((lane & 7) ^ ((p >> 1) & 7)))
+                           : (const void*)h3f::g_zero;
+      h3f::glds(src, smem + ins * 8 * ROWB);
+    }
+  };
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = zero16();
+  for (int cc = cc0; cc < cc1; ++cc) {
+    // the previous chunk's halo and ring reads are done (and the zero row is written)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_halo(cc);
+#pragma unroll
+    for (int t = 0; t < RB - 1; ++t) issue_b(t, cc, t);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ahead = min(RB - 2, 8 - t);
+      if (ahead >= 2)
+        h3f::wait_vm<2 * GB>();
+      else if (ahead == 1)
+        h3f::wait_vm<GB>();
+      else
+        h3f::wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring slot (t - 1) % RB read
+      __builtin_amdgcn_s_barrier();
+      if (t + RB - 1 < 9) issue_b(t + RB - 1, cc, (t + RB - 1) % RB);
+      const int kh = t / 3, kw = t - 3 * kh;
+      int hrow[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int iy = oys[i] + kh - 1, ix = oxs[i] + kw - 1;
+        const bool ok = mv[i] && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        hrow[i] = ok ? (gl[i] + kh - 1) * W + ix : HCAP;
+      }
+      const char* B = smem + HB + (t % RB) * BSZ;
+#pragma unroll
+      for (int c = 0; c < CH / 8; ++c) {
+        const int ck = 2 * c + h;
+        float4 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const float4*>(smem + hrow[i] * ROWB +
+                                                  ((ck ^ ((hrow[i] >> 1) & 7)) << 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int R = wn * (BN / 2) + 32 * j + r;
+          b[j] = *reinterpret_cast<const float4*>(B + R * ROWB + ((ck ^ ((R >> 1) & 7)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = mfma32x32x2(a[i].x, b[j].x, acc[i][j]);
+            acc[i][j] = mfma32x32x2(a[i].y, b[j].y, acc[i][j]);
+            acc[i][j] = mfma32x32x2(a[i].z, b[j].z, acc[i][j]);
+            acc[i][j] = mfma32x32x2(a[i].w, b[j].w, acc[i][j]);
+          }
+      }
+    }
+  }
+  // epilogue (conv_bf16.hip conv3_kernel EPI 0): lane (r, h) of 32 x 32 tile
+  // (i, j) holds rows 4h + (q & 3) + 8 (q >> 2), column r; the addend (a
+  // gradient join, unsplit only) loaded for the tile before its stores
+  y += (size_t)blockIdx.y * M * s.K;
+  const size_t K = s.K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = m0 + wm * (BM / 2) + 32 * i + 4 * h;
+    const bool full = m0 + wm * (BM / 2) + 32 * i + 32 <= M;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int co = n0 + wn * (BN / 2) + 32 * j + r;
+      float* p = y + (size_t)mb * K + co;
+      if (full && addend) {
+        const float* ap = addend + (size_t)mb * K + co;
+        float av[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) av[q] = ap[(size_t)((q & 3) + 8 * (q >> 2)) * K];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[(size_t)((q & 3) + 8 * (q >> 2)) * K] = acc[i][j][q] + av[q];
+      } else if (full) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) p[(size_t)((q & 3) + 8 * (q >> 2)) * K] = acc[i][j][q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int rr = (q & 3) + 8 * (q >> 2);
+          if (mb + rr >= M) continue;
+          float v = acc[i][j][q];
+          if (addend) v += addend[(size_t)(mb + rr) * K + co];
+          p[(size_t)rr * K] = v;
+        }
+      }
+    }
+  }
+}
+
 // Stride-1 backward-data as a forward conv of dY (fp32): dX = conv(dY, W')
 // with pad R - 1 - pad and W'[kh][kw][co][ci] = W[R-1-kh][S-1-kw][ci][co].
 // The forward kernel's operands are both float4 rows into LDS; the dgrad
@@ -1022,9 +1219,55 @@ static long long dgrad_fwd_ws_floats(const ConvShape& s) {
   return wf + conv_fwd_tiled_ws_floats(dgrad_fwd_shape(s), false);
 }
 
+// fp32 3x3 stride-1 halo conv (conv3f_kernel): block rows, channel-chunk split
+static bool conv3f_plan(const ConvShape& s, int& bm, int& z, int& cps) {
+  using namespace tiled;
+  if (!tiled_plan().halo_f32) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.OH == s.H && s.OW == s.W))
+    return false;
+  if (s.C % h3f::CH || s.K % 64 || (long long)s.N * s.H * s.W * std::max(s.C, s.K) >= (1LL << 31))
+    return false;
+  const long long M = (long long)s.N * s.H * s.W;
+  bm = (cdiv(M, 128) * (s.K / 64) >= 256 && h3f::halo_rows(s, 128) <= h3f::HCAP) ? 128 : 64;
+  if (h3f::halo_rows(s, bm) > h3f::HCAP) return false;
+  const long long blocks = cdiv(M, bm) * (s.K / 64);
+  const int nch = s.C / h3f::CH;
+  z = 1;
+  if (blocks < 512) z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
+  cps = cdiv(nch, z);
+  z = cdiv(nch, cps);
+  return true;
+}
+bool conv3f_ok(const ConvShape& s) {
+  int bm, z, cps;
+  return conv3f_plan(s, bm, z, cps);
+}
+long long conv3f_ws_floats(const ConvShape& s) {
+  int bm, z, cps;
+  if (!conv3f_plan(s, bm, z, cps) || z == 1) return 0;
+  return (long long)z * s.N * s.H * s.W * s.K;
+}
+// wt: [9][K][C] read at tap 8 - t (see conv3f_kernel)
+void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float* ws,
+            hipStream_t st, const float* addend) {
+  using namespace tiled;
+  int bm, z, cps;
+  if (!conv3f_plan(s, bm, z, cps)) throw std::runtime_error("conv3f: unsupported shape");
+  if (z > 1 && !ws) throw std::runtime_error("conv3f: split-K needs a workspace");
+  const long long M = (long long)s.N * s.H * s.W;
+  float* out = z > 1 ? ws : y;
+  const float* add = z > 1 ? nullptr : addend;
+  const dim3 grid(cdiv(M, bm) * (s.K / 64), z);
+  if (bm == 128)
+    conv3f_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, cps, add);
+  else
+    conv3f_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, cps, add);
+  if (z > 1) slab_sum(ws, z, M * s.K, y, st, addend);
+}
+
 // workspace for either operand precision (the plans differ in tile shape)
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
-  long long n = 0;
+  long long n = conv3f_ws_floats(s);
   for (const bool b : {false, true}) {
     tiled::Tile t;
     int z, kps;
@@ -1036,6 +1279,7 @@ long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
 
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
   long long n = dgrad_fwd_ok(s) ? dgrad_fwd_ws_floats(s) : 0;
+  if (dgrad_fwd_ok(s)) n = std::max(n, conv3f_ws_floats(dgrad_fwd_shape(s)));
   for (const bool b : {false, true}) {
     tiled::Tile t;
     int z, kps;
@@ -1112,6 +1356,10 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
   using namespace tiled;
   if (!bf16 && dy && ws && dgrad_fwd_ok(s)) {
     const ConvShape f = dgrad_fwd_shape(s);
+    if (conv3f_ok(f)) {  // the halo kernel reads W itself, taps reversed (conv3f_kernel)
+      conv3f(f, dy, w, dx, ws, st, addend);
+      return;
+    }
     float* fws = ws + ((long long)s.R * s.S * s.C * s.K + 3) / 4 * 4;
     const float* wt = wflip;  // kept current by the step's SGD (gops::sgd_wcvt)
     if (!wt) {

@@ -162,7 +162,15 @@ struct TiledPlan {
   int vcap = 64;                          // filter gradient slice cap, vector path
   bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
   bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
+  bool halo_f32 = true;                   // fp32 3x3 stride-1 convs on conv3f_kernel
 };
+// fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
+// [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy
+// (wflip layout), the dgrad the HWIO weights; ws: conv3f_ws_floats
+bool conv3f_ok(const ConvShape& s);
+long long conv3f_ws_floats(const ConvShape& s);
+void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float* ws,
+            hipStream_t st, const float* addend);
 TiledPlan& tiled_plan();
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s);
 int conv_filter_tiled_splits(const ConvShape& s);

@@ -1017,6 +1017,10 @@ void conv_fwd(const ConvShape& s, const float* x, const float* w, const float* b
       throw std::runtime_error("conv_fwd: BatchNorm statistics need the bf16 or fp32 tiled family");
     return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, false, stats);
   }
+  // fp32 with the stride-1 dgrad weight copy (wtb, ConvWeightCopies f32flip):
+  // the 3x3 stride-1 layers on the halo kernel
+  if (!bf16 && wtb && !bias && !relu && conv3f_ok(s))
+    return conv3f(s, x, static_cast<const float*>(wtb), y, ws, st, nullptr);
   if (conv_fwd_tiled_ok(s)) return conv_fwd_tiled(s, x, w, bias, y, relu, ws, st, bf16);
   if (conv_fwd_direct_ok(s)) {
     const long long total = (long long)s.N * s.OH * s.OW * s.K;

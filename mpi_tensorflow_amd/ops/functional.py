@@ -359,8 +359,11 @@ class _ConvFn(torch.autograd.Function):
             # bf16 output: the bf16 family; fp32: the tiled forward (conv2d checks)
             rows = C.ops.conv_fwd_stats_rows(shape, bool(out_bf16))
             part = torch.empty(2 * shape.K * rows, dtype=torch.float32, device=x.device)
+        # fp32: the stride-1 dgrad copy (f32flip) also feeds the forward's halo
+        # kernel (conv_tiled.hip conv3f_kernel reads it with the taps reversed)
         C.ops.conv_fwd(shape, ptr(x), ptr(w), ptr(b), 0 if out_bf16 else ptr(y), relu, ptr(ws), s,
-                       ctx.bf16, ptr(xb), ptr(wtb), ptr(y) if out_bf16 else 0, ptr(part), rows,
+                       ctx.bf16, ptr(xb), ptr(wtb if ctx.bf16 else wtb_d),
+                       ptr(y) if out_bf16 else 0, ptr(part), rows,
                        ptr(bn_out.shift) if part is not None else 0)
         if part is not None:
             bn_out.fwd = (part, rows)

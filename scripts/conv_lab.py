@@ -65,11 +65,20 @@ def main():
         xb = dyb = None
         if bf16 and g.conv_bf16_ok(sh):
             xb, dyb = x.to(torch.bfloat16), dy.to(torch.bfloat16)
+        # fp32: the engine's stride-1 dgrad weight copy (ConvWeightCopies
+        # f32flip), which the fp32 dgrad and the halo forward read
+        wfl = None
+        if not bf16 and R > 1 and Cin % 32 == 0 and K % 32 == 0:
+            from mpi_tensorflow_amd.ops import functional as Fn
+            prm = Fn.Param(w, dw)
+            wc = Fn.ConvWeightCopies({"w": prm}, dev, kind="f32flip")
+            wc.refresh()
+            wfl = prm.wtb_d
         ops = {
             "fwd": lambda: g.conv_fwd(sh, ptr(x), ptr(w), 0, ptr(y), False, ptr(ws), s, bf16,
-                                      ptr(xb)),
+                                      ptr(xb), ptr(wfl)),
             "dgrad": lambda: g.conv_bwd_data(sh, ptr(dy), ptr(w), ptr(dx), ptr(ws), s, bf16,
-                                             ptr(dyb)),
+                                             ptr(dyb), 0, ptr(wfl)),
             "wgrad": lambda: g.conv_bwd_filter(sh, ptr(x), ptr(dy), ptr(ws), ptr(dw), s, bf16,
                                                ptr(xb), ptr(dyb)),
         }
