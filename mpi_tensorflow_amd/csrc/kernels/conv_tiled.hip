@@ -876,15 +876,16 @@ __global__ __launch_bounds__(256) void slab_sum4_stats_kernel(const float4* __re
 // tile through L2 for each of the 9 taps, one K tile in flight: on the
 // 56x56x64 layer at B = 32 it ran 100 us, 47 % of the fp32 MFMA rate.  Here a
 // block owns BM consecutive output pixels x BN output channels and, per
-// 32-channel chunk (128-byte LDS rows, the bf16 kernel's geometry):
+// CH-channel chunk (CH = 32: 128-byte LDS rows, the bf16 kernel's geometry;
+// CH = 16: 64-byte rows, so 128-column weight tiles still fit two blocks a CU):
 //   * stages the activation halo once (the stacked image rows from one above
 //     the tile to one below) with global_load_lds_dwordx4;
 //   * reads each tap's A fragments out of it at per-lane shifted rows
 //     (padding taps read an all-zero row);
 //   * streams the 9 taps' weight tiles [BN out][32 in] through an RB-deep LDS
 //     ring, RB - 1 in flight.
-// 16-byte chunks are XOR-swizzled by ((row >> 1) & 7) through the DMA source
-// address, so a ds_read_b128 lane group reads 16 rows conflict-free.  MFMA
+// 16-byte pieces are XOR-swizzled by the row's bank line (h3f::Geo) through the
+// DMA source address, so a ds_read_b128 lane group reads 16 rows conflict-free.  MFMA
 // v_mfma_f32_32x32x2f32: lane (r, h) of a fragment read takes chunk 2c + h
 // (channels 8c + 4h .. + 3) and element e feeds MFMA e, so MFMA e of group c
 // reduces the channel pair {8c + e, 8c + 4 + e} on both operands.
@@ -892,12 +893,14 @@ __global__ __launch_bounds__(256) void slab_sum4_stats_kernel(const float4* __re
 // forward passes the stride-1 dgrad copy (wflip_kernel / the SGD's kind-1
 // job: W[8 - t] transposed), the dgrad the original HWIO weights (W[8 - t]
 // with in = the conv's K is already [out = C][in = K]).
-// LDS (HCAP + 1) x 128 B + RB x BN x 128 B = 76 KiB at BN = 64, RB = 4: two
-// blocks a CU.  Split-K over channel chunks (blockIdx.y, slabs) for small M.
+// LDS (HCAP + 1) x 4 CH + RB x BN x 4 CH bytes: 77 KiB at (BN 64, CH 32),
+// 54 KiB at (BN 128, CH 16), RB = 4: two blocks a CU.  Split-K over channel
+// chunks (blockIdx.y, slabs) for small M.
 namespace h3f {
-constexpr int ROWB = 128;  // bytes per LDS row: 32 fp32 channels
-constexpr int CH = 32;     // channels per chunk
-constexpr int HCAP = 344;  // halo pixel rows (multiple of 8); row HCAP is all zeros
+// halo pixel rows, a multiple of every RPI (the DMA fills whole groups of RPI
+// rows, so the last group of a halo of <= HCAP pixels ends at or below row
+// HCAP - 1); row HCAP is all zeros
+constexpr int HCAP = 352;
 __device__ uint4 g_zero[4];  // never written: the DMA source of rows outside the tensor
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -907,21 +910,34 @@ __device__ __forceinline__ void glds(const void* src, char* dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
 }
 inline int halo_rows(const ConvShape& s, int bm) { return ((bm + s.W - 2) / s.W + 3) * s.W; }
+// LDS row geometry of a CH-channel chunk: NCK 16-byte pieces a row, the piece
+// index XOR-swizzled by the row's 256-byte bank line (RPL rows a line), so a
+// ds_read_b128 lane group (16 consecutive rows, one piece each) is conflict-free
+template <int CH>
+struct Geo {
+  static constexpr int ROWB = CH * 4;
+  static constexpr int NCK = CH / 4;
+  static constexpr int RPL = 256 / ROWB;
+  static constexpr int RPI = 64 / NCK;  // rows one wave-wide DMA instruction fills
+  __device__ static __forceinline__ int swz(int row) { return (row / RPL) & (NCK - 1); }
+};
 }  // namespace h3f
 
-template <int BM, int BN, int RB>
+template <int BM, int BN, int RB, int CH>
 __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __restrict__ x,
                                                     const float* __restrict__ wt,
                                                     float* __restrict__ y, int cps,
                                                     const float* __restrict__ addend) {
-  using h3f::ROWB;
   using h3f::HCAP;
-  using h3f::CH;
+  using G3 = h3f::Geo<CH>;
+  constexpr int ROWB = G3::ROWB, NCK = G3::NCK, RPI = G3::RPI;
   constexpr int TM = BM / 64, TN = BN / 64;
-  constexpr int GB = BN / 32;  // weight DMA instructions per wave per tap
+  constexpr int GB = (BN / 4) / RPI;  // weight DMA instructions per wave per tap
   constexpr int HB = (HCAP + 1) * ROWB;
   constexpr int BSZ = BN * ROWB;
   static_assert(RB >= 3 && RB <= 4, "ring depth");
+  static_assert(GB >= 1 && (BN / 4) % RPI == 0, "weight rows per wave");
+  static_assert(HCAP % RPI == 0, "halo DMA groups end below the zero row");
   __shared__ __attribute__((aligned(1024))) char smem[HB + RB * BSZ];
   const int M = s.N * s.H * s.W;
   const int W = s.W, H = s.H;
@@ -933,10 +949,10 @@ __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __
   const int g_first = m0 / W, g_last = (min(m0 + BM, M) - 1) / W;
   const long long hbase = (long long)(g_first - 1) * W;  // global pixel of halo row 0
   const int npix = (g_last - g_first + 3) * W;
-  const int nins = (npix + 7) >> 3;
+  const int nins = (npix + RPI - 1) / RPI;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
-  const int r = lane & 31, h = lane >> 5, lr = lane >> 3;
-  if (tid < 8) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  const int r = lane & 31, h = lane >> 5, lr = lane / NCK, lp = lane % NCK;
+  if (tid < NCK) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
   int gl[TM], oxs[TM], oys[TM];
   bool mv[TM];
 #pragma unroll
@@ -952,24 +968,23 @@ __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __
   const float* bsrc[GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
-    const int row = wave * (BN / 4) + 8 * j + lr;
-    bsrc[j] = wt + (size_t)(n0 + row) * s.C + 4 * ((lane & 7) ^ ((row >> 1) & 7));
+    const int row = wave * (BN / 4) + RPI * j + lr;
+    bsrc[j] = wt + (size_t)(n0 + row) * s.C + 4 * (lp ^ G3::swz(row));
   }
   auto issue_b = [&](int tap, int cc, int slot) {
     const size_t o = (size_t)(8 - tap) * s.K * s.C + (size_t)cc * CH;
     char* dst = smem + HB + slot * BSZ + wave * (BN / 4) * ROWB;
 #pragma unroll
-    for (int j = 0; j < GB; ++j) h3f::glds(bsrc[j] + o, dst + 8 * j * ROWB);
+    for (int j = 0; j < GB; ++j) h3f::glds(bsrc[j] + o, dst + RPI * j * ROWB);
   };
   auto issue_halo = [&](int cc) {
     for (int ins = wave; ins < nins; ins += 4) {
-      const int p = 8 * ins + lr;
+      const int p = RPI * ins + lr;
       const long long gp = hbase + p;
       const bool ok = p < npix && gp >= 0 && gp < M;
-      const void* src = ok ? (const void*)(x + gp * s.C + (size_t)cc * CH +
-                                           4 * ((lane & 7) ^ ((p >> 1) & 7)))
+      const void* src = ok ? (const void*)(x + gp * s.C + (size_t)cc * CH + 4 * (lp ^ G3::swz(p)))
                            : (const void*)h3f::g_zero;
-      h3f::glds(src, smem + ins * 8 * ROWB);
+      h3f::glds(src, smem + ins * RPI * ROWB);
     }
   };
   f32x16 acc[TM][TN];
@@ -1012,11 +1027,11 @@ __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           a[i] = *reinterpret_cast<const float4*>(smem + hrow[i] * ROWB +
-                                                  ((ck ^ ((hrow[i] >> 1) & 7)) << 4));
+                                                  ((ck ^ G3::swz(hrow[i])) << 4));
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int R = wn * (BN / 2) + 32 * j + r;
-          b[j] = *reinterpret_cast<const float4*>(B + R * ROWB + ((ck ^ ((R >> 1) & 7)) << 4));
+          b[j] = *reinterpret_cast<const float4*>(B + R * ROWB + ((ck ^ G3::swz(R)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1220,49 +1235,64 @@ static long long dgrad_fwd_ws_floats(const ConvShape& s) {
 }
 
 // fp32 3x3 stride-1 halo conv (conv3f_kernel): block rows, channel-chunk split
-static bool conv3f_plan(const ConvShape& s, int& bm, int& z, int& cps) {
+// TiledPlan halo_f32_wide: 128-column tiles on 16-channel chunks where K allows
+struct C3fPlan {
+  int bm, bn, ch, z, cps;
+};
+static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   using namespace tiled;
   if (!tiled_plan().halo_f32) return false;
   if (!(s.R == 3 && s.S == 3 && s.stride == 1 && s.pad == 1 && s.OH == s.H && s.OW == s.W))
     return false;
-  if (s.C % h3f::CH || s.K % 64 || (long long)s.N * s.H * s.W * std::max(s.C, s.K) >= (1LL << 31))
+  if (s.C % 32 || s.K % 64 || (long long)s.N * s.H * s.W * std::max(s.C, s.K) >= (1LL << 31))
     return false;
   const long long M = (long long)s.N * s.H * s.W;
-  bm = (cdiv(M, 128) * (s.K / 64) >= 256 && h3f::halo_rows(s, 128) <= h3f::HCAP) ? 128 : 64;
-  if (h3f::halo_rows(s, bm) > h3f::HCAP) return false;
-  const long long blocks = cdiv(M, bm) * (s.K / 64);
-  const int nch = s.C / h3f::CH;
-  z = 1;
-  if (blocks < 512) z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
-  cps = cdiv(nch, z);
-  z = cdiv(nch, cps);
+  const bool wide = tiled_plan().halo_f32_wide && s.K % 128 == 0;
+  p.bn = wide ? 128 : 64;
+  p.ch = wide ? 16 : 32;
+  p.bm = (cdiv(M, 128) * (s.K / p.bn) >= 256 && h3f::halo_rows(s, 128) <= h3f::HCAP) ? 128 : 64;
+  if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
+  const long long blocks = cdiv(M, p.bm) * (s.K / p.bn);
+  const int nch = s.C / p.ch;
+  p.z = 1;
+  if (blocks < 512) p.z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
+  p.cps = cdiv(nch, p.z);
+  p.z = cdiv(nch, p.cps);
   return true;
 }
 bool conv3f_ok(const ConvShape& s) {
-  int bm, z, cps;
-  return conv3f_plan(s, bm, z, cps);
+  C3fPlan p;
+  return conv3f_plan(s, p);
 }
 long long conv3f_ws_floats(const ConvShape& s) {
-  int bm, z, cps;
-  if (!conv3f_plan(s, bm, z, cps) || z == 1) return 0;
-  return (long long)z * s.N * s.H * s.W * s.K;
+  C3fPlan p;
+  if (!conv3f_plan(s, p) || p.z == 1) return 0;
+  return (long long)p.z * s.N * s.H * s.W * s.K;
 }
 // wt: [9][K][C] read at tap 8 - t (see conv3f_kernel)
 void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float* ws,
             hipStream_t st, const float* addend) {
   using namespace tiled;
-  int bm, z, cps;
-  if (!conv3f_plan(s, bm, z, cps)) throw std::runtime_error("conv3f: unsupported shape");
-  if (z > 1 && !ws) throw std::runtime_error("conv3f: split-K needs a workspace");
+  C3fPlan p;
+  if (!conv3f_plan(s, p)) throw std::runtime_error("conv3f: unsupported shape");
+  if (p.z > 1 && !ws) throw std::runtime_error("conv3f: split-K needs a workspace");
   const long long M = (long long)s.N * s.H * s.W;
-  float* out = z > 1 ? ws : y;
-  const float* add = z > 1 ? nullptr : addend;
-  const dim3 grid(cdiv(M, bm) * (s.K / 64), z);
-  if (bm == 128)
-    conv3f_kernel<128, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, cps, add);
-  else
-    conv3f_kernel<64, 64, 4><<<grid, NT, 0, st>>>(s, x, wt, out, cps, add);
-  if (z > 1) slab_sum(ws, z, M * s.K, y, st, addend);
+  float* out = p.z > 1 ? ws : y;
+  const float* add = p.z > 1 ? nullptr : addend;
+  const dim3 grid(cdiv(M, p.bm) * (s.K / p.bn), p.z);
+#define C3F(BM_, BN_, CH_) conv3f_kernel<BM_, BN_, 4, CH_><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add)
+  if (p.bn == 128) {
+    if (p.bm == 128)
+      C3F(128, 128, 16);
+    else
+      C3F(64, 128, 16);
+  } else if (p.bm == 128) {
+    C3F(128, 64, 32);
+  } else {
+    C3F(64, 64, 32);
+  }
+#undef C3F
+  if (p.z > 1) slab_sum(ws, p.z, M * s.K, y, st, addend);
 }
 
 // workspace for either operand precision (the plans differ in tile shape)

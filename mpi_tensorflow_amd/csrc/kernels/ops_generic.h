@@ -163,6 +163,9 @@ struct TiledPlan {
   bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
   bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
   bool halo_f32 = true;                   // fp32 3x3 stride-1 convs on conv3f_kernel
+  // ... with 128-column tiles on 16-channel chunks for K % 128 == 0: measured a
+  // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off
+  bool halo_f32_wide = false;
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy

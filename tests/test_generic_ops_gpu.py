@@ -435,16 +435,18 @@ def test_s2d_stem_preload_bit_identical(cuda_dev, hw):
 @pytest.mark.parametrize("N,H,W,C,K", [
     (8, 56, 56, 64, 64),    # 128-row tiles (ResNet layer 1 at B = 8), unsplit
     (2, 56, 56, 64, 64),    # 64-row tiles, 2 channel-chunk slices
-    (4, 14, 14, 256, 256),  # split-K over 8 chunks
+    (4, 14, 14, 256, 256),  # split-K over the channel chunks
+    (4, 28, 28, 128, 128),  # 128-row x 128-column tiles on the wide path
     (3, 7, 7, 512, 512),    # 16 chunks, partial last tile
     (2, 13, 9, 32, 64),     # odd image, one chunk
 ])
 def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
     """fp32 3x3 / stride 1 / pad 1 convs on the halo kernel (conv_tiled.hip
-    conv3f_kernel): forward (reading the f32flip weight copy, taps reversed)
-    and the stride-1 dgrad (the HWIO weights, taps reversed), against a
-    float64 torch reference and against the tiled kernels (TiledPlan
-    halo_f32 = False), through Fn.conv2d as the engine runs it."""
+    conv3f_kernel: forward reading the f32flip weight copy, taps reversed, and
+    the stride-1 dgrad reading the HWIO weights, taps reversed) against a
+    float64 torch reference and against the tiled kernels (TiledPlan halo_f32
+    = False), through Fn.conv2d as the engine runs it (the filter gradient,
+    tiled either way, checked alongside)."""
     from mpi_tensorflow_amd.ops import native
 
     ops = native().ops
@@ -454,15 +456,18 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
     w = torch.randn(3, 3, C, K, generator=g) * (9 * C) ** -0.5
     dy = torch.randn(N, H, W, K, generator=g)
     xr = x.double().requires_grad_(True)
-    yr = F.conv2d(xr.permute(0, 3, 1, 2), w.double().permute(3, 2, 0, 1),
+    wr = w.double().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1),
                   padding=1).permute(0, 2, 3, 1)
     yr.backward(dy.double())
     plan = ops.get_tiled_plan()
     outs = []
     try:
-        for halo in (True, False):
+        # the halo kernel with 128-column tiles on 16-channel chunks (K % 128
+        # == 0), with 64-column tiles on 32-channel chunks, and the tiled kernels
+        for halo, wide in ((True, True), (True, False), (False, False)):
             p = ops.get_tiled_plan()
-            p.halo_f32 = halo
+            p.halo_f32, p.halo_f32_wide = halo, wide
             ops.set_tiled_plan(p)
             wp = _param(w.to(cuda_dev))
             Fn.ConvWeightCopies({"w": wp}, cuda_dev, kind="f32flip").refresh()
@@ -470,13 +475,16 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
             yg = Fn.conv2d(xg, wp, None, 1, 1, False)
             yg.backward(dy.to(cuda_dev))
             torch.cuda.synchronize()
-            outs.append((yg.detach().cpu(), xg.grad.cpu()))
+            outs.append((yg.detach().cpu(), xg.grad.cpu(), wp.grad_view.detach().cpu().clone()))
     finally:
         ops.set_tiled_plan(plan)
-    for yv, dx in outs:
+    for yv, dx, dw in outs:
         assert _rel(yv.double(), yr.detach()) < 1e-5
         assert _rel(dx.double(), xr.grad) < 1e-5
-    assert _rel(outs[0][0], outs[1][0]) < 1e-5 and _rel(outs[0][1], outs[1][1]) < 1e-5
+        assert _rel(dw.double(), wr.grad) < 1e-5
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert _rel(a, b) < 1e-5
 
 
 def test_bn_bf16_twin_feeds_conv(cuda_dev):
