@@ -1251,6 +1251,7 @@ static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   p.bn = wide ? 128 : 64;
   p.ch = wide ? 16 : 32;
   p.bm = (cdiv(M, 128) * (s.K / p.bn) >= 256 && h3f::halo_rows(s, 128) <= h3f::HCAP) ? 128 : 64;
+  if (tiled_plan().halo_f32_bm == 64 || tiled_plan().halo_f32_bm == 128) p.bm = tiled_plan().halo_f32_bm;
   if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
   const long long blocks = cdiv(M, p.bm) * (s.K / p.bn);
   const int nch = s.C / p.ch;
