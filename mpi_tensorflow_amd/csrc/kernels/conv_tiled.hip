@@ -1250,8 +1250,9 @@ static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   const bool wide = tiled_plan().halo_f32_wide && s.K % 128 == 0;
   p.bn = wide ? 128 : 64;
   p.ch = wide ? 16 : 32;
-  p.bm = (cdiv(M, 128) * (s.K / p.bn) >= 256 && h3f::halo_rows(s, 128) <= h3f::HCAP) ? 128 : 64;
-  if (tiled_plan().halo_f32_bm == 64 || tiled_plan().halo_f32_bm == 128) p.bm = tiled_plan().halo_f32_bm;
+  // 64-row blocks: conv_lab fp32 fwd + dgrad 2201 us a step against 2223 with
+  // 128-row blocks where the grid allows them (2312 with 128 everywhere)
+  p.bm = tiled_plan().halo_f32_bm == 128 ? 128 : 64;
   if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
   const long long blocks = cdiv(M, p.bm) * (s.K / p.bn);
   const int nch = s.C / p.ch;

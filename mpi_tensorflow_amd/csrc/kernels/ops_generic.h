@@ -166,7 +166,7 @@ struct TiledPlan {
   // ... with 128-column tiles on 16-channel chunks for K % 128 == 0: measured a
   // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off
   bool halo_f32_wide = false;
-  int halo_f32_bm = 0;                    // conv3f block rows: 0 = by grid size, else 64 / 128 (labs)
+  int halo_f32_bm = 64;                   // conv3f block rows: 64, or 128 (labs)
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy
