@@ -75,6 +75,9 @@ def parse(argv=None):
                          "the separate finalize launch (A/B; default: the library's)")
     ap.add_argument("--bn-fused-bpc", type=int, default=None,
                     help="fused BatchNorm grid: blocks a CU (1..8)")
+    ap.add_argument("--tiled-plan", default="",
+                    help="generic conv TiledPlan overrides, k=v comma list (A/B labs; "
+                         "e.g. vcap=128,halo_f32_bm=128)")
     ap.add_argument("--xgmi-mode", default="pull", choices=("two-phase", "push", "pull"),
                     help="lenet5 over xGMI: the two-phase all-reduce + SGD launch, the push sync "
                          "fused into the update launch, or the one-barrier pull of every rank's "
@@ -217,8 +220,16 @@ def main(argv=None) -> int:
     device = D.resolve_device("auto")
     di = D.init(str(device))
     N = di.world
-    if device.type == "cuda" and (a.bn_fused is not None or a.bn_fused_bpc is not None):
+    if device.type == "cuda" and (a.bn_fused is not None or a.bn_fused_bpc is not None
+                                  or a.tiled_plan):
         from mpi_tensorflow_amd.ops import native as _native
+        if a.tiled_plan:
+            plan = _native().ops.get_tiled_plan()
+            for kv in a.tiled_plan.split(","):
+                k, v = kv.split("=")
+                cur = getattr(plan, k)
+                setattr(plan, k, (v not in ("0", "false")) if isinstance(cur, bool) else int(v))
+            _native().ops.set_tiled_plan(plan)
         if a.bn_fused is not None:
             _native().ops.bn_set_fused(a.bn_fused == "on")
         if a.bn_fused_bpc is not None:

@@ -548,10 +548,50 @@ __global__ __launch_bounds__(NT) void data_b16_kernel(ConvShape s, const __bf16*
 }
 
 // ----------------------------------------------------- backward-filter ----
+// XCD-aware split-K order.  Block b runs on XCD (b + o) mod 8 and each XCD
+// dispatches its blocks in id order, so with the slice count a multiple of 8
+// XCD x gets the slices z = x (mod 8), each with all of its tiles back to back:
+// every tap / channel tile of a pixel slice reads that slice's X and dY rows,
+// which then come from one L2 instead of up to eight (the 56x56 layer's nine
+// tap blocks of a slice otherwise landed on nine consecutive ids: eight XCDs).
+__device__ __forceinline__ int xcd_slice_bid(int bid, int tiles, bool xcd) {
+  if (!xcd || gridDim.x % (8 * tiles)) return bid;
+  const int x = bid & 7, idx = bid >> 3;
+  return (x + 8 * (idx / tiles)) * tiles + idx % tiles;
+}
+
 // dW[tap][ci][co] = sum_{pix} X[pix shifted by tap][ci] dY[pix][co]; per
 // block: one tap, a BM x BN (ci x co) tile, one split-K slice of the pixels;
 // K tile = 32 output pixels.  Both operands load float4 along their channel
 // axis straight into the k-major LDS image.  Requires C % 4 == 0, K % 4 == 0.
+// Output-pixel coordinates of one A row of the filter-gradient loaders, walked
+// forward BK pixels a K tile: mainloop calls load(kt) for kt = k0, k0 + 1, ...
+// in order, so the four runtime integer divisions per row per tile (~200 VALU
+// instructions a K tile per wave, more than the tile's 16 MFMAs could hide)
+// happen once per thread.  Past the last pixel the walk runs on (n >= N); the
+// loaders clamp the image index and mask the row by its pixel index.
+struct PixWalk {
+  int n, oy, ox;
+  __device__ __forceinline__ void init(const ConvShape& s, int pix) {
+    ox = pix % s.OW;
+    const int t = pix / s.OW;
+    oy = t % s.OH;
+    n = t / s.OH;
+  }
+  __device__ __forceinline__ void step(const ConvShape& s, int dox, int doy) {
+    ox += dox;
+    oy += doy;
+    if (ox >= s.OW) {
+      ox -= s.OW;
+      ++oy;
+    }
+    while (oy >= s.OH) {
+      oy -= s.OH;
+      ++n;
+    }
+  }
+};
+
 template <int BM, int BN>
 struct FilterLoader {
   static constexpr int AR = BM * BK / 4 / NT;
@@ -559,15 +599,21 @@ struct FilterLoader {
   ConvShape s;
   const float* x;
   const float* dy;
-  int m0, n0, kh, kw, pix0, npix;
+  int m0, n0, kh, kw, pix0, npix, dox, doy;
+  PixWalk pw[AR];
   float4 ra[AR], rb[BR];
   __device__ FilterLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0_, int n0_,
                           int tap, int pix0_, int npix_)
       : s(s_), x(x_), dy(dy_), m0(m0_), n0(n0_), pix0(pix0_), npix(npix_) {
     kh = tap / s.S;
     kw = tap % s.S;
+    dox = BK % s.OW;
+    doy = BK / s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      pw[i].init(s, min(pix0 + (int)threadIdx.x / (BM / 4) + (NT / (BM / 4)) * i, npix - 1));
   }
-  __device__ __forceinline__ void load(int kt) {
+  __device__ __forceinline__ void load(int kt) {  // kt = k0, k0 + 1, ... in order
     const int tid = threadIdx.x;
     const int ma = 4 * (tid % (BM / 4)), nb = 4 * (tid % (BN / 4));
     const int ci = min(m0 + ma, s.C - 4), co = min(n0 + nb, s.K - 4);
@@ -576,13 +622,13 @@ struct FilterLoader {
     for (int i = 0; i < AR; ++i) {
       const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
       const int pix = pix0 + kt * BK + k;
-      const int pc = min(pix, npix - 1);
-      const int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
-      const int iy = oy * s.stride - s.pad + kh, ix = ox * s.stride - s.pad + kw;
+      const int n = min(pw[i].n, s.N - 1);
+      const int iy = pw[i].oy * s.stride - s.pad + kh, ix = pw[i].ox * s.stride - s.pad + kw;
       const bool ok = cv && pix < npix && iy >= 0 && iy < s.H && ix >= 0 && ix < s.W;
       const int iyc = min(max(iy, 0), s.H - 1), ixc = min(max(ix, 0), s.W - 1);
       ra[i] = sel4(ok, *reinterpret_cast<const float4*>(
                            x + (((size_t)n * s.H + iyc) * s.W + ixc) * s.C + ci));
+      pw[i].step(s, dox, doy);
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -611,13 +657,14 @@ struct FilterLoader {
 template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void filter_kernel(ConvShape s, const float* __restrict__ x,
                                                     const float* __restrict__ dy,
-                                                    float* __restrict__ part, int kchunk_tiles) {
+                                                    float* __restrict__ part, int kchunk_tiles,
+                                                    bool xcd) {
   using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int mt = (s.C + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
   const int taps = s.R * s.S;
   const int tiles = mt * nt * taps;
-  const int bid = blockIdx.x;
+  const int bid = xcd_slice_bid(blockIdx.x, tiles, xcd);
   const int z = bid / tiles, rem = bid % tiles;
   const int tap = rem % taps, t2 = rem / taps;
   const int m0 = (t2 % mt) * BM, n0 = (t2 / mt) * BN;
@@ -656,13 +703,19 @@ struct FilterGatherLoader {
   ConvShape s;
   const float* x;
   const float* dy;
-  int n0, pix0, npix;
+  int n0, pix0, npix, dox, doy;
   int dh[4], dw[4], ci[4];  // this thread's 4 A columns (m = ma + j)
   bool mv[4];
+  PixWalk pw[AR];
   float4 ra[AR], rb[BR];
   __device__ FilterGatherLoader(const ConvShape& s_, const float* x_, const float* dy_, int m0,
                                 int n0_, int pix0_, int npix_)
       : s(s_), x(x_), dy(dy_), n0(n0_), pix0(pix0_), npix(npix_) {
+    dox = BK % s.OW;
+    doy = BK / s.OW;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      pw[i].init(s, min(pix0 + (int)threadIdx.x / (BM / 4) + (NT / (BM / 4)) * i, npix - 1));
     const int Mw = s.R * s.S * s.C;
     const int ma = m0 + 4 * (threadIdx.x % (BM / 4));
 #pragma unroll
@@ -685,9 +738,9 @@ struct FilterGatherLoader {
     for (int i = 0; i < AR; ++i) {
       const int k = tid / (BM / 4) + (NT / (BM / 4)) * i;
       const int pix = pix0 + kt * BK + k;
-      const int pc = min(pix, npix - 1);
-      const int ox = pc % s.OW, t = pc / s.OW, oy = t % s.OH, n = t / s.OH;
-      const float* img = x + (size_t)n * s.H * s.W * s.C;
+      const int oy = pw[i].oy, ox = pw[i].ox;
+      const float* img = x + (size_t)min(pw[i].n, s.N - 1) * s.H * s.W * s.C;
+      pw[i].step(s, dox, doy);
       float v[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -727,12 +780,13 @@ template <int BM, int BN, int P>
 __global__ __launch_bounds__(NT) void filter_gather_kernel(ConvShape s, const float* __restrict__ x,
                                                            const float* __restrict__ dy,
                                                            float* __restrict__ part,
-                                                           int kchunk_tiles) {
+                                                           int kchunk_tiles, bool xcd) {
   using G = Geo<BM, BN, P>;
   __shared__ float smem[G::SMEM];
   const int Mw = s.R * s.S * s.C;
   const int mt = (Mw + BM - 1) / BM, nt = (s.K + BN - 1) / BN;
-  const int z = blockIdx.x / (mt * nt), rem = blockIdx.x % (mt * nt);
+  const int bid = xcd_slice_bid(blockIdx.x, mt * nt, xcd);
+  const int z = bid / (mt * nt), rem = bid % (mt * nt);
   const int m0 = (rem % mt) * BM, n0 = (rem / mt) * BN;
   const int npix = s.N * s.OH * s.OW;
   const int pix0 = z * kchunk_tiles * BK;
@@ -1439,8 +1493,10 @@ static inline int filter_blocks_per_split(const ConvShape& s) {
 }
 }  // namespace tiled
 
-int conv_filter_tiled_splits(const ConvShape& s) {
-  using namespace tiled;
+namespace tiled {
+// slices launched (padded to a multiple of 8 for the XCD order) and the K
+// tiles of each
+static int filter_splits(const ConvShape& s, int& kchunk) {
   const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
   const bool vec = s.C % 4 == 0;
   const int tiles = vec ? filter_blocks_per_split(s) : cdiv(s.R * s.S * s.C, 64) * cdiv(s.K, 64);
@@ -1453,35 +1509,46 @@ int conv_filter_tiled_splits(const ConvShape& s) {
   // 12544 K tiles) went 271 -> 197 us from 128 to 256 slices (512: 196, 1024: 198)
   const int gcap = tiled_plan().gcap;
   // vector-path slice cap (TiledPlan vcap).  conv_lab fp32: the 56x56x64 filter
-  // gradient (9 tiles) 152.5 -> 129.0 -> 117.2 us at caps 64 -> 128 -> 256 (all
-  // layers 2120 -> 1984 / 2021 us); not yet verified in a full step, so 64 stays
+  // gradient (9 tiles) 152.2 -> 132.3 -> 120.8 us at caps 64 -> 128 -> 256 (all
+  // layers 2076 -> 1994 / 1979 us); ResNet-18 fp32 step 5.93 -> 5.845 / 5.82 ms
+  // (r6_s22.steps, two runs each), so 256
   const int vcap = tiled_plan().vcap;
   if (z > (vec ? vcap : gcap)) z = vec ? vcap : gcap;
-  const int kchunk = cdiv(ktiles, z);
-  return cdiv(ktiles, kchunk);  // splits actually launched
+  kchunk = cdiv(ktiles, z);
+  const int zr = cdiv(ktiles, kchunk);
+  // XCD-aware slice order (xcd_slice_bid) wants a multiple of 8 slices: the
+  // padding slices have no pixels and write zero slabs
+  if (tiled_plan().wg_xcd && zr > 8) return (zr + 7) / 8 * 8;
+  return zr;
+}
+}  // namespace tiled
+
+int conv_filter_tiled_splits(const ConvShape& s) {
+  int kchunk;
+  return tiled::filter_splits(s, kchunk);
 }
 
 void conv_bwd_filter_tiled(const ConvShape& s, const float* x, const float* dy, float* part,
                            float* dw, hipStream_t st, bool bf16) {
   using namespace tiled;
-  const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
-  const int z = conv_filter_tiled_splits(s);
-  const int kchunk = cdiv(ktiles, z);
+  int kchunk;
+  const int z = filter_splits(s, kchunk);
+  const bool xcd = tiled_plan().wg_xcd;
   const int taps = s.R * s.S;
   if (s.C % 4 != 0) {  // (tap, ci) gather rows, 64x64 tiles
     const int Mw = taps * s.C;
     if (bf16)
       filter_gather_kernel<64, 64, BF16><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
-          s, x, dy, z == 1 ? dw : part, kchunk);
+          s, x, dy, z == 1 ? dw : part, kchunk, xcd);
     else
       filter_gather_kernel<64, 64, F32><<<cdiv(Mw, 64) * cdiv(s.K, 64) * z, NT, 0, st>>>(
-          s, x, dy, z == 1 ? dw : part, kchunk);
+          s, x, dy, z == 1 ? dw : part, kchunk, xcd);
     if (z > 1) slab_sum(part, z, (long long)Mw * s.K, dw, st);
     return;
   }
   const Tile t = filter_tile(s);
 #define GRID(BM_, BN_) dim3(cdiv(s.C, BM_) * cdiv(s.K, BN_) * taps * z)
-  TILED_DISPATCH(t, filter_kernel, GRID, s, x, dy, z == 1 ? dw : part, kchunk)
+  TILED_DISPATCH(t, filter_kernel, GRID, s, x, dy, z == 1 ? dw : part, kchunk, xcd)
 #undef GRID
   if (z > 1) slab_sum(part, z, (long long)taps * s.C * s.K, dw, st);
 }

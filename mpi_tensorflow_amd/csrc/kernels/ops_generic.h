@@ -159,7 +159,8 @@ struct TiledPlan {
   int ksplit_target = 1024;               // forward / dgrad split-K: blocks to aim for
   int wgsplit_target = 2048;              // filter gradient: blocks to aim for
   int gcap = 256;                         // filter gradient slice cap, gather path
-  int vcap = 64;                          // filter gradient slice cap, vector path
+  int vcap = 256;                         // filter gradient slice cap, vector path
+  bool wg_xcd = false;                    // filter gradient slices grouped by XCD (xcd_slice_bid; slower)
   bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
   bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
   bool halo_f32 = true;                   // fp32 3x3 stride-1 convs on conv3f_kernel

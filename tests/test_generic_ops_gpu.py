@@ -489,6 +489,47 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
             assert _rel(a, b) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [
+    (8, 56, 64, 64, 3, 1, 1),   # 9 tiles x 256 slices (the 56x56 layer's plan)
+    (4, 28, 64, 128, 3, 2, 1),  # stride 2, padded slice count
+    (4, 28, 64, 128, 1, 2, 0),  # 1x1 stride 2
+    (2, 40, 3, 64, 7, 2, 3),    # gather path (C = 3)
+])
+def test_fp32_filter_grad_xcd_slice_order(cuda_dev, N, H, C, K, R, stride, pad):
+    """The fp32 filter gradient (conv_tiled.hip filter_kernel /
+    filter_gather_kernel) with the XCD-grouped slice order and its zero padding
+    slices (TiledPlan wg_xcd) and without, against a float64 torch reference."""
+    from mpi_tensorflow_amd.ops import native
+
+    ops = native().ops
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, H, H, C, generator=g)
+    w = torch.randn(R, R, C, K, generator=g) * (R * R * C) ** -0.5
+    xr = x.double()
+    wr = w.double().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(3, 2, 0, 1), stride=stride,
+                  padding=pad).permute(0, 2, 3, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy.double())
+    plan = ops.get_tiled_plan()
+    outs = []
+    try:
+        for xcd in (True, False):
+            p = ops.get_tiled_plan()
+            p.wg_xcd = xcd
+            ops.set_tiled_plan(p)
+            wp = _param(w.to(cuda_dev))
+            yg = Fn.conv2d(x.to(cuda_dev), wp, None, stride, pad, False)
+            yg.backward(dy.to(cuda_dev))
+            torch.cuda.synchronize()
+            outs.append(wp.grad_view.detach().cpu().clone())
+    finally:
+        ops.set_tiled_plan(plan)
+    for dw in outs:
+        assert _rel(dw.double(), wr.grad) < 1e-5
+    assert _rel(outs[0], outs[1]) < 1e-6
+
+
 def test_bn_bf16_twin_feeds_conv(cuda_dev):
     """bf16 mode: BatchNorm writes a bf16 twin of y (forward) and dx
     (backward); the consuming conv reads it instead of converting.  The result
