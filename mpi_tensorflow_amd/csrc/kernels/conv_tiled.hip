@@ -1303,7 +1303,7 @@ static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   const long long M = (long long)s.N * s.H * s.W;
   const bool wide = tiled_plan().halo_f32_wide && s.K % 128 == 0;
   p.bn = wide ? 128 : 64;
-  p.ch = wide ? 16 : 32;
+  p.ch = wide || tiled_plan().halo_f32_ch == 16 ? 16 : 32;
   // 64-row blocks: conv_lab fp32 fwd + dgrad 2201 us a step against 2223 with
   // 128-row blocks where the grid allows them (2312 with 128 everywhere)
   p.bm = tiled_plan().halo_f32_bm == 128 ? 128 : 64;
@@ -1342,6 +1342,11 @@ void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float
       C3F(128, 128, 16);
     else
       C3F(64, 128, 16);
+  } else if (p.ch == 16) {  // 64-byte rows: 38 KiB of LDS, four blocks a CU
+    if (p.bm == 128)
+      C3F(128, 64, 16);
+    else
+      C3F(64, 64, 16);
   } else if (p.bm == 128) {
     C3F(128, 64, 32);
   } else {
@@ -1500,8 +1505,11 @@ static int filter_splits(const ConvShape& s, int& kchunk) {
   const int ktiles = cdiv((long long)s.N * s.OH * s.OW, BK);
   const bool vec = s.C % 4 == 0;
   const int tiles = vec ? filter_blocks_per_split(s) : cdiv(s.R * s.S * s.C, 64) * cdiv(s.K, 64);
-  // aim for ~2048 blocks (measured: fewer, larger slices - 512 or 1024 blocks -
-  // cost 4-20 % ResNet-18 step time despite the smaller slab traffic)
+  // blocks to aim for (TiledPlan wgsplit_target).  With the walked pixel
+  // coordinates (PixWalk) fewer, longer slices pay: ResNet-18 fp32 filter
+  // gradients in conv_lab 1934 / 1805 / 1836 / 1901 us a step at 2048 / 1024 /
+  // 768 / 512 blocks, the full step 5.69 / 5.75 / 5.65 ms at 2048 / 1024 / 768
+  // (r6_s26 / r6_s27.steps, two runs each), so 768
   int z = cdiv(wgsplit_target(), tiles);
   if (z < 1) z = 1;
   if (z > ktiles) z = ktiles;

@@ -157,7 +157,7 @@ struct TiledPlan {
   long long m128_min_bf16 = 128LL * 256;  // 128-row tiles from M >= this (bf16)
   long long m128_min_f32 = 1LL << 62;     // fp32: never (64-row tiles measured faster)
   int ksplit_target = 1024;               // forward / dgrad split-K: blocks to aim for
-  int wgsplit_target = 2048;              // filter gradient: blocks to aim for
+  int wgsplit_target = 768;               // filter gradient: blocks to aim for
   int gcap = 256;                         // filter gradient slice cap, gather path
   int vcap = 256;                         // filter gradient slice cap, vector path
   bool wg_xcd = false;                    // filter gradient slices grouped by XCD (xcd_slice_bid; slower)
@@ -168,6 +168,10 @@ struct TiledPlan {
   // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off
   bool halo_f32_wide = false;
   int halo_f32_bm = 64;                   // conv3f block rows: 64, or 128 (labs)
+  // conv3f channels a chunk with 64 columns: 16 (64-byte rows, 38 KiB of LDS,
+  // four blocks a CU) or 32 (77 KiB, two): conv_lab fwd + dgrad 2188 vs 2212 us
+  // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)
+  int halo_f32_ch = 16;
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy

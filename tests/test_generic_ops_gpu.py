@@ -466,10 +466,13 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
         # the halo kernel with 128-column tiles on 16-channel chunks (K % 128
         # == 0), with 64-column tiles on 32-channel chunks, each on 64- and
         # 128-row blocks, and the tiled kernels
-        for halo, wide, bm in ((True, True, 64), (True, True, 128), (True, False, 64),
-                               (True, False, 128), (False, False, 64)):
+        # (64-column tiles also on 16-channel chunks)
+        for halo, wide, bm, ch in ((True, True, 64, 16), (True, True, 128, 16),
+                                   (True, False, 64, 32), (True, False, 128, 32),
+                                   (True, False, 64, 16), (True, False, 128, 16),
+                                   (False, False, 64, 32)):
             p = ops.get_tiled_plan()
-            p.halo_f32, p.halo_f32_wide, p.halo_f32_bm = halo, wide, bm
+            p.halo_f32, p.halo_f32_wide, p.halo_f32_bm, p.halo_f32_ch = halo, wide, bm, ch
             ops.set_tiled_plan(p)
             wp = _param(w.to(cuda_dev))
             Fn.ConvWeightCopies({"w": wp}, cuda_dev, kind="f32flip").refresh()
