@@ -1304,16 +1304,30 @@ static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   const bool wide = tiled_plan().halo_f32_wide && s.K % 128 == 0;
   p.bn = wide ? 128 : 64;
   p.ch = wide || tiled_plan().halo_f32_ch == 16 ? 16 : 32;
-  // 64-row blocks: conv_lab fp32 fwd + dgrad 2201 us a step against 2223 with
-  // 128-row blocks where the grid allows them (2312 with 128 everywhere)
-  p.bm = tiled_plan().halo_f32_bm == 128 ? 128 : 64;
-  if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
-  const long long blocks = cdiv(M, p.bm) * (s.K / p.bn);
   const int nch = s.C / p.ch;
-  p.z = 1;
-  if (blocks < 512) p.z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
-  p.cps = cdiv(nch, p.z);
-  p.z = cdiv(nch, p.cps);
+  // blocks launched with bm-row tiles (channel-chunk split-K below 512 tiles)
+  auto grid = [&](int bm, int& z, int& cps) {
+    const long long blocks = cdiv(M, bm) * (s.K / p.bn);
+    z = 1;
+    if (blocks < 512) z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
+    cps = cdiv(nch, z);
+    z = cdiv(nch, cps);
+    return blocks * z;
+  };
+  // block rows (TiledPlan halo_f32_bm; 0 = auto): 128 when that launches at
+  // least as many blocks as 64 without adding a split-K 64 does not need (the
+  // 14x14 layer: the same split count, fewer halo re-reads: conv_lab 88.5 ->
+  // 80.2 us), else 64 (the 56x56 layer would fill under one round of four
+  // blocks a CU, the 7x7 one gets fewer blocks, the 28x28 one a split for
+  // nothing: 88.5 vs 89.3 us; r6_s29.steps)
+  int z64, c64, z128, c128;
+  const long long b64 = grid(64, z64, c64), b128 = grid(128, z128, c128);
+  const int want = tiled_plan().halo_f32_bm;
+  p.bm = want == 128 || (want == 0 && b128 >= b64 && (z64 > 1 || z128 == 1)) ? 128 : 64;
+  if (h3f::halo_rows(s, p.bm) > h3f::HCAP) p.bm = 64;
+  if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
+  p.z = p.bm == 128 ? z128 : z64;
+  p.cps = p.bm == 128 ? c128 : c64;
   return true;
 }
 bool conv3f_ok(const ConvShape& s) {

@@ -167,7 +167,7 @@ struct TiledPlan {
   // ... with 128-column tiles on 16-channel chunks for K % 128 == 0: measured a
   // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off
   bool halo_f32_wide = false;
-  int halo_f32_bm = 64;                   // conv3f block rows: 64, or 128 (labs)
+  int halo_f32_bm = 0;                    // conv3f block rows: 0 = by grid (conv3f_plan), 64, 128
   // conv3f channels a chunk with 64 columns: 16 (64-byte rows, 38 KiB of LDS,
   // four blocks a CU) or 32 (77 KiB, two): conv_lab fwd + dgrad 2188 vs 2212 us
   // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)

@@ -469,7 +469,7 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
         # (64-column tiles also on 16-channel chunks)
         for halo, wide, bm, ch in ((True, True, 64, 16), (True, True, 128, 16),
                                    (True, False, 64, 32), (True, False, 128, 32),
-                                   (True, False, 64, 16), (True, False, 128, 16),
+                                   (True, False, 64, 16), (True, False, 128, 16), (True, False, 0, 16),
                                    (False, False, 64, 32)):
             p = ops.get_tiled_plan()
             p.halo_f32, p.halo_f32_wide, p.halo_f32_bm, p.halo_f32_ch = halo, wide, bm, ch
