@@ -1143,6 +1143,184 @@ __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __
 // contiguous axis) and measured 119-129 us against 96-104 us forward on the
 // same ResNet-18 shapes.  One 32 x 32 LDS tile transpose per (tap, ci, co)
 // block: coalesced reads along co, coalesced writes along ci.
+// ----------------------- fp32 3x3 stride-2 backward-data (halo form) ----
+// conv_bf16.hip dgrad3s2_kernel's design on conv3f_kernel's fp32 staging: dX
+// of a 3x3 / stride 2 / pad 1 conv on an even input, output pixel
+// (2a + py, 2b + px) taking only the taps of its parity class -
+//   py = 0: kh = 1 on dY row a;  py = 1: kh = 0 on row a + 1, kh = 2 on row a
+// (likewise px / kw / columns).  A block owns BM dY-grid pixels (n, a, b) x
+// BN input channels and keeps four accumulator sets, one per class; the dY
+// halo (the tile's stacked rows plus one below) is staged once per CH-channel
+// chunk of the reduction (the output channels) and each tap reads it at a
+// per-lane (+1 row / +1 column) shift, the zero row past the image.  B: the
+// HWIO weights themselves, [tap][ci][co] (rows = input channels, the output
+// channels contiguous) through the RB-deep ring.  Split-K over the output-
+// channel chunks (blockIdx.y, slabs).  Replaces the phase-split data_kernel.
+template <int BM, int BN, int RB, int CH>
+__global__ __launch_bounds__(NT) void dgrad3s2f_kernel(ConvShape s, const float* __restrict__ dy,
+                                                       const float* __restrict__ w,
+                                                       float* __restrict__ dx, int cps,
+                                                       const float* __restrict__ addend) {
+  using h3f::HCAP;
+  using G3 = h3f::Geo<CH>;
+  constexpr int ROWB = G3::ROWB, NCK = G3::NCK, RPI = G3::RPI;
+  constexpr int TM = BM / 64, TN = BN / 64;
+  constexpr int GB = (BN / 4) / RPI;  // weight DMA instructions per wave per tap
+  constexpr int HB = (HCAP + 1) * ROWB;
+  constexpr int BSZ = BN * ROWB;
+  static_assert(RB >= 3 && RB <= 4, "ring depth");
+  static_assert(GB >= 1 && (BN / 4) % RPI == 0, "weight rows per wave");
+  static_assert(HCAP % RPI == 0, "halo DMA groups end below the zero row");
+  __shared__ __attribute__((aligned(1024))) char smem[HB + RB * BSZ];
+  const int OH = s.OH, OW = s.OW;
+  const int M = s.N * OH * OW;  // dY-grid pixels
+  const int mt = (M + BM - 1) / BM;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (bid % mt) * BM, n0 = (bid / mt) * BN;  // n: input channel ci
+  const int nch = s.K / CH;
+  const int cc0 = blockIdx.y * cps, cc1 = min(nch, cc0 + cps);
+  const int g_first = m0 / OW, g_last = (min(m0 + BM, M) - 1) / OW;
+  const long long hbase = (long long)g_first * OW;  // global dY pixel of halo row 0
+  const int npix = (g_last - g_first + 2) * OW;
+  const int nins = (npix + RPI - 1) / RPI;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave & 1, wn = wave >> 1;
+  const int r = lane & 31, h = lane >> 5, lr = lane / NCK, lp = lane % NCK;
+  if (tid < NCK) *reinterpret_cast<uint4*>(smem + HCAP * ROWB + 16 * tid) = make_uint4(0u, 0u, 0u, 0u);
+  int gl[TM], bs[TM], as[TM];
+  bool mv[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * (BM / 2) + 32 * i + r;
+    mv[i] = m < M;
+    const int mm = mv[i] ? m : m0;
+    const int g = mm / OW;
+    bs[i] = mm - g * OW;
+    as[i] = g % OH;
+    gl[i] = g - g_first;
+  }
+  const float* bsrc[GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = wave * (BN / 4) + RPI * j + lr;
+    bsrc[j] = w + (size_t)(n0 + row) * s.K + 4 * (lp ^ G3::swz(row));
+  }
+  auto issue_b = [&](int tap, int cc, int slot) {
+    const size_t o = (size_t)tap * s.C * s.K + (size_t)cc * CH;
+    char* dst = smem + HB + slot * BSZ + wave * (BN / 4) * ROWB;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) h3f::glds(bsrc[j] + o, dst + RPI * j * ROWB);
+  };
+  auto issue_halo = [&](int cc) {
+    for (int ins = wave; ins < nins; ins += 4) {
+      const int p = RPI * ins + lr;
+      const long long gp = hbase + p;
+      const bool ok = p < npix && gp < M;
+      const void* src = ok ? (const void*)(dy + gp * s.K + (size_t)cc * CH + 4 * (lp ^ G3::swz(p)))
+                           : (const void*)h3f::g_zero;
+      h3f::glds(src, smem + ins * RPI * ROWB);
+    }
+  };
+  f32x16 acc[4][TM][TN];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[c][i][j] = zero16();
+  for (int cc = cc0; cc < cc1; ++cc) {
+    // the previous chunk's halo and ring reads are done (and the zero row is written)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue_halo(cc);
+#pragma unroll
+    for (int t = 0; t < RB - 1; ++t) issue_b(t, cc, t);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ahead = min(RB - 2, 8 - t);
+      if (ahead >= 2)
+        h3f::wait_vm<2 * GB>();
+      else if (ahead == 1)
+        h3f::wait_vm<GB>();
+      else
+        h3f::wait_vm<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring slot (t - 1) % RB read
+      __builtin_amdgcn_s_barrier();
+      if (t + RB - 1 < 9) issue_b(t + RB - 1, cc, (t + RB - 1) % RB);
+      const int kh = t / 3, kw = t - 3 * kh;
+      const int cls = (kh != 1 ? 2 : 0) + (kw != 1 ? 1 : 0);  // (py, px)
+      const int dh = kh == 0 ? 1 : 0, dw = kw == 0 ? 1 : 0;
+      int hrow[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const bool ok = mv[i] && as[i] + dh < OH && bs[i] + dw < OW;
+        hrow[i] = ok ? (gl[i] + dh) * OW + bs[i] + dw : HCAP;
+      }
+      const char* B = smem + HB + (t % RB) * BSZ;
+#pragma unroll
+      for (int c = 0; c < CH / 8; ++c) {
+        const int ck = 2 * c + h;
+        float4 a[TM], b[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          a[i] = *reinterpret_cast<const float4*>(smem + hrow[i] * ROWB +
+                                                  ((ck ^ G3::swz(hrow[i])) << 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int R = wn * (BN / 2) + 32 * j + r;
+          b[j] = *reinterpret_cast<const float4*>(B + R * ROWB + ((ck ^ G3::swz(R)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[cls][i][j] = mfma32x32x2(a[i].x, b[j].x, acc[cls][i][j]);
+            acc[cls][i][j] = mfma32x32x2(a[i].y, b[j].y, acc[cls][i][j]);
+            acc[cls][i][j] = mfma32x32x2(a[i].z, b[j].z, acc[cls][i][j]);
+            acc[cls][i][j] = mfma32x32x2(a[i].w, b[j].w, acc[cls][i][j]);
+          }
+      }
+    }
+  }
+  // epilogue: grid pixel m = (n, a, b) -> dX pixels (n, 2a + py, 2b + px);
+  // the addend (a gradient join, unsplit only) of four rows loaded before
+  // their stores (vmcnt counts both: interleaved, every load would wait for
+  // the stores ahead of it)
+  dx += (size_t)blockIdx.y * s.N * s.H * s.W * s.C;
+  const size_t C = s.C, W = s.W;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int ci = n0 + wn * (BN / 2) + 32 * j + r;
+#pragma unroll
+      for (int q4 = 0; q4 < 16; q4 += 4) {
+        size_t o[4];
+        bool ok[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int m = m0 + wm * (BM / 2) + 32 * i + mfma32_row(q4 + u, lane);
+          ok[u] = m < M;
+          const int mm = ok[u] ? m : 0;
+          const int g = mm / OW, b = mm - g * OW;  // g = n * OH + a
+          o[u] = ((size_t)(2 * g) * W + 2 * b) * C + ci;  // (n, 2a, 2b)
+        }
+        float av[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            av[u][c] = addend && ok[u] ? addend[o[u] + ((c >> 1) * W + (c & 1)) * C] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (!ok[u]) continue;
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            dx[o[u] + ((c >> 1) * W + (c & 1)) * C] = acc[c][i][j][q4 + u] + av[u][c];
+        }
+      }
+    }
+}
+
 __global__ __launch_bounds__(256) void wflip_kernel(const float* __restrict__ w,
                                                     float* __restrict__ wt, int R, int S, int C,
                                                     int K) {
@@ -1370,6 +1548,33 @@ void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float
   if (p.z > 1) slab_sum(ws, p.z, M * s.K, y, st, addend);
 }
 
+// fp32 3x3 stride-2 dgrad on the halo kernel (dgrad3s2f_kernel): 64 x 64 tiles
+// on 16-channel chunks (38 KiB of LDS), channel-chunk split-K below 512 tiles
+struct D3s2fPlan {
+  int z, cps;
+};
+static bool dgrad3s2f_plan(const ConvShape& s, D3s2fPlan& p) {
+  using namespace tiled;
+  if (!tiled_plan().halo_f32_s2) return false;
+  if (!(s.R == 3 && s.S == 3 && s.stride == 2 && s.pad == 1 && s.H == 2 * s.OH && s.W == 2 * s.OW))
+    return false;
+  if (s.C % 64 || s.K % 16 || (long long)s.N * s.H * s.W * std::max(s.C, s.K) >= (1LL << 31))
+    return false;
+  if (((64 + s.OW - 2) / s.OW + 2) * s.OW > h3f::HCAP) return false;  // halo rows
+  const long long blocks = cdiv((long long)s.N * s.OH * s.OW, 64) * (s.C / 64);
+  const int nch = s.K / 16;
+  p.z = 1;
+  if (blocks < 512) p.z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
+  p.cps = cdiv(nch, p.z);
+  p.z = cdiv(nch, p.cps);
+  return true;
+}
+static long long dgrad3s2f_ws_floats(const ConvShape& s) {
+  D3s2fPlan p;
+  if (!dgrad3s2f_plan(s, p) || p.z == 1) return 0;
+  return (long long)p.z * s.N * s.H * s.W * s.C;
+}
+
 // workspace for either operand precision (the plans differ in tile shape)
 long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
   long long n = conv3f_ws_floats(s);
@@ -1384,6 +1589,7 @@ long long conv_fwd_tiled_ws_floats(const ConvShape& s, bool epilogue) {
 
 long long conv_bwd_data_tiled_ws_floats(const ConvShape& s) {
   long long n = dgrad_fwd_ok(s) ? dgrad_fwd_ws_floats(s) : 0;
+  n = std::max(n, dgrad3s2f_ws_floats(s));
   if (dgrad_fwd_ok(s)) n = std::max(n, conv3f_ws_floats(dgrad_fwd_shape(s)));
   for (const bool b : {false, true}) {
     tiled::Tile t;
@@ -1473,6 +1679,15 @@ void conv_bwd_data_tiled(const ConvShape& s, const float* dy, const float* w, fl
       wt = ws;
     }
     conv_fwd_tiled_impl(f, dy, wt, nullptr, dx, false, fws, st, false, nullptr, addend);
+    return;
+  }
+  D3s2fPlan dp;
+  if (!bf16 && dy && dgrad3s2f_plan(s, dp)) {
+    if (dp.z > 1 && !ws) throw std::runtime_error("dgrad3s2f: split-K needs a workspace");
+    const dim3 grid(cdiv((long long)s.N * s.OH * s.OW, 64) * (s.C / 64), dp.z);
+    dgrad3s2f_kernel<64, 64, 4, 16><<<grid, NT, 0, st>>>(s, dy, w, dp.z > 1 ? ws : dx, dp.cps,
+                                                         dp.z > 1 ? nullptr : addend);
+    if (dp.z > 1) slab_sum(ws, dp.z, (long long)s.N * s.H * s.W * s.C, dx, st, addend);
     return;
   }
   const int sd = s.stride;

@@ -172,6 +172,7 @@ struct TiledPlan {
   // four blocks a CU) or 32 (77 KiB, two): conv_lab fwd + dgrad 2188 vs 2212 us
   // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)
   int halo_f32_ch = 16;
+  bool halo_f32_s2 = true;                // fp32 3x3 stride-2 dgrad on dgrad3s2f_kernel
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy

@@ -533,6 +533,48 @@ def test_fp32_filter_grad_xcd_slice_order(cuda_dev, N, H, C, K, R, stride, pad):
     assert _rel(outs[0], outs[1]) < 1e-6
 
 
+@pytest.mark.parametrize("N,H,C,K", [
+    (4, 56, 64, 128),   # split over the output-channel chunks
+    (2, 28, 128, 256),
+    (3, 14, 256, 512),  # 7x7 dY grid, partial last tile
+    (2, 10, 64, 32),    # 5x5 dY grid, two chunks
+])
+def test_fp32_dgrad3s2_halo(cuda_dev, N, H, C, K):
+    """fp32 3x3 / stride 2 / pad 1 backward-data on the halo kernel
+    (conv_tiled.hip dgrad3s2f_kernel: four parity-class accumulators over the
+    staged dY halo, HWIO weights) and on the phase-split tiled kernel
+    (TiledPlan halo_f32_s2 = False), against a float64 torch reference."""
+    from mpi_tensorflow_amd.ops import native
+
+    ops = native().ops
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, H, H, C, generator=g)
+    w = torch.randn(3, 3, C, K, generator=g) * (9 * C) ** -0.5
+    xr = x.double().requires_grad_(True)
+    yr = F.conv2d(xr.permute(0, 3, 1, 2), w.double().permute(3, 2, 0, 1), stride=2,
+                  padding=1).permute(0, 2, 3, 1)
+    dy = torch.randn(yr.shape, generator=g)
+    yr.backward(dy.double())
+    plan = ops.get_tiled_plan()
+    outs = []
+    try:
+        for halo in (True, False):
+            p = ops.get_tiled_plan()
+            p.halo_f32_s2 = halo
+            ops.set_tiled_plan(p)
+            wp = _param(w.to(cuda_dev))
+            xg = x.to(cuda_dev).requires_grad_(True)
+            yg = Fn.conv2d(xg, wp, None, 2, 1, False)
+            yg.backward(dy.to(cuda_dev))
+            torch.cuda.synchronize()
+            outs.append(xg.grad.cpu())
+    finally:
+        ops.set_tiled_plan(plan)
+    for dx in outs:
+        assert _rel(dx.double(), xr.grad) < 1e-5
+    assert _rel(outs[0], outs[1]) < 1e-5
+
+
 def test_bn_bf16_twin_feeds_conv(cuda_dev):
     """bf16 mode: BatchNorm writes a bf16 twin of y (forward) and dx
     (backward); the consuming conv reads it instead of converting.  The result
