@@ -377,7 +377,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("halo_f32_wide", &gops::TiledPlan::halo_f32_wide)
       .def_readwrite("halo_f32_bm", &gops::TiledPlan::halo_f32_bm)
       .def_readwrite("halo_f32_ch", &gops::TiledPlan::halo_f32_ch)
-      .def_readwrite("halo_f32_s2", &gops::TiledPlan::halo_f32_s2);
+      .def_readwrite("halo_f32_s2", &gops::TiledPlan::halo_f32_s2)
+      .def_readwrite("ksplit_s2", &gops::TiledPlan::ksplit_s2);
   g.def("conv3f_ok", &gops::conv3f_ok);
   g.def("get_tiled_plan", []() { return gops::tiled_plan(); });
   g.def("set_tiled_plan", [](const gops::TiledPlan& p) { gops::tiled_plan() = p; });

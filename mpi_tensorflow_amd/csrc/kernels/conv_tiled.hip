@@ -1563,8 +1563,9 @@ static bool dgrad3s2f_plan(const ConvShape& s, D3s2fPlan& p) {
   if (((64 + s.OW - 2) / s.OW + 2) * s.OW > h3f::HCAP) return false;  // halo rows
   const long long blocks = cdiv((long long)s.N * s.OH * s.OW, 64) * (s.C / 64);
   const int nch = s.K / 16;
+  const int target = tiled_plan().ksplit_s2 > 0 ? tiled_plan().ksplit_s2 : ksplit_target();
   p.z = 1;
-  if (blocks < 512) p.z = (int)std::min<long long>(nch, cdiv(ksplit_target(), blocks));
+  if (blocks < 512) p.z = (int)std::min<long long>(nch, cdiv(target, blocks));
   p.cps = cdiv(nch, p.z);
   p.z = cdiv(nch, p.cps);
   return true;
@@ -1738,7 +1739,9 @@ static int filter_splits(const ConvShape& s, int& kchunk) {
   // coordinates (PixWalk) fewer, longer slices pay: ResNet-18 fp32 filter
   // gradients in conv_lab 1934 / 1805 / 1836 / 1901 us a step at 2048 / 1024 /
   // 768 / 512 blocks, the full step 5.69 / 5.75 / 5.65 ms at 2048 / 1024 / 768
-  // (r6_s26 / r6_s27.steps, two runs each), so 768
+  // (r6_s26 / r6_s27.steps, two runs each); with the halo convs on 16-channel
+  // chunks and the stride-2 halo dgrad the order changed: 5.50 / 5.46 / 5.58 ms
+  // at 768 / 1024 / 640 (r6_s32.steps), so 1024
   int z = cdiv(wgsplit_target(), tiles);
   if (z < 1) z = 1;
   if (z > ktiles) z = ktiles;

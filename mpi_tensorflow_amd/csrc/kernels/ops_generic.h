@@ -157,7 +157,7 @@ struct TiledPlan {
   long long m128_min_bf16 = 128LL * 256;  // 128-row tiles from M >= this (bf16)
   long long m128_min_f32 = 1LL << 62;     // fp32: never (64-row tiles measured faster)
   int ksplit_target = 1024;               // forward / dgrad split-K: blocks to aim for
-  int wgsplit_target = 768;               // filter gradient: blocks to aim for
+  int wgsplit_target = 1024;              // filter gradient: blocks to aim for
   int gcap = 256;                         // filter gradient slice cap, gather path
   int vcap = 256;                         // filter gradient slice cap, vector path
   bool wg_xcd = false;                    // filter gradient slices grouped by XCD (xcd_slice_bid; slower)
@@ -173,6 +173,7 @@ struct TiledPlan {
   // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)
   int halo_f32_ch = 16;
   bool halo_f32_s2 = true;                // fp32 3x3 stride-2 dgrad on dgrad3s2f_kernel
+  int ksplit_s2 = 0;                      // ... its split-K target (0: ksplit_target)
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy
