@@ -173,7 +173,10 @@ struct TiledPlan {
   // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)
   int halo_f32_ch = 16;
   bool halo_f32_s2 = true;                // fp32 3x3 stride-2 dgrad on dgrad3s2f_kernel
-  int ksplit_s2 = 0;                      // ... its split-K target (0: ksplit_target)
+  // ... its split-K target (0: ksplit_target): fewer, longer slices than the
+  // other convs (three blocks a CU, a dX four times the dY grid to sum):
+  // ResNet-18 fp32 5.462 / 5.465 -> 5.432 / 5.416 ms at 1024 -> 512 (r6_s33.steps)
+  int ksplit_s2 = 512;
 };
 // fp32 3x3 / stride 1 / pad 1 halo conv (conv_tiled.hip conv3f_kernel); wt:
 // [9][K][C] read at tap 8 - t - the forward passes the stride-1 dgrad copy
