@@ -1717,7 +1717,7 @@ static inline Tile filter_tile(const ConvShape& s) {  // ci x co tiles
   // (14x14), 116 -> 102 us (7x7), step 6.96 -> 6.78 ms; twice the tiles, so half
   // the split-K slices (the bf16 models take the conv_bf16 filter kernels).
   // TiledPlan wg64 = false: 128-wide ci tiles from C >= 128 (the old plan)
-  const bool bm = s.C >= 128 && !tiled_plan().wg64, bn = s.K > 64;
+  const bool bm = s.C >= 128 && !tiled_plan().wg64, bn = s.K > 64 && !tiled_plan().wg_n64;
   return bm ? (bn ? T128x128 : T128x64) : (bn ? T64x128 : T64x64);
 }
 static inline int filter_blocks_per_split(const ConvShape& s) {

@@ -163,6 +163,7 @@ struct TiledPlan {
   bool wg_xcd = false;                    // filter gradient slices grouped by XCD (xcd_slice_bid; slower)
   bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
   bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
+  bool wg_n64 = false;                    // ... and 64-wide co tiles (labs)
   bool halo_f32 = true;                   // fp32 3x3 stride-1 convs on conv3f_kernel
   // ... with 128-column tiles on 16-channel chunks for K % 128 == 0: measured a
   // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off
