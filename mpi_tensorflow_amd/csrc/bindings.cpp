@@ -378,6 +378,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("halo_f32_wide", &gops::TiledPlan::halo_f32_wide)
       .def_readwrite("halo_f32_bm", &gops::TiledPlan::halo_f32_bm)
       .def_readwrite("halo_f32_ch", &gops::TiledPlan::halo_f32_ch)
+      .def_readwrite("halo_f32_small", &gops::TiledPlan::halo_f32_small)
       .def_readwrite("halo_f32_s2", &gops::TiledPlan::halo_f32_s2)
       .def_readwrite("ksplit_s2", &gops::TiledPlan::ksplit_s2);
   g.def("conv3f_ok", &gops::conv3f_ok);

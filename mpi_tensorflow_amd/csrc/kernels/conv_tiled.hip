@@ -977,12 +977,13 @@ struct Geo {
 };
 }  // namespace h3f
 
-template <int BM, int BN, int RB, int CH>
+// HC: halo rows of the LDS image (h3f::HCAP, or fewer for a smaller footprint)
+template <int BM, int BN, int RB, int CH, int HC = h3f::HCAP>
 __global__ __launch_bounds__(NT) void conv3f_kernel(ConvShape s, const float* __restrict__ x,
                                                     const float* __restrict__ wt,
                                                     float* __restrict__ y, int cps,
                                                     const float* __restrict__ addend) {
-  using h3f::HCAP;
+  constexpr int HCAP = HC;
   using G3 = h3f::Geo<CH>;
   constexpr int ROWB = G3::ROWB, NCK = G3::NCK, RPI = G3::RPI;
   constexpr int TM = BM / 64, TN = BN / 64;
@@ -1470,7 +1471,9 @@ static long long dgrad_fwd_ws_floats(const ConvShape& s) {
 // TiledPlan halo_f32_wide: 128-column tiles on 16-channel chunks where K allows
 struct C3fPlan {
   int bm, bn, ch, z, cps;
+  bool small;  // 64 x 64 on 16-channel chunks with a 288-row halo and a 3-deep ring
 };
+constexpr int C3F_SMALL_ROWS = 288;
 static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   using namespace tiled;
   if (!tiled_plan().halo_f32) return false;
@@ -1506,6 +1509,9 @@ static bool conv3f_plan(const ConvShape& s, C3fPlan& p) {
   if (h3f::halo_rows(s, p.bm) > h3f::HCAP) return false;
   p.z = p.bm == 128 ? z128 : z64;
   p.cps = p.bm == 128 ? c128 : c64;
+  // TiledPlan halo_f32_small: 30.5 KiB of LDS, five blocks a CU instead of four
+  p.small = tiled_plan().halo_f32_small && p.bm == 64 && p.bn == 64 && p.ch == 16 &&
+            h3f::halo_rows(s, 64) <= C3F_SMALL_ROWS;
   return true;
 }
 bool conv3f_ok(const ConvShape& s) {
@@ -1534,6 +1540,8 @@ void conv3f(const ConvShape& s, const float* x, const float* wt, float* y, float
       C3F(128, 128, 16);
     else
       C3F(64, 128, 16);
+  } else if (p.small) {
+    conv3f_kernel<64, 64, 3, 16, C3F_SMALL_ROWS><<<grid, NT, 0, st>>>(s, x, wt, out, p.cps, add);
   } else if (p.ch == 16) {  // 64-byte rows: 38 KiB of LDS, four blocks a CU
     if (p.bm == 128)
       C3F(128, 64, 16);

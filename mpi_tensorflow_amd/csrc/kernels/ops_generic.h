@@ -173,6 +173,7 @@ struct TiledPlan {
   // four blocks a CU) or 32 (77 KiB, two): conv_lab fwd + dgrad 2188 vs 2212 us
   // a step, ResNet-18 fp32 5.573 / 5.562 vs 5.674 / 5.680 ms (r6_s29.steps)
   int halo_f32_ch = 16;
+  bool halo_f32_small = false;            // conv3f 64 x 64 / 16 ch with a 288-row halo, 3-deep ring
   bool halo_f32_s2 = true;                // fp32 3x3 stride-2 dgrad on dgrad3s2f_kernel
   // ... its split-K target (0: ksplit_target): fewer, longer slices than the
   // other convs (three blocks a CU, a dX four times the dY grid to sum):

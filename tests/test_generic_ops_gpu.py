@@ -467,12 +467,15 @@ def test_fp32_halo_conv3x3_fwd_and_dgrad(cuda_dev, N, H, W, C, K):
         # == 0), with 64-column tiles on 32-channel chunks, each on 64- and
         # 128-row blocks, and the tiled kernels
         # (64-column tiles also on 16-channel chunks)
-        for halo, wide, bm, ch in ((True, True, 64, 16), (True, True, 128, 16),
-                                   (True, False, 64, 32), (True, False, 128, 32),
-                                   (True, False, 64, 16), (True, False, 128, 16), (True, False, 0, 16),
-                                   (False, False, 64, 32)):
+        # (and the small-footprint 64 x 64 variant: 288-row halo, 3-deep ring)
+        for halo, wide, bm, ch, small in ((True, True, 64, 16, False), (True, True, 128, 16, False),
+                                          (True, False, 64, 32, False), (True, False, 128, 32, False),
+                                          (True, False, 64, 16, False), (True, False, 128, 16, False),
+                                          (True, False, 0, 16, False), (True, False, 64, 16, True),
+                                          (False, False, 64, 32, False)):
             p = ops.get_tiled_plan()
             p.halo_f32, p.halo_f32_wide, p.halo_f32_bm, p.halo_f32_ch = halo, wide, bm, ch
+            p.halo_f32_small = small
             ops.set_tiled_plan(p)
             wp = _param(w.to(cuda_dev))
             Fn.ConvWeightCopies({"w": wp}, cuda_dev, kind="f32flip").refresh()
