@@ -372,6 +372,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("vcap", &gops::TiledPlan::vcap)
       .def_readwrite("wg_xcd", &gops::TiledPlan::wg_xcd)
       .def_readwrite("wg_n64", &gops::TiledPlan::wg_n64)
+      .def_readwrite("wg_bk16", &gops::TiledPlan::wg_bk16)
+      .def_readwrite("wg_bk16_64", &gops::TiledPlan::wg_bk16_64)
       .def_readwrite("dgrad_fwd", &gops::TiledPlan::dgrad_fwd)
       .def_readwrite("wg64", &gops::TiledPlan::wg64)
       .def_readwrite("halo_f32", &gops::TiledPlan::halo_f32)

@@ -164,6 +164,8 @@ struct TiledPlan {
   bool dgrad_fwd = true;                  // fp32 stride-1 dgrad through the forward kernel
   bool wg64 = true;                       // 64-wide ci tiles for every filter gradient
   bool wg_n64 = false;                    // ... and 64-wide co tiles (labs)
+  bool wg_bk16 = true;                    // fp32 64 x 128 filter tiles on 16-pixel K tiles
+  bool wg_bk16_64 = false;                // ... and the 64 x 64 ones (56x56 layer 109 -> 117 us: off)
   bool halo_f32 = true;                   // fp32 3x3 stride-1 convs on conv3f_kernel
   // ... with 128-column tiles on 16-channel chunks for K % 128 == 0: measured a
   // wash (conv_lab fwd + dgrad 2292 vs 2270 us a step), so off

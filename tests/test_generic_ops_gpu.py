@@ -520,9 +520,10 @@ def test_fp32_filter_grad_xcd_slice_order(cuda_dev, N, H, C, K, R, stride, pad):
     plan = ops.get_tiled_plan()
     outs = []
     try:
-        for xcd in (True, False):
+        # (and the 16-pixel K tiles of the 64 x 128 fp32 filter kernel)
+        for xcd, bk16 in ((True, False), (False, False), (False, True)):
             p = ops.get_tiled_plan()
-            p.wg_xcd = xcd
+            p.wg_xcd, p.wg_bk16, p.wg_bk16_64 = xcd, bk16, bk16
             ops.set_tiled_plan(p)
             wp = _param(w.to(cuda_dev))
             yg = Fn.conv2d(x.to(cuda_dev), wp, None, stride, pad, False)
@@ -533,7 +534,7 @@ def test_fp32_filter_grad_xcd_slice_order(cuda_dev, N, H, C, K, R, stride, pad):
         ops.set_tiled_plan(plan)
     for dw in outs:
         assert _rel(dw.double(), wr.grad) < 1e-5
-    assert _rel(outs[0], outs[1]) < 1e-6
+    assert _rel(outs[0], outs[1]) < 1e-6 and _rel(outs[1], outs[2]) < 1e-5
 
 
 @pytest.mark.parametrize("N,H,C,K", [
